@@ -1,0 +1,80 @@
+// Container-side configuration of the vGPU shim, parsed once from the environment.
+//
+// This is the consumer half of the plugin→shim ABI. The reference
+// reads CUDA_DEVICE_MEMORY_LIMIT[_i], CUDA_DEVICE_SM_LIMIT, NVIDIA_DEVICE_MAP,
+// CUDA_DEVICE_MEMORY_SHARED_CACHE, CUDA_OVERSUBSCRIBE, CUDA_TASK_PRIORITY,
+// GPU_CORE_UTILIZATION_POLICY, ACTIVE_OOM_KILLER and MEMORY_OVERRIDE
+// (libvgpu.so:get_limit_from_env [multiprocess_memory_limit.c:101-111],
+// postInit@0x16ded, set_env_utilization_switch@0x569dc). The MI355X names are the
+// VGPU_* equivalents, plus the CU range the plugin assigns for spatial partitioning.
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+namespace vgpu {
+
+constexpr int kMaxDevices = 16;     // same hard cap as the reference (virtual_map[16])
+constexpr int kMaxProcs = 1024;     // process slots per region (reference: cmp 0x3ff)
+constexpr int kMaxCUs = 256;        // MI355X: 8 XCDs x 32 CUs
+constexpr int kCuMaskWords = kMaxCUs / 32;
+
+// How the CU share (VGPU_DEVICE_CU_LIMIT) is enforced.
+enum class CuMode : int {
+  kOff = 0,       // no compute limit
+  kSpatial = 1,   // per-queue CU mask (hsa_amd_queue_cu_set_mask): default on MI355X
+  kTemporal = 2,  // reference-parity token bucket at kernel launch
+  kBoth = 3,
+};
+
+// GPU_CORE_UTILIZATION_POLICY analogue.
+enum class CuPolicy : int { kDefault = 0, kForce = 1, kDisable = 2 };
+
+struct DeviceConfig {
+  uint64_t mem_limit = 0;      // bytes, 0 = unlimited
+  int cu_limit_pct = 0;        // 0 or >= 100 = unlimited
+  int cu_range_begin = -1;     // explicit logical CU range [begin, end) or -1 = derive
+  int cu_range_end = -1;
+  char uuid[64] = {0};         // physical UUID from VGPU_DEVICE_MAP (may be empty)
+};
+
+struct Config {
+  bool disabled = false;                 // VGPU_DISABLE=1: shim is fully inert
+  int num_devices = 0;                   // devices that carry an explicit config
+  DeviceConfig dev[kMaxDevices];
+  std::string shared_cache = "/tmp/vgpushr.cache";
+  bool oversubscribe = false;            // VGPU_OVERSUBSCRIBE
+  int priority = 1;                      // VGPU_TASK_PRIORITY
+  CuMode cu_mode = CuMode::kSpatial;     // VGPU_CU_MODE
+  CuPolicy cu_policy = CuPolicy::kDefault;
+  bool active_oom_killer = false;        // VGPU_ACTIVE_OOM_KILLER
+  bool memory_override = false;          // VGPU_MEMORY_OVERRIDE
+  bool signal_control = false;           // VGPU_SIGNAL_CONTROL: also honour SIGUSR1/2
+  bool hook_smi = true;                  // VGPU_HOOK_SMI: virtualise amd-smi/rocm-smi
+  int util_period_ms = 120;              // feedback period (reference: 120 ms)
+  int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
+
+  bool any_memory_limit() const;
+  bool any_cu_limit() const;
+};
+
+// Parses "NNN[KkMmGg][iB|B]" into bytes. Returns false on syntax error or overflow.
+// Bare numbers are bytes; "m"/"M" is MiB, as in the reference ("<MiB>m").
+bool parse_size(const char* s, uint64_t* out);
+
+// Parses "<begin>-<end>" (end exclusive) or "<begin>:<count>".
+bool parse_range(const char* s, int* begin, int* end);
+
+// Fills `cfg` from the environment. `getenv_fn` is injectable for unit tests.
+using GetenvFn = const char* (*)(const char*);
+void load_config(Config* cfg, GetenvFn getenv_fn = nullptr);
+
+// KEY=VALUE lines applied with setenv(…, overwrite=1) before the config is parsed
+// (reference: nvml_preInit → load_env_from_file("/overrideEnv")).
+int apply_override_env_file(const char* path);
+
+// The process-wide config (filled by shim init).
+const Config& config();
+Config& mutable_config();
+
+}  // namespace vgpu

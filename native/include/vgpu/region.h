@@ -1,0 +1,186 @@
+// Per-container shared accounting region (mmap'd file shared by every process of a
+// container, and optionally by a node monitor through a host path).
+//
+// Reference behaviour (libvgpu.so, src/multiprocess/multiprocess_memory_limit.c):
+//   try_create_shrreg [645-741]  create/attach, init limits from env, verify consistency
+//   lock_shrreg/fix_lock_shrreg  POSIX sem + "kick the dead owner" heuristic
+//   init_proc_slot_withlock      <=1024 process slots, exit/atfork handlers
+//   add/rm_gpu_device_memory_usage, get_gpu_memory_usage (sum over all slots)
+//   rm_quitted_process           popen("ps a -o pid=") reclaim of dead slots
+//   suspend_all/resume_all       SIGUSR2/SIGUSR1 broadcast
+//
+// MI355X-native redesign (not a layout copy):
+//   * versioned header (magic + version + struct size) so a monitor can reject a
+//     foreign layout instead of mis-reading it;
+//   * robust process-shared pthread mutex (EOWNERDEAD -> consistent + reclaim)
+//     instead of sem_timedwait + owner kick;
+//   * a per-device aggregate `used` counter updated with a CAS admission loop, so the
+//     OOM check is one atomic load and two concurrent allocators can never jointly
+//     overshoot the quota (the reference sums 1024 slots without a lock);
+//   * dead-process reclaim by kill(pid, 0) + /proc start-time check (PID reuse safe),
+//     no subprocess;
+//   * suspend/resume and the launch block are region state polled by the gates, so
+//     the shim does not have to own SIGUSR1/SIGUSR2 in the user's process (opt-in
+//     VGPU_SIGNAL_CONTROL keeps the signal protocol for parity);
+//   * per-device CU mask + token bucket live in the region, so every process of a
+//     container shares one compute budget.
+#pragma once
+
+#include <pthread.h>
+#include <sys/types.h>
+
+#include <atomic>
+#include <cstdint>
+
+#include "vgpu/config.h"
+
+namespace vgpu {
+
+constexpr uint32_t kRegionMagic = 0x56475055u;  // "VGPU"
+constexpr uint32_t kRegionVersion = 1;
+
+enum ProcStatus : int32_t { kProcFree = 0, kProcRunning = 1, kProcSuspended = 2 };
+
+// Memory categories tracked per process and device (reference: {context, module,
+// data, offset, total} per device in each proc slot).
+enum MemKind : int { kMemData = 0, kMemContext = 1, kMemModule = 2, kMemSpill = 3, kMemKinds = 4 };
+
+struct alignas(64) DeviceUsage {
+  std::atomic<uint64_t> total;            // sum of all kinds
+  std::atomic<uint64_t> kind[kMemKinds];
+  std::atomic<uint64_t> peak;
+};
+
+struct alignas(64) ProcSlot {
+  std::atomic<int32_t> pid;               // 0 = free slot
+  std::atomic<int32_t> hostpid;           // PID in the host namespace (0 = unknown)
+  std::atomic<int32_t> status;            // ProcStatus
+  int32_t priority;
+  uint64_t start_time;                    // /proc/<pid>/stat field 22, guards PID reuse
+  std::atomic<uint64_t> launches;         // kernel launches through the gates
+  std::atomic<uint64_t> throttle_ns;      // time spent blocked in the rate limiter
+  std::atomic<uint64_t> suspend_ns;       // time spent blocked by suspend
+  std::atomic<uint64_t> oom_events;
+  DeviceUsage used[kMaxDevices];
+};
+
+struct alignas(64) DeviceState {
+  char uuid[64];
+  uint64_t mem_limit;                     // bytes, 0 = unlimited
+  uint64_t phys_total;                    // physical HBM bytes reported by ROCr
+  int32_t cu_limit_pct;                   // 0 / >=100 = unlimited
+  int32_t cu_count;                       // physical CUs of the agent
+  int32_t num_xcc;
+  int32_t cu_mask_bits;                   // number of valid bits in cu_mask
+  uint32_t cu_mask[kCuMaskWords];         // spatial mask applied to every queue
+  std::atomic<uint64_t> used;             // aggregate bytes charged (all live slots)
+  std::atomic<uint64_t> spilled;          // portion of `used` served from host memory
+  std::atomic<uint64_t> monitor_used;     // sampled physical usage of the region's PIDs
+  std::atomic<int64_t> tokens;            // temporal mode bucket (workgroups)
+  std::atomic<int64_t> token_cap;
+  std::atomic<int64_t> share;             // refill per period
+  std::atomic<int32_t> util_pct;          // last sampled utilisation (0..100)
+  uint32_t gpu_id;                        // KFD gpu_id (stats_<gpu_id> in sysfs)
+  uint32_t bdf;                           // PCI bus/device/function (HSA BDFID)
+  uint32_t domain;                        // PCI domain
+  uint32_t configured;                    // 1 once a GPU process filled the agent info
+};
+
+struct RegionHeader {
+  uint32_t magic;
+  uint32_t version;
+  uint64_t region_size;                   // sizeof(Region) of the writer
+  pthread_mutex_t mutex;                  // robust + process-shared
+  std::atomic<int32_t> initialized;
+  int32_t num_devices;
+  std::atomic<int32_t> utilization_switch;  // 1 = temporal limiter on (reference init 1)
+  std::atomic<int32_t> recent_kernel;       // < 0 blocks every launch (reference init 2)
+  std::atomic<int32_t> priority;
+  std::atomic<int32_t> proc_num;            // live slots
+  std::atomic<int32_t> suspend_all;         // 1 = every gate blocks
+  std::atomic<int32_t> watcher_pid;         // process that runs the utilisation watcher
+  std::atomic<uint64_t> watcher_heartbeat;  // CLOCK_MONOTONIC ns of the last tick
+  uint32_t flags;                           // RegionFlags
+  uint32_t pad0;
+  std::atomic<uint64_t> generation;         // bumped on any limit change
+};
+
+enum RegionFlags : uint32_t { kFlagOversubscribe = 1u, kFlagActiveOomKiller = 2u };
+
+struct Region {
+  RegionHeader hdr;
+  DeviceState dev[kMaxDevices];
+  ProcSlot procs[kMaxProcs];
+};
+
+// Result of an admission check.
+enum class Charge : int { kOk = 0, kOverLimit = 1 };
+
+// A process's handle on an attached region.
+class SharedRegion {
+ public:
+  SharedRegion() = default;
+  ~SharedRegion();
+  SharedRegion(const SharedRegion&) = delete;
+  SharedRegion& operator=(const SharedRegion&) = delete;
+
+  // Opens (creating if needed) and maps `path`. When the region is fresh, device
+  // limits are initialised from `cfg`; when it exists, `cfg` is checked against the
+  // stored limits ("Limit inconsistency detected" in the reference) and the stored
+  // values win. Returns 0 or -errno.
+  int attach(const char* path, const Config* cfg, bool create);
+  void detach();
+  bool attached() const { return r_ != nullptr; }
+  Region* raw() { return r_; }
+  const Region* raw() const { return r_; }
+  const char* path() const { return path_; }
+
+  // Robust lock. Returns false only if the mutex is unrecoverable.
+  bool lock();
+  void unlock();
+
+  // Process slots.
+  int register_process(pid_t pid, pid_t hostpid, int priority);  // slot index or -1
+  void unregister_process(int slot);
+  int find_slot(pid_t pid) const;
+  int reclaim_dead();               // frees slots of exited processes, returns count
+
+  // Accounting. charge() admits `bytes` on `dev` against the limit (CAS loop, with a
+  // single reclaim-and-retry when over, as oom_check does in the reference).
+  Charge charge(int slot, int dev, uint64_t bytes, MemKind kind);
+  void uncharge(int slot, int dev, uint64_t bytes, MemKind kind);
+  // Unconditional charge (used for memory the runtime already owns, e.g. a spill
+  // fallback that must be recorded even past the limit).
+  void force_charge(int slot, int dev, uint64_t bytes, MemKind kind);
+
+  uint64_t usage(int dev) const;
+  uint64_t limit(int dev) const;
+  uint64_t proc_usage(int slot, int dev) const;
+
+  // External control API (reference: set_current_device_memory_limit,
+  // set_current_device_sm_limit_scale, suspend_all, resume_all, priority,
+  // recent_kernel).
+  void set_limit(int dev, uint64_t bytes);
+  void set_cu_limit(int dev, int pct);
+  void suspend_all();
+  void resume_all();
+  void set_proc_status(int slot, int status);
+  int num_devices() const;
+
+ private:
+  static void init_mutex(pthread_mutex_t* m);
+  void init_fresh(const Config* cfg);
+  void check_consistency(const Config* cfg);
+  void clear_slot_locked(int slot);
+
+  Region* r_ = nullptr;
+  int fd_ = -1;
+  char path_[512] = {0};
+};
+
+// /proc/<pid>/stat start time (clock ticks since boot), 0 if unavailable.
+uint64_t proc_start_time(pid_t pid);
+// True if `pid` is alive and (when start_time != 0) is the same process.
+bool proc_alive(pid_t pid, uint64_t start_time);
+
+}  // namespace vgpu

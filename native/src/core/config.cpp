@@ -1,0 +1,195 @@
+// Env contract parser (see vgpu/config.h for the reference mapping).
+#include "vgpu/config.h"
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "vgpu/log.h"
+
+namespace vgpu {
+
+namespace {
+Config g_config;
+
+bool parse_bool(const char* s, bool dflt) {
+  if (!s || !*s) return dflt;
+  if (!strcasecmp(s, "1") || !strcasecmp(s, "true") || !strcasecmp(s, "yes") || !strcasecmp(s, "on"))
+    return true;
+  if (!strcasecmp(s, "0") || !strcasecmp(s, "false") || !strcasecmp(s, "no") || !strcasecmp(s, "off"))
+    return false;
+  return dflt;
+}
+
+bool parse_int(const char* s, long lo, long hi, long* out) {
+  if (!s || !*s) return false;
+  char* end = nullptr;
+  errno = 0;
+  long v = strtol(s, &end, 10);
+  if (errno || end == s) return false;
+  while (*end == ' ' || *end == '%') end++;
+  if (*end) return false;
+  if (v < lo || v > hi) return false;
+  *out = v;
+  return true;
+}
+}  // namespace
+
+bool Config::any_memory_limit() const {
+  for (int i = 0; i < kMaxDevices; i++)
+    if (dev[i].mem_limit) return true;
+  return false;
+}
+
+bool Config::any_cu_limit() const {
+  for (int i = 0; i < kMaxDevices; i++)
+    if (dev[i].cu_limit_pct > 0 && dev[i].cu_limit_pct < 100) return true;
+  return false;
+}
+
+bool parse_size(const char* s, uint64_t* out) {
+  if (!s) return false;
+  while (*s == ' ') s++;
+  if (!*s || *s == '-') return false;
+  char* end = nullptr;
+  errno = 0;
+  unsigned long long v = strtoull(s, &end, 10);
+  if (errno || end == s) return false;
+  unsigned shift = 0;
+  switch (*end) {
+    case 'k': case 'K': shift = 10; end++; break;
+    case 'm': case 'M': shift = 20; end++; break;
+    case 'g': case 'G': shift = 30; end++; break;
+    case 't': case 'T': shift = 40; end++; break;
+    case 0: break;
+    default:
+      if (*end != 'b' && *end != 'B') return false;
+  }
+  if (shift && (*end == 'i')) end++;
+  if (*end == 'b' || *end == 'B') end++;
+  while (*end == ' ') end++;
+  if (*end) return false;
+  if (shift && v > (~0ULL >> shift)) return false;  // overflow (reference rejects too)
+  *out = (uint64_t)(v << shift);
+  return true;
+}
+
+bool parse_range(const char* s, int* begin, int* end) {
+  if (!s || !*s) return false;
+  int a = 0, b = 0;
+  char sep = 0;
+  if (sscanf(s, "%d%c%d", &a, &sep, &b) != 3) return false;
+  if (sep == ':') b = a + b;
+  else if (sep != '-') return false;
+  if (a < 0 || b <= a || b > kMaxCUs) return false;
+  *begin = a;
+  *end = b;
+  return true;
+}
+
+int apply_override_env_file(const char* path) {
+  FILE* f = fopen(path, "r");
+  if (!f) return 0;
+  char line[1024];
+  int n = 0;
+  while (fgets(line, sizeof(line), f)) {
+    size_t len = strlen(line);
+    while (len && (line[len - 1] == '\n' || line[len - 1] == '\r')) line[--len] = 0;
+    char* p = line;
+    while (*p == ' ' || *p == '\t') p++;
+    if (!*p || *p == '#') continue;
+    if (!strncmp(p, "export ", 7)) p += 7;
+    char* eq = strchr(p, '=');
+    if (!eq || eq == p) continue;
+    *eq = 0;
+    if (setenv(p, eq + 1, 1) == 0) n++;
+  }
+  fclose(f);
+  return n;
+}
+
+void load_config(Config* cfg, GetenvFn getenv_fn) {
+  if (!getenv_fn) getenv_fn = [](const char* k) -> const char* { return getenv(k); };
+  *cfg = Config();
+  cfg->disabled = parse_bool(getenv_fn("VGPU_DISABLE"), false);
+
+  uint64_t global_limit = 0;
+  if (const char* s = getenv_fn("VGPU_DEVICE_MEMORY_LIMIT")) {
+    if (!parse_size(s, &global_limit)) VLOG_WARN("invalid VGPU_DEVICE_MEMORY_LIMIT=%s ignored", s);
+  }
+  long global_cu = 0;
+  if (const char* s = getenv_fn("VGPU_DEVICE_CU_LIMIT")) {
+    if (!parse_int(s, 0, 100, &global_cu)) {
+      VLOG_WARN("invalid VGPU_DEVICE_CU_LIMIT=%s ignored", s);
+      global_cu = 0;
+    }
+  }
+  char key[96];
+  int max_idx = -1;
+  for (int i = 0; i < kMaxDevices; i++) {
+    DeviceConfig& d = cfg->dev[i];
+    d.mem_limit = global_limit;
+    d.cu_limit_pct = (int)global_cu;
+    snprintf(key, sizeof(key), "VGPU_DEVICE_MEMORY_LIMIT_%d", i);
+    if (const char* s = getenv_fn(key)) {
+      uint64_t v = 0;
+      if (parse_size(s, &v)) {
+        d.mem_limit = v;
+        max_idx = i > max_idx ? i : max_idx;
+      } else {
+        VLOG_WARN("invalid %s=%s ignored", key, s);
+      }
+    }
+    snprintf(key, sizeof(key), "VGPU_DEVICE_CU_LIMIT_%d", i);
+    if (const char* s = getenv_fn(key)) {
+      long v = 0;
+      if (parse_int(s, 0, 100, &v)) {
+        d.cu_limit_pct = (int)v;
+        max_idx = i > max_idx ? i : max_idx;
+      } else {
+        VLOG_WARN("invalid %s=%s ignored", key, s);
+      }
+    }
+    snprintf(key, sizeof(key), "VGPU_DEVICE_CU_RANGE_%d", i);
+    if (const char* s = getenv_fn(key)) {
+      if (!parse_range(s, &d.cu_range_begin, &d.cu_range_end)) {
+        VLOG_WARN("invalid %s=%s ignored", key, s);
+        d.cu_range_begin = d.cu_range_end = -1;
+      }
+    }
+  }
+  cfg->num_devices = max_idx + 1;
+
+  if (const char* s = getenv_fn("VGPU_SHARED_CACHE")) {
+    if (*s) cfg->shared_cache = s;
+  }
+  cfg->oversubscribe = parse_bool(getenv_fn("VGPU_OVERSUBSCRIBE"), false);
+  long prio = 1;
+  if (parse_int(getenv_fn("VGPU_TASK_PRIORITY"), -1000, 1000, &prio)) cfg->priority = (int)prio;
+
+  if (const char* s = getenv_fn("VGPU_CU_MODE")) {
+    if (!strcasecmp(s, "spatial")) cfg->cu_mode = CuMode::kSpatial;
+    else if (!strcasecmp(s, "temporal")) cfg->cu_mode = CuMode::kTemporal;
+    else if (!strcasecmp(s, "both")) cfg->cu_mode = CuMode::kBoth;
+    else if (!strcasecmp(s, "off") || !strcasecmp(s, "none")) cfg->cu_mode = CuMode::kOff;
+    else VLOG_WARN("invalid VGPU_CU_MODE=%s, using spatial", s);
+  }
+  if (const char* s = getenv_fn("VGPU_CU_POLICY")) {
+    if (!strcasecmp(s, "force")) cfg->cu_policy = CuPolicy::kForce;
+    else if (!strcasecmp(s, "disable")) cfg->cu_policy = CuPolicy::kDisable;
+  }
+  cfg->active_oom_killer = parse_bool(getenv_fn("VGPU_ACTIVE_OOM_KILLER"), false);
+  cfg->memory_override = parse_bool(getenv_fn("VGPU_MEMORY_OVERRIDE"), false);
+  cfg->signal_control = parse_bool(getenv_fn("VGPU_SIGNAL_CONTROL"), false);
+  cfg->hook_smi = parse_bool(getenv_fn("VGPU_HOOK_SMI"), true);
+  long period = 120;
+  if (parse_int(getenv_fn("VGPU_UTIL_PERIOD_MS"), 10, 10000, &period)) cfg->util_period_ms = (int)period;
+  long merge = 1;
+  if (parse_int(getenv_fn("VGPU_DUPLICATE_MERGE"), 0, 1, &merge)) cfg->duplicate_merge = (int)merge;
+}
+
+const Config& config() { return g_config; }
+Config& mutable_config() { return g_config; }
+
+}  // namespace vgpu

@@ -1,0 +1,385 @@
+// Shared accounting region. Behavioural parity target: libvgpu.so
+// src/multiprocess/multiprocess_memory_limit.c (try_create_shrreg [645-741],
+// lock_shrreg [516-540], init_proc_slot_withlock, exit_handler [475-494],
+// add/rm_gpu_device_memory_usage [359-382], rm_quitted_process [234-248]).
+// Design notes are in vgpu/region.h.
+#include "vgpu/region.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/file.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+
+#include "vgpu/log.h"
+
+namespace vgpu {
+
+uint64_t proc_start_time(pid_t pid) {
+  char path[64];
+  snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+  FILE* f = fopen(path, "r");
+  if (!f) return 0;
+  char buf[1024];
+  size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  // comm may contain spaces/parens: fields restart after the last ')'.
+  char* p = strrchr(buf, ')');
+  if (!p) return 0;
+  p++;
+  // After ')' come fields 3.. ; start time is field 22 -> 20th token after ')'.
+  int field = 2;
+  char* save = nullptr;
+  for (char* tok = strtok_r(p, " ", &save); tok; tok = strtok_r(nullptr, " ", &save)) {
+    field++;
+    if (field == 22) return strtoull(tok, nullptr, 10);
+  }
+  return 0;
+}
+
+bool proc_alive(pid_t pid, uint64_t start_time) {
+  if (pid <= 0) return false;
+  if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+  if (start_time) {
+    uint64_t st = proc_start_time(pid);
+    if (st && st != start_time) return false;  // PID was reused
+  }
+  return true;
+}
+
+SharedRegion::~SharedRegion() { detach(); }
+
+void SharedRegion::init_mutex(pthread_mutex_t* m) {
+  pthread_mutexattr_t a;
+  pthread_mutexattr_init(&a);
+  pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+  pthread_mutexattr_setrobust(&a, PTHREAD_MUTEX_ROBUST);
+  pthread_mutex_init(m, &a);
+  pthread_mutexattr_destroy(&a);
+}
+
+int SharedRegion::attach(const char* path, const Config* cfg, bool create) {
+  detach();
+  snprintf(path_, sizeof(path_), "%s", path);
+  mode_t old = umask(0);
+  int fd = open(path, O_RDWR | (create ? O_CREAT : 0) | O_CLOEXEC, 0666);
+  umask(old);
+  if (fd < 0) return -errno;
+  // Serialise creation/initialisation with an advisory file lock (reference: lockf).
+  if (flock(fd, LOCK_EX) != 0) {
+    int e = errno;
+    close(fd);
+    return -e;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    int e = errno;
+    flock(fd, LOCK_UN);
+    close(fd);
+    return -e;
+  }
+  if ((size_t)st.st_size < sizeof(Region)) {
+    if (!create || ftruncate(fd, sizeof(Region)) != 0) {
+      int e = create ? errno : EINVAL;
+      flock(fd, LOCK_UN);
+      close(fd);
+      return -e;
+    }
+  }
+  void* p = mmap(nullptr, sizeof(Region), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (p == MAP_FAILED) {
+    int e = errno;
+    flock(fd, LOCK_UN);
+    close(fd);
+    return -e;
+  }
+  r_ = static_cast<Region*>(p);
+  fd_ = fd;
+  if (r_->hdr.magic != kRegionMagic) {
+    if (!create) {
+      munmap(p, sizeof(Region));
+      r_ = nullptr;
+      flock(fd, LOCK_UN);
+      close(fd);
+      fd_ = -1;
+      return -EINVAL;
+    }
+    init_fresh(cfg);
+  } else if (r_->hdr.version != kRegionVersion || r_->hdr.region_size != sizeof(Region)) {
+    VLOG_ERROR("shared region %s has layout v%u/%lu, this shim expects v%u/%zu", path,
+               r_->hdr.version, (unsigned long)r_->hdr.region_size, kRegionVersion, sizeof(Region));
+    munmap(p, sizeof(Region));
+    r_ = nullptr;
+    flock(fd, LOCK_UN);
+    close(fd);
+    fd_ = -1;
+    return -EPROTO;
+  } else if (cfg) {
+    check_consistency(cfg);
+  }
+  flock(fd, LOCK_UN);
+  return 0;
+}
+
+void SharedRegion::detach() {
+  if (r_) munmap(r_, sizeof(Region));
+  if (fd_ >= 0) close(fd_);
+  r_ = nullptr;
+  fd_ = -1;
+}
+
+void SharedRegion::init_fresh(const Config* cfg) {
+  memset(static_cast<void*>(r_), 0, sizeof(Region));
+  r_->hdr.version = kRegionVersion;
+  r_->hdr.region_size = sizeof(Region);
+  init_mutex(&r_->hdr.mutex);
+  r_->hdr.utilization_switch.store(1);
+  r_->hdr.recent_kernel.store(2);
+  r_->hdr.priority.store(cfg ? cfg->priority : 1);
+  uint32_t flags = 0;
+  if (cfg && cfg->oversubscribe) flags |= kFlagOversubscribe;
+  if (cfg && cfg->active_oom_killer) flags |= kFlagActiveOomKiller;
+  r_->hdr.flags = flags;
+  int n = 0;
+  if (cfg) {
+    for (int i = 0; i < kMaxDevices; i++) {
+      DeviceState& d = r_->dev[i];
+      d.mem_limit = cfg->dev[i].mem_limit;
+      d.cu_limit_pct = cfg->dev[i].cu_limit_pct;
+      memcpy(d.uuid, cfg->dev[i].uuid, sizeof(d.uuid));
+      d.uuid[sizeof(d.uuid) - 1] = 0;
+    }
+    n = cfg->num_devices;
+  }
+  r_->hdr.num_devices = n;
+  r_->hdr.initialized.store(1);
+  std::atomic_thread_fence(std::memory_order_release);
+  r_->hdr.magic = kRegionMagic;  // published last
+}
+
+void SharedRegion::check_consistency(const Config* cfg) {
+  for (int i = 0; i < kMaxDevices; i++) {
+    uint64_t have = r_->dev[i].mem_limit;
+    uint64_t want = cfg->dev[i].mem_limit;
+    if (want && have != want) {
+      VLOG_WARN("limit inconsistency on device %d: region=%lu env=%lu (region wins)", i,
+                (unsigned long)have, (unsigned long)want);
+    }
+    if (cfg->dev[i].cu_limit_pct && r_->dev[i].cu_limit_pct != cfg->dev[i].cu_limit_pct) {
+      VLOG_WARN("CU limit inconsistency on device %d: region=%d env=%d (region wins)", i,
+                r_->dev[i].cu_limit_pct, cfg->dev[i].cu_limit_pct);
+    }
+  }
+  if (cfg->num_devices > r_->hdr.num_devices) r_->hdr.num_devices = cfg->num_devices;
+}
+
+bool SharedRegion::lock() {
+  int rc = pthread_mutex_lock(&r_->hdr.mutex);
+  if (rc == EOWNERDEAD) {
+    // The previous owner died inside the critical section. State it protects is
+    // either consistent (all updates are single atomics) or repaired by reclaim.
+    VLOG_WARN("shared region lock owner died; recovering");
+    pthread_mutex_consistent(&r_->hdr.mutex);
+    return true;
+  }
+  if (rc == ENOTRECOVERABLE) {
+    VLOG_ERROR("shared region mutex is not recoverable");
+    return false;
+  }
+  return rc == 0;
+}
+
+void SharedRegion::unlock() { pthread_mutex_unlock(&r_->hdr.mutex); }
+
+int SharedRegion::num_devices() const { return r_ ? r_->hdr.num_devices : 0; }
+
+int SharedRegion::find_slot(pid_t pid) const {
+  for (int i = 0; i < kMaxProcs; i++)
+    if (r_->procs[i].pid.load(std::memory_order_relaxed) == pid) return i;
+  return -1;
+}
+
+int SharedRegion::register_process(pid_t pid, pid_t hostpid, int priority) {
+  if (!lock()) return -1;
+  int slot = -1;
+  for (int attempt = 0; attempt < 2 && slot < 0; attempt++) {
+    for (int i = 0; i < kMaxProcs; i++) {
+      int32_t cur = r_->procs[i].pid.load(std::memory_order_relaxed);
+      if (cur == pid) {  // stale slot of a previous process with our PID
+        clear_slot_locked(i);
+        cur = 0;
+      }
+      if (cur == 0) {
+        slot = i;
+        break;
+      }
+    }
+    if (slot < 0) {
+      unlock();
+      reclaim_dead();
+      if (!lock()) return -1;
+    }
+  }
+  if (slot >= 0) {
+    ProcSlot& s = r_->procs[slot];
+    memset(static_cast<void*>(&s.used), 0, sizeof(s.used));
+    s.launches.store(0);
+    s.throttle_ns.store(0);
+    s.suspend_ns.store(0);
+    s.oom_events.store(0);
+    s.priority = priority;
+    s.start_time = proc_start_time(pid);
+    s.hostpid.store(hostpid);
+    s.status.store(r_->hdr.suspend_all.load() ? kProcSuspended : kProcRunning);
+    s.pid.store(pid, std::memory_order_release);
+    r_->hdr.proc_num.fetch_add(1);
+  } else {
+    VLOG_ERROR("no free process slot in shared region (%d in use)", kMaxProcs);
+  }
+  unlock();
+  return slot;
+}
+
+void SharedRegion::clear_slot_locked(int slot) {
+  ProcSlot& s = r_->procs[slot];
+  if (s.pid.load() == 0) return;
+  for (int d = 0; d < kMaxDevices; d++) {
+    uint64_t t = s.used[d].total.exchange(0);
+    uint64_t sp = s.used[d].kind[kMemSpill].load();
+    for (int k = 0; k < kMemKinds; k++) s.used[d].kind[k].store(0);
+    if (t) r_->dev[d].used.fetch_sub(t);
+    if (sp) r_->dev[d].spilled.fetch_sub(sp);
+  }
+  s.status.store(kProcFree);
+  s.hostpid.store(0);
+  s.pid.store(0, std::memory_order_release);
+  r_->hdr.proc_num.fetch_sub(1);
+}
+
+void SharedRegion::unregister_process(int slot) {
+  if (!r_ || slot < 0 || slot >= kMaxProcs) return;
+  if (!lock()) return;
+  clear_slot_locked(slot);
+  unlock();
+}
+
+int SharedRegion::reclaim_dead() {
+  if (!r_) return 0;
+  if (!lock()) return 0;
+  int n = 0;
+  for (int i = 0; i < kMaxProcs; i++) {
+    ProcSlot& s = r_->procs[i];
+    int32_t pid = s.pid.load();
+    if (pid == 0) continue;
+    if (!proc_alive(pid, s.start_time)) {
+      VLOG_INFO("reclaiming slot %d of exited pid %d", i, pid);
+      clear_slot_locked(i);
+      n++;
+    }
+  }
+  unlock();
+  return n;
+}
+
+Charge SharedRegion::charge(int slot, int dev, uint64_t bytes, MemKind kind) {
+  DeviceState& d = r_->dev[dev];
+  for (int attempt = 0; attempt < 2; attempt++) {
+    uint64_t lim = d.mem_limit;
+    uint64_t cur = d.used.load(std::memory_order_relaxed);
+    bool admitted = false;
+    while (true) {
+      if (lim && cur + bytes > lim) break;
+      if (d.used.compare_exchange_weak(cur, cur + bytes, std::memory_order_acq_rel)) {
+        admitted = true;
+        break;
+      }
+    }
+    if (admitted) {
+      if (slot >= 0) {
+        DeviceUsage& u = r_->procs[slot].used[dev];
+        uint64_t t = u.total.fetch_add(bytes) + bytes;
+        u.kind[kind].fetch_add(bytes);
+        uint64_t pk = u.peak.load();
+        while (t > pk && !u.peak.compare_exchange_weak(pk, t)) {
+        }
+      }
+      if (kind == kMemSpill) d.spilled.fetch_add(bytes);
+      return Charge::kOk;
+    }
+    // Over the limit: memory of exited processes may still be charged. Reclaim once
+    // and retry (reference oom_check → rm_quitted_process → retry).
+    if (attempt == 0 && reclaim_dead() == 0) break;
+  }
+  if (slot >= 0) r_->procs[slot].oom_events.fetch_add(1);
+  return Charge::kOverLimit;
+}
+
+void SharedRegion::force_charge(int slot, int dev, uint64_t bytes, MemKind kind) {
+  r_->dev[dev].used.fetch_add(bytes);
+  if (kind == kMemSpill) r_->dev[dev].spilled.fetch_add(bytes);
+  if (slot >= 0) {
+    r_->procs[slot].used[dev].total.fetch_add(bytes);
+    r_->procs[slot].used[dev].kind[kind].fetch_add(bytes);
+  }
+}
+
+void SharedRegion::uncharge(int slot, int dev, uint64_t bytes, MemKind kind) {
+  DeviceState& d = r_->dev[dev];
+  // Saturating subtraction: a slot reclaimed concurrently must not underflow.
+  auto sat_sub = [](std::atomic<uint64_t>& a, uint64_t v) {
+    uint64_t cur = a.load(std::memory_order_relaxed);
+    while (!a.compare_exchange_weak(cur, cur > v ? cur - v : 0)) {
+    }
+  };
+  if (slot >= 0) {
+    DeviceUsage& u = r_->procs[slot].used[dev];
+    uint64_t have = u.total.load();
+    if (have < bytes) bytes = have;  // slot already reclaimed/cleared
+    sat_sub(u.total, bytes);
+    sat_sub(u.kind[kind], bytes);
+  }
+  sat_sub(d.used, bytes);
+  if (kind == kMemSpill) sat_sub(d.spilled, bytes);
+}
+
+uint64_t SharedRegion::usage(int dev) const { return r_->dev[dev].used.load(std::memory_order_relaxed); }
+uint64_t SharedRegion::limit(int dev) const { return r_->dev[dev].mem_limit; }
+uint64_t SharedRegion::proc_usage(int slot, int dev) const { return r_->procs[slot].used[dev].total.load(); }
+
+void SharedRegion::set_limit(int dev, uint64_t bytes) {
+  r_->dev[dev].mem_limit = bytes;
+  if (dev >= r_->hdr.num_devices) r_->hdr.num_devices = dev + 1;
+  r_->hdr.generation.fetch_add(1);
+}
+
+void SharedRegion::set_cu_limit(int dev, int pct) {
+  r_->dev[dev].cu_limit_pct = pct;
+  if (dev >= r_->hdr.num_devices) r_->hdr.num_devices = dev + 1;
+  r_->hdr.generation.fetch_add(1);
+}
+
+void SharedRegion::suspend_all() {
+  r_->hdr.suspend_all.store(1);
+  for (int i = 0; i < kMaxProcs; i++)
+    if (r_->procs[i].pid.load()) r_->procs[i].status.store(kProcSuspended);
+  r_->hdr.generation.fetch_add(1);
+}
+
+void SharedRegion::resume_all() {
+  r_->hdr.suspend_all.store(0);
+  for (int i = 0; i < kMaxProcs; i++)
+    if (r_->procs[i].pid.load()) r_->procs[i].status.store(kProcRunning);
+  r_->hdr.generation.fetch_add(1);
+}
+
+void SharedRegion::set_proc_status(int slot, int status) {
+  if (slot >= 0 && slot < kMaxProcs) r_->procs[slot].status.store(status);
+}
+
+}  // namespace vgpu

@@ -1,0 +1,81 @@
+// In-process control API exported by the shim (reference-name mapping):
+//   suspend_all / resume_all                → vgpu_suspend_all / vgpu_resume_all
+//   set_current_device_memory_limit         → vgpu_set_current_device_memory_limit
+//   set_current_device_sm_limit_scale       → vgpu_set_current_device_cu_limit
+//   get_current_device_{memory_limit,usage} → vgpu_get_current_device_*
+//   cuVGPUViewAllocator (debug dump)        → vgpu_view_allocator
+// Names are prefixed: the shim is preloaded into arbitrary programs and must not
+// collide with their symbols.
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+
+#include <cstdio>
+
+#include "real.h"
+#include "shim.h"
+
+using namespace vgpu;
+
+namespace {
+int current_device() {
+  ShimState& s = shim();
+  if (s.n_agents <= 1) return 0;
+  VGPU_REAL_HIP(hipGetDevice);
+  int d = 0;
+  if (!real_hipGetDevice || real_hipGetDevice(&d) != hipSuccess) d = 0;
+  return d;
+}
+bool ok() { return shim_attach_region_only(); }
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) int vgpu_suspend_all() {
+  if (!ok()) return -1;
+  shim().region.suspend_all();
+  return 0;
+}
+
+__attribute__((visibility("default"))) int vgpu_resume_all() {
+  if (!ok()) return -1;
+  shim().region.resume_all();
+  return 0;
+}
+
+__attribute__((visibility("default"))) int vgpu_set_current_device_memory_limit(uint64_t bytes) {
+  if (!ok()) return -1;
+  shim().region.set_limit(current_device(), bytes);
+  return 0;
+}
+
+__attribute__((visibility("default"))) uint64_t vgpu_get_current_device_memory_limit() {
+  return ok() ? shim().region.limit(current_device()) : 0;
+}
+
+__attribute__((visibility("default"))) uint64_t vgpu_get_current_device_memory_usage() {
+  return ok() ? shim().region.usage(current_device()) : 0;
+}
+
+__attribute__((visibility("default"))) int vgpu_set_current_device_cu_limit(int pct) {
+  if (!ok() || pct < 0 || pct > 100) return -1;
+  shim().region.set_cu_limit(current_device(), pct);
+  return 0;
+}
+
+__attribute__((visibility("default"))) int vgpu_get_current_device_cu_limit() {
+  return ok() ? shim().region.raw()->dev[current_device()].cu_limit_pct : -1;
+}
+
+__attribute__((visibility("default"))) int vgpu_shim_active() { return shim().active ? 1 : 0; }
+
+__attribute__((visibility("default"))) void vgpu_view_allocator() {
+  ShimState& s = shim();
+  std::lock_guard<std::mutex> g(s.alloc_mu);
+  fprintf(stderr, "[vGPU] allocator: %zu live allocations, %zu vmem handles, slot %d\n", s.allocs.size(),
+          s.vmem.size(), s.slot);
+  for (const auto& kv : s.allocs)
+    fprintf(stderr, "  %p size=%lu dev=%d kind=%d\n", (void*)kv.first, (unsigned long)kv.second.size, kv.second.dev,
+            kv.second.kind);
+}
+
+}  // extern "C"

@@ -1,0 +1,312 @@
+// ROCr (HSA) interposition: the single choke point for device memory, memory-info
+// queries and queue creation on MI355X.
+//
+// Verified on box (profiles/shim_probe.md): libamdhip64 imports these entry points as
+// `U sym@ROCR_1`; every hipMalloc / hipMallocAsync / library workspace reaches
+// hsa_amd_memory_pool_allocate, hipMemGetInfo reads HSA_AMD_AGENT_INFO_MEMORY_AVAIL,
+// and HIP's total memory comes from HSA_AMD_MEMORY_POOL_INFO_SIZE.
+//
+// Reference parity (libvgpu.so src/cuda/memory.c, src/allocator/allocator.c):
+//   cuMemAlloc_v2 → suspend gate → oom_check → real alloc → add usage   (allocate)
+//   cuMemFree_v2  → remove_chunk → rm usage                              (free)
+//   cuMemGetInfo_v2 / cuDeviceTotalMem_v2 → limit-based answers          (info hooks)
+//   CUDA_OVERSUBSCRIBE → managed memory                                  (host spill)
+//   cuIpc* pass-through without double charge                            (not hooked)
+// MI355X-only: hsa_queue_create applies the vGPU's CU mask to every HW queue and
+// hsa_amd_queue_cu_set_mask cannot widen it.
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "real.h"
+#include "shim.h"
+#include "vgpu/kfd.h"
+#include "vgpu/log.h"
+
+using namespace vgpu;
+
+namespace {
+
+void record_alloc(uintptr_t key, uint64_t size, int dev, int kind) {
+  ShimState& s = shim();
+  std::lock_guard<std::mutex> g(s.alloc_mu);
+  s.allocs[key] = AllocRec{size, dev, kind};
+}
+
+bool take_alloc(uintptr_t key, AllocRec* out) {
+  ShimState& s = shim();
+  std::lock_guard<std::mutex> g(s.alloc_mu);
+  auto it = s.allocs.find(key);
+  if (it == s.allocs.end()) return false;
+  *out = it->second;
+  s.allocs.erase(it);
+  return true;
+}
+
+// Host spill for virtual device memory: serve an allocation the HBM cannot hold
+// from pinned host memory reachable by the GPU.
+hsa_status_t spill_allocate(int dev, size_t size, void** ptr) {
+  ShimState& s = shim();
+  AgentInfo& a = s.agents[dev];
+  if (!a.spill_pool.handle) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  VGPU_REAL_HSA(hsa_amd_memory_pool_allocate);
+  VGPU_REAL_HSA(hsa_amd_agents_allow_access);
+  VGPU_REAL_HSA(hsa_amd_memory_pool_free);
+  hsa_status_t st = real_hsa_amd_memory_pool_allocate(a.spill_pool, size, 0, ptr);
+  if (st != HSA_STATUS_SUCCESS) return st;
+  st = real_hsa_amd_agents_allow_access(1, &a.agent, nullptr, *ptr);
+  if (st != HSA_STATUS_SUCCESS) {
+    real_hsa_amd_memory_pool_free(*ptr);
+    *ptr = nullptr;
+    return st;
+  }
+  VLOG_INFO("device %d: %zu bytes spilled to host memory at %p", dev, size, *ptr);
+  return HSA_STATUS_SUCCESS;
+}
+
+inline bool ready() {
+  ShimState& s = shim();
+  int ph = s.phase.load(std::memory_order_acquire);
+  if (__builtin_expect(ph == 0, 0)) {
+    // ROCr was initialised without going through our hsa_init hook (e.g. the shim
+    // was loaded late); initialise on first use.
+    shim_init_after_hsa();
+    ph = s.phase.load(std::memory_order_acquire);
+  }
+  return ph == 2 && s.active && !s.exiting.load(std::memory_order_relaxed);
+}
+
+void charge_context_once(int dev) {
+  // Per-process runtime overhead (queues, scratch, code objects) is allocated by
+  // ROCr internally and bypasses the pool hooks. Charge it once as "context" memory
+  // from KFD's own per-process VRAM counter (reference: primary context size).
+  ShimState& s = shim();
+  AgentInfo& a = s.agents[dev];
+  if (a.context_charged || !s.hostpid || !a.gpu_id) return;
+  a.context_charged = true;
+  int64_t vram = kfd_vram_usage(s.hostpid, a.gpu_id);
+  if (vram <= 0) return;
+  uint64_t mine = s.region.proc_usage(s.slot, dev);
+  if ((uint64_t)vram > mine) {
+    uint64_t ctx = (uint64_t)vram - mine;
+    if (ctx < (1ull << 30)) s.region.force_charge(s.slot, dev, ctx, kMemContext);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+hsa_status_t hsa_init() {
+  VGPU_REAL_HSA(hsa_init);
+  if (!real_hsa_init) return HSA_STATUS_ERROR;
+  ShimState& s = shim();
+  std::vector<int> before;
+  bool first = s.phase.load() == 0;
+  if (first) before = kfd_list_pids();
+  hsa_status_t st = real_hsa_init();
+  if (st == HSA_STATUS_SUCCESS && first) {
+    if (!s.hostpid) {
+      std::vector<int> after = kfd_list_pids();
+      if (std::binary_search(after.begin(), after.end(), (int)getpid())) s.hostpid = getpid();
+      else s.hostpid = kfd_diff_pid(before, after);
+    }
+    shim_init_after_hsa();
+  }
+  return st;
+}
+
+hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr) {
+  VGPU_REAL_HSA(hsa_amd_memory_pool_allocate);
+  if (!real_hsa_amd_memory_pool_allocate) return HSA_STATUS_ERROR;
+  if (!ready() || size == 0) return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
+  int dev = pool_ordinal(pool);
+  if (dev < 0) return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
+  ShimState& s = shim();
+  gate_suspend();
+  if (s.region.charge(s.slot, dev, size, kMemData) != Charge::kOk) {
+    VLOG_WARN("device %d OOM: request %zu bytes, usage %lu of limit %lu", dev, size,
+              (unsigned long)s.region.usage(dev), (unsigned long)s.region.limit(dev));
+    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  }
+  hsa_status_t st = real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
+  if (st == HSA_STATUS_SUCCESS) {
+    record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemData);
+    return st;
+  }
+  if (st == HSA_STATUS_ERROR_OUT_OF_RESOURCES && config().oversubscribe) {
+    // Under quota but the physical HBM is exhausted: virtual device memory.
+    st = spill_allocate(dev, size, ptr);
+    if (st == HSA_STATUS_SUCCESS) {
+      s.region.uncharge(s.slot, dev, size, kMemData);
+      s.region.force_charge(s.slot, dev, size, kMemSpill);
+      record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemSpill);
+      return st;
+    }
+  }
+  s.region.uncharge(s.slot, dev, size, kMemData);
+  return st;
+}
+
+hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
+  VGPU_REAL_HSA(hsa_amd_memory_pool_free);
+  if (!real_hsa_amd_memory_pool_free) return HSA_STATUS_ERROR;
+  ShimState& s = shim();
+  if (ptr && s.phase.load(std::memory_order_relaxed) == 2) {
+    AllocRec rec;
+    if (take_alloc(reinterpret_cast<uintptr_t>(ptr), &rec) && s.slot >= 0 && !s.exiting.load())
+      s.region.uncharge(s.slot, rec.dev, rec.size, (MemKind)rec.kind);
+  }
+  return real_hsa_amd_memory_pool_free(ptr);
+}
+
+hsa_status_t hsa_amd_vmem_handle_create(hsa_amd_memory_pool_t pool, size_t size, hsa_amd_memory_type_t type,
+                                        uint64_t flags, hsa_amd_vmem_alloc_handle_t* handle) {
+  VGPU_REAL_HSA(hsa_amd_vmem_handle_create);
+  if (!real_hsa_amd_vmem_handle_create) return HSA_STATUS_ERROR;
+  if (!ready() || size == 0) return real_hsa_amd_vmem_handle_create(pool, size, type, flags, handle);
+  int dev = pool_ordinal(pool);
+  if (dev < 0) return real_hsa_amd_vmem_handle_create(pool, size, type, flags, handle);
+  ShimState& s = shim();
+  gate_suspend();
+  if (s.region.charge(s.slot, dev, size, kMemData) != Charge::kOk) {
+    VLOG_WARN("device %d OOM (vmem): request %zu bytes, usage %lu of limit %lu", dev, size,
+              (unsigned long)s.region.usage(dev), (unsigned long)s.region.limit(dev));
+    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  }
+  hsa_status_t st = real_hsa_amd_vmem_handle_create(pool, size, type, flags, handle);
+  if (st != HSA_STATUS_SUCCESS) {
+    s.region.uncharge(s.slot, dev, size, kMemData);
+    return st;
+  }
+  std::lock_guard<std::mutex> g(s.alloc_mu);
+  s.vmem[handle->handle] = AllocRec{size, dev, kMemData};
+  return st;
+}
+
+hsa_status_t hsa_amd_vmem_handle_release(hsa_amd_vmem_alloc_handle_t handle) {
+  VGPU_REAL_HSA(hsa_amd_vmem_handle_release);
+  if (!real_hsa_amd_vmem_handle_release) return HSA_STATUS_ERROR;
+  ShimState& s = shim();
+  if (s.phase.load(std::memory_order_relaxed) == 2) {
+    AllocRec rec{0, -1, 0};
+    {
+      std::lock_guard<std::mutex> g(s.alloc_mu);
+      auto it = s.vmem.find(handle.handle);
+      if (it != s.vmem.end()) {
+        rec = it->second;
+        s.vmem.erase(it);
+      }
+    }
+    if (rec.dev >= 0 && s.slot >= 0 && !s.exiting.load()) s.region.uncharge(s.slot, rec.dev, rec.size, kMemData);
+  }
+  return real_hsa_amd_vmem_handle_release(handle);
+}
+
+hsa_status_t hsa_amd_memory_pool_get_info(hsa_amd_memory_pool_t pool, hsa_amd_memory_pool_info_t attr, void* value) {
+  VGPU_REAL_HSA(hsa_amd_memory_pool_get_info);
+  if (!real_hsa_amd_memory_pool_get_info) return HSA_STATUS_ERROR;
+  hsa_status_t st = real_hsa_amd_memory_pool_get_info(pool, attr, value);
+  if (st != HSA_STATUS_SUCCESS || attr != HSA_AMD_MEMORY_POOL_INFO_SIZE || !value) return st;
+  if (!ready()) return st;
+  int dev = pool_ordinal(pool);
+  if (dev < 0) return st;
+  uint64_t lim = shim().region.limit(dev);
+  if (!lim) return st;
+  size_t* v = static_cast<size_t*>(value);
+  // Virtual device memory: with oversubscription the quota may exceed the HBM and
+  // is reported as is (reference: total = limit in cuDeviceTotalMem/cuMemGetInfo).
+  if (config().oversubscribe || lim < *v) *v = (size_t)lim;
+  return st;
+}
+
+hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* value) {
+  VGPU_REAL_HSA(hsa_agent_get_info);
+  if (!real_hsa_agent_get_info) return HSA_STATUS_ERROR;
+  hsa_status_t st = real_hsa_agent_get_info(agent, attr, value);
+  if (__builtin_expect((int)attr != HSA_AMD_AGENT_INFO_MEMORY_AVAIL, 1) || st != HSA_STATUS_SUCCESS) return st;
+  if (!ready()) return st;
+  int dev = agent_ordinal(agent);
+  if (dev < 0) return st;
+  ShimState& s = shim();
+  uint64_t lim = s.region.limit(dev);
+  if (!lim) return st;
+  uint64_t used = s.region.usage(dev);
+  uint64_t avail = lim > used ? lim - used : 0;
+  uint64_t* v = static_cast<uint64_t*>(value);
+  if (!config().oversubscribe && *v < avail) avail = *v;  // other tenants may hold HBM
+  *v = avail;
+  return st;
+}
+
+hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
+                              void (*callback)(hsa_status_t, hsa_queue_t*, void*), void* data,
+                              uint32_t private_segment_size, uint32_t group_segment_size, hsa_queue_t** queue) {
+  VGPU_REAL_HSA(hsa_queue_create);
+  if (!real_hsa_queue_create) return HSA_STATUS_ERROR;
+  hsa_status_t st =
+      real_hsa_queue_create(agent, size, type, callback, data, private_segment_size, group_segment_size, queue);
+  if (st != HSA_STATUS_SUCCESS || !queue || !*queue || !ready()) return st;
+  int dev = agent_ordinal(agent);
+  if (dev < 0) return st;
+  ShimState& s = shim();
+  AgentInfo& a = s.agents[dev];
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    s.queues[reinterpret_cast<uintptr_t>(*queue)] = dev;
+  }
+  if (a.mask_active) {
+    VGPU_REAL_HSA(hsa_amd_queue_cu_set_mask);
+    uint32_t nbits = (uint32_t)((a.cu_count + 31) / 32 * 32);
+    hsa_status_t ms = real_hsa_amd_queue_cu_set_mask(*queue, nbits, a.mask.words);
+    if (ms != HSA_STATUS_SUCCESS && (int)ms != (int)HSA_STATUS_CU_MASK_REDUCED)
+      VLOG_ERROR("device %d: cannot apply CU mask to queue %p (status %d)", dev, (void*)*queue, (int)ms);
+    else
+      VLOG_DEBUG("device %d: queue %p confined to %d CUs", dev, (void*)*queue, a.mask.count());
+  }
+  charge_context_once(dev);
+  return st;
+}
+
+hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* queue, uint32_t num_cu_mask_count, const uint32_t* cu_mask) {
+  VGPU_REAL_HSA(hsa_amd_queue_cu_set_mask);
+  if (!real_hsa_amd_queue_cu_set_mask) return HSA_STATUS_ERROR;
+  if (!ready()) return real_hsa_amd_queue_cu_set_mask(queue, num_cu_mask_count, cu_mask);
+  ShimState& s = shim();
+  int dev = -1;
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    auto it = s.queues.find(reinterpret_cast<uintptr_t>(queue));
+    if (it != s.queues.end()) dev = it->second;
+  }
+  if (dev < 0 || !s.agents[dev].mask_active) return real_hsa_amd_queue_cu_set_mask(queue, num_cu_mask_count, cu_mask);
+  AgentInfo& a = s.agents[dev];
+  // A user mask (hipExtStreamCreateWithCUMask, ROC_GLOBAL_CU_MASK) may only narrow
+  // the vGPU's partition, never widen it; count 0 means "all CUs" → the vGPU mask.
+  CuMask user;
+  user.nbits = a.cu_count;
+  if (num_cu_mask_count == 0 || !cu_mask) {
+    user = a.mask;
+  } else {
+    for (uint32_t i = 0; i < num_cu_mask_count && i < (uint32_t)kMaxCUs; i++)
+      if ((cu_mask[i / 32] >> (i % 32)) & 1u) user.set((int)i);
+  }
+  CuMask eff = cu_mask_intersect(user, a.mask, a.num_xcc);
+  uint32_t nbits = (uint32_t)((a.cu_count + 31) / 32 * 32);
+  return real_hsa_amd_queue_cu_set_mask(queue, nbits, eff.words);
+}
+
+hsa_status_t hsa_queue_destroy(hsa_queue_t* queue) {
+  VGPU_REAL_HSA(hsa_queue_destroy);
+  if (!real_hsa_queue_destroy) return HSA_STATUS_ERROR;
+  ShimState& s = shim();
+  if (s.phase.load(std::memory_order_relaxed) == 2) {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    s.queues.erase(reinterpret_cast<uintptr_t>(queue));
+  }
+  return real_hsa_queue_destroy(queue);
+}
+
+}  // extern "C"

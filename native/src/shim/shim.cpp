@@ -1,0 +1,319 @@
+// Shim lifecycle: lazy init inside hsa_init, fork/exit handling, launch gates.
+#include "shim.h"
+
+#include <pthread.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <vector>
+
+#include "real.h"
+#include "vgpu/devmap.h"
+#include "vgpu/kfd.h"
+#include "vgpu/log.h"
+#include "vgpu/ratelimit.h"
+
+namespace vgpu {
+
+ShimState& shim() {
+  static ShimState* s = new ShimState();  // never destroyed: hooks may run during exit
+  return *s;
+}
+
+namespace {
+
+struct AgentScan {
+  ShimState* s;
+  hsa_agent_t cpus[kMaxDevices];
+  int n_cpu;
+};
+
+hsa_status_t pool_cb(hsa_amd_memory_pool_t pool, void* data) {
+  AgentInfo* a = static_cast<AgentInfo*>(data);
+  VGPU_REAL_HSA(hsa_amd_memory_pool_get_info);
+  hsa_amd_segment_t seg;
+  if (real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
+  if (a->n_pools < 8) a->pools[a->n_pools++] = pool;
+  size_t sz = 0;
+  uint32_t flags = 0;
+  real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SIZE, &sz);
+  real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && sz > a->phys_total) a->phys_total = sz;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t cpu_pool_cb(hsa_amd_memory_pool_t pool, void* data) {
+  AgentInfo* a = static_cast<AgentInfo*>(data);
+  VGPU_REAL_HSA(hsa_amd_memory_pool_get_info);
+  hsa_amd_segment_t seg;
+  uint32_t flags = 0;
+  bool alloc_ok = false;
+  if (real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc_ok);
+  if (!alloc_ok || (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT)) return HSA_STATUS_SUCCESS;
+  // Prefer coarse-grained host memory for spill (no coherence traffic); a fine
+  // grained pool is the fallback.
+  if (!a->spill_pool.handle || (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED)) a->spill_pool = pool;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t agent_cb(hsa_agent_t agent, void* data) {
+  AgentScan* sc = static_cast<AgentScan*>(data);
+  VGPU_REAL_HSA(hsa_agent_get_info);
+  hsa_device_type_t type;
+  if (real_hsa_agent_get_info(agent, HSA_AGENT_INFO_DEVICE, &type) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (type == HSA_DEVICE_TYPE_CPU) {
+    if (sc->n_cpu < kMaxDevices) sc->cpus[sc->n_cpu++] = agent;
+    return HSA_STATUS_SUCCESS;
+  }
+  if (type != HSA_DEVICE_TYPE_GPU || sc->s->n_agents >= kMaxDevices) return HSA_STATUS_SUCCESS;
+  AgentInfo& a = sc->s->agents[sc->s->n_agents++];
+  a.agent = agent;
+  uint32_t v = 0;
+  if (real_hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT, &v) == HSA_STATUS_SUCCESS)
+    a.cu_count = (int)v;
+  v = 1;
+  if (real_hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_NUM_XCC, &v) == HSA_STATUS_SUCCESS && v)
+    a.num_xcc = (int)v;
+  v = 0;
+  if (real_hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DRIVER_UID, &v) == HSA_STATUS_SUCCESS)
+    a.gpu_id = v;
+  v = 0;
+  if (real_hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MAX_WAVES_PER_CU, &v) == HSA_STATUS_SUCCESS && v)
+    a.max_waves_per_cu = (int)v;
+  hsa_agent_t cpu{0};
+  if (real_hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_NEAREST_CPU, &cpu) == HSA_STATUS_SUCCESS)
+    a.cpu_agent = cpu;
+  VGPU_REAL_HSA(hsa_amd_agent_iterate_memory_pools);
+  real_hsa_amd_agent_iterate_memory_pools(agent, pool_cb, &a);
+  return HSA_STATUS_SUCCESS;
+}
+
+void on_signal_suspend(int) {
+  ShimState& s = shim();
+  if (s.slot >= 0 && s.region.attached()) s.region.raw()->procs[s.slot].status.store(kProcSuspended);
+}
+void on_signal_resume(int) {
+  ShimState& s = shim();
+  if (s.slot >= 0 && s.region.attached()) s.region.raw()->procs[s.slot].status.store(kProcRunning);
+}
+
+void atfork_child() {
+  // A forked child is a different process: it must not inherit the parent's slot
+  // or allocation records (reference: child_reinit_flag). ROCr state does not
+  // survive fork either, so the child re-initialises if it calls hsa_init again.
+  ShimState& s = shim();
+  s.slot = -1;
+  s.active = false;
+  s.allocs.clear();
+  s.vmem.clear();
+  s.queues.clear();
+  s.watcher_started.store(false);
+  s.phase.store(0);
+  s.pid = getpid();
+}
+
+void on_exit() {
+  ShimState& s = shim();
+  s.exiting.store(true);
+  if (s.slot >= 0 && s.region.attached() && s.pid == getpid()) {
+    // Reference exit_handler [475-494]: release the slot and its charges.
+    s.region.unregister_process(s.slot);
+    s.slot = -1;
+  }
+}
+
+void load_env_config() {
+  log_init_from_env();
+  const char* ovr = getenv("VGPU_OVERRIDE_ENV_FILE");
+  int n = apply_override_env_file(ovr && *ovr ? ovr : "/vgpu/override.env");
+  if (n) log_init_from_env();
+  load_config(&mutable_config());
+  if (n) VLOG_INFO("applied %d override env entries", n);
+}
+
+}  // namespace
+
+int agent_ordinal(hsa_agent_t a) {
+  ShimState& s = shim();
+  for (int i = 0; i < s.n_agents; i++)
+    if (s.agents[i].agent.handle == a.handle) return i;
+  return -1;
+}
+
+int pool_ordinal(hsa_amd_memory_pool_t p) {
+  ShimState& s = shim();
+  for (int i = 0; i < s.n_agents; i++)
+    for (int j = 0; j < s.agents[i].n_pools; j++)
+      if (s.agents[i].pools[j].handle == p.handle) return i;
+  return -1;
+}
+
+bool shim_attach_region_only() {
+  ShimState& s = shim();
+  if (s.region.attached()) return true;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    load_env_config();
+    const Config& cfg = config();
+    if (cfg.disabled) return;
+    shim().region.attach(cfg.shared_cache.c_str(), &cfg, true);
+  });
+  return s.region.attached();
+}
+
+void shim_init_after_hsa() {
+  ShimState& s = shim();
+  int expected = 0;
+  if (!s.phase.compare_exchange_strong(expected, 1)) {
+    while (s.phase.load() == 1) {
+      struct timespec ts = {0, 1000000};
+      nanosleep(&ts, nullptr);
+    }
+    return;
+  }
+  s.pid = getpid();
+  load_env_config();
+  const Config& cfg = config();
+  if (cfg.disabled) {
+    s.phase.store(3);
+    return;
+  }
+
+  AgentScan sc{&s, {}, 0};
+  s.n_agents = 0;
+  VGPU_REAL_HSA(hsa_iterate_agents);
+  if (real_hsa_iterate_agents) real_hsa_iterate_agents(agent_cb, &sc);
+  for (int i = 0; i < s.n_agents; i++) {
+    AgentInfo& a = s.agents[i];
+    if (!a.cpu_agent.handle && sc.n_cpu) a.cpu_agent = sc.cpus[0];
+    if (a.cpu_agent.handle) {
+      VGPU_REAL_HSA(hsa_amd_agent_iterate_memory_pools);
+      real_hsa_amd_agent_iterate_memory_pools(a.cpu_agent, cpu_pool_cb, &a);
+    }
+  }
+
+  // Resolve the vGPU map onto the visible agents.
+  char uuids[kMaxDevices][64];
+  const char* uuid_ptrs[kMaxDevices];
+  VGPU_REAL_HSA(hsa_agent_get_info);
+  for (int i = 0; i < s.n_agents; i++) {
+    uuids[i][0] = 0;
+    real_hsa_agent_get_info(s.agents[i].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_UUID, uuids[i]);
+    uuids[i][63] = 0;
+    uuid_ptrs[i] = uuids[i];
+  }
+  DeviceMap map;
+  const char* map_env = getenv("VGPU_DEVICE_MAP");
+  if (!parse_device_map(map_env, &map)) {
+    VLOG_WARN("invalid VGPU_DEVICE_MAP=%s, using positional limits", map_env);
+    map = DeviceMap();
+  }
+  Config resolved = cfg;
+  DeviceConfig per_agent[kMaxDevices];
+  resolve_devices(cfg, map, uuid_ptrs, s.n_agents, per_agent);
+  for (int i = 0; i < kMaxDevices; i++) resolved.dev[i] = i < s.n_agents ? per_agent[i] : DeviceConfig();
+  resolved.num_devices = s.n_agents;
+
+  // Host PID: sysfs is not PID-namespaced; outside a container it equals getpid().
+  if (!s.hostpid) {
+    std::vector<int> pids = kfd_list_pids();
+    if (std::binary_search(pids.begin(), pids.end(), (int)s.pid)) s.hostpid = s.pid;
+  }
+
+  int rc = s.region.attach(cfg.shared_cache.c_str(), &resolved, true);
+  if (rc != 0) {
+    VLOG_ERROR("cannot attach shared region %s (%s); limits are NOT enforced", cfg.shared_cache.c_str(),
+               strerror(-rc));
+    s.phase.store(3);
+    return;
+  }
+  Region* r = s.region.raw();
+  s.region.lock();
+  if (r->hdr.num_devices < s.n_agents) r->hdr.num_devices = s.n_agents;
+  for (int i = 0; i < s.n_agents; i++) {
+    AgentInfo& a = s.agents[i];
+    DeviceState& d = r->dev[i];
+    if (!d.configured) {
+      snprintf(d.uuid, sizeof(d.uuid), "%s", uuids[i]);
+      d.phys_total = a.phys_total;
+      d.cu_count = a.cu_count;
+      d.num_xcc = a.num_xcc;
+      d.gpu_id = a.gpu_id;
+      VGPU_REAL_HSA(hsa_agent_get_info);
+      uint32_t bdf = 0, dom = 0;
+      real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+      real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+      d.bdf = bdf;
+      d.domain = dom;
+      if (!d.mem_limit && per_agent[i].mem_limit) d.mem_limit = per_agent[i].mem_limit;
+      if (!d.cu_limit_pct && per_agent[i].cu_limit_pct) d.cu_limit_pct = per_agent[i].cu_limit_pct;
+      CuMask m = cu_mask_for(a.cu_count, a.num_xcc, d.cu_limit_pct, per_agent[i].cu_range_begin,
+                             per_agent[i].cu_range_end);
+      memcpy(d.cu_mask, m.words, sizeof(d.cu_mask));
+      d.cu_mask_bits = m.nbits;
+      LimiterSpec spec{a.cu_count, a.max_waves_per_cu * 64};
+      d.token_cap.store(spec.total());
+      d.tokens.store(spec.total());
+      d.share.store(spec.total() / 10);
+      d.configured = 1;
+    }
+    memcpy(a.mask.words, d.cu_mask, sizeof(a.mask.words));
+    a.mask.nbits = d.cu_mask_bits ? d.cu_mask_bits : a.cu_count;
+    bool limited = d.cu_limit_pct > 0 && d.cu_limit_pct < 100;
+    bool spatial = cfg.cu_mode == CuMode::kSpatial || cfg.cu_mode == CuMode::kBoth;
+    bool temporal = cfg.cu_mode == CuMode::kTemporal || cfg.cu_mode == CuMode::kBoth;
+    bool force = cfg.cu_policy == CuPolicy::kForce, off = cfg.cu_policy == CuPolicy::kDisable;
+    a.mask_active = !off && spatial && (limited || per_agent[i].cu_range_begin >= 0) &&
+                    a.mask.count() < a.cu_count && a.mask.count() > 0;
+    a.temporal_active = !off && temporal && (limited || force);
+  }
+  s.region.unlock();
+
+  s.slot = s.region.register_process(s.pid, s.hostpid, cfg.priority);
+  s.active = s.slot >= 0;
+  if (cfg.signal_control) {
+    signal(SIGUSR2, on_signal_suspend);
+    signal(SIGUSR1, on_signal_resume);
+  }
+  static std::once_flag hooks_once;
+  std::call_once(hooks_once, [] {
+    pthread_atfork(nullptr, nullptr, atfork_child);
+    atexit(on_exit);
+  });
+  for (int i = 0; i < s.n_agents; i++) {
+    const DeviceState& d = r->dev[i];
+    VLOG_INFO("device %d uuid=%s gpu_id=%u cus=%d xcc=%d limit=%lu MiB cu_limit=%d%% mask=%d CUs%s%s", i, d.uuid,
+              s.agents[i].gpu_id, s.agents[i].cu_count, s.agents[i].num_xcc, (unsigned long)(d.mem_limit >> 20),
+              d.cu_limit_pct, s.agents[i].mask.count(), s.agents[i].mask_active ? " [spatial]" : "",
+              s.agents[i].temporal_active ? " [temporal]" : "");
+  }
+  s.phase.store(2);
+  start_watcher_if_needed();
+}
+
+void gate_suspend_slow() {
+  ShimState& s = shim();
+  uint64_t t0 = now_ns();
+  bool logged = false;
+  struct timespec ts = {0, 1000000};
+  while (gate_needed()) {
+    if (!logged) {
+      VLOG_INFO("process suspended by controller; waiting");
+      logged = true;
+    }
+    nanosleep(&ts, nullptr);
+  }
+  if (s.slot >= 0) s.region.raw()->procs[s.slot].suspend_ns.fetch_add(now_ns() - t0);
+}
+
+}  // namespace vgpu

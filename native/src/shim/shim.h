@@ -1,0 +1,96 @@
+// Process-wide state of the interception shim (libvgpu_hip.so).
+//
+// Reference init sequence: cuInit → preInit (load real driver
+// table, nvmlInit, /overrideEnv, device map, shared region, visible devices) →
+// real cuInit → postInit (allocmode, allocator, virtual PCI ids, host-PID discovery,
+// utilisation watcher). Here the equivalent runs inside the hsa_init hook: every
+// HIP program initialises ROCr exactly there, and the shim stays inert in processes
+// that never touch the GPU (it is force-preloaded into every container process).
+#pragma once
+
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <atomic>
+#include <cstdint>
+#include <mutex>
+#include <unordered_map>
+
+#include "vgpu/config.h"
+#include "vgpu/cumask.h"
+#include "vgpu/region.h"
+
+namespace vgpu {
+
+struct AgentInfo {
+  hsa_agent_t agent{0};
+  hsa_agent_t cpu_agent{0};          // nearest CPU agent (host-spill pool owner)
+  hsa_amd_memory_pool_t spill_pool{0};
+  uint32_t gpu_id = 0;               // KFD gpu_id
+  int cu_count = 0;
+  int num_xcc = 1;
+  int max_waves_per_cu = 32;
+  uint64_t phys_total = 0;
+  bool mask_active = false;          // spatial mask applied to its queues
+  bool temporal_active = false;      // token bucket gates its launches
+  bool context_charged = false;
+  CuMask mask;
+  hsa_amd_memory_pool_t pools[8]{};  // GPU-local pools of this agent
+  int n_pools = 0;
+};
+
+struct AllocRec {
+  uint64_t size;
+  int dev;
+  int kind;
+};
+
+struct ShimState {
+  std::atomic<int> phase{0};         // 0 = not initialised, 1 = initialising, 2 = ready, 3 = inert
+  bool active = false;               // accounting + gates enabled
+  SharedRegion region;
+  int slot = -1;
+  pid_t pid = 0;
+  pid_t hostpid = 0;
+  int n_agents = 0;
+  AgentInfo agents[kMaxDevices];
+  std::mutex alloc_mu;
+  std::unordered_map<uintptr_t, AllocRec> allocs;   // device pointer → record
+  std::unordered_map<uint64_t, AllocRec> vmem;      // vmem handle → record
+  std::unordered_map<uintptr_t, int> queues;        // hsa_queue_t* → ordinal
+  std::atomic<bool> exiting{false};
+  std::atomic<bool> watcher_started{false};
+};
+
+ShimState& shim();
+
+// Runs the one-time initialisation (after ROCr is up). Safe to call repeatedly.
+void shim_init_after_hsa();
+// Lightweight attach for processes that never initialise ROCr (e.g. amd-smi).
+bool shim_attach_region_only();
+
+// Ordinal of a GPU agent / pool, or -1.
+int agent_ordinal(hsa_agent_t a);
+int pool_ordinal(hsa_amd_memory_pool_t p);
+
+// Suspend gate: blocks while the container is suspended (reference wait_status_self).
+void gate_suspend_slow();
+inline bool gate_needed() {
+  ShimState& s = shim();
+  if (__builtin_expect(!s.active || s.slot < 0, 1)) return false;
+  Region* r = s.region.raw();
+  return r->hdr.suspend_all.load(std::memory_order_relaxed) ||
+         r->procs[s.slot].status.load(std::memory_order_relaxed) == kProcSuspended;
+}
+inline void gate_suspend() {
+  if (__builtin_expect(gate_needed(), 0)) gate_suspend_slow();
+}
+
+// Kernel-launch gate: suspend check + temporal token bucket for device `dev`
+// (dev < 0 = current HIP device).
+void gate_launch(int64_t workgroups, int dev);
+
+// Utilisation watcher (temporal mode, monitor-based OOM killer, memory override).
+void start_watcher_if_needed();
+
+}  // namespace vgpu

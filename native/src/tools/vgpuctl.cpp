@@ -1,0 +1,82 @@
+// vgpuctl: inspect and control a container's shared region from the node.
+//
+// The reference exposes this control surface only as symbols of libvgpu.so
+// (suspend_all, resume_all, set_current_device_sm_limit_scale, ...) for an
+// out-of-tree monitor (observability). This is the in-tree tool.
+//
+//   vgpuctl <region> show                 JSON dump (devices + processes)
+//   vgpuctl <region> suspend|resume       block / unblock every gate
+//   vgpuctl <region> block|unblock        launch block (recent_kernel < 0)
+//   vgpuctl <region> set-limit <dev> <size>
+//   vgpuctl <region> set-cu <dev> <pct>
+//   vgpuctl <region> priority <n>
+//   vgpuctl <region> reclaim              free slots of exited processes
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "vgpu/region_api.h"
+
+static int usage() {
+  fprintf(stderr,
+          "usage: vgpuctl <region-file> show|suspend|resume|block|unblock|reclaim|"
+          "set-limit <dev> <size>|set-cu <dev> <pct>|priority <n>\n");
+  return 2;
+}
+
+static void show(vgpu_region* r) {
+  printf("{\"version\": %u, \"num_devices\": %d, \"suspended\": %d, \"priority\": %d, \"recent_kernel\": %d,\n",
+         vgpu_region_version(), vgpu_region_num_devices(r), vgpu_region_suspended(r), vgpu_region_get_priority(r),
+         vgpu_region_get_recent_kernel(r));
+  printf(" \"devices\": [");
+  int nd = vgpu_region_num_devices(r);
+  for (int d = 0; d < nd; d++) {
+    vgpu_device_info di;
+    vgpu_region_device_info(r, d, &di);
+    printf("%s\n  {\"index\": %d, \"uuid\": \"%s\", \"mem_limit\": %llu, \"phys_total\": %llu, \"used\": %llu, "
+           "\"spilled\": %llu, \"monitor_used\": %llu, \"cu_limit_pct\": %d, \"cu_count\": %d, \"cu_mask_count\": %d, "
+           "\"util_pct\": %d, \"tokens\": %lld, \"share\": %lld}",
+           d ? "," : "", d, di.uuid, (unsigned long long)di.mem_limit, (unsigned long long)di.phys_total,
+           (unsigned long long)di.used, (unsigned long long)di.spilled, (unsigned long long)di.monitor_used,
+           di.cu_limit_pct, di.cu_count, di.cu_mask_count, di.util_pct, (long long)di.tokens, (long long)di.share);
+  }
+  printf("],\n \"processes\": [");
+  static vgpu_proc_info procs[1024];
+  int np = vgpu_region_procs(r, procs, 1024);
+  for (int i = 0; i < np; i++) {
+    const vgpu_proc_info& p = procs[i];
+    printf("%s\n  {\"pid\": %d, \"hostpid\": %d, \"status\": %d, \"launches\": %llu, \"throttle_ns\": %llu, "
+           "\"suspend_ns\": %llu, \"oom_events\": %llu, \"used\": [",
+           i ? "," : "", p.pid, p.hostpid, p.status, (unsigned long long)p.launches,
+           (unsigned long long)p.throttle_ns, (unsigned long long)p.suspend_ns, (unsigned long long)p.oom_events);
+    for (int d = 0; d < (nd ? nd : 1); d++) printf("%s%llu", d ? ", " : "", (unsigned long long)p.used[d]);
+    printf("]}");
+  }
+  printf("]}\n");
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) return usage();
+  int err = 0;
+  vgpu_region* r = vgpu_region_open(argv[1], 0, &err);
+  if (!r) {
+    fprintf(stderr, "vgpuctl: cannot open region %s: %s\n", argv[1], strerror(-err));
+    return 1;
+  }
+  const char* cmd = argv[2];
+  int rc = 0;
+  if (!strcmp(cmd, "show")) show(r);
+  else if (!strcmp(cmd, "suspend")) rc = vgpu_region_suspend_all(r);
+  else if (!strcmp(cmd, "resume")) rc = vgpu_region_resume_all(r);
+  else if (!strcmp(cmd, "block")) rc = vgpu_region_set_recent_kernel(r, -1);
+  else if (!strcmp(cmd, "unblock")) rc = vgpu_region_set_recent_kernel(r, 2);
+  else if (!strcmp(cmd, "reclaim")) printf("%d\n", vgpu_region_reclaim(r));
+  else if (!strcmp(cmd, "set-limit") && argc == 5) {
+    int64_t v = vgpu_parse_size(argv[4]);
+    rc = v < 0 ? -1 : vgpu_region_set_memory_limit(r, atoi(argv[3]), (uint64_t)v);
+  } else if (!strcmp(cmd, "set-cu") && argc == 5) rc = vgpu_region_set_cu_limit(r, atoi(argv[3]), atoi(argv[4]));
+  else if (!strcmp(cmd, "priority") && argc == 4) rc = vgpu_region_set_priority(r, atoi(argv[3]));
+  else rc = usage();
+  vgpu_region_close(r);
+  return rc == 0 ? 0 : 1;
+}

@@ -1,0 +1,508 @@
+// Native unit tests of the shim core (no GPU). Driven by tests/test_native_core.py;
+// run one case with `vgpu_core_tests <name>` or all with no argument.
+// Built plain and with -fsanitize=thread / address (make SAN=thread|address).
+#include <signal.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "vgpu/config.h"
+#include "vgpu/cumask.h"
+#include "vgpu/devmap.h"
+#include "vgpu/kfd.h"
+#include "vgpu/ratelimit.h"
+#include "vgpu/region.h"
+
+using namespace vgpu;
+
+static int g_failures = 0;
+#define CHECK(cond)                                                              \
+  do {                                                                           \
+    if (!(cond)) {                                                               \
+      fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond);    \
+      g_failures++;                                                              \
+    }                                                                            \
+  } while (0)
+#define CHECK_EQ(a, b)                                                                              \
+  do {                                                                                              \
+    auto _a = (a);                                                                                  \
+    auto _b = (b);                                                                                  \
+    if (!(_a == _b)) {                                                                              \
+      fprintf(stderr, "CHECK_EQ failed %s:%d: %s (%lld) != %s (%lld)\n", __FILE__, __LINE__, #a,    \
+              (long long)_a, #b, (long long)_b);                                                    \
+      g_failures++;                                                                                 \
+    }                                                                                               \
+  } while (0)
+
+static std::string tmp_region(const char* tag) {
+  char buf[256];
+  snprintf(buf, sizeof(buf), "/tmp/vgpu_core_test_%s_%d.cache", tag, (int)getpid());
+  unlink(buf);
+  return buf;
+}
+
+static std::map<std::string, const char*> g_env;
+static const char* fake_getenv(const char* k) {
+  auto it = g_env.find(k);
+  return it == g_env.end() ? nullptr : it->second;
+}
+
+static void test_parse_size() {
+  uint64_t v = 0;
+  CHECK(parse_size("1024", &v) && v == 1024);
+  CHECK(parse_size("73728m", &v) && v == 73728ull << 20);
+  CHECK(parse_size("16G", &v) && v == 16ull << 30);
+  CHECK(parse_size("4k", &v) && v == 4096);
+  CHECK(parse_size("2GiB", &v) && v == 2ull << 30);
+  CHECK(parse_size("10MB", &v) && v == 10ull << 20);
+  CHECK(!parse_size("", &v));
+  CHECK(!parse_size("-5m", &v));
+  CHECK(!parse_size("12x", &v));
+  CHECK(!parse_size("99999999999999999999", &v));
+  CHECK(!parse_size("17179869184T", &v));  // overflow after shift
+}
+
+static void test_parse_range() {
+  int b = 0, e = 0;
+  CHECK(parse_range("64-128", &b, &e) && b == 64 && e == 128);
+  CHECK(parse_range("32:64", &b, &e) && b == 32 && e == 96);
+  CHECK(!parse_range("128-64", &b, &e));
+  CHECK(!parse_range("0-300", &b, &e));
+  CHECK(!parse_range("abc", &b, &e));
+}
+
+static void test_config() {
+  g_env.clear();
+  g_env["VGPU_DEVICE_MEMORY_LIMIT_0"] = "73728m";
+  g_env["VGPU_DEVICE_MEMORY_LIMIT_1"] = "36864m";
+  g_env["VGPU_DEVICE_CU_LIMIT"] = "25";
+  g_env["VGPU_DEVICE_CU_RANGE_1"] = "64-128";
+  g_env["VGPU_SHARED_CACHE"] = "/tmp/x.cache";
+  g_env["VGPU_OVERSUBSCRIBE"] = "true";
+  g_env["VGPU_TASK_PRIORITY"] = "3";
+  g_env["VGPU_CU_MODE"] = "temporal";
+  g_env["VGPU_CU_POLICY"] = "FORCE";
+  g_env["VGPU_ACTIVE_OOM_KILLER"] = "1";
+  Config c;
+  load_config(&c, fake_getenv);
+  CHECK_EQ(c.num_devices, 2);
+  CHECK_EQ(c.dev[0].mem_limit, 73728ull << 20);
+  CHECK_EQ(c.dev[1].mem_limit, 36864ull << 20);
+  CHECK_EQ(c.dev[0].cu_limit_pct, 25);
+  CHECK_EQ(c.dev[1].cu_range_begin, 64);
+  CHECK_EQ(c.dev[1].cu_range_end, 128);
+  CHECK(c.shared_cache == "/tmp/x.cache");
+  CHECK(c.oversubscribe);
+  CHECK_EQ(c.priority, 3);
+  CHECK(c.cu_mode == CuMode::kTemporal);
+  CHECK(c.cu_policy == CuPolicy::kForce);
+  CHECK(c.active_oom_killer);
+  CHECK(c.any_memory_limit() && c.any_cu_limit());
+  // Global fallback and invalid values.
+  g_env.clear();
+  g_env["VGPU_DEVICE_MEMORY_LIMIT"] = "1g";
+  g_env["VGPU_DEVICE_MEMORY_LIMIT_3"] = "garbage";
+  g_env["VGPU_DEVICE_CU_LIMIT"] = "150";
+  load_config(&c, fake_getenv);
+  CHECK_EQ(c.dev[3].mem_limit, 1ull << 30);
+  CHECK_EQ(c.dev[7].mem_limit, 1ull << 30);
+  CHECK_EQ(c.dev[0].cu_limit_pct, 0);
+  CHECK(!c.oversubscribe);
+  CHECK(c.cu_mode == CuMode::kSpatial);
+}
+
+static void test_override_file() {
+  std::string p = tmp_region("override");
+  FILE* f = fopen(p.c_str(), "w");
+  fprintf(f, "# comment\nVGPU_TEST_OVR_A=1\nexport VGPU_TEST_OVR_B=hello world\n\nbad line\n");
+  fclose(f);
+  CHECK_EQ(apply_override_env_file(p.c_str()), 2);
+  CHECK(!strcmp(getenv("VGPU_TEST_OVR_A"), "1"));
+  CHECK(!strcmp(getenv("VGPU_TEST_OVR_B"), "hello world"));
+  CHECK_EQ(apply_override_env_file("/nonexistent/file"), 0);
+  unlink(p.c_str());
+}
+
+static Config limits_cfg(uint64_t lim0) {
+  Config c;
+  c.dev[0].mem_limit = lim0;
+  c.num_devices = 1;
+  return c;
+}
+
+static void test_region_basic() {
+  std::string p = tmp_region("basic");
+  Config c = limits_cfg(1000);
+  SharedRegion r;
+  CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+  CHECK_EQ(r.limit(0), 1000u);
+  int s = r.register_process(getpid(), getpid(), 1);
+  CHECK(s >= 0);
+  CHECK(r.charge(s, 0, 600, kMemData) == Charge::kOk);
+  CHECK(r.charge(s, 0, 500, kMemData) == Charge::kOverLimit);
+  CHECK(r.charge(s, 0, 400, kMemData) == Charge::kOk);
+  CHECK_EQ(r.usage(0), 1000u);
+  r.uncharge(s, 0, 600, kMemData);
+  CHECK_EQ(r.usage(0), 400u);
+  CHECK_EQ(r.proc_usage(s, 0), 400u);
+  CHECK_EQ(r.raw()->procs[s].used[0].peak.load(), 1000u);
+  CHECK_EQ(r.raw()->procs[s].oom_events.load(), 1u);
+  // A second attach sees the same state; env limits do not override stored ones.
+  Config c2 = limits_cfg(5000);
+  SharedRegion r2;
+  CHECK_EQ(r2.attach(p.c_str(), &c2, true), 0);
+  CHECK_EQ(r2.limit(0), 1000u);
+  CHECK_EQ(r2.usage(0), 400u);
+  // Unregister releases the slot's charges.
+  r.unregister_process(s);
+  CHECK_EQ(r2.usage(0), 0u);
+  CHECK_EQ(r2.raw()->hdr.proc_num.load(), 0);
+  // Control API.
+  r2.set_limit(0, 2000);
+  CHECK_EQ(r.limit(0), 2000u);
+  r2.suspend_all();
+  CHECK_EQ(r.raw()->hdr.suspend_all.load(), 1);
+  r2.resume_all();
+  CHECK_EQ(r.raw()->hdr.suspend_all.load(), 0);
+  // Attach without create to a missing file fails.
+  SharedRegion r3;
+  CHECK(r3.attach("/tmp/vgpu_core_test_missing.cache", nullptr, false) < 0);
+  unlink(p.c_str());
+}
+
+static void test_region_unlimited_and_kinds() {
+  std::string p = tmp_region("kinds");
+  Config c = limits_cfg(0);
+  SharedRegion r;
+  CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+  int s = r.register_process(getpid(), 0, 1);
+  CHECK(r.charge(s, 0, 1ull << 40, kMemData) == Charge::kOk);
+  r.force_charge(s, 0, 100, kMemSpill);
+  CHECK_EQ(r.raw()->dev[0].spilled.load(), 100u);
+  r.uncharge(s, 0, 100, kMemSpill);
+  CHECK_EQ(r.raw()->dev[0].spilled.load(), 0u);
+  // Uncharging more than charged saturates instead of wrapping.
+  r.uncharge(s, 0, (1ull << 40) + 12345, kMemData);
+  CHECK_EQ(r.usage(0), 0u);
+  r.unregister_process(s);
+  unlink(p.c_str());
+}
+
+static void test_region_threads_never_overshoot() {
+  std::string p = tmp_region("threads");
+  const uint64_t limit = 1000000;
+  Config c = limits_cfg(limit);
+  SharedRegion r;
+  CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+  int s = r.register_process(getpid(), 0, 1);
+  std::atomic<uint64_t> granted{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 8; t++) {
+    th.emplace_back([&] {
+      for (int i = 0; i < 20000; i++) {
+        if (r.charge(s, 0, 7, kMemData) == Charge::kOk) {
+          granted.fetch_add(7);
+          if (i % 3 == 0) {
+            r.uncharge(s, 0, 7, kMemData);
+            granted.fetch_sub(7);
+          }
+        }
+        CHECK(r.usage(0) <= limit);
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  CHECK_EQ(r.usage(0), granted.load());
+  CHECK(r.usage(0) <= limit);
+  r.unregister_process(s);
+  unlink(p.c_str());
+}
+
+static void test_region_multiprocess_and_reclaim() {
+  std::string p = tmp_region("mp");
+  Config c = limits_cfg(1000);
+  SharedRegion r;
+  CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+  // Children charge and exit without unregistering (crash): reclaim must free it.
+  for (int k = 0; k < 4; k++) {
+    pid_t pid = fork();
+    if (pid == 0) {
+      SharedRegion rc;
+      if (rc.attach(p.c_str(), nullptr, false) != 0) _exit(2);
+      int s = rc.register_process(getpid(), 0, 1);
+      if (s < 0) _exit(3);
+      _exit(rc.charge(s, 0, 200, kMemData) == Charge::kOk ? 0 : 4);
+    }
+    int st = 0;
+    waitpid(pid, &st, 0);
+    CHECK(WIFEXITED(st) && WEXITSTATUS(st) == 0);
+  }
+  CHECK_EQ(r.usage(0), 800u);
+  CHECK_EQ(r.raw()->hdr.proc_num.load(), 4);
+  // Over the limit: charge() reclaims the dead slots and retries (reference oom_check).
+  int s = r.register_process(getpid(), 0, 1);
+  CHECK(r.charge(s, 0, 900, kMemData) == Charge::kOk);
+  CHECK_EQ(r.usage(0), 900u);
+  CHECK_EQ(r.raw()->hdr.proc_num.load(), 1);
+  CHECK_EQ(r.reclaim_dead(), 0);
+  r.unregister_process(s);
+  unlink(p.c_str());
+}
+
+static void test_region_robust_lock() {
+  std::string p = tmp_region("robust");
+  Config c = limits_cfg(1000);
+  SharedRegion r;
+  CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+  pid_t pid = fork();
+  if (pid == 0) {
+    SharedRegion rc;
+    if (rc.attach(p.c_str(), nullptr, false) != 0) _exit(2);
+    rc.lock();
+    _exit(0);  // dies holding the lock
+  }
+  int st = 0;
+  waitpid(pid, &st, 0);
+  CHECK(r.lock());  // EOWNERDEAD → consistent
+  r.unlock();
+  CHECK(r.lock());
+  r.unlock();
+  unlink(p.c_str());
+}
+
+static void test_region_version_guard() {
+  std::string p = tmp_region("ver");
+  Config c = limits_cfg(1);
+  {
+    SharedRegion r;
+    CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+    r.raw()->hdr.version = 999;
+  }
+  SharedRegion r2;
+  CHECK(r2.attach(p.c_str(), &c, true) < 0);
+  unlink(p.c_str());
+}
+
+static void test_proc_alive() {
+  CHECK(proc_alive(getpid(), proc_start_time(getpid())));
+  CHECK(!proc_alive(getpid(), proc_start_time(getpid()) + 1));
+  pid_t pid = fork();
+  if (pid == 0) _exit(0);
+  int st;
+  waitpid(pid, &st, 0);
+  CHECK(!proc_alive(pid, 0));
+}
+
+static void test_cumask() {
+  CHECK_EQ(cu_share_count(256, 8, 25), 64);
+  CHECK_EQ(cu_share_count(256, 8, 50), 128);
+  CHECK_EQ(cu_share_count(256, 8, 33), 80);    // 84.48 → 80 (multiple of 8)
+  CHECK_EQ(cu_share_count(256, 8, 1), 8);      // at least one CU per XCC
+  CHECK_EQ(cu_share_count(256, 8, 0), 256);
+  CHECK_EQ(cu_share_count(256, 8, 100), 256);
+  CuMask m = cu_mask_for(256, 8, 25, -1, -1);
+  CHECK_EQ(m.count(), 64);
+  CHECK(m.test(0) && m.test(63) && !m.test(64));
+  CHECK(cu_mask_balanced(m, 8));
+  CuMask r = cu_mask_range(256, 8, 3, 61);  // snapped to [0,64)
+  CHECK_EQ(r.count(), 64);
+  // Partition 256 CUs among 3 tenants: 88/88/80, disjoint, covering.
+  int b[3], e[3];
+  for (int i = 0; i < 3; i++) cu_partition_range(256, 8, 3, i, &b[i], &e[i]);
+  CHECK_EQ(b[0], 0);
+  CHECK_EQ(e[0] - b[0], 88);
+  CHECK_EQ(b[1], e[0]);
+  CHECK_EQ(e[1] - b[1], 88);
+  CHECK_EQ(b[2], e[1]);
+  CHECK_EQ(e[2], 256);
+  for (int split = 1; split <= 32; split++) {
+    int covered = 0, prev_end = 0;
+    for (int i = 0; i < split; i++) {
+      int bb, ee;
+      cu_partition_range(256, 8, split, i, &bb, &ee);
+      CHECK_EQ(bb, prev_end);
+      CHECK(ee > bb);
+      CHECK_EQ((ee - bb) % 8, 0);
+      CHECK(cu_mask_balanced(cu_mask_range(256, 8, bb, ee), 8));
+      covered += ee - bb;
+      prev_end = ee;
+    }
+    CHECK_EQ(covered, 256);
+  }
+  // Unbalanced masks.
+  CuMask u;
+  u.nbits = 256;
+  u.set(0);
+  CHECK(!cu_mask_balanced(u, 8));
+  // Intersection: a user mask cannot escape the vGPU; an unbalanced result falls back.
+  CuMask vg = cu_mask_range(256, 8, 64, 128);
+  CuMask user = cu_mask_range(256, 8, 0, 96);
+  CuMask x = cu_mask_intersect(user, vg, 8);
+  CHECK_EQ(x.count(), 32);
+  CHECK(x.test(64) && !x.test(96) && !x.test(0));
+  CuMask bad = cu_mask_intersect(u, vg, 8);
+  CHECK_EQ(bad.count(), 64);
+}
+
+static void test_devmap() {
+  DeviceMap m;
+  CHECK(parse_device_map("0:GPU-aaaa 1:GPU-bbbb", &m));
+  CHECK_EQ(m.n, 2);
+  CHECK_EQ(m.duplicates, 0);
+  CHECK(parse_device_map("0:GPU-aaaa 1:gpu-AAAA", &m));
+  CHECK_EQ(m.duplicates, 1);
+  CHECK(!parse_device_map("0-GPU", &m));
+  CHECK(!parse_device_map("99:GPU-x", &m));
+  CHECK(parse_device_map("", &m) && m.n == 0);
+  CHECK(parse_device_map(nullptr, &m) && m.n == 0);
+  char u[64];
+  normalize_uuid("GPU-98139BA16298D729", u, sizeof(u));
+  CHECK(!strcmp(u, "98139ba16298d729"));
+
+  Config c;
+  c.dev[0].mem_limit = 100;
+  c.dev[0].cu_limit_pct = 25;
+  c.dev[0].cu_range_begin = 0;
+  c.dev[0].cu_range_end = 64;
+  c.dev[1].mem_limit = 200;
+  c.dev[1].cu_limit_pct = 25;
+  c.dev[1].cu_range_begin = 64;
+  c.dev[1].cu_range_end = 128;
+  c.dev[2].mem_limit = 300;
+  // Map order differs from agent order; vGPUs 0 and 1 share physical GPU bbbb.
+  CHECK(parse_device_map("0:GPU-bbbb 1:GPU-bbbb 2:GPU-aaaa", &m));
+  const char* agents[2] = {"GPU-aaaa", "GPU-bbbb"};
+  DeviceConfig out[kMaxDevices];
+  CHECK_EQ(resolve_devices(c, m, agents, 2, out), 2);
+  CHECK_EQ(out[0].mem_limit, 300u);
+  CHECK_EQ(out[1].mem_limit, 300u);  // 100 + 200 merged
+  CHECK_EQ(out[1].cu_limit_pct, 50);
+  CHECK_EQ(out[1].cu_range_begin, 0);
+  CHECK_EQ(out[1].cu_range_end, 128);
+  // No map: positional.
+  DeviceMap empty;
+  resolve_devices(c, empty, agents, 2, out);
+  CHECK_EQ(out[0].mem_limit, 100u);
+  CHECK_EQ(out[1].mem_limit, 200u);
+}
+
+static void test_ratelimit() {
+  LimiterSpec spec{256, 2048};
+  // Below the limit the share grows, above it shrinks, and stays clamped.
+  int64_t s = limiter_delta(spec, 50, 10, 0);
+  CHECK(s > 0);
+  int64_t s2 = limiter_delta(spec, 50, 90, s);
+  CHECK(s2 < s);
+  CHECK_EQ(limiter_delta(spec, 50, 100, 0), 0);
+  CHECK(limiter_delta(spec, 50, 0, spec.total()) <= spec.total());
+  // Small error still moves by the minimum step (diff clamp 5).
+  CHECK(limiter_delta(spec, 50, 49, 1000) > 1000);
+
+  std::string p = tmp_region("rl");
+  Config c = limits_cfg(0);
+  SharedRegion r;
+  CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+  DeviceState& d = r.raw()->dev[0];
+  d.token_cap.store(1000);
+  d.tokens.store(1000);
+  d.share.store(0);
+  r.raw()->hdr.watcher_heartbeat.store(now_ns());
+  CHECK_EQ(limiter_acquire(r.raw()->hdr, d, 600, 1000000), 0u);
+  CHECK_EQ(d.tokens.load(), 400);
+  // Exhausted bucket blocks until a refill arrives from another thread.
+  std::thread refill([&] {
+    usleep(30000);
+    r.raw()->hdr.watcher_heartbeat.store(now_ns());
+    d.tokens.store(1000);
+  });
+  uint64_t waited = limiter_acquire(r.raw()->hdr, d, 600, 1000000);
+  refill.join();
+  CHECK(waited >= 20000000u);
+  // A dead watcher (stale heartbeat) never blocks launches forever.
+  d.tokens.store(-100000);
+  r.raw()->hdr.watcher_heartbeat.store(now_ns() - 5'000'000'000ull);
+  limiter_acquire(r.raw()->hdr, d, 1, 1000000);
+  // Refill honours the cap and the doubling rule.
+  d.tokens.store(-5);
+  d.share.store(1000);
+  d.token_cap.store(1000);
+  limiter_refill(d, spec, 50, 10);
+  CHECK_EQ(d.token_cap.load(), 2000);
+  CHECK(d.tokens.load() <= 2000);
+  CHECK_EQ(d.util_pct.load(), 10);
+  unlink(p.c_str());
+}
+
+static void test_kfd() {
+  char dir[] = "/tmp/vgpu_kfd_XXXXXX";
+  CHECK(mkdtemp(dir) != nullptr);
+  std::string root = dir;
+  auto mk = [&](const std::string& s) { CHECK(system(("mkdir -p " + root + "/" + s).c_str()) == 0); };
+  mk("100/stats_7");
+  mk("200");
+  FILE* f = fopen((root + "/100/stats_7/cu_occupancy").c_str(), "w");
+  fprintf(f, "64\n");
+  fclose(f);
+  f = fopen((root + "/100/vram_7").c_str(), "w");
+  fprintf(f, "4096\n");
+  fclose(f);
+  g_kfd_proc_root = strdup(root.c_str());
+  std::vector<int> before = kfd_list_pids();
+  CHECK_EQ(before.size(), 2u);
+  mk("300");
+  std::vector<int> after = kfd_list_pids();
+  CHECK_EQ(kfd_diff_pid(before, after), 300);
+  mk("400");
+  CHECK_EQ(kfd_diff_pid(before, kfd_list_pids()), 0);  // ambiguous → unknown
+  CHECK_EQ(kfd_cu_occupancy(100, 7), 64);
+  CHECK_EQ(kfd_vram_usage(100, 7), 4096);
+  CHECK_EQ(kfd_cu_occupancy(100, 8), -1);
+  CHECK(system(("rm -rf " + root).c_str()) == 0);
+  g_kfd_proc_root = "/sys/class/kfd/kfd/proc";
+}
+
+int main(int argc, char** argv) {
+  std::vector<std::pair<const char*, std::function<void()>>> tests = {
+      {"parse_size", test_parse_size},
+      {"parse_range", test_parse_range},
+      {"config", test_config},
+      {"override_file", test_override_file},
+      {"region_basic", test_region_basic},
+      {"region_kinds", test_region_unlimited_and_kinds},
+      {"region_threads", test_region_threads_never_overshoot},
+      {"region_multiprocess", test_region_multiprocess_and_reclaim},
+      {"region_robust_lock", test_region_robust_lock},
+      {"region_version_guard", test_region_version_guard},
+      {"proc_alive", test_proc_alive},
+      {"cumask", test_cumask},
+      {"devmap", test_devmap},
+      {"ratelimit", test_ratelimit},
+      {"kfd", test_kfd},
+  };
+  if (argc > 1 && !strcmp(argv[1], "--list")) {
+    for (auto& t : tests) printf("%s\n", t.first);
+    return 0;
+  }
+  int ran = 0;
+  for (auto& t : tests) {
+    if (argc > 1 && strcmp(argv[1], t.first)) continue;
+    int before = g_failures;
+    t.second();
+    printf("%s %s\n", g_failures == before ? "PASS" : "FAIL", t.first);
+    ran++;
+  }
+  if (!ran) {
+    fprintf(stderr, "no such test\n");
+    return 2;
+  }
+  return g_failures ? 1 : 0;
+}
