@@ -14,23 +14,33 @@ uint64_t now_ns() {
 }
 
 int64_t limiter_delta(const LimiterSpec& spec, int limit_pct, int util_pct, int64_t share) {
-  const int64_t total = spec.total();
-  int64_t diff = std::abs(limit_pct - util_pct);
-  if (diff < 5) diff = 5;
-  int64_t inc = (int64_t)spec.cu_count * spec.cu_count * spec.max_threads_per_cu * diff / 2560;
-  if (diff > limit_pct / 2) inc = inc * diff * 2 / (limit_pct + 1);
-  if (util_pct < limit_pct) share = std::min(share + inc, total);
-  else share = std::max<int64_t>(share - inc, 0);
+  const int64_t floor = spec.floor();
+  const int64_t ceil = spec.total();
+  if (share < floor) share = floor;
+  if (util_pct > limit_pct) {
+    // Proportional decrease toward limit/util, at most halving per period.
+    int64_t num = std::max(limit_pct, util_pct / 2);
+    share = std::max(floor, share * num / std::max(util_pct, 1));
+  } else if (util_pct < limit_pct) {
+    // Multiplicative increase by the relative headroom (<= +50 %) plus one chip wave,
+    // so an idle or under-share tenant ramps up in a few periods.
+    int64_t grow = share * std::min(limit_pct - util_pct, 50) / 100 + floor;
+    share = std::min(ceil, share + grow);
+  }
   return share;
 }
 
+int64_t limiter_initial_share(const LimiterSpec& spec, int limit_pct) {
+  int64_t pct = limit_pct > 0 && limit_pct < 100 ? limit_pct : 100;
+  return std::max(spec.floor(), spec.wave() * pct / 100);
+}
+
 void limiter_refill(DeviceState& d, const LimiterSpec& spec, int limit_pct, int util_pct) {
-  int64_t cap = d.token_cap.load();
-  if (cap <= 0) cap = spec.total();
-  int64_t share = d.share.load();
-  int64_t tokens = d.tokens.load();
-  if (share >= cap && tokens < 0) cap *= 2;  // grids larger than the bucket
-  share = limiter_delta(spec, limit_pct, util_pct, share);
+  int64_t share = limiter_delta(spec, limit_pct, util_pct, d.share.load());
+  // Burst capacity of two periods: small enough that a saturating tenant is throttled
+  // within ~2 periods of exceeding its share; grids larger than the bucket simply
+  // wait for several refills (tokens go negative, never deadlock).
+  int64_t cap = 2 * share;
   d.share.store(share);
   d.token_cap.store(cap);
   d.util_pct.store(util_pct);

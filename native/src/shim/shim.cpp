@@ -262,9 +262,10 @@ void shim_init_after_hsa() {
       memcpy(d.cu_mask, m.words, sizeof(d.cu_mask));
       d.cu_mask_bits = m.nbits;
       LimiterSpec spec{a.cu_count, a.max_waves_per_cu * 64};
-      d.token_cap.store(spec.total());
-      d.tokens.store(spec.total());
-      d.share.store(spec.total() / 10);
+      int64_t share0 = limiter_initial_share(spec, d.cu_limit_pct);
+      d.share.store(share0);
+      d.tokens.store(share0);
+      d.token_cap.store(2 * share0);
       d.configured = 1;
     }
     memcpy(a.mask.words, d.cu_mask, sizeof(a.mask.words));

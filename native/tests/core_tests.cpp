@@ -402,7 +402,17 @@ static void test_ratelimit() {
   CHECK(s > 0);
   int64_t s2 = limiter_delta(spec, 50, 90, s);
   CHECK(s2 < s);
-  CHECK_EQ(limiter_delta(spec, 50, 100, 0), 0);
+  CHECK_EQ(limiter_delta(spec, 50, 100, 0), spec.floor());  // never starved below one WG per CU
+  // Far over the limit the share at most halves per period.
+  CHECK_EQ(limiter_delta(spec, 10, 100, 100000), 50000);
+  // Converges: iterate util = f(share) for a workload whose util is proportional to share.
+  {
+    int64_t sh = limiter_initial_share(spec, 30);
+    const int64_t full = 4000000;  // share that would give 100 % utilisation
+    for (int i = 0; i < 60; i++) sh = limiter_delta(spec, 30, (int)std::min<int64_t>(100, sh * 100 / full), sh);
+    int u = (int)(sh * 100 / full);
+    CHECK(u >= 20 && u <= 40);
+  }
   CHECK(limiter_delta(spec, 50, 0, spec.total()) <= spec.total());
   // Small error still moves by the minimum step (diff clamp 5).
   CHECK(limiter_delta(spec, 50, 49, 1000) > 1000);
@@ -436,8 +446,10 @@ static void test_ratelimit() {
   d.share.store(1000);
   d.token_cap.store(1000);
   limiter_refill(d, spec, 50, 10);
-  CHECK_EQ(d.token_cap.load(), 2000);
-  CHECK(d.tokens.load() <= 2000);
+  int64_t sh = d.share.load();
+  CHECK(sh > 1000);
+  CHECK_EQ(d.token_cap.load(), 2 * sh);
+  CHECK_EQ(d.tokens.load(), sh - 5);
   CHECK_EQ(d.util_pct.load(), 10);
   unlink(p.c_str());
 }
@@ -455,7 +467,9 @@ static void test_kfd() {
   f = fopen((root + "/100/vram_7").c_str(), "w");
   fprintf(f, "4096\n");
   fclose(f);
-  g_kfd_proc_root = strdup(root.c_str());
+  static std::string kfd_root;  // outlives the test: g_kfd_proc_root keeps a pointer
+  kfd_root = root;
+  g_kfd_proc_root = kfd_root.c_str();
   std::vector<int> before = kfd_list_pids();
   CHECK_EQ(before.size(), 2u);
   mk("300");

@@ -1,0 +1,237 @@
+"""Data-plane tests on a real MI355X: stock PyTorch-ROCm processes run as vGPU 'containers'
+under the interception shim (SURVEY.md §4 tier 3).
+
+Each test starts child processes with the Allocate-contract env + preload (the shim has to
+be in the process from the start, like /etc/ld.so.preload in a pod) and asserts on what
+the children observe.
+"""
+import os
+import time
+
+import pytest
+
+from amdvgpu.shim.launcher import vgpu_env
+from conftest import child_results, run_child, spawn_child
+
+pytestmark = pytest.mark.gpu
+
+GiB = 1 << 30
+MiB = 1 << 20
+
+
+def test_mem_get_info_reports_quota(tmp_region):
+    c = vgpu_env(mem_limit=72 * GiB, shared_cache=tmp_region)
+    res, _ = run_child("""
+import torch
+free, total = torch.cuda.mem_get_info(0)
+p = torch.cuda.get_device_properties(0)
+x = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
+free2, total2 = torch.cuda.mem_get_info(0)
+emit(free=free, total=total, props_total=p.total_memory, free2=free2, total2=total2)
+""", c)
+    r = res[0]
+    assert r["total"] == 72 * GiB
+    assert r["props_total"] == 72 * GiB
+    assert r["free"] <= 72 * GiB
+    assert r["free"] - r["free2"] >= 4 * GiB  # the 4 GiB tensor is charged
+
+
+def test_oom_at_quota(tmp_region):
+    c = vgpu_env(mem_limit=2 * GiB, shared_cache=tmp_region)
+    res, _ = run_child("""
+import torch
+ok = []
+try:
+    a = torch.empty(1536 << 20, dtype=torch.uint8, device="cuda")
+    ok.append(1)
+    b = torch.empty(1024 << 20, dtype=torch.uint8, device="cuda")
+    ok.append(2)
+    emit(oom=False, ok=ok)
+except torch.OutOfMemoryError as e:
+    emit(oom=True, ok=ok, msg=str(e)[:200])
+""", c)
+    assert res[0]["oom"] is True
+    assert res[0]["ok"] == [1]
+
+
+def test_native_process_is_unlimited():
+    res, _ = run_child("""
+import torch
+free, total = torch.cuda.mem_get_info(0)
+emit(total=total)
+""", None)
+    assert res[0]["total"] > 250 * GiB
+
+
+def test_multiprocess_shared_quota(tmp_region):
+    """Two processes of one container share one quota (reference: shared region)."""
+    c = vgpu_env(mem_limit=6 * GiB, shared_cache=tmp_region)
+    holder = spawn_child("""
+import torch
+x = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
+torch.cuda.synchronize()
+emit(held=True)
+sys.stdout.flush()
+time.sleep(60)
+""", c)
+    # wait until the holder has allocated
+    line = holder.stdout.readline()
+    assert line.startswith("RESULT"), line + holder.stderr.read()
+    try:
+        res, _ = run_child("""
+import torch
+from amdvgpu.shim.region import Region
+free, total = torch.cuda.mem_get_info(0)
+try:
+    y = torch.empty(3 << 30, dtype=torch.uint8, device="cuda")
+    big = False
+except torch.OutOfMemoryError:
+    big = True
+z = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+r = Region(os.environ["VGPU_SHARED_CACHE"])
+emit(free=free, total=total, oom_3g=big, procs=len(r.procs()), used=r.device(0)["used"])
+""", c)
+    finally:
+        holder.kill()
+        holder.wait()
+    r = res[0]
+    assert r["total"] == 6 * GiB
+    assert r["free"] <= 2 * GiB + 64 * MiB
+    assert r["oom_3g"] is True
+    assert r["procs"] == 2
+    assert r["used"] >= 5 * GiB
+
+
+def test_dead_process_reclaim(tmp_region):
+    """A SIGKILLed process's charges are reclaimed when the quota is hit."""
+    c = vgpu_env(mem_limit=4 * GiB, shared_cache=tmp_region)
+    p = spawn_child("""
+import torch
+x = torch.empty(3 << 30, dtype=torch.uint8, device="cuda")
+torch.cuda.synchronize()
+emit(held=True)
+time.sleep(120)
+""", c)
+    assert p.stdout.readline().startswith("RESULT")
+    p.kill()
+    p.wait()
+    res, _ = run_child("""
+import torch
+y = torch.empty(3 << 30, dtype=torch.uint8, device="cuda")
+emit(ok=True)
+""", c)
+    assert res[0]["ok"]
+
+
+@pytest.mark.parametrize("pct,expect", [(25, 64), (50, 128)])
+def test_cu_mask_confinement(tmp_region, pct, expect):
+    c = vgpu_env(cu_limit=pct, shared_cache=tmp_region)
+    res, _ = run_child("""
+import torch
+from amdvgpu.ops import cu_census
+locs = cu_census(nblocks=8192, spin_us=300)
+xcc = sorted({l[0] for l in locs})
+per_xcc = {x: sum(1 for l in locs if l[0] == x) for x in xcc}
+emit(n=len(locs), xcc=xcc, per_xcc=per_xcc)
+""", c)
+    r = res[0]
+    assert r["n"] == expect, r
+    assert len(r["xcc"]) == 8
+    assert len(set(r["per_xcc"].values())) == 1  # XCD-balanced
+
+
+def test_cu_unmasked_uses_whole_chip():
+    res, _ = run_child("""
+import torch
+from amdvgpu.ops import cu_census
+emit(n=len(cu_census(nblocks=8192, spin_us=300)))
+""", None)
+    assert res[0]["n"] == 256
+
+
+def test_disjoint_cu_ranges(tmp_region):
+    """Two co-resident vGPUs with plugin-assigned ranges get disjoint physical CUs."""
+    from amdvgpu.shim.region import cu_partition_range
+    seen = []
+    for slot in range(2):
+        b, e = cu_partition_range(256, 8, 2, slot)
+        c = vgpu_env(cu_limit=50, cu_range=(b, e), shared_cache=tmp_region + f".{slot}")
+        res, _ = run_child("""
+from amdvgpu.ops import cu_census
+emit(locs=sorted(cu_census(nblocks=8192, spin_us=300)))
+""", c)
+        seen.append({tuple(x) for x in res[0]["locs"]})
+        os.unlink(tmp_region + f".{slot}")
+    assert len(seen[0]) == 128 and len(seen[1]) == 128
+    assert not (seen[0] & seen[1])
+
+
+def test_suspend_resume_blocks_launches(tmp_region):
+    c = vgpu_env(mem_limit=8 * GiB, shared_cache=tmp_region)
+    p = spawn_child("""
+import torch
+x = torch.ones(1 << 20, device="cuda")
+torch.cuda.synchronize()
+emit(ready=True)
+t0 = time.time()
+for i in range(200):
+    x.add_(1)
+    torch.cuda.synchronize()
+    time.sleep(0.01)
+emit(elapsed=time.time() - t0, val=float(x[0]))
+""", c)
+    assert p.stdout.readline().startswith("RESULT")
+    from amdvgpu.shim.region import Region
+    r = Region(tmp_region)
+    r.suspend_all()
+    time.sleep(3.0)
+    assert r.suspended
+    r.resume_all()
+    out, err = p.communicate(timeout=120)
+    assert p.returncode == 0, err[-3000:]
+    res = child_results(out)[0]
+    assert res["val"] == 201.0
+    assert res["elapsed"] >= 4.0  # ~2 s of work + ~3 s suspended
+    procs = r.procs()
+    r.close()
+    assert not procs  # the exited process released its slot
+
+
+def test_temporal_limiter_duty_cycle(tmp_region):
+    """Temporal (reference-parity) mode slows a saturating workload toward its share."""
+    code = """
+import torch
+from amdvgpu.ops import spin
+spin(256 * 32, 200); torch.cuda.synchronize()
+t0 = time.time()
+for i in range(2000):
+    spin(256 * 32, 500)
+    if i % 50 == 0:
+        torch.cuda.synchronize()
+torch.cuda.synchronize()
+emit(t=time.time() - t0)
+"""
+    base, _ = run_child(code, None)
+    c = vgpu_env(cu_limit=40, cu_mode="temporal", shared_cache=tmp_region)
+    lim, _ = run_child(code, c, timeout=900)
+    ratio = base[0]["t"] / lim[0]["t"]
+    assert ratio < 0.8, (base, lim)
+
+
+def test_hip_graph_replay_under_shim(tmp_region):
+    c = vgpu_env(mem_limit=16 * GiB, shared_cache=tmp_region)
+    res, _ = run_child("""
+import torch
+x = torch.zeros(1 << 20, device="cuda")
+s = torch.cuda.Stream()
+with torch.cuda.stream(s):
+    for _ in range(3): x.add_(1)
+torch.cuda.synchronize()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    x.add_(1)
+for _ in range(10): g.replay()
+torch.cuda.synchronize()
+emit(v=float(x[0]))
+""", c)
+    assert res[0]["v"] == 13.0  # 3 eager + 10 replays (capture itself does not execute)

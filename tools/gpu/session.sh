@@ -1,0 +1,39 @@
+#!/bin/bash
+# One gpurun session: build, GPU tests, smoke, bench, rocprof profile.
+# Usage (from the repo root, on the box):  bash tools/gpu/session.sh <tag> [steps...]
+# steps: build tests smoke bench prof (default: all). Every GPU step has its own time
+# limit and the script stops at the first failure.
+set -o pipefail
+TAG=${1:-run}; shift
+STEPS=${*:-"build tests smoke bench prof"}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+has() { [[ " $STEPS " == *" $1 "* ]]; }
+step() { echo "== $1 $(date +%T)"; }
+if has build; then
+  step build
+  make -C native -j16 > $OUT/build.log 2>&1 || { echo "build failed"; tail -20 $OUT/build.log; exit 1; }
+fi
+if has tests; then
+  step tests
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+  rc=$?; tail -15 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has smoke; then
+  step smoke
+  timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+  rc=$?; tail -3 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has bench; then
+  step bench
+  timeout -k 10 900 python bench.py --steps 20 --warmup 5 --json-out $OUT/bench.json > $OUT/bench.log 2>&1
+  rc=$?; tail -3 $OUT/bench.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has prof; then
+  step prof
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- \
+    python3 bench.py --steps 10 --warmup 3 --modes vgpu > $OUT/prof.log 2>&1
+  rc=$?; tail -3 $OUT/prof.log; [ $rc -eq 0 ] || exit $rc
+fi
+echo "== done $(date +%T)"
