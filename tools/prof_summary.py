@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 rocpd database (kernel trace) as markdown.
+
+    python tools/prof_summary.py gpurun_out/<tag>/prof/<name>_results.db [--top 25] [--title T]
+"""
+import argparse
+import glob
+import sqlite3
+
+
+def summarize(db_path, top=25, title=None):
+    db = sqlite3.connect(db_path)
+    cur = db.cursor()
+    procs = cur.execute("select pid, command from processes").fetchall()
+    total_n, total_ns = cur.execute("select count(*), sum(duration) from kernels").fetchone()
+    span = cur.execute("select min(start), max(end) from kernels").fetchone()
+    rows = cur.execute("select name, total_calls, total_duration, average, percentage from top_kernels "
+                       "order by total_duration desc limit ?", (top,)).fetchall()
+    out = [f"# {title or 'rocprofv3 kernel summary'}", "",
+           f"source: `{db_path}` (rocprofv3 --kernel-trace --stats)", ""]
+    for pid, cmd in procs:
+        out.append(f"* process {pid}: `{cmd[:200]}`")
+    out += ["", f"* kernels dispatched: {total_n}", f"* summed kernel time: {total_ns / 1e6:.2f} ms",
+            f"* first-to-last dispatch span: {(span[1] - span[0]) / 1e6:.2f} ms" if span[0] else "", "",
+            "| # | kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|---|"]
+    for i, (name, calls, tot, avg, pct) in enumerate(rows):
+        short = name if len(name) < 110 else name[:107] + "..."
+        short = short.replace("|", "\\|")
+        out.append(f"| {i + 1} | `{short}` | {calls} | {tot / 1e3:.3f} | {avg:.1f} | {pct:.1f} |")
+    return "\n".join(out) + "\n"
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db", nargs="+")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--title", default=None)
+    ap.add_argument("-o", "--out", default=None)
+    a = ap.parse_args()
+    paths = [p for g in a.db for p in glob.glob(g)]
+    text = "\n".join(summarize(p, a.top, a.title) for p in paths)
+    if a.out:
+        open(a.out, "w").write(text)
+    else:
+        print(text)
