@@ -1,0 +1,150 @@
+"""Plugin flags with environment fallbacks and validation.
+
+Reference: ``main.go:55-133`` (11 urfave/cli flags, each with an env var) and
+``validateFlags`` (``main.go:143-161``). Same flag names where the concept carries
+over; NVIDIA-specific names get AMD equivalents (``--mig-strategy`` is accepted as an
+alias of ``--partition-strategy``) and MI355X-only knobs are added (CU-limit mode,
+device backend, paths used by the stub-kubelet tests).
+"""
+import argparse
+import os
+from dataclasses import dataclass, field
+
+PARTITION_NONE, PARTITION_SINGLE, PARTITION_MIXED = "none", "single", "mixed"
+LIST_ENVVAR, LIST_AMD_RUNTIME, LIST_VOLUME_MOUNTS = "envvar", "amd-container-runtime", "volume-mounts"
+ID_UUID, ID_INDEX = "uuid", "index"
+CU_MODES = ("spatial", "temporal", "both", "off")
+DEFAULT_RESOURCE = "amd.com/gpu"
+DEFAULT_PLUGIN_DIR = "/var/lib/kubelet/device-plugins/"
+DEFAULT_VGPU_DIR = "/usr/local/vgpu"
+
+
+def _env_bool(v, default):
+    if v is None:
+        return default
+    return str(v).strip().lower() in ("1", "true", "yes", "on")
+
+
+@dataclass
+class PluginConfig:
+    partition_strategy: str = PARTITION_NONE
+    fail_on_init_error: bool = True
+    pass_device_specs: bool = True           # AMD has no runtime hook: default on
+    device_list_strategy: str = LIST_ENVVAR
+    device_id_strategy: str = ID_UUID
+    driver_root: str = "/"
+    device_split_count: int = 2
+    device_memory_scaling: float = 1.0
+    device_cores_scaling: float = 1.0
+    enable_legacy_preferred: bool = False
+    verbose: int = 0
+    # MI355X additions
+    cu_mode: str = "spatial"
+    backend: str = "auto"
+    fake_devices: str = ""
+    resource_name: str = DEFAULT_RESOURCE
+    device_plugin_path: str = DEFAULT_PLUGIN_DIR
+    vgpu_dir: str = DEFAULT_VGPU_DIR
+    monitor_mode: bool = False
+    pcibus_file: str = ""
+    disable_healthchecks: str = ""          # DP_DISABLE_HEALTHCHECKS: "all" | "events"/"xids"
+    health_interval_s: float = 5.0
+    node_name: str = ""
+    shared_cache_dir: str = "/tmp"
+    version_requested: bool = False
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def kubelet_socket(self):
+        return os.path.join(self.device_plugin_path, "kubelet.sock")
+
+    def validate(self):
+        if self.partition_strategy not in (PARTITION_NONE, PARTITION_SINGLE, PARTITION_MIXED):
+            raise ValueError(f"invalid --partition-strategy option: {self.partition_strategy}")
+        if self.device_list_strategy not in (LIST_ENVVAR, LIST_AMD_RUNTIME, LIST_VOLUME_MOUNTS):
+            raise ValueError(f"invalid --device-list-strategy option: {self.device_list_strategy}")
+        if self.device_id_strategy not in (ID_UUID, ID_INDEX):
+            raise ValueError(f"invalid --device-id-strategy option: {self.device_id_strategy}")
+        if self.device_split_count < 1:
+            raise ValueError(f"invalid --device-split-count option: {self.device_split_count}")
+        if self.device_memory_scaling <= 0:
+            raise ValueError(f"invalid --device-memory-scaling option: {self.device_memory_scaling}")
+        if self.device_cores_scaling <= 0:
+            raise ValueError(f"invalid --device-cores-scaling option: {self.device_cores_scaling}")
+        if self.cu_mode not in CU_MODES:
+            raise ValueError(f"invalid --cu-mode option: {self.cu_mode}")
+        return self
+
+
+# (flag, dest, type, env vars, help)
+_FLAGS = [
+    ("--partition-strategy", "partition_strategy", str, ["PARTITION_STRATEGY", "MIG_STRATEGY"],
+     "compute/memory partition strategy: none | single | mixed"),
+    ("--fail-on-init-error", "fail_on_init_error", "bool", ["FAIL_ON_INIT_ERROR"],
+     "fail the plugin if device discovery fails (false: wait forever, for non-GPU nodes)"),
+    ("--pass-device-specs", "pass_device_specs", "bool", ["PASS_DEVICE_SPECS"],
+     "pass /dev/kfd and /dev/dri nodes to the kubelet as DeviceSpecs"),
+    ("--device-list-strategy", "device_list_strategy", str, ["DEVICE_LIST_STRATEGY"],
+     "how visible devices reach the container: envvar | amd-container-runtime | volume-mounts"),
+    ("--device-id-strategy", "device_id_strategy", str, ["DEVICE_ID_STRATEGY"], "uuid | index"),
+    ("--driver-root", "driver_root", str, ["AMD_DRIVER_ROOT", "DRIVER_ROOT"], "root of the host's /dev tree"),
+    ("--device-split-count", "device_split_count", int, ["DEVICE_SPLIT_COUNT"], "vGPUs per physical GPU"),
+    ("--device-memory-scaling", "device_memory_scaling", float, ["DEVICE_MEMORY_SCALING"],
+     "memory oversubscription ratio (>1 spills to host memory)"),
+    ("--device-cores-scaling", "device_cores_scaling", float, ["DEVICE_CORES_SCALING"],
+     "compute oversubscription ratio (CU share = 100 * scaling / split)"),
+    ("--enable-legacy-preferred", "enable_legacy_preferred", "bool", ["ENABLE_LEGACY_PREFERRED"],
+     "preferred allocation for kubelets without GetPreferredAllocation"),
+    ("--verbose", "verbose", int, ["VERBOSE"], "log verbosity"),
+    ("--cu-mode", "cu_mode", str, ["CU_MODE"], "CU limit enforcement: spatial | temporal | both | off"),
+    ("--backend", "backend", str, ["DEVICE_BACKEND"], "device backend: auto | amdsmi | sysfs | fake"),
+    ("--fake-devices", "fake_devices", str, ["FAKE_DEVICES"], "JSON spec (or file) for the fake backend"),
+    ("--resource-name", "resource_name", str, ["RESOURCE_NAME"], "extended resource name"),
+    ("--device-plugin-path", "device_plugin_path", str, ["DEVICE_PLUGIN_PATH"], "kubelet device-plugin dir"),
+    ("--vgpu-dir", "vgpu_dir", str, ["VGPU_DIR"], "host dir holding the shim (/usr/local/vgpu)"),
+    ("--monitor-mode", "monitor_mode", "bool", ["VGPU_MONITOR_MODE"],
+     "expose each container's region on a host path for the node monitor"),
+    ("--pcibus-file", "pcibus_file", str, ["VGPU_PCIBUS_FILE", "PCIBUSFILE"], "write the GPU BDF list here"),
+    ("--health-interval", "health_interval_s", float, ["HEALTH_INTERVAL"], "health poll period (s)"),
+    ("--node-name", "node_name", str, ["NODE_NAME"], "this node (legacy-preferred / monitor mode)"),
+]
+
+
+def build_parser():
+    ap = argparse.ArgumentParser(prog="amd-vgpu-device-plugin",
+                                 description="MI355X vGPU device plugin for Kubernetes")
+    for flag, dest, typ, envs, help_ in _FLAGS:
+        names = [flag] + (["--mig-strategy"] if dest == "partition_strategy" else [])
+        if typ == "bool":
+            ap.add_argument(*names, dest=dest, nargs="?", const="true", default=None,
+                            help=f"{help_} (env {', '.join(envs)})")
+        else:
+            ap.add_argument(*names, dest=dest, type=typ, default=None, help=f"{help_} (env {', '.join(envs)})")
+    ap.add_argument("--version", action="store_true")
+    return ap
+
+
+def parse_config(argv=None, environ=None):
+    """Flags > env vars > defaults, then validate (reference: cli flag EnvVars + Before)."""
+    environ = os.environ if environ is None else environ
+    ns = build_parser().parse_args(argv)
+    cfg = PluginConfig()
+    for _flag, dest, typ, envs, _h in _FLAGS:
+        val = getattr(ns, dest)
+        if val is None:
+            for e in envs:
+                if e in environ and environ[e] != "":
+                    val = environ[e]
+                    break
+        if val is None:
+            continue
+        if typ == "bool":
+            val = _env_bool(val, getattr(cfg, dest))
+        elif typ in (int, float):
+            val = typ(val)
+        setattr(cfg, dest, val)
+    cfg.disable_healthchecks = environ.get("DP_DISABLE_HEALTHCHECKS", "")
+    if not cfg.device_plugin_path.endswith("/"):
+        cfg.device_plugin_path += "/"
+    cfg.version_requested = bool(ns.version)
+    return cfg.validate()

@@ -1,0 +1,143 @@
+"""The plugin -> shim contract: what ``Allocate`` puts into a ContainerAllocateResponse.
+
+Reference: ``server.go:459-522`` (visible devices, DeviceSpecs, annotations,
+``CUDA_DEVICE_MEMORY_LIMIT_<i>``, ``CUDA_DEVICE_SM_LIMIT``, ``NVIDIA_DEVICE_MAP``,
+``CUDA_DEVICE_MEMORY_SHARED_CACHE``, ``CUDA_OVERSUBSCRIBE``, and the mounts of the shim,
+``/etc/ld.so.preload``, ``pciinfo.vgpu``, the validator and the license dir), plus
+``apiEnvs``/``apiMounts``/``apiDeviceSpecs`` (:598-655). Env names are the VGPU_*
+equivalents read by ``native/src/core/config.cpp``.
+
+Differences from the reference, by design:
+* visible devices go through ``ROCR_VISIBLE_DEVICES`` (ROCr accepts ``GPU-<uuid>``) and
+  the device nodes (/dev/kfd, /dev/dri/renderD*, /dev/dri/card*) are always passed as
+  DeviceSpecs by default — AMD has no container-runtime hook that would add them;
+* CU share and CU range are per vdevice (``VGPU_DEVICE_CU_LIMIT_<i>``/``_RANGE_<i>``),
+  not one value for the whole container (quirk ``server.go:492``);
+* with memory oversubscription the HBM-resident cap (``VGPU_DEVICE_HBM_LIMIT_<i>``)
+  is the tenant's physical share and the rest of the quota spills to host memory;
+* the pciinfo mount is only emitted when the BDF file exists (the reference mounts an
+  empty host path when ``PCIBUSFILE`` is unset, ``server.go:516``).
+"""
+import os
+import uuid as _uuid
+
+from ..utils.sizes import format_mib
+from . import api
+from .config import ID_INDEX, LIST_AMD_RUNTIME, LIST_ENVVAR, LIST_VOLUME_MOUNTS
+
+VISIBLE_ENV = "ROCR_VISIBLE_DEVICES"
+AMD_RUNTIME_ENV = "AMD_VISIBLE_DEVICES"
+VOLUME_MOUNTS_ROOT = "/var/run/amd-container-devices"
+VOLUME_MOUNTS_HOST = "/dev/null"
+CONTAINER_SHIM = "/usr/local/vgpu/libvgpu_hip.so"
+CONTAINER_PRELOAD = "/etc/ld.so.preload"
+CONTAINER_PCIINFO = "/usr/local/vgpu/pciinfo.vgpu"
+CONTAINER_VALIDATOR = "/usr/bin/vgpu-validate"
+CONTAINER_ALLOWLIST_DIR = "/vgpu"
+SHARED_HOST_DIR = "shared"
+ANN_REQUEST = "amd-vgpu/request"
+ANN_USING = "amd-vgpu/using"
+
+
+def device_ids(cfg, devices_by_uuid, uuids):
+    if cfg.device_id_strategy == ID_INDEX:
+        return [str(devices_by_uuid[u].index) for u in uuids if u in devices_by_uuid]
+    return list(uuids)
+
+
+def device_specs(cfg, devices):
+    """/dev/kfd once, then render + card node of every device (permissions rw)."""
+    specs, seen = [], set()
+    for d in devices:
+        for p in d.device_paths:
+            if p in seen:
+                continue
+            seen.add(p)
+            specs.append(api.DeviceSpec(container_path=p, host_path=os.path.join(cfg.driver_root, p.lstrip("/")),
+                                        permissions="rw"))
+    return specs
+
+
+def visible_envs(cfg, ids):
+    if cfg.device_list_strategy == LIST_ENVVAR:
+        return {VISIBLE_ENV: ",".join(ids)}
+    if cfg.device_list_strategy == LIST_AMD_RUNTIME:
+        return {AMD_RUNTIME_ENV: ",".join(ids)}
+    return {AMD_RUNTIME_ENV: VOLUME_MOUNTS_ROOT}
+
+
+def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, using_ids=None, pod_tag=None):
+    """ContainerAllocateResponse for one container holding vGPUs ``vdevs``."""
+    resp = api.ContainerAllocateResponse()
+    uuids = []
+    for v in vdevs:
+        if v.uuid not in uuids:
+            uuids.append(v.uuid)
+    ids = device_ids(cfg, devices_by_uuid, uuids)
+    resp.envs.update(visible_envs(cfg, ids))
+    if cfg.device_list_strategy == LIST_VOLUME_MOUNTS:
+        for i in ids:
+            resp.mounts.add(container_path=os.path.join(VOLUME_MOUNTS_ROOT, i), host_path=VOLUME_MOUNTS_HOST)
+    if cfg.pass_device_specs:
+        resp.devices.extend(device_specs(cfg, [devices_by_uuid[u] for u in uuids if u in devices_by_uuid]))
+    if request_ids is not None:
+        resp.annotations[ANN_REQUEST] = ",".join(request_ids)
+        resp.annotations[ANN_USING] = ",".join(using_ids or request_ids)
+
+    # Per-vGPU limits, indexed like the container's device ordinals (VGPU_DEVICE_MAP order).
+    dmap = []
+    for i, v in enumerate(vdevs):
+        if v.memory:
+            resp.envs[f"VGPU_DEVICE_MEMORY_LIMIT_{i}"] = format_mib(v.memory)
+        if v.hbm_limit and v.hbm_limit < v.memory:
+            resp.envs[f"VGPU_DEVICE_HBM_LIMIT_{i}"] = format_mib(v.hbm_limit)
+        if v.cu_pct:
+            resp.envs[f"VGPU_DEVICE_CU_LIMIT_{i}"] = str(v.cu_pct)
+            if v.cu_range:
+                resp.envs[f"VGPU_DEVICE_CU_RANGE_{i}"] = f"{v.cu_range[0]}-{v.cu_range[1]}"
+        dmap.append(f"{i}:{v.uuid}")
+    resp.envs["VGPU_DEVICE_MAP"] = " ".join(dmap)
+    if cfg.cu_mode != "spatial":
+        resp.envs["VGPU_CU_MODE"] = cfg.cu_mode
+
+    cache_name = f"{_uuid.uuid4()}.cache"
+    if cfg.monitor_mode and pod_tag:
+        host_dir = os.path.join(cfg.vgpu_dir, SHARED_HOST_DIR, pod_tag)
+        os.makedirs(host_dir, exist_ok=True)
+        resp.mounts.add(container_path=f"/{pod_tag}", host_path=host_dir, read_only=False)
+        resp.envs["VGPU_SHARED_CACHE"] = f"/{pod_tag}/{cache_name}"
+    else:
+        resp.envs["VGPU_SHARED_CACHE"] = os.path.join(cfg.shared_cache_dir, cache_name)
+    if cfg.device_memory_scaling > 1:
+        resp.envs["VGPU_OVERSUBSCRIBE"] = "true"
+
+    vdir = cfg.vgpu_dir
+    resp.mounts.add(container_path=CONTAINER_SHIM, host_path=os.path.join(vdir, "libvgpu_hip.so"), read_only=True)
+    resp.mounts.add(container_path=CONTAINER_PRELOAD, host_path=os.path.join(vdir, "ld.so.preload"), read_only=True)
+    if cfg.pcibus_file and os.path.exists(cfg.pcibus_file):
+        resp.mounts.add(container_path=CONTAINER_PCIINFO, host_path=cfg.pcibus_file, read_only=True)
+    resp.mounts.add(container_path=CONTAINER_VALIDATOR, host_path=os.path.join(vdir, "vgpu-validate"),
+                    read_only=True)
+    resp.mounts.add(container_path=CONTAINER_ALLOWLIST_DIR, host_path=os.path.join(vdir, "allowlist"),
+                    read_only=True)
+    return resp
+
+
+def build_partition_response(cfg, devices):
+    """Whole-device response for partition resources (reference MIGAllocate :329-358):
+    visible devices + device specs, no quota, no shim contract."""
+    resp = api.ContainerAllocateResponse()
+    by_uuid = {d.uuid: d for d in devices}
+    ids = device_ids(cfg, by_uuid, [d.uuid for d in devices])
+    resp.envs.update(visible_envs(cfg, ids))
+    if cfg.device_list_strategy == LIST_VOLUME_MOUNTS:
+        for i in ids:
+            resp.mounts.add(container_path=os.path.join(VOLUME_MOUNTS_ROOT, i), host_path=VOLUME_MOUNTS_HOST)
+    if cfg.pass_device_specs:
+        resp.devices.extend(device_specs(cfg, devices))
+    return resp
+
+
+def response_to_env(resp):
+    """(envs dict, [(container_path, host_path)]) — the view the launcher applies."""
+    return dict(resp.envs), [(m.container_path, m.host_path) for m in resp.mounts]

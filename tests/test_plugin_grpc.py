@@ -1,0 +1,163 @@
+"""Control plane end to end against a stub kubelet over unix sockets (BASELINE.json
+config 1: ListAndWatch/Allocate with 2 fake devices, no GPU)."""
+import os
+import threading
+import time
+
+import pytest
+
+from amdvgpu.plugin import api
+from amdvgpu.plugin.config import PluginConfig
+from amdvgpu.plugin.devices import FakeBackend
+from amdvgpu.plugin.kubelet_stub import StubKubelet
+from amdvgpu.plugin.main import Supervisor
+
+
+@pytest.fixture
+def plugin_dir(tmp_path):
+    d = tmp_path / "dp"
+    d.mkdir()
+    return str(d)
+
+
+def start(plugin_dir, backend=None, **kw):
+    cfg = PluginConfig(device_plugin_path=plugin_dir + "/", backend="fake", health_interval_s=0.1,
+                       vgpu_dir="/usr/local/vgpu", **kw).validate()
+    kubelet = StubKubelet(plugin_dir).start()
+    sup = Supervisor(cfg, backend=backend or FakeBackend(n=2), install_signals=False)
+    stop = threading.Event()
+    th = threading.Thread(target=sup.run, args=(stop,), daemon=True)
+    th.start()
+    return cfg, kubelet, sup, stop, th
+
+
+def shutdown(kubelet, stop, th):
+    stop.set()
+    th.join(timeout=10)
+    kubelet.stop()
+
+
+def test_register_list_and_allocate(plugin_dir):
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=2)
+    try:
+        reg = k.wait_registered("amd.com/gpu")
+        assert reg.version == "v1beta1" and reg.endpoint == "amd-vgpu.sock"
+        assert reg.options.get_preferred_allocation_available
+        devs = k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
+        assert all(h == api.HEALTHY for h in devs.values())
+        ids, resp = k.allocate("amd.com/gpu", 1)
+        envs = dict(resp.envs)
+        uuid = ids[0].rsplit("-", 1)[0]
+        assert envs["ROCR_VISIBLE_DEVICES"] == uuid
+        assert envs["VGPU_DEVICE_MAP"] == f"0:{uuid}"
+        total = FakeBackend(n=2).devices()[0].memory_total >> 20
+        assert envs["VGPU_DEVICE_MEMORY_LIMIT_0"] == f"{total // 2}m"
+        assert envs["VGPU_DEVICE_CU_LIMIT_0"] == "50"
+        assert envs["VGPU_SHARED_CACHE"].startswith("/tmp/") and envs["VGPU_SHARED_CACHE"].endswith(".cache")
+        assert "VGPU_OVERSUBSCRIBE" not in envs
+        mounts = {m.container_path: (m.host_path, m.read_only) for m in resp.mounts}
+        assert mounts["/usr/local/vgpu/libvgpu_hip.so"] == ("/usr/local/vgpu/libvgpu_hip.so", True)
+        assert mounts["/etc/ld.so.preload"] == ("/usr/local/vgpu/ld.so.preload", True)
+        specs = [d.container_path for d in resp.devices]
+        assert specs[0] == "/dev/kfd" and any(p.startswith("/dev/dri/renderD") for p in specs)
+        # second vGPU on the other slot of some GPU gets a disjoint CU range
+        ids2, resp2 = k.allocate("amd.com/gpu", 1)
+        assert ids2 != ids
+    finally:
+        shutdown(k, stop, th)
+
+
+def test_multi_gpu_request_spreads_over_gpus(plugin_dir):
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=2, backend=FakeBackend(n=4, topology="xgmi"))
+    try:
+        k.wait_registered("amd.com/gpu")
+        k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 8)
+        ids, resp = k.allocate("amd.com/gpu", 2)
+        uuids = {i.rsplit("-", 1)[0] for i in ids}
+        assert len(uuids) == 2
+        envs = dict(resp.envs)
+        assert len(envs["ROCR_VISIBLE_DEVICES"].split(",")) == 2
+        assert "VGPU_DEVICE_MEMORY_LIMIT_1" in envs
+    finally:
+        shutdown(k, stop, th)
+
+
+def test_health_unhealthy_then_recovered(plugin_dir):
+    be = FakeBackend(n=2)
+    cfg, k, sup, stop, th = start(plugin_dir, backend=be)
+    try:
+        k.wait_registered("amd.com/gpu")
+        k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
+        bad = be.devices()[1].uuid
+        be.inject(bad, False, "GPU_PRE_RESET")
+        devs = k.wait_devices("amd.com/gpu", predicate=lambda d: sum(h == api.UNHEALTHY for h in d.values()) == 2)
+        assert {i for i, h in devs.items() if h == api.UNHEALTHY} == {f"{bad}-0", f"{bad}-1"}
+        be.inject(bad, True, "GPU_POST_RESET")
+        k.wait_devices("amd.com/gpu", predicate=lambda d: all(h == api.HEALTHY for h in d.values()))
+    finally:
+        shutdown(k, stop, th)
+
+
+def test_healthchecks_disabled(plugin_dir, monkeypatch):
+    be = FakeBackend(n=1)
+    cfg, k, sup, stop, th = start(plugin_dir, backend=be, disable_healthchecks="all")
+    try:
+        k.wait_registered("amd.com/gpu")
+        k.wait_devices("amd.com/gpu")
+        be.inject(be.devices()[0].uuid, False, "x")
+        time.sleep(0.5)
+        assert all(h == api.HEALTHY for h in k.devices["amd.com/gpu"].values())
+    finally:
+        shutdown(k, stop, th)
+
+
+def test_kubelet_restart_triggers_reregistration(plugin_dir):
+    cfg, k, sup, stop, th = start(plugin_dir)
+    try:
+        k.wait_registered("amd.com/gpu")
+        n0 = sup.restarts
+        k.restart()  # re-creates kubelet.sock
+        k.wait_registered("amd.com/gpu", timeout=15)
+        assert sup.restarts > n0
+        k.wait_devices("amd.com/gpu")
+    finally:
+        shutdown(k, stop, th)
+
+
+def test_unknown_device_rejected(plugin_dir):
+    import grpc
+    cfg, k, sup, stop, th = start(plugin_dir)
+    try:
+        k.wait_registered("amd.com/gpu")
+        stub = k.stub_for("amd.com/gpu")
+        with pytest.raises(grpc.RpcError) as e:
+            stub.Allocate(api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devicesIDs=["x"])]))
+        assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        assert isinstance(stub.PreStartContainer(api.PreStartContainerRequest()), api.PreStartContainerResponse)
+    finally:
+        shutdown(k, stop, th)
+
+
+def test_mixed_partition_strategy(plugin_dir):
+    class Mixed(FakeBackend):
+        def __init__(self):
+            super().__init__(n=1)
+            part = FakeBackend(n=1, partitions_per_gpu=4, compute_partition="CPX", uuid_prefix="GPU-cafe").devices()
+            for i, p in enumerate(part):
+                p.index = 1 + i
+                p.memory_partition = "NPS2"
+            self._devs = self._devs + part
+
+    cfg, k, sup, stop, th = start(plugin_dir, backend=Mixed(), partition_strategy="mixed")
+    try:
+        k.wait_registered("amd.com/gpu")
+        reg = k.wait_registered("amd.com/cpx-nps2")
+        assert reg.endpoint == "amd-cpx-nps2.sock"
+        assert not reg.options.get_preferred_allocation_available
+        devs = k.wait_devices("amd.com/cpx-nps2", predicate=lambda d: len(d) == 4)
+        ids, resp = k.allocate("amd.com/cpx-nps2", 1)
+        envs = dict(resp.envs)
+        assert "VGPU_DEVICE_MEMORY_LIMIT_0" not in envs and "ROCR_VISIBLE_DEVICES" in envs
+        assert len(k.wait_devices("amd.com/gpu")) == 2
+    finally:
+        shutdown(k, stop, th)

@@ -1,0 +1,87 @@
+"""vGPU model (reference vdevice.go) and the Python/C++ CU-partition twins."""
+import pytest
+
+from amdvgpu.plugin.devices import FakeBackend
+from amdvgpu.plugin.vdevice import (cu_partition_range, cu_range_for, cu_share_count, device_to_vdevices,
+                                    physical_uuid, unique_device_uuids, vdevices_by_ids)
+
+MiB = 1 << 20
+
+
+def test_split_memory_formula():
+    devs = FakeBackend(n=2).devices()
+    vds = device_to_vdevices(devs, 4)
+    assert len(vds) == 8
+    total_mib = devs[0].memory_total // MiB
+    assert all(v.memory == (total_mib // 4) * MiB for v in vds)
+    assert vds[0].id == f"{devs[0].uuid}-0" and vds[5].id == f"{devs[1].uuid}-1"
+    assert all(v.cu_pct == 25 for v in vds)
+
+
+def test_memory_scaling_and_hbm_share():
+    devs = FakeBackend(n=1).devices()
+    vds = device_to_vdevices(devs, 2, memory_scaling=1.8)
+    total_mib = devs[0].memory_total // MiB
+    assert vds[0].memory == int(total_mib * 1.8 / 2) * MiB
+    assert vds[0].hbm_limit == (total_mib // 2) * MiB
+
+
+def test_disjoint_cu_ranges_per_slot():
+    devs = FakeBackend(n=1).devices()
+    vds = device_to_vdevices(devs, 4)
+    ranges = [v.cu_range for v in vds]
+    assert ranges == [(0, 64), (64, 128), (128, 192), (192, 256)]
+
+
+def test_cores_scaling_widens_ranges():
+    devs = FakeBackend(n=1).devices()
+    vds = device_to_vdevices(devs, 4, cores_scaling=2.0)
+    assert all(v.cu_pct == 50 for v in vds)
+    assert all(v.cu_range[1] - v.cu_range[0] == 128 for v in vds)
+    assert all(0 <= v.cu_range[0] and v.cu_range[1] <= 256 for v in vds)
+
+
+def test_split_one_is_unlimited_compute():
+    vds = device_to_vdevices(FakeBackend(n=1).devices(), 1)
+    assert vds[0].cu_pct == 0 and vds[0].cu_range is None
+
+
+def test_partitions_are_whole_devices():
+    devs = FakeBackend(n=1, partitions_per_gpu=8, compute_partition="CPX").devices()
+    vds = device_to_vdevices(devs, 4)
+    assert len(vds) == 8 and all(v.memory == 0 and v.cu_pct == 0 for v in vds)
+
+
+def test_lookup_helpers():
+    vds = device_to_vdevices(FakeBackend(n=2).devices(), 2)
+    got = vdevices_by_ids(vds, [vds[3].id, vds[0].id])
+    assert [v.id for v in got] == [vds[3].id, vds[0].id]
+    with pytest.raises(KeyError):
+        vdevices_by_ids(vds, ["nope"])
+    assert unique_device_uuids([vds[0], vds[1], vds[2]]) == [vds[0].uuid, vds[2].uuid]
+    assert physical_uuid(vds[3].id) == vds[3].uuid
+
+
+@pytest.mark.parametrize("cu,xcc", [(256, 8), (32, 1), (128, 4), (80, 8)])
+def test_python_cu_math_matches_native(cu, xcc):
+    from amdvgpu.shim import region
+    for pct in (0, 1, 10, 25, 33, 50, 99, 100):
+        assert cu_share_count(cu, xcc, pct) == region.cu_share_count(cu, xcc, pct)
+    for split in range(1, 40):
+        for slot in range(split):
+            assert cu_partition_range(cu, xcc, split, slot) == region.cu_partition_range(cu, xcc, split, slot)
+
+
+def test_partition_ranges_cover_chip_disjointly():
+    for split in range(1, 33):
+        rs = [cu_partition_range(256, 8, split, s) for s in range(split)]
+        cov = [0] * 256
+        for b, e in rs:
+            assert b % 8 == 0 and e % 8 == 0 and e > b
+            for i in range(b, e):
+                cov[i] += 1
+        assert all(c == 1 for c in cov)
+
+
+def test_cu_range_for_clamps():
+    assert cu_range_for(256, 8, 4, 3, 50) == (128, 256)
