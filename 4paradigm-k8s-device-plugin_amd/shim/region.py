@@ -34,6 +34,7 @@ class DeviceInfo(C.Structure):
         ("cu_count", C.c_int32), ("num_xcc", C.c_int32), ("cu_mask_count", C.c_int32),
         ("cu_mask", C.c_uint32 * 8), ("tokens", C.c_int64), ("share", C.c_int64), ("util_pct", C.c_int32),
         ("gpu_id", C.c_uint32), ("bdf", C.c_uint32), ("domain", C.c_uint32), ("configured", C.c_uint32),
+        ("hbm_limit", C.c_uint64),
     ]
 
 
@@ -141,7 +142,7 @@ class Region:
             "cu_limit_pct": d.cu_limit_pct, "cu_count": d.cu_count, "num_xcc": d.num_xcc,
             "cu_mask_count": d.cu_mask_count, "cu_mask": mask, "tokens": d.tokens, "share": d.share,
             "util_pct": d.util_pct, "gpu_id": d.gpu_id, "bdf": d.bdf, "domain": d.domain,
-            "configured": bool(d.configured),
+            "configured": bool(d.configured), "hbm_limit": d.hbm_limit,
         }
 
     def devices(self):

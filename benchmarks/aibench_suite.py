@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""The reference's ten ai-benchmark cases, native vs inside a vGPU, on one MI355X.
+
+Reference numbers: BASELINE.md (2xV100, TF 2.4.1; native = official plugin, vGPU = split
+2 / memScaling 1.8 with the temporal SM limit). Columns measured here:
+
+* native        no shim
+* vgpu          1 vGPU of a 2-way split: quota = HBM/2, no CU limit (the interception
+                overhead the reference's "vGPU" column measures)
+* vgpu-cu50     same, plus a 50 % spatial CU mask (128 of 256 CUs) — what a tenant of a
+                2-way split with --device-cores-scaling=1 gets
+* vgpu-t50      same share enforced temporally (reference-parity token bucket)
+
+One worker process per column runs every case (warmup W, then K timed steps bracketed by
+synchronize). Output: JSON + a markdown table with ms/batch, throughput and overhead.
+
+    python benchmarks/aibench_suite.py [--cases all] [--modes native,vgpu,vgpu-cu50] [--steps 20]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+HBM = 309220868096
+
+MODES = {
+    "native": None,
+    "vgpu": dict(mem_limit=HBM // 2),
+    "vgpu-cu50": dict(mem_limit=HBM // 2, cu_limit=50),
+    "vgpu-t50": dict(mem_limit=HBM // 2, cu_limit=50, cu_mode="temporal"),
+}
+
+
+def worker(cases, steps, warmup, out):
+    import torch
+    from amdvgpu.models.aibench import Runner, get_case
+    res = {}
+    for name in cases:
+        case = get_case(name)
+        r = Runner(case, "cuda:0")
+        for _ in range(warmup):
+            r.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r.step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1000 / steps
+        res[name] = {"ms_per_batch": ms, "throughput": case.batch * 1000 / ms, "batch": case.batch}
+        print(f"  {name}: {ms:.3f} ms/batch, {case.batch * 1000 / ms:.1f} {case.unit}", flush=True)
+        del r
+        torch.cuda.empty_cache()
+    with open(out, "w") as f:
+        json.dump(res, f)
+
+
+def run_mode(mode, cases, steps, warmup):
+    from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
+    fd, out = tempfile.mkstemp(suffix=".json")
+    os.close(fd)
+    contract = vgpu_env(**MODES[mode]) if MODES[mode] else {}
+    env = apply_contract(contract) if contract else dict(os.environ)
+    cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--cases", ",".join(cases), "--steps", str(steps),
+           "--warmup", str(warmup), "--out", out]
+    print(f"[{mode}]", flush=True)
+    try:
+        rc = subprocess.call(cmd, env=env)
+        if rc:
+            raise SystemExit(f"{mode} worker failed ({rc})")
+        return json.load(open(out))
+    finally:
+        os.unlink(out)
+        cleanup_region(contract)
+
+
+def table(results, modes):
+    from amdvgpu.models.aibench import CASES
+    lines = ["| test | case | batch | " + " | ".join(f"{m} ms/batch" for m in modes) +
+             " | vgpu overhead | reference vGPU overhead (V100) | vgpu throughput | V100 vGPU throughput | x |",
+             "|" + "---|" * (8 + len(modes))]
+    ovs = []
+    for c in CASES:
+        if c.name not in results[modes[0]]:
+            continue
+        row = [c.test_id, c.name, str(c.batch)] + [f"{results[m][c.name]['ms_per_batch']:.2f}" for m in modes]
+        ov = ""
+        if "native" in results and "vgpu" in results:
+            n, v = results["native"][c.name]["ms_per_batch"], results["vgpu"][c.name]["ms_per_batch"]
+            ovs.append((v - n) / n * 100)
+            ov = f"{ovs[-1]:+.2f} %"
+        ref = (c.baseline_native / c.baseline_vgpu - 1) * 100
+        tp = results.get("vgpu", results[modes[-1]])[c.name]["throughput"]
+        row += [ov, f"{ref:+.1f} %", f"{tp:.1f} {c.unit}", f"{c.baseline_vgpu}", f"{tp / c.baseline_vgpu:.1f}"]
+        lines.append("| " + " | ".join(row) + " |")
+    if ovs:
+        s = sorted(ovs)
+        med = s[len(s) // 2] if len(s) % 2 else (s[len(s) // 2 - 1] + s[len(s) // 2]) / 2
+        lines.append("")
+        lines.append(f"vGPU overhead: median {med:+.2f} %, range {min(ovs):+.2f} % .. {max(ovs):+.2f} % "
+                     f"(reference: median +2.5 %, range -3.8 % .. +17.7 %)")
+    return "\n".join(lines)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", default="all")
+    ap.add_argument("--modes", default="native,vgpu,vgpu-cu50")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--worker", action="store_true")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--json-out", default=None)
+    ap.add_argument("--md-out", default=None)
+    a = ap.parse_args()
+    from amdvgpu.models.aibench import CASES
+    cases = [c.name for c in CASES] if a.cases == "all" else a.cases.split(",")
+    if a.worker:
+        return worker(cases, a.steps, a.warmup, a.out)
+    modes = a.modes.split(",")
+    results = {m: run_mode(m, cases, a.steps, a.warmup) for m in modes}
+    md = table(results, modes)
+    print(md)
+    if a.json_out:
+        json.dump({"steps": a.steps, "warmup": a.warmup, "results": results}, open(a.json_out, "w"), indent=1)
+    if a.md_out:
+        open(a.md_out, "w").write(md + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -32,6 +32,7 @@ enum class CuPolicy : int { kDefault = 0, kForce = 1, kDisable = 2 };
 
 struct DeviceConfig {
   uint64_t mem_limit = 0;      // bytes, 0 = unlimited
+  uint64_t hbm_limit = 0;      // HBM-resident cap (oversubscription), 0 = mem_limit
   int cu_limit_pct = 0;        // 0 or >= 100 = unlimited
   int cu_range_begin = -1;     // explicit logical CU range [begin, end) or -1 = derive
   int cu_range_end = -1;

@@ -37,7 +37,7 @@
 namespace vgpu {
 
 constexpr uint32_t kRegionMagic = 0x56475055u;  // "VGPU"
-constexpr uint32_t kRegionVersion = 1;
+constexpr uint32_t kRegionVersion = 2;
 
 enum ProcStatus : int32_t { kProcFree = 0, kProcRunning = 1, kProcSuspended = 2 };
 
@@ -67,6 +67,7 @@ struct alignas(64) ProcSlot {
 struct alignas(64) DeviceState {
   char uuid[64];
   uint64_t mem_limit;                     // bytes, 0 = unlimited
+  uint64_t hbm_limit;                     // HBM-resident cap; beyond it allocations spill (0 = off)
   uint64_t phys_total;                    // physical HBM bytes reported by ROCr
   int32_t cu_limit_pct;                   // 0 / >=100 = unlimited
   int32_t cu_count;                       // physical CUs of the agent
@@ -155,6 +156,9 @@ class SharedRegion {
 
   uint64_t usage(int dev) const;
   uint64_t limit(int dev) const;
+  uint64_t hbm_limit(int dev) const;
+  // Bytes of `dev` resident in HBM (charged minus spilled).
+  uint64_t resident(int dev) const;
   uint64_t proc_usage(int slot, int dev) const;
 
   // External control API (reference: set_current_device_memory_limit,

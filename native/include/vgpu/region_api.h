@@ -51,6 +51,7 @@ typedef struct {
   uint32_t bdf;
   uint32_t domain;
   uint32_t configured;
+  uint64_t hbm_limit;
 } vgpu_device_info;
 
 /* Returns NULL on failure; *err receives -errno. */

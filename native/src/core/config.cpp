@@ -118,6 +118,10 @@ void load_config(Config* cfg, GetenvFn getenv_fn) {
   if (const char* s = getenv_fn("VGPU_DEVICE_MEMORY_LIMIT")) {
     if (!parse_size(s, &global_limit)) VLOG_WARN("invalid VGPU_DEVICE_MEMORY_LIMIT=%s ignored", s);
   }
+  uint64_t global_hbm = 0;
+  if (const char* s = getenv_fn("VGPU_DEVICE_HBM_LIMIT")) {
+    if (!parse_size(s, &global_hbm)) VLOG_WARN("invalid VGPU_DEVICE_HBM_LIMIT=%s ignored", s);
+  }
   long global_cu = 0;
   if (const char* s = getenv_fn("VGPU_DEVICE_CU_LIMIT")) {
     if (!parse_int(s, 0, 100, &global_cu)) {
@@ -130,6 +134,7 @@ void load_config(Config* cfg, GetenvFn getenv_fn) {
   for (int i = 0; i < kMaxDevices; i++) {
     DeviceConfig& d = cfg->dev[i];
     d.mem_limit = global_limit;
+    d.hbm_limit = global_hbm;
     d.cu_limit_pct = (int)global_cu;
     snprintf(key, sizeof(key), "VGPU_DEVICE_MEMORY_LIMIT_%d", i);
     if (const char* s = getenv_fn(key)) {
@@ -140,6 +145,12 @@ void load_config(Config* cfg, GetenvFn getenv_fn) {
       } else {
         VLOG_WARN("invalid %s=%s ignored", key, s);
       }
+    }
+    snprintf(key, sizeof(key), "VGPU_DEVICE_HBM_LIMIT_%d", i);
+    if (const char* s = getenv_fn(key)) {
+      uint64_t v = 0;
+      if (parse_size(s, &v)) d.hbm_limit = v;
+      else VLOG_WARN("invalid %s=%s ignored", key, s);
     }
     snprintf(key, sizeof(key), "VGPU_DEVICE_CU_LIMIT_%d", i);
     if (const char* s = getenv_fn(key)) {

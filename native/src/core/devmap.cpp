@@ -79,6 +79,8 @@ int resolve_devices(const Config& cfg, const DeviceMap& map, const char* const* 
           // Second vGPU of the same physical GPU: merge quota and CU share.
           if (out[k].mem_limit && c.mem_limit) out[k].mem_limit += c.mem_limit;
           else out[k].mem_limit = 0;
+          if (out[k].hbm_limit && c.hbm_limit) out[k].hbm_limit += c.hbm_limit;
+          else out[k].hbm_limit = 0;
           int pct = out[k].cu_limit_pct + c.cu_limit_pct;
           out[k].cu_limit_pct = (out[k].cu_limit_pct && c.cu_limit_pct && pct < 100) ? pct : 0;
           // Adjacent CU ranges from the plugin collapse into one; anything else falls

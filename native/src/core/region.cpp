@@ -151,6 +151,7 @@ void SharedRegion::init_fresh(const Config* cfg) {
     for (int i = 0; i < kMaxDevices; i++) {
       DeviceState& d = r_->dev[i];
       d.mem_limit = cfg->dev[i].mem_limit;
+      d.hbm_limit = cfg->dev[i].hbm_limit;
       d.cu_limit_pct = cfg->dev[i].cu_limit_pct;
       memcpy(d.uuid, cfg->dev[i].uuid, sizeof(d.uuid));
       d.uuid[sizeof(d.uuid) - 1] = 0;
@@ -350,6 +351,12 @@ void SharedRegion::uncharge(int slot, int dev, uint64_t bytes, MemKind kind) {
 
 uint64_t SharedRegion::usage(int dev) const { return r_->dev[dev].used.load(std::memory_order_relaxed); }
 uint64_t SharedRegion::limit(int dev) const { return r_->dev[dev].mem_limit; }
+uint64_t SharedRegion::hbm_limit(int dev) const { return r_->dev[dev].hbm_limit; }
+uint64_t SharedRegion::resident(int dev) const {
+  uint64_t u = r_->dev[dev].used.load(std::memory_order_relaxed);
+  uint64_t s = r_->dev[dev].spilled.load(std::memory_order_relaxed);
+  return u > s ? u - s : 0;
+}
 uint64_t SharedRegion::proc_usage(int slot, int dev) const { return r_->procs[slot].used[dev].total.load(); }
 
 void SharedRegion::set_limit(int dev, uint64_t bytes) {

@@ -60,6 +60,7 @@ int vgpu_region_device_info(vgpu_region* r, int dev, vgpu_device_info* out) {
   out->bdf = d.bdf;
   out->domain = d.domain;
   out->configured = d.configured;
+  out->hbm_limit = d.hbm_limit;
   return 0;
 }
 

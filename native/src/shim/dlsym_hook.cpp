@@ -1,0 +1,105 @@
+// dlsym interposition for SMI libraries that are dlopen'ed (amd-smi / rocm-smi CLIs).
+//
+// Reference: libvgpu.so overrides dlsym [src/libvgpu.c:109-124] so that runtimes that
+// dlopen the driver still reach the hooks. On MI355X the HIP runtime links ROCr
+// directly (no dlsym needed for the HSA/HIP hooks), but the in-container SMI tools
+// are Python (ctypes over libamd_smi.so / librocm_smi64.so): ctypes resolves every
+// entry point with dlsym(handle, name), which never consults the preloaded shim. So
+// dlsym is interposed, but narrowly:
+//   * only names starting with "amdsmi_" / "rsmi_" that resolve into an SMI library
+//     and have a virtualising hook are redirected (to smi_hooks.cpp);
+//   * every other lookup is a guaranteed tail call ([[clang::musttail]]) into glibc,
+//     so RTLD_NEXT keeps resolving relative to the *original* caller - other
+//     interposers preloaded alongside the shim are unaffected.
+// Both glibc symbol versions are provided (dlsym@GLIBC_2.2.5 for old binaries,
+// dlsym@@GLIBC_2.34 for current ones). This file is compiled with clang (musttail).
+#include <dlfcn.h>
+
+#include <atomic>
+#include <cstring>
+
+#include <amd_smi/amdsmi.h>
+#include <rocm_smi/rocm_smi.h>
+
+extern "C" {
+amdsmi_status_t amdsmi_get_gpu_memory_total(amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*);
+amdsmi_status_t amdsmi_get_gpu_memory_usage(amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*);
+amdsmi_status_t amdsmi_get_gpu_vram_usage(amdsmi_processor_handle, amdsmi_vram_usage_t*);
+rsmi_status_t rsmi_dev_memory_total_get(uint32_t, rsmi_memory_type_t, uint64_t*);
+rsmi_status_t rsmi_dev_memory_usage_get(uint32_t, rsmi_memory_type_t, uint64_t*);
+}
+
+namespace {
+
+using DlsymFn = void* (*)(void*, const char*);
+
+std::atomic<DlsymFn> g_real_234{nullptr};
+std::atomic<DlsymFn> g_real_225{nullptr};
+
+DlsymFn load_real(std::atomic<DlsymFn>& slot, const char* ver) {
+  DlsymFn f = slot.load(std::memory_order_acquire);
+  if (__builtin_expect(f != nullptr, 1)) return f;
+  f = reinterpret_cast<DlsymFn>(dlvsym(RTLD_NEXT, "dlsym", ver));
+  if (!f) f = reinterpret_cast<DlsymFn>(dlvsym(RTLD_NEXT, "dlsym", ver[7] == '3' ? "GLIBC_2.2.5" : "GLIBC_2.34"));
+  slot.store(f, std::memory_order_release);
+  return f;
+}
+
+struct Hook {
+  const char* name;
+  void* fn;
+};
+
+const Hook kHooks[] = {
+    {"amdsmi_get_gpu_memory_total", reinterpret_cast<void*>(&amdsmi_get_gpu_memory_total)},
+    {"amdsmi_get_gpu_memory_usage", reinterpret_cast<void*>(&amdsmi_get_gpu_memory_usage)},
+    {"amdsmi_get_gpu_vram_usage", reinterpret_cast<void*>(&amdsmi_get_gpu_vram_usage)},
+    {"rsmi_dev_memory_total_get", reinterpret_cast<void*>(&rsmi_dev_memory_total_get)},
+    {"rsmi_dev_memory_usage_get", reinterpret_cast<void*>(&rsmi_dev_memory_usage_get)},
+};
+
+__attribute__((noinline)) void* maybe_hook(void* handle, const char* name, DlsymFn real) {
+  if (handle == RTLD_NEXT || handle == RTLD_DEFAULT) return nullptr;
+  if (strncmp(name, "amdsmi_", 7) != 0 && strncmp(name, "rsmi_", 5) != 0) return nullptr;
+  for (const Hook& h : kHooks) {
+    if (strcmp(name, h.name) != 0) continue;
+    void* p = real(handle, name);
+    if (!p) return nullptr;
+    Dl_info info;
+    if (!dladdr(p, &info) || !info.dli_fname) return nullptr;
+    const char* f = info.dli_fname;
+    if ((strstr(f, "amd_smi") || strstr(f, "rocm_smi")) && !strstr(f, "vgpu")) return h.fn;
+    return nullptr;
+  }
+  return nullptr;
+}
+
+}  // namespace
+
+namespace vgpu {
+// The shim's own lookups must bypass the interposer (they want the real SMI symbols).
+void* real_dlsym(void* handle, const char* name) { return load_real(g_real_234, "GLIBC_2.34")(handle, name); }
+}  // namespace vgpu
+
+extern "C" {
+
+__attribute__((visibility("default"))) void* shim_dlsym_v234(void* handle, const char* name) {
+  DlsymFn real = load_real(g_real_234, "GLIBC_2.34");
+  if (__builtin_expect(name && (name[0] == 'a' || name[0] == 'r'), 0)) {
+    if (void* h = maybe_hook(handle, name, real)) return h;
+  }
+  [[clang::musttail]] return real(handle, name);
+}
+
+__attribute__((visibility("default"))) void* shim_dlsym_v225(void* handle, const char* name) {
+  DlsymFn real = load_real(g_real_225, "GLIBC_2.2.5");
+  if (__builtin_expect(name && (name[0] == 'a' || name[0] == 'r'), 0)) {
+    if (void* h = maybe_hook(handle, name, real)) return h;
+  }
+  [[clang::musttail]] return real(handle, name);
+}
+
+}  // extern "C"
+
+__asm__(".symver shim_dlsym_v234, dlsym@@GLIBC_2.34");
+__asm__(".symver shim_dlsym_v225, dlsym@GLIBC_2.2.5");

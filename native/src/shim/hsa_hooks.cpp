@@ -131,7 +131,21 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
               (unsigned long)s.region.usage(dev), (unsigned long)s.region.limit(dev));
     return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   }
-  hsa_status_t st = real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
+  hsa_status_t st;
+  // Virtual device memory: past the tenant's HBM-resident share the quota is served
+  // from host memory (VGPU_DEVICE_HBM_LIMIT_<i>, emitted by the plugin when
+  // --device-memory-scaling > 1), so one tenant cannot crowd the others out of HBM.
+  uint64_t hbm = config().oversubscribe ? s.region.hbm_limit(dev) : 0;
+  if (hbm && s.region.resident(dev) > hbm) {
+    st = spill_allocate(dev, size, ptr);
+    if (st == HSA_STATUS_SUCCESS) {
+      s.region.uncharge(s.slot, dev, size, kMemData);
+      s.region.force_charge(s.slot, dev, size, kMemSpill);
+      record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemSpill);
+      return st;
+    }
+  }
+  st = real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
   if (st == HSA_STATUS_SUCCESS) {
     record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemData);
     return st;

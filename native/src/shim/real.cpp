@@ -39,13 +39,13 @@ void* resolve_real(const char* lib_substr, const char* name, const char* ver) {
     void* h = dlopen(f.path, RTLD_NOLOAD | RTLD_LAZY);
     if (h) {
       p = ver ? dlvsym(h, name, ver) : nullptr;
-      if (!p) p = dlsym(h, name);
+      if (!p) p = real_dlsym(h, name);
       // dlopen(RTLD_NOLOAD) took a reference; the object stays loaded regardless.
       dlclose(h);
     }
   }
   if (!p) p = ver ? dlvsym(RTLD_NEXT, name, ver) : nullptr;
-  if (!p) p = dlsym(RTLD_NEXT, name);
+  if (!p) p = real_dlsym(RTLD_NEXT, name);
   if (!p) VLOG_ERROR("cannot resolve real %s in %s", name, lib_substr);
   return p;
 }

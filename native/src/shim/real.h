@@ -10,6 +10,9 @@
 
 namespace vgpu {
 
+// glibc's dlsym, bypassing the shim's own dlsym interposer (dlsym_hook.cpp).
+void* real_dlsym(void* handle, const char* name);
+
 // Looks `name` (version `ver`, may be null) up in the first loaded object whose path
 // contains `lib_substr`; falls back to RTLD_NEXT. Returns null when absent.
 void* resolve_real(const char* lib_substr, const char* name, const char* ver);

@@ -256,6 +256,7 @@ void shim_init_after_hsa() {
       d.bdf = bdf;
       d.domain = dom;
       if (!d.mem_limit && per_agent[i].mem_limit) d.mem_limit = per_agent[i].mem_limit;
+      if (!d.hbm_limit && per_agent[i].hbm_limit) d.hbm_limit = per_agent[i].hbm_limit;
       if (!d.cu_limit_pct && per_agent[i].cu_limit_pct) d.cu_limit_pct = per_agent[i].cu_limit_pct;
       CuMask m = cu_mask_for(a.cu_count, a.num_xcc, d.cu_limit_pct, per_agent[i].cu_range_begin,
                              per_agent[i].cu_range_end);

@@ -1,0 +1,139 @@
+"""Allocate contract details, flag/env parsing, legacy checkpoint and monitor-mode matching."""
+import base64
+import json
+import os
+
+import pytest
+
+from amdvgpu.plugin import api
+from amdvgpu.plugin.config import PluginConfig, parse_config
+from amdvgpu.plugin.contract import ANN_REQUEST, ANN_USING, build_container_response, response_to_env
+from amdvgpu.plugin.devices import FakeBackend
+from amdvgpu.plugin.k8s import PodMatcher, pod_summary
+from amdvgpu.plugin.legacy import LegacyController
+from amdvgpu.plugin.vdevice import device_to_vdevices
+
+
+def _setup(**kw):
+    cfg = PluginConfig(**kw).validate()
+    devs = FakeBackend(n=2).devices()
+    vds = device_to_vdevices(devs, cfg.device_split_count, cfg.device_memory_scaling, cfg.device_cores_scaling)
+    return cfg, devs, vds, {d.uuid: d for d in devs}
+
+
+def test_oversubscription_contract():
+    cfg, devs, vds, by = _setup(device_split_count=2, device_memory_scaling=1.8)
+    envs = dict(build_container_response(cfg, [vds[0]], by).envs)
+    total = devs[0].memory_total >> 20
+    assert envs["VGPU_OVERSUBSCRIBE"] == "true"
+    assert envs["VGPU_DEVICE_MEMORY_LIMIT_0"] == f"{int(total * 1.8 / 2)}m"
+    assert envs["VGPU_DEVICE_HBM_LIMIT_0"] == f"{total // 2}m"
+
+
+def test_index_strategy_and_runtime_list():
+    cfg, devs, vds, by = _setup(device_id_strategy="index", device_list_strategy="amd-container-runtime")
+    envs = dict(build_container_response(cfg, [vds[2]], by).envs)
+    assert envs["AMD_VISIBLE_DEVICES"] == "1"
+    assert "ROCR_VISIBLE_DEVICES" not in envs
+
+
+def test_volume_mounts_strategy():
+    cfg, devs, vds, by = _setup(device_list_strategy="volume-mounts")
+    r = build_container_response(cfg, [vds[0]], by)
+    assert any(m.container_path.startswith("/var/run/amd-container-devices/") for m in r.mounts)
+
+
+def test_no_device_specs_when_disabled():
+    cfg, devs, vds, by = _setup(pass_device_specs=False)
+    assert len(build_container_response(cfg, [vds[0]], by).devices) == 0
+
+
+def test_monitor_mode_host_path(tmp_path):
+    cfg, devs, vds, by = _setup(monitor_mode=True, vgpu_dir=str(tmp_path))
+    r = build_container_response(cfg, [vds[0]], by, pod_tag="mypod_main")
+    envs, mounts = response_to_env(r)
+    assert envs["VGPU_SHARED_CACHE"].startswith("/mypod_main/")
+    assert ("/mypod_main", str(tmp_path / "shared" / "mypod_main")) in mounts
+    assert (tmp_path / "shared" / "mypod_main").is_dir()
+
+
+def test_temporal_mode_env():
+    cfg, devs, vds, by = _setup(cu_mode="temporal")
+    assert dict(build_container_response(cfg, [vds[0]], by).envs)["VGPU_CU_MODE"] == "temporal"
+
+
+def test_pcibus_mount_only_when_present(tmp_path):
+    f = tmp_path / "pci"
+    cfg, devs, vds, by = _setup(pcibus_file=str(f))
+    paths = [m.container_path for m in build_container_response(cfg, [vds[0]], by).mounts]
+    assert "/usr/local/vgpu/pciinfo.vgpu" not in paths
+    f.write_text("0000:05:00.0\n")
+    paths = [m.container_path for m in build_container_response(cfg, [vds[0]], by).mounts]
+    assert "/usr/local/vgpu/pciinfo.vgpu" in paths
+
+
+def test_flags_env_fallback_and_validation():
+    cfg = parse_config([], environ={"DEVICE_SPLIT_COUNT": "4", "DEVICE_MEMORY_SCALING": "1.5",
+                                    "MIG_STRATEGY": "mixed", "PASS_DEVICE_SPECS": "false"})
+    assert cfg.device_split_count == 4 and cfg.device_memory_scaling == 1.5
+    assert cfg.partition_strategy == "mixed" and cfg.pass_device_specs is False
+    cfg = parse_config(["--device-split-count", "8", "--mig-strategy", "single"], environ={"DEVICE_SPLIT_COUNT": "3"})
+    assert cfg.device_split_count == 8 and cfg.partition_strategy == "single"
+    for bad in (["--device-split-count", "0"], ["--device-memory-scaling", "0"], ["--device-cores-scaling", "-1"],
+                ["--device-list-strategy", "x"], ["--device-id-strategy", "x"], ["--cu-mode", "x"],
+                ["--partition-strategy", "x"]):
+        with pytest.raises(ValueError):
+            parse_config(bad, environ={})
+    assert parse_config(["--fail-on-init-error=false"], environ={}).fail_on_init_error is False
+
+
+def _checkpoint(tmp_path, entries):
+    data = {"Data": {"PodDeviceEntries": entries, "RegisteredDevices": {"amd.com/gpu": []}}, "Checksum": 1}
+    (tmp_path / "kubelet_internal_checkpoint").write_text(json.dumps(data))
+
+
+def _alloc_resp(request, using):
+    r = api.ContainerAllocateResponse()
+    r.annotations[ANN_REQUEST] = ",".join(request)
+    r.annotations[ANN_USING] = ",".join(using)
+    return base64.b64encode(r.SerializeToString()).decode()
+
+
+def test_legacy_checkpoint_acquire_release(tmp_path):
+    ids = ["g-0", "g-1", "h-0", "h-1"]
+    _checkpoint(tmp_path, [
+        {"PodUID": "p1", "ContainerName": "c", "ResourceName": "amd.com/gpu", "DeviceIDs": ["g-0"],
+         "AllocResp": _alloc_resp(["g-0"], ["h-0"])},
+        {"PodUID": "p2", "ContainerName": "c", "ResourceName": "amd.com/gpu", "DeviceIDs": {"0": ["g-1"]},
+         "AllocResp": _alloc_resp(["g-1"], ["h-1"])},
+        {"PodUID": "p3", "ContainerName": "c", "ResourceName": "other/res", "DeviceIDs": ["x"],
+         "AllocResp": _alloc_resp(["x"], ["g-0"])},
+    ])
+    lc = LegacyController(ids, "amd.com/gpu", str(tmp_path),
+                          pod_lister=lambda: [{"uid": "p1", "phase": "Running"}, {"uid": "p2", "phase": "Succeeded"}])
+    assert lc.update_from_checkpoint()
+    assert lc.id_map["h-0"] == "g-0"     # live pod keeps its substitution
+    assert lc.id_map["h-1"] == ""        # finished pod released
+    assert lc.available(ids) == ["g-0", "g-1", "h-1"]
+    lc.release_by_request(["g-0"])
+    assert lc.id_map["h-0"] == ""
+
+
+def test_legacy_missing_checkpoint(tmp_path):
+    lc = LegacyController(["a"], "amd.com/gpu", str(tmp_path))
+    assert lc.update_from_checkpoint() is False
+
+
+def test_monitor_pod_matcher():
+    pods = [
+        pod_summary({"metadata": {"uid": "1", "name": "old", "creationTimestamp": "2024-01-01"},
+                     "spec": {"containers": [{"name": "a", "resources": {"limits": {"amd.com/gpu": "2"}}}]},
+                     "status": {"phase": "Running"}}),
+        pod_summary({"metadata": {"uid": "2", "name": "new", "creationTimestamp": "2024-01-02"},
+                     "spec": {"containers": [{"name": "side"}, {"name": "main", "resources": {
+                         "limits": {"amd.com/gpu": "1"}}}]}, "status": {"phase": "Pending"}}),
+    ]
+    m = PodMatcher(lambda: pods)
+    assert m.match([1]) == ["new_main"]
+    with pytest.raises(LookupError):
+        m.match([2])

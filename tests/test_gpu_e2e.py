@@ -1,0 +1,186 @@
+"""End-to-end on a real MI355X: plugin (sysfs backend) -> stub kubelet -> Allocate ->
+'container' running stock PyTorch-ROCm under the returned contract,
+plus oversubscription spill, SMI virtualisation and RCCL through the shim."""
+import os
+import threading
+
+import pytest
+
+from amdvgpu.plugin.config import PluginConfig
+from amdvgpu.plugin.devices import SysfsBackend
+from amdvgpu.plugin.kubelet_stub import StubKubelet, run_pod
+from amdvgpu.plugin.main import Supervisor
+from amdvgpu.shim.launcher import vgpu_env
+from conftest import CHILD_PRELUDE, run_child
+
+pytestmark = pytest.mark.gpu
+
+GiB = 1 << 30
+MiB = 1 << 20
+
+
+def test_sysfs_backend_sees_the_mi355x():
+    devs = SysfsBackend().devices()
+    assert len(devs) >= 1
+    d = devs[0]
+    assert d.cu_count == 256 and d.num_xcc == 8
+    assert d.memory_total >= 280 * GiB
+    assert d.render_minor >= 128
+    assert d.uuid.startswith("GPU-")
+
+
+def test_sysfs_uuid_matches_rocr(tmp_region):
+    """The plugin's UUIDs (VGPU_DEVICE_MAP / ROCR_VISIBLE_DEVICES) are ROCr's UUIDs."""
+    devs = SysfsBackend().devices()
+    c = vgpu_env(mem_limit=8 * GiB, shared_cache=tmp_region, device_map=[devs[0].uuid])
+    res, _ = run_child("""
+import torch
+from amdvgpu.shim.region import Region
+torch.cuda.mem_get_info(0)
+emit(uuid=Region(os.environ["VGPU_SHARED_CACHE"]).device(0)["uuid"])
+""", c, extra_env={"ROCR_VISIBLE_DEVICES": devs[0].uuid})
+    assert res[0]["uuid"].lower() == devs[0].uuid.lower()
+
+
+@pytest.fixture
+def plugin(tmp_path):
+    pdir = str(tmp_path / "dp")
+    os.makedirs(pdir)
+    cfg = PluginConfig(device_plugin_path=pdir + "/", backend="sysfs", device_split_count=4,
+                       shared_cache_dir=str(tmp_path)).validate()
+    k = StubKubelet(pdir).start()
+    sup = Supervisor(cfg, backend=SysfsBackend(), install_signals=False)
+    stop = threading.Event()
+    th = threading.Thread(target=sup.run, args=(stop,), daemon=True)
+    th.start()
+    k.wait_registered("amd.com/gpu", timeout=20)
+    yield k
+    stop.set()
+    th.join(10)
+    k.stop()
+
+
+def test_slice_resnet50_in_allocated_vgpu(plugin):
+    """4-way split: quota = HBM/4 (72 GiB), kernels confined to 64 CUs, model runs."""
+    code = CHILD_PRELUDE + """
+import torch
+from amdvgpu.models.aibench import Runner, get_case
+from amdvgpu.ops import cu_census
+free, total = torch.cuda.mem_get_info(0)
+r = Runner(get_case("resnet50-inf"), "cuda:0")
+for _ in range(3): r.step()
+torch.cuda.synchronize()
+t0 = time.time()
+for _ in range(10): r.step()
+torch.cuda.synchronize()
+dt = (time.time() - t0) / 10
+ncu = len(cu_census(nblocks=8192, spin_us=300))
+emit(total=total, ms=dt * 1000, ips=50 / dt, ncu=ncu)
+"""
+    import sys
+    ids, envs, proc = run_pod(plugin, "amd.com/gpu", 1, [sys.executable, "-c", code], capture_output=True,
+                              text=True, timeout=600)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    import json
+    r = [json.loads(l[7:]) for l in proc.stdout.splitlines() if l.startswith("RESULT ")][0]
+    quota = int(envs["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m")) * MiB
+    assert r["total"] == quota and 70 * GiB <= quota <= 73 * GiB
+    assert r["ncu"] == 64
+    assert envs["VGPU_DEVICE_CU_RANGE_0"] in ("0-64", "64-128", "128-192", "192-256")
+    print(f"slice: ResNet-V2-50 b=50 inference in a 1/4 vGPU (64 CUs): {r['ips']:.1f} img/s")
+
+
+def test_oversubscription_spills_past_hbm_share(tmp_region):
+    c = vgpu_env(mem_limit=8 * GiB, shared_cache=tmp_region, oversubscribe=True,
+                 extra={"VGPU_DEVICE_HBM_LIMIT_0": "2048m"})
+    res, _ = run_child("""
+import torch
+from amdvgpu.shim.region import Region
+from amdvgpu.ops import stream_copy
+free, total = torch.cuda.mem_get_info(0)
+a = torch.ones(1536 << 20, dtype=torch.uint8, device="cuda")     # resident
+b = torch.full((1024 << 20,), 3, dtype=torch.uint8, device="cuda")  # crosses the share -> host
+c = torch.full((1024 << 20,), 5, dtype=torch.uint8, device="cuda")  # host
+torch.cuda.synchronize()
+s = int(a[:1 << 20].sum()) + int(b.sum()) + int(c.sum())
+r = Region(os.environ["VGPU_SHARED_CACHE"]).device(0)
+# bandwidth of a kernel reading spilled memory
+dst = torch.empty_like(c)
+stream_copy(dst, c); torch.cuda.synchronize()
+t0 = time.time()
+for _ in range(5): stream_copy(dst, c)
+torch.cuda.synchronize()
+bw = 5 * c.numel() / (time.time() - t0) / 1e9
+try:
+    d = torch.empty(6 << 30, dtype=torch.uint8, device="cuda")
+    over = False
+except torch.OutOfMemoryError:
+    over = True
+emit(total=total, s=s, spilled=r["spilled"], used=r["used"], hbm=r["hbm_limit"], bw=bw, over=over,
+     ok=bool((dst == 5).all()))
+""", c)
+    r = res[0]
+    assert r["total"] == 8 * GiB
+    assert r["s"] == (1 << 20) + 3 * (1024 << 20) + 5 * (1024 << 20)
+    assert r["spilled"] >= 2 * GiB - 64 * MiB
+    assert r["hbm"] == 2 * GiB
+    assert r["ok"] and r["over"]
+    print(f"spill read bandwidth {r['bw']:.1f} GB/s")
+
+
+def test_amdsmi_reports_quota(tmp_region):
+    """In-container amd-smi (Python amdsmi over ctypes) sees the vGPU quota."""
+    c = vgpu_env(mem_limit=24 * GiB, shared_cache=tmp_region)
+    res, _ = run_child("""
+import torch
+torch.cuda.mem_get_info(0)          # first GPU process records the device's BDF in the region
+x = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+try:
+    import amdsmi
+    amdsmi.amdsmi_init()
+    h = amdsmi.amdsmi_get_processor_handles()[0]
+    total = amdsmi.amdsmi_get_gpu_memory_total(h, amdsmi.AmdSmiMemoryType.VRAM)
+    used = amdsmi.amdsmi_get_gpu_memory_usage(h, amdsmi.AmdSmiMemoryType.VRAM)
+    emit(ok=True, total=total, used=used)
+except Exception as e:
+    emit(ok=False, err=repr(e)[:300])
+""", c)
+    r = res[0]
+    if not r["ok"]:
+        pytest.skip(f"amdsmi unavailable on this box: {r['err']}")
+    assert r["total"] == 24 * GiB
+    assert GiB <= r["used"] <= 24 * GiB
+
+
+def test_rccl_allreduce_through_shim(tmp_region):
+    c = vgpu_env(mem_limit=16 * GiB, shared_cache=tmp_region)
+    res, _ = run_child("""
+import torch, torch.distributed as dist
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29611")
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+x = torch.ones(1 << 24, device="cuda")
+dist.all_reduce(x)
+torch.cuda.synchronize()
+emit(v=float(x[0]))
+dist.destroy_process_group()
+""", c)
+    assert res[0]["v"] == 1.0
+
+
+def test_temporal_mode_graph_launch(tmp_region):
+    c = vgpu_env(cu_limit=50, cu_mode="temporal", shared_cache=tmp_region)
+    res, _ = run_child("""
+import torch
+x = torch.zeros(1 << 20, device="cuda")
+s = torch.cuda.Stream()
+with torch.cuda.stream(s):
+    x.add_(1)
+torch.cuda.synchronize()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    for _ in range(4): x.add_(1)
+for _ in range(50): g.replay()
+torch.cuda.synchronize()
+emit(v=float(x[0]))
+""", c)
+    assert res[0]["v"] == 201.0

@@ -30,6 +30,18 @@ if has bench; then
   timeout -k 10 900 python bench.py --steps 20 --warmup 5 --json-out $OUT/bench.json > $OUT/bench.log 2>&1
   rc=$?; tail -3 $OUT/bench.log; [ $rc -eq 0 ] || exit $rc
 fi
+if has suite; then
+  step suite
+  timeout -k 10 900 python benchmarks/aibench_suite.py --steps 20 --warmup 5 --modes ${SUITE_MODES:-native,vgpu,vgpu-cu50} \
+    --json-out $OUT/suite.json --md-out $OUT/suite.md > $OUT/suite.log 2>&1
+  rc=$?; tail -16 $OUT/suite.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has scaling; then
+  step scaling
+  timeout -k 10 900 python benchmarks/vgpu_scaling.py --json-out $OUT/scaling.json --md-out $OUT/scaling.md \
+    > $OUT/scaling.log 2>&1
+  rc=$?; tail -14 $OUT/scaling.log; [ $rc -eq 0 ] || exit $rc
+fi
 if has prof; then
   step prof
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- \
