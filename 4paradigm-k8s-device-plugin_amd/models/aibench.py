@@ -275,7 +275,7 @@ class Runner:
     device (the reference's ai-benchmark also feeds a fixed random batch).
     """
 
-    def __init__(self, case, device, dtype=torch.bfloat16, batch=None, channels_last=True, seed=0):
+    def __init__(self, case, device, dtype=torch.bfloat16, batch=None, channels_last=True, seed=0, fuse=True):
         self.case, self.device, self.dtype = case, torch.device(device), dtype
         self.batch = batch or case.batch
         g = torch.Generator(device="cpu").manual_seed(seed)
@@ -296,9 +296,19 @@ class Runner:
             self.opt = torch.optim.SGD(model.parameters(), lr=1e-3, momentum=0.9)
         else:
             model.eval()
-            model = model.to(dtype)
+            if fuse and isinstance(model, ResNetV2) and dtype == torch.bfloat16 and channels_last:
+                # Inference epilogues fused into one HIP pass each (ops/fused.py); BN
+                # scale/shift are derived in fp32 before the weights are cast.
+                from ..ops.fused import fuse_resnet_v2
+                model = fuse_resnet_v2(model, impl="hip" if self.device.type == "cuda" else "torch")
+                for m in model.modules():
+                    if isinstance(m, (nn.Conv2d, nn.Linear)):
+                        m.to(dtype)
+            else:
+                model = model.to(dtype)
             self.x = self.x.to(dtype)
             self.opt = None
+        self.fused = fuse and not case.train and isinstance(model, nn.Module) and type(model).__name__ == "FusedResNetV2"
         self.model = model
 
     def step(self):

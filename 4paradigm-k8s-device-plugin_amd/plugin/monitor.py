@@ -1,0 +1,210 @@
+"""Node-side vGPU monitor: Prometheus metrics + control API over the containers' regions.
+
+Reference: with ``VGPU_MONITOR_MODE`` each container's shared region lives on a host path
+``/usr/local/vgpu/shared/<pod>_<ctr>/<uuid>.cache`` (``server.go:494-501``) so that an
+*external* monitor can mmap it and drive the control API exported by libvgpu.so
+(``suspend_all``, ``resume_all``, ``set_current_device_sm_limit_scale``,
+``set_current_device_memory_limit``, ``recent_kernel``, ``priority``).
+That monitor is not part of the reference; this is the in-tree one.
+
+* ``GET /metrics``  Prometheus text: per container/device memory limit, usage, spill,
+  monitored usage, CU limit/mask width, utilisation, token bucket, per process
+  launches / throttle / suspend seconds / OOM events, suspend state;
+* ``GET /regions``  JSON snapshot of every region;
+* ``POST /regions/<pod_ctr>/{suspend,resume,block,unblock,reclaim}`` and
+  ``POST /regions/<pod_ctr>/limit?dev=0&bytes=N`` / ``cu?dev=0&pct=P`` / ``priority?value=N``.
+
+    python -m amdvgpu.plugin.monitor --root /usr/local/vgpu/shared --port 9394
+"""
+import argparse
+import glob
+import json
+import logging
+import os
+import threading
+import urllib.parse
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+from ..shim.region import Region
+
+log = logging.getLogger("amdvgpu.monitor")
+
+
+def discover(root):
+    """{container tag: [region paths]} under ``root/<pod>_<ctr>/*.cache``."""
+    out = {}
+    for p in sorted(glob.glob(os.path.join(root, "*", "*.cache"))):
+        out.setdefault(os.path.basename(os.path.dirname(p)), []).append(p)
+    return out
+
+
+def _esc(v):
+    return str(v).replace("\\", "\\\\").replace('"', '\\"').replace("\n", " ")
+
+
+def _labels(**kw):
+    return "{" + ",".join(f'{k}="{_esc(v)}"' for k, v in kw.items()) + "}"
+
+
+class MetricsWriter:
+    def __init__(self):
+        self.lines = []
+        self._seen = set()
+
+    def metric(self, name, mtype, help_, labels, value):
+        if name not in self._seen:
+            self._seen.add(name)
+            self.lines.append(f"# HELP {name} {help_}")
+            self.lines.append(f"# TYPE {name} {mtype}")
+        self.lines.append(f"{name}{_labels(**labels)} {value}")
+
+    def text(self):
+        return "\n".join(self.lines) + "\n"
+
+
+def render_metrics(root):
+    w = MetricsWriter()
+    regions = discover(root)
+    w.metric("vgpu_monitor_regions", "gauge", "container regions found", {}, sum(len(v) for v in regions.values()))
+    for tag, paths in regions.items():
+        for path in paths:
+            try:
+                with Region(path) as r:
+                    snap = r.snapshot()
+            except OSError as e:
+                log.warning("skip region %s: %s", path, e)
+                continue
+            base = {"container": tag, "region": os.path.basename(path)}
+            w.metric("vgpu_container_suspended", "gauge", "1 while every gate of the container blocks", base,
+                     int(snap["suspended"]))
+            w.metric("vgpu_container_priority", "gauge", "task priority", base, snap["priority"])
+            w.metric("vgpu_container_processes", "gauge", "processes attached to the region", base,
+                     len(snap["procs"]))
+            for d in snap["devices"]:
+                if not d["configured"] and not d["mem_limit"]:
+                    continue
+                lb = dict(base, device=d["index"], uuid=d["uuid"])
+                w.metric("vgpu_memory_limit_bytes", "gauge", "device memory quota (0 = unlimited)", lb,
+                         d["mem_limit"])
+                w.metric("vgpu_memory_used_bytes", "gauge", "bytes charged to the container", lb, d["used"])
+                w.metric("vgpu_memory_spilled_bytes", "gauge", "bytes served from host memory", lb, d["spilled"])
+                w.metric("vgpu_memory_monitored_bytes", "gauge", "KFD-measured VRAM of the container's processes",
+                         lb, d["monitor_used"])
+                w.metric("vgpu_cu_limit_percent", "gauge", "CU share (0 = unlimited)", lb, d["cu_limit_pct"])
+                w.metric("vgpu_cu_mask_count", "gauge", "CUs in the spatial mask", lb, d["cu_mask_count"])
+                w.metric("vgpu_utilization_percent", "gauge", "last sampled utilisation", lb, d["util_pct"])
+                w.metric("vgpu_tokens", "gauge", "temporal-limiter bucket (workgroups)", lb, d["tokens"])
+            for p in snap["procs"]:
+                lp = dict(base, pid=p["pid"], hostpid=p["hostpid"])
+                w.metric("vgpu_process_launches_total", "counter", "kernel launches through the gates", lp,
+                         p["launches"])
+                w.metric("vgpu_process_throttle_seconds_total", "counter", "time blocked by the rate limiter", lp,
+                         p["throttle_ns"] / 1e9)
+                w.metric("vgpu_process_suspend_seconds_total", "counter", "time blocked while suspended", lp,
+                         p["suspend_ns"] / 1e9)
+                w.metric("vgpu_process_oom_events_total", "counter", "allocations refused at the quota", lp,
+                         p["oom_events"])
+                for dev, used in enumerate(p["used"]):
+                    if used:
+                        w.metric("vgpu_process_memory_used_bytes", "gauge", "bytes charged to the process",
+                                 dict(lp, device=dev), used)
+    return w.text()
+
+
+def control(root, tag, action, params):
+    paths = discover(root).get(tag)
+    if not paths:
+        raise KeyError(tag)
+    done = 0
+    for path in paths:
+        with Region(path) as r:
+            if action == "suspend":
+                r.suspend_all()
+            elif action == "resume":
+                r.resume_all()
+            elif action == "block":
+                r.recent_kernel = -1
+            elif action == "unblock":
+                r.recent_kernel = 2
+            elif action == "reclaim":
+                r.reclaim()
+            elif action == "limit":
+                r.set_memory_limit(int(params.get("dev", 0)), int(params["bytes"]))
+            elif action == "cu":
+                r.set_cu_limit(int(params.get("dev", 0)), int(params["pct"]))
+            elif action == "priority":
+                r.priority = int(params["value"])
+            else:
+                raise ValueError(action)
+            done += 1
+    return done
+
+
+def make_handler(root):
+    class Handler(BaseHTTPRequestHandler):
+        def _send(self, code, body, ctype="text/plain; version=0.0.4"):
+            data = body.encode()
+            self.send_response(code)
+            self.send_header("Content-Type", ctype)
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+
+        def do_GET(self):
+            u = urllib.parse.urlparse(self.path)
+            if u.path == "/metrics":
+                return self._send(200, render_metrics(root))
+            if u.path == "/regions":
+                snaps = {}
+                for tag, paths in discover(root).items():
+                    snaps[tag] = []
+                    for p in paths:
+                        try:
+                            with Region(p) as r:
+                                snaps[tag].append(r.snapshot())
+                        except OSError:
+                            pass
+                return self._send(200, json.dumps(snaps), "application/json")
+            if u.path == "/healthz":
+                return self._send(200, "ok\n")
+            return self._send(404, "not found\n")
+
+        def do_POST(self):
+            u = urllib.parse.urlparse(self.path)
+            parts = u.path.strip("/").split("/")
+            if len(parts) != 3 or parts[0] != "regions":
+                return self._send(404, "not found\n")
+            params = dict(urllib.parse.parse_qsl(u.query))
+            try:
+                n = control(root, parts[1], parts[2], params)
+            except KeyError:
+                return self._send(404, "unknown container\n")
+            except (ValueError, TypeError) as e:
+                return self._send(400, f"bad request: {e}\n")
+            return self._send(200, json.dumps({"regions": n}), "application/json")
+
+        def log_message(self, fmt, *args):
+            log.debug(fmt, *args)
+
+    return Handler
+
+
+def serve(root, host="0.0.0.0", port=9394):
+    srv = ThreadingHTTPServer((host, port), make_handler(root))
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    return srv
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--root", default="/usr/local/vgpu/shared")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=9394)
+    a = ap.parse_args(argv)
+    srv = ThreadingHTTPServer((a.host, a.port), make_handler(a.root))
+    srv.serve_forever()
+
+
+if __name__ == "__main__":
+    main()

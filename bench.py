@@ -44,6 +44,7 @@ def parse(argv=None):
     ap.add_argument("--cu-limit", type=int, default=0, help="CU share %% of the vGPU (0 = quota only)")
     ap.add_argument("--cu-mode", default="spatial", choices=["spatial", "temporal", "both", "off"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-fuse", action="store_true", help="eager PyTorch epilogues (no fused HIP BN+ReLU)")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     # worker-only
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
@@ -79,7 +80,7 @@ def worker(args):
 
     case = get_case(args.case)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    runner = Runner(case, device, dtype=dtype)
+    runner = Runner(case, device, dtype=dtype, fuse=not args.no_fuse)
     for _ in range(args.warmup):
         runner.step()
     torch.cuda.synchronize(device)
@@ -123,7 +124,7 @@ def run_mode(args, mode, port):
     os.close(fd)
     cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--mode", mode, "--result-file", result,
            "--port", str(port), "--case", args.case, "--steps", str(args.steps), "--warmup", str(args.warmup),
-           "--dtype", args.dtype]
+           "--dtype", args.dtype] + (["--no-fuse"] if args.no_fuse else [])
     contract = {}
     if mode == "vgpu":
         quota = int(MI355X_HBM_BYTES * args.memory_scaling / args.split)
@@ -186,6 +187,7 @@ def main(argv=None):
             "global_batch": case.batch * world, "per_gpu_batch": case.batch,
             "input_shape": list(case.input_shape), "seq_len": None,
             "parallelism": f"dp{world} (one independent vGPU replica per GPU)",
+            "fused_epilogues": not args.no_fuse,
             "vgpu": {"split": args.split, "quota_bytes": int(MI355X_HBM_BYTES * args.memory_scaling / args.split),
                      "cu_limit_pct": args.cu_limit, "cu_mode": args.cu_mode,
                      "memory_scaling": args.memory_scaling},

@@ -113,6 +113,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--worker", action="store_true")
+    ap.add_argument("--in-process", action="store_true",
+                    help="run every case in this process (inside a pod whose shim is already preloaded)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--md-out", default=None)
@@ -121,6 +123,9 @@ def main():
     cases = [c.name for c in CASES] if a.cases == "all" else a.cases.split(",")
     if a.worker:
         return worker(cases, a.steps, a.warmup, a.out)
+    if a.in_process:
+        out = a.json_out or os.path.join(tempfile.gettempdir(), "aibench.json")
+        return worker(cases, a.steps, a.warmup, out)
     modes = a.modes.split(",")
     results = {m: run_mode(m, cases, a.steps, a.warmup) for m in modes}
     md = table(results, modes)

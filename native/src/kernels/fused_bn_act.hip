@@ -1,0 +1,158 @@
+// Fused inference epilogues for the in-pod benchmark workloads (gfx950, bf16, NHWC).
+//
+//   y   = act(x * scale[c] + shift[c])                      (BN(eval) + ReLU)
+//   s   = x + r ;  y = act(s * scale[c] + shift[c])          (residual add + next BN + ReLU)
+//
+// In a pre-activation ResNet every block boundary is "add the shortcut, then the next
+// block's BN + ReLU", and every conv inside a block is followed by BN + ReLU. Eager
+// PyTorch runs each of those as 3-5 separate passes over the activation (BN transform,
+// clamp, add, the bf16<->f32 copies and the inv-std kernel: ~37 % of the ResNet-V2-50
+// inference step on MI355X, profiles/r1a_resnet50_inf_vgpu.md). These kernels do one
+// pass: 16-byte (8 x bf16) loads/stores per lane, fp32 math, per-channel scale/shift
+// from the L1/L2-resident parameter vectors, round-to-nearest-even back to bf16
+// (v_cvt_pk_bf16_f32). Memory bound by design: bytes moved = inputs + outputs once.
+//
+// C ABI (ctypes): pointers are device pointers, `stream` a hipStream_t.
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf_lo(unsigned v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bf_hi(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
+
+__device__ __forceinline__ unsigned pack_bf16(float lo, float hi) {
+  __hip_bfloat16 a = __float2bfloat16(lo);
+  __hip_bfloat16 b = __float2bfloat16(hi);
+  return (unsigned)__bfloat16_as_ushort(a) | ((unsigned)__bfloat16_as_ushort(b) << 16);
+}
+
+template <bool kAdd, bool kWriteSum, int kAct>
+__device__ __forceinline__ void apply8(const u32x4& xv, const u32x4& rv, const float* __restrict__ scale,
+                                       const float* __restrict__ shift, unsigned c0, u32x4* yv, u32x4* sv) {
+  const float4 s0 = *reinterpret_cast<const float4*>(scale + c0);
+  const float4 s1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
+  const float4 t0 = *reinterpret_cast<const float4*>(shift + c0);
+  const float4 t1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
+  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float sh[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    v[2 * k] = bf_lo(xv[k]);
+    v[2 * k + 1] = bf_hi(xv[k]);
+  }
+  if constexpr (kAdd) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      v[2 * k] += bf_lo(rv[k]);
+      v[2 * k + 1] += bf_hi(rv[k]);
+    }
+    if constexpr (kWriteSum) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) (*sv)[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    float o = fmaf(v[j], sc[j], sh[j]);
+    if constexpr (kAct == 1) o = fmaxf(o, 0.0f);
+    if constexpr (kAct == 2) o = fminf(fmaxf(o, 0.0f), 6.0f);
+    v[j] = o;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) (*yv)[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
+}
+
+// Each lane handles two 16-byte vectors per iteration (ILP: both loads in flight before
+// the math). nvec < 2^31 is checked on the host, so indexing stays 32-bit.
+template <bool kAdd, bool kWriteSum, int kAct>
+__global__ void __launch_bounds__(256) bn_act_kernel(const u32x4* __restrict__ x, const u32x4* __restrict__ r,
+                                                     const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, u32x4* __restrict__ y,
+                                                     u32x4* __restrict__ sum, unsigned nvec, unsigned cvec) {
+  const unsigned stride = gridDim.x * 256u;
+  unsigned i = blockIdx.x * 256u + threadIdx.x;
+  for (; i + stride < nvec; i += 2 * stride) {
+    const unsigned j = i + stride;
+    u32x4 xa = __builtin_nontemporal_load(&x[i]);
+    u32x4 xb = __builtin_nontemporal_load(&x[j]);
+    u32x4 ra{}, rb{};
+    if constexpr (kAdd) {
+      ra = __builtin_nontemporal_load(&r[i]);
+      rb = __builtin_nontemporal_load(&r[j]);
+    }
+    u32x4 ya, yb, sa, sb;
+    apply8<kAdd, kWriteSum, kAct>(xa, ra, scale, shift, (i % cvec) * 8u, &ya, &sa);
+    apply8<kAdd, kWriteSum, kAct>(xb, rb, scale, shift, (j % cvec) * 8u, &yb, &sb);
+    y[i] = ya;
+    y[j] = yb;
+    if constexpr (kWriteSum) {
+      sum[i] = sa;
+      sum[j] = sb;
+    }
+  }
+  if (i < nvec) {
+    u32x4 xa = __builtin_nontemporal_load(&x[i]);
+    u32x4 ra{};
+    if constexpr (kAdd) ra = __builtin_nontemporal_load(&r[i]);
+    u32x4 ya, sa;
+    apply8<kAdd, kWriteSum, kAct>(xa, ra, scale, shift, (i % cvec) * 8u, &ya, &sa);
+    y[i] = ya;
+    if constexpr (kWriteSum) sum[i] = sa;
+  }
+}
+
+template <bool kAdd, bool kWriteSum, int kAct>
+void launch(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum, unsigned nvec,
+            unsigned cvec, hipStream_t stream) {
+  // Enough waves to cover HBM latency on 256 CUs (>= 8 blocks/CU), capped so every
+  // lane does at least a couple of iterations on large tensors.
+  unsigned blocks = (nvec + 511u) / 512u;
+  if (blocks > 256u * 16u) blocks = 256u * 16u;
+  if (blocks < 1u) blocks = 1u;
+  hipLaunchKernelGGL((bn_act_kernel<kAdd, kWriteSum, kAct>), dim3(blocks), dim3(256), 0, stream,
+                     static_cast<const u32x4*>(x), static_cast<const u32x4*>(r), scale, shift,
+                     static_cast<u32x4*>(y), static_cast<u32x4*>(sum), nvec, cvec);
+}
+
+template <int kAct>
+int dispatch(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum,
+             unsigned nvec, unsigned cvec, hipStream_t s) {
+  if (!r) launch<false, false, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
+  else if (!sum) launch<true, false, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
+  else launch<true, true, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace
+
+extern "C" {
+
+// x, r, y, sum: bf16 NHWC tensors of `numel` elements with `channels` innermost.
+// r/sum may be null (no residual / do not materialise the sum). act: 0 none, 1 relu,
+// 2 relu6. Requirements (checked): channels % 8 == 0, 16-byte aligned pointers,
+// numel / 8 < 2^31. Returns 0 on success, -1 on bad arguments, -2 on launch failure.
+int vgpu_bn_act_bf16(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum,
+                     int64_t numel, int channels, int act, void* stream) {
+  if (!x || !y || !scale || !shift || channels <= 0 || channels % 8 || numel <= 0 || numel % channels) return -1;
+  if (numel / 8 >= (int64_t)1 << 31) return -1;
+  auto misaligned = [](const void* p) { return p && (reinterpret_cast<uintptr_t>(p) & 15u); };
+  if (misaligned(x) || misaligned(r) || misaligned(y) || misaligned(sum) || misaligned(scale) || misaligned(shift))
+    return -1;
+  if (sum && !r) return -1;
+  const unsigned nvec = (unsigned)(numel / 8), cvec = (unsigned)(channels / 8);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (act) {
+    case 0: return dispatch<0>(x, r, scale, shift, y, sum, nvec, cvec, s);
+    case 1: return dispatch<1>(x, r, scale, shift, y, sum, nvec, cvec, s);
+    case 2: return dispatch<2>(x, r, scale, shift, y, sum, nvec, cvec, s);
+    default: return -1;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,45 @@
+"""Deployment artefacts are consistent with the plugin's flag surface."""
+import glob
+import os
+import re
+
+import yaml
+
+from amdvgpu.plugin.config import build_parser, parse_config
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _known_flags():
+    flags = set()
+    for a in build_parser()._actions:
+        flags.update(s for s in a.option_strings if s.startswith("--"))
+    return flags
+
+
+def test_static_manifests_parse_and_args_are_valid():
+    files = glob.glob(os.path.join(REPO, "deployments", "static", "*.yml"))
+    assert len(files) >= 3
+    for f in files:
+        docs = [d for d in yaml.safe_load_all(open(f)) if d]
+        ds = [d for d in docs if d["kind"] == "DaemonSet"]
+        assert ds, f
+        for c in ds[0]["spec"]["template"]["spec"]["containers"]:
+            if "args" in c:
+                parse_config(c["args"], environ={})
+
+
+def test_helm_template_flags_exist():
+    tpl = open(os.path.join(REPO, "deployments", "helm", "amd-vgpu-device-plugin", "templates",
+                            "daemonset.yml")).read()
+    used = set(re.findall(r'"(--[a-z-]+)=', tpl))
+    assert used and used <= _known_flags(), used - _known_flags()
+    values = yaml.safe_load(open(os.path.join(REPO, "deployments", "helm", "amd-vgpu-device-plugin",
+                                              "values.yaml")))
+    for key in re.findall(r"\.Values\.([A-Za-z]+)", tpl):
+        assert key in values, key
+
+
+def test_preload_file_points_at_container_shim():
+    from amdvgpu.plugin.contract import CONTAINER_SHIM
+    assert open(os.path.join(REPO, "vgpu", "ld.so.preload")).read().strip() == CONTAINER_SHIM

@@ -102,7 +102,7 @@ a = torch.ones(1536 << 20, dtype=torch.uint8, device="cuda")     # resident
 b = torch.full((1024 << 20,), 3, dtype=torch.uint8, device="cuda")  # crosses the share -> host
 c = torch.full((1024 << 20,), 5, dtype=torch.uint8, device="cuda")  # host
 torch.cuda.synchronize()
-s = int(a[:1 << 20].sum()) + int(b.sum()) + int(c.sum())
+ok_ab = bool((a[:1 << 20] == 1).all()) and bool((b == 3).all()) and bool((c == 5).all())
 r = Region(os.environ["VGPU_SHARED_CACHE"]).device(0)
 # bandwidth of a kernel reading spilled memory
 dst = torch.empty_like(c)
@@ -116,12 +116,12 @@ try:
     over = False
 except torch.OutOfMemoryError:
     over = True
-emit(total=total, s=s, spilled=r["spilled"], used=r["used"], hbm=r["hbm_limit"], bw=bw, over=over,
+emit(total=total, ok_ab=ok_ab, spilled=r["spilled"], used=r["used"], hbm=r["hbm_limit"], bw=bw, over=over,
      ok=bool((dst == 5).all()))
 """, c)
     r = res[0]
     assert r["total"] == 8 * GiB
-    assert r["s"] == (1 << 20) + 3 * (1024 << 20) + 5 * (1024 << 20)
+    assert r["ok_ab"]
     assert r["spilled"] >= 2 * GiB - 64 * MiB
     assert r["hbm"] == 2 * GiB
     assert r["ok"] and r["over"]

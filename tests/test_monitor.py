@@ -1,0 +1,61 @@
+"""Node monitor over container regions (no GPU: regions filled through the same
+admission path the shim uses)."""
+import json
+import os
+import urllib.request
+
+from amdvgpu.plugin.monitor import control, discover, render_metrics, serve
+from amdvgpu.shim.region import Region
+
+
+def make_region(root, tag, limit=8 << 30, used=3 << 30):
+    d = os.path.join(root, tag)
+    os.makedirs(d, exist_ok=True)
+    p = os.path.join(d, "abc.cache")
+    r = Region(p, create=True)
+    r.set_memory_limit(0, limit)
+    slot = r.register(os.getpid())
+    assert r.charge(slot, 0, used, 0) == 0
+    return r, slot
+
+
+def test_metrics_and_control(tmp_path):
+    root = str(tmp_path)
+    r, slot = make_region(root, "pod1_main")
+    assert list(discover(root)) == ["pod1_main"]
+    text = render_metrics(root)
+    assert 'vgpu_memory_limit_bytes{container="pod1_main",region="abc.cache",device="0"' in text
+    assert f"vgpu_memory_used_bytes" in text and str(3 << 30) in text
+    assert "vgpu_process_oom_events_total" in text
+    # quota enforcement through the region: a charge past the limit is refused
+    assert r.charge(slot, 0, 6 << 30, 0) != 0
+    assert control(root, "pod1_main", "suspend", {}) == 1
+    assert r.suspended
+    control(root, "pod1_main", "resume", {})
+    assert not r.suspended
+    control(root, "pod1_main", "limit", {"dev": "0", "bytes": str(16 << 30)})
+    assert r.device(0)["mem_limit"] == 16 << 30
+    control(root, "pod1_main", "block", {})
+    assert r.recent_kernel < 0
+    control(root, "pod1_main", "unblock", {})
+    control(root, "pod1_main", "priority", {"value": "3"})
+    assert r.priority == 3
+    r.close()
+
+
+def test_http_endpoints(tmp_path):
+    root = str(tmp_path)
+    r, slot = make_region(root, "pod2_c")
+    srv = serve(root, "127.0.0.1", 0)
+    port = srv.server_address[1]
+    try:
+        body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics").read().decode()
+        assert "vgpu_container_processes" in body
+        snap = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{port}/regions").read())
+        assert snap["pod2_c"][0]["devices"][0]["used"] == 3 << 30
+        req = urllib.request.Request(f"http://127.0.0.1:{port}/regions/pod2_c/suspend", method="POST", data=b"")
+        assert json.loads(urllib.request.urlopen(req).read())["regions"] == 1
+        assert r.suspended
+    finally:
+        srv.shutdown()
+        r.close()
