@@ -315,7 +315,7 @@ class Runner:
         if not self.case.train:
             with torch.inference_mode():
                 return self.model(self.x)
-        with torch.autocast("cuda", dtype=self.dtype):
+        with torch.autocast(self.device.type, dtype=self.dtype, enabled=self.dtype != torch.float32):
             out = self.model(self.x)
             loss = F.cross_entropy(out.float(), self.y)
         self.opt.zero_grad(set_to_none=True)

@@ -51,6 +51,8 @@ def parse(argv=None):
     ap.add_argument("--mode", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--result-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--port", type=int, default=0, help=argparse.SUPPRESS)
+    # CPU rehearsal of the multi-rank orchestration (gloo, tiny batch); not a measurement
+    ap.add_argument("--cpu-rehearsal", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -66,35 +68,47 @@ def worker(args):
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    cpu = args.cpu_rehearsal
+    if cpu:
+        device = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
     if world > 1:
-        os.environ["MASTER_PORT"] = str(args.port)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        init = f"tcp://{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{args.port}"
+        if cpu:
+            dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", init_method=init, rank=rank, world_size=world, device_id=device)
 
-    free0, total = torch.cuda.mem_get_info(device)
-    if args.mode == "vgpu":
+    sync = (lambda: None) if cpu else (lambda: torch.cuda.synchronize(device))
+    free0, total = torch.cuda.mem_get_info(device) if not cpu else (0, 0)
+    if args.mode == "vgpu" and not cpu:
         quota = int(os.environ["VGPU_DEVICE_MEMORY_LIMIT"].rstrip("m")) << 20
         if total != min(quota, MI355X_HBM_BYTES) and not os.environ.get("VGPU_OVERSUBSCRIBE"):
             raise SystemExit(f"vGPU shim not in effect: mem_get_info total {total} != quota {quota}")
 
     case = get_case(args.case)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    runner = Runner(case, device, dtype=dtype, fuse=not args.no_fuse)
+    if cpu:
+        runner = Runner(case, device, dtype=torch.float32, batch=2, channels_last=False, fuse=False)
+        runner.x = runner.x[..., :64, :64].contiguous() if runner.x.dim() == 4 else runner.x[:, :16].contiguous()
+    else:
+        runner = Runner(case, device, dtype=dtype, fuse=not args.no_fuse)
     for _ in range(args.warmup):
         runner.step()
-    torch.cuda.synchronize(device)
+    sync()
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
-        torch.cuda.synchronize(device)
+            dist.barrier(device_ids=[local]) if not cpu else dist.barrier()
+        sync()
 
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         runner.step()
-    torch.cuda.synchronize(device)
+    sync()
     barrier()
     dt = time.perf_counter() - t0
     ms = torch.tensor([dt * 1000.0 / args.steps], dtype=torch.float64, device=device)
@@ -102,13 +116,14 @@ def worker(args):
         dist.all_reduce(ms, op=dist.ReduceOp.MAX)
     res = {
         "mode": args.mode, "ms_per_step": ms.item(), "items_per_step": runner.items_per_step,
-        "mem_total": total, "peak_allocated": torch.cuda.max_memory_allocated(device), "world": world,
+        "mem_total": total, "world": world,
+        "peak_allocated": torch.cuda.max_memory_allocated(device) if not cpu else 0,
     }
     if rank == 0 and args.result_file:
         with open(args.result_file, "w") as f:
             json.dump(res, f)
     if world > 1:
-        dist.barrier(device_ids=[local])
+        barrier()
         dist.destroy_process_group()
     return 0
 
@@ -124,7 +139,8 @@ def run_mode(args, mode, port):
     os.close(fd)
     cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--mode", mode, "--result-file", result,
            "--port", str(port), "--case", args.case, "--steps", str(args.steps), "--warmup", str(args.warmup),
-           "--dtype", args.dtype] + (["--no-fuse"] if args.no_fuse else [])
+           "--dtype", args.dtype] + (["--no-fuse"] if args.no_fuse else []) + \
+        (["--cpu-rehearsal"] if args.cpu_rehearsal else [])
     contract = {}
     if mode == "vgpu":
         quota = int(MI355X_HBM_BYTES * args.memory_scaling / args.split)
@@ -134,6 +150,10 @@ def run_mode(args, mode, port):
         env = apply_contract(contract)
     else:
         env = dict(os.environ)
+    # The worker hosts its own rendezvous store on `port` (rank 0); under
+    # torch.distributed.run the agent's store flag would make every worker a client of a
+    # store that does not exist on that port.
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
     try:
         rc = subprocess.call(cmd, env=env)
         if rc != 0:

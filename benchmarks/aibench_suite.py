@@ -111,7 +111,9 @@ def main():
     ap.add_argument("--cases", default="all")
     ap.add_argument("--modes", default="native,vgpu,vgpu-cu50")
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--repeats", type=int, default=1,
+                    help="run the modes this many times in alternating order; keep each mode's best")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--in-process", action="store_true",
                     help="run every case in this process (inside a pod whose shim is already preloaded)")
@@ -127,7 +129,17 @@ def main():
         out = a.json_out or os.path.join(tempfile.gettempdir(), "aibench.json")
         return worker(cases, a.steps, a.warmup, out)
     modes = a.modes.split(",")
-    results = {m: run_mode(m, cases, a.steps, a.warmup) for m in modes}
+    results = {}
+    for rep in range(a.repeats):
+        order = modes if rep % 2 == 0 else modes[::-1]  # ABBA: cancels drift between runs
+        for m in order:
+            r = run_mode(m, cases, a.steps, a.warmup)
+            if m not in results:
+                results[m] = r
+            else:
+                for k, v in r.items():
+                    if v["ms_per_batch"] < results[m][k]["ms_per_batch"]:
+                        results[m][k] = v
     md = table(results, modes)
     print(md)
     if a.json_out:

@@ -9,6 +9,10 @@ Policies:
             (what the plugin hands out with --device-split-count=N)
 * shared    quota HBM/N, no CU limit: tenants time-share all 256 CUs (hardware
             scheduling between queues)
+* spatial-interleave  same slices in the plain interleaved mask layout (every tenant
+            on every SE) instead of the default SE-major layout
+* vdm       the reference's "virtual device memory" setting: quota 1.8 x HBM/N with
+            oversubscription (HBM share HBM/N, rest spills), CU limit 100*1/N spatial
 
     python benchmarks/vgpu_scaling.py [--case resnet50-inf] [--tenants 1,2,4,8] [--policy spatial,shared]
 """
@@ -53,9 +57,14 @@ def run_point(case, n, policy, steps, warmup):
     procs, contracts, outs = [], [], []
     for i in range(n):
         kw = dict(mem_limit=HBM // n)
-        if policy == "spatial" and n > 1:
+        if policy == "vdm":
+            kw = dict(mem_limit=int(HBM * 1.8 / n), oversubscribe=True,
+                      extra={"VGPU_DEVICE_HBM_LIMIT_0": f"{HBM // n >> 20}m"})
+        if policy in ("spatial", "spatial-interleave", "vdm") and n > 1:
             b, e = cu_partition_range(256, 8, n, i)
             kw.update(cu_limit=100 * (e - b) // 256, cu_range=(b, e))
+        if policy == "spatial-interleave":
+            kw["extra"] = dict(kw.get("extra") or {}, VGPU_CU_LAYOUT="interleave")
         c = vgpu_env(**kw)
         out = os.path.join(tmp, f"t{i}.json")
         cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--case", case, "--steps", str(steps),

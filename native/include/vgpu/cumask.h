@@ -4,8 +4,17 @@
 // MI355X the hardware offers per-queue CU masks (hsa_amd_queue_cu_set_mask,
 // hsa_ext_amd.h:1359), which partition the chip spatially with zero per-launch cost.
 //
-// Logical mask bit i is mapped by KFD to XCC (i % num_xcc), then round-robin over
-// that XCC's shader engines (measured on box, profiles/cu_mask_calibration.md).
+// Physical mask bit b is mapped by KFD to XCC (b % num_xcc); the XCC-local index
+// l = b / num_xcc then goes round-robin over that XCC's shader engines: SE = l % num_se,
+// and it is the (l / num_se)-th active CU of that SE (measured on box with a
+// HW_ID-recording kernel, profiles/cu_mask_calibration.md).
+//
+// The *logical* CU index used by ranges below is SE-major inside each XCC: logical L
+// -> XCC L % num_xcc, rank r = L / num_xcc, SE = r / cus_per_se, k = r % cus_per_se,
+// physical bit = (k * num_se + SE) * num_xcc + XCC. A contiguous logical range of
+// 256/N CUs is then "the same whole shader engine(s) on every XCC" for N <= 4 tenants
+// (half an SE for N = 8), so co-resident vGPUs do not share an SE's workgroup
+// dispatcher. num_se = 1 reproduces the plain interleaved layout.
 // Workgroups of a dispatch are dealt round-robin over all 8 XCCs regardless of the
 // mask, so a mask must give every XCC the same number of CUs or the slowest XCC
 // bounds the kernel - and an XCC with no CU falls back to "all CUs". Masks built
@@ -33,11 +42,14 @@ struct CuMask {
 int cu_share_count(int cu_count, int num_xcc, int pct);
 
 // Mask for logical range [begin, end). begin/end are snapped to multiples of num_xcc.
-CuMask cu_mask_range(int cu_count, int num_xcc, int begin, int end);
+CuMask cu_mask_range(int cu_count, int num_xcc, int begin, int end, int num_se = 1);
 
 // Mask for a vGPU: explicit range if given (begin >= 0), else the first
 // cu_share_count() CUs.
-CuMask cu_mask_for(int cu_count, int num_xcc, int pct, int range_begin, int range_end);
+CuMask cu_mask_for(int cu_count, int num_xcc, int pct, int range_begin, int range_end, int num_se = 1);
+
+// Physical mask bit of logical CU index L (layout described above).
+int cu_logical_to_bit(int cu_count, int num_xcc, int num_se, int L);
 
 // The logical range of vGPU `slot` among `split` equal tenants of one GPU; the
 // remainder (in units of num_xcc) goes to the lowest slots. Used by the plugin to

@@ -20,20 +20,31 @@ int cu_share_count(int cu_count, int num_xcc, int pct) {
   return std::min(n, cu_count);
 }
 
-CuMask cu_mask_range(int cu_count, int num_xcc, int begin, int end) {
+int cu_logical_to_bit(int cu_count, int num_xcc, int num_se, int L) {
+  if (num_xcc <= 0) num_xcc = 1;
+  const int per_xcc = cu_count / num_xcc;
+  if (num_se <= 1 || per_xcc % num_se) return L;  // no (or irregular) SE structure: identity
+  const int per_se = per_xcc / num_se;
+  const int xcc = L % num_xcc, r = L / num_xcc;
+  const int se = r / per_se, k = r % per_se;
+  return (k * num_se + se) * num_xcc + xcc;
+}
+
+CuMask cu_mask_range(int cu_count, int num_xcc, int begin, int end, int num_se) {
   CuMask m;
   if (num_xcc <= 0) num_xcc = 1;
   cu_count = std::min(cu_count, kMaxCUs);
   m.nbits = cu_count;
   begin = std::max(0, begin / num_xcc * num_xcc);
   end = std::min(cu_count, (end + num_xcc - 1) / num_xcc * num_xcc);
-  for (int i = begin; i < end; i++) m.set(i);
+  for (int i = begin; i < end; i++) m.set(cu_logical_to_bit(cu_count, num_xcc, num_se, i));
   return m;
 }
 
-CuMask cu_mask_for(int cu_count, int num_xcc, int pct, int range_begin, int range_end) {
-  if (range_begin >= 0 && range_end > range_begin) return cu_mask_range(cu_count, num_xcc, range_begin, range_end);
-  return cu_mask_range(cu_count, num_xcc, 0, cu_share_count(cu_count, num_xcc, pct));
+CuMask cu_mask_for(int cu_count, int num_xcc, int pct, int range_begin, int range_end, int num_se) {
+  if (range_begin >= 0 && range_end > range_begin)
+    return cu_mask_range(cu_count, num_xcc, range_begin, range_end, num_se);
+  return cu_mask_range(cu_count, num_xcc, 0, cu_share_count(cu_count, num_xcc, pct), num_se);
 }
 
 void cu_partition_range(int cu_count, int num_xcc, int split, int slot, int* begin, int* end) {

@@ -3,6 +3,7 @@
 
 #include <pthread.h>
 #include <signal.h>
+#include <strings.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -84,6 +85,12 @@ hsa_status_t agent_cb(hsa_agent_t agent, void* data) {
   v = 1;
   if (real_hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_NUM_XCC, &v) == HSA_STATUS_SUCCESS && v)
     a.num_xcc = (int)v;
+  v = 0;
+  if (real_hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_NUM_SHADER_ENGINES, &v) == HSA_STATUS_SUCCESS &&
+      v) {
+    // Reported for the whole agent on multi-XCC parts; normalise to per XCC.
+    a.num_se = (v >= (uint32_t)a.num_xcc && v % a.num_xcc == 0) ? (int)(v / a.num_xcc) : (int)v;
+  }
   v = 0;
   if (real_hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DRIVER_UID, &v) == HSA_STATUS_SUCCESS)
     a.gpu_id = v;
@@ -258,8 +265,10 @@ void shim_init_after_hsa() {
       if (!d.mem_limit && per_agent[i].mem_limit) d.mem_limit = per_agent[i].mem_limit;
       if (!d.hbm_limit && per_agent[i].hbm_limit) d.hbm_limit = per_agent[i].hbm_limit;
       if (!d.cu_limit_pct && per_agent[i].cu_limit_pct) d.cu_limit_pct = per_agent[i].cu_limit_pct;
+      const char* layout = getenv("VGPU_CU_LAYOUT");  // "se" (default) | "interleave"
+      int se = (layout && !strcasecmp(layout, "interleave")) ? 1 : a.num_se;
       CuMask m = cu_mask_for(a.cu_count, a.num_xcc, d.cu_limit_pct, per_agent[i].cu_range_begin,
-                             per_agent[i].cu_range_end);
+                             per_agent[i].cu_range_end, se);
       memcpy(d.cu_mask, m.words, sizeof(d.cu_mask));
       d.cu_mask_bits = m.nbits;
       LimiterSpec spec{a.cu_count, a.max_waves_per_cu * 64};

@@ -29,6 +29,7 @@ struct AgentInfo {
   uint32_t gpu_id = 0;               // KFD gpu_id
   int cu_count = 0;
   int num_xcc = 1;
+  int num_se = 1;                    // shader engines per XCC (mask layout)
   int max_waves_per_cu = 32;
   uint64_t phys_total = 0;
   bool mask_active = false;          // spatial mask applied to its queues

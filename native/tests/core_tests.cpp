@@ -353,6 +353,30 @@ static void test_cumask() {
   CHECK_EQ(bad.count(), 64);
 }
 
+static void test_cumask_se_layout() {
+  // Bijection over the chip.
+  std::vector<int> seen(256, 0);
+  for (int L = 0; L < 256; L++) seen[cu_logical_to_bit(256, 8, 4, L)]++;
+  for (int b = 0; b < 256; b++) CHECK_EQ(seen[b], 1);
+  // N = 4 tenants: each gets one whole SE on every XCC, disjoint between tenants.
+  for (int slot = 0; slot < 4; slot++) {
+    CuMask m = cu_mask_range(256, 8, slot * 64, slot * 64 + 64, 4);
+    CHECK_EQ(m.count(), 64);
+    CHECK(cu_mask_balanced(m, 8));
+    for (int b = 0; b < 256; b++)
+      if (m.test(b)) CHECK_EQ((b / 8) % 4, slot);  // KFD: SE = local index % num_se
+  }
+  // N = 8: half an SE each; N = 2: two SEs each.
+  CuMask h = cu_mask_range(256, 8, 32, 64, 4);
+  for (int b = 0; b < 256; b++)
+    if (h.test(b)) CHECK_EQ((b / 8) % 4, 0);
+  CuMask two = cu_mask_range(256, 8, 128, 256, 4);
+  for (int b = 0; b < 256; b++)
+    if (two.test(b)) CHECK((b / 8) % 4 >= 2);
+  // num_se = 1 is the identity (interleaved layout).
+  for (int L = 0; L < 256; L++) CHECK_EQ(cu_logical_to_bit(256, 8, 1, L), L);
+}
+
 static void test_devmap() {
   DeviceMap m;
   CHECK(parse_device_map("0:GPU-aaaa 1:GPU-bbbb", &m));
@@ -498,6 +522,7 @@ int main(int argc, char** argv) {
       {"region_version_guard", test_region_version_guard},
       {"proc_alive", test_proc_alive},
       {"cumask", test_cumask},
+      {"cumask_se_layout", test_cumask_se_layout},
       {"devmap", test_devmap},
       {"ratelimit", test_ratelimit},
       {"kfd", test_kfd},

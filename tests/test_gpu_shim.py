@@ -235,3 +235,22 @@ torch.cuda.synchronize()
 emit(v=float(x[0]))
 """, c)
     assert res[0]["v"] == 13.0  # 3 eager + 10 replays (capture itself does not execute)
+
+
+def test_se_exclusive_layout_for_four_tenants(tmp_region):
+    """SE-major logical CU layout: each of 4 co-resident vGPUs owns one whole shader
+    engine on every XCD (no shared SE dispatcher between tenants)."""
+    from amdvgpu.shim.region import cu_partition_range
+    code = """
+from amdvgpu.ops import cu_census
+emit(locs=sorted(cu_census(nblocks=8192, spin_us=300)))
+"""
+    for slot in (0, 3):
+        b, e = cu_partition_range(256, 8, 4, slot)
+        c = vgpu_env(cu_limit=25, cu_range=(b, e), shared_cache=tmp_region + f".{slot}")
+        res, _ = run_child(code, c)
+        os.unlink(tmp_region + f".{slot}")
+        locs = [tuple(x) for x in res[0]["locs"]]
+        assert len(locs) == 64
+        assert {l[1] for l in locs} == {slot}, sorted({(l[0], l[1]) for l in locs})
+        assert len({l[0] for l in locs}) == 8

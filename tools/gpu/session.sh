@@ -17,7 +17,7 @@ if has build; then
 fi
 if has tests; then
   step tests
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q -rs -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
   rc=$?; tail -15 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 fi
 if has smoke; then
@@ -32,15 +32,26 @@ if has bench; then
 fi
 if has suite; then
   step suite
-  timeout -k 10 900 python benchmarks/aibench_suite.py --steps 20 --warmup 5 --modes ${SUITE_MODES:-native,vgpu,vgpu-cu50} \
+  timeout -k 10 1000 python benchmarks/aibench_suite.py --steps 20 --warmup 10 --repeats ${SUITE_REPEATS:-2} --modes ${SUITE_MODES:-native,vgpu,vgpu-cu50} \
     --json-out $OUT/suite.json --md-out $OUT/suite.md > $OUT/suite.log 2>&1
   rc=$?; tail -16 $OUT/suite.log; [ $rc -eq 0 ] || exit $rc
 fi
 if has scaling; then
   step scaling
-  timeout -k 10 900 python benchmarks/vgpu_scaling.py --json-out $OUT/scaling.json --md-out $OUT/scaling.md \
+  timeout -k 10 900 python benchmarks/vgpu_scaling.py --policy ${SCALING_POLICY:-spatial,shared} --json-out $OUT/scaling.json --md-out $OUT/scaling.md \
     > $OUT/scaling.log 2>&1
   rc=$?; tail -14 $OUT/scaling.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has hooks; then
+  step hooks
+  timeout -k 10 600 python benchmarks/hook_overhead.py --json-out $OUT/hooks.json --md-out $OUT/hooks.md \
+    > $OUT/hooks.log 2>&1
+  rc=$?; tail -8 $OUT/hooks.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has oversub; then
+  step oversub
+  timeout -k 10 600 python benchmarks/oversubscribe.py --json-out $OUT/oversub.json > $OUT/oversub.log 2>&1
+  rc=$?; tail -4 $OUT/oversub.log; [ $rc -eq 0 ] || exit $rc
 fi
 if has prof; then
   step prof
