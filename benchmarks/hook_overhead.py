@@ -94,6 +94,7 @@ def main():
         return worker(a.iters, a.out)
     from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
     modes = {"native": None, "vgpu": dict(mem_limit=64 << 30),
+             "vgpu-stats": dict(mem_limit=64 << 30, extra={"VGPU_STATS": "1"}),
              "vgpu-temporal": dict(mem_limit=64 << 30, cu_limit=99, cu_mode="temporal")}
     best = {}
     for rep in range(a.repeats):

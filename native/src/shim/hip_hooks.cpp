@@ -54,6 +54,7 @@ int temporal_any() {
 }
 
 inline void launch_gate(int64_t workgroups) {
+  VGPU_STAT(kStatLaunch);
   ShimState& s = shim();
   if (__builtin_expect(!s.active, 1)) return;
   gate_suspend();
@@ -143,11 +144,9 @@ hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t globalWorkSizeX, u
                                     void** kernelParams, void** extra, hipEvent_t startEvent, hipEvent_t stopEvent,
                                     uint32_t flags) {
   VGPU_REAL_HIP(hipExtModuleLaunchKernel);
-  if (__builtin_expect(shim().active, 0)) {
-    auto wg = [](uint32_t g, uint32_t l) -> int64_t { return l ? (g + l - 1) / l : g; };
-    launch_gate(wg(globalWorkSizeX, localWorkSizeX) * wg(globalWorkSizeY, localWorkSizeY) *
-                wg(globalWorkSizeZ, localWorkSizeZ));
-  }
+  auto wg = [](uint32_t g, uint32_t l) -> int64_t { return l ? (g + l - 1) / l : g; };
+  launch_gate(wg(globalWorkSizeX, localWorkSizeX) * wg(globalWorkSizeY, localWorkSizeY) *
+              wg(globalWorkSizeZ, localWorkSizeZ));
   return real_hipExtModuleLaunchKernel(f, globalWorkSizeX, globalWorkSizeY, globalWorkSizeZ, localWorkSizeX,
                                        localWorkSizeY, localWorkSizeZ, sharedMemBytes, hStream, kernelParams, extra,
                                        startEvent, stopEvent, flags);
@@ -187,6 +186,7 @@ hipError_t hipGraphInstantiateWithFlags(hipGraphExec_t* pGraphExec, hipGraph_t g
 
 hipError_t hipGraphLaunch(hipGraphExec_t graphExec, hipStream_t stream) {
   VGPU_REAL_HIP(hipGraphLaunch);
+  VGPU_STAT(kStatGraphLaunch);
   ShimState& s = shim();
   if (__builtin_expect(s.active, 0)) {
     gate_suspend();
@@ -218,18 +218,21 @@ hipError_t hipGraphExecDestroy(hipGraphExec_t graphExec) {
 // Copy/set gates (suspend only), mirroring the reference's wait_status_self set.
 hipError_t hipMemcpy(void* dst, const void* src, size_t sizeBytes, hipMemcpyKind kind) {
   VGPU_REAL_HIP(hipMemcpy);
+  VGPU_STAT(kStatCopy);
   gate_suspend();
   return real_hipMemcpy(dst, src, sizeBytes, kind);
 }
 
 hipError_t hipMemcpyAsync(void* dst, const void* src, size_t sizeBytes, hipMemcpyKind kind, hipStream_t stream) {
   VGPU_REAL_HIP(hipMemcpyAsync);
+  VGPU_STAT(kStatCopy);
   gate_suspend();
   return real_hipMemcpyAsync(dst, src, sizeBytes, kind, stream);
 }
 
 hipError_t hipMemcpyWithStream(void* dst, const void* src, size_t sizeBytes, hipMemcpyKind kind, hipStream_t stream) {
   VGPU_REAL_HIP(hipMemcpyWithStream);
+  VGPU_STAT(kStatCopy);
   gate_suspend();
   return real_hipMemcpyWithStream(dst, src, sizeBytes, kind, stream);
 }
@@ -237,24 +240,28 @@ hipError_t hipMemcpyWithStream(void* dst, const void* src, size_t sizeBytes, hip
 hipError_t hipMemcpyPeerAsync(void* dst, int dstDeviceId, const void* src, int srcDevice, size_t sizeBytes,
                               hipStream_t stream) {
   VGPU_REAL_HIP(hipMemcpyPeerAsync);
+  VGPU_STAT(kStatCopy);
   gate_suspend();
   return real_hipMemcpyPeerAsync(dst, dstDeviceId, src, srcDevice, sizeBytes, stream);
 }
 
 hipError_t hipMemset(void* dst, int value, size_t sizeBytes) {
   VGPU_REAL_HIP(hipMemset);
+  VGPU_STAT(kStatSet);
   gate_suspend();
   return real_hipMemset(dst, value, sizeBytes);
 }
 
 hipError_t hipMemsetAsync(void* dst, int value, size_t sizeBytes, hipStream_t stream) {
   VGPU_REAL_HIP(hipMemsetAsync);
+  VGPU_STAT(kStatSet);
   gate_suspend();
   return real_hipMemsetAsync(dst, value, sizeBytes, stream);
 }
 
 hipError_t hipMemsetD32Async(hipDeviceptr_t dst, int value, size_t count, hipStream_t stream) {
   VGPU_REAL_HIP(hipMemsetD32Async);
+  VGPU_STAT(kStatSet);
   gate_suspend();
   return real_hipMemsetD32Async(dst, value, count, stream);
 }

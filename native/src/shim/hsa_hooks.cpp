@@ -120,6 +120,7 @@ hsa_status_t hsa_init() {
 
 hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr) {
   VGPU_REAL_HSA(hsa_amd_memory_pool_allocate);
+  VGPU_STAT(kStatAlloc);
   if (!real_hsa_amd_memory_pool_allocate) return HSA_STATUS_ERROR;
   if (!ready() || size == 0) return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
   int dev = pool_ordinal(pool);
@@ -166,6 +167,7 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
 
 hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
   VGPU_REAL_HSA(hsa_amd_memory_pool_free);
+  VGPU_STAT(kStatFree);
   if (!real_hsa_amd_memory_pool_free) return HSA_STATUS_ERROR;
   ShimState& s = shim();
   if (ptr && s.phase.load(std::memory_order_relaxed) == 2) {
@@ -221,6 +223,7 @@ hsa_status_t hsa_amd_vmem_handle_release(hsa_amd_vmem_alloc_handle_t handle) {
 
 hsa_status_t hsa_amd_memory_pool_get_info(hsa_amd_memory_pool_t pool, hsa_amd_memory_pool_info_t attr, void* value) {
   VGPU_REAL_HSA(hsa_amd_memory_pool_get_info);
+  VGPU_STAT(kStatPoolInfo);
   if (!real_hsa_amd_memory_pool_get_info) return HSA_STATUS_ERROR;
   hsa_status_t st = real_hsa_amd_memory_pool_get_info(pool, attr, value);
   if (st != HSA_STATUS_SUCCESS || attr != HSA_AMD_MEMORY_POOL_INFO_SIZE || !value) return st;
@@ -238,6 +241,7 @@ hsa_status_t hsa_amd_memory_pool_get_info(hsa_amd_memory_pool_t pool, hsa_amd_me
 
 hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* value) {
   VGPU_REAL_HSA(hsa_agent_get_info);
+  VGPU_STAT(kStatAgentInfo);
   if (!real_hsa_agent_get_info) return HSA_STATUS_ERROR;
   hsa_status_t st = real_hsa_agent_get_info(agent, attr, value);
   if (__builtin_expect((int)attr != HSA_AMD_AGENT_INFO_MEMORY_AVAIL, 1) || st != HSA_STATUS_SUCCESS) return st;
@@ -259,6 +263,7 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
                               void (*callback)(hsa_status_t, hsa_queue_t*, void*), void* data,
                               uint32_t private_segment_size, uint32_t group_segment_size, hsa_queue_t** queue) {
   VGPU_REAL_HSA(hsa_queue_create);
+  VGPU_STAT(kStatQueueCreate);
   if (!real_hsa_queue_create) return HSA_STATUS_ERROR;
   hsa_status_t st =
       real_hsa_queue_create(agent, size, type, callback, data, private_segment_size, group_segment_size, queue);
@@ -286,6 +291,7 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
 
 hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* queue, uint32_t num_cu_mask_count, const uint32_t* cu_mask) {
   VGPU_REAL_HSA(hsa_amd_queue_cu_set_mask);
+  VGPU_STAT(kStatCuMask);
   if (!real_hsa_amd_queue_cu_set_mask) return HSA_STATUS_ERROR;
   if (!ready()) return real_hsa_amd_queue_cu_set_mask(queue, num_cu_mask_count, cu_mask);
   ShimState& s = shim();

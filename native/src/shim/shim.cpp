@@ -20,6 +20,30 @@
 
 namespace vgpu {
 
+bool g_stats_on = false;
+std::atomic<uint64_t> g_stats[kStatCount];
+
+namespace {
+const char* const kStatNames[kStatCount] = {"hsa_agent_get_info", "hsa_amd_memory_pool_get_info",
+                                            "hsa_amd_memory_pool_allocate", "hsa_amd_memory_pool_free",
+                                            "hsa_queue_create", "hsa_amd_queue_cu_set_mask", "kernel launches",
+                                            "hipGraphLaunch", "memcpy", "memset"};
+
+void print_stats() {
+  fprintf(stderr, "[vGPU stats pid %d]", (int)getpid());
+  for (int i = 0; i < kStatCount; i++) fprintf(stderr, " %s=%lu", kStatNames[i], (unsigned long)g_stats[i].load());
+  fprintf(stderr, "\n");
+}
+
+__attribute__((constructor)) void stats_ctor() {
+  const char* s = getenv("VGPU_STATS");
+  if (s && *s && *s != '0') {
+    g_stats_on = true;
+    atexit(print_stats);
+  }
+}
+}  // namespace
+
 ShimState& shim() {
   static ShimState* s = new ShimState();  // never destroyed: hooks may run during exit
   return *s;

@@ -70,6 +70,20 @@ void shim_init_after_hsa();
 // Lightweight attach for processes that never initialise ROCr (e.g. amd-smi).
 bool shim_attach_region_only();
 
+// Per-hook call counters (diagnostics, VGPU_STATS=1 prints them at exit). Off by
+// default: a disabled counter costs one predictable branch on a plain bool.
+enum StatId : int {
+  kStatAgentInfo, kStatPoolInfo, kStatAlloc, kStatFree, kStatQueueCreate, kStatCuMask,
+  kStatLaunch, kStatGraphLaunch, kStatCopy, kStatSet, kStatCount
+};
+extern bool g_stats_on;
+extern std::atomic<uint64_t> g_stats[kStatCount];
+#define VGPU_STAT(id)                                                                  \
+  do {                                                                                 \
+    if (__builtin_expect(::vgpu::g_stats_on, 0))                                       \
+      ::vgpu::g_stats[::vgpu::id].fetch_add(1, std::memory_order_relaxed);             \
+  } while (0)
+
 // Ordinal of a GPU agent / pool, or -1.
 int agent_ordinal(hsa_agent_t a);
 int pool_ordinal(hsa_amd_memory_pool_t p);

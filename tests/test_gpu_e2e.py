@@ -184,3 +184,37 @@ torch.cuda.synchronize()
 emit(v=float(x[0]))
 """, c)
     assert res[0]["v"] == 201.0
+
+
+def test_rocm_smi_lib_reports_quota(tmp_region):
+    """rocm_smi (ctypes over librocm_smi64, as the rocm-smi CLI does) sees the quota."""
+    c = vgpu_env(mem_limit=24 * GiB, shared_cache=tmp_region)
+    res, _ = run_child("""
+import ctypes, torch
+torch.cuda.mem_get_info(0)
+lib = ctypes.CDLL("/opt/rocm/lib/librocm_smi64.so")
+rc = lib.rsmi_init(ctypes.c_uint64(0))
+if rc != 0:
+    emit(ok=False, err=f"rsmi_init {rc}")
+else:
+    total = ctypes.c_uint64()
+    rc = lib.rsmi_dev_memory_total_get(ctypes.c_uint32(0), ctypes.c_int(0), ctypes.byref(total))
+    emit(ok=rc == 0, total=total.value, err=f"rc {rc}")
+""", c)
+    r = res[0]
+    if not r["ok"]:
+        pytest.skip(f"rocm_smi unavailable on this box: {r['err']}")
+    assert r["total"] == 24 * GiB
+
+
+def test_amdsmi_native_diagnostic():
+    """Diagnostic: does amdsmi initialise on this box without the shim?"""
+    res, p = run_child("""
+try:
+    import amdsmi
+    amdsmi.amdsmi_init()
+    emit(ok=True, n=len(amdsmi.amdsmi_get_processor_handles()))
+except Exception as e:
+    emit(ok=False, err=repr(e)[:300])
+""", None)
+    print("amdsmi native:", res[0])
