@@ -45,6 +45,8 @@ def parse(argv=None):
     ap.add_argument("--cu-mode", default="spatial", choices=["spatial", "temporal", "both", "off"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-fuse", action="store_true", help="eager PyTorch epilogues (no fused HIP BN+ReLU)")
+    ap.add_argument("--tune", type=int, default=0, choices=[0, 1],
+                    help="1: MIOpen find-mode conv autotuning (torch.backends.cudnn.benchmark)")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     # worker-only
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
@@ -88,6 +90,7 @@ def worker(args):
         if total != min(quota, MI355X_HBM_BYTES) and not os.environ.get("VGPU_OVERSUBSCRIBE"):
             raise SystemExit(f"vGPU shim not in effect: mem_get_info total {total} != quota {quota}")
 
+    torch.backends.cudnn.benchmark = bool(args.tune)
     case = get_case(args.case)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     if cpu:
@@ -139,7 +142,7 @@ def run_mode(args, mode, port):
     os.close(fd)
     cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--mode", mode, "--result-file", result,
            "--port", str(port), "--case", args.case, "--steps", str(args.steps), "--warmup", str(args.warmup),
-           "--dtype", args.dtype] + (["--no-fuse"] if args.no_fuse else []) + \
+           "--dtype", args.dtype, "--tune", str(args.tune)] + (["--no-fuse"] if args.no_fuse else []) + \
         (["--cpu-rehearsal"] if args.cpu_rehearsal else [])
     contract = {}
     if mode == "vgpu":
@@ -208,6 +211,7 @@ def main(argv=None):
             "input_shape": list(case.input_shape), "seq_len": None,
             "parallelism": f"dp{world} (one independent vGPU replica per GPU)",
             "fused_epilogues": not args.no_fuse,
+            "conv_autotune": bool(args.tune),
             "vgpu": {"split": args.split, "quota_bytes": int(MI355X_HBM_BYTES * args.memory_scaling / args.split),
                      "cu_limit_pct": args.cu_limit, "cu_mode": args.cu_mode,
                      "memory_scaling": args.memory_scaling},

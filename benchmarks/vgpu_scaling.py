@@ -49,13 +49,13 @@ def worker(case_name, steps, warmup, out, go_file):
                "throughput": case.batch * steps / (t1 - t0)}, open(out, "w"))
 
 
-def run_point(case, n, policy, steps, warmup):
+def run_point(case, n, policy, steps, warmup, solo=False):
     from amdvgpu.plugin.vdevice import cu_partition_range
     from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
     tmp = tempfile.mkdtemp(prefix="scal-")
     go = os.path.join(tmp, "go")
     procs, contracts, outs = [], [], []
-    for i in range(n):
+    for i in range(1 if solo else n):
         kw = dict(mem_limit=HBM // n)
         if policy == "vdm":
             kw = dict(mem_limit=int(HBM * 1.8 / n), oversubscribe=True,
@@ -91,7 +91,7 @@ def run_point(case, n, policy, steps, warmup):
             cleanup_region(c)
     span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
     agg = sum(r["batch"] * steps for r in res) / span
-    return {"tenants": n, "policy": policy, "aggregate_throughput": agg,
+    return {"tenants": n, "policy": policy + ("-solo" if solo else ""), "aggregate_throughput": agg,
             "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res]}
 
 
@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--policy", default="spatial,shared")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--solo", action="store_true", help="run only tenant 0 of each N (its slice alone)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--go")
@@ -113,10 +114,12 @@ def main():
     rows = []
     for pol in a.policy.split(","):
         for n in [int(x) for x in a.tenants.split(",")]:
-            r = run_point(a.case, n, pol, a.steps, a.warmup)
+            r = run_point(a.case, n, pol, a.steps, a.warmup, solo=a.solo)
             rows.append(r)
             print(json.dumps(r), flush=True)
     base = {r["policy"]: r["aggregate_throughput"] for r in rows if r["tenants"] == 1}
+    for r in rows:
+        base.setdefault(r["policy"], rows[0]["aggregate_throughput"])
     md = [f"# concurrent vGPUs on one MI355X — {a.case}", "",
           "| policy | tenants | aggregate | vs 1 tenant | per-tenant (min..max) |", "|---|---|---|---|---|"]
     for r in rows:

@@ -79,7 +79,9 @@ except torch.OutOfMemoryError:
 emit(first=first)
 while not os.path.exists({go!r}):
     time.sleep(0.02)
-y = torch.empty(3 << 30, dtype=torch.uint8, device="cuda")
+# HIP rejects a single allocation larger than the device size it cached at init (the
+# old 2 GiB), so grow in 1 GiB steps: 3 GiB in total only fits under the raised limit.
+y = [torch.empty(1 << 30, dtype=torch.uint8, device="cuda") for _ in range(3)]
 free, total = torch.cuda.mem_get_info(0)
 emit(second=True, total=total)
 """, c)
