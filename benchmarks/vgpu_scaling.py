@@ -60,9 +60,11 @@ def run_point(case, n, policy, steps, warmup, solo=False):
         if policy == "vdm":
             kw = dict(mem_limit=int(HBM * 1.8 / n), oversubscribe=True,
                       extra={"VGPU_DEVICE_HBM_LIMIT_0": f"{HBM // n >> 20}m"})
-        if policy in ("spatial", "spatial-interleave", "vdm") and n > 1:
+        if policy in ("spatial", "spatial-interleave", "spatial-q1", "vdm") and n > 1:
             b, e = cu_partition_range(256, 8, n, i)
             kw.update(cu_limit=100 * (e - b) // 256, cu_range=(b, e))
+        if policy == "spatial-q1":
+            kw["extra"] = dict(kw.get("extra") or {}, GPU_MAX_HW_QUEUES="1")
         if policy == "spatial-interleave":
             kw["extra"] = dict(kw.get("extra") or {}, VGPU_CU_LAYOUT="interleave")
         c = vgpu_env(**kw)

@@ -16,6 +16,7 @@
 #include <dlfcn.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 
 #include <amd_smi/amdsmi.h>
@@ -32,6 +33,13 @@ rsmi_status_t rsmi_dev_memory_usage_get(uint32_t, rsmi_memory_type_t, uint64_t*)
 namespace {
 
 using DlsymFn = void* (*)(void*, const char*);
+
+// VGPU_HOOK_DLSYM=0 turns the redirection off (read once when the shim is loaded).
+bool g_dlsym_hook_on = true;
+__attribute__((constructor)) void dlsym_hook_ctor() {
+  const char* s = getenv("VGPU_HOOK_DLSYM");
+  if (s && (*s == '0' || *s == 'f' || *s == 'F' || *s == 'n' || *s == 'N')) g_dlsym_hook_on = false;
+}
 
 std::atomic<DlsymFn> g_real_234{nullptr};
 std::atomic<DlsymFn> g_real_225{nullptr};
@@ -85,7 +93,7 @@ extern "C" {
 
 __attribute__((visibility("default"))) void* shim_dlsym_v234(void* handle, const char* name) {
   DlsymFn real = load_real(g_real_234, "GLIBC_2.34");
-  if (__builtin_expect(name && (name[0] == 'a' || name[0] == 'r'), 0)) {
+  if (__builtin_expect(g_dlsym_hook_on && name && (name[0] == 'a' || name[0] == 'r'), 0)) {
     if (void* h = maybe_hook(handle, name, real)) return h;
   }
   [[clang::musttail]] return real(handle, name);
@@ -93,7 +101,7 @@ __attribute__((visibility("default"))) void* shim_dlsym_v234(void* handle, const
 
 __attribute__((visibility("default"))) void* shim_dlsym_v225(void* handle, const char* name) {
   DlsymFn real = load_real(g_real_225, "GLIBC_2.2.5");
-  if (__builtin_expect(name && (name[0] == 'a' || name[0] == 'r'), 0)) {
+  if (__builtin_expect(g_dlsym_hook_on && name && (name[0] == 'a' || name[0] == 'r'), 0)) {
     if (void* h = maybe_hook(handle, name, real)) return h;
   }
   [[clang::musttail]] return real(handle, name);
