@@ -45,8 +45,9 @@ def parse(argv=None):
     ap.add_argument("--cu-mode", default="spatial", choices=["spatial", "temporal", "both", "off"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-fuse", action="store_true", help="eager PyTorch epilogues (no fused HIP BN+ReLU)")
-    ap.add_argument("--tune", type=int, default=0, choices=[0, 1],
-                    help="1: MIOpen find-mode conv autotuning (torch.backends.cudnn.benchmark)")
+    ap.add_argument("--tune", type=int, default=1, choices=[0, 1],
+                    help="MIOpen find-mode conv autotuning during warmup (torch.backends.cudnn.benchmark); "
+                         "the reference's TensorFlow autotunes convolutions too")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     # worker-only
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)

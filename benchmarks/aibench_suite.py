@@ -39,6 +39,7 @@ MODES = {
 def worker(cases, steps, warmup, out):
     import torch
     from amdvgpu.models.aibench import Runner, get_case
+    torch.backends.cudnn.benchmark = os.environ.get("VGPU_BENCH_TUNE", "1") == "1"  # MIOpen find mode
     res = {}
     for name in cases:
         case = get_case(name)

@@ -25,6 +25,7 @@ GiB = 1 << 30
 def worker(case, ballast_gib, steps, warmup, out):
     import torch
     from amdvgpu.models.aibench import Runner, get_case
+    torch.backends.cudnn.benchmark = os.environ.get("VGPU_BENCH_TUNE", "1") == "1"  # MIOpen find mode
     from amdvgpu.shim.region import Region
     free, total = torch.cuda.mem_get_info(0)
     ballast = []

@@ -32,6 +32,7 @@ HBM = 309220868096
 def worker(case_name, steps, warmup, out, go_file):
     import torch
     from amdvgpu.models.aibench import Runner, get_case
+    torch.backends.cudnn.benchmark = os.environ.get("VGPU_BENCH_TUNE", "1") == "1"  # MIOpen find mode
     case = get_case(case_name)
     r = Runner(case, "cuda:0")
     for _ in range(warmup):

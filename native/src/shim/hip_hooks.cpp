@@ -33,6 +33,7 @@ extern "C" hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t globalW
 
 using LaunchKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t);
 using CoopKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, unsigned int, hipStream_t);
+using MallocManagedFn = hipError_t (*)(void**, size_t, unsigned int);
 using ExtLaunchKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t, hipEvent_t, hipEvent_t,
                                          int);
 
@@ -213,6 +214,58 @@ hipError_t hipGraphExecDestroy(hipGraphExec_t graphExec) {
     g_graph_wgs.erase(reinterpret_cast<uintptr_t>(graphExec));
   }
   return real_hipGraphExecDestroy(graphExec);
+}
+
+// Managed memory (reference: cuMemAllocManaged is an accounted allocation, class (a) in
+// SURVEY.md §2.3). Depending on XNACK/HMM mode CLR may back it with system memory that
+// never reaches the HSA pool hooks, so it is charged here unless the pool hook already
+// charged the same pointer; past the quota the allocation is released and refused.
+hipError_t hipMallocManaged(void** dev_ptr, size_t size, unsigned int flags) {
+  VGPU_REAL_HIP_T(hipMallocManaged, MallocManagedFn);
+  VGPU_REAL_HIP(hipFree);
+  ShimState& s = shim();
+  if (__builtin_expect(!s.active, 1) || size == 0) return real_hipMallocManaged(dev_ptr, size, flags);
+  gate_suspend();
+  hipError_t e = real_hipMallocManaged(dev_ptr, size, flags);
+  if (e != hipSuccess || !dev_ptr || !*dev_ptr) return e;
+  uintptr_t key = reinterpret_cast<uintptr_t>(*dev_ptr);
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    if (s.allocs.count(key)) return e;  // already charged by hsa_amd_memory_pool_allocate
+  }
+  int dev = 0;
+  if (s.n_agents > 1) {
+    VGPU_REAL_HIP(hipGetDevice);
+    if (!real_hipGetDevice || real_hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= s.n_agents) dev = 0;
+  }
+  if (s.region.charge(s.slot, dev, size, kMemData) != Charge::kOk) {
+    (void)real_hipFree(*dev_ptr);
+    *dev_ptr = nullptr;
+    return hipErrorOutOfMemory;
+  }
+  std::lock_guard<std::mutex> g(s.alloc_mu);
+  s.managed[key] = AllocRec{size, dev, kMemData};
+  return e;
+}
+
+hipError_t hipFree(void* ptr) {
+  VGPU_REAL_HIP(hipFree);
+  ShimState& s = shim();
+  if (__builtin_expect(s.active && ptr != nullptr, 1)) {
+    AllocRec rec{0, -1, 0};
+    {
+      std::lock_guard<std::mutex> g(s.alloc_mu);
+      if (!s.managed.empty()) {
+        auto it = s.managed.find(reinterpret_cast<uintptr_t>(ptr));
+        if (it != s.managed.end()) {
+          rec = it->second;
+          s.managed.erase(it);
+        }
+      }
+    }
+    if (rec.dev >= 0 && s.slot >= 0 && !s.exiting.load()) s.region.uncharge(s.slot, rec.dev, rec.size, kMemData);
+  }
+  return real_hipFree(ptr);
 }
 
 // Copy/set gates (suspend only), mirroring the reference's wait_status_self set.

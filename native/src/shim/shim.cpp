@@ -147,6 +147,7 @@ void atfork_child() {
   s.active = false;
   s.allocs.clear();
   s.vmem.clear();
+  s.managed.clear();
   s.queues.clear();
   s.watcher_started.store(false);
   s.phase.store(0);

@@ -58,6 +58,7 @@ struct ShimState {
   std::mutex alloc_mu;
   std::unordered_map<uintptr_t, AllocRec> allocs;   // device pointer → record
   std::unordered_map<uint64_t, AllocRec> vmem;      // vmem handle → record
+  std::unordered_map<uintptr_t, AllocRec> managed;  // hipMallocManaged pointers charged at HIP level
   std::unordered_map<uintptr_t, int> queues;        // hsa_queue_t* → ordinal
   std::atomic<bool> exiting{false};
   std::atomic<bool> watcher_started{false};

@@ -11,7 +11,7 @@ from amdvgpu.plugin.devices import SysfsBackend
 from amdvgpu.plugin.kubelet_stub import StubKubelet, run_pod
 from amdvgpu.plugin.main import Supervisor
 from amdvgpu.shim.launcher import vgpu_env
-from conftest import CHILD_PRELUDE, run_child
+from conftest import CHILD_PRELUDE, run_child, spawn_child
 
 pytestmark = pytest.mark.gpu
 
@@ -128,13 +128,23 @@ emit(total=total, ok_ab=ok_ab, spilled=r["spilled"], used=r["used"], hbm=r["hbm_
     print(f"spill read bandwidth {r['bw']:.1f} GB/s")
 
 
-def test_amdsmi_reports_quota(tmp_region):
-    """In-container amd-smi (Python amdsmi over ctypes) sees the vGPU quota."""
-    c = vgpu_env(mem_limit=24 * GiB, shared_cache=tmp_region)
-    res, _ = run_child("""
+CONFIGURE = """
 import torch
-torch.cuda.mem_get_info(0)          # first GPU process records the device's BDF in the region
+torch.cuda.mem_get_info(0)    # a GPU process of the container records the device (BDF) in the region
 x = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+emit(ok=True)
+time.sleep(30)
+"""
+
+
+def test_amdsmi_reports_quota(tmp_region):
+    """In-container amd-smi (Python amdsmi over ctypes) sees the vGPU quota while a GPU
+    process of the same container is running."""
+    c = vgpu_env(mem_limit=24 * GiB, shared_cache=tmp_region)
+    holder = spawn_child(CONFIGURE, c)
+    try:
+        assert holder.stdout.readline().startswith("RESULT")
+        res, _ = run_child("""
 try:
     import amdsmi
     amdsmi.amdsmi_init()
@@ -145,6 +155,9 @@ try:
 except Exception as e:
     emit(ok=False, err=repr(e)[:300])
 """, c)
+    finally:
+        holder.kill()
+        holder.wait()
     r = res[0]
     if not r["ok"]:
         pytest.skip(f"amdsmi unavailable on this box: {r['err']}")
@@ -189,22 +202,29 @@ emit(v=float(x[0]))
 def test_rocm_smi_lib_reports_quota(tmp_region):
     """rocm_smi (ctypes over librocm_smi64, as the rocm-smi CLI does) sees the quota."""
     c = vgpu_env(mem_limit=24 * GiB, shared_cache=tmp_region)
-    res, _ = run_child("""
-import ctypes, torch
-torch.cuda.mem_get_info(0)
+    holder = spawn_child(CONFIGURE, c)
+    try:
+        assert holder.stdout.readline().startswith("RESULT")
+        res, _ = run_child("""
+import ctypes
 lib = ctypes.CDLL("/opt/rocm/lib/librocm_smi64.so")
 rc = lib.rsmi_init(ctypes.c_uint64(0))
 if rc != 0:
     emit(ok=False, err=f"rsmi_init {rc}")
 else:
-    total = ctypes.c_uint64()
+    total, used = ctypes.c_uint64(), ctypes.c_uint64()
     rc = lib.rsmi_dev_memory_total_get(ctypes.c_uint32(0), ctypes.c_int(0), ctypes.byref(total))
-    emit(ok=rc == 0, total=total.value, err=f"rc {rc}")
+    lib.rsmi_dev_memory_usage_get(ctypes.c_uint32(0), ctypes.c_int(0), ctypes.byref(used))
+    emit(ok=rc == 0, total=total.value, used=used.value, err=f"rc {rc}")
 """, c)
+    finally:
+        holder.kill()
+        holder.wait()
     r = res[0]
     if not r["ok"]:
         pytest.skip(f"rocm_smi unavailable on this box: {r['err']}")
     assert r["total"] == 24 * GiB
+    assert GiB <= r["used"] <= 24 * GiB
 
 
 def test_amdsmi_native_diagnostic():

@@ -254,3 +254,19 @@ emit(locs=sorted(cu_census(nblocks=8192, spin_us=300)))
         assert len(locs) == 64
         assert {l[1] for l in locs} == {slot}, sorted({(l[0], l[1]) for l in locs})
         assert len({l[0] for l in locs}) == 8
+
+
+def test_managed_memory_is_accounted(tmp_region):
+    c = vgpu_env(mem_limit=2 * GiB, shared_cache=tmp_region)
+    res, _ = run_child("""
+import ctypes
+hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+a, b, d = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+r1 = hip.hipMallocManaged(ctypes.byref(a), ctypes.c_size_t(1536 << 20), ctypes.c_uint(1))
+r2 = hip.hipMallocManaged(ctypes.byref(b), ctypes.c_size_t(1024 << 20), ctypes.c_uint(1))
+f1 = hip.hipFree(a)
+r3 = hip.hipMallocManaged(ctypes.byref(d), ctypes.c_size_t(1024 << 20), ctypes.c_uint(1))
+emit(r1=r1, r2=r2, f1=f1, r3=r3)
+""", c)
+    r = res[0]
+    assert r["r1"] == 0 and r["r2"] != 0 and r["f1"] == 0 and r["r3"] == 0, r
