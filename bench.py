@@ -214,6 +214,8 @@ def main(argv=None):
             "fused_epilogues": not args.no_fuse,
             "conv_autotune": bool(args.tune),
             "vgpu": {"split": args.split, "quota_bytes": int(MI355X_HBM_BYTES * args.memory_scaling / args.split),
+                     # CU-mask granularity is one CU per XCD (8 CUs): 256 / 8 disjoint slices
+                     "max_vgpus_per_gpu_spatial": 32,
                      "cu_limit_pct": args.cu_limit, "cu_mode": args.cu_mode,
                      "memory_scaling": args.memory_scaling},
         },

@@ -165,7 +165,10 @@ void SharedRegion::init_fresh(const Config* cfg) {
 }
 
 void SharedRegion::check_consistency(const Config* cfg) {
-  for (int i = 0; i < kMaxDevices; i++) {
+  // Only devices the region actually describes: a GPU process records the visible agents,
+  // while an attach-only process (e.g. amd-smi) carries the raw env for all 16 slots.
+  const int n = r_->hdr.num_devices > 0 ? r_->hdr.num_devices : kMaxDevices;
+  for (int i = 0; i < n && i < kMaxDevices; i++) {
     uint64_t have = r_->dev[i].mem_limit;
     uint64_t want = cfg->dev[i].mem_limit;
     if (want && have != want) {

@@ -224,14 +224,18 @@ hipError_t hipMallocManaged(void** dev_ptr, size_t size, unsigned int flags) {
   VGPU_REAL_HIP_T(hipMallocManaged, MallocManagedFn);
   VGPU_REAL_HIP(hipFree);
   ShimState& s = shim();
-  if (__builtin_expect(!s.active, 1) || size == 0) return real_hipMallocManaged(dev_ptr, size, flags);
   gate_suspend();
+  // The first HIP call of a process initialises the runtime (and the shim, from the
+  // hsa_init hook) inside the real call, so `active` is only meaningful afterwards:
+  // charge after the allocation and release it again when over the quota.
   hipError_t e = real_hipMallocManaged(dev_ptr, size, flags);
-  if (e != hipSuccess || !dev_ptr || !*dev_ptr) return e;
+  if (!s.active || size == 0 || e != hipSuccess || !dev_ptr || !*dev_ptr) return e;
   uintptr_t key = reinterpret_cast<uintptr_t>(*dev_ptr);
   {
     std::lock_guard<std::mutex> g(s.alloc_mu);
-    if (s.allocs.count(key)) return e;  // already charged by hsa_amd_memory_pool_allocate
+    bool pooled = s.allocs.count(key) != 0;
+    VLOG_DEBUG("hipMallocManaged(%zu) -> %p (%s)", size, *dev_ptr, pooled ? "charged by the pool hook" : "charging");
+    if (pooled) return e;  // already charged by hsa_amd_memory_pool_allocate
   }
   int dev = 0;
   if (s.n_agents > 1) {

@@ -124,6 +124,7 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   if (!real_hsa_amd_memory_pool_allocate) return HSA_STATUS_ERROR;
   if (!ready() || size == 0) return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
   int dev = pool_ordinal(pool);
+  VLOG_DEBUG("pool_allocate pool=%lx size=%zu flags=%u dev=%d", (unsigned long)pool.handle, size, flags, dev);
   if (dev < 0) return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
   ShimState& s = shim();
   gate_suspend();

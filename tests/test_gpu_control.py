@@ -54,8 +54,11 @@ time.sleep(60)
 """, c)
     assert p.stdout.readline().startswith("RESULT")
     r = Region(tmp_region)
-    time.sleep(0.5)
-    assert r.device(0)["monitor_used"] >= 6 * GiB  # KFD-measured VRAM of the region's processes
+    deadline = time.time() + 10
+    while r.device(0)["monitor_used"] < 6 * GiB and time.time() < deadline:
+        time.sleep(0.1)
+    # KFD-measured VRAM of the region's processes, sampled by the watcher every period
+    assert r.device(0)["monitor_used"] >= 6 * GiB, (r.device(0), r.procs())
     r.set_memory_limit(0, 2 * GiB)                  # operator shrinks the quota below usage
     try:
         p.wait(timeout=20)

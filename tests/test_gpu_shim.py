@@ -256,17 +256,18 @@ emit(locs=sorted(cu_census(nblocks=8192, spin_us=300)))
         assert len({l[0] for l in locs}) == 8
 
 
-def test_managed_memory_is_accounted(tmp_region):
+@pytest.mark.parametrize("kind", ["managed", "malloc"])
+def test_hip_allocations_are_accounted(tmp_region, kind):
+    """A plain HIP program (linked normally against libamdhip64) under a 2 GiB quota:
+    1.5 GiB fits, +1 GiB is refused, after freeing the first block 1 GiB fits again."""
+    import json
+    import subprocess
+    from amdvgpu.shim.launcher import apply_contract
+    from amdvgpu.shim.native import LIB_DIR
     c = vgpu_env(mem_limit=2 * GiB, shared_cache=tmp_region)
-    res, _ = run_child("""
-import ctypes
-hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
-a, b, d = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
-r1 = hip.hipMallocManaged(ctypes.byref(a), ctypes.c_size_t(1536 << 20), ctypes.c_uint(1))
-r2 = hip.hipMallocManaged(ctypes.byref(b), ctypes.c_size_t(1024 << 20), ctypes.c_uint(1))
-f1 = hip.hipFree(a)
-r3 = hip.hipMallocManaged(ctypes.byref(d), ctypes.c_size_t(1024 << 20), ctypes.c_uint(1))
-emit(r1=r1, r2=r2, f1=f1, r3=r3)
-""", c)
-    r = res[0]
+    p = subprocess.run([os.path.join(LIB_DIR, "hip_alloc_probe"), kind], env=apply_contract(c),
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["r1"] == 0 and r["r2"] != 0 and r["f1"] == 0 and r["r3"] == 0, r
+    assert r["total"] == 2 * GiB
