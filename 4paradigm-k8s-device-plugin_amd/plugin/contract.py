@@ -110,6 +110,8 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         resp.envs["VGPU_SHARED_CACHE"] = os.path.join(cfg.shared_cache_dir, cache_name)
     if cfg.device_memory_scaling > 1:
         resp.envs["VGPU_OVERSUBSCRIBE"] = "true"
+    # Device authorisation against the node's allow-list (mounted below at /vgpu).
+    resp.envs["VGPU_ALLOWLIST"] = CONTAINER_ALLOWLIST_DIR + "/allowlist"
 
     vdir = cfg.vgpu_dir
     resp.mounts.add(container_path=CONTAINER_SHIM, host_path=os.path.join(vdir, "libvgpu_hip.so"), read_only=True)

@@ -74,8 +74,9 @@ def apply_contract(contract_envs, mounts=(), base_env=None, preload=True, shim=N
     remap = {c: h for c, h in mounts}
     for k, v in contract_envs.items():
         for c, h in remap.items():
-            if c in v and c != "/":
-                v = v.replace(c, h)
+            if c != "/" and (v == c or v.startswith(c.rstrip("/") + "/")):
+                v = h + v[len(c):]
+                break
         env[k] = v
     if preload:
         lib = shim or remap.get(CONTAINER_SHIM)

@@ -128,6 +128,7 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   if (dev < 0) return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
   ShimState& s = shim();
   gate_suspend();
+  if (__builtin_expect(!s.agents[dev].authorised, 0)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   if (s.region.charge(s.slot, dev, size, kMemData) != Charge::kOk) {
     VLOG_WARN("device %d OOM: request %zu bytes, usage %lu of limit %lu", dev, size,
               (unsigned long)s.region.usage(dev), (unsigned long)s.region.limit(dev));

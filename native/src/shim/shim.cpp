@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <string>
 #include <vector>
 
 #include "real.h"
@@ -249,6 +250,29 @@ void shim_init_after_hsa() {
   if (!parse_device_map(map_env, &map)) {
     VLOG_WARN("invalid VGPU_DEVICE_MAP=%s, using positional limits", map_env);
     map = DeviceMap();
+  }
+  // Device authorisation (reference: vgpuvalidator, dormant there): with VGPU_ALLOWLIST
+  // set, GPUs whose ROCr UUID is not listed get no device memory at all.
+  if (const char* al = getenv("VGPU_ALLOWLIST")) {
+    if (FILE* f = *al ? fopen(al, "r") : nullptr) {
+      std::vector<std::string> allowed;
+      char line[128];
+      while (fgets(line, sizeof(line), f)) {
+        char norm[64];
+        line[strcspn(line, "\r\n")] = 0;
+        normalize_uuid(line, norm, sizeof(norm));
+        if (norm[0]) allowed.emplace_back(norm);
+      }
+      fclose(f);
+      for (int i = 0; i < s.n_agents; i++) {
+        char norm[64];
+        normalize_uuid(uuids[i], norm, sizeof(norm));
+        s.agents[i].authorised = std::find(allowed.begin(), allowed.end(), std::string(norm)) != allowed.end();
+        if (!s.agents[i].authorised) VLOG_ERROR("device %d (%s) is not authorised for this container", i, uuids[i]);
+      }
+    } else {
+      VLOG_WARN("VGPU_ALLOWLIST=%s is not readable; device authorisation skipped", al);
+    }
   }
   Config resolved = cfg;
   DeviceConfig per_agent[kMaxDevices];

@@ -33,6 +33,7 @@ struct AgentInfo {
   int max_waves_per_cu = 32;
   uint64_t phys_total = 0;
   bool mask_active = false;          // spatial mask applied to its queues
+  bool authorised = true;            // listed in VGPU_ALLOWLIST (when one is configured)
   bool temporal_active = false;      // token bucket gates its launches
   bool context_charged = false;
   CuMask mask;

@@ -271,3 +271,23 @@ def test_hip_allocations_are_accounted(tmp_region, kind):
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["r1"] == 0 and r["r2"] != 0 and r["f1"] == 0 and r["r3"] == 0, r
     assert r["total"] == 2 * GiB
+
+
+def test_allowlist_authorisation(tmp_region, tmp_path):
+    from amdvgpu.plugin.devices import SysfsBackend
+    uuid = SysfsBackend().devices()[0].uuid
+    code = """
+import torch
+try:
+    x = torch.empty(1 << 20, device="cuda"); ok = True
+except torch.OutOfMemoryError:
+    ok = False
+emit(ok=ok)
+"""
+    allow = tmp_path / "allowlist"
+    allow.write_text(uuid + "\n")
+    c = vgpu_env(mem_limit=8 * GiB, shared_cache=tmp_region, extra={"VGPU_ALLOWLIST": str(allow)})
+    assert run_child(code, c)[0][0]["ok"] is True
+    allow.write_text("GPU-0000000000000000\n")
+    os.unlink(tmp_region)
+    assert run_child(code, c)[0][0]["ok"] is False

@@ -8,16 +8,25 @@ import glob
 import sqlite3
 
 
-def summarize(db_path, top=25, title=None):
+def summarize(db_path, top=25, title=None, after_last=None):
     db = sqlite3.connect(db_path)
     cur = db.cursor()
     procs = cur.execute("select pid, command from processes").fetchall()
-    total_n, total_ns = cur.execute("select count(*), sum(duration) from kernels").fetchone()
-    span = cur.execute("select min(start), max(end) from kernels").fetchone()
-    rows = cur.execute("select name, total_calls, total_duration, average, percentage from top_kernels "
-                       "order by total_duration desc limit ?", (top,)).fetchall()
+    t0 = 0
+    if after_last:
+        # steady state only: dispatches after the last kernel matching the pattern (e.g. the
+        # MIOpen find-mode reference kernels that run during warmup)
+        row = cur.execute("select max(end) from kernels where name like ?", (f"%{after_last}%",)).fetchone()
+        t0 = row[0] or 0
+    total_n, total_ns = cur.execute("select count(*), sum(duration) from kernels where start > ?", (t0,)).fetchone()
+    span = cur.execute("select min(start), max(end) from kernels where start > ?", (t0,)).fetchone()
+    tot = total_ns or 1
+    rows = cur.execute("select name, count(*), sum(duration), avg(duration), 100.0 * sum(duration) / ? from kernels "
+                       "where start > ? group by name order by sum(duration) desc limit ?", (tot, t0, top)).fetchall()
+    rows = [(n, c, t / 1e3, a / 1e3, pct) for n, c, t, a, pct in rows]
     out = [f"# {title or 'rocprofv3 kernel summary'}", "",
-           f"source: `{db_path}` (rocprofv3 --kernel-trace --stats)", ""]
+           f"source: `{db_path}` (rocprofv3 --kernel-trace --stats)"
+           + (f"; steady state after the last `{after_last}` dispatch" if after_last else ""), ""]
     for pid, cmd in procs:
         out.append(f"* process {pid}: `{cmd[:200]}`")
     out += ["", f"* kernels dispatched: {total_n}", f"* summed kernel time: {total_ns / 1e6:.2f} ms",
@@ -36,9 +45,10 @@ if __name__ == "__main__":
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--title", default=None)
     ap.add_argument("-o", "--out", default=None)
+    ap.add_argument("--after-last", default=None, help="only dispatches after the last kernel matching this")
     a = ap.parse_args()
     paths = [p for g in a.db for p in glob.glob(g)]
-    text = "\n".join(summarize(p, a.top, a.title) for p in paths)
+    text = "\n".join(summarize(p, a.top, a.title, a.after_last) for p in paths)
     if a.out:
         open(a.out, "w").write(text)
     else:
