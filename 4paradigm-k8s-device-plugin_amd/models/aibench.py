@@ -311,7 +311,27 @@ class Runner:
         self.fused = fuse and not case.train and isinstance(model, nn.Module) and type(model).__name__ == "FusedResNetV2"
         self.model = model
 
+    def capture(self, warmup=3):
+        """Capture the inference forward into a HIP graph (torch.cuda.CUDAGraph); later
+        steps replay it with one launch. Warm-up runs on a side stream first so lazy
+        initialisation and autotuning happen outside the capture."""
+        if self.case.train or self.device.type != "cuda":
+            raise ValueError("graph capture is for inference on a GPU")
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s), torch.inference_mode():
+            for _ in range(warmup):
+                self.model(self.x)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.inference_mode(), torch.cuda.graph(self.graph):
+            self.graph_out = self.model(self.x)
+        return self
+
     def step(self):
+        if getattr(self, "graph", None) is not None:
+            self.graph.replay()
+            return self.graph_out
         if not self.case.train:
             with torch.inference_mode():
                 return self.model(self.x)

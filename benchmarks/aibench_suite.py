@@ -33,6 +33,12 @@ MODES = {
     "vgpu": dict(mem_limit=HBM // 2),
     "vgpu-cu50": dict(mem_limit=HBM // 2, cu_limit=50),
     "vgpu-t50": dict(mem_limit=HBM // 2, cu_limit=50, cu_mode="temporal"),
+    # inference replayed from a captured HIP graph (training cases run eagerly)
+    "vgpu-graph": dict(mem_limit=HBM // 2, extra={"VGPU_BENCH_GRAPH": "1"}),
+    "native-graph": {"extra": {"VGPU_BENCH_GRAPH": "1"}, "native": True},
+    # diagnostics: launch hooks as pure pass-throughs / per-hook call counters
+    "vgpu-nolaunch": dict(mem_limit=HBM // 2, extra={"VGPU_HOOK_LAUNCH": "0"}),
+    "vgpu-stats": dict(mem_limit=HBM // 2, extra={"VGPU_STATS": "1"}),
 }
 
 
@@ -46,6 +52,8 @@ def worker(cases, steps, warmup, out):
         r = Runner(case, "cuda:0")
         for _ in range(warmup):
             r.step()
+        if os.environ.get("VGPU_BENCH_GRAPH") == "1" and not case.train:
+            r.capture()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -64,8 +72,14 @@ def run_mode(mode, cases, steps, warmup):
     from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
     fd, out = tempfile.mkstemp(suffix=".json")
     os.close(fd)
-    contract = vgpu_env(**MODES[mode]) if MODES[mode] else {}
-    env = apply_contract(contract) if contract else dict(os.environ)
+    spec = dict(MODES[mode] or {})
+    native = spec.pop("native", False) or not MODES[mode]
+    if native:
+        contract = {}
+        env = dict(os.environ, **spec.get("extra", {}))
+    else:
+        contract = vgpu_env(**spec)
+        env = apply_contract(contract)
     cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--cases", ",".join(cases), "--steps", str(steps),
            "--warmup", str(warmup), "--out", out]
     print(f"[{mode}]", flush=True)

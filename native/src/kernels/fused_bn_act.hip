@@ -31,15 +31,27 @@ __device__ __forceinline__ unsigned pack_bf16(float lo, float hi) {
   return (unsigned)__bfloat16_as_ushort(a) | ((unsigned)__bfloat16_as_ushort(b) << 16);
 }
 
-template <bool kAdd, bool kWriteSum, int kAct>
-__device__ __forceinline__ void apply8(const u32x4& xv, const u32x4& rv, const float* __restrict__ scale,
-                                       const float* __restrict__ shift, unsigned c0, u32x4* yv, u32x4* sv) {
+struct Params8 {
+  float sc[8];
+  float sh[8];
+};
+
+__device__ __forceinline__ Params8 load_params(const float* __restrict__ scale, const float* __restrict__ shift,
+                                               unsigned c0) {
+  Params8 p;
   const float4 s0 = *reinterpret_cast<const float4*>(scale + c0);
   const float4 s1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
   const float4 t0 = *reinterpret_cast<const float4*>(shift + c0);
   const float4 t1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
-  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-  const float sh[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+  p.sc[0] = s0.x; p.sc[1] = s0.y; p.sc[2] = s0.z; p.sc[3] = s0.w;
+  p.sc[4] = s1.x; p.sc[5] = s1.y; p.sc[6] = s1.z; p.sc[7] = s1.w;
+  p.sh[0] = t0.x; p.sh[1] = t0.y; p.sh[2] = t0.z; p.sh[3] = t0.w;
+  p.sh[4] = t1.x; p.sh[5] = t1.y; p.sh[6] = t1.z; p.sh[7] = t1.w;
+  return p;
+}
+
+template <bool kAdd, bool kWriteSum, int kAct>
+__device__ __forceinline__ void apply8(const u32x4& xv, const u32x4& rv, const Params8& p, u32x4* yv, u32x4* sv) {
   float v[8];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -59,7 +71,7 @@ __device__ __forceinline__ void apply8(const u32x4& xv, const u32x4& rv, const f
   }
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    float o = fmaf(v[j], sc[j], sh[j]);
+    float o = fmaf(v[j], p.sc[j], p.sh[j]);
     if constexpr (kAct == 1) o = fmaxf(o, 0.0f);
     if constexpr (kAct == 2) o = fminf(fmaxf(o, 0.0f), 6.0f);
     v[j] = o;
@@ -70,13 +82,21 @@ __device__ __forceinline__ void apply8(const u32x4& xv, const u32x4& rv, const f
 
 // Each lane handles two 16-byte vectors per iteration (ILP: both loads in flight before
 // the math). nvec < 2^31 is checked on the host, so indexing stays 32-bit.
-template <bool kAdd, bool kWriteSum, int kAct>
+//
+// kHoist: the grid stride (blocks * 256) is a multiple of C/8, so a lane's channel group
+// never changes across iterations - its 8 scales and 8 shifts are loaded once into
+// registers instead of 64 parameter bytes per 16 activation bytes re-read from L1 on
+// every iteration. Holds for every power-of-two C <= 2048 (all ResNet widths); other
+// widths (MobileNet's 96/144/...) take the per-vector path.
+template <bool kAdd, bool kWriteSum, int kAct, bool kHoist>
 __global__ void __launch_bounds__(256) bn_act_kernel(const u32x4* __restrict__ x, const u32x4* __restrict__ r,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, u32x4* __restrict__ y,
                                                      u32x4* __restrict__ sum, unsigned nvec, unsigned cvec) {
   const unsigned stride = gridDim.x * 256u;
   unsigned i = blockIdx.x * 256u + threadIdx.x;
+  Params8 ph;
+  if constexpr (kHoist) ph = load_params(scale, shift, (i % cvec) * 8u);
   for (; i + stride < nvec; i += 2 * stride) {
     const unsigned j = i + stride;
     u32x4 xa = __builtin_nontemporal_load(&x[i]);
@@ -87,8 +107,13 @@ __global__ void __launch_bounds__(256) bn_act_kernel(const u32x4* __restrict__ x
       rb = __builtin_nontemporal_load(&r[j]);
     }
     u32x4 ya, yb, sa, sb;
-    apply8<kAdd, kWriteSum, kAct>(xa, ra, scale, shift, (i % cvec) * 8u, &ya, &sa);
-    apply8<kAdd, kWriteSum, kAct>(xb, rb, scale, shift, (j % cvec) * 8u, &yb, &sb);
+    if constexpr (kHoist) {
+      apply8<kAdd, kWriteSum, kAct>(xa, ra, ph, &ya, &sa);
+      apply8<kAdd, kWriteSum, kAct>(xb, rb, ph, &yb, &sb);
+    } else {
+      apply8<kAdd, kWriteSum, kAct>(xa, ra, load_params(scale, shift, (i % cvec) * 8u), &ya, &sa);
+      apply8<kAdd, kWriteSum, kAct>(xb, rb, load_params(scale, shift, (j % cvec) * 8u), &yb, &sb);
+    }
     y[i] = ya;
     y[j] = yb;
     if constexpr (kWriteSum) {
@@ -101,7 +126,8 @@ __global__ void __launch_bounds__(256) bn_act_kernel(const u32x4* __restrict__ x
     u32x4 ra{};
     if constexpr (kAdd) ra = __builtin_nontemporal_load(&r[i]);
     u32x4 ya, sa;
-    apply8<kAdd, kWriteSum, kAct>(xa, ra, scale, shift, (i % cvec) * 8u, &ya, &sa);
+    if constexpr (kHoist) apply8<kAdd, kWriteSum, kAct>(xa, ra, ph, &ya, &sa);
+    else apply8<kAdd, kWriteSum, kAct>(xa, ra, load_params(scale, shift, (i % cvec) * 8u), &ya, &sa);
     y[i] = ya;
     if constexpr (kWriteSum) sum[i] = sa;
   }
@@ -115,9 +141,15 @@ void launch(const void* x, const void* r, const float* scale, const float* shift
   unsigned blocks = (nvec + 511u) / 512u;
   if (blocks > 256u * 16u) blocks = 256u * 16u;
   if (blocks < 1u) blocks = 1u;
-  hipLaunchKernelGGL((bn_act_kernel<kAdd, kWriteSum, kAct>), dim3(blocks), dim3(256), 0, stream,
-                     static_cast<const u32x4*>(x), static_cast<const u32x4*>(r), scale, shift,
-                     static_cast<u32x4*>(y), static_cast<u32x4*>(sum), nvec, cvec);
+  if (256u % cvec == 0u) {  // stride = blocks * 256 is then a multiple of cvec
+    hipLaunchKernelGGL((bn_act_kernel<kAdd, kWriteSum, kAct, true>), dim3(blocks), dim3(256), 0, stream,
+                       static_cast<const u32x4*>(x), static_cast<const u32x4*>(r), scale, shift,
+                       static_cast<u32x4*>(y), static_cast<u32x4*>(sum), nvec, cvec);
+  } else {
+    hipLaunchKernelGGL((bn_act_kernel<kAdd, kWriteSum, kAct, false>), dim3(blocks), dim3(256), 0, stream,
+                       static_cast<const u32x4*>(x), static_cast<const u32x4*>(r), scale, shift,
+                       static_cast<u32x4*>(y), static_cast<u32x4*>(sum), nvec, cvec);
+  }
 }
 
 template <int kAct>

@@ -40,7 +40,8 @@ def test_fused_graph_equals_original_fp32_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(2, 64, 17, 17), (3, 256, 9, 7), (1, 2048, 11, 11), (50, 64, 87, 87)])
+@pytest.mark.parametrize("shape", [(2, 64, 17, 17), (3, 256, 9, 7), (1, 2048, 11, 11), (50, 64, 87, 87),
+                                   (2, 96, 9, 9), (1, 8, 3, 5)])
 @pytest.mark.parametrize("mode", ["plain", "residual", "residual_sum"])
 @pytest.mark.parametrize("act", ["relu", "relu6", "none"])
 def test_bn_act_kernel_numerics(shape, mode, act):
