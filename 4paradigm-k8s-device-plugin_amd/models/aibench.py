@@ -296,52 +296,75 @@ class Runner:
             self.opt = torch.optim.SGD(model.parameters(), lr=1e-3, momentum=0.9)
         else:
             model.eval()
-            if fuse and isinstance(model, ResNetV2) and dtype == torch.bfloat16 and channels_last:
+            if fuse and isinstance(model, (ResNetV2, DeepLabV3Plus)) and dtype == torch.bfloat16 and channels_last:
                 # Inference epilogues fused into one HIP pass each (ops/fused.py); BN
                 # scale/shift are derived in fp32 before the weights are cast.
-                from ..ops.fused import fuse_resnet_v2
-                model = fuse_resnet_v2(model, impl="hip" if self.device.type == "cuda" else "torch")
+                from ..ops.fused import fuse_conv_bn_act, fuse_resnet_v2
+                impl = "hip" if self.device.type == "cuda" else "torch"
+                if isinstance(model, ResNetV2):
+                    model = fuse_resnet_v2(model, impl=impl)
+                else:
+                    model = fuse_conv_bn_act(model, impl=impl)
                 for m in model.modules():
-                    if isinstance(m, (nn.Conv2d, nn.Linear)):
+                    if isinstance(m, (nn.Conv2d, nn.Linear, nn.BatchNorm2d)):
                         m.to(dtype)
             else:
                 model = model.to(dtype)
             self.x = self.x.to(dtype)
             self.opt = None
-        self.fused = fuse and not case.train and isinstance(model, nn.Module) and type(model).__name__ == "FusedResNetV2"
+        self.fused = fuse and not case.train and (type(model).__name__ == "FusedResNetV2" or any(
+            type(m).__name__ == "ConvBNAct" for m in model.modules()))
         self.model = model
 
     def capture(self, warmup=3):
-        """Capture the inference forward into a HIP graph (torch.cuda.CUDAGraph); later
-        steps replay it with one launch. Warm-up runs on a side stream first so lazy
-        initialisation and autotuning happen outside the capture."""
-        if self.case.train or self.device.type != "cuda":
-            raise ValueError("graph capture is for inference on a GPU")
+        """Capture one step into a HIP graph (torch.cuda.CUDAGraph); later steps replay it
+        with a single launch. Inference captures the forward; training captures forward,
+        loss, backward and the optimizer step (the "whole network" pattern: gradients are
+        None at capture so every replay writes them afresh, autocast runs without its
+        weight cache). Warm-up runs on a side stream first so lazy initialisation, MIOpen
+        autotuning and optimizer-state creation happen outside the capture."""
+        if self.device.type != "cuda":
+            raise ValueError("graph capture needs a GPU")
+        if self.case.train and self.case.kind == "sequence":
+            # Measured on MI355X (ROCm 7.2, PyTorch 2.10): capturing the MIOpen RNN
+            # backward kills the process, so recurrent training always runs eagerly.
+            raise NotImplementedError("MIOpen RNN training is not HIP-graph capturable")
+        cur = torch.cuda.current_stream(self.device)
         s = torch.cuda.Stream(self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s), torch.inference_mode():
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
             for _ in range(warmup):
-                self.model(self.x)
-        torch.cuda.current_stream(self.device).wait_stream(s)
+                self._eager_step(cache=False)
+        cur.wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.inference_mode(), torch.cuda.graph(self.graph):
-            self.graph_out = self.model(self.x)
+        if self.case.train:
+            self.opt.zero_grad(set_to_none=True)
+            with torch.cuda.graph(self.graph):
+                self.graph_out = self._eager_step(cache=False, zero_grad=False)
+        else:
+            with torch.inference_mode(), torch.cuda.graph(self.graph):
+                self.graph_out = self.model(self.x)
         return self
+
+    def _eager_step(self, cache=True, zero_grad=True):
+        if not self.case.train:
+            with torch.inference_mode():
+                return self.model(self.x)
+        with torch.autocast(self.device.type, dtype=self.dtype, enabled=self.dtype != torch.float32,
+                            cache_enabled=cache):
+            out = self.model(self.x)
+            loss = F.cross_entropy(out.float(), self.y)
+        if zero_grad:
+            self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        self.opt.step()
+        return loss
 
     def step(self):
         if getattr(self, "graph", None) is not None:
             self.graph.replay()
             return self.graph_out
-        if not self.case.train:
-            with torch.inference_mode():
-                return self.model(self.x)
-        with torch.autocast(self.device.type, dtype=self.dtype, enabled=self.dtype != torch.float32):
-            out = self.model(self.x)
-            loss = F.cross_entropy(out.float(), self.y)
-        self.opt.zero_grad(set_to_none=True)
-        loss.backward()
-        self.opt.step()
-        return loss
+        return self._eager_step()
 
     @property
     def items_per_step(self):

@@ -1,7 +1,10 @@
 // Fused inference epilogues for the in-pod benchmark workloads (gfx950, bf16, NHWC).
 //
 //   y   = act(x * scale[c] + shift[c])                      (BN(eval) + ReLU)
-//   s   = x + r ;  y = act(s * scale[c] + shift[c])          (residual add + next BN + ReLU)
+//   s   = x + r ;  y = act(s * scale[c] + shift[c])          (residual add + next BN + ReLU;
+//                                                             pre-activation ResNet blocks)
+//   y   = act(x * scale[c] + shift[c] + r)                  (BN of the last conv + residual;
+//                                                             MobileNet-V2 / post-activation)
 //
 // In a pre-activation ResNet every block boundary is "add the shortcut, then the next
 // block's BN + ReLU", and every conv inside a block is followed by BN + ReLU. Eager
@@ -50,7 +53,8 @@ __device__ __forceinline__ Params8 load_params(const float* __restrict__ scale, 
   return p;
 }
 
-template <bool kAdd, bool kWriteSum, int kAct>
+// kAdd: 0 no residual, 1 residual added before the affine, 2 residual added after it.
+template <int kAdd, bool kWriteSum, int kAct>
 __device__ __forceinline__ void apply8(const u32x4& xv, const u32x4& rv, const Params8& p, u32x4* yv, u32x4* sv) {
   float v[8];
 #pragma unroll
@@ -58,7 +62,7 @@ __device__ __forceinline__ void apply8(const u32x4& xv, const u32x4& rv, const P
     v[2 * k] = bf_lo(xv[k]);
     v[2 * k + 1] = bf_hi(xv[k]);
   }
-  if constexpr (kAdd) {
+  if constexpr (kAdd == 1) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       v[2 * k] += bf_lo(rv[k]);
@@ -69,9 +73,18 @@ __device__ __forceinline__ void apply8(const u32x4& xv, const u32x4& rv, const P
       for (int k = 0; k < 4; k++) (*sv)[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
     }
   }
+  float post[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (kAdd == 2) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      post[2 * k] = bf_lo(rv[k]);
+      post[2 * k + 1] = bf_hi(rv[k]);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     float o = fmaf(v[j], p.sc[j], p.sh[j]);
+    if constexpr (kAdd == 2) o += post[j];
     if constexpr (kAct == 1) o = fmaxf(o, 0.0f);
     if constexpr (kAct == 2) o = fminf(fmaxf(o, 0.0f), 6.0f);
     v[j] = o;
@@ -88,7 +101,7 @@ __device__ __forceinline__ void apply8(const u32x4& xv, const u32x4& rv, const P
 // registers instead of 64 parameter bytes per 16 activation bytes re-read from L1 on
 // every iteration. Holds for every power-of-two C <= 2048 (all ResNet widths); other
 // widths (MobileNet's 96/144/...) take the per-vector path.
-template <bool kAdd, bool kWriteSum, int kAct, bool kHoist>
+template <int kAdd, bool kWriteSum, int kAct, bool kHoist>
 __global__ void __launch_bounds__(256) bn_act_kernel(const u32x4* __restrict__ x, const u32x4* __restrict__ r,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, u32x4* __restrict__ y,
@@ -133,7 +146,7 @@ __global__ void __launch_bounds__(256) bn_act_kernel(const u32x4* __restrict__ x
   }
 }
 
-template <bool kAdd, bool kWriteSum, int kAct>
+template <int kAdd, bool kWriteSum, int kAct>
 void launch(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum, unsigned nvec,
             unsigned cvec, hipStream_t stream) {
   // Enough waves to cover HBM latency on 256 CUs (>= 8 blocks/CU), capped so every
@@ -154,10 +167,11 @@ void launch(const void* x, const void* r, const float* scale, const float* shift
 
 template <int kAct>
 int dispatch(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum,
-             unsigned nvec, unsigned cvec, hipStream_t s) {
-  if (!r) launch<false, false, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
-  else if (!sum) launch<true, false, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
-  else launch<true, true, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
+             unsigned nvec, unsigned cvec, bool post, hipStream_t s) {
+  if (!r) launch<0, false, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
+  else if (post) launch<2, false, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
+  else if (!sum) launch<1, false, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
+  else launch<1, true, kAct>(x, r, scale, shift, y, sum, nvec, cvec, s);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -169,22 +183,34 @@ extern "C" {
 // r/sum may be null (no residual / do not materialise the sum). act: 0 none, 1 relu,
 // 2 relu6. Requirements (checked): channels % 8 == 0, 16-byte aligned pointers,
 // numel / 8 < 2^31. Returns 0 on success, -1 on bad arguments, -2 on launch failure.
-int vgpu_bn_act_bf16(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum,
-                     int64_t numel, int channels, int act, void* stream) {
+static int bn_act_impl(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum,
+                       int64_t numel, int channels, int act, bool post, void* stream) {
   if (!x || !y || !scale || !shift || channels <= 0 || channels % 8 || numel <= 0 || numel % channels) return -1;
   if (numel / 8 >= (int64_t)1 << 31) return -1;
   auto misaligned = [](const void* p) { return p && (reinterpret_cast<uintptr_t>(p) & 15u); };
   if (misaligned(x) || misaligned(r) || misaligned(y) || misaligned(sum) || misaligned(scale) || misaligned(shift))
     return -1;
-  if (sum && !r) return -1;
+  if (sum && (!r || post)) return -1;
+  if (post && !r) return -1;
   const unsigned nvec = (unsigned)(numel / 8), cvec = (unsigned)(channels / 8);
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (act) {
-    case 0: return dispatch<0>(x, r, scale, shift, y, sum, nvec, cvec, s);
-    case 1: return dispatch<1>(x, r, scale, shift, y, sum, nvec, cvec, s);
-    case 2: return dispatch<2>(x, r, scale, shift, y, sum, nvec, cvec, s);
+    case 0: return dispatch<0>(x, r, scale, shift, y, sum, nvec, cvec, post, s);
+    case 1: return dispatch<1>(x, r, scale, shift, y, sum, nvec, cvec, post, s);
+    case 2: return dispatch<2>(x, r, scale, shift, y, sum, nvec, cvec, post, s);
     default: return -1;
   }
+}
+
+int vgpu_bn_act_bf16(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum,
+                     int64_t numel, int channels, int act, void* stream) {
+  return bn_act_impl(x, r, scale, shift, y, sum, numel, channels, act, false, stream);
+}
+
+// y = act(x * scale[c] + shift[c] + r): the residual joins after the affine.
+int vgpu_bn_act_post_bf16(const void* x, const void* r, const float* scale, const float* shift, void* y,
+                          int64_t numel, int channels, int act, void* stream) {
+  return bn_act_impl(x, r, scale, shift, y, nullptr, numel, channels, act, true, stream);
 }
 
 }  // extern "C"

@@ -287,6 +287,16 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
     else
       VLOG_DEBUG("device %d: queue %p confined to %d CUs", dev, (void*)*queue, a.mask.count());
   }
+  // Task priority (reference CUDA_TASK_PRIORITY, only stored there) becomes the hardware
+  // queue priority: 0 = high (e.g. latency-critical inference next to batch jobs),
+  // 1 = normal (default), >= 2 = low. Read from the region so an operator can change it.
+  int prio = s.region.raw()->hdr.priority.load(std::memory_order_relaxed);
+  if (prio != 1) {
+    VGPU_REAL_HSA(hsa_amd_queue_set_priority);
+    hsa_amd_queue_priority_t qp = prio <= 0 ? HSA_AMD_QUEUE_PRIORITY_HIGH : HSA_AMD_QUEUE_PRIORITY_LOW;
+    if (real_hsa_amd_queue_set_priority && real_hsa_amd_queue_set_priority(*queue, qp) != HSA_STATUS_SUCCESS)
+      VLOG_WARN("device %d: cannot set queue priority %d", dev, (int)qp);
+  }
   charge_context_once(dev);
   return st;
 }

@@ -42,7 +42,7 @@ def test_fused_graph_equals_original_fp32_cpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", [(2, 64, 17, 17), (3, 256, 9, 7), (1, 2048, 11, 11), (50, 64, 87, 87),
                                    (2, 96, 9, 9), (1, 8, 3, 5)])
-@pytest.mark.parametrize("mode", ["plain", "residual", "residual_sum"])
+@pytest.mark.parametrize("mode", ["plain", "residual", "residual_sum", "residual_post"])
 @pytest.mark.parametrize("act", ["relu", "relu6", "none"])
 def test_bn_act_kernel_numerics(shape, mode, act):
     g = torch.Generator().manual_seed(2)
@@ -52,8 +52,9 @@ def test_bn_act_kernel_numerics(shape, mode, act):
     sc = (torch.rand(C, generator=g) + 0.5).cuda()
     sh = torch.randn(C, generator=g).cuda()
     res = r if mode != "plain" else None
-    out = bn_act(x, sc, sh, res, act, write_sum=(mode == "residual_sum"))
-    y_ref, s_ref = bn_act_reference(x, sc, sh, res, act)
+    post = mode == "residual_post"
+    out = bn_act(x, sc, sh, res, act, write_sum=(mode == "residual_sum"), post=post)
+    y_ref, s_ref = bn_act_reference(x, sc, sh, res, act, post=post)
     y = out[0] if mode == "residual_sum" else out
     # one bf16 rounding of the output (the sum is rounded once more before BN in the kernel)
     torch.testing.assert_close(y.float(), y_ref, rtol=2e-2, atol=2e-2)
@@ -78,3 +79,74 @@ def test_fused_resnet50_matches_eager_bf16():
         got = f(x.to(torch.bfloat16)).float()
     cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0)
     assert cos > 0.995, cos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["resnet50-train", "deeplab-inf", "lstm-inf"])
+def test_graph_capture_steps(case):
+    """Whole-step HIP-graph capture (forward, or forward+backward+SGD) replays correctly."""
+    from amdvgpu.models.aibench import Runner, get_case
+    r = Runner(get_case(case), "cuda:0", batch=2)
+    if r.x.dim() == 4:
+        r.x = r.x[..., :128, :128].contiguous(memory_format=torch.channels_last)
+    r.step()
+    r.capture()
+    assert r.graph is not None
+    if r.case.train:
+        p = next(r.model.parameters())
+        before = p.detach().clone()
+        losses = [float(r.step()) for _ in range(3)]
+        torch.cuda.synchronize()
+        assert all(torch.isfinite(torch.tensor(losses)))
+        assert not torch.equal(before, p.detach())  # the optimizer step is in the graph
+    else:
+        out = r.step()
+        torch.cuda.synchronize()
+        with torch.inference_mode():
+            ref = r.model(r.x)
+        torch.testing.assert_close(out.float(), ref.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_fused_deeplab_graph_equals_original_fp32_cpu():
+    import copy
+    from amdvgpu.models.aibench import DeepLabV3Plus
+    from amdvgpu.ops.fused import fuse_conv_bn_act
+    g = torch.Generator().manual_seed(4)
+    torch.manual_seed(4)
+    m = DeepLabV3Plus().eval()
+    _randomize_bn(m, g)
+    x = torch.randn(1, 3, 64, 64, generator=g)
+    with torch.no_grad():
+        ref = m(x)
+        got = fuse_conv_bn_act(copy.deepcopy(m), impl="torch")(x)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_fused_deeplab_matches_eager_bf16():
+    import copy
+    from amdvgpu.models.aibench import DeepLabV3Plus
+    from amdvgpu.ops.fused import fuse_conv_bn_act
+    torch.manual_seed(0)
+    g = torch.Generator().manual_seed(5)
+    m = DeepLabV3Plus().eval()
+    _randomize_bn(m, g)
+    m = m.to("cuda", memory_format=torch.channels_last)
+    x = torch.randn(2, 3, 256, 256, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    with torch.inference_mode():
+        ref = m(x)
+        f = fuse_conv_bn_act(copy.deepcopy(m), impl="hip")
+        for mod in f.modules():
+            if isinstance(mod, (nn.Conv2d, nn.Linear, nn.BatchNorm2d)):
+                mod.to(torch.bfloat16)
+        got = f(x.to(torch.bfloat16)).float()
+    cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0)
+    assert cos > 0.99, cos
+
+
+def test_recurrent_training_capture_is_refused():
+    from amdvgpu.models.aibench import Runner, get_case
+    r = Runner(get_case("lstm-train"), "cpu", batch=1, dtype=torch.float32)
+    r.device = torch.device("cuda", 0)  # only the policy check runs
+    with pytest.raises(NotImplementedError):
+        r.capture()

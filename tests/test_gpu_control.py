@@ -121,3 +121,41 @@ def test_validator_lists_and_authorises(tmp_path):
     allow.write_text("GPU-0000000000000000\n")
     bad = subprocess.run([exe, "--allowlist", str(allow)], capture_output=True, text=True, timeout=120)
     assert bad.returncode == 1 and "UNAUTHORIZED" in bad.stdout
+
+
+def test_task_priority_maps_to_queue_priority(tmp_region):
+    """Two saturating tenants on the same CUs: the high-priority one (VGPU_TASK_PRIORITY=0)
+    finishes its fixed work before the low-priority one (=2)."""
+    code = """
+import torch
+from amdvgpu.ops import spin
+spin(256 * 32, 50); torch.cuda.synchronize()
+go = os.environ["GO_FILE"]
+emit(ready=True)
+while not os.path.exists(go):
+    time.sleep(0.002)
+t0 = time.time()
+for i in range(400):
+    spin(256 * 32, 500)
+torch.cuda.synchronize()
+emit(t=time.time() - t0)
+"""
+    go = tmp_region + ".go"
+    procs = []
+    for prio in ("0", "2"):
+        c = vgpu_env(mem_limit=8 * GiB, shared_cache=tmp_region + prio, extra={"VGPU_TASK_PRIORITY": prio})
+        procs.append(spawn_child(code, c, extra_env={"GO_FILE": go}))
+    try:
+        for p in procs:
+            assert p.stdout.readline().startswith("RESULT")
+        open(go, "w").close()
+        outs = [p.communicate(timeout=300) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for f in (go, tmp_region + "0", tmp_region + "2"):
+            if os.path.exists(f):
+                os.unlink(f)
+    t_high, t_low = (child_results(o[0])[-1]["t"] for o in outs)
+    assert t_high < t_low, (t_high, t_low)
