@@ -220,6 +220,13 @@ class SysfsBackend(Backend):
 # ----------------------------------------------------------------------------- amdsmi
 
 
+def _handle_key(h):
+    """amdsmi processor handles are ctypes pointers; events carry a fresh wrapper object
+    for the same device, so compare the pointer value, not the Python object."""
+    v = getattr(h, "value", None)
+    return v if v is not None else id(h)
+
+
 class AmdSmiBackend(SysfsBackend):
     """sysfs inventory + amdsmi event notifications (reset / ring hang -> Unhealthy,
     post-reset -> Healthy; VM faults are application errors and are ignored, the
@@ -271,9 +278,9 @@ class AmdSmiBackend(SysfsBackend):
             got = smi.amdsmi_get_gpu_event_notification(0)
         except Exception:
             return events
-        by_handle = {id(h): u for u, h in self._handles.items()}
+        by_handle = {_handle_key(h): u for u, h in self._handles.items()}
         for ev in got or []:
-            uuid = by_handle.get(id(ev.get("processor_handle")))
+            uuid = by_handle.get(_handle_key(ev.get("processor_handle")))
             kind = str(ev.get("event", ""))
             if not uuid:
                 continue

@@ -22,10 +22,15 @@ int64_t limiter_delta(const LimiterSpec& spec, int limit_pct, int util_pct, int6
     int64_t num = std::max(limit_pct, util_pct / 2);
     share = std::max(floor, share * num / std::max(util_pct, 1));
   } else if (util_pct < limit_pct) {
-    // Multiplicative increase by the relative headroom (<= +50 %) plus one chip wave,
-    // so an idle or under-share tenant ramps up in a few periods.
-    int64_t grow = share * std::min(limit_pct - util_pct, 50) / 100 + floor;
-    share = std::min(ceil, share + grow);
+    // Proportional increase toward limit/util (at most 4x per period), so a saturating
+    // tenant reaches its share in a handful of 120 ms periods instead of ramping +50 %
+    // at a time; an idle tenant (util 0) grows 1.5x plus one wave.
+    if (util_pct > 0) {
+      int64_t num = std::min<int64_t>(limit_pct, 4 * (int64_t)util_pct);
+      share = std::min(ceil, std::max(share + floor, share * num / util_pct));
+    } else {
+      share = std::min(ceil, share + share / 2 + floor);
+    }
   }
   return share;
 }

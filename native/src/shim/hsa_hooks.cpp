@@ -296,6 +296,8 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
     hsa_amd_queue_priority_t qp = prio <= 0 ? HSA_AMD_QUEUE_PRIORITY_HIGH : HSA_AMD_QUEUE_PRIORITY_LOW;
     if (real_hsa_amd_queue_set_priority && real_hsa_amd_queue_set_priority(*queue, qp) != HSA_STATUS_SUCCESS)
       VLOG_WARN("device %d: cannot set queue priority %d", dev, (int)qp);
+    else
+      VLOG_INFO("device %d: queue %p priority %s", dev, (void*)*queue, prio <= 0 ? "high" : "low");
   }
   charge_context_once(dev);
   return st;
