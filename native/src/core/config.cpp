@@ -109,8 +109,45 @@ int apply_override_env_file(const char* path) {
   return n;
 }
 
-void load_config(Config* cfg, GetenvFn getenv_fn) {
-  if (!getenv_fn) getenv_fn = [](const char* k) -> const char* { return getenv(k); };
+namespace {
+// Pod specs written for the reference set some shim knobs by hand; those names are
+// accepted when the VGPU_* name is absent (the plugin itself only emits VGPU_* names).
+struct Alias {
+  const char* name;
+  const char* legacy;
+};
+const Alias kAliases[] = {
+    {"VGPU_DEVICE_MEMORY_LIMIT", "CUDA_DEVICE_MEMORY_LIMIT"},
+    {"VGPU_DEVICE_CU_LIMIT", "CUDA_DEVICE_SM_LIMIT"},
+    {"VGPU_SHARED_CACHE", "CUDA_DEVICE_MEMORY_SHARED_CACHE"},
+    {"VGPU_OVERSUBSCRIBE", "CUDA_OVERSUBSCRIBE"},
+    {"VGPU_TASK_PRIORITY", "CUDA_TASK_PRIORITY"},
+    {"VGPU_CU_POLICY", "GPU_CORE_UTILIZATION_POLICY"},
+    {"VGPU_ACTIVE_OOM_KILLER", "ACTIVE_OOM_KILLER"},
+    {"VGPU_MEMORY_OVERRIDE", "MEMORY_OVERRIDE"},
+};
+
+struct Env {
+  GetenvFn fn;
+  const char* operator()(const char* key) const {
+    if (const char* v = fn(key)) return v;
+    for (const Alias& a : kAliases)
+      if (!strcmp(key, a.name)) return fn(a.legacy);
+    // per-device memory limits: VGPU_DEVICE_MEMORY_LIMIT_<i> <- CUDA_DEVICE_MEMORY_LIMIT_<i>
+    static const char kMem[] = "VGPU_DEVICE_MEMORY_LIMIT_";
+    if (!strncmp(key, kMem, sizeof(kMem) - 1)) {
+      char legacy[128];
+      snprintf(legacy, sizeof(legacy), "CUDA_DEVICE_MEMORY_LIMIT_%.64s", key + sizeof(kMem) - 1);
+      return fn(legacy);
+    }
+    return nullptr;
+  }
+};
+}  // namespace
+
+void load_config(Config* cfg, GetenvFn raw_getenv) {
+  if (!raw_getenv) raw_getenv = [](const char* k) -> const char* { return getenv(k); };
+  const Env getenv_fn{raw_getenv};
   *cfg = Config();
   cfg->disabled = parse_bool(getenv_fn("VGPU_DISABLE"), false);
 

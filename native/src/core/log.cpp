@@ -13,6 +13,7 @@ int g_log_level = kWarn;
 
 void log_init_from_env() {
   const char* s = getenv("VGPU_LOG_LEVEL");
+  if (!s || !*s) s = getenv("LIBCUDA_LOG_LEVEL");  // reference name (README.md:224-234)
   if (s && *s) g_log_level = atoi(s);
 }
 

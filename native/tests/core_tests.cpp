@@ -120,6 +120,28 @@ static void test_config() {
   CHECK(c.cu_mode == CuMode::kSpatial);
 }
 
+static const char* legacy_env(const char* k) {
+  static const std::map<std::string, std::string> m = {
+      {"CUDA_DEVICE_MEMORY_LIMIT", "4g"}, {"CUDA_DEVICE_MEMORY_LIMIT_1", "2048m"},
+      {"CUDA_DEVICE_SM_LIMIT", "30"},     {"VGPU_DEVICE_MEMORY_LIMIT_2", "1g"},
+      {"CUDA_DEVICE_MEMORY_LIMIT_2", "9g"}, {"CUDA_TASK_PRIORITY", "0"},
+      {"GPU_CORE_UTILIZATION_POLICY", "FORCE"}, {"CUDA_OVERSUBSCRIBE", "true"}};
+  auto it = m.find(k);
+  return it == m.end() ? nullptr : it->second.c_str();
+}
+
+static void test_legacy_env_names() {
+  Config c;
+  load_config(&c, legacy_env);
+  CHECK_EQ(c.dev[0].mem_limit, 4ull << 30);
+  CHECK_EQ(c.dev[1].mem_limit, 2048ull << 20);
+  CHECK_EQ(c.dev[2].mem_limit, 1ull << 30);  // the VGPU_* name wins over the legacy one
+  CHECK_EQ(c.dev[0].cu_limit_pct, 30);
+  CHECK_EQ(c.priority, 0);
+  CHECK(c.cu_policy == CuPolicy::kForce);
+  CHECK(c.oversubscribe);
+}
+
 static void test_override_file() {
   std::string p = tmp_region("override");
   FILE* f = fopen(p.c_str(), "w");
@@ -513,6 +535,7 @@ int main(int argc, char** argv) {
       {"parse_size", test_parse_size},
       {"parse_range", test_parse_range},
       {"config", test_config},
+      {"legacy_env_names", test_legacy_env_names},
       {"override_file", test_override_file},
       {"region_basic", test_region_basic},
       {"region_kinds", test_region_unlimited_and_kinds},
