@@ -161,3 +161,29 @@ def test_mixed_partition_strategy(plugin_dir):
         assert len(k.wait_devices("amd.com/gpu")) == 2
     finally:
         shutdown(k, stop, th)
+
+
+def test_eight_gpu_node_advertises_32_vgpus(plugin_dir):
+    """BASELINE config 5 control-plane half: an 8xMI355X node (xGMI all-to-all, two NUMA
+    nodes) split 4-way advertises 32 vGPUs; 4-vGPU requests land on 4 distinct GPUs of one
+    NUMA node, 8 such pods exhaust the node without double-booking a vGPU."""
+    be = FakeBackend(n=8, topology="xgmi", numa_split=4)
+    cfg, k, sup, stop, th = start(plugin_dir, backend=be, device_split_count=4)
+    try:
+        k.wait_registered("amd.com/gpu")
+        devs = k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 32)
+        assert len(devs) == 32
+        numa = {d.uuid: d.numa_node for d in be.devices()}
+        seen = set()
+        for _ in range(8):
+            ids, resp = k.allocate("amd.com/gpu", 4)
+            assert not (set(ids) & seen)
+            seen |= set(ids)
+            gpus = {i.rsplit("-", 1)[0] for i in ids}
+            if len(gpus) == 4:
+                assert len({numa[g] for g in gpus}) == 1
+        assert len(seen) == 32
+        with pytest.raises(RuntimeError):
+            k.allocate("amd.com/gpu", 1)
+    finally:
+        shutdown(k, stop, th)
