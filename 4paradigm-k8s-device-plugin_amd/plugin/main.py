@@ -135,6 +135,10 @@ class Supervisor:
             except queue.Empty:
                 if stop_event is not None and stop_event.is_set():
                     return 0
+                fatal = [p.fatal for p in self.plugins if p.fatal]
+                if fatal:
+                    log.error("fatal: %s", fatal[0])
+                    return 1
                 continue
             if isinstance(ev, tuple) and ev[0] == "signal":
                 if ev[1] == signal.SIGHUP:

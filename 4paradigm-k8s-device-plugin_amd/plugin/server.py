@@ -31,6 +31,7 @@ log = logging.getLogger("amdvgpu.plugin")
 RESTART_BUDGET = 5          # gRPC server restarts allowed ...
 RESTART_WINDOW_S = 3600.0   # ... per hour (reference server.go:180-207)
 DIAL_TIMEOUT_S = 5.0
+WATCHDOG_PERIOD_S = 5.0
 
 
 class AllocationError(Exception):
@@ -55,7 +56,10 @@ class DevicePluginServer:
         self._stopped = threading.Event()
         self._server = None
         self._health_thread = None
+        self._watchdog_thread = None
         self._restarts = []
+        self.fatal = None            # set when the restart budget is exhausted
+        self.watchdog_period_s = WATCHDOG_PERIOD_S
         self.vdevices = []
         self.allocations = []  # (request ids, using ids) — observability / tests
 
@@ -83,6 +87,9 @@ class DevicePluginServer:
         self._health_thread = threading.Thread(target=self._health_loop, name=f"health-{self.resource_name}",
                                                daemon=True)
         self._health_thread.start()
+        self._watchdog_thread = threading.Thread(target=self._watchdog, name=f"watchdog-{self.resource_name}",
+                                                 daemon=True)
+        self._watchdog_thread.start()
 
     def stop(self):
         self._stopped.set()
@@ -127,6 +134,37 @@ class DevicePluginServer:
             self._server.stop(0)
             self._server = None
         self.serve()
+
+    def _serving(self):
+        if not os.path.exists(self.socket):
+            return False
+        ch = grpc.insecure_channel(api.unix_target(self.socket))
+        try:
+            grpc.channel_ready_future(ch).result(timeout=2.0)
+            return True
+        except grpc.FutureTimeoutError:
+            return False
+        finally:
+            ch.close()
+
+    def _watchdog(self):
+        """The Go server's crash-restart goroutine (server.go:180-207): if the socket
+        stops answering (deleted, server died), serve again and re-register, at most
+        RESTART_BUDGET times per hour; past that the plugin is marked fatal and the
+        supervisor exits (the DaemonSet restarts the pod, like log.Fatal)."""
+        while not self._stopped.wait(self.watchdog_period_s):
+            if self._serving():
+                continue
+            log.error("device plugin socket %s is not serving; restarting the gRPC server", self.socket)
+            try:
+                self.restart_server()
+                self.register()
+            except RuntimeError as e:
+                self.fatal = str(e)
+                log.error("%s", e)
+                return
+            except Exception as e:  # kubelet away: the supervisor's inotify loop handles it
+                log.warning("re-register after restart failed: %s", e)
 
     def options(self):
         return api.DevicePluginOptions(pre_start_required=False,

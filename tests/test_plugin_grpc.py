@@ -187,3 +187,24 @@ def test_eight_gpu_node_advertises_32_vgpus(plugin_dir):
             k.allocate("amd.com/gpu", 1)
     finally:
         shutdown(k, stop, th)
+
+
+def test_grpc_server_watchdog_restarts_and_budget(plugin_dir):
+    """Socket deleted under the plugin -> served again and re-registered; more than 5
+    restarts within the hour -> fatal, the supervisor exits (server.go:180-207)."""
+    cfg, k, sup, stop, th = start(plugin_dir)
+    try:
+        k.wait_registered("amd.com/gpu")
+        p = sup.plugins[0]
+        p.watchdog_period_s = 0.1
+        time.sleep(0.3)  # the watchdog thread picks up the shorter period after one tick
+        n0 = len(k.registrations)
+        os.unlink(p.socket)
+        k.wait_registered("amd.com/gpu", count=n0 + 1, timeout=15)
+        assert os.path.exists(p.socket)
+        p._restarts = [time.monotonic()] * 5  # budget already spent this hour
+        os.unlink(p.socket)
+        th.join(timeout=20)
+        assert not th.is_alive() and p.fatal
+    finally:
+        shutdown(k, stop, th)
