@@ -9,6 +9,7 @@ restructured graph with plain PyTorch ops (used on CPU and as the numerics refer
 otherwise.
 """
 import ctypes as C
+import os
 
 import torch
 import torch.nn as nn
@@ -31,6 +32,9 @@ def _ops():
         L.vgpu_bn_act_post_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_int64, C.c_int, C.c_int, C.c_void_p]
         L.vgpu_bn_act_post_bf16.restype = C.c_int
+        L.vgpu_conv1x1_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.vgpu_conv1x1_bf16.restype = C.c_int
         _lib = L
     return _lib
 
@@ -99,6 +103,81 @@ def bn_act(x, scale, shift, residual=None, act="relu", write_sum=False, post=Fal
     return (y, s) if write_sum else y
 
 
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def conv1x1_reference(x, w2d, scale=None, shift=None, residual=None, act="relu"):
+    """fp32 reference of the fused 1x1 conv: returns (y, sum or None) as NCHW views of
+    channels-last data. y = act((x . w^T [+ residual]) * scale + shift) per pixel; the
+    sum is x . w^T + residual."""
+    N, K, H, W = x.shape
+    acc = x.permute(0, 2, 3, 1).reshape(-1, K).float() @ w2d.float().t()
+    s = None
+    if residual is not None:
+        acc = acc + residual.permute(0, 2, 3, 1).reshape(acc.shape).float()
+        s = acc
+    y = acc if scale is None else _act_torch(acc * scale.float() + shift.float(), act)
+
+    def nchw(t):
+        return t.reshape(N, H, W, -1).permute(0, 3, 1, 2)
+
+    return nchw(y), (nchw(s) if s is not None else None)
+
+
+def conv1x1(x, w2d, scale=None, shift=None, residual=None, act="relu", write_sum=False):
+    """HIP MFMA 1x1 convolution (``conv1x1_mfma.hip``) with the epilogue fused:
+    y = act((x . w^T [+ residual]) * scale + shift), bf16 channels-last in and out,
+    fp32 accumulation. ``w2d`` is the [Cout, Cin] weight. With ``write_sum`` also
+    returns x . w^T + residual (the next block's identity shortcut)."""
+    if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 4:
+        raise TypeError("conv1x1 needs a 4-D bf16 CUDA tensor")
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv1x1 needs channels_last input")
+    N, K, H, W = x.shape
+    cout = w2d.shape[0]
+    if tuple(w2d.shape) != (cout, K) or w2d.dtype != torch.bfloat16 or not w2d.is_contiguous():
+        raise ValueError(f"weight must be a contiguous bf16 [{cout}, {K}] matrix")
+    if K % 64 or cout % 64:
+        raise ValueError(f"conv1x1 needs Cin and Cout multiples of 64 (got {K}, {cout})")
+    if (scale is None) != (shift is None) or (residual is not None and scale is None):
+        raise ValueError("residual epilogue needs scale and shift")
+    for v in (scale, shift):
+        if v is not None and (v.dtype != torch.float32 or v.numel() != cout or not v.is_contiguous()):
+            raise ValueError("scale/shift must be contiguous fp32 vectors of Cout")
+    y = torch.empty((N, cout, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    if residual is not None and (residual.shape != y.shape or residual.dtype != y.dtype or residual.stride() != y.stride()):
+        raise ValueError("residual must match the output in shape, dtype and layout")
+    if write_sum and residual is None:
+        raise ValueError("write_sum needs a residual")
+    s = torch.empty_like(y) if write_sum else None
+    epi = 0 if scale is None else 1 if residual is None else 3 if write_sum else 2
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    rc = _ops().vgpu_conv1x1_bf16(_ptr(x), _ptr(w2d), _ptr(scale), _ptr(shift), _ptr(residual), _ptr(y), _ptr(s),
+                                  N * H * W, cout, K, epi, ACT[act], C.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"vgpu_conv1x1_bf16 failed ({rc}) for x {tuple(x.shape)} w {tuple(w2d.shape)}")
+    return (y, s) if write_sum else y
+
+
+def is_pointwise(conv):
+    """A bias-free 1x1/stride-1 convolution whose channels the MFMA kernel tiles."""
+    return (isinstance(conv, nn.Conv2d) and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+            and conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
+
+
+def _time_us(fn, reps=3):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1000.0 / reps
+
+
 class FusedBNAct(nn.Module):
     """Frozen BN + activation (+ optional residual add)."""
 
@@ -125,11 +204,24 @@ class FusedResNetV2(nn.Module):
     Per block (pre-activation bottleneck): pre = act(bn1(x)) arrives precomputed;
     y = conv1(pre) -> [bn2+relu] -> conv2 -> [bn3+relu] -> conv3; the block boundary
     computes x' = y + shortcut and pre' = act(bn1'(x')) in one kernel (bn1' = next
-    block's bn1, or the final post_bn)."""
+    block's bn1, or the final post_bn).
 
-    def __init__(self, model, impl="hip"):
+    The 1x1 convs (conv1, conv3) can also take their epilogue inside the conv: the MFMA
+    kernel of :func:`conv1x1` computes conv1 + bn2 + ReLU, and conv3 + shortcut + next
+    BN + ReLU (+ the sum), so those outputs never round-trip through HBM before the
+    elementwise pass. ``conv1x1``: "on", "off" or "auto" (default, env
+    ``VGPU_CONV1X1``): per layer, the first forward times the fused kernel against
+    library conv + separate epilogue and keeps the faster (like MIOpen find mode).
+    """
+
+    def __init__(self, model, impl="hip", conv1x1=None):
         super().__init__()
         self.impl = impl
+        self.conv1x1_mode = conv1x1 or os.environ.get("VGPU_CONV1X1", "auto")
+        if self.conv1x1_mode not in ("on", "off", "auto"):
+            raise ValueError(f"conv1x1 mode must be on, off or auto (got {self.conv1x1_mode!r})")
+        self.plan = {}      # (block, conv, input shape) -> fused kernel chosen
+        self._wcache = {}   # conv id -> (weight data_ptr, dtype, [Cout, Cin] view)
         self.stem, self.pool, self.fc = model.stem, model.pool, model.fc
         blocks = list(model.blocks)
         self.convs = nn.ModuleList()
@@ -143,6 +235,35 @@ class FusedResNetV2(nn.Module):
         self.entry = FusedBNAct(blocks[0].bn1, "relu", impl)
         self.boundary = nn.ModuleList([FusedBNAct(blocks[i + 1].bn1, "relu", impl) for i in range(len(blocks) - 1)] +
                                       [FusedBNAct(model.post_bn, "relu", impl)])
+        self.pointwise = [(is_pointwise(b.conv1), is_pointwise(b.conv3)) for b in blocks]
+
+    def _w2d(self, conv):
+        w = conv.weight
+        hit = self._wcache.get(id(conv))
+        if hit is None or hit[0] != w.data_ptr() or hit[1] != w.dtype:
+            w2 = w.detach().reshape(w.shape[0], w.shape[1])
+            hit = (w.data_ptr(), w.dtype, w2 if w2.is_contiguous() else w2.contiguous())
+            self._wcache[id(conv)] = hit
+        return hit[2]
+
+    def _pw(self, x, conv, bn, residual=None, write_sum=False):
+        """conv (1x1) with bn's epilogue fused: the HIP MFMA kernel, or its fp32 torch
+        reference for impl="torch"."""
+        if self.impl == "hip":
+            return conv1x1(x, self._w2d(conv), bn.scale, bn.shift, residual, bn.act, write_sum)
+        y, s = conv1x1_reference(x, conv.weight.reshape(conv.out_channels, -1), bn.scale, bn.shift, residual, bn.act)
+        y = y.to(x.dtype)
+        return (y, s.to(x.dtype)) if write_sum else y
+
+    def _use_pw(self, key, fused, unfused):
+        if self.conv1x1_mode != "auto" or self.impl != "hip":
+            return self.conv1x1_mode == "on"
+        d = self.plan.get(key)
+        if d is None:
+            if torch.cuda.is_current_stream_capturing():
+                return True  # no timing inside a graph capture: take the kernel
+            d = self.plan[key] = _time_us(fused) <= _time_us(unfused)
+        return d
 
     def forward(self, x):
         x = self.pool(self.stem(x))
@@ -150,20 +271,30 @@ class FusedResNetV2(nn.Module):
         n = len(self.convs)
         for i in range(n):
             c1, c2, c3 = self.convs[i]
+            bn2, bn3 = self.mid[i]
+            bnd, last = self.boundary[i], i + 1 == n
             sc = self.shortcuts[i](pre) if self.has_sc[i] else x
-            y = self.mid[i][0](c1(pre))
-            y = self.mid[i][1](c2(y))
-            y = c3(y)
-            if i + 1 < n:
-                pre, x = self.boundary[i](y, residual=sc, write_sum=True)
+            p1, p3 = self.pointwise[i]
+            if p1 and self._use_pw((i, 1, tuple(pre.shape)), lambda: self._pw(pre, c1, bn2), lambda: bn2(c1(pre))):
+                y = self._pw(pre, c1, bn2)
             else:
-                pre = self.boundary[i](y, residual=sc)
+                y = bn2(c1(pre))
+            y = bn3(c2(y))
+            if p3 and self._use_pw((i, 3, tuple(y.shape)), lambda: self._pw(y, c3, bnd, sc, not last),
+                                   lambda: bnd(c3(y), residual=sc, write_sum=not last)):
+                out = self._pw(y, c3, bnd, sc, not last)
+            else:
+                out = bnd(c3(y), residual=sc, write_sum=not last)
+            if last:
+                pre = out
+            else:
+                pre, x = out
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(pre, 1), 1))
 
 
-def fuse_resnet_v2(model, impl="hip"):
+def fuse_resnet_v2(model, impl="hip", conv1x1=None):
     model.eval()
-    return FusedResNetV2(model, impl).eval()
+    return FusedResNetV2(model, impl, conv1x1).eval()
 
 
 class ConvBNAct(nn.Module):

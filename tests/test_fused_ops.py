@@ -5,7 +5,8 @@ import torch
 import torch.nn as nn
 
 from amdvgpu.models.aibench import ResNetV2, resnet_v2_50
-from amdvgpu.ops.fused import FusedResNetV2, bn_act, bn_act_reference, bn_scale_shift
+from amdvgpu.ops.fused import (FusedResNetV2, bn_act, bn_act_reference, bn_scale_shift, conv1x1,
+                                conv1x1_reference)
 
 
 def _randomize_bn(model, g):
@@ -26,7 +27,8 @@ def test_scale_shift_matches_bn_eval():
     torch.testing.assert_close(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1), bn(x), rtol=1e-5, atol=1e-5)
 
 
-def test_fused_graph_equals_original_fp32_cpu():
+@pytest.mark.parametrize("conv1x1_mode", ["off", "on"])
+def test_fused_graph_equals_original_fp32_cpu(conv1x1_mode):
     g = torch.Generator().manual_seed(1)
     torch.manual_seed(1)
     m = ResNetV2([1, 2, 1, 1], num_classes=10).eval()
@@ -35,8 +37,56 @@ def test_fused_graph_equals_original_fp32_cpu():
     m = m.to(memory_format=torch.channels_last)
     with torch.no_grad():
         ref = m(x)
-        got = FusedResNetV2(m, impl="torch")(x)
+        got = FusedResNetV2(m, impl="torch", conv1x1=conv1x1_mode)(x)
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_conv1x1_reference_matches_conv2d_cpu():
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 64, 5, 3, generator=g).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(128, 64, 1, 1, generator=g)
+    r = torch.randn(2, 128, 5, 3, generator=g)
+    sc, sh = torch.rand(128, generator=g) + 0.5, torch.randn(128, generator=g)
+    y, s = conv1x1_reference(x, w.view(128, 64), sc, sh, r, "relu")
+    conv = torch.nn.functional.conv2d(x, w)
+    torch.testing.assert_close(s, conv + r, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(y, torch.relu((conv + r) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)),
+                               rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nhw,k,n", [((2, 7, 9), 64, 64), ((1, 11, 11), 2048, 512), ((50, 22, 22), 256, 1024),
+                                      ((3, 5, 5), 128, 192), ((4, 16, 16), 512, 128), ((1, 1, 3), 64, 256)])
+@pytest.mark.parametrize("epi", ["plain", "bn_act", "residual", "residual_sum"])
+def test_conv1x1_kernel_numerics(nhw, k, n, epi):
+    """MFMA 1x1 conv + fused epilogue vs an fp32 PyTorch reference (odd M exercises the
+    row clamp, Cout 192 the 64-wide tile, K 2048 the multi-step K loop)."""
+    g = torch.Generator().manual_seed(11)
+    N, H, W = nhw
+    x = torch.randn(N, k, H, W, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(n, k, generator=g) / k ** 0.5).to("cuda", torch.bfloat16)
+    r = torch.randn(N, n, H, W, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    sc = (torch.rand(n, generator=g) + 0.5).cuda()
+    sh = torch.randn(n, generator=g).cuda()
+    kw = {}
+    if epi != "plain":
+        kw = dict(scale=sc, shift=sh)
+    if epi.startswith("residual"):
+        kw.update(residual=r, write_sum=epi == "residual_sum")
+    out = conv1x1(x, w, act="relu", **kw)
+    y_ref, s_ref = conv1x1_reference(x, w, kw.get("scale"), kw.get("shift"), kw.get("residual"), "relu")
+    y = out[0] if epi == "residual_sum" else out
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), y_ref, rtol=2e-2, atol=3e-2)
+    if epi == "residual_sum":
+        torch.testing.assert_close(out[1].float(), s_ref, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.gpu
+def test_conv1x1_rejects_unsupported_shapes():
+    x = torch.zeros(1, 96, 4, 4, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with pytest.raises(ValueError):
+        conv1x1(x, torch.zeros(64, 96, device="cuda", dtype=torch.bfloat16))
 
 
 @pytest.mark.gpu
@@ -63,7 +113,8 @@ def test_bn_act_kernel_numerics(shape, mode, act):
 
 
 @pytest.mark.gpu
-def test_fused_resnet50_matches_eager_bf16():
+@pytest.mark.parametrize("conv1x1_mode", ["off", "on", "auto"])
+def test_fused_resnet50_matches_eager_bf16(conv1x1_mode):
     torch.manual_seed(0)
     g = torch.Generator().manual_seed(3)
     m = resnet_v2_50().eval()
@@ -72,7 +123,7 @@ def test_fused_resnet50_matches_eager_bf16():
     x = torch.randn(4, 3, 224, 224, generator=g).cuda().contiguous(memory_format=torch.channels_last)
     with torch.inference_mode():
         ref = m(x)  # fp32 eager
-        f = FusedResNetV2(m, impl="hip")
+        f = FusedResNetV2(m, impl="hip", conv1x1=conv1x1_mode)
         for mod in f.modules():
             if isinstance(mod, (nn.Conv2d, nn.Linear)):
                 mod.to(torch.bfloat16)
