@@ -1,8 +1,12 @@
-"""Fused BN(eval)+activation (+ residual add) for inference, backed by the gfx950 kernel in
-``native/src/kernels/fused_bn_act.hip`` (``libvgpu_ops.so``).
+"""Fused inference ops for the benchmark models, backed by the gfx950 kernels in
+``libvgpu_ops.so``: BN(eval)+activation (+ residual add) in one pass
+(``native/src/kernels/fused_bn_act.hip``), and MFMA convolutions over channels-last
+activations with those epilogues applied to the accumulator tile
+(``native/src/kernels/conv_nhwc_mfma.hip``).
 
-``bn_act`` is the op; ``fuse_resnet_v2`` rewrites a ``models.aibench.ResNetV2`` for
-inference so that every "BN + ReLU" and every "shortcut add + next BN + ReLU" is one pass
+``bn_act`` / ``conv_nhwc`` are the ops; ``fuse_resnet_v2`` rewrites a
+``models.aibench.ResNetV2`` for inference so that every "BN + ReLU" and every "shortcut
+add + next BN + ReLU" is fused into the conv that produces its input, or else one pass
 over the activation instead of 3-5 eager kernels. ``impl="torch"`` runs the same
 restructured graph with plain PyTorch ops (used on CPU and as the numerics reference);
 ``impl="hip"`` requires the native library and a CUDA (ROCm) device and fails loudly
@@ -35,6 +39,8 @@ def _ops():
         L.vgpu_conv1x1_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.vgpu_conv1x1_bf16.restype = C.c_int
+        L.vgpu_conv_nhwc_bf16.argtypes = [C.c_void_p] * 7 + [C.c_int] * 11 + [C.c_void_p]
+        L.vgpu_conv_nhwc_bf16.restype = C.c_int
         _lib = L
     return _lib
 
@@ -126,7 +132,7 @@ def conv1x1_reference(x, w2d, scale=None, shift=None, residual=None, act="relu")
 
 
 def conv1x1(x, w2d, scale=None, shift=None, residual=None, act="relu", write_sum=False):
-    """HIP MFMA 1x1 convolution (``conv1x1_mfma.hip``) with the epilogue fused:
+    """HIP MFMA 1x1 convolution (``conv_nhwc_mfma.hip``) with the epilogue fused:
     y = act((x . w^T [+ residual]) * scale + shift), bf16 channels-last in and out,
     fp32 accumulation. ``w2d`` is the [Cout, Cin] weight. With ``write_sum`` also
     returns x . w^T + residual (the next block's identity shortcut)."""
@@ -158,6 +164,87 @@ def conv1x1(x, w2d, scale=None, shift=None, residual=None, act="relu", write_sum
     if rc != 0:
         raise RuntimeError(f"vgpu_conv1x1_bf16 failed ({rc}) for x {tuple(x.shape)} w {tuple(w2d.shape)}")
     return (y, s) if write_sum else y
+
+
+def conv_weight_2d(w):
+    """[Cout, KH*KW*Cin] view of a conv weight in (kh, kw, c) order, the K order of the
+    implicit GEMM (a view when the weight is channels_last, else a copy)."""
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()
+
+
+def conv_reference(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, act="relu", post=False):
+    """fp32 reference of :func:`conv_nhwc`: returns (y, sum or None)."""
+    acc = F.conv2d(x.float(), w.float(), stride=stride, padding=padding)
+    shape = [1, -1, 1, 1]
+    s = None
+    if residual is not None and not post:
+        acc = acc + residual.float()
+        s = acc
+    if scale is None:
+        return acc, s
+    y = acc * scale.float().view(shape) + shift.float().view(shape)
+    if post:
+        y = y + residual.float()
+    return _act_torch(y, act), s
+
+
+def conv_nhwc(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, act="relu", write_sum=False,
+              post=False, w2d=None):
+    """HIP MFMA convolution (``conv_nhwc_mfma.hip``: implicit GEMM over channels-last
+    activations) with the epilogue fused: y = act((conv(x, w) [+ residual]) * scale +
+    shift), or with ``post`` act(conv * scale + shift + residual). ``w`` is the 4-D conv
+    weight (``w2d``: its cached :func:`conv_weight_2d`). Cin and Cout must be multiples
+    of 64; padding symmetric and smaller than the kernel."""
+    if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 4:
+        raise TypeError("conv_nhwc needs a 4-D bf16 CUDA tensor")
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv_nhwc needs channels_last input")
+    N, Cin, H, W = x.shape
+    cout, cin_w, kh, kw = w.shape
+    if cin_w != Cin or w.dtype != torch.bfloat16:
+        raise ValueError(f"weight {tuple(w.shape)} does not match input channels {Cin}")
+    if Cin % 64 or cout % 64:
+        raise ValueError(f"conv_nhwc needs Cin and Cout multiples of 64 (got {Cin}, {cout})")
+    if not (0 <= padding < min(kh, kw)) or stride < 1:
+        raise ValueError("unsupported stride/padding")
+    w2d = conv_weight_2d(w) if w2d is None else w2d
+    if tuple(w2d.shape) != (cout, kh * kw * Cin) or not w2d.is_contiguous():
+        raise ValueError("w2d must be the contiguous [Cout, KH*KW*Cin] weight")
+    if (scale is None) != (shift is None) or (residual is not None and scale is None):
+        raise ValueError("residual epilogue needs scale and shift")
+    for v in (scale, shift):
+        if v is not None and (v.dtype != torch.float32 or v.numel() != cout or not v.is_contiguous()):
+            raise ValueError("scale/shift must be contiguous fp32 vectors of Cout")
+    oh, ow = (H + 2 * padding - kh) // stride + 1, (W + 2 * padding - kw) // stride + 1
+    y = torch.empty((N, cout, oh, ow), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    if residual is not None and (residual.shape != y.shape or residual.dtype != y.dtype or residual.stride() != y.stride()):
+        raise ValueError("residual must match the output in shape, dtype and layout")
+    if write_sum and (residual is None or post):
+        raise ValueError("write_sum needs a pre-BN residual")
+    s = torch.empty_like(y) if write_sum else None
+    if scale is None:
+        epi = 0
+    elif residual is None:
+        epi = 1
+    else:
+        epi = 4 if post else 3 if write_sum else 2
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    rc = _ops().vgpu_conv_nhwc_bf16(_ptr(x), _ptr(w2d), _ptr(scale), _ptr(shift), _ptr(residual), _ptr(y), _ptr(s),
+                                    N, H, W, Cin, cout, kh, kw, stride, padding, epi, ACT[act], C.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"vgpu_conv_nhwc_bf16 failed ({rc}) for x {tuple(x.shape)} w {tuple(w.shape)}")
+    return (y, s) if write_sum else y
+
+
+def is_mfma_conv(conv):
+    """A bias-free dense convolution the MFMA kernel tiles: channels multiples of 64,
+    square stride and symmetric padding smaller than the kernel, no dilation."""
+    if not isinstance(conv, nn.Conv2d) or conv.groups != 1 or conv.bias is not None or conv.dilation != (1, 1):
+        return False
+    if conv.in_channels % 64 or conv.out_channels % 64 or not isinstance(conv.padding, tuple):
+        return False
+    (sh, sw), (ph, pw), (kh, kw) = conv.stride, conv.padding, conv.kernel_size
+    return sh == sw and ph == pw and ph < min(kh, kw)
 
 
 def is_pointwise(conv):
@@ -206,22 +293,23 @@ class FusedResNetV2(nn.Module):
     computes x' = y + shortcut and pre' = act(bn1'(x')) in one kernel (bn1' = next
     block's bn1, or the final post_bn).
 
-    The 1x1 convs (conv1, conv3) can also take their epilogue inside the conv: the MFMA
-    kernel of :func:`conv1x1` computes conv1 + bn2 + ReLU, and conv3 + shortcut + next
-    BN + ReLU (+ the sum), so those outputs never round-trip through HBM before the
-    elementwise pass. ``conv1x1``: "on", "off" or "auto" (default, env
-    ``VGPU_CONV1X1``): per layer, the first forward times the fused kernel against
-    library conv + separate epilogue and keeps the faster (like MIOpen find mode).
+    Every conv can also take its epilogue inside the conv: the MFMA kernel of
+    :func:`conv_nhwc` computes conv1 + bn2 + ReLU, conv2 (3x3, implicit GEMM) + bn3 +
+    ReLU, the strided shortcut, and conv3 + shortcut + next BN + ReLU (+ the sum), so no
+    conv output round-trips through HBM before its elementwise pass. ``mfma_conv``:
+    "on", "off" or "auto" (default, env ``VGPU_MFMA_CONV``): per layer, the first forward
+    times the fused kernel against library conv + separate epilogue and keeps the faster
+    (like MIOpen find mode).
     """
 
-    def __init__(self, model, impl="hip", conv1x1=None):
+    def __init__(self, model, impl="hip", mfma_conv=None):
         super().__init__()
         self.impl = impl
-        self.conv1x1_mode = conv1x1 or os.environ.get("VGPU_CONV1X1", "auto")
-        if self.conv1x1_mode not in ("on", "off", "auto"):
-            raise ValueError(f"conv1x1 mode must be on, off or auto (got {self.conv1x1_mode!r})")
+        self.mfma_mode = mfma_conv or os.environ.get("VGPU_MFMA_CONV", os.environ.get("VGPU_CONV1X1", "auto"))
+        if self.mfma_mode not in ("on", "off", "auto"):
+            raise ValueError(f"mfma_conv mode must be on, off or auto (got {self.mfma_mode!r})")
         self.plan = {}      # (block, conv, input shape) -> fused kernel chosen
-        self._wcache = {}   # conv id -> (weight data_ptr, dtype, [Cout, Cin] view)
+        self._wcache = {}   # conv id -> (weight data_ptr, dtype, [Cout, KH*KW*Cin] matrix)
         self.stem, self.pool, self.fc = model.stem, model.pool, model.fc
         blocks = list(model.blocks)
         self.convs = nn.ModuleList()
@@ -235,29 +323,31 @@ class FusedResNetV2(nn.Module):
         self.entry = FusedBNAct(blocks[0].bn1, "relu", impl)
         self.boundary = nn.ModuleList([FusedBNAct(blocks[i + 1].bn1, "relu", impl) for i in range(len(blocks) - 1)] +
                                       [FusedBNAct(model.post_bn, "relu", impl)])
-        self.pointwise = [(is_pointwise(b.conv1), is_pointwise(b.conv3)) for b in blocks]
+        self.eligible = [(is_mfma_conv(b.conv1), is_mfma_conv(b.conv2), is_mfma_conv(b.conv3),
+                          b.shortcut is not None and is_mfma_conv(b.shortcut)) for b in blocks]
 
     def _w2d(self, conv):
         w = conv.weight
         hit = self._wcache.get(id(conv))
         if hit is None or hit[0] != w.data_ptr() or hit[1] != w.dtype:
-            w2 = w.detach().reshape(w.shape[0], w.shape[1])
-            hit = (w.data_ptr(), w.dtype, w2 if w2.is_contiguous() else w2.contiguous())
+            hit = (w.data_ptr(), w.dtype, conv_weight_2d(w.detach()))
             self._wcache[id(conv)] = hit
         return hit[2]
 
-    def _pw(self, x, conv, bn, residual=None, write_sum=False):
-        """conv (1x1) with bn's epilogue fused: the HIP MFMA kernel, or its fp32 torch
+    def _conv(self, x, conv, bn=None, residual=None, write_sum=False):
+        """conv with bn's epilogue fused: the HIP MFMA kernel, or its fp32 torch
         reference for impl="torch"."""
+        st, pad = conv.stride[0], conv.padding[0]
+        sc, sh, act = (bn.scale, bn.shift, bn.act) if bn is not None else (None, None, "none")
         if self.impl == "hip":
-            return conv1x1(x, self._w2d(conv), bn.scale, bn.shift, residual, bn.act, write_sum)
-        y, s = conv1x1_reference(x, conv.weight.reshape(conv.out_channels, -1), bn.scale, bn.shift, residual, bn.act)
-        y = y.to(x.dtype)
-        return (y, s.to(x.dtype)) if write_sum else y
+            return conv_nhwc(x, conv.weight, st, pad, sc, sh, residual, act, write_sum, w2d=self._w2d(conv))
+        y, s = conv_reference(x, conv.weight, st, pad, sc, sh, residual, act)
+        y = y.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        return (y, s.to(x.dtype).contiguous(memory_format=torch.channels_last)) if write_sum else y
 
-    def _use_pw(self, key, fused, unfused):
-        if self.conv1x1_mode != "auto" or self.impl != "hip":
-            return self.conv1x1_mode == "on"
+    def _use(self, key, fused, unfused):
+        if self.mfma_mode != "auto" or self.impl != "hip":
+            return self.mfma_mode == "on"
         d = self.plan.get(key)
         if d is None:
             if torch.cuda.is_current_stream_capturing():
@@ -273,16 +363,25 @@ class FusedResNetV2(nn.Module):
             c1, c2, c3 = self.convs[i]
             bn2, bn3 = self.mid[i]
             bnd, last = self.boundary[i], i + 1 == n
-            sc = self.shortcuts[i](pre) if self.has_sc[i] else x
-            p1, p3 = self.pointwise[i]
-            if p1 and self._use_pw((i, 1, tuple(pre.shape)), lambda: self._pw(pre, c1, bn2), lambda: bn2(c1(pre))):
-                y = self._pw(pre, c1, bn2)
+            e1, e2, e3, esc = self.eligible[i]
+            if not self.has_sc[i]:
+                sc = x
+            elif esc and self._use((i, 0, tuple(pre.shape)), lambda: self._conv(pre, self.shortcuts[i]),
+                                   lambda: self.shortcuts[i](pre)):
+                sc = self._conv(pre, self.shortcuts[i])
+            else:
+                sc = self.shortcuts[i](pre)
+            if e1 and self._use((i, 1, tuple(pre.shape)), lambda: self._conv(pre, c1, bn2), lambda: bn2(c1(pre))):
+                y = self._conv(pre, c1, bn2)
             else:
                 y = bn2(c1(pre))
-            y = bn3(c2(y))
-            if p3 and self._use_pw((i, 3, tuple(y.shape)), lambda: self._pw(y, c3, bnd, sc, not last),
-                                   lambda: bnd(c3(y), residual=sc, write_sum=not last)):
-                out = self._pw(y, c3, bnd, sc, not last)
+            if e2 and self._use((i, 2, tuple(y.shape)), lambda: self._conv(y, c2, bn3), lambda: bn3(c2(y))):
+                y = self._conv(y, c2, bn3)
+            else:
+                y = bn3(c2(y))
+            if e3 and self._use((i, 3, tuple(y.shape)), lambda: self._conv(y, c3, bnd, sc, not last),
+                                lambda: bnd(c3(y), residual=sc, write_sum=not last)):
+                out = self._conv(y, c3, bnd, sc, not last)
             else:
                 out = bnd(c3(y), residual=sc, write_sum=not last)
             if last:
@@ -292,9 +391,9 @@ class FusedResNetV2(nn.Module):
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(pre, 1), 1))
 
 
-def fuse_resnet_v2(model, impl="hip", conv1x1=None):
+def fuse_resnet_v2(model, impl="hip", mfma_conv=None):
     model.eval()
-    return FusedResNetV2(model, impl, conv1x1).eval()
+    return FusedResNetV2(model, impl, mfma_conv).eval()
 
 
 class ConvBNAct(nn.Module):

@@ -1,19 +1,26 @@
-// 1x1 convolution on gfx950 matrix cores with the benchmark models' inference epilogues
-// fused into the output pass (bf16 NHWC in/out, fp32 accumulate).
+// NHWC convolution on gfx950 matrix cores with the benchmark models' inference epilogues
+// fused into the output pass (bf16 in/out, fp32 accumulate).
 //
-// A 1x1 convolution over a channels-last activation is a GEMM: X[M = N*H*W, K = Cin]
-// times W[Cout, K]^T. In the pre-activation ResNet every such conv is followed by an
-// elementwise pass over its output:
+// Over a channels-last activation a convolution is a GEMM: Y[M = N*OH*OW, Cout] =
+// im2col(X)[M, K = KH*KW*Cin] . W[Cout, K]^T, with the weight in its channels-last layout
+// [Cout][KH][KW][Cin]. A 1x1/stride-1 conv needs no im2col at all (X itself is the
+// [M, Cin] operand); every other shape (3x3, strided 1x1 shortcuts) gathers its A tile
+// implicitly: a 64-wide K-tile always lies inside one (kh, kw) tap because Cin % 64 == 0,
+// so each staged row is one contiguous 128-B piece of one input pixel, or zeros for the
+// padding. In the pre-activation ResNet every conv is followed by an elementwise pass:
 //
-//   conv1 -> BN + ReLU                          y = act(acc * s[n] + t[n])          (epi 1)
+//   conv1, conv2 -> BN + ReLU                   y = act(acc * s[n] + t[n])          (epi 1)
 //   conv3 -> + shortcut -> next BN + ReLU       x = acc + r ; y = act(x * s + t)    (epi 2)
 //                                               (+ x itself for the next identity
 //                                                shortcut)                           (epi 3)
+//   MobileNet projection (+ residual after BN)  y = act(acc * s + t + r)            (epi 4)
+//   shortcut conv                               y = acc                             (epi 0)
 //
 // Run separately (library conv + fused_bn_act.hip) the epilogue re-reads the conv output
 // from HBM and writes it again; here it is applied while the accumulator tile is still
 // on chip, so the conv output never makes the round trip (profiles/r1g: the epilogue
-// passes were 33 % of the ResNet-V2-50 inference step).
+// passes were 33 % of the ResNet-V2-50 inference step; profiles/r1n: the 1x1 layers alone
+// went 1.15-1.65x faster).
 //
 // Kernel shape (CDNA4-first, not a CUDA warp tiling):
 //   * 256 threads = 4 wave64s; block tile 128 (M) x BN (64 or 128), K-step 64.
@@ -21,7 +28,9 @@
 //     FM x FN 16x16 accumulators. Both operands are K-contiguous, so one lane's
 //     fragment (8 consecutive k of one row) is a single 16-byte LDS read.
 //   * Global -> registers -> LDS staging, double-buffered: the next K-tile's loads are in
-//     flight while the current one feeds the MFMAs; one barrier per K-step.
+//     flight while the current one feeds the MFMAs; one barrier per K-step. Padding rows
+//     load from a valid address and are zeroed after the load (a select, not a branch
+//     around the load, so the loads stay in flight together).
 //   * LDS rows are 128 B (64 bf16); the 16-B chunk index is XOR-swizzled with
 //     (row >> 1) & 7 so the 16 lanes of a ds_read_b128 phase hit 16 distinct 16-B slots
 //     of the 256-B bank row (conflict-free), for reads and for the staging writes.
@@ -32,9 +41,9 @@
 //     block id is remapped (bijectively) such that the N-tiles of one M-tile run on the
 //     same XCD and share its L2 copy of the activation rows.
 //
-// Requirements (checked on the host): K % 64 == 0, Cout % 64 == 0, 16-byte aligned
-// pointers, M*K and M*Cout below 2^34 elements. Rows past M are clamped on load (they
-// read a valid row) and never stored.
+// Requirements (checked on the host): Cin % 64 == 0, Cout % 64 == 0, 16-byte aligned
+// pointers, input/output/weight element counts below 2^34. Rows past M are clamped on
+// load (they read a valid row) and never stored.
 //
 // C ABI (ctypes): pointers are device pointers, `stream` a hipStream_t.
 #include <hip/hip_bf16.h>
@@ -51,6 +60,19 @@ using bf16x8 = __bf16 __attribute__((ext_vector_type(8)));
 constexpr int kBM = 128;
 constexpr int kBK = 64;
 constexpr int kThreads = 256;
+
+struct ConvArgs {
+  const u32x4* x;
+  const u32x4* w;
+  const float* scale;
+  const float* shift;
+  const u32x4* r;
+  u32x4* y;
+  u32x4* s;
+  unsigned M, N, K;                             // GEMM: M = Nb*OH*OW, N = Cout, K = KH*KW*C
+  unsigned H, W, C, OH, OW, KW, stride, pad;    // geometry (implicit-GEMM path)
+  unsigned tiles_n, ntiles;
+};
 
 __device__ __forceinline__ unsigned swz(unsigned row, unsigned chunk) { return chunk ^ ((row >> 1) & 7u); }
 
@@ -78,14 +100,10 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned ntiles) {
 }
 
 // kEpi: 0 plain (y = acc), 1 y = act(acc*s+t), 2 x = acc + r; y = act(x*s+t),
-//       3 as 2 and also writes x (bf16) to `sum`.
-template <int BN, int WM, int WN, int kEpi, int kAct>
-__global__ void __launch_bounds__(kThreads) conv1x1_kernel(const u32x4* __restrict__ A, const u32x4* __restrict__ W,
-                                                          const float* __restrict__ scale,
-                                                          const float* __restrict__ shift,
-                                                          const u32x4* __restrict__ R, u32x4* __restrict__ Y,
-                                                          u32x4* __restrict__ S, unsigned M, unsigned N, unsigned K,
-                                                          unsigned tiles_n, unsigned ntiles) {
+//       3 as 2 and also writes x (bf16) to `s`, 4 y = act(acc*s + t + r).
+// kIm2col: false = 1x1/stride-1 (A is X itself), true = implicit GEMM gather.
+template <int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col>
+__global__ void __launch_bounds__(kThreads) conv_kernel(const ConvArgs p) {
   static_assert(WM * WN == kThreads / 64, "4 waves");
   constexpr int FM = kBM / WM / 16;
   constexpr int FN = BN / WN / 16;
@@ -99,24 +117,37 @@ __global__ void __launch_bounds__(kThreads) conv1x1_kernel(const u32x4* __restri
   constexpr int kWLoads = BN * 8 / kThreads;
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLds];
 
+  const unsigned M = p.M, N = p.N, K = p.K;
   const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const unsigned tile = xcd_remap(blockIdx.x, ntiles);
-  const unsigned m0 = (tile / tiles_n) * kBM, n0 = (tile % tiles_n) * BN;
-  const size_t kvec = K >> 3;  // row stride of A and W in 16-B chunks
+  const unsigned tile = xcd_remap(blockIdx.x, p.ntiles);
+  const unsigned m0 = (tile / p.tiles_n) * kBM, n0 = (tile % p.tiles_n) * BN;
+  const size_t kvec = K >> 3;  // row stride of W (and of A on the 1x1 path) in 16-B chunks
 
   // Buffer b of each operand (computed, not a pointer table: a table of LDS addresses
   // would be a static initializer, which the AMDGPU backend cannot emit).
   auto a_lds = [&](int b) { return reinterpret_cast<u32x4*>(smem + b * kAStage); };
   auto w_lds = [&](int b) { return reinterpret_cast<u32x4*>(smem + 2 * kAStage + b * kWStage); };
 
-  // Per-thread staging sources (row, chunk) are fixed across K-tiles; only the k offset moves.
+  // Per-thread staging sources (row, chunk) are fixed across K-tiles; only k moves.
   const u32x4* a_src[kALoads];
+  int a_ih0[kALoads], a_iw0[kALoads];
   unsigned a_dst[kALoads];
+  const size_t cvec = p.C >> 3;  // input pixel stride in 16-B chunks (im2col path)
 #pragma unroll
   for (int i = 0; i < kALoads; i++) {
     const unsigned c = tid + i * kThreads, r = c >> 3, ch = c & 7u;
     const unsigned gm = (m0 + r < M) ? m0 + r : M - 1u;
-    a_src[i] = A + (size_t)gm * kvec + ch;
+    if constexpr (kIm2col) {
+      const unsigned plane = p.OH * p.OW;
+      const unsigned img = gm / plane, rem = gm - img * plane;
+      const unsigned oh = rem / p.OW, ow = rem - oh * p.OW;
+      a_src[i] = p.x + (size_t)img * p.H * p.W * cvec + ch;
+      a_ih0[i] = (int)(oh * p.stride) - (int)p.pad;
+      a_iw0[i] = (int)(ow * p.stride) - (int)p.pad;
+    } else {
+      a_src[i] = p.x + (size_t)gm * kvec + ch;
+      a_ih0[i] = a_iw0[i] = 0;
+    }
     a_dst[i] = r * 8u + swz(r, ch);
   }
   const u32x4* w_src[kWLoads];
@@ -124,15 +155,29 @@ __global__ void __launch_bounds__(kThreads) conv1x1_kernel(const u32x4* __restri
 #pragma unroll
   for (int i = 0; i < kWLoads; i++) {
     const unsigned c = tid + i * kThreads, r = c >> 3, ch = c & 7u;
-    w_src[i] = W + (size_t)(n0 + r) * kvec + ch;
+    w_src[i] = p.w + (size_t)(n0 + r) * kvec + ch;
     w_dst[i] = r * 8u + swz(r, ch);
   }
 
   u32x4 ra[kALoads], rw[kWLoads];
   auto load_tile = [&](unsigned kt) {
     const size_t off = (size_t)kt * (kBK / 8);
+    if constexpr (kIm2col) {
+      // Wave-uniform tap of this K-tile: k0 = ((kh * KW) + kw) * C + c0.
+      const unsigned k0 = kt * kBK, tap = k0 / p.C, c0v = (k0 - tap * p.C) >> 3;
+      const int kh = (int)(tap / p.KW), kw = (int)(tap - (unsigned)kh * p.KW);
 #pragma unroll
-    for (int i = 0; i < kALoads; i++) ra[i] = a_src[i][off];
+      for (int i = 0; i < kALoads; i++) {
+        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+        const bool ok = (unsigned)ih < p.H && (unsigned)iw < p.W;
+        const size_t pix = ok ? (size_t)ih * p.W + (unsigned)iw : 0;
+        const u32x4 v = a_src[i][pix * cvec + c0v];
+        ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kALoads; i++) ra[i] = a_src[i][off];
+    }
 #pragma unroll
     for (int i = 0; i < kWLoads; i++) rw[i] = w_src[i][off];
   };
@@ -206,67 +251,75 @@ __global__ void __launch_bounds__(kThreads) conv1x1_kernel(const u32x4* __restri
     float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
     const unsigned n = n0 + cc * 8u;
     const size_t o = (size_t)gm * nvec + (n >> 3);
+    float rr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (kEpi >= 2) {
-      const u32x4 rv = __builtin_nontemporal_load(&R[o]);
+      const u32x4 rv = __builtin_nontemporal_load(&p.r[o]);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        v[2 * k] += bf_lo(rv[k]);
-        v[2 * k + 1] += bf_hi(rv[k]);
+        rr[2 * k] = bf_lo(rv[k]);
+        rr[2 * k + 1] = bf_hi(rv[k]);
       }
+    }
+    if constexpr (kEpi == 2 || kEpi == 3) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[k] += rr[k];
       if constexpr (kEpi == 3) {
         u32x4 sv;
 #pragma unroll
         for (int k = 0; k < 4; k++) sv[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
-        S[o] = sv;
+        p.s[o] = sv;
       }
     }
     if constexpr (kEpi >= 1) {
-      const float4 s0 = *reinterpret_cast<const float4*>(scale + n);
-      const float4 s1 = *reinterpret_cast<const float4*>(scale + n + 4);
-      const float4 t0 = *reinterpret_cast<const float4*>(shift + n);
-      const float4 t1 = *reinterpret_cast<const float4*>(shift + n + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(p.scale + n);
+      const float4 s1 = *reinterpret_cast<const float4*>(p.scale + n + 4);
+      const float4 t0 = *reinterpret_cast<const float4*>(p.shift + n);
+      const float4 t1 = *reinterpret_cast<const float4*>(p.shift + n + 4);
       const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
       const float sh[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
 #pragma unroll
-      for (int k = 0; k < 8; k++) v[k] = act<kAct>(fmaf(v[k], sc[k], sh[k]));
+      for (int k = 0; k < 8; k++) {
+        float o_ = fmaf(v[k], sc[k], sh[k]);
+        if constexpr (kEpi == 4) o_ += rr[k];
+        v[k] = act<kAct>(o_);
+      }
     }
     u32x4 yv;
 #pragma unroll
     for (int k = 0; k < 4; k++) yv[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
-    Y[o] = yv;
+    p.y[o] = yv;
   }
 }
 
 template <int BN, int WM, int WN, int kEpi, int kAct>
-int launch(const void* a, const void* w, const float* scale, const float* shift, const void* r, void* y, void* s,
-           unsigned M, unsigned N, unsigned K, hipStream_t stream) {
-  const unsigned tiles_m = (M + kBM - 1) / kBM, tiles_n = N / BN, ntiles = tiles_m * tiles_n;
-  hipLaunchKernelGGL((conv1x1_kernel<BN, WM, WN, kEpi, kAct>), dim3(ntiles), dim3(kThreads), 0, stream,
-                     static_cast<const u32x4*>(a), static_cast<const u32x4*>(w), scale, shift,
-                     static_cast<const u32x4*>(r), static_cast<u32x4*>(y), static_cast<u32x4*>(s), M, N, K, tiles_n,
-                     ntiles);
+int launch(ConvArgs a, bool im2col, hipStream_t stream) {
+  a.tiles_n = a.N / BN;
+  a.ntiles = (a.M + kBM - 1) / kBM * a.tiles_n;
+  if (im2col)
+    hipLaunchKernelGGL((conv_kernel<BN, WM, WN, kEpi, kAct, true>), dim3(a.ntiles), dim3(kThreads), 0, stream, a);
+  else
+    hipLaunchKernelGGL((conv_kernel<BN, WM, WN, kEpi, kAct, false>), dim3(a.ntiles), dim3(kThreads), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 template <int BN, int WM, int WN, int kAct>
-int by_epi(int epi, const void* a, const void* w, const float* scale, const float* shift, const void* r, void* y,
-           void* s, unsigned M, unsigned N, unsigned K, hipStream_t st) {
+int by_epi(int epi, const ConvArgs& a, bool im2col, hipStream_t st) {
   switch (epi) {
-    case 0: return launch<BN, WM, WN, 0, 0>(a, w, scale, shift, r, y, s, M, N, K, st);
-    case 1: return launch<BN, WM, WN, 1, kAct>(a, w, scale, shift, r, y, s, M, N, K, st);
-    case 2: return launch<BN, WM, WN, 2, kAct>(a, w, scale, shift, r, y, s, M, N, K, st);
-    case 3: return launch<BN, WM, WN, 3, kAct>(a, w, scale, shift, r, y, s, M, N, K, st);
+    case 0: return launch<BN, WM, WN, 0, 0>(a, im2col, st);
+    case 1: return launch<BN, WM, WN, 1, kAct>(a, im2col, st);
+    case 2: return launch<BN, WM, WN, 2, kAct>(a, im2col, st);
+    case 3: return launch<BN, WM, WN, 3, kAct>(a, im2col, st);
+    case 4: return launch<BN, WM, WN, 4, kAct>(a, im2col, st);
     default: return -1;
   }
 }
 
 template <int BN, int WM, int WN>
-int by_act(int act, int epi, const void* a, const void* w, const float* scale, const float* shift, const void* r,
-           void* y, void* s, unsigned M, unsigned N, unsigned K, hipStream_t st) {
+int by_act(int act, int epi, const ConvArgs& a, bool im2col, hipStream_t st) {
   switch (act) {
-    case 0: return by_epi<BN, WM, WN, 0>(epi, a, w, scale, shift, r, y, s, M, N, K, st);
-    case 1: return by_epi<BN, WM, WN, 1>(epi, a, w, scale, shift, r, y, s, M, N, K, st);
-    case 2: return by_epi<BN, WM, WN, 2>(epi, a, w, scale, shift, r, y, s, M, N, K, st);
+    case 0: return by_epi<BN, WM, WN, 0>(epi, a, im2col, st);
+    case 1: return by_epi<BN, WM, WN, 1>(epi, a, im2col, st);
+    case 2: return by_epi<BN, WM, WN, 2>(epi, a, im2col, st);
     default: return -1;
   }
 }
@@ -275,27 +328,60 @@ int by_act(int act, int epi, const void* a, const void* w, const float* scale, c
 
 extern "C" {
 
-// y[M, N] = epilogue(x[M, K] . w[N, K]^T), bf16 row-major (NHWC activations, [Cout, Cin]
-// weights), fp32 accumulation. epi: 0 plain, 1 act(acc*scale+shift), 2 act((acc+r)*scale
-// + shift), 3 as 2 and sum = acc + r. act: 0 none, 1 relu, 2 relu6. scale/shift: fp32[N].
+// y[Nb, OH, OW, Cout] = epilogue(conv(x[Nb, H, W, C], w[Cout, KH, KW, C])), bf16 NHWC,
+// fp32 accumulation, OH = (H + 2 pad - KH) / stride + 1 (same for OW). epi: 0 plain,
+// 1 act(acc*scale+shift), 2 act((acc+r)*scale+shift), 3 as 2 and sum = acc + r,
+// 4 act(acc*scale + shift + r). act: 0 none, 1 relu, 2 relu6. scale/shift: fp32[Cout].
 // Returns 0 on success, -1 on bad arguments, -2 on launch failure.
-int vgpu_conv1x1_bf16(const void* x, const void* w, const float* scale, const float* shift, const void* r, void* y,
-                      void* sum, int64_t M, int N, int K, int epi, int act, void* stream) {
-  if (!x || !w || !y || M <= 0 || N <= 0 || K <= 0 || N % 64 || K % kBK) return -1;
-  if (epi < 0 || epi > 3 || act < 0 || act > 2) return -1;
+int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const float* shift, const void* r, void* y,
+                        void* sum, int nb, int h, int wd, int c, int cout, int kh, int kw, int stride, int pad, int epi,
+                        int act, void* stream) {
+  if (!x || !w || !y || nb <= 0 || h <= 0 || wd <= 0 || c <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
+      pad < 0 || pad >= kh || pad >= kw)
+    return -1;
+  if (c % kBK || cout % 64) return -1;
+  if (epi < 0 || epi > 4 || act < 0 || act > 2) return -1;
   if (epi >= 1 && (!scale || !shift)) return -1;
   if (epi >= 2 && !r) return -1;
-  if (epi == 3 && !sum) return -1;
-  if (M >= ((int64_t)1 << 32) || M * (int64_t)K >= ((int64_t)1 << 34) || M * (int64_t)N >= ((int64_t)1 << 34))
-    return -1;
-  auto misaligned = [](const void* p) { return p && (reinterpret_cast<uintptr_t>(p) & 15u); };
+  if ((epi == 3) != (sum != nullptr)) return -1;
+  const int64_t oh = ((int64_t)h + 2 * pad - kh) / stride + 1, ow = ((int64_t)wd + 2 * pad - kw) / stride + 1;
+  if (oh <= 0 || ow <= 0 || h + 2 * pad < kh || wd + 2 * pad < kw) return -1;
+  const int64_t m = (int64_t)nb * oh * ow, k = (int64_t)kh * kw * c, lim = (int64_t)1 << 34;
+  if (m >= ((int64_t)1 << 32) || (int64_t)nb * h * wd * c >= lim || m * cout >= lim || k * cout >= lim) return -1;
+  auto misaligned = [](const void* q) { return q && (reinterpret_cast<uintptr_t>(q) & 15u); };
   if (misaligned(x) || misaligned(w) || misaligned(y) || misaligned(r) || misaligned(sum) || misaligned(scale) ||
       misaligned(shift))
     return -1;
+  ConvArgs a{};
+  a.x = static_cast<const u32x4*>(x);
+  a.w = static_cast<const u32x4*>(w);
+  a.scale = scale;
+  a.shift = shift;
+  a.r = static_cast<const u32x4*>(r);
+  a.y = static_cast<u32x4*>(y);
+  a.s = static_cast<u32x4*>(sum);
+  a.M = (unsigned)m;
+  a.N = (unsigned)cout;
+  a.K = (unsigned)k;
+  a.H = (unsigned)h;
+  a.W = (unsigned)wd;
+  a.C = (unsigned)c;
+  a.OH = (unsigned)oh;
+  a.OW = (unsigned)ow;
+  a.KW = (unsigned)kw;
+  a.stride = (unsigned)stride;
+  a.pad = (unsigned)pad;
+  const bool im2col = !(kh == 1 && kw == 1 && stride == 1 && pad == 0);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const unsigned m = (unsigned)M, n = (unsigned)N, k = (unsigned)K;
-  if (N % 128 == 0) return by_act<128, 2, 2>(act, epi, x, w, scale, shift, r, y, sum, m, n, k, st);
-  return by_act<64, 4, 1>(act, epi, x, w, scale, shift, r, y, sum, m, n, k, st);
+  if (cout % 128 == 0) return by_act<128, 2, 2>(act, epi, a, im2col, st);
+  return by_act<64, 4, 1>(act, epi, a, im2col, st);
+}
+
+// 1x1 / stride-1 convolution over M pixels: y[M, N] = epilogue(x[M, K] . w[N, K]^T).
+int vgpu_conv1x1_bf16(const void* x, const void* w, const float* scale, const float* shift, const void* r, void* y,
+                      void* sum, int64_t M, int N, int K, int epi, int act, void* stream) {
+  if (M <= 0 || M >= ((int64_t)1 << 31)) return -1;
+  return vgpu_conv_nhwc_bf16(x, w, scale, shift, r, y, sum, (int)M, 1, 1, K, N, 1, 1, 1, 0, epi, act, stream);
 }
 
 }  // extern "C"

@@ -6,7 +6,7 @@ import torch.nn as nn
 
 from amdvgpu.models.aibench import ResNetV2, resnet_v2_50
 from amdvgpu.ops.fused import (FusedResNetV2, bn_act, bn_act_reference, bn_scale_shift, conv1x1,
-                                conv1x1_reference)
+                                conv1x1_reference, conv_nhwc, conv_reference)
 
 
 def _randomize_bn(model, g):
@@ -27,8 +27,8 @@ def test_scale_shift_matches_bn_eval():
     torch.testing.assert_close(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1), bn(x), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("conv1x1_mode", ["off", "on"])
-def test_fused_graph_equals_original_fp32_cpu(conv1x1_mode):
+@pytest.mark.parametrize("mfma_mode", ["off", "on"])
+def test_fused_graph_equals_original_fp32_cpu(mfma_mode):
     g = torch.Generator().manual_seed(1)
     torch.manual_seed(1)
     m = ResNetV2([1, 2, 1, 1], num_classes=10).eval()
@@ -37,7 +37,7 @@ def test_fused_graph_equals_original_fp32_cpu(conv1x1_mode):
     m = m.to(memory_format=torch.channels_last)
     with torch.no_grad():
         ref = m(x)
-        got = FusedResNetV2(m, impl="torch", conv1x1=conv1x1_mode)(x)
+        got = FusedResNetV2(m, impl="torch", mfma_conv=mfma_mode)(x)
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
 
 
@@ -82,6 +82,52 @@ def test_conv1x1_kernel_numerics(nhw, k, n, epi):
         torch.testing.assert_close(out[1].float(), s_ref, rtol=2e-2, atol=3e-2)
 
 
+def test_conv_reference_epilogues_cpu():
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(2, 64, 9, 7, generator=g)
+    w = torch.randn(64, 64, 3, 3, generator=g)
+    r = torch.randn(2, 64, 5, 4, generator=g)
+    sc, sh = torch.rand(64, generator=g) + 0.5, torch.randn(64, generator=g)
+    conv = torch.nn.functional.conv2d(x, w, stride=2, padding=1)
+    v = lambda t: t.view(1, -1, 1, 1)  # noqa: E731
+    y, s = conv_reference(x, w, 2, 1, sc, sh, r, "relu")
+    torch.testing.assert_close(s, conv + r)
+    torch.testing.assert_close(y, torch.relu((conv + r) * v(sc) + v(sh)))
+    y, s = conv_reference(x, w, 2, 1, sc, sh, r, "relu6", post=True)
+    assert s is None
+    torch.testing.assert_close(y, torch.nn.functional.relu6(conv * v(sc) + v(sh) + r))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("geom", [(2, 64, 9, 11, 64, 3, 1, 1), (3, 128, 22, 22, 128, 3, 2, 1), (1, 64, 5, 5, 192, 3, 1, 1),
+                                  (2, 256, 44, 44, 512, 1, 2, 0), (50, 64, 22, 22, 64, 3, 1, 1),
+                                  (1, 64, 3, 2, 64, 3, 1, 1), (2, 128, 7, 7, 128, 3, 1, 0)])
+@pytest.mark.parametrize("epi", ["plain", "bn_act", "residual_sum", "post"])
+def test_conv_nhwc_kernel_numerics(geom, epi):
+    """Implicit-GEMM MFMA conv (3x3 pad 1, strided 1x1, valid 3x3, tiny images where most
+    taps hit padding) + fused epilogue vs an fp32 PyTorch reference."""
+    N, cin, H, W, cout, k, stride, pad = geom
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(N, cin, H, W, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to("cuda", torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    oh, ow = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    r = torch.randn(N, cout, oh, ow, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    sc = (torch.rand(cout, generator=g) + 0.5).cuda()
+    sh = torch.randn(cout, generator=g).cuda()
+    kw = {} if epi == "plain" else dict(scale=sc, shift=sh)
+    if epi in ("residual_sum", "post"):
+        kw.update(residual=r, write_sum=epi == "residual_sum", post=epi == "post")
+    out = conv_nhwc(x, w, stride, pad, act="relu", **kw)
+    y_ref, s_ref = conv_reference(x, w, stride, pad, kw.get("scale"), kw.get("shift"), kw.get("residual"), "relu",
+                                  post=epi == "post")
+    y = out[0] if epi == "residual_sum" else out
+    assert y.shape == y_ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), y_ref, rtol=2e-2, atol=3e-2)
+    if epi == "residual_sum":
+        torch.testing.assert_close(out[1].float(), s_ref, rtol=2e-2, atol=3e-2)
+
+
 @pytest.mark.gpu
 def test_conv1x1_rejects_unsupported_shapes():
     x = torch.zeros(1, 96, 4, 4, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -113,8 +159,8 @@ def test_bn_act_kernel_numerics(shape, mode, act):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("conv1x1_mode", ["off", "on", "auto"])
-def test_fused_resnet50_matches_eager_bf16(conv1x1_mode):
+@pytest.mark.parametrize("mfma_mode", ["off", "on", "auto"])
+def test_fused_resnet50_matches_eager_bf16(mfma_mode):
     torch.manual_seed(0)
     g = torch.Generator().manual_seed(3)
     m = resnet_v2_50().eval()
@@ -123,7 +169,7 @@ def test_fused_resnet50_matches_eager_bf16(conv1x1_mode):
     x = torch.randn(4, 3, 224, 224, generator=g).cuda().contiguous(memory_format=torch.channels_last)
     with torch.inference_mode():
         ref = m(x)  # fp32 eager
-        f = FusedResNetV2(m, impl="hip", conv1x1=conv1x1_mode)
+        f = FusedResNetV2(m, impl="hip", mfma_conv=mfma_mode)
         for mod in f.modules():
             if isinstance(mod, (nn.Conv2d, nn.Linear)):
                 mod.to(torch.bfloat16)
