@@ -47,7 +47,7 @@ if __name__ == "__main__":
     ap.add_argument("-o", "--out", default=None)
     ap.add_argument("--after-last", default=None, help="only dispatches after the last kernel matching this")
     a = ap.parse_args()
-    paths = [p for g in a.db for p in glob.glob(g)]
+    paths = [p for g in a.db for p in glob.glob(g, recursive=True)]
     text = "\n".join(summarize(p, a.top, a.title, a.after_last) for p in paths)
     if a.out:
         open(a.out, "w").write(text)
