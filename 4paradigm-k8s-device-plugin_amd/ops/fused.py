@@ -254,7 +254,8 @@ def is_pointwise(conv):
             and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
 
 
-def _time_us(fn, reps=3):
+def _time_us(fn, reps=5):
+    fn()
     fn()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()

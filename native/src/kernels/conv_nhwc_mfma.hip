@@ -61,17 +61,24 @@ constexpr int kBM = 128;
 constexpr int kBK = 64;
 constexpr int kThreads = 256;
 
-struct ConvArgs {
-  const u32x4* x;
-  const u32x4* w;
-  const float* scale;
-  const float* shift;
-  const u32x4* r;
-  u32x4* y;
-  u32x4* s;
+// Shape of one launch. The tensors travel as separate __restrict__ kernel arguments:
+// pointers inside a by-value struct lose `noalias`, and a build that passed them that
+// way ran the stage-1 conv3 (+ residual + sum epilogue) in 175 us instead of 139 us.
+struct ConvGeom {
   unsigned M, N, K;                             // GEMM: M = Nb*OH*OW, N = Cout, K = KH*KW*C
   unsigned H, W, C, OH, OW, KW, stride, pad;    // geometry (implicit-GEMM path)
   unsigned tiles_n, ntiles;
+};
+
+struct ConvArgs {
+  const void* x;
+  const void* w;
+  const float* scale;
+  const float* shift;
+  const void* r;
+  void* y;
+  void* s;
+  ConvGeom g;
 };
 
 __device__ __forceinline__ unsigned swz(unsigned row, unsigned chunk) { return chunk ^ ((row >> 1) & 7u); }
@@ -103,7 +110,10 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned ntiles) {
 //       3 as 2 and also writes x (bf16) to `s`, 4 y = act(acc*s + t + r).
 // kIm2col: false = 1x1/stride-1 (A is X itself), true = implicit GEMM gather.
 template <int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col>
-__global__ void __launch_bounds__(kThreads) conv_kernel(const ConvArgs p) {
+__global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict__ X, const u32x4* __restrict__ Wt,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       const u32x4* __restrict__ R, u32x4* __restrict__ Y,
+                                                       u32x4* __restrict__ S, const ConvGeom p) {
   static_assert(WM * WN == kThreads / 64, "4 waves");
   constexpr int FM = kBM / WM / 16;
   constexpr int FN = BN / WN / 16;
@@ -141,11 +151,11 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const ConvArgs p) {
       const unsigned plane = p.OH * p.OW;
       const unsigned img = gm / plane, rem = gm - img * plane;
       const unsigned oh = rem / p.OW, ow = rem - oh * p.OW;
-      a_src[i] = p.x + (size_t)img * p.H * p.W * cvec + ch;
+      a_src[i] = X + (size_t)img * p.H * p.W * cvec + ch;
       a_ih0[i] = (int)(oh * p.stride) - (int)p.pad;
       a_iw0[i] = (int)(ow * p.stride) - (int)p.pad;
     } else {
-      a_src[i] = p.x + (size_t)gm * kvec + ch;
+      a_src[i] = X + (size_t)gm * kvec + ch;
       a_ih0[i] = a_iw0[i] = 0;
     }
     a_dst[i] = r * 8u + swz(r, ch);
@@ -155,7 +165,7 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const ConvArgs p) {
 #pragma unroll
   for (int i = 0; i < kWLoads; i++) {
     const unsigned c = tid + i * kThreads, r = c >> 3, ch = c & 7u;
-    w_src[i] = p.w + (size_t)(n0 + r) * kvec + ch;
+    w_src[i] = Wt + (size_t)(n0 + r) * kvec + ch;
     w_dst[i] = r * 8u + swz(r, ch);
   }
 
@@ -253,7 +263,7 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const ConvArgs p) {
     const size_t o = (size_t)gm * nvec + (n >> 3);
     float rr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (kEpi >= 2) {
-      const u32x4 rv = __builtin_nontemporal_load(&p.r[o]);
+      const u32x4 rv = __builtin_nontemporal_load(&R[o]);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         rr[2 * k] = bf_lo(rv[k]);
@@ -267,14 +277,14 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const ConvArgs p) {
         u32x4 sv;
 #pragma unroll
         for (int k = 0; k < 4; k++) sv[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
-        p.s[o] = sv;
+        S[o] = sv;
       }
     }
     if constexpr (kEpi >= 1) {
-      const float4 s0 = *reinterpret_cast<const float4*>(p.scale + n);
-      const float4 s1 = *reinterpret_cast<const float4*>(p.scale + n + 4);
-      const float4 t0 = *reinterpret_cast<const float4*>(p.shift + n);
-      const float4 t1 = *reinterpret_cast<const float4*>(p.shift + n + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(scale + n);
+      const float4 s1 = *reinterpret_cast<const float4*>(scale + n + 4);
+      const float4 t0 = *reinterpret_cast<const float4*>(shift + n);
+      const float4 t1 = *reinterpret_cast<const float4*>(shift + n + 4);
       const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
       const float sh[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
 #pragma unroll
@@ -287,18 +297,19 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const ConvArgs p) {
     u32x4 yv;
 #pragma unroll
     for (int k = 0; k < 4; k++) yv[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
-    p.y[o] = yv;
+    Y[o] = yv;
   }
 }
 
 template <int BN, int WM, int WN, int kEpi, int kAct>
 int launch(ConvArgs a, bool im2col, hipStream_t stream) {
-  a.tiles_n = a.N / BN;
-  a.ntiles = (a.M + kBM - 1) / kBM * a.tiles_n;
-  if (im2col)
-    hipLaunchKernelGGL((conv_kernel<BN, WM, WN, kEpi, kAct, true>), dim3(a.ntiles), dim3(kThreads), 0, stream, a);
-  else
-    hipLaunchKernelGGL((conv_kernel<BN, WM, WN, kEpi, kAct, false>), dim3(a.ntiles), dim3(kThreads), 0, stream, a);
+  ConvGeom g = a.g;
+  g.tiles_n = g.N / BN;
+  g.ntiles = (g.M + kBM - 1) / kBM * g.tiles_n;
+  auto kern = im2col ? conv_kernel<BN, WM, WN, kEpi, kAct, true> : conv_kernel<BN, WM, WN, kEpi, kAct, false>;
+  hipLaunchKernelGGL(kern, dim3(g.ntiles), dim3(kThreads), 0, stream, static_cast<const u32x4*>(a.x),
+                     static_cast<const u32x4*>(a.w), a.scale, a.shift, static_cast<const u32x4*>(a.r),
+                     static_cast<u32x4*>(a.y), static_cast<u32x4*>(a.s), g);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -353,24 +364,24 @@ int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const 
       misaligned(shift))
     return -1;
   ConvArgs a{};
-  a.x = static_cast<const u32x4*>(x);
-  a.w = static_cast<const u32x4*>(w);
+  a.x = x;
+  a.w = w;
   a.scale = scale;
   a.shift = shift;
-  a.r = static_cast<const u32x4*>(r);
-  a.y = static_cast<u32x4*>(y);
-  a.s = static_cast<u32x4*>(sum);
-  a.M = (unsigned)m;
-  a.N = (unsigned)cout;
-  a.K = (unsigned)k;
-  a.H = (unsigned)h;
-  a.W = (unsigned)wd;
-  a.C = (unsigned)c;
-  a.OH = (unsigned)oh;
-  a.OW = (unsigned)ow;
-  a.KW = (unsigned)kw;
-  a.stride = (unsigned)stride;
-  a.pad = (unsigned)pad;
+  a.r = r;
+  a.y = y;
+  a.s = sum;
+  a.g.M = (unsigned)m;
+  a.g.N = (unsigned)cout;
+  a.g.K = (unsigned)k;
+  a.g.H = (unsigned)h;
+  a.g.W = (unsigned)wd;
+  a.g.C = (unsigned)c;
+  a.g.OH = (unsigned)oh;
+  a.g.OW = (unsigned)ow;
+  a.g.KW = (unsigned)kw;
+  a.g.stride = (unsigned)stride;
+  a.g.pad = (unsigned)pad;
   const bool im2col = !(kh == 1 && kw == 1 && stride == 1 && pad == 0);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (cout % 128 == 0) return by_act<128, 2, 2>(act, epi, a, im2col, st);

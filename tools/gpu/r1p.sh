@@ -1,7 +1,7 @@
 set -o pipefail
-# r1o: implicit-GEMM MFMA conv (3x3, strided shortcuts) with fused epilogues: numerics,
+# r1p: implicit-GEMM MFMA conv (3x3, strided shortcuts) with fused epilogues: numerics,
 # per-layer A/B against MIOpen/CK + epilogue, headline bench A/B, kernel-trace profile.
-OUT=gpurun_out/r1o; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=gpurun_out/r1p; mkdir -p $OUT; export TMPDIR=/tmp
 make -C native -j16 > $OUT/build.log 2>&1 || exit 1
 echo "conv tests"
 timeout -k 10 600 python -u -m pytest tests/test_fused_ops.py -m gpu -x -v --timeout 120 --timeout-method thread \
@@ -21,5 +21,5 @@ echo "profile"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 10 \
   --modes vgpu > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 10; }
 python3 tools/prof_summary.py "$OUT/prof/**/*results.db" --top 30 -o $OUT/prof_summary.md \
-  --title "ResNet-V2-50 inference b=50 bf16 in a vGPU, MFMA convs with fused epilogues (r1o)" > /dev/null || true
+  --title "ResNet-V2-50 inference b=50 bf16 in a vGPU, MFMA convs with fused epilogues (r1p)" > /dev/null || true
 ls $OUT/prof | head
