@@ -41,6 +41,8 @@ def _ops():
         L.vgpu_conv1x1_bf16.restype = C.c_int
         L.vgpu_conv_nhwc_bf16.argtypes = [C.c_void_p] * 7 + [C.c_int] * 11 + [C.c_void_p]
         L.vgpu_conv_nhwc_bf16.restype = C.c_int
+        L.vgpu_stem_bf16.argtypes = [C.c_void_p] * 5 + [C.c_int] * 3 + [C.c_void_p]
+        L.vgpu_stem_bf16.restype = C.c_int
         _lib = L
     return _lib
 
@@ -236,6 +238,54 @@ def conv_nhwc(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, 
     return (y, s) if write_sum else y
 
 
+def is_resnet_stem(conv, pool):
+    """conv7x7/2 (3 -> 64, pad 3, no bias) followed by maxpool3x3/2 pad 1: the shape
+    ``stem_mfma.hip`` fuses."""
+    return (isinstance(conv, nn.Conv2d) and conv.in_channels == 3 and conv.out_channels == 64
+            and conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and isinstance(pool, nn.MaxPool2d) and pool.kernel_size in (3, (3, 3)) and pool.stride in (2, (2, 2))
+            and pool.padding in (1, (1, 1)) and pool.dilation in (1, (1, 1)) and not pool.ceil_mode)
+
+
+def stem_weight(w):
+    """[64, 192] matrix of a [64, 3, 7, 7] stem weight in the kernel's K order: 24 groups
+    of 8 = (kh, c) pairs x kw padded 7 -> 8, groups 21..23 zero."""
+    cout = w.shape[0]
+    m = torch.zeros(cout, 24, 8, dtype=w.dtype, device=w.device)
+    m[:, :21, :7] = w.permute(0, 2, 1, 3).reshape(cout, 21, 7)
+    return m.reshape(cout, 192).contiguous()
+
+
+def stem_reference(x, w, scale, shift):
+    """fp32 reference: relu(bn(maxpool3x3/2(conv7x7/2(x))))."""
+    y = F.max_pool2d(F.conv2d(x.float(), w.float(), stride=2, padding=3), 3, 2, 1)
+    return F.relu(y * scale.float().view(1, -1, 1, 1) + shift.float().view(1, -1, 1, 1))
+
+
+def stem_pool_bn_act(x, w192, scale, shift):
+    """HIP fused ResNet stem (``stem_mfma.hip``): conv7x7/2 + maxpool3x3/2 + BN + ReLU in
+    one kernel on bf16 channels-last input; ``w192`` from :func:`stem_weight`."""
+    if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 4 or x.shape[1] != 3:
+        raise TypeError("stem needs a [N, 3, H, W] bf16 CUDA tensor")
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("stem needs channels_last input")
+    if tuple(w192.shape) != (64, 192) or w192.dtype != torch.bfloat16 or not w192.is_contiguous():
+        raise ValueError("w192 must be the contiguous [64, 192] bf16 stem matrix")
+    for v in (scale, shift):
+        if v.dtype != torch.float32 or v.numel() != 64 or not v.is_contiguous():
+            raise ValueError("scale/shift must be contiguous fp32 vectors of 64")
+    N, _, H, W = x.shape
+    ch, cw = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    ph, pw = (ch - 1) // 2 + 1, (cw - 1) // 2 + 1
+    y = torch.empty((N, 64, ph, pw), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    rc = _ops().vgpu_stem_bf16(_ptr(x), _ptr(w192), _ptr(scale), _ptr(shift), _ptr(y), N, H, W, C.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"vgpu_stem_bf16 failed ({rc}) for x {tuple(x.shape)}")
+    return y
+
+
 def is_mfma_conv(conv):
     """A bias-free dense convolution the MFMA kernel tiles: channels multiples of 64,
     square stride and symmetric padding smaller than the kernel, no dilation."""
@@ -326,6 +376,9 @@ class FusedResNetV2(nn.Module):
                                       [FusedBNAct(model.post_bn, "relu", impl)])
         self.eligible = [(is_mfma_conv(b.conv1), is_mfma_conv(b.conv2), is_mfma_conv(b.conv3),
                           b.shortcut is not None and is_mfma_conv(b.shortcut)) for b in blocks]
+        # Fused stem (conv + pool + first BN/ReLU) needs block 0 to project its shortcut
+        # from `pre`, since the pooled map itself is never materialised.
+        self.stem_fusable = is_resnet_stem(model.stem, model.pool) and self.has_sc[0]
 
     def _w2d(self, conv):
         w = conv.weight
@@ -356,9 +409,23 @@ class FusedResNetV2(nn.Module):
             d = self.plan[key] = _time_us(fused) <= _time_us(unfused)
         return d
 
+    def _stem_fused(self, x):
+        if self.impl == "hip":
+            w = self.stem.weight
+            hit = self._wcache.get("stem")
+            if hit is None or hit[0] != w.data_ptr() or hit[1] != w.dtype:
+                hit = self._wcache["stem"] = (w.data_ptr(), w.dtype, stem_weight(w.detach()))
+            return stem_pool_bn_act(x, hit[2], self.entry.scale, self.entry.shift)
+        y = stem_reference(x, self.stem.weight, self.entry.scale, self.entry.shift)
+        return y.to(x.dtype).contiguous(memory_format=torch.channels_last)
+
     def forward(self, x):
-        x = self.pool(self.stem(x))
-        pre = self.entry(x)
+        if self.stem_fusable and self._use(("stem", tuple(x.shape)), lambda: self._stem_fused(x),
+                                           lambda: self.entry(self.pool(self.stem(x)))):
+            pre, x = self._stem_fused(x), None  # block 0 projects its shortcut from pre
+        else:
+            x = self.pool(self.stem(x))
+            pre = self.entry(x)
         n = len(self.convs)
         for i in range(n):
             c1, c2, c3 = self.convs[i]

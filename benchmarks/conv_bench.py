@@ -101,6 +101,26 @@ def main():
                      "speedup": t_l / t_f, "fused_TBps": nbytes / t_f / 1e6, "fused_TFLOPs": flops / t_f / 1e6,
                      "max_abs_diff_vs_library": err})
         print(json.dumps(rows[-1]), flush=True)
+    # The stem: conv7x7/2 (3 -> 64) + maxpool3x3/2 + first BN + ReLU, one fused kernel
+    # (stem_mfma.hip) vs library conv + max-pool + the fused BN+ReLU pass.
+    from amdvgpu.ops.fused import stem_pool_bn_act, stem_weight
+    x = torch.randn(50, 3, 346, 346, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(64, 3, 7, 7, device="cuda") / 147 ** 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w192 = stem_weight(wt)
+    sc, sh = torch.rand(64, device="cuda") + 0.5, torch.randn(64, device="cuda")
+    with torch.inference_mode():
+        fused = lambda: stem_pool_bn_act(x, w192, sc, sh)  # noqa: E731
+        conv_only = lambda: F.conv2d(x, wt, stride=2, padding=3)  # noqa: E731
+        lib = lambda: bn_act(F.max_pool2d(conv_only(), 3, 2, 1), sc, sh, act="relu")  # noqa: E731
+        t_f, t_l, t_c = timeit(fused, a.iters), timeit(lib, a.iters), timeit(conv_only, a.iters)
+        err = (fused().float() - lib().float()).abs().max().item()
+    m = 50 * 173 * 173
+    rows.append({"layer": "stem conv7x7/2 + pool + bn", "M": m, "K": 147, "N": 64, "epilogue": "pool_bn_act",
+                 "fused_us": t_f, "library_conv_plus_epilogue_us": t_l, "library_conv_only_us": t_c,
+                 "speedup": t_l / t_f, "fused_TBps": 2 * (x.numel() + 50 * 64 * 87 * 87) / t_f / 1e6,
+                 "fused_TFLOPs": 2.0 * m * 147 * 64 / t_f / 1e6, "max_abs_diff_vs_library": err})
+    print(json.dumps(rows[-1]), flush=True)
     tot_f = sum(r_["fused_us"] for r_ in rows)
     tot_l = sum(r_["library_conv_plus_epilogue_us"] for r_ in rows)
     md = ["| layer | M | K | N | epilogue | fused MFMA us | library conv + epilogue us | conv alone us | speedup "

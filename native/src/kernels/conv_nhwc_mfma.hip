@@ -208,6 +208,23 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
 
   const unsigned nk = K / kBK;
   load_tile(0);
+  // The residual tile does not depend on the GEMM: its loads go out right behind the
+  // first K-tile's, so they are in flight together and complete under the MFMAs instead
+  // of stalling the epilogue (vmcnt retires loads in order, so the first LDS store only
+  // waits for the older A/W loads).
+  constexpr unsigned kChunksPerRow = BN / 8;
+  constexpr int kEpiIters = kBM * kChunksPerRow / kThreads;
+  static_assert(kEpiIters * kThreads == kBM * kChunksPerRow, "whole epilogue iterations");
+  const size_t nvec = N >> 3;  // output row stride in 16-B chunks
+  u32x4 rpre[kEpi >= 2 ? kEpiIters : 1];
+  if constexpr (kEpi >= 2) {
+#pragma unroll
+    for (int j = 0; j < kEpiIters; j++) {
+      const unsigned c = tid + j * kThreads, r = c / kChunksPerRow, cc = c % kChunksPerRow;
+      const unsigned gm = (m0 + r < M) ? m0 + r : M - 1u;
+      rpre[j] = __builtin_nontemporal_load(&R[(size_t)gm * nvec + (n0 >> 3) + cc]);
+    }
+  }
   store_tile(0);
   __syncthreads();
   for (unsigned kt = 0; kt < nk; kt++) {
@@ -249,11 +266,9 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
             acc[i][j][r];
   __syncthreads();
 
-  const size_t nvec = N >> 3;  // output row stride in 16-B chunks
-  constexpr unsigned kChunksPerRow = BN / 8;
-#pragma unroll 2
-  for (unsigned c = tid; c < kBM * kChunksPerRow; c += kThreads) {
-    const unsigned r = c / kChunksPerRow, cc = c % kChunksPerRow;
+#pragma unroll
+  for (int j = 0; j < kEpiIters; j++) {
+    const unsigned c = tid + j * kThreads, r = c / kChunksPerRow, cc = c % kChunksPerRow;
     const unsigned gm = m0 + r;
     if (gm >= M) continue;
     const float4 v0 = *reinterpret_cast<const float4*>(ctile + r * kCStride + cc * 8u);
@@ -263,7 +278,7 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
     const size_t o = (size_t)gm * nvec + (n >> 3);
     float rr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (kEpi >= 2) {
-      const u32x4 rv = __builtin_nontemporal_load(&R[o]);
+      const u32x4 rv = rpre[j];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         rr[2 * k] = bf_lo(rv[k]);

@@ -6,7 +6,8 @@ import torch.nn as nn
 
 from amdvgpu.models.aibench import ResNetV2, resnet_v2_50
 from amdvgpu.ops.fused import (FusedResNetV2, bn_act, bn_act_reference, bn_scale_shift, conv1x1,
-                                conv1x1_reference, conv_nhwc, conv_reference)
+                                conv1x1_reference, conv_nhwc, conv_reference, stem_pool_bn_act, stem_reference,
+                                stem_weight)
 
 
 def _randomize_bn(model, g):
@@ -126,6 +127,40 @@ def test_conv_nhwc_kernel_numerics(geom, epi):
     torch.testing.assert_close(y.float(), y_ref, rtol=2e-2, atol=3e-2)
     if epi == "residual_sum":
         torch.testing.assert_close(out[1].float(), s_ref, rtol=2e-2, atol=3e-2)
+
+
+def test_stem_weight_layout_cpu():
+    """The [64, 192] stem matrix in (kh, c, kw8) order reproduces conv7x7 on an im2col
+    built in the same order."""
+    g = torch.Generator().manual_seed(9)
+    w = torch.randn(64, 3, 7, 7, generator=g)
+    x = torch.randn(1, 3, 7, 7, generator=g)
+    m = stem_weight(w)
+    assert m.shape == (64, 192) and torch.all(m.view(64, 24, 8)[:, 21:] == 0) and torch.all(m.view(64, 24, 8)[:, :, 7] == 0)
+    cols = torch.zeros(24, 8)
+    cols[:21, :7] = x[0].permute(1, 0, 2).reshape(21, 7)  # (kh, c, kw)
+    torch.testing.assert_close(m @ cols.reshape(192), F_conv_valid(x, w))
+
+
+def F_conv_valid(x, w):
+    return torch.nn.functional.conv2d(x, w).reshape(-1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 346, 346), (1, 64, 48), (3, 31, 29), (1, 7, 7)])
+def test_stem_kernel_numerics(shape):
+    """Fused conv7x7/2 + maxpool3x3/2 + BN + ReLU vs fp32 PyTorch (odd sizes exercise the
+    partial pooled tiles and the image-border padding of both conv and pool)."""
+    N, H, W = shape
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, 3, H, W, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, generator=g) / 147 ** 0.5).to("cuda", torch.bfloat16)
+    sc = (torch.rand(64, generator=g) + 0.5).cuda()
+    sh = torch.randn(64, generator=g).cuda()
+    y = stem_pool_bn_act(x, stem_weight(w), sc, sh)
+    ref = stem_reference(x, w, sc, sh)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)
 
 
 @pytest.mark.gpu

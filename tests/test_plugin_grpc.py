@@ -118,6 +118,11 @@ def test_kubelet_restart_triggers_reregistration(plugin_dir):
         n0 = sup.restarts
         k.restart()  # re-creates kubelet.sock
         k.wait_registered("amd.com/gpu", timeout=15)
+        # The kubelet records the registration before Supervisor.start_plugins returns
+        # and counts the restart; give the supervisor thread a moment to finish it.
+        deadline = time.time() + 10
+        while sup.restarts <= n0 and time.time() < deadline:
+            time.sleep(0.05)
         assert sup.restarts > n0
         k.wait_devices("amd.com/gpu")
     finally:
