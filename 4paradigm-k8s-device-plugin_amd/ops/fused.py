@@ -39,7 +39,7 @@ def _ops():
         L.vgpu_conv1x1_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.vgpu_conv1x1_bf16.restype = C.c_int
-        L.vgpu_conv_nhwc_bf16.argtypes = [C.c_void_p] * 7 + [C.c_int] * 11 + [C.c_void_p]
+        L.vgpu_conv_nhwc_bf16.argtypes = [C.c_void_p] * 9 + [C.c_int] * 11 + [C.c_void_p]
         L.vgpu_conv_nhwc_bf16.restype = C.c_int
         L.vgpu_stem_bf16.argtypes = [C.c_void_p] * 5 + [C.c_int] * 3 + [C.c_void_p]
         L.vgpu_stem_bf16.restype = C.c_int
@@ -174,10 +174,16 @@ def conv_weight_2d(w):
     return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()
 
 
-def conv_reference(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, act="relu", post=False):
-    """fp32 reference of :func:`conv_nhwc`: returns (y, sum or None)."""
-    acc = F.conv2d(x.float(), w.float(), stride=stride, padding=padding)
+def conv_reference(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, act="relu", post=False,
+                   prologue=None):
+    """fp32 reference of :func:`conv_nhwc`: returns (y, sum or None). ``prologue``:
+    (scale, shift) applied as relu(x * scale + shift) to the input, rounded to x's dtype
+    as the kernel stages it."""
     shape = [1, -1, 1, 1]
+    if prologue is not None:
+        ps, pt = prologue
+        x = F.relu(x.float() * ps.float().view(shape) + pt.float().view(shape)).to(x.dtype)
+    acc = F.conv2d(x.float(), w.float(), stride=stride, padding=padding)
     s = None
     if residual is not None and not post:
         acc = acc + residual.float()
@@ -191,12 +197,14 @@ def conv_reference(x, w, stride=1, padding=0, scale=None, shift=None, residual=N
 
 
 def conv_nhwc(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, act="relu", write_sum=False,
-              post=False, w2d=None):
+              post=False, w2d=None, prologue=None):
     """HIP MFMA convolution (``conv_nhwc_mfma.hip``: implicit GEMM over channels-last
     activations) with the epilogue fused: y = act((conv(x, w) [+ residual]) * scale +
-    shift), or with ``post`` act(conv * scale + shift + residual). ``w`` is the 4-D conv
-    weight (``w2d``: its cached :func:`conv_weight_2d`). Cin and Cout must be multiples
-    of 64; padding symmetric and smaller than the kernel."""
+    shift), or with ``post`` act(conv * scale + shift + residual), or without scale/shift
+    conv (+ residual). ``w`` is the 4-D conv weight (``w2d``: its cached
+    :func:`conv_weight_2d`). ``prologue`` = (scale, shift): the input is read as
+    relu(x * scale + shift) (1x1 stride-1 convs with a BN + ReLU epilogue). Cin and Cout
+    must be multiples of 64; padding symmetric and smaller than the kernel."""
     if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 4:
         raise TypeError("conv_nhwc needs a 4-D bf16 CUDA tensor")
     if not x.is_contiguous(memory_format=torch.channels_last):
@@ -212,11 +220,19 @@ def conv_nhwc(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, 
     w2d = conv_weight_2d(w) if w2d is None else w2d
     if tuple(w2d.shape) != (cout, kh * kw * Cin) or not w2d.is_contiguous():
         raise ValueError("w2d must be the contiguous [Cout, KH*KW*Cin] weight")
-    if (scale is None) != (shift is None) or (residual is not None and scale is None):
-        raise ValueError("residual epilogue needs scale and shift")
+    if (scale is None) != (shift is None) or (residual is not None and scale is None and (post or write_sum)):
+        raise ValueError("post-BN residual and sum output need scale and shift")
     for v in (scale, shift):
         if v is not None and (v.dtype != torch.float32 or v.numel() != cout or not v.is_contiguous()):
             raise ValueError("scale/shift must be contiguous fp32 vectors of Cout")
+    ps = pt = None
+    if prologue is not None:
+        ps, pt = prologue
+        if (kh, kw, stride, padding) != (1, 1, 1, 0) or scale is None or residual is not None or act != "relu":
+            raise ValueError("the input prologue is for 1x1 stride-1 convs with a BN + ReLU epilogue")
+        for v in (ps, pt):
+            if v.dtype != torch.float32 or v.numel() != Cin or not v.is_contiguous():
+                raise ValueError("prologue scale/shift must be contiguous fp32 vectors of Cin")
     oh, ow = (H + 2 * padding - kh) // stride + 1, (W + 2 * padding - kw) // stride + 1
     y = torch.empty((N, cout, oh, ow), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
     if residual is not None and (residual.shape != y.shape or residual.dtype != y.dtype or residual.stride() != y.stride()):
@@ -225,14 +241,15 @@ def conv_nhwc(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, 
         raise ValueError("write_sum needs a pre-BN residual")
     s = torch.empty_like(y) if write_sum else None
     if scale is None:
-        epi = 0
+        epi = 0 if residual is None else 5
     elif residual is None:
         epi = 1
     else:
         epi = 4 if post else 3 if write_sum else 2
     stream = torch.cuda.current_stream(x.device).cuda_stream
     rc = _ops().vgpu_conv_nhwc_bf16(_ptr(x), _ptr(w2d), _ptr(scale), _ptr(shift), _ptr(residual), _ptr(y), _ptr(s),
-                                    N, H, W, Cin, cout, kh, kw, stride, padding, epi, ACT[act], C.c_void_p(stream))
+                                    _ptr(ps), _ptr(pt), N, H, W, Cin, cout, kh, kw, stride, padding, epi, ACT[act],
+                                    C.c_void_p(stream))
     if rc != 0:
         raise RuntimeError(f"vgpu_conv_nhwc_bf16 failed ({rc}) for x {tuple(x.shape)} w {tuple(w.shape)}")
     return (y, s) if write_sum else y
@@ -379,6 +396,13 @@ class FusedResNetV2(nn.Module):
         # Fused stem (conv + pool + first BN/ReLU) needs block 0 to project its shortcut
         # from `pre`, since the pooled map itself is never materialised.
         self.stem_fusable = is_resnet_stem(model.stem, model.pool) and self.has_sc[0]
+        # Block j's conv1 reads x and applies bn1_j + ReLU itself (the previous conv3 then
+        # writes only x) when pre_j has no other reader (identity shortcut) and both convs
+        # run on the MFMA kernel. Not timed in "auto": it removes a full activation write
+        # and read, and the 1x1 kernel beats library conv + BN on every ResNet-50 layer.
+        on = self.mfma_mode == "on" or (self.mfma_mode == "auto" and impl == "hip")
+        self.prologue = [on and j > 0 and not self.has_sc[j] and is_pointwise(blocks[j].conv1)
+                         and self.eligible[j - 1][2] for j in range(len(blocks))]
 
     def _w2d(self, conv):
         w = conv.weight
@@ -388,14 +412,16 @@ class FusedResNetV2(nn.Module):
             self._wcache[id(conv)] = hit
         return hit[2]
 
-    def _conv(self, x, conv, bn=None, residual=None, write_sum=False):
-        """conv with bn's epilogue fused: the HIP MFMA kernel, or its fp32 torch
-        reference for impl="torch"."""
+    def _conv(self, x, conv, bn=None, residual=None, write_sum=False, prologue=None):
+        """conv with bn's epilogue (and optionally the input's BN + ReLU as a prologue)
+        fused: the HIP MFMA kernel, or its fp32 torch reference for impl="torch"."""
         st, pad = conv.stride[0], conv.padding[0]
         sc, sh, act = (bn.scale, bn.shift, bn.act) if bn is not None else (None, None, "none")
+        pro = (prologue.scale, prologue.shift) if prologue is not None else None
         if self.impl == "hip":
-            return conv_nhwc(x, conv.weight, st, pad, sc, sh, residual, act, write_sum, w2d=self._w2d(conv))
-        y, s = conv_reference(x, conv.weight, st, pad, sc, sh, residual, act)
+            return conv_nhwc(x, conv.weight, st, pad, sc, sh, residual, act, write_sum, w2d=self._w2d(conv),
+                             prologue=pro)
+        y, s = conv_reference(x, conv.weight, st, pad, sc, sh, residual, act, prologue=pro)
         y = y.to(x.dtype).contiguous(memory_format=torch.channels_last)
         return (y, s.to(x.dtype).contiguous(memory_format=torch.channels_last)) if write_sum else y
 
@@ -432,6 +458,9 @@ class FusedResNetV2(nn.Module):
             bn2, bn3 = self.mid[i]
             bnd, last = self.boundary[i], i + 1 == n
             e1, e2, e3, esc = self.eligible[i]
+            # pre is None when the previous conv3 wrote only x: this block's conv1 then
+            # applies its pre-activation BN + ReLU (bn_in) while loading x.
+            bn_in = self.entry if i == 0 else self.boundary[i - 1]
             if not self.has_sc[i]:
                 sc = x
             elif esc and self._use((i, 0, tuple(pre.shape)), lambda: self._conv(pre, self.shortcuts[i]),
@@ -439,7 +468,9 @@ class FusedResNetV2(nn.Module):
                 sc = self._conv(pre, self.shortcuts[i])
             else:
                 sc = self.shortcuts[i](pre)
-            if e1 and self._use((i, 1, tuple(pre.shape)), lambda: self._conv(pre, c1, bn2), lambda: bn2(c1(pre))):
+            if pre is None:
+                y = self._conv(x, c1, bn2, prologue=bn_in)
+            elif e1 and self._use((i, 1, tuple(pre.shape)), lambda: self._conv(pre, c1, bn2), lambda: bn2(c1(pre))):
                 y = self._conv(pre, c1, bn2)
             else:
                 y = bn2(c1(pre))
@@ -447,15 +478,15 @@ class FusedResNetV2(nn.Module):
                 y = self._conv(y, c2, bn3)
             else:
                 y = bn3(c2(y))
-            if e3 and self._use((i, 3, tuple(y.shape)), lambda: self._conv(y, c3, bnd, sc, not last),
-                                lambda: bnd(c3(y), residual=sc, write_sum=not last)):
+            if not last and self.prologue[i + 1]:
+                x, pre = self._conv(y, c3, None, sc), None  # next conv1 applies bnd itself
+            elif e3 and self._use((i, 3, tuple(y.shape)), lambda: self._conv(y, c3, bnd, sc, not last),
+                                  lambda: bnd(c3(y), residual=sc, write_sum=not last)):
                 out = self._conv(y, c3, bnd, sc, not last)
+                pre, x = (out, None) if last else out
             else:
                 out = bnd(c3(y), residual=sc, write_sum=not last)
-            if last:
-                pre = out
-            else:
-                pre, x = out
+                pre, x = (out, None) if last else out
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(pre, 1), 1))
 
 

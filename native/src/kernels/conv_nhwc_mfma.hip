@@ -15,6 +15,13 @@
 //                                                shortcut)                           (epi 3)
 //   MobileNet projection (+ residual after BN)  y = act(acc * s + t + r)            (epi 4)
 //   shortcut conv                               y = acc                             (epi 0)
+//   conv3 when the next block's conv1 takes     x = acc + r                         (epi 5)
+//   its BN + ReLU as a prologue
+//
+// Prologue: before an identity-shortcut block, the activation pre = relu(bn1(x)) is only
+// read by that block's 1x1 conv1. That conv1 then stages relu(x * s + t) itself while
+// loading its A tile, and the previous conv3 writes only x (epi 5): one fewer full-size
+// activation written and read per block (e.g. 194 MB at stage 1, batch 50).
 //
 // Run separately (library conv + fused_bn_act.hip) the epilogue re-reads the conv output
 // from HBM and writes it again; here it is applied while the accumulator tile is still
@@ -78,6 +85,8 @@ struct ConvArgs {
   const void* r;
   void* y;
   void* s;
+  const float* pscale;  // prologue (1x1 path): A = relu(X * pscale + pshift), or null
+  const float* pshift;
   ConvGeom g;
 };
 
@@ -107,13 +116,18 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned ntiles) {
 }
 
 // kEpi: 0 plain (y = acc), 1 y = act(acc*s+t), 2 x = acc + r; y = act(x*s+t),
-//       3 as 2 and also writes x (bf16) to `s`, 4 y = act(acc*s + t + r).
+//       3 as 2 and also writes x (bf16) to `s`, 4 y = act(acc*s + t + r), 5 y = acc + r.
 // kIm2col: false = 1x1/stride-1 (A is X itself), true = implicit GEMM gather.
-template <int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col>
+// kPro (1x1 path): the A operand is relu(X * pscale[c] + pshift[c]) (the consumer's
+//       pre-activation BN + ReLU applied while staging, rounded to bf16 as a separate
+//       pass would store it), so the producer never writes that activation to HBM.
+template <int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro>
 __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict__ X, const u32x4* __restrict__ Wt,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        const u32x4* __restrict__ R, u32x4* __restrict__ Y,
-                                                       u32x4* __restrict__ S, const ConvGeom p) {
+                                                       u32x4* __restrict__ S, const float* __restrict__ pscale,
+                                                       const float* __restrict__ pshift, const ConvGeom p) {
+  static_assert(!(kPro && kIm2col), "prologue only on the 1x1 path");
   static_assert(WM * WN == kThreads / 64, "4 waves");
   constexpr int FM = kBM / WM / 16;
   constexpr int FN = BN / WN / 16;
@@ -170,8 +184,22 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
   }
 
   u32x4 ra[kALoads], rw[kWLoads];
+  // Prologue parameters: a thread's A chunks all hold channels (tid & 7) * 8 .. + 7 of
+  // the K-tile (256 threads cover 8 chunks per row), so one set of 8 per K-tile.
+  float pro_s[8], pro_t[8];
   auto load_tile = [&](unsigned kt) {
     const size_t off = (size_t)kt * (kBK / 8);
+    if constexpr (kPro) {
+      const unsigned c0 = kt * kBK + (tid & 7u) * 8u;
+      const float4 s0 = *reinterpret_cast<const float4*>(pscale + c0);
+      const float4 s1 = *reinterpret_cast<const float4*>(pscale + c0 + 4);
+      const float4 t0 = *reinterpret_cast<const float4*>(pshift + c0);
+      const float4 t1 = *reinterpret_cast<const float4*>(pshift + c0 + 4);
+      pro_s[0] = s0.x; pro_s[1] = s0.y; pro_s[2] = s0.z; pro_s[3] = s0.w;
+      pro_s[4] = s1.x; pro_s[5] = s1.y; pro_s[6] = s1.z; pro_s[7] = s1.w;
+      pro_t[0] = t0.x; pro_t[1] = t0.y; pro_t[2] = t0.z; pro_t[3] = t0.w;
+      pro_t[4] = t1.x; pro_t[5] = t1.y; pro_t[6] = t1.z; pro_t[7] = t1.w;
+    }
     if constexpr (kIm2col) {
       // Wave-uniform tap of this K-tile: k0 = ((kh * KW) + kw) * C + c0.
       const unsigned k0 = kt * kBK, tap = k0 / p.C, c0v = (k0 - tap * p.C) >> 3;
@@ -192,6 +220,15 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
     for (int i = 0; i < kWLoads; i++) rw[i] = w_src[i][off];
   };
   auto store_tile = [&](int b) {
+    if constexpr (kPro) {
+#pragma unroll
+      for (int i = 0; i < kALoads; i++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          ra[i][k] = pack_bf16(fmaxf(fmaf(bf_lo(ra[i][k]), pro_s[2 * k], pro_t[2 * k]), 0.f),
+                               fmaxf(fmaf(bf_hi(ra[i][k]), pro_s[2 * k + 1], pro_t[2 * k + 1]), 0.f));
+      }
+    }
 #pragma unroll
     for (int i = 0; i < kALoads; i++) a_lds(b)[a_dst[i]] = ra[i];
 #pragma unroll
@@ -285,7 +322,7 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
         rr[2 * k + 1] = bf_hi(rv[k]);
       }
     }
-    if constexpr (kEpi == 2 || kEpi == 3) {
+    if constexpr (kEpi == 2 || kEpi == 3 || kEpi == 5) {
 #pragma unroll
       for (int k = 0; k < 8; k++) v[k] += rr[k];
       if constexpr (kEpi == 3) {
@@ -295,7 +332,7 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
         S[o] = sv;
       }
     }
-    if constexpr (kEpi >= 1) {
+    if constexpr (kEpi >= 1 && kEpi <= 4) {
       const float4 s0 = *reinterpret_cast<const float4*>(scale + n);
       const float4 s1 = *reinterpret_cast<const float4*>(scale + n + 4);
       const float4 t0 = *reinterpret_cast<const float4*>(shift + n);
@@ -321,10 +358,17 @@ int launch(ConvArgs a, bool im2col, hipStream_t stream) {
   ConvGeom g = a.g;
   g.tiles_n = g.N / BN;
   g.ntiles = (g.M + kBM - 1) / kBM * g.tiles_n;
-  auto kern = im2col ? conv_kernel<BN, WM, WN, kEpi, kAct, true> : conv_kernel<BN, WM, WN, kEpi, kAct, false>;
+  auto kern = conv_kernel<BN, WM, WN, kEpi, kAct, false, false>;
+  if (im2col) {
+    kern = conv_kernel<BN, WM, WN, kEpi, kAct, true, false>;
+  } else if (a.pscale) {
+    // The prologue exists for the ResNet-V2 conv1 (BN + ReLU epilogue) only.
+    if constexpr (kEpi == 1 && kAct == 1) kern = conv_kernel<BN, WM, WN, kEpi, kAct, false, true>;
+    else return -1;
+  }
   hipLaunchKernelGGL(kern, dim3(g.ntiles), dim3(kThreads), 0, stream, static_cast<const u32x4*>(a.x),
                      static_cast<const u32x4*>(a.w), a.scale, a.shift, static_cast<const u32x4*>(a.r),
-                     static_cast<u32x4*>(a.y), static_cast<u32x4*>(a.s), g);
+                     static_cast<u32x4*>(a.y), static_cast<u32x4*>(a.s), a.pscale, a.pshift, g);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -336,6 +380,7 @@ int by_epi(int epi, const ConvArgs& a, bool im2col, hipStream_t st) {
     case 2: return launch<BN, WM, WN, 2, kAct>(a, im2col, st);
     case 3: return launch<BN, WM, WN, 3, kAct>(a, im2col, st);
     case 4: return launch<BN, WM, WN, 4, kAct>(a, im2col, st);
+    case 5: return launch<BN, WM, WN, 5, 0>(a, im2col, st);
     default: return -1;
   }
 }
@@ -357,17 +402,21 @@ extern "C" {
 // y[Nb, OH, OW, Cout] = epilogue(conv(x[Nb, H, W, C], w[Cout, KH, KW, C])), bf16 NHWC,
 // fp32 accumulation, OH = (H + 2 pad - KH) / stride + 1 (same for OW). epi: 0 plain,
 // 1 act(acc*scale+shift), 2 act((acc+r)*scale+shift), 3 as 2 and sum = acc + r,
-// 4 act(acc*scale + shift + r). act: 0 none, 1 relu, 2 relu6. scale/shift: fp32[Cout].
-// Returns 0 on success, -1 on bad arguments, -2 on launch failure.
+// 4 act(acc*scale + shift + r), 5 acc + r. act: 0 none, 1 relu, 2 relu6. scale/shift:
+// fp32[Cout]. pscale/pshift (optional, fp32[C], 1x1 stride-1 with epi 1 + relu only): the
+// input is read as relu(x * pscale + pshift). Returns 0 on success, -1 on bad arguments,
+// -2 on launch failure.
 int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const float* shift, const void* r, void* y,
-                        void* sum, int nb, int h, int wd, int c, int cout, int kh, int kw, int stride, int pad, int epi,
-                        int act, void* stream) {
+                        void* sum, const float* pscale, const float* pshift, int nb, int h, int wd, int c, int cout,
+                        int kh, int kw, int stride, int pad, int epi, int act, void* stream) {
   if (!x || !w || !y || nb <= 0 || h <= 0 || wd <= 0 || c <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
       pad < 0 || pad >= kh || pad >= kw)
     return -1;
   if (c % kBK || cout % 64) return -1;
-  if (epi < 0 || epi > 4 || act < 0 || act > 2) return -1;
-  if (epi >= 1 && (!scale || !shift)) return -1;
+  if (epi < 0 || epi > 5 || act < 0 || act > 2) return -1;
+  if (epi >= 1 && epi <= 4 && (!scale || !shift)) return -1;
+  if ((pscale == nullptr) != (pshift == nullptr)) return -1;
+  if (pscale && (epi != 1 || act != 1 || kh != 1 || kw != 1 || stride != 1 || pad != 0)) return -1;
   if (epi >= 2 && !r) return -1;
   if ((epi == 3) != (sum != nullptr)) return -1;
   const int64_t oh = ((int64_t)h + 2 * pad - kh) / stride + 1, ow = ((int64_t)wd + 2 * pad - kw) / stride + 1;
@@ -376,9 +425,11 @@ int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const 
   if (m >= ((int64_t)1 << 32) || (int64_t)nb * h * wd * c >= lim || m * cout >= lim || k * cout >= lim) return -1;
   auto misaligned = [](const void* q) { return q && (reinterpret_cast<uintptr_t>(q) & 15u); };
   if (misaligned(x) || misaligned(w) || misaligned(y) || misaligned(r) || misaligned(sum) || misaligned(scale) ||
-      misaligned(shift))
+      misaligned(shift) || misaligned(pscale) || misaligned(pshift))
     return -1;
   ConvArgs a{};
+  a.pscale = pscale;
+  a.pshift = pshift;
   a.x = x;
   a.w = w;
   a.scale = scale;
@@ -407,7 +458,8 @@ int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const 
 int vgpu_conv1x1_bf16(const void* x, const void* w, const float* scale, const float* shift, const void* r, void* y,
                       void* sum, int64_t M, int N, int K, int epi, int act, void* stream) {
   if (M <= 0 || M >= ((int64_t)1 << 31)) return -1;
-  return vgpu_conv_nhwc_bf16(x, w, scale, shift, r, y, sum, (int)M, 1, 1, K, N, 1, 1, 1, 0, epi, act, stream);
+  return vgpu_conv_nhwc_bf16(x, w, scale, shift, r, y, sum, nullptr, nullptr, (int)M, 1, 1, K, N, 1, 1, 1, 0, epi, act,
+                             stream);
 }
 
 }  // extern "C"

@@ -164,6 +164,27 @@ def test_stem_kernel_numerics(shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nhw,k,n", [((2, 7, 9), 64, 64), ((50, 22, 22), 1024, 256), ((3, 5, 5), 256, 192)])
+def test_conv_prologue_and_sum_only_numerics(nhw, k, n):
+    """1x1 conv reading relu(x * s + t) (the consumer-side BN + ReLU prologue) with a
+    BN + ReLU epilogue, and the producer-side "x = conv + residual only" epilogue."""
+    N, H, W = nhw
+    g = torch.Generator().manual_seed(14)
+    x = torch.randn(N, k, H, W, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(n, k, 1, 1, generator=g) / k ** 0.5).to("cuda", torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    ps, pt = (torch.rand(k, generator=g) + 0.5).cuda(), torch.randn(k, generator=g).cuda()
+    sc, sh = (torch.rand(n, generator=g) + 0.5).cuda(), torch.randn(n, generator=g).cuda()
+    y = conv_nhwc(x, w, scale=sc, shift=sh, act="relu", prologue=(ps, pt))
+    y_ref, _ = conv_reference(x, w, scale=sc, shift=sh, act="relu", prologue=(ps, pt))
+    torch.testing.assert_close(y.float(), y_ref, rtol=2e-2, atol=3e-2)
+    r = torch.randn(N, n, H, W, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    s = conv_nhwc(x, w, residual=r)
+    s_ref, _ = conv_reference(x, w, residual=r)
+    torch.testing.assert_close(s.float(), s_ref, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.gpu
 def test_conv1x1_rejects_unsupported_shapes():
     x = torch.zeros(1, 96, 4, 4, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     with pytest.raises(ValueError):
