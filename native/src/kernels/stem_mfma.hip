@@ -77,16 +77,34 @@ __global__ void __launch_bounds__(kThreads) stem_kernel(const unsigned short* __
   const int ir0 = 4 * py0 - 5, ic0 = 4 * px0 - 5;  // input window origin (conv row 2*py0-1)
 
   // 1. Input window, NHWC-order walk (coalesced: consecutive threads read consecutive
-  //    bf16 of a row), stored planar; padding and out-of-image pixels are zero.
+  //    bf16 of a row), stored planar; padding and out-of-image pixels are zero. All of a
+  //    thread's loads are issued before any is used (an out-of-window element loads a
+  //    valid address and is zeroed afterwards, so no branch separates the loads): a
+  //    load -> store loop would pay one memory latency per element.
   const unsigned short* const ximg = X + (size_t)img * H * W * kCin;
-  for (unsigned e = tid; e < (unsigned)(kIT * kIP * kCin); e += kThreads) {
+  constexpr unsigned kElems = kIT * kIP * kCin, kPer = (kElems + kThreads - 1) / kThreads;
+  unsigned short pv[kPer];
+  unsigned pdst[kPer];
+#pragma unroll
+  for (unsigned q = 0; q < kPer; q++) {
+    const unsigned e0 = tid + q * kThreads, e = e0 < kElems ? e0 : kElems - 1u;
     const unsigned r = e / (kIP * kCin), rem = e - r * (kIP * kCin), col = rem / kCin, c = rem - col * kCin;
     const int ih = ir0 + (int)r, iw = ic0 + (int)col;
-    unsigned short v = 0;
-    if ((unsigned)ih < H && (unsigned)iw < W) v = ximg[((size_t)ih * W + (unsigned)iw) * kCin + c];
-    patch[(c * kIT + r) * kIP + col] = v;
+    const bool ok = (unsigned)ih < H && (unsigned)iw < W;
+    const unsigned short v = ximg[ok ? ((size_t)ih * W + (unsigned)iw) * kCin + c : 0];
+    pv[q] = ok ? v : (unsigned short)0;
+    pdst[q] = e0 < kElems ? (c * kIT + r) * kIP + col : ~0u;
   }
-  for (unsigned i = tid; i < (unsigned)(kCout * kGroups); i += kThreads) wl[i] = Wk[i];
+  constexpr unsigned kWPer = kCout * kGroups / kThreads;
+  static_assert(kWPer * kThreads == kCout * kGroups, "whole weight loads");
+  u32x4 wv[kWPer];
+#pragma unroll
+  for (unsigned q = 0; q < kWPer; q++) wv[q] = Wk[tid + q * kThreads];
+#pragma unroll
+  for (unsigned q = 0; q < kPer; q++)
+    if (pdst[q] != ~0u) patch[pdst[q]] = pv[q];
+#pragma unroll
+  for (unsigned q = 0; q < kWPer; q++) wl[tid + q * kThreads] = wv[q];
   __syncthreads();
 
   // 2. Conv tile GEMM: wave w owns M-fragments w, w+4, ... (wave-uniform guard).
