@@ -34,8 +34,9 @@
 //   * v_mfma_f32_16x16x32_bf16: each wave owns a (128/WM) x (BN/WN) sub-tile as
 //     FM x FN 16x16 accumulators. Both operands are K-contiguous, so one lane's
 //     fragment (8 consecutive k of one row) is a single 16-byte LDS read.
-//   * Global -> registers -> LDS staging, double-buffered: the next K-tile's loads are in
-//     flight while the current one feeds the MFMAs; one barrier per K-step. Padding rows
+//   * Global -> registers -> LDS staging, double-buffered LDS and two register stages:
+//     tile k+2's loads are in flight while tile k feeds the MFMAs and tile k+1 waits in
+//     registers for its LDS buffer; one barrier per K-step. Padding rows
 //     load from a valid address and are zeroed after the load (a select, not a branch
 //     around the load, so the loads stay in flight together).
 //   * LDS rows are 128 B (64 bf16); the 16-B chunk index is XOR-swizzled with
@@ -63,6 +64,14 @@ namespace {
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 using f32x4 = float __attribute__((ext_vector_type(4)));
 using bf16x8 = __bf16 __attribute__((ext_vector_type(8)));
+
+// Two register stages (tile k+2 in flight while tile k computes) for the non-residual
+// epilogues: costs occupancy (BN=128: 1 wave/SIMD instead of 2), so it is a build-time
+// choice measured by benchmarks/conv_bench.py (libvgpu_ops_deep.so) rather than the default.
+#ifndef VGPU_CONV_DEEP_PIPELINE
+#define VGPU_CONV_DEEP_PIPELINE 0
+#endif
+constexpr bool kDeepPipeline = VGPU_CONV_DEEP_PIPELINE != 0;
 
 constexpr int kBM = 128;
 constexpr int kBK = 64;
@@ -183,11 +192,16 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
     w_dst[i] = r * 8u + swz(r, ch);
   }
 
-  u32x4 ra[kALoads], rw[kWLoads];
-  // Prologue parameters: a thread's A chunks all hold channels (tid & 7) * 8 .. + 7 of
-  // the K-tile (256 threads cover 8 chunks per row), so one set of 8 per K-tile.
-  float pro_s[8], pro_t[8];
-  auto load_tile = [&](unsigned kt) {
+  // One K-tile in registers on its way to LDS. Two of them are in flight: the loads for
+  // tile k+2 are issued while tile k feeds the MFMAs and tile k+1 waits to be stored, so
+  // a load has two compute phases to land instead of one.
+  struct Stage {
+    u32x4 ra[kALoads], rw[kWLoads];
+    // Prologue parameters: a thread's A chunks all hold channels (tid & 7) * 8 .. + 7 of
+    // the K-tile (256 threads cover 8 chunks per row), so one set of 8 per K-tile.
+    float ps[kPro ? 8 : 1], pt[kPro ? 8 : 1];
+  };
+  auto load_tile = [&](unsigned kt, Stage& st) {
     const size_t off = (size_t)kt * (kBK / 8);
     if constexpr (kPro) {
       const unsigned c0 = kt * kBK + (tid & 7u) * 8u;
@@ -195,10 +209,10 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
       const float4 s1 = *reinterpret_cast<const float4*>(pscale + c0 + 4);
       const float4 t0 = *reinterpret_cast<const float4*>(pshift + c0);
       const float4 t1 = *reinterpret_cast<const float4*>(pshift + c0 + 4);
-      pro_s[0] = s0.x; pro_s[1] = s0.y; pro_s[2] = s0.z; pro_s[3] = s0.w;
-      pro_s[4] = s1.x; pro_s[5] = s1.y; pro_s[6] = s1.z; pro_s[7] = s1.w;
-      pro_t[0] = t0.x; pro_t[1] = t0.y; pro_t[2] = t0.z; pro_t[3] = t0.w;
-      pro_t[4] = t1.x; pro_t[5] = t1.y; pro_t[6] = t1.z; pro_t[7] = t1.w;
+      st.ps[0] = s0.x; st.ps[1] = s0.y; st.ps[2] = s0.z; st.ps[3] = s0.w;
+      st.ps[4] = s1.x; st.ps[5] = s1.y; st.ps[6] = s1.z; st.ps[7] = s1.w;
+      st.pt[0] = t0.x; st.pt[1] = t0.y; st.pt[2] = t0.z; st.pt[3] = t0.w;
+      st.pt[4] = t1.x; st.pt[5] = t1.y; st.pt[6] = t1.z; st.pt[7] = t1.w;
     }
     if constexpr (kIm2col) {
       // Wave-uniform tap of this K-tile: k0 = ((kh * KW) + kw) * C + c0.
@@ -210,29 +224,29 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
         const bool ok = (unsigned)ih < p.H && (unsigned)iw < p.W;
         const size_t pix = ok ? (size_t)ih * p.W + (unsigned)iw : 0;
         const u32x4 v = a_src[i][pix * cvec + c0v];
-        ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+        st.ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < kALoads; i++) ra[i] = a_src[i][off];
+      for (int i = 0; i < kALoads; i++) st.ra[i] = a_src[i][off];
     }
 #pragma unroll
-    for (int i = 0; i < kWLoads; i++) rw[i] = w_src[i][off];
+    for (int i = 0; i < kWLoads; i++) st.rw[i] = w_src[i][off];
   };
-  auto store_tile = [&](int b) {
+  auto store_tile = [&](int b, Stage& st) {
     if constexpr (kPro) {
 #pragma unroll
       for (int i = 0; i < kALoads; i++) {
 #pragma unroll
         for (int k = 0; k < 4; k++)
-          ra[i][k] = pack_bf16(fmaxf(fmaf(bf_lo(ra[i][k]), pro_s[2 * k], pro_t[2 * k]), 0.f),
-                               fmaxf(fmaf(bf_hi(ra[i][k]), pro_s[2 * k + 1], pro_t[2 * k + 1]), 0.f));
+          st.ra[i][k] = pack_bf16(fmaxf(fmaf(bf_lo(st.ra[i][k]), st.ps[2 * k], st.pt[2 * k]), 0.f),
+                                  fmaxf(fmaf(bf_hi(st.ra[i][k]), st.ps[2 * k + 1], st.pt[2 * k + 1]), 0.f));
       }
     }
 #pragma unroll
-    for (int i = 0; i < kALoads; i++) a_lds(b)[a_dst[i]] = ra[i];
+    for (int i = 0; i < kALoads; i++) a_lds(b)[a_dst[i]] = st.ra[i];
 #pragma unroll
-    for (int i = 0; i < kWLoads; i++) w_lds(b)[w_dst[i]] = rw[i];
+    for (int i = 0; i < kWLoads; i++) w_lds(b)[w_dst[i]] = st.rw[i];
   };
 
   const unsigned wm = wave / WN, wn = wave % WN;
@@ -243,8 +257,31 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
 #pragma unroll
     for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  auto compute = [&](int b) {
+#pragma unroll
+    for (int kk = 0; kk < kBK / 32; kk++) {
+      const unsigned chunk = kk * 4u + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; i++) {
+        const unsigned r = row_base + i * 16u + (lane & 15u);
+        af[i] = __builtin_bit_cast(bf16x8, a_lds(b)[r * 8u + swz(r, chunk)]);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; j++) {
+        const unsigned r = col_base + j * 16u + (lane & 15u);
+        bfr[j] = __builtin_bit_cast(bf16x8, w_lds(b)[r * 8u + swz(r, chunk)]);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
   const unsigned nk = K / kBK;
-  load_tile(0);
+  Stage s0, s1;
+  load_tile(0, s0);
   // The residual tile does not depend on the GEMM: its loads go out right behind the
   // first K-tile's, so they are in flight together and complete under the MFMAs instead
   // of stalling the epilogue (vmcnt retires loads in order, so the first LDS store only
@@ -262,32 +299,35 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
       rpre[j] = __builtin_nontemporal_load(&R[(size_t)gm * nvec + (n0 >> 3) + cc]);
     }
   }
-  store_tile(0);
-  __syncthreads();
-  for (unsigned kt = 0; kt < nk; kt++) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
-#pragma unroll
-    for (int kk = 0; kk < kBK / 32; kk++) {
-      const unsigned chunk = kk * 4u + (lane >> 4);
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int i = 0; i < FM; i++) {
-        const unsigned r = row_base + i * 16u + (lane & 15u);
-        af[i] = __builtin_bit_cast(bf16x8, a_lds(cur)[r * 8u + swz(r, chunk)]);
-      }
-#pragma unroll
-      for (int j = 0; j < FN; j++) {
-        const unsigned r = col_base + j * 16u + (lane & 15u);
-        bfr[j] = __builtin_bit_cast(bf16x8, w_lds(cur)[r * 8u + swz(r, chunk)]);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; i++)
-#pragma unroll
-        for (int j = 0; j < FN; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
+  store_tile(0, s0);
+  if constexpr (kEpi < 2 && kDeepPipeline) {
+    if (nk > 1) load_tile(1, s1);
     __syncthreads();
+    // Invariant at step kt: LDS buffer kt&1 holds tile kt; the other register stage holds
+    // tile kt+1 (in flight); the stage that held tile kt is free and receives tile kt+2.
+    // Unrolled by two so both stages stay in registers (no dynamic indexing).
+    for (unsigned kt = 0; kt < nk; kt += 2) {
+      if (kt + 2 < nk) load_tile(kt + 2, s0);
+      compute(0);
+      if (kt + 1 < nk) store_tile(1, s1);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 3 < nk) load_tile(kt + 3, s1);
+      compute(1);
+      if (kt + 2 < nk) store_tile(0, s0);
+      __syncthreads();
+    }
+  } else {
+    // Residual epilogues (conv3: K <= 512, mostly one or two K-tiles) keep their
+    // registers for the residual prefetch instead: one register stage (a second would
+    // push them past 256 VGPR+AGPR, i.e. below two waves per SIMD).
+    __syncthreads();
+    for (unsigned kt = 0; kt < nk; kt++) {
+      if (kt + 1 < nk) load_tile(kt + 1, s0);
+      compute(kt & 1);
+      if (kt + 1 < nk) store_tile((kt & 1) ^ 1, s0);
+      __syncthreads();
+    }
   }
 
   // Accumulators -> LDS (fp32, row-major [128][BN + 4]); C/D map of 16x16x32:
