@@ -21,7 +21,7 @@ import torch.nn.functional as F
 
 from ..shim.native import lib_path
 
-OPS = os.environ.get("VGPU_OPS_LIB", "libvgpu_ops.so")  # libvgpu_ops_deep.so: pipeline A/B variant
+OPS = os.environ.get("VGPU_OPS_LIB", "libvgpu_ops.so")  # override: A/B builds of the ops library
 ACT = {"none": 0, "relu": 1, "relu6": 2}
 _lib = None
 

@@ -34,9 +34,8 @@
 //   * v_mfma_f32_16x16x32_bf16: each wave owns a (128/WM) x (BN/WN) sub-tile as
 //     FM x FN 16x16 accumulators. Both operands are K-contiguous, so one lane's
 //     fragment (8 consecutive k of one row) is a single 16-byte LDS read.
-//   * Global -> registers -> LDS staging, double-buffered LDS and two register stages:
-//     tile k+2's loads are in flight while tile k feeds the MFMAs and tile k+1 waits in
-//     registers for its LDS buffer; one barrier per K-step. Padding rows
+//   * Global -> registers -> LDS staging, double-buffered: the next K-tile's loads are in
+//     flight while the current one feeds the MFMAs; one barrier per K-step. Padding rows
 //     load from a valid address and are zeroed after the load (a select, not a branch
 //     around the load, so the loads stay in flight together).
 //   * LDS rows are 128 B (64 bf16); the 16-B chunk index is XOR-swizzled with
@@ -64,14 +63,6 @@ namespace {
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 using f32x4 = float __attribute__((ext_vector_type(4)));
 using bf16x8 = __bf16 __attribute__((ext_vector_type(8)));
-
-// Two register stages (tile k+2 in flight while tile k computes) for the non-residual
-// epilogues: costs occupancy (BN=128: 1 wave/SIMD instead of 2), so it is a build-time
-// choice measured by benchmarks/conv_bench.py (libvgpu_ops_deep.so) rather than the default.
-#ifndef VGPU_CONV_DEEP_PIPELINE
-#define VGPU_CONV_DEEP_PIPELINE 0
-#endif
-constexpr bool kDeepPipeline = VGPU_CONV_DEEP_PIPELINE != 0;
 
 constexpr int kBM = 128;
 constexpr int kBK = 64;
@@ -192,9 +183,7 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
     w_dst[i] = r * 8u + swz(r, ch);
   }
 
-  // One K-tile in registers on its way to LDS. Two of them are in flight: the loads for
-  // tile k+2 are issued while tile k feeds the MFMAs and tile k+1 waits to be stored, so
-  // a load has two compute phases to land instead of one.
+  // One K-tile in registers on its way to LDS.
   struct Stage {
     u32x4 ra[kALoads], rw[kWLoads];
     // Prologue parameters: a thread's A chunks all hold channels (tid & 7) * 8 .. + 7 of
@@ -280,7 +269,7 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
   };
 
   const unsigned nk = K / kBK;
-  Stage s0, s1;
+  Stage s0;
   load_tile(0, s0);
   // The residual tile does not depend on the GEMM: its loads go out right behind the
   // first K-tile's, so they are in flight together and complete under the MFMAs instead
@@ -300,34 +289,15 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
     }
   }
   store_tile(0, s0);
-  if constexpr (kEpi < 2 && kDeepPipeline) {
-    if (nk > 1) load_tile(1, s1);
+  __syncthreads();
+  // One register stage: tile k+1's loads are in flight while tile k feeds the MFMAs. A
+  // second stage (tile k+2 in flight) was measured slower on every ResNet-50 layer: it
+  // needs 32 more VGPRs per stage and drops BN=128 to one wave per SIMD (profiles/r1t).
+  for (unsigned kt = 0; kt < nk; kt++) {
+    if (kt + 1 < nk) load_tile(kt + 1, s0);
+    compute(kt & 1);
+    if (kt + 1 < nk) store_tile((kt & 1) ^ 1, s0);
     __syncthreads();
-    // Invariant at step kt: LDS buffer kt&1 holds tile kt; the other register stage holds
-    // tile kt+1 (in flight); the stage that held tile kt is free and receives tile kt+2.
-    // Unrolled by two so both stages stay in registers (no dynamic indexing).
-    for (unsigned kt = 0; kt < nk; kt += 2) {
-      if (kt + 2 < nk) load_tile(kt + 2, s0);
-      compute(0);
-      if (kt + 1 < nk) store_tile(1, s1);
-      __syncthreads();
-      if (kt + 1 >= nk) break;
-      if (kt + 3 < nk) load_tile(kt + 3, s1);
-      compute(1);
-      if (kt + 2 < nk) store_tile(0, s0);
-      __syncthreads();
-    }
-  } else {
-    // Residual epilogues (conv3: K <= 512, mostly one or two K-tiles) keep their
-    // registers for the residual prefetch instead: one register stage (a second would
-    // push them past 256 VGPR+AGPR, i.e. below two waves per SIMD).
-    __syncthreads();
-    for (unsigned kt = 0; kt < nk; kt++) {
-      if (kt + 1 < nk) load_tile(kt + 1, s0);
-      compute(kt & 1);
-      if (kt + 1 < nk) store_tile((kt & 1) ^ 1, s0);
-      __syncthreads();
-    }
   }
 
   // Accumulators -> LDS (fp32, row-major [128][BN + 4]); C/D map of 16x16x32:
