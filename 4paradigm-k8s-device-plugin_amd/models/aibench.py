@@ -296,13 +296,17 @@ class Runner:
             self.opt = torch.optim.SGD(model.parameters(), lr=1e-3, momentum=0.9)
         else:
             model.eval()
-            if fuse and isinstance(model, (ResNetV2, DeepLabV3Plus)) and dtype == torch.bfloat16 and channels_last:
-                # Inference epilogues fused into one HIP pass each (ops/fused.py); BN
-                # scale/shift are derived in fp32 before the weights are cast.
-                from ..ops.fused import fuse_conv_bn_act, fuse_resnet_v2
+            if fuse and isinstance(model, (ResNetV2, DeepLabV3Plus, VGG16)) and dtype == torch.bfloat16 \
+                    and channels_last:
+                # Inference epilogues fused into the producing conv or one HIP pass each
+                # (ops/fused.py); BN scale/shift and conv biases are taken in fp32 before
+                # the weights are cast.
+                from ..ops.fused import fuse_conv_bn_act, fuse_conv_relu, fuse_resnet_v2
                 impl = "hip" if self.device.type == "cuda" else "torch"
                 if isinstance(model, ResNetV2):
                     model = fuse_resnet_v2(model, impl=impl)
+                elif isinstance(model, VGG16):
+                    model = fuse_conv_relu(model, impl=impl)
                 else:
                     model = fuse_conv_bn_act(model, impl=impl)
                 for m in model.modules():
@@ -313,7 +317,7 @@ class Runner:
             self.x = self.x.to(dtype)
             self.opt = None
         self.fused = fuse and not case.train and (type(model).__name__ == "FusedResNetV2" or any(
-            type(m).__name__ == "ConvBNAct" for m in model.modules()))
+            type(m).__name__ in ("ConvBNAct", "ConvBiasAct") for m in model.modules()))
         self.model = model
 
     def capture(self, warmup=3):

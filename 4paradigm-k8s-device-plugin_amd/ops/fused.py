@@ -303,10 +303,13 @@ def stem_pool_bn_act(x, w192, scale, shift):
     return y
 
 
-def is_mfma_conv(conv):
-    """A bias-free dense convolution the MFMA kernel tiles: channels multiples of 64,
-    square stride and symmetric padding smaller than the kernel, no dilation."""
-    if not isinstance(conv, nn.Conv2d) or conv.groups != 1 or conv.bias is not None or conv.dilation != (1, 1):
+def is_mfma_conv(conv, allow_bias=False):
+    """A dense convolution the MFMA kernel tiles: channels multiples of 64, square stride
+    and symmetric padding smaller than the kernel, no dilation, no bias (unless the
+    caller folds it into the epilogue shift)."""
+    if not isinstance(conv, nn.Conv2d) or conv.groups != 1 or conv.dilation != (1, 1):
+        return False
+    if conv.bias is not None and not allow_bias:
         return False
     if conv.in_channels % 64 or conv.out_channels % 64 or not isinstance(conv.padding, tuple):
         return False
@@ -493,6 +496,64 @@ class FusedResNetV2(nn.Module):
 def fuse_resnet_v2(model, impl="hip", mfma_conv=None):
     model.eval()
     return FusedResNetV2(model, impl, mfma_conv).eval()
+
+
+class ConvBiasAct(nn.Module):
+    """Conv2d(+bias) + ReLU as one MFMA kernel (:func:`conv_nhwc` with scale 1 and the
+    bias as shift): the VGG pattern. Falls back to library conv + ReLU for shapes the
+    kernel does not tile; in "auto" mode (env ``VGPU_MFMA_CONV``) the first forward per
+    input shape times both and keeps the faster."""
+
+    def __init__(self, conv, act="relu", impl="hip", mfma_conv=None):
+        super().__init__()
+        self.conv, self.act, self.impl = conv, act, impl
+        self.mode = mfma_conv or os.environ.get("VGPU_MFMA_CONV", os.environ.get("VGPU_CONV1X1", "auto"))
+        bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(conv.out_channels)
+        self.register_buffer("shift", bias.contiguous())
+        self.register_buffer("scale", torch.ones(conv.out_channels))
+        self.eligible = is_mfma_conv(conv, allow_bias=True)
+        self.plan = {}
+        self._w = None
+
+    def _library(self, x):
+        return _act_torch(self.conv(x), self.act)
+
+    def _fused(self, x):
+        w = self.conv.weight
+        if self._w is None or self._w[0] != w.data_ptr() or self._w[1] != w.dtype:
+            self._w = (w.data_ptr(), w.dtype, conv_weight_2d(w.detach()))
+        return conv_nhwc(x, w, self.conv.stride[0], self.conv.padding[0], self.scale, self.shift, act=self.act,
+                         w2d=self._w[2])
+
+    def forward(self, x):
+        ok = (self.eligible and self.impl == "hip" and self.mode != "off" and x.is_cuda and x.dtype == torch.bfloat16
+              and x.is_contiguous(memory_format=torch.channels_last))
+        if not ok:
+            return self._library(x)
+        if self.mode == "on":
+            return self._fused(x)
+        key = tuple(x.shape)
+        d = self.plan.get(key)
+        if d is None:
+            if torch.cuda.is_current_stream_capturing():
+                return self._fused(x)
+            d = self.plan[key] = _time_us(lambda: self._fused(x)) <= _time_us(lambda: self._library(x))
+        return self._fused(x) if d else self._library(x)
+
+
+def fuse_conv_relu(model, impl="hip", mfma_conv=None):
+    """In-place inference rewrite of every (Conv2d, ReLU) pair inside a Sequential into a
+    :class:`ConvBiasAct` (the ReLU becomes Identity)."""
+    model.eval()
+    for child in model.children():
+        if isinstance(child, nn.Sequential):
+            mods = list(child)
+            for j in range(len(mods) - 1):
+                if isinstance(mods[j], nn.Conv2d) and isinstance(mods[j + 1], nn.ReLU):
+                    child[j] = ConvBiasAct(mods[j], "relu", impl, mfma_conv)
+                    child[j + 1] = nn.Identity()
+        fuse_conv_relu(child, impl, mfma_conv)
+    return model
 
 
 class ConvBNAct(nn.Module):

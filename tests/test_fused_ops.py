@@ -303,3 +303,37 @@ def test_recurrent_training_capture_is_refused():
     r.device = torch.device("cuda", 0)  # only the policy check runs
     with pytest.raises(NotImplementedError):
         r.capture()
+
+
+def test_fuse_conv_relu_rewrites_vgg_cpu():
+    from amdvgpu.models.aibench import VGG16
+    from amdvgpu.ops.fused import ConvBiasAct, fuse_conv_relu
+    torch.manual_seed(0)
+    m = VGG16(num_classes=10).eval()
+    x = torch.randn(1, 3, 64, 64)
+    with torch.no_grad():
+        ref = m(x)
+        f = fuse_conv_relu(m, impl="torch")
+        got = f(x)
+    assert sum(isinstance(mod, ConvBiasAct) for mod in f.modules()) == 13
+    torch.testing.assert_close(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["on", "auto"])
+def test_vgg16_fused_matches_eager_bf16(mode):
+    from amdvgpu.models.aibench import VGG16
+    from amdvgpu.ops.fused import fuse_conv_relu
+    import copy
+    torch.manual_seed(0)
+    m = VGG16().eval().to("cuda", memory_format=torch.channels_last)
+    x = torch.randn(2, 3, 224, 224, device="cuda").contiguous(memory_format=torch.channels_last)
+    with torch.inference_mode():
+        ref = m(x)
+        f = fuse_conv_relu(copy.deepcopy(m), impl="hip", mfma_conv=mode)
+        for mod in f.modules():
+            if isinstance(mod, (nn.Conv2d, nn.Linear)):
+                mod.to(torch.bfloat16)
+        got = f(x.to(torch.bfloat16)).float()
+    cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0)
+    assert cos > 0.99, cos
