@@ -91,6 +91,7 @@ def bn_act(x, scale, shift, residual=None, act="relu", write_sum=False, post=Fal
     if residual is not None:
         if residual.shape != x.shape or residual.dtype != x.dtype or residual.stride() != x.stride():
             raise ValueError("residual must match x in shape, dtype and layout")
+    _same_device(x, scale, shift, residual)
     stream = torch.cuda.current_stream(x.device).cuda_stream
     if post:
         if residual is None or write_sum:
@@ -113,6 +114,14 @@ def bn_act(x, scale, shift, residual=None, act="relu", write_sum=False, post=Fal
 
 def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _same_device(x, *tensors):
+    """Every tensor handed to a kernel must live on x's GPU: a host (or other-device)
+    pointer would be dereferenced by the kernel and fault the GPU."""
+    for t in tensors:
+        if t is not None and t.device != x.device:
+            raise ValueError(f"tensor on {t.device} passed to a kernel running on {x.device}")
 
 
 def conv1x1_reference(x, w2d, scale=None, shift=None, residual=None, act="relu"):
@@ -160,6 +169,7 @@ def conv1x1(x, w2d, scale=None, shift=None, residual=None, act="relu", write_sum
         raise ValueError("write_sum needs a residual")
     s = torch.empty_like(y) if write_sum else None
     epi = 0 if scale is None else 1 if residual is None else 3 if write_sum else 2
+    _same_device(x, w2d, scale, shift, residual)
     stream = torch.cuda.current_stream(x.device).cuda_stream
     rc = _ops().vgpu_conv1x1_bf16(_ptr(x), _ptr(w2d), _ptr(scale), _ptr(shift), _ptr(residual), _ptr(y), _ptr(s),
                                   N * H * W, cout, K, epi, ACT[act], C.c_void_p(stream))
@@ -246,6 +256,7 @@ def conv_nhwc(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, 
         epi = 1
     else:
         epi = 4 if post else 3 if write_sum else 2
+    _same_device(x, w2d, scale, shift, residual, ps, pt)
     stream = torch.cuda.current_stream(x.device).cuda_stream
     rc = _ops().vgpu_conv_nhwc_bf16(_ptr(x), _ptr(w2d), _ptr(scale), _ptr(shift), _ptr(residual), _ptr(y), _ptr(s),
                                     _ptr(ps), _ptr(pt), N, H, W, Cin, cout, kh, kw, stride, padding, epi, ACT[act],
@@ -296,6 +307,7 @@ def stem_pool_bn_act(x, w192, scale, shift):
     ch, cw = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     ph, pw = (ch - 1) // 2 + 1, (cw - 1) // 2 + 1
     y = torch.empty((N, 64, ph, pw), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    _same_device(x, w192, scale, shift)
     stream = torch.cuda.current_stream(x.device).cuda_stream
     rc = _ops().vgpu_stem_bf16(_ptr(x), _ptr(w192), _ptr(scale), _ptr(shift), _ptr(y), N, H, W, C.c_void_p(stream))
     if rc != 0:
@@ -508,9 +520,10 @@ class ConvBiasAct(nn.Module):
         super().__init__()
         self.conv, self.act, self.impl = conv, act, impl
         self.mode = mfma_conv or os.environ.get("VGPU_MFMA_CONV", os.environ.get("VGPU_CONV1X1", "auto"))
-        bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(conv.out_channels)
+        dev = conv.weight.device
+        bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(conv.out_channels, device=dev)
         self.register_buffer("shift", bias.contiguous())
-        self.register_buffer("scale", torch.ones(conv.out_channels))
+        self.register_buffer("scale", torch.ones(conv.out_channels, device=dev))
         self.eligible = is_mfma_conv(conv, allow_bias=True)
         self.plan = {}
         self._w = None

@@ -185,6 +185,17 @@ def test_conv_prologue_and_sum_only_numerics(nhw, k, n):
 
 
 @pytest.mark.gpu
+def test_kernels_reject_host_tensors():
+    """A CPU parameter tensor must raise before any launch (its pointer would fault the GPU)."""
+    x = torch.zeros(1, 64, 4, 4, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.zeros(64, 64, 3, 3, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        conv_nhwc(x, w, 1, 1, torch.ones(64), torch.zeros(64, device="cuda"))
+    with pytest.raises(ValueError):
+        bn_act(x, torch.ones(64), torch.zeros(64, device="cuda"))
+
+
+@pytest.mark.gpu
 def test_conv1x1_rejects_unsupported_shapes():
     x = torch.zeros(1, 96, 4, 4, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     with pytest.raises(ValueError):
@@ -303,6 +314,13 @@ def test_recurrent_training_capture_is_refused():
     r.device = torch.device("cuda", 0)  # only the policy check runs
     with pytest.raises(NotImplementedError):
         r.capture()
+
+
+def test_conv_bias_act_buffers_follow_the_conv_device():
+    from amdvgpu.ops.fused import ConvBiasAct
+    conv = torch.nn.Conv2d(64, 64, 3, padding=1).to("meta")
+    m = ConvBiasAct(conv)
+    assert m.scale.device == conv.weight.device and m.shift.device == conv.weight.device
 
 
 def test_fuse_conv_relu_rewrites_vgg_cpu():
