@@ -1,28 +1,129 @@
 // Allocation probe linked against libamdhip64 the normal way (global symbol scope), so
 // every HIP call goes through the preloaded shim exactly like a C++/HIP application's
 // would (ctypes lookups with a library handle would bypass the interposer).
-//   hip_alloc_probe managed   hipMallocManaged 1.5 GiB, 1 GiB, free, 1 GiB  -> JSON rcs
-//   hip_alloc_probe malloc    hipMalloc the same sequence                   -> JSON rcs
+//
+//   hip_alloc_probe <kind>   allocate 1.5 GiB, then 1 GiB, free the first, 1 GiB again
+//                            -> one JSON line with the return codes and hipMemGetInfo
+//
+// kinds (SURVEY.md §7.4 "choke-point completeness": every HIP device allocation API must
+// reach the quota):
+//   malloc     hipMalloc
+//   managed    hipMallocManaged (reference class (a): cuMemAllocManaged)
+//   pitch      hipMallocPitch (1 MiB rows; reference cuMemAllocPitch_v2)
+//   3d         hipMalloc3D
+//   ext        hipExtMallocWithFlags(hipDeviceMallocDefault)
+//   async      hipMallocAsync / hipFreeAsync on a stream (default stream-ordered pool,
+//              trimmed after the free so the pool returns the memory)
+//   vmm        hipMemCreate / hipMemRelease (virtual memory management handles)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstring>
 
+namespace {
+
+enum Kind { kMalloc, kManaged, kPitch, k3d, kExt, kAsync, kVmm };
+
+struct Slot {
+  void* p = nullptr;
+  hipMemGenericAllocationHandle_t h{};
+  bool live = false;
+};
+
+hipStream_t g_stream = nullptr;
+size_t g_gran = 1;
+
+int alloc(Kind k, Slot& s, size_t n) {
+  hipError_t e = hipSuccess;
+  switch (k) {
+    case kMalloc: e = hipMalloc(&s.p, n); break;
+    case kManaged: e = hipMallocManaged(&s.p, n, hipMemAttachGlobal); break;
+    case kPitch: {
+      size_t pitch = 0;
+      e = hipMallocPitch(&s.p, &pitch, 1u << 20, n >> 20);
+      break;
+    }
+    case k3d: {
+      hipPitchedPtr pp{};
+      e = hipMalloc3D(&pp, make_hipExtent(1u << 20, n >> 20, 1));
+      s.p = pp.ptr;
+      break;
+    }
+    case kExt: e = hipExtMallocWithFlags(&s.p, n, hipDeviceMallocDefault); break;
+    case kAsync:
+      e = hipMallocAsync(&s.p, n, g_stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(g_stream);
+      break;
+    case kVmm: {
+      hipMemAllocationProp prop{};
+      prop.type = hipMemAllocationTypePinned;
+      prop.location.type = hipMemLocationTypeDevice;
+      prop.location.id = 0;
+      e = hipMemCreate(&s.h, (n + g_gran - 1) / g_gran * g_gran, &prop, 0);
+      break;
+    }
+  }
+  s.live = e == hipSuccess;
+  return (int)e;
+}
+
+int release(Kind k, Slot& s) {
+  if (!s.live) return 0;
+  hipError_t e = hipSuccess;
+  switch (k) {
+    case kVmm: e = hipMemRelease(s.h); break;
+    case kAsync: {
+      e = hipFreeAsync(s.p, g_stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(g_stream);
+      hipMemPool_t pool = nullptr;
+      if (e == hipSuccess) e = hipDeviceGetDefaultMemPool(&pool, 0);
+      if (e == hipSuccess) e = hipMemPoolTrimTo(pool, 0);
+      break;
+    }
+    default: e = hipFree(s.p); break;
+  }
+  s.live = false;
+  return (int)e;
+}
+
+}  // namespace
+
 int main(int argc, char** argv) {
-  bool managed = argc > 1 && !strcmp(argv[1], "managed");
-  void *a = nullptr, *b = nullptr, *d = nullptr;
-  auto alloc = [&](void** p, size_t n) -> int {
-    return managed ? (int)hipMallocManaged(p, n, hipMemAttachGlobal) : (int)hipMalloc(p, n);
-  };
-  int r1 = alloc(&a, 1536ull << 20);
-  int r2 = alloc(&b, 1024ull << 20);
-  int f1 = (int)hipFree(a);
-  int r3 = alloc(&d, 1024ull << 20);
+  const char* name = argc > 1 ? argv[1] : "malloc";
+  const struct {
+    const char* n;
+    Kind k;
+  } kinds[] = {{"malloc", kMalloc}, {"managed", kManaged}, {"pitch", kPitch}, {"3d", k3d},
+               {"ext", kExt},       {"async", kAsync},     {"vmm", kVmm}};
+  Kind k = kMalloc;
+  bool found = false;
+  for (const auto& e : kinds)
+    if (!strcmp(name, e.n)) k = e.k, found = true;
+  if (!found) {
+    fprintf(stderr, "unknown kind %s\n", name);
+    return 2;
+  }
+  if (k == kAsync && hipStreamCreate(&g_stream) != hipSuccess) return 3;
+  if (k == kVmm) {
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = 0;
+    if (hipMemGetAllocationGranularity(&g_gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess ||
+        g_gran == 0)
+      return 4;
+  }
+  Slot a, b, d;
+  int r1 = alloc(k, a, 1536ull << 20);
+  int r2 = alloc(k, b, 1024ull << 20);
+  int f1 = release(k, a);
+  int r3 = alloc(k, d, 1024ull << 20);
   size_t free_b = 0, total_b = 0;
   (void)hipMemGetInfo(&free_b, &total_b);
-  printf("{\"r1\": %d, \"r2\": %d, \"f1\": %d, \"r3\": %d, \"free\": %zu, \"total\": %zu}\n", r1, r2, f1, r3, free_b,
-         total_b);
-  if (b) (void)hipFree(b);
-  if (d) (void)hipFree(d);
+  printf("{\"kind\": \"%s\", \"r1\": %d, \"r2\": %d, \"f1\": %d, \"r3\": %d, \"free\": %zu, \"total\": %zu}\n", name,
+         r1, r2, f1, r3, free_b, total_b);
+  release(k, b);
+  release(k, d);
+  if (g_stream) (void)hipStreamDestroy(g_stream);
   return 0;
 }

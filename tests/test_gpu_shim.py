@@ -256,10 +256,12 @@ emit(locs=sorted(cu_census(nblocks=8192, spin_us=300)))
         assert len({l[0] for l in locs}) == 8
 
 
-@pytest.mark.parametrize("kind", ["managed", "malloc"])
+@pytest.mark.parametrize("kind", ["managed", "malloc", "pitch", "3d", "ext", "async", "vmm"])
 def test_hip_allocations_are_accounted(tmp_region, kind):
-    """A plain HIP program (linked normally against libamdhip64) under a 2 GiB quota:
-    1.5 GiB fits, +1 GiB is refused, after freeing the first block 1 GiB fits again."""
+    """A plain HIP program (linked normally against libamdhip64) under a 2 GiB quota, for
+    every HIP device allocation API (malloc, managed, pitch, 3D, ext flags, stream-ordered
+    async pool, VMM handles): 1.5 GiB fits, +1 GiB is refused, after freeing the first
+    block 1 GiB fits again."""
     import json
     import subprocess
     from amdvgpu.shim.launcher import apply_contract
