@@ -34,6 +34,8 @@ extern "C" hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t globalW
 using LaunchKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t);
 using CoopKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, unsigned int, hipStream_t);
 using MallocManagedFn = hipError_t (*)(void**, size_t, unsigned int);
+using MallocAsyncFn = hipError_t (*)(void**, size_t, hipStream_t);
+using MallocFromPoolAsyncFn = hipError_t (*)(void**, size_t, hipMemPool_t, hipStream_t);
 using ExtLaunchKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t, hipEvent_t, hipEvent_t,
                                          int);
 
@@ -259,6 +261,66 @@ hipError_t hipMallocManaged(void** dev_ptr, size_t size, unsigned int flags) {
   std::lock_guard<std::mutex> g(s.alloc_mu);
   s.managed[key] = AllocRec{size, dev, kMemData};
   return e;
+}
+
+// Stream-ordered allocations (hipMallocAsync / hipMallocFromPoolAsync) come from a HIP
+// memory pool that grows through hsa_amd_vmem_handle_create in chunks; the quota is
+// enforced there like for every other allocation. But when a chunk is refused, the HIP
+// runtime of ROCm 7.x does not unwind the partly grown request and crashes (measured:
+// hip_alloc_probe async segfaults right after the refused chunk, profiles/r1w). So such a
+// request is admitted here, before the pool grows: it proceeds when the quota has room
+// for all of it (plus one pool chunk of slack), or when the pool's cached free memory
+// (reserved - used) can hold it; otherwise the caller gets hipErrorOutOfMemory, as for
+// any refused allocation.
+namespace {
+
+constexpr uint64_t kPoolSlack = 64ull << 20;
+
+bool async_admissible(hipMemPool_t pool, size_t size) {
+  ShimState& s = shim();
+  if (!s.active || size == 0) return true;
+  int dev = 0;
+  if (s.n_agents > 1) {
+    VGPU_REAL_HIP(hipGetDevice);
+    if (!real_hipGetDevice || real_hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= s.n_agents) dev = 0;
+  }
+  const uint64_t lim = s.region.limit(dev);
+  if (!lim || config().oversubscribe) return true;
+  if (s.region.usage(dev) + size + kPoolSlack <= lim) return true;
+  if (!pool) {
+    VGPU_REAL_HIP(hipDeviceGetMemPool);
+    if (!real_hipDeviceGetMemPool || real_hipDeviceGetMemPool(&pool, dev) != hipSuccess) pool = nullptr;
+  }
+  if (pool) {
+    VGPU_REAL_HIP(hipMemPoolGetAttribute);
+    uint64_t reserved = 0, used = 0;
+    if (real_hipMemPoolGetAttribute &&
+        real_hipMemPoolGetAttribute(pool, hipMemPoolAttrReservedMemCurrent, &reserved) == hipSuccess &&
+        real_hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, &used) == hipSuccess && reserved >= used &&
+        size <= reserved - used)
+      return true;  // served from memory the pool already holds (and the quota counts)
+  }
+  VLOG_WARN("device %d OOM (stream-ordered): request %zu bytes, usage %lu of limit %lu", dev, size,
+            (unsigned long)s.region.usage(dev), (unsigned long)lim);
+  return false;
+}
+
+}  // namespace
+
+hipError_t hipMallocAsync(void** dev_ptr, size_t size, hipStream_t stream) {
+  VGPU_REAL_HIP_T(hipMallocAsync, MallocAsyncFn);
+  if (!real_hipMallocAsync) return hipErrorNotSupported;
+  gate_suspend();
+  if (!async_admissible(nullptr, size)) return hipErrorOutOfMemory;
+  return real_hipMallocAsync(dev_ptr, size, stream);
+}
+
+hipError_t hipMallocFromPoolAsync(void** dev_ptr, size_t size, hipMemPool_t mem_pool, hipStream_t stream) {
+  VGPU_REAL_HIP_T(hipMallocFromPoolAsync, MallocFromPoolAsyncFn);
+  if (!real_hipMallocFromPoolAsync) return hipErrorNotSupported;
+  gate_suspend();
+  if (!async_admissible(mem_pool, size)) return hipErrorOutOfMemory;
+  return real_hipMallocFromPoolAsync(dev_ptr, size, mem_pool, stream);
 }
 
 hipError_t hipFree(void* ptr) {

@@ -1,0 +1,14 @@
+set -o pipefail
+OUT=gpurun_out/r1w; mkdir -p $OUT; export TMPDIR=/tmp
+make -C native -j16 > $OUT/build.log 2>&1 || exit 1
+P=4paradigm-k8s-device-plugin_amd/lib
+echo "native async:"; timeout -k 10 60 $P/hip_alloc_probe async > $OUT/native_async.log 2>&1; echo "rc=$?"; tail -2 $OUT/native_async.log
+echo "native vmm:"; timeout -k 10 60 $P/hip_alloc_probe vmm > $OUT/native_vmm.log 2>&1; echo "rc=$?"; tail -2 $OUT/native_vmm.log
+echo "shim async (debug log):"
+VGPU_LOG_LEVEL=4 VGPU_DEVICE_MEMORY_LIMIT=2048m VGPU_SHARED_CACHE=/tmp/probe-a.cache LD_PRELOAD=$PWD/$P/libvgpu_hip.so \
+  timeout -k 10 60 $P/hip_alloc_probe async > $OUT/shim_async.log 2>&1; echo "rc=$?"; tail -25 $OUT/shim_async.log | cut -c1-200
+rm -f /tmp/probe-a.cache
+echo "shim vmm:"
+VGPU_DEVICE_MEMORY_LIMIT=2048m VGPU_SHARED_CACHE=/tmp/probe-v.cache LD_PRELOAD=$PWD/$P/libvgpu_hip.so \
+  timeout -k 10 60 $P/hip_alloc_probe vmm > $OUT/shim_vmm.log 2>&1; echo "rc=$?"; tail -3 $OUT/shim_vmm.log
+true
