@@ -2,8 +2,9 @@
 // every HIP call goes through the preloaded shim exactly like a C++/HIP application's
 // would (ctypes lookups with a library handle would bypass the interposer).
 //
-//   hip_alloc_probe <kind>   allocate 1.5 GiB, then 1 GiB, free the first, 1 GiB again
-//                            -> one JSON line with the return codes and hipMemGetInfo
+//   hip_alloc_probe <kind>   allocate 3/4 of the free memory, then 1/2, free the first,
+//                            1/2 again -> one JSON line with the return codes and
+//                            hipMemGetInfo before and after
 //
 // kinds (SURVEY.md §7.4 "choke-point completeness": every HIP device allocation API must
 // reach the quota):
@@ -113,15 +114,25 @@ int main(int argc, char** argv) {
         g_gran == 0)
       return 4;
   }
+  // Sizes relative to what the device (the vGPU quota) has left after setup: a stream's
+  // hardware queue carries per-process runtime memory (its context-save area is hundreds
+  // of MiB on 256 CUs) that the shim charges to the quota as "context", like the
+  // reference charges the primary context. 3/4 fits, +1/2 does not, 1/2 fits after the
+  // free. Under a 2 GiB quota with no queue: 1.5 GiB, 1 GiB, 1 GiB.
+  size_t free0 = 0, total0 = 0;
+  if (hipMemGetInfo(&free0, &total0) != hipSuccess) return 5;
+  const size_t unit = 2ull << 20;
+  const size_t big = free0 / 4 * 3 / unit * unit, half = free0 / 2 / unit * unit;
   Slot a, b, d;
-  int r1 = alloc(k, a, 1536ull << 20);
-  int r2 = alloc(k, b, 1024ull << 20);
+  int r1 = alloc(k, a, big);
+  int r2 = alloc(k, b, half);
   int f1 = release(k, a);
-  int r3 = alloc(k, d, 1024ull << 20);
+  int r3 = alloc(k, d, half);
   size_t free_b = 0, total_b = 0;
   (void)hipMemGetInfo(&free_b, &total_b);
-  printf("{\"kind\": \"%s\", \"r1\": %d, \"r2\": %d, \"f1\": %d, \"r3\": %d, \"free\": %zu, \"total\": %zu}\n", name,
-         r1, r2, f1, r3, free_b, total_b);
+  printf("{\"kind\": \"%s\", \"r1\": %d, \"r2\": %d, \"f1\": %d, \"r3\": %d, \"free0\": %zu, \"free\": %zu, "
+         "\"total\": %zu}\n",
+         name, r1, r2, f1, r3, free0, free_b, total_b);
   release(k, b);
   release(k, d);
   if (g_stream) (void)hipStreamDestroy(g_stream);
