@@ -74,10 +74,33 @@ def summarize(runs, title):
     return "\n".join(lines) + "\n"
 
 
+def summarize_all(runs, title):
+    """One row per (run, kernel name): dispatches, mean duration and the per-dispatch mean
+    of every counter present."""
+    lines = [f"# {title}", ""]
+    for label, path in runs:
+        data = load(path)
+        names = sorted({c for d in data.values() for c in d if c not in ("name", "dur_ns")})
+        by = collections.defaultdict(list)
+        for d in data.values():
+            by[d["name"]].append(d)
+        lines += [f"## {label}", "", "| kernel | dispatches | mean us | " + " | ".join(names) + " |",
+                  "|---|---|---|" + "---|" * len(names)]
+        for kname, ds in sorted(by.items(), key=lambda kv: -sum(d.get("dur_ns", 0) for d in kv[1])):
+            durs = [d["dur_ns"] for d in ds if "dur_ns" in d]
+            short = (kname if len(kname) < 70 else kname[:67] + "...").replace("|", "\\|")
+            vals = [sum(d.get(c, 0.0) for d in ds) / len(ds) for c in names]
+            lines.append(f"| `{short}` | {len(ds)} | {(sum(durs) / len(durs) / 1e3) if durs else float('nan'):.1f} | "
+                         + " | ".join(f"{v:.4g}" for v in vals) + " |")
+        lines.append("")
+    return "\n".join(lines) + "\n"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("runs", nargs="+", help="label=path (path may be a glob)")
     ap.add_argument("--title", default="rocprofv3 --pmc summary")
+    ap.add_argument("--all-counters", action="store_true", help="per-kernel table of every counter in the CSVs")
     ap.add_argument("-o", "--out")
     a = ap.parse_args()
     runs = []
@@ -87,7 +110,7 @@ def main():
         if not paths:
             raise SystemExit(f"no file matches {pat}")
         runs += [(label, p) for p in paths]
-    text = summarize(runs, a.title)
+    text = summarize_all(runs, a.title) if a.all_counters else summarize(runs, a.title)
     if a.out:
         open(a.out, "w").write(text)
     print(text)
