@@ -27,6 +27,8 @@ def _k():
         L.vgpu_cu_census.restype = C.c_int
         L.vgpu_spin.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.vgpu_spin.restype = C.c_int
+        L.vgpu_spin_lds.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.vgpu_spin_lds.restype = C.c_int
         L.vgpu_stream_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.vgpu_stream_copy.restype = C.c_int
         _lib = L
@@ -63,6 +65,16 @@ def spin(nblocks, spin_us, device=None, counter=None):
     rc = _k().vgpu_spin(int(nblocks), int(spin_us), ptr, _stream(torch, device))
     if rc != 0:
         raise RuntimeError(f"vgpu_spin launch failed ({rc})")
+
+
+def spin_lds(nblocks, spin_us, lds_bytes, device=None):
+    """Launches ``nblocks`` workgroups spinning ``spin_us`` each while holding
+    ``lds_bytes`` of LDS (asynchronous): a grid dispatched over many rounds."""
+    import torch
+    device = torch.device(device or "cuda")
+    rc = _k().vgpu_spin_lds(int(nblocks), int(spin_us), int(lds_bytes), _stream(torch, device))
+    if rc != 0:
+        raise RuntimeError(f"vgpu_spin_lds launch failed ({rc})")
 
 
 def stream_copy(dst, src, nbytes=None):

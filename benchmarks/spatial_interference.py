@@ -3,8 +3,11 @@
 CU slices (and, for comparison, unmasked) with two synthetic workloads built from the
 calibration kernels:
 
-* spin   compute-only: single-wave workgroups that spin a fixed time (no memory traffic)
-* copy   memory-only: 16 B/lane stream copy of a 1 GiB buffer
+* spin     compute-only: single-wave workgroups that spin a fixed time (no memory traffic);
+           every workgroup of a launch fits on the slice at once
+* copy     memory-only: 16 B/lane stream copy of a 1 GiB buffer
+* spin-lds compute-only like spin, but each workgroup holds 64 KiB of LDS, so a launch is
+           dispatched over many rounds (the shape of a GEMM/conv grid)
 
 Reports per-tenant time for a fixed amount of work, solo vs concurrent.
 
@@ -29,6 +32,11 @@ def worker(kind, iters, out, go):
         a = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
         b = torch.empty_like(a)
         fn = lambda: stream_copy(b, a)  # noqa: E731
+    elif kind == "spin-lds":
+        # 2 workgroups per CU at a time (64 KiB LDS each), 4096 per launch: like a GEMM
+        # grid, dispatched over many rounds on a CU slice.
+        from amdvgpu.ops import spin_lds
+        fn = lambda: spin_lds(4096, 20, 64 << 10)  # noqa: E731
     else:
         fn = lambda: spin(256 * 8, 200)  # noqa: E731
     for _ in range(5):
@@ -88,12 +96,14 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--go")
     ap.add_argument("--md-out")
+    ap.add_argument("--kinds", default="spin,copy,spin-lds")
     a = ap.parse_args()
     if a.worker:
         return worker(a.kind, a.iters, a.out, a.go)
     n = a.tenants
     rows = []
-    for kind, iters in (("spin", 200), ("copy", 50)):
+    kinds = [(k, {"spin": 200, "copy": 50, "spin-lds": 20}[k]) for k in a.kinds.split(",")]
+    for kind, iters in kinds:
         for masked in (True, False):
             solo = run(kind, n, masked, iters, solo=True)[0]
             conc = run(kind, n, masked, iters)

@@ -8,7 +8,8 @@
 //                     CU the queue may use: the number of distinct CUs observed is
 //                     the spatial partition actually enforced.
 //  * vgpu_spin        fixed-duration workgroups (s_memrealtime, 100 MHz) for
-//                     duty-cycle / temporal-limit measurements.
+//                     duty-cycle / temporal-limit measurements; vgpu_spin_lds the
+//                     same holding dynamic LDS (few workgroups per CU at a time).
 //  * vgpu_stream_copy 16-byte-per-lane grid-stride copy; with the source in spilled
 //                     host memory it measures the oversubscription path's bandwidth.
 //
@@ -43,6 +44,16 @@ __global__ void __launch_bounds__(64) spin_kernel(uint64_t spin_ticks, uint64_t*
   if (threadIdx.x == 0 && done) atomicAdd(reinterpret_cast<unsigned long long*>(done), 1ull);
 }
 
+// Same spin, but each workgroup also holds `dynamic LDS` bytes, so only a few fit on a CU
+// at once: the grid has to be dispatched over many rounds (like a GEMM kernel's), which
+// exposes dispatcher-level interference between CU-masked queues.
+__global__ void __launch_bounds__(64) spin_lds_kernel(uint64_t spin_ticks) {
+  extern __shared__ unsigned char dyn_lds[];
+  uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < spin_ticks) __builtin_amdgcn_s_sleep(1);
+  if (threadIdx.x == 0) dyn_lds[0] = 1;
+}
+
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(256) copy_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src, size_t n) {
@@ -67,6 +78,14 @@ int vgpu_cu_census(uint32_t* out, int nblocks, int spin_us, void* stream) {
 int vgpu_spin(int nblocks, int spin_us, uint64_t* done, void* stream) {
   if (nblocks <= 0) return -1;
   hipLaunchKernelGGL(spin_kernel, dim3(nblocks), dim3(64), 0, (hipStream_t)stream, (uint64_t)spin_us * 100, done);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// `nblocks` single-wave workgroups spinning `spin_us` each while holding `lds_bytes` of LDS.
+int vgpu_spin_lds(int nblocks, int spin_us, int lds_bytes, void* stream) {
+  if (nblocks <= 0 || lds_bytes < 1 || lds_bytes > 160 * 1024) return -1;
+  hipLaunchKernelGGL(spin_lds_kernel, dim3(nblocks), dim3(64), (size_t)lds_bytes, (hipStream_t)stream,
+                     (uint64_t)spin_us * 100);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
