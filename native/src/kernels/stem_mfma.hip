@@ -9,13 +9,16 @@
 // BN 8 us per ResNet-V2-50 step). Here one block computes an 8x8 tile of pooled outputs:
 //
 //   1. its 39x39x3 input window is staged in LDS as planar [c][row][col] (zero padding
-//      at the image border), the 64x192 weight matrix next to it;
+//      at the image border; one thread per input pixel), the 64x192 weight matrix next
+//      to it;
 //   2. the 17x17 conv outputs under the tile (pool windows overlap by one conv row, so
 //      1.13x recompute) are a [289, K] x [K, 64] GEMM on v_mfma_f32_16x16x32_bf16 with
 //      K ordered (kh, c, kw) and kw padded 7 -> 8: a lane's 8-element fragment is then 8
 //      consecutive input columns of one (kh, c) row, i.e. four aligned 4-byte LDS reads
 //      (the stride-2 conv makes every fragment start on an even column);
 //      K = 7 x 3 groups of 8 (+3 zero groups) = 192 = 6 MFMA k-steps;
+//      the product is computed transposed (weights as the A operand) so each lane holds
+//      4 consecutive channels of one pixel;
 //   3. the conv tile is rounded to bf16 into LDS (as the library conv would store it),
 //      max-pooled over 3x3/2 with -inf padding, and BN + ReLU applied in fp32; each lane
 //      writes 8 channels of one pooled pixel with a 16-byte store.
@@ -60,7 +63,7 @@ __device__ __forceinline__ unsigned pack_bf16(float lo, float hi) {
   return (unsigned)__bfloat16_as_ushort(a) | ((unsigned)__bfloat16_as_ushort(b) << 16);
 }
 
-__global__ void __launch_bounds__(kThreads) stem_kernel(const unsigned short* __restrict__ X,
+__global__ void __launch_bounds__(kThreads, 3) stem_kernel(const unsigned short* __restrict__ X,
                                                        const u32x4* __restrict__ Wk, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, u32x4* __restrict__ Y,
                                                        unsigned H, unsigned W, unsigned CH, unsigned CW, unsigned PH,
@@ -76,24 +79,28 @@ __global__ void __launch_bounds__(kThreads) stem_kernel(const unsigned short* __
   const int py0 = (int)(ty * kPT), px0 = (int)(tx * kPT);
   const int ir0 = 4 * py0 - 5, ic0 = 4 * px0 - 5;  // input window origin (conv row 2*py0-1)
 
-  // 1. Input window, NHWC-order walk (coalesced: consecutive threads read consecutive
-  //    bf16 of a row), stored planar; padding and out-of-image pixels are zero. All of a
-  //    thread's loads are issued before any is used (an out-of-window element loads a
-  //    valid address and is zeroed afterwards, so no branch separates the loads): a
-  //    load -> store loop would pay one memory latency per element.
+  // 1. Input window: each thread stages whole input pixels (3 consecutive bf16, one
+  //    address computation per pixel), stored planar; padding and out-of-image pixels are
+  //    zero. All of a thread's loads are issued before any is used (an out-of-window pixel
+  //    loads a valid address and is zeroed afterwards, so no branch separates the loads):
+  //    a load -> store loop would pay one memory latency per element.
   const unsigned short* const ximg = X + (size_t)img * H * W * kCin;
-  constexpr unsigned kElems = kIT * kIP * kCin, kPer = (kElems + kThreads - 1) / kThreads;
-  unsigned short pv[kPer];
+  constexpr unsigned kPix = kIT * kIP, kPer = (kPix + kThreads - 1) / kThreads;
+  unsigned short pv[kPer][kCin];
   unsigned pdst[kPer];
 #pragma unroll
   for (unsigned q = 0; q < kPer; q++) {
-    const unsigned e0 = tid + q * kThreads, e = e0 < kElems ? e0 : kElems - 1u;
-    const unsigned r = e / (kIP * kCin), rem = e - r * (kIP * kCin), col = rem / kCin, c = rem - col * kCin;
+    const unsigned e0 = tid + q * kThreads, e = e0 < kPix ? e0 : kPix - 1u;
+    const unsigned r = e / kIP, col = e - r * kIP;
     const int ih = ir0 + (int)r, iw = ic0 + (int)col;
     const bool ok = (unsigned)ih < H && (unsigned)iw < W;
-    const unsigned short v = ximg[ok ? ((size_t)ih * W + (unsigned)iw) * kCin + c : 0];
-    pv[q] = ok ? v : (unsigned short)0;
-    pdst[q] = e0 < kElems ? (c * kIT + r) * kIP + col : ~0u;
+    const unsigned short* src = ximg + (ok ? ((size_t)ih * W + (unsigned)iw) * kCin : 0);
+#pragma unroll
+    for (int c = 0; c < kCin; c++) {
+      const unsigned short v = src[c];
+      pv[q][c] = ok ? v : (unsigned short)0;
+    }
+    pdst[q] = e0 < kPix ? r * kIP + col : ~0u;
   }
   constexpr unsigned kWPer = kCout * kGroups / kThreads;
   static_assert(kWPer * kThreads == kCout * kGroups, "whole weight loads");
@@ -102,56 +109,73 @@ __global__ void __launch_bounds__(kThreads) stem_kernel(const unsigned short* __
   for (unsigned q = 0; q < kWPer; q++) wv[q] = Wk[tid + q * kThreads];
 #pragma unroll
   for (unsigned q = 0; q < kPer; q++)
-    if (pdst[q] != ~0u) patch[pdst[q]] = pv[q];
+    if (pdst[q] != ~0u) {
+#pragma unroll
+      for (int c = 0; c < kCin; c++) patch[c * (kIT * kIP) + pdst[q]] = pv[q][c];
+    }
 #pragma unroll
   for (unsigned q = 0; q < kWPer; q++) wl[tid + q * kThreads] = wv[q];
   __syncthreads();
 
-  // 2. Conv tile GEMM: wave w owns M-fragments w, w+4, ... (wave-uniform guard).
+  // 2. Conv tile GEMM, computed transposed (D = W . patch^T): lane l16 is a conv pixel
+  //    and the accumulator registers run over channels, so each lane ends up holding 4
+  //    consecutive channels of one pixel (one packed 8-byte LDS store per fragment in
+  //    step 3a instead of four 2-byte ones). The operand reads are the same as for the
+  //    untransposed product: the weight fragment (row = channel) is the A operand, the
+  //    patch fragment (column = pixel) the B operand. Wave w owns pixel fragments w, w+4,
+  //    ... (wave-uniform guard).
   const unsigned h = lane >> 4, l16 = lane & 15u;
   f32x4 acc[5][4];
 #pragma unroll
   for (int i = 0; i < 5; i++)
 #pragma unroll
     for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  unsigned pix_off[5];  // this lane's pixel of fragment i, as an offset into a patch row
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    unsigned p = (wave + 4u * i) * 16u + l16;
+    p = p < (unsigned)kCPix ? p : (unsigned)kCPix - 1u;
+    const unsigned crl = p / kCT, ccl = p - crl * kCT;
+    pix_off[i] = 2u * crl * kIP + 2u * ccl;
+  }
 #pragma unroll
   for (int kk = 0; kk < kGroups / 4; kk++) {
     const unsigned g = kk * 4u + h;            // this lane's K group
     const bool real = g < (unsigned)kRealGroups;
     const unsigned gg = real ? g : 0u;         // zero groups read a valid address, then zeroed
     const unsigned kh = gg / kCin, c = gg - kh * kCin;
-    bf16x8 bfr[4];
+    const unsigned short* const prow = patch + (c * kIT + kh) * kIP;
+    bf16x8 wfr[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) bfr[j] = __builtin_bit_cast(bf16x8, wl[(j * 16u + l16) * kGroups + g]);
+    for (int j = 0; j < 4; j++) wfr[j] = __builtin_bit_cast(bf16x8, wl[(j * 16u + l16) * kGroups + g]);
 #pragma unroll
     for (int i = 0; i < 5; i++) {
       const unsigned mf = wave + 4u * i;
       if (mf >= (unsigned)kMFrags) continue;
-      unsigned p = mf * 16u + l16;
-      p = p < (unsigned)kCPix ? p : (unsigned)kCPix - 1u;
-      const unsigned crl = p / kCT, ccl = p - crl * kCT;
-      const unsigned* src = reinterpret_cast<const unsigned*>(patch + (c * kIT + 2u * crl + kh) * kIP + 2u * ccl);
+      const unsigned* src = reinterpret_cast<const unsigned*>(prow + pix_off[i]);
       u32x4 a{src[0], src[1], src[2], src[3]};
       if (!real) a = u32x4{0u, 0u, 0u, 0u};
-      const bf16x8 af = __builtin_bit_cast(bf16x8, a);
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, a);
 #pragma unroll
-      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[j], pf, acc[i][j], 0, 0, 0);
     }
   }
   __syncthreads();  // the conv tile aliases the input window and weights
 
-  // 3a. Conv tile -> LDS as bf16 (C/D map: channel = l16 in fragment j, pixel = 4h + r).
+  // 3a. Conv tile -> LDS as bf16. Transposed C/D map: pixel = l16 of fragment i,
+  //     channels 16 j + 4 h + r (r = 0..3) in the lane's 4 registers.
 #pragma unroll
   for (int i = 0; i < 5; i++) {
     const unsigned mf = wave + 4u * i;
     if (mf >= (unsigned)kMFrags) continue;
+    const unsigned p = mf * 16u + l16;
+    if (p >= (unsigned)kCPix) continue;
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const unsigned p = mf * 16u + 4u * h + r;
-      if (p >= (unsigned)kCPix) continue;
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        ctile[p * kCTP + j * 16u + l16] = __bfloat16_as_ushort(__float2bfloat16(acc[i][j][r]));
+    for (int j = 0; j < 4; j++) {
+      uint2 v;
+      v.x = pack_bf16(acc[i][j][0], acc[i][j][1]);
+      v.y = pack_bf16(acc[i][j][2], acc[i][j][3]);
+      *reinterpret_cast<uint2*>(ctile + p * kCTP + j * 16u + 4u * h) = v;
     }
   }
   __syncthreads();
