@@ -39,7 +39,7 @@ def _ops():
         L.vgpu_conv1x1_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.vgpu_conv1x1_bf16.restype = C.c_int
-        L.vgpu_conv_nhwc_bf16.argtypes = [C.c_void_p] * 9 + [C.c_int] * 11 + [C.c_void_p]
+        L.vgpu_conv_nhwc_bf16.argtypes = [C.c_void_p] * 9 + [C.c_int] * 12 + [C.c_void_p]
         L.vgpu_conv_nhwc_bf16.restype = C.c_int
         L.vgpu_stem_bf16.argtypes = [C.c_void_p] * 5 + [C.c_int] * 3 + [C.c_void_p]
         L.vgpu_stem_bf16.restype = C.c_int
@@ -206,8 +206,25 @@ def conv_reference(x, w, stride=1, padding=0, scale=None, shift=None, residual=N
     return _act_torch(y, act), s
 
 
+def grid_cap(cout, device=None):
+    """Block cap for :func:`conv_nhwc` inside a CU-masked vGPU: the slice's capacity
+    (CUs x blocks per CU of the chosen tile), so a launch is placed in one round
+    (profiles/r1z: multi-round grids of masked tenants stall each other's dispatch).
+    0 (no cap) outside a spatially limited vGPU. Reads the vGPU contract env
+    (VGPU_DEVICE_CU_LIMIT, VGPU_CU_MODE) the container was started with."""
+    try:
+        pct = int(os.environ.get("VGPU_DEVICE_CU_LIMIT", os.environ.get("VGPU_DEVICE_CU_LIMIT_0", "0")))
+    except ValueError:
+        return 0
+    if not 0 < pct < 100 or os.environ.get("VGPU_CU_MODE", "spatial") not in ("spatial", "both"):
+        return 0
+    cus = torch.cuda.get_device_properties(device if device is not None else torch.cuda.current_device()).multi_processor_count
+    slice_cus = max(8, cus * pct // 100 // 8 * 8)  # masks are XCD-balanced (8 XCDs)
+    return slice_cus * (2 if cout % 128 == 0 else 3)
+
+
 def conv_nhwc(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, act="relu", write_sum=False,
-              post=False, w2d=None, prologue=None):
+              post=False, w2d=None, prologue=None, max_blocks=None):
     """HIP MFMA convolution (``conv_nhwc_mfma.hip``: implicit GEMM over channels-last
     activations) with the epilogue fused: y = act((conv(x, w) [+ residual]) * scale +
     shift), or with ``post`` act(conv * scale + shift + residual), or without scale/shift
@@ -258,9 +275,11 @@ def conv_nhwc(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, 
         epi = 4 if post else 3 if write_sum else 2
     _same_device(x, w2d, scale, shift, residual, ps, pt)
     stream = torch.cuda.current_stream(x.device).cuda_stream
+    if max_blocks is None:
+        max_blocks = grid_cap(cout, x.device)
     rc = _ops().vgpu_conv_nhwc_bf16(_ptr(x), _ptr(w2d), _ptr(scale), _ptr(shift), _ptr(residual), _ptr(y), _ptr(s),
                                     _ptr(ps), _ptr(pt), N, H, W, Cin, cout, kh, kw, stride, padding, epi, ACT[act],
-                                    C.c_void_p(stream))
+                                    int(max_blocks), C.c_void_p(stream))
     if rc != 0:
         raise RuntimeError(f"vgpu_conv_nhwc_bf16 failed ({rc}) for x {tuple(x.shape)} w {tuple(w.shape)}")
     return (y, s) if write_sum else y

@@ -87,6 +87,7 @@ struct ConvArgs {
   void* s;
   const float* pscale;  // prologue (1x1 path): A = relu(X * pscale + pshift), or null
   const float* pshift;
+  int max_blocks;       // grid cap (persistent blocks), 0 = one block per tile
   ConvGeom g;
 };
 
@@ -122,11 +123,11 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned ntiles) {
 //       pre-activation BN + ReLU applied while staging, rounded to bf16 as a separate
 //       pass would store it), so the producer never writes that activation to HBM.
 template <int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro>
-__global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict__ X, const u32x4* __restrict__ Wt,
-                                                       const float* __restrict__ scale, const float* __restrict__ shift,
-                                                       const u32x4* __restrict__ R, u32x4* __restrict__ Y,
-                                                       u32x4* __restrict__ S, const float* __restrict__ pscale,
-                                                       const float* __restrict__ pshift, const ConvGeom p) {
+__device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32x4* __restrict__ Wt,
+                                          const float* __restrict__ scale, const float* __restrict__ shift,
+                                          const u32x4* __restrict__ R, u32x4* __restrict__ Y, u32x4* __restrict__ S,
+                                          const float* __restrict__ pscale, const float* __restrict__ pshift,
+                                          const ConvGeom& p, const unsigned tile) {
   static_assert(!(kPro && kIm2col), "prologue only on the 1x1 path");
   static_assert(WM * WN == kThreads / 64, "4 waves");
   constexpr int FM = kBM / WM / 16;
@@ -143,7 +144,6 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
 
   const unsigned M = p.M, N = p.N, K = p.K;
   const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const unsigned tile = xcd_remap(blockIdx.x, p.ntiles);
   const unsigned m0 = (tile / p.tiles_n) * kBM, n0 = (tile % p.tiles_n) * BN;
   const size_t kvec = K >> 3;  // row stride of W (and of A on the 1x1 path) in 16-B chunks
 
@@ -363,6 +363,24 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict_
   }
 }
 
+// One tile per block, or persistent when the grid is capped below the tile count: on a
+// CU-masked vGPU the cap is the slice's block capacity, so the whole grid is placed in
+// one round and this tenant's dispatch never waits for room on its slice while holding
+// up the other tenants' dispatches (profiles/r1z). The grid is a multiple of 8 when
+// capped, so every tile a block visits keeps the block's XCD in xcd_remap.
+template <int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro>
+__global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict__ X, const u32x4* __restrict__ Wt,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       const u32x4* __restrict__ R, u32x4* __restrict__ Y,
+                                                       u32x4* __restrict__ S, const float* __restrict__ pscale,
+                                                       const float* __restrict__ pshift, const ConvGeom p) {
+  for (unsigned t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+    conv_tile<BN, WM, WN, kEpi, kAct, kIm2col, kPro>(X, Wt, scale, shift, R, Y, S, pscale, pshift, p,
+                                                      xcd_remap(t, p.ntiles));
+    __syncthreads();  // the next tile's staging overwrites this tile's epilogue image in LDS
+  }
+}
+
 template <int BN, int WM, int WN, int kEpi, int kAct>
 int launch(ConvArgs a, bool im2col, hipStream_t stream) {
   ConvGeom g = a.g;
@@ -376,7 +394,10 @@ int launch(ConvArgs a, bool im2col, hipStream_t stream) {
     if constexpr (kEpi == 1 && kAct == 1) kern = conv_kernel<BN, WM, WN, kEpi, kAct, false, true>;
     else return -1;
   }
-  hipLaunchKernelGGL(kern, dim3(g.ntiles), dim3(kThreads), 0, stream, static_cast<const u32x4*>(a.x),
+  unsigned grid = g.ntiles;
+  if (a.max_blocks > 0 && (unsigned)a.max_blocks < grid) grid = a.max_blocks < 8 ? 8u : (unsigned)a.max_blocks / 8u * 8u;
+  if (grid > g.ntiles) grid = g.ntiles;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, stream, static_cast<const u32x4*>(a.x),
                      static_cast<const u32x4*>(a.w), a.scale, a.shift, static_cast<const u32x4*>(a.r),
                      static_cast<u32x4*>(a.y), static_cast<u32x4*>(a.s), a.pscale, a.pshift, g);
   return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -414,11 +435,12 @@ extern "C" {
 // 1 act(acc*scale+shift), 2 act((acc+r)*scale+shift), 3 as 2 and sum = acc + r,
 // 4 act(acc*scale + shift + r), 5 acc + r. act: 0 none, 1 relu, 2 relu6. scale/shift:
 // fp32[Cout]. pscale/pshift (optional, fp32[C], 1x1 stride-1 with epi 1 + relu only): the
-// input is read as relu(x * pscale + pshift). Returns 0 on success, -1 on bad arguments,
+// input is read as relu(x * pscale + pshift). max_blocks > 0 caps the grid (persistent
+// blocks; rounded down to a multiple of 8). Returns 0 on success, -1 on bad arguments,
 // -2 on launch failure.
 int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const float* shift, const void* r, void* y,
                         void* sum, const float* pscale, const float* pshift, int nb, int h, int wd, int c, int cout,
-                        int kh, int kw, int stride, int pad, int epi, int act, void* stream) {
+                        int kh, int kw, int stride, int pad, int epi, int act, int max_blocks, void* stream) {
   if (!x || !w || !y || nb <= 0 || h <= 0 || wd <= 0 || c <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
       pad < 0 || pad >= kh || pad >= kw)
     return -1;
@@ -440,6 +462,7 @@ int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const 
   ConvArgs a{};
   a.pscale = pscale;
   a.pshift = pshift;
+  a.max_blocks = max_blocks < 0 ? 0 : max_blocks;
   a.x = x;
   a.w = w;
   a.scale = scale;
@@ -469,7 +492,7 @@ int vgpu_conv1x1_bf16(const void* x, const void* w, const float* scale, const fl
                       void* sum, int64_t M, int N, int K, int epi, int act, void* stream) {
   if (M <= 0 || M >= ((int64_t)1 << 31)) return -1;
   return vgpu_conv_nhwc_bf16(x, w, scale, shift, r, y, sum, nullptr, nullptr, (int)M, 1, 1, K, N, 1, 1, 1, 0, epi, act,
-                             stream);
+                             0, stream);
 }
 
 }  // extern "C"

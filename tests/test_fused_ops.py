@@ -6,8 +6,8 @@ import torch.nn as nn
 
 from amdvgpu.models.aibench import ResNetV2, resnet_v2_50
 from amdvgpu.ops.fused import (FusedResNetV2, bn_act, bn_act_reference, bn_scale_shift, conv1x1,
-                                conv1x1_reference, conv_nhwc, conv_reference, stem_pool_bn_act, stem_reference,
-                                stem_weight)
+                                conv1x1_reference, conv_nhwc, conv_reference, grid_cap, stem_pool_bn_act,
+                                stem_reference, stem_weight)
 
 
 def _randomize_bn(model, g):
@@ -182,6 +182,39 @@ def test_conv_prologue_and_sum_only_numerics(nhw, k, n):
     s = conv_nhwc(x, w, residual=r)
     s_ref, _ = conv_reference(x, w, residual=r)
     torch.testing.assert_close(s.float(), s_ref, rtol=2e-2, atol=3e-2)
+
+
+def test_grid_cap_follows_the_vgpu_cu_share(monkeypatch):
+    class Props:
+        multi_processor_count = 256
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d: Props())
+    monkeypatch.delenv("VGPU_DEVICE_CU_LIMIT", raising=False)
+    assert grid_cap(256, 0) == 0                       # not in a vGPU
+    monkeypatch.setenv("VGPU_DEVICE_CU_LIMIT", "100")
+    assert grid_cap(256, 0) == 0                       # whole GPU
+    monkeypatch.setenv("VGPU_DEVICE_CU_LIMIT", "25")
+    assert grid_cap(256, 0) == 64 * 2 and grid_cap(192, 0) == 64 * 3
+    monkeypatch.setenv("VGPU_CU_MODE", "temporal")
+    assert grid_cap(256, 0) == 0                       # no CU mask in temporal mode
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [8, 24, 130])
+def test_conv_persistent_grid_numerics(cap):
+    """Capped (persistent) grids: every block loops over several tiles."""
+    g = torch.Generator().manual_seed(15)
+    for (N, cin, H, W, cout, k, st, pad) in [(2, 64, 22, 22, 128, 3, 1, 1), (3, 128, 17, 13, 64, 1, 1, 0),
+                                             (2, 64, 15, 15, 192, 3, 2, 1)]:
+        x = torch.randn(N, cin, H, W, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        w = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to("cuda", torch.bfloat16)
+        w = w.contiguous(memory_format=torch.channels_last)
+        oh, ow = (H + 2 * pad - k) // st + 1, (W + 2 * pad - k) // st + 1
+        r = torch.randn(N, cout, oh, ow, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        sc, sh = (torch.rand(cout, generator=g) + 0.5).cuda(), torch.randn(cout, generator=g).cuda()
+        y, s = conv_nhwc(x, w, st, pad, sc, sh, r, "relu", write_sum=True, max_blocks=cap)
+        y_ref, s_ref = conv_reference(x, w, st, pad, sc, sh, r, "relu")
+        torch.testing.assert_close(y.float(), y_ref, rtol=2e-2, atol=3e-2)
+        torch.testing.assert_close(s.float(), s_ref, rtol=2e-2, atol=3e-2)
 
 
 @pytest.mark.gpu
