@@ -43,6 +43,13 @@ def _ops():
         L.vgpu_conv_nhwc_bf16.restype = C.c_int
         L.vgpu_stem_bf16.argtypes = [C.c_void_p] * 5 + [C.c_int] * 3 + [C.c_void_p]
         L.vgpu_stem_bf16.restype = C.c_int
+        L.vgpu_stem_set_block_cap.argtypes = [C.c_int]
+        L.vgpu_bn_act_set_block_cap.argtypes = [C.c_int]
+        # Inside a CU-masked vGPU every kernel's grid is capped to one dispatch round on
+        # the slice (see grid_cap): persistent stem 2 blocks/CU, elementwise 8 blocks/CU.
+        slice_cus = grid_cap(128) // 2
+        L.vgpu_stem_set_block_cap(slice_cus * 2)
+        L.vgpu_bn_act_set_block_cap(slice_cus * 8)
         _lib = L
     return _lib
 

@@ -146,6 +146,8 @@ __global__ void __launch_bounds__(256) bn_act_kernel(const u32x4* __restrict__ x
   }
 }
 
+int g_block_cap = 0;  // vgpu_bn_act_set_block_cap
+
 template <int kAdd, bool kWriteSum, int kAct>
 void launch(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum, unsigned nvec,
             unsigned cvec, hipStream_t stream) {
@@ -153,6 +155,9 @@ void launch(const void* x, const void* r, const float* scale, const float* shift
   // lane does at least a couple of iterations on large tensors.
   unsigned blocks = (nvec + 511u) / 512u;
   if (blocks > 256u * 16u) blocks = 256u * 16u;
+  // Inside a CU-masked vGPU: no more blocks than the slice holds at once (one dispatch
+  // round, profiles/r1z); the grid-stride loop covers the rest.
+  if (g_block_cap > 0 && blocks > (unsigned)g_block_cap) blocks = (unsigned)g_block_cap;
   if (blocks < 1u) blocks = 1u;
   if (256u % cvec == 0u) {  // stride = blocks * 256 is then a multiple of cvec
     hipLaunchKernelGGL((bn_act_kernel<kAdd, kWriteSum, kAct, true>), dim3(blocks), dim3(256), 0, stream,
@@ -201,6 +206,9 @@ static int bn_act_impl(const void* x, const void* r, const float* scale, const f
     default: return -1;
   }
 }
+
+// Caps the elementwise grid at `blocks` (0 = default sizing).
+void vgpu_bn_act_set_block_cap(int blocks) { g_block_cap = blocks < 0 ? 0 : blocks; }
 
 int vgpu_bn_act_bf16(const void* x, const void* r, const float* scale, const float* shift, void* y, void* sum,
                      int64_t numel, int channels, int act, void* stream) {

@@ -63,18 +63,18 @@ __device__ __forceinline__ unsigned pack_bf16(float lo, float hi) {
   return (unsigned)__bfloat16_as_ushort(a) | ((unsigned)__bfloat16_as_ushort(b) << 16);
 }
 
-__global__ void __launch_bounds__(kThreads, 3) stem_kernel(const unsigned short* __restrict__ X,
-                                                       const u32x4* __restrict__ Wk, const float* __restrict__ scale,
-                                                       const float* __restrict__ shift, u32x4* __restrict__ Y,
-                                                       unsigned H, unsigned W, unsigned CH, unsigned CW, unsigned PH,
-                                                       unsigned PW, unsigned tiles_x, unsigned tiles_per_img) {
+__device__ __forceinline__ void stem_tile(const unsigned short* __restrict__ X, const u32x4* __restrict__ Wk,
+                                          const float* __restrict__ scale, const float* __restrict__ shift,
+                                          u32x4* __restrict__ Y, unsigned H, unsigned W, unsigned CH, unsigned CW,
+                                          unsigned PH, unsigned PW, unsigned tiles_x, unsigned tiles_per_img,
+                                          unsigned bid) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLds];
   unsigned short* const patch = reinterpret_cast<unsigned short*>(smem);       // [3][39][40]
   u32x4* const wl = reinterpret_cast<u32x4*>(smem + kPatchBytes);              // [64][24] 16-B groups
   unsigned short* const ctile = reinterpret_cast<unsigned short*>(smem);       // [289][72] after the GEMM
 
   const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const unsigned img = blockIdx.x / tiles_per_img, t = blockIdx.x - img * tiles_per_img;
+  const unsigned img = bid / tiles_per_img, t = bid - img * tiles_per_img;
   const unsigned ty = t / tiles_x, tx = t - ty * tiles_x;
   const int py0 = (int)(ty * kPT), px0 = (int)(tx * kPT);
   const int ir0 = 4 * py0 - 5, ic0 = 4 * px0 - 5;  // input window origin (conv row 2*py0-1)
@@ -221,6 +221,31 @@ __global__ void __launch_bounds__(kThreads, 3) stem_kernel(const unsigned short*
   }
 }
 
+// One pooled tile per block (3 blocks per CU: 122 VGPRs, no spill).
+__global__ void __launch_bounds__(kThreads, 3) stem_kernel(const unsigned short* __restrict__ X,
+                                                          const u32x4* __restrict__ Wk, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, u32x4* __restrict__ Y,
+                                                          unsigned H, unsigned W, unsigned CH, unsigned CW,
+                                                          unsigned PH, unsigned PW, unsigned tiles_x,
+                                                          unsigned tiles_per_img, unsigned ntiles) {
+  stem_tile(X, Wk, scale, shift, Y, H, W, CH, CW, PH, PW, tiles_x, tiles_per_img, blockIdx.x);
+}
+
+// Persistent variant for a capped grid (CU-masked vGPU: one dispatch round on the slice,
+// profiles/r1z). The tile loop raises register use, so it gets its own build (2 blocks
+// per CU) instead of slowing down the uncapped kernel.
+__global__ void __launch_bounds__(kThreads) stem_kernel_persistent(
+    const unsigned short* __restrict__ X, const u32x4* __restrict__ Wk, const float* __restrict__ scale,
+    const float* __restrict__ shift, u32x4* __restrict__ Y, unsigned H, unsigned W, unsigned CH, unsigned CW,
+    unsigned PH, unsigned PW, unsigned tiles_x, unsigned tiles_per_img, unsigned ntiles) {
+  for (unsigned b = blockIdx.x; b < ntiles; b += gridDim.x) {
+    stem_tile(X, Wk, scale, shift, Y, H, W, CH, CW, PH, PW, tiles_x, tiles_per_img, b);
+    __syncthreads();  // the next tile's input window overwrites this tile's conv image
+  }
+}
+
+int g_stem_block_cap = 0;  // vgpu_stem_set_block_cap
+
 }  // namespace
 
 extern "C" {
@@ -241,10 +266,17 @@ int vgpu_stem_bf16(const void* x, const void* w, const float* scale, const float
   const unsigned tiles_x = (pw + kPT - 1) / kPT, tiles_y = (ph + kPT - 1) / kPT;
   const uint64_t blocks = (uint64_t)n * tiles_x * tiles_y;
   if (blocks >= (1ull << 31)) return -1;
-  hipLaunchKernelGGL(stem_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+  unsigned grid = (unsigned)blocks;
+  const bool capped = g_stem_block_cap > 0 && (unsigned)g_stem_block_cap < grid;
+  if (capped) grid = (unsigned)g_stem_block_cap;
+  hipLaunchKernelGGL(capped ? stem_kernel_persistent : stem_kernel, dim3(grid), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
                      static_cast<const unsigned short*>(x), static_cast<const u32x4*>(w), scale, shift,
-                     static_cast<u32x4*>(y), (unsigned)h, (unsigned)wd, ch, cw, ph, pw, tiles_x, tiles_x * tiles_y);
+                     static_cast<u32x4*>(y), (unsigned)h, (unsigned)wd, ch, cw, ph, pw, tiles_x, tiles_x * tiles_y,
+                     (unsigned)blocks);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// Caps the stem grid at `blocks` (persistent blocks; 0 = one block per pooled tile).
+void vgpu_stem_set_block_cap(int blocks) { g_stem_block_cap = blocks < 0 ? 0 : blocks; }
 
 }  // extern "C"

@@ -218,6 +218,33 @@ def test_conv_persistent_grid_numerics(cap):
 
 
 @pytest.mark.gpu
+def test_capped_stem_and_elementwise_grids():
+    """Persistent stem and capped elementwise grids (as inside a CU-masked vGPU) give the
+    same results as the uncapped launches."""
+    from amdvgpu.ops.fused import _ops
+    g = torch.Generator().manual_seed(16)
+    x = torch.randn(2, 3, 70, 61, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, generator=g) / 147 ** 0.5).to("cuda", torch.bfloat16)
+    sc, sh = (torch.rand(64, generator=g) + 0.5).cuda(), torch.randn(64, generator=g).cuda()
+    r = torch.randn(3, 256, 9, 7, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    s2, t2 = (torch.rand(256, generator=g) + 0.5).cuda(), torch.randn(256, generator=g).cuda()
+    ref_stem = stem_pool_bn_act(x, stem_weight(w), sc, sh)
+    ref_bn = bn_act(r, s2, t2, r, write_sum=True)
+    L = _ops()
+    try:
+        L.vgpu_stem_set_block_cap(8)
+        L.vgpu_bn_act_set_block_cap(3)
+        got_stem = stem_pool_bn_act(x, stem_weight(w), sc, sh)
+        got_bn = bn_act(r, s2, t2, r, write_sum=True)
+    finally:
+        L.vgpu_stem_set_block_cap(0)
+        L.vgpu_bn_act_set_block_cap(0)
+    torch.testing.assert_close(got_stem, ref_stem, rtol=0, atol=0)
+    torch.testing.assert_close(got_bn[0], ref_bn[0], rtol=0, atol=0)
+    torch.testing.assert_close(got_bn[1], ref_bn[1], rtol=0, atol=0)
+
+
+@pytest.mark.gpu
 def test_kernels_reject_host_tensors():
     """A CPU parameter tensor must raise before any launch (its pointer would fault the GPU)."""
     x = torch.zeros(1, 64, 4, 4, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
