@@ -217,8 +217,11 @@ class LSTMSentiment(nn.Module):
         super().__init__()
         self.lstm = nn.LSTM(features, hidden, batch_first=True)
         self.fc = nn.Linear(hidden, num_classes)
+        self.last = None  # inference: ops.fused.FusedLSTMLast (the last hidden state only)
 
     def forward(self, x):
+        if self.last is not None:
+            return self.fc(self.last(x))
         out, _ = self.lstm(x)
         return self.fc(out[:, -1])
 
@@ -296,7 +299,12 @@ class Runner:
             self.opt = torch.optim.SGD(model.parameters(), lr=1e-3, momentum=0.9)
         else:
             model.eval()
-            if fuse and isinstance(model, (ResNetV2, DeepLabV3Plus, VGG16)) and dtype == torch.bfloat16 \
+            if fuse and isinstance(model, LSTMSentiment) and dtype == torch.bfloat16 and self.device.type == "cuda":
+                # Whole-sequence recurrence in one HIP kernel (ops/fused.py::FusedLSTMLast).
+                from ..ops.fused import FusedLSTMLast
+                model.last = FusedLSTMLast(model.lstm)
+                model.fc.to(dtype)
+            elif fuse and isinstance(model, (ResNetV2, DeepLabV3Plus, VGG16)) and dtype == torch.bfloat16 \
                     and channels_last:
                 # Inference epilogues fused into the producing conv or one HIP pass each
                 # (ops/fused.py); BN scale/shift and conv biases are taken in fp32 before
@@ -317,7 +325,7 @@ class Runner:
             self.x = self.x.to(dtype)
             self.opt = None
         self.fused = fuse and not case.train and (type(model).__name__ == "FusedResNetV2" or any(
-            type(m).__name__ in ("ConvBNAct", "ConvBiasAct") for m in model.modules()))
+            type(m).__name__ in ("ConvBNAct", "ConvBiasAct", "FusedLSTMLast") for m in model.modules()))
         self.model = model
 
     def capture(self, warmup=3):

@@ -43,6 +43,8 @@ def _ops():
         L.vgpu_conv_nhwc_bf16.restype = C.c_int
         L.vgpu_stem_bf16.argtypes = [C.c_void_p] * 5 + [C.c_int] * 3 + [C.c_void_p]
         L.vgpu_stem_bf16.restype = C.c_int
+        L.vgpu_lstm_seq_bf16.argtypes = [C.c_void_p] * 6 + [C.c_int] * 3 + [C.c_void_p]
+        L.vgpu_lstm_seq_bf16.restype = C.c_int
         L.vgpu_stem_set_block_cap.argtypes = [C.c_int]
         L.vgpu_bn_act_set_block_cap.argtypes = [C.c_int]
         # Inside a CU-masked vGPU every kernel's grid is capped to one dispatch round on
@@ -593,6 +595,83 @@ def fuse_conv_relu(model, impl="hip", mfma_conv=None):
                     child[j + 1] = nn.Identity()
         fuse_conv_relu(child, impl, mfma_conv)
     return model
+
+
+def lstm_recurrence(gx, whh, h0=None, c0=None):
+    """HIP LSTM recurrence (``lstm_mfma.hip``) over a whole sequence: ``gx`` [B, T, 128, 4]
+    bf16 gate inputs (x . W_ih^T + b, gates i, f, g, o of a unit adjacent), ``whh`` the
+    [512, 128] bf16 weight_hh. Returns (h_T, c_T) fp32 [B, 128]."""
+    if gx.dtype != torch.bfloat16 or not gx.is_cuda or gx.dim() != 4 or gx.shape[2:] != (128, 4):
+        raise TypeError("gx must be a [B, T, 128, 4] bf16 CUDA tensor")
+    if not gx.is_contiguous() or tuple(whh.shape) != (512, 128) or whh.dtype != torch.bfloat16 or not whh.is_contiguous():
+        raise ValueError("gx must be contiguous and whh a contiguous [512, 128] bf16 matrix")
+    B, T = gx.shape[:2]
+    for t in (h0, c0):
+        if t is not None and (t.dtype != torch.float32 or tuple(t.shape) != (B, 128) or not t.is_contiguous()):
+            raise ValueError("h0/c0 must be contiguous fp32 [B, 128]")
+    hT = torch.empty(B, 128, dtype=torch.float32, device=gx.device)
+    cT = torch.empty_like(hT)
+    _same_device(gx, whh, h0, c0)
+    stream = torch.cuda.current_stream(gx.device).cuda_stream
+    rc = _ops().vgpu_lstm_seq_bf16(_ptr(gx), _ptr(whh), _ptr(h0), _ptr(c0), _ptr(hT), _ptr(cT), B, T, 128,
+                                   C.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"vgpu_lstm_seq_bf16 failed ({rc}) for gx {tuple(gx.shape)}")
+    return hT, cT
+
+
+class FusedLSTMLast(nn.Module):
+    """Inference form of a single-layer, unidirectional, batch-first ``nn.LSTM`` with 128
+    hidden units whose caller only needs the last hidden state (the sentiment model):
+    one library GEMM for the input projection of every step (W_ih rows permuted so a
+    unit's four gates are adjacent), then the whole recurrence in one HIP kernel. The
+    original module stays as the library path for "off" / "auto" (``VGPU_MFMA_CONV``
+    governs the in-pod kernels)."""
+
+    def __init__(self, lstm, impl="hip", mode=None):
+        super().__init__()
+        if (lstm.num_layers != 1 or lstm.bidirectional or not lstm.batch_first or lstm.hidden_size != 128
+                or not lstm.bias or getattr(lstm, "proj_size", 0)):
+            raise ValueError("FusedLSTMLast needs a 1-layer, unidirectional, batch-first LSTM with 128 units")
+        self.lstm, self.impl = lstm, impl
+        self.mode = mode or os.environ.get("VGPU_MFMA_CONV", os.environ.get("VGPU_CONV1X1", "auto"))
+        H, Fin = lstm.hidden_size, lstm.input_size
+        w = lstm.weight_ih_l0.detach().float().view(4, H, Fin).permute(1, 0, 2).reshape(4 * H, Fin)
+        b = (lstm.bias_ih_l0.detach().float() + lstm.bias_hh_l0.detach().float()).view(4, H).t().reshape(4 * H)
+        self.register_buffer("w_ih_perm", w.contiguous())
+        self.register_buffer("b_perm", b.contiguous())
+        self.plan = {}
+        self._cast = None
+
+    def _fused(self, x):
+        if self._cast is None or self._cast[0] != x.dtype:
+            self._cast = (x.dtype, self.w_ih_perm.to(x.dtype).t(), self.b_perm.to(x.dtype),
+                          self.lstm.weight_hh_l0.detach().to(x.dtype).contiguous())
+        _, wt, b, whh = self._cast
+        B, T, Fin = x.shape
+        gx = torch.addmm(b, x.reshape(B * T, Fin), wt).view(B, T, 128, 4)
+        hT, _ = lstm_recurrence(gx, whh)
+        return hT.to(x.dtype)
+
+    def _library(self, x):
+        if next(self.lstm.parameters()).dtype != x.dtype:
+            self.lstm.to(x.dtype)
+        out, _ = self.lstm(x)
+        return out[:, -1]
+
+    def forward(self, x):
+        ok = self.impl == "hip" and self.mode != "off" and x.is_cuda and x.dtype == torch.bfloat16
+        if not ok:
+            return self._library(x)
+        if self.mode == "on":
+            return self._fused(x)
+        key = tuple(x.shape)
+        d = self.plan.get(key)
+        if d is None:
+            if torch.cuda.is_current_stream_capturing():
+                return self._fused(x)
+            d = self.plan[key] = _time_us(lambda: self._fused(x)) <= _time_us(lambda: self._library(x))
+        return self._fused(x) if d else self._library(x)
 
 
 class ConvBNAct(nn.Module):
