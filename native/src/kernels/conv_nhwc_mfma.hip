@@ -30,7 +30,8 @@
 // went 1.15-1.65x faster).
 //
 // Kernel shape (CDNA4-first, not a CUDA warp tiling):
-//   * 256 threads = 4 wave64s; block tile 128 (M) x BN (64 or 128), K-step 64.
+//   * 256 threads = 4 wave64s; block tile BM (128, or 64 when 128-row tiles would leave
+//     the chip under-filled) x BN (64 or 128), K-step 64.
 //   * v_mfma_f32_16x16x32_bf16: each wave owns a (128/WM) x (BN/WN) sub-tile as
 //     FM x FN 16x16 accumulators. Both operands are K-contiguous, so one lane's
 //     fragment (8 consecutive k of one row) is a single 16-byte LDS read.
@@ -64,7 +65,6 @@ using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 using f32x4 = float __attribute__((ext_vector_type(4)));
 using bf16x8 = __bf16 __attribute__((ext_vector_type(8)));
 
-constexpr int kBM = 128;
 constexpr int kBK = 64;
 constexpr int kThreads = 256;
 
@@ -122,7 +122,7 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned ntiles) {
 // kPro (1x1 path): the A operand is relu(X * pscale[c] + pshift[c]) (the consumer's
 //       pre-activation BN + ReLU applied while staging, rounded to bf16 as a separate
 //       pass would store it), so the producer never writes that activation to HBM.
-template <int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro>
+template <int BM, int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro>
 __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32x4* __restrict__ Wt,
                                           const float* __restrict__ scale, const float* __restrict__ shift,
                                           const u32x4* __restrict__ R, u32x4* __restrict__ Y, u32x4* __restrict__ S,
@@ -130,21 +130,21 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
                                           const ConvGeom& p, const unsigned tile) {
   static_assert(!(kPro && kIm2col), "prologue only on the 1x1 path");
   static_assert(WM * WN == kThreads / 64, "4 waves");
-  constexpr int FM = kBM / WM / 16;
+  constexpr int FM = BM / WM / 16;
   constexpr int FN = BN / WN / 16;
-  constexpr int kAStage = kBM * kBK * 2;  // bytes per buffer
+  constexpr int kAStage = BM * kBK * 2;  // bytes per buffer
   constexpr int kWStage = BN * kBK * 2;
   constexpr int kStage = 2 * (kAStage + kWStage);
   constexpr int kCStride = BN + 4;  // fp32 epilogue tile row stride (16-B multiple)
-  constexpr int kEpiBytes = kBM * kCStride * 4;
+  constexpr int kEpiBytes = BM * kCStride * 4;
   constexpr int kLds = kStage > kEpiBytes ? kStage : kEpiBytes;
-  constexpr int kALoads = kBM * 8 / kThreads;  // 16-B chunks per thread per K-tile
+  constexpr int kALoads = BM * 8 / kThreads;  // 16-B chunks per thread per K-tile
   constexpr int kWLoads = BN * 8 / kThreads;
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLds];
 
   const unsigned M = p.M, N = p.N, K = p.K;
   const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const unsigned m0 = (tile / p.tiles_n) * kBM, n0 = (tile % p.tiles_n) * BN;
+  const unsigned m0 = (tile / p.tiles_n) * BM, n0 = (tile % p.tiles_n) * BN;
   const size_t kvec = K >> 3;  // row stride of W (and of A on the 1x1 path) in 16-B chunks
 
   // Buffer b of each operand (computed, not a pointer table: a table of LDS addresses
@@ -239,7 +239,7 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   };
 
   const unsigned wm = wave / WN, wn = wave % WN;
-  const unsigned row_base = wm * (kBM / WM), col_base = wn * (BN / WN);
+  const unsigned row_base = wm * (BM / WM), col_base = wn * (BN / WN);
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; i++)
@@ -276,8 +276,8 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   // of stalling the epilogue (vmcnt retires loads in order, so the first LDS store only
   // waits for the older A/W loads).
   constexpr unsigned kChunksPerRow = BN / 8;
-  constexpr int kEpiIters = kBM * kChunksPerRow / kThreads;
-  static_assert(kEpiIters * kThreads == kBM * kChunksPerRow, "whole epilogue iterations");
+  constexpr int kEpiIters = BM * kChunksPerRow / kThreads;
+  static_assert(kEpiIters * kThreads == BM * kChunksPerRow, "whole epilogue iterations");
   const size_t nvec = N >> 3;  // output row stride in 16-B chunks
   u32x4 rpre[kEpi >= 2 ? kEpiIters : 1];
   if constexpr (kEpi >= 2) {
@@ -368,30 +368,30 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
 // one round and this tenant's dispatch never waits for room on its slice while holding
 // up the other tenants' dispatches (profiles/r1z). The grid is a multiple of 8 when
 // capped, so every tile a block visits keeps the block's XCD in xcd_remap.
-template <int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro>
+template <int BM, int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro>
 __global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict__ X, const u32x4* __restrict__ Wt,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        const u32x4* __restrict__ R, u32x4* __restrict__ Y,
                                                        u32x4* __restrict__ S, const float* __restrict__ pscale,
                                                        const float* __restrict__ pshift, const ConvGeom p) {
   for (unsigned t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
-    conv_tile<BN, WM, WN, kEpi, kAct, kIm2col, kPro>(X, Wt, scale, shift, R, Y, S, pscale, pshift, p,
+    conv_tile<BM, BN, WM, WN, kEpi, kAct, kIm2col, kPro>(X, Wt, scale, shift, R, Y, S, pscale, pshift, p,
                                                       xcd_remap(t, p.ntiles));
     __syncthreads();  // the next tile's staging overwrites this tile's epilogue image in LDS
   }
 }
 
-template <int BN, int WM, int WN, int kEpi, int kAct>
+template <int BM, int BN, int WM, int WN, int kEpi, int kAct>
 int launch(ConvArgs a, bool im2col, hipStream_t stream) {
   ConvGeom g = a.g;
   g.tiles_n = g.N / BN;
-  g.ntiles = (g.M + kBM - 1) / kBM * g.tiles_n;
-  auto kern = conv_kernel<BN, WM, WN, kEpi, kAct, false, false>;
+  g.ntiles = (g.M + BM - 1) / BM * g.tiles_n;
+  auto kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, false, false>;
   if (im2col) {
-    kern = conv_kernel<BN, WM, WN, kEpi, kAct, true, false>;
+    kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, true, false>;
   } else if (a.pscale) {
     // The prologue exists for the ResNet-V2 conv1 (BN + ReLU epilogue) only.
-    if constexpr (kEpi == 1 && kAct == 1) kern = conv_kernel<BN, WM, WN, kEpi, kAct, false, true>;
+    if constexpr (kEpi == 1 && kAct == 1) kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, false, true>;
     else return -1;
   }
   unsigned grid = g.ntiles;
@@ -403,25 +403,25 @@ int launch(ConvArgs a, bool im2col, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <int BN, int WM, int WN, int kAct>
+template <int BM, int BN, int WM, int WN, int kAct>
 int by_epi(int epi, const ConvArgs& a, bool im2col, hipStream_t st) {
   switch (epi) {
-    case 0: return launch<BN, WM, WN, 0, 0>(a, im2col, st);
-    case 1: return launch<BN, WM, WN, 1, kAct>(a, im2col, st);
-    case 2: return launch<BN, WM, WN, 2, kAct>(a, im2col, st);
-    case 3: return launch<BN, WM, WN, 3, kAct>(a, im2col, st);
-    case 4: return launch<BN, WM, WN, 4, kAct>(a, im2col, st);
-    case 5: return launch<BN, WM, WN, 5, 0>(a, im2col, st);
+    case 0: return launch<BM, BN, WM, WN, 0, 0>(a, im2col, st);
+    case 1: return launch<BM, BN, WM, WN, 1, kAct>(a, im2col, st);
+    case 2: return launch<BM, BN, WM, WN, 2, kAct>(a, im2col, st);
+    case 3: return launch<BM, BN, WM, WN, 3, kAct>(a, im2col, st);
+    case 4: return launch<BM, BN, WM, WN, 4, kAct>(a, im2col, st);
+    case 5: return launch<BM, BN, WM, WN, 5, 0>(a, im2col, st);
     default: return -1;
   }
 }
 
-template <int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN>
 int by_act(int act, int epi, const ConvArgs& a, bool im2col, hipStream_t st) {
   switch (act) {
-    case 0: return by_epi<BN, WM, WN, 0>(epi, a, im2col, st);
-    case 1: return by_epi<BN, WM, WN, 1>(epi, a, im2col, st);
-    case 2: return by_epi<BN, WM, WN, 2>(epi, a, im2col, st);
+    case 0: return by_epi<BM, BN, WM, WN, 0>(epi, a, im2col, st);
+    case 1: return by_epi<BM, BN, WM, WN, 1>(epi, a, im2col, st);
+    case 2: return by_epi<BM, BN, WM, WN, 2>(epi, a, im2col, st);
     default: return -1;
   }
 }
@@ -483,8 +483,13 @@ int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const 
   a.g.pad = (unsigned)pad;
   const bool im2col = !(kh == 1 && kw == 1 && stride == 1 && pad == 0);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (cout % 128 == 0) return by_act<128, 2, 2>(act, epi, a, im2col, st);
-  return by_act<64, 4, 1>(act, epi, a, im2col, st);
+  // Small-M layers (fewer than two 128-row tiles per CU) use 64-row tiles, so the grid
+  // still fills the chip (e.g. ResNet stage 4: 6050 rows x 512 -> 192 vs 380 blocks).
+  const int64_t bn = cout % 128 == 0 ? 128 : 64;
+  const bool small_m = (m + 127) / 128 * (cout / bn) < 512;
+  if (bn == 128)
+    return small_m ? by_act<64, 128, 2, 2>(act, epi, a, im2col, st) : by_act<128, 128, 2, 2>(act, epi, a, im2col, st);
+  return small_m ? by_act<64, 64, 2, 2>(act, epi, a, im2col, st) : by_act<128, 64, 4, 1>(act, epi, a, im2col, st);
 }
 
 // 1x1 / stride-1 convolution over M pixels: y[M, N] = epilogue(x[M, K] . w[N, K]^T).
