@@ -36,9 +36,12 @@
 //     FM x FN 16x16 accumulators. Both operands are K-contiguous, so one lane's
 //     fragment (8 consecutive k of one row) is a single 16-byte LDS read.
 //   * Global -> registers -> LDS staging, double-buffered: the next K-tile's loads are in
-//     flight while the current one feeds the MFMAs; one barrier per K-step. Padding rows
-//     load from a valid address and are zeroed after the load (a select, not a branch
-//     around the load, so the loads stay in flight together).
+//     flight while the current one feeds the MFMAs; one barrier per K-step. Loads go
+//     through raw buffer descriptors: a fixed per-thread voffset plus the K position as
+//     the scalar soffset, and padding taps get an out-of-range voffset, for which the
+//     hardware returns zeros. A select after the load (the first version) made every
+//     K-step wait for its loads before the MFMAs and cost ~90 VALU per K-step in 64-bit
+//     address arithmetic; now the main loop is ~MFMA + LDS only.
 //   * LDS rows are 128 B (64 bf16); the 16-B chunk index is XOR-swizzled with
 //     (row >> 1) & 7 so the 16 lanes of a ds_read_b128 phase hit 16 distinct 16-B slots
 //     of the 256-B bank row (conflict-free), for reads and for the staging writes.
@@ -50,8 +53,9 @@
 //     same XCD and share its L2 copy of the activation rows.
 //
 // Requirements (checked on the host): Cin % 64 == 0, Cout % 64 == 0, 16-byte aligned
-// pointers, input/output/weight element counts below 2^34. Rows past M are clamped on
-// load (they read a valid row) and never stored.
+// pointers, the weight and one image's input and output below 2 GiB (larger batches are
+// split into several launches). Rows past M are clamped on load (they read a valid row)
+// and never stored.
 //
 // C ABI (ctypes): pointers are device pointers, `stream` a hipStream_t.
 #include <hip/hip_bf16.h>
@@ -75,6 +79,7 @@ struct ConvGeom {
   unsigned M, N, K;                             // GEMM: M = Nb*OH*OW, N = Cout, K = KH*KW*C
   unsigned H, W, C, OH, OW, KW, stride, pad;    // geometry (implicit-GEMM path)
   unsigned tiles_n, ntiles;
+  unsigned x_bytes, w_bytes;                    // buffer-descriptor ranges (< 2^31, host-checked)
 };
 
 struct ConvArgs {
@@ -92,6 +97,25 @@ struct ConvArgs {
 };
 
 __device__ __forceinline__ unsigned swz(unsigned row, unsigned chunk) { return chunk ^ ((row >> 1) & 7u); }
+
+// Raw buffer descriptor over [p, p + bytes) (bytes < 2^31). The inputs are made provably
+// wave-uniform so the loads through it are not wrapped in waterfall loops.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  // (readfirstlane returns int: widen through uint32_t, not by sign extension.)
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// A voffset at or past every descriptor's range: the hardware range check returns zeros
+// (the implicit GEMM's padding taps, without a select after the load).
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+}
 
 __device__ __forceinline__ float bf_lo(unsigned v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float bf_hi(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
@@ -145,18 +169,21 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   const unsigned M = p.M, N = p.N, K = p.K;
   const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const unsigned m0 = (tile / p.tiles_n) * BM, n0 = (tile % p.tiles_n) * BN;
-  const size_t kvec = K >> 3;  // row stride of W (and of A on the 1x1 path) in 16-B chunks
 
   // Buffer b of each operand (computed, not a pointer table: a table of LDS addresses
   // would be a static initializer, which the AMDGPU backend cannot emit).
   auto a_lds = [&](int b) { return reinterpret_cast<u32x4*>(smem + b * kAStage); };
   auto w_lds = [&](int b) { return reinterpret_cast<u32x4*>(smem + 2 * kAStage + b * kWStage); };
 
-  // Per-thread staging sources (row, chunk) are fixed across K-tiles; only k moves.
-  const u32x4* a_src[kALoads];
-  int a_ih0[kALoads], a_iw0[kALoads];
+  // Operands are read through buffer descriptors with 32-bit byte offsets: per thread a
+  // fixed voffset, the K position as the scalar soffset, so a K-tile's loads cost no
+  // vector address arithmetic (the host keeps every launch's tensors below 2 GiB).
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(X, p.x_bytes), wr = make_rsrc(Wt, p.w_bytes);
+  const unsigned krow = K * 2u;  // W row (and 1x1 A row) in bytes
+  unsigned a_vo[kALoads];        // 1x1: row start; im2col: current tap's pixel, or kOOB
+  int a_pix[kALoads], a_ih0[kALoads], a_iw0[kALoads];
   unsigned a_dst[kALoads];
-  const size_t cvec = p.C >> 3;  // input pixel stride in 16-B chunks (im2col path)
+  const unsigned cbytes = p.C * 2u;  // input pixel stride (im2col path)
 #pragma unroll
   for (int i = 0; i < kALoads; i++) {
     const unsigned c = tid + i * kThreads, r = c >> 3, ch = c & 7u;
@@ -165,23 +192,29 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
       const unsigned plane = p.OH * p.OW;
       const unsigned img = gm / plane, rem = gm - img * plane;
       const unsigned oh = rem / p.OW, ow = rem - oh * p.OW;
-      a_src[i] = X + (size_t)img * p.H * p.W * cvec + ch;
       a_ih0[i] = (int)(oh * p.stride) - (int)p.pad;
       a_iw0[i] = (int)(ow * p.stride) - (int)p.pad;
+      // Byte offset of the (possibly padding) pixel (ih0, iw0): may be negative, every
+      // in-bounds tap lands inside the tensor.
+      a_pix[i] = (int)(((img * p.H) * p.W) * cbytes) + (a_ih0[i] * (int)p.W + a_iw0[i]) * (int)cbytes + (int)(ch * 16u);
+      a_vo[i] = kOOB;
     } else {
-      a_src[i] = X + (size_t)gm * kvec + ch;
-      a_ih0[i] = a_iw0[i] = 0;
+      a_vo[i] = gm * krow + ch * 16u;
+      a_pix[i] = a_ih0[i] = a_iw0[i] = 0;
     }
     a_dst[i] = r * 8u + swz(r, ch);
   }
-  const u32x4* w_src[kWLoads];
-  unsigned w_dst[kWLoads];
+  unsigned w_vo[kWLoads], w_dst[kWLoads];
 #pragma unroll
   for (int i = 0; i < kWLoads; i++) {
     const unsigned c = tid + i * kThreads, r = c >> 3, ch = c & 7u;
-    w_src[i] = Wt + (size_t)(n0 + r) * kvec + ch;
+    w_vo[i] = (n0 + r) * krow + ch * 16u;
     w_dst[i] = r * 8u + swz(r, ch);
   }
+  // im2col: the K-tile's (kh, kw) tap and channel block, advanced one K-tile per load
+  // (wave-uniform scalars). A tap's bounds checks run once per tap, not per K-tile.
+  const unsigned cpt = p.C / kBK;
+  unsigned t_c0 = 0, t_kw = 0, t_kh = 0;
 
   // One K-tile in registers on its way to LDS.
   struct Stage {
@@ -191,7 +224,7 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
     float ps[kPro ? 8 : 1], pt[kPro ? 8 : 1];
   };
   auto load_tile = [&](unsigned kt, Stage& st) {
-    const size_t off = (size_t)kt * (kBK / 8);
+    const unsigned koff = kt * (kBK * 2u);  // bytes along K
     if constexpr (kPro) {
       const unsigned c0 = kt * kBK + (tid & 7u) * 8u;
       const float4 s0 = *reinterpret_cast<const float4*>(pscale + c0);
@@ -204,23 +237,27 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
       st.pt[4] = t1.x; st.pt[5] = t1.y; st.pt[6] = t1.z; st.pt[7] = t1.w;
     }
     if constexpr (kIm2col) {
-      // Wave-uniform tap of this K-tile: k0 = ((kh * KW) + kw) * C + c0.
-      const unsigned k0 = kt * kBK, tap = k0 / p.C, c0v = (k0 - tap * p.C) >> 3;
-      const int kh = (int)(tap / p.KW), kw = (int)(tap - (unsigned)kh * p.KW);
+      if (t_c0 == 0) {  // first K-tile of a new tap
+        const int toff = ((int)t_kh * (int)p.W + (int)t_kw) * (int)cbytes;
 #pragma unroll
-      for (int i = 0; i < kALoads; i++) {
-        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
-        const bool ok = (unsigned)ih < p.H && (unsigned)iw < p.W;
-        const size_t pix = ok ? (size_t)ih * p.W + (unsigned)iw : 0;
-        const u32x4 v = a_src[i][pix * cvec + c0v];
-        st.ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+        for (int i = 0; i < kALoads; i++) {
+          const bool ok = (unsigned)(a_ih0[i] + (int)t_kh) < p.H && (unsigned)(a_iw0[i] + (int)t_kw) < p.W;
+          a_vo[i] = ok ? (unsigned)(a_pix[i] + toff) : kOOB;
+        }
+      }
+      const unsigned soff = t_c0 * (kBK * 2u);
+#pragma unroll
+      for (int i = 0; i < kALoads; i++) st.ra[i] = ld16(xr, a_vo[i], soff);
+      if (++t_c0 == cpt) {
+        t_c0 = 0;
+        if (++t_kw == p.KW) t_kw = 0, t_kh++;
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < kALoads; i++) st.ra[i] = a_src[i][off];
+      for (int i = 0; i < kALoads; i++) st.ra[i] = ld16(xr, a_vo[i], koff);
     }
 #pragma unroll
-    for (int i = 0; i < kWLoads; i++) st.rw[i] = w_src[i][off];
+    for (int i = 0; i < kWLoads; i++) st.rw[i] = ld16(wr, w_vo[i], koff);
   };
   auto store_tile = [&](int b, Stage& st) {
     if constexpr (kPro) {
@@ -453,43 +490,60 @@ int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const 
   if ((epi == 3) != (sum != nullptr)) return -1;
   const int64_t oh = ((int64_t)h + 2 * pad - kh) / stride + 1, ow = ((int64_t)wd + 2 * pad - kw) / stride + 1;
   if (oh <= 0 || ow <= 0 || h + 2 * pad < kh || wd + 2 * pad < kw) return -1;
-  const int64_t m = (int64_t)nb * oh * ow, k = (int64_t)kh * kw * c, lim = (int64_t)1 << 34;
-  if (m >= ((int64_t)1 << 32) || (int64_t)nb * h * wd * c >= lim || m * cout >= lim || k * cout >= lim) return -1;
+  // Buffer descriptors address with 32-bit offsets below 2^31: the weight must fit, and
+  // larger batches run as several launches over groups of whole images.
+  const int64_t k = (int64_t)kh * kw * c, lim = ((int64_t)1 << 31) - 1;
+  const int64_t img_x = (int64_t)h * wd * c * 2, img_y = oh * ow * cout * 2;
+  if (k * cout * 2 > lim || img_x > lim || img_y > lim) return -1;
   auto misaligned = [](const void* q) { return q && (reinterpret_cast<uintptr_t>(q) & 15u); };
   if (misaligned(x) || misaligned(w) || misaligned(y) || misaligned(r) || misaligned(sum) || misaligned(scale) ||
       misaligned(shift) || misaligned(pscale) || misaligned(pshift))
     return -1;
-  ConvArgs a{};
-  a.pscale = pscale;
-  a.pshift = pshift;
-  a.max_blocks = max_blocks < 0 ? 0 : max_blocks;
-  a.x = x;
-  a.w = w;
-  a.scale = scale;
-  a.shift = shift;
-  a.r = r;
-  a.y = y;
-  a.s = sum;
-  a.g.M = (unsigned)m;
-  a.g.N = (unsigned)cout;
-  a.g.K = (unsigned)k;
-  a.g.H = (unsigned)h;
-  a.g.W = (unsigned)wd;
-  a.g.C = (unsigned)c;
-  a.g.OH = (unsigned)oh;
-  a.g.OW = (unsigned)ow;
-  a.g.KW = (unsigned)kw;
-  a.g.stride = (unsigned)stride;
-  a.g.pad = (unsigned)pad;
+  const int64_t per = lim / (img_x > img_y ? img_x : img_y);  // images per launch
   const bool im2col = !(kh == 1 && kw == 1 && stride == 1 && pad == 0);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // Small-M layers (fewer than two 128-row tiles per CU) use 64-row tiles, so the grid
-  // still fills the chip (e.g. ResNet stage 4: 6050 rows x 512 -> 192 vs 380 blocks).
-  const int64_t bn = cout % 128 == 0 ? 128 : 64;
-  const bool small_m = (m + 127) / 128 * (cout / bn) < 512;
-  if (bn == 128)
-    return small_m ? by_act<64, 128, 2, 2>(act, epi, a, im2col, st) : by_act<128, 128, 2, 2>(act, epi, a, im2col, st);
-  return small_m ? by_act<64, 64, 2, 2>(act, epi, a, im2col, st) : by_act<128, 64, 4, 1>(act, epi, a, im2col, st);
+  for (int64_t i0 = 0; i0 < nb; i0 += per) {
+    const int64_t ni = nb - i0 < per ? nb - i0 : per;
+    auto at = [](const void* q, int64_t off) {
+      return q ? static_cast<const void*>(static_cast<const char*>(q) + off) : nullptr;
+    };
+    ConvArgs a{};
+    a.pscale = pscale;
+    a.pshift = pshift;
+    a.max_blocks = max_blocks < 0 ? 0 : max_blocks;
+    a.x = at(x, i0 * img_x);
+    a.w = w;
+    a.scale = scale;
+    a.shift = shift;
+    a.r = at(r, i0 * img_y);
+    a.y = const_cast<void*>(at(y, i0 * img_y));
+    a.s = const_cast<void*>(at(sum, i0 * img_y));
+    const int64_t m = ni * oh * ow;
+    a.g.M = (unsigned)m;
+    a.g.N = (unsigned)cout;
+    a.g.K = (unsigned)k;
+    a.g.H = (unsigned)h;
+    a.g.W = (unsigned)wd;
+    a.g.C = (unsigned)c;
+    a.g.OH = (unsigned)oh;
+    a.g.OW = (unsigned)ow;
+    a.g.KW = (unsigned)kw;
+    a.g.stride = (unsigned)stride;
+    a.g.pad = (unsigned)pad;
+    a.g.x_bytes = (unsigned)(ni * img_x);
+    a.g.w_bytes = (unsigned)(k * cout * 2);
+    // Small-M layers (fewer than two 128-row tiles per CU) use 64-row tiles, so the grid
+    // still fills the chip (e.g. ResNet stage 4: 6050 rows x 512 -> 192 vs 380 blocks).
+    const int64_t bn = cout % 128 == 0 ? 128 : 64;
+    const bool small_m = (m + 127) / 128 * (cout / bn) < 512;
+    int rc;
+    if (bn == 128)
+      rc = small_m ? by_act<64, 128, 2, 2>(act, epi, a, im2col, st) : by_act<128, 128, 2, 2>(act, epi, a, im2col, st);
+    else
+      rc = small_m ? by_act<64, 64, 2, 2>(act, epi, a, im2col, st) : by_act<128, 64, 4, 1>(act, epi, a, im2col, st);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 // 1x1 / stride-1 convolution over M pixels: y[M, N] = epilogue(x[M, K] . w[N, K]^T).
