@@ -117,6 +117,13 @@ __device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, unsigned voff, u
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
 }
 
+// LDS-DMA: 16 B per lane from the buffer straight into LDS at lds + 16 * lane (`lds` is
+// wave-uniform), no VGPR destination and no ds_write.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, u32x4* lds, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff, (int)soff,
+                                           0, 0);
+}
+
 __device__ __forceinline__ float bf_lo(unsigned v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float bf_hi(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
 
@@ -184,9 +191,15 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   int a_pix[kALoads], a_ih0[kALoads], a_iw0[kALoads];
   unsigned a_dst[kALoads];
   const unsigned cbytes = p.C * 2u;  // input pixel stride (im2col path)
+  // Staging: LDS-DMA except on the prologue path (it transforms A in registers). An
+  // LDS-DMA image is lane-linear (lane l of piece i fills 16-B slot (tid + 256 i) of the
+  // buffer), so the XOR swizzle moves to the source: slot (row r, chunk ch) is loaded
+  // from logical chunk swz(r, ch) (the swizzle is an involution).
+  constexpr bool kDma = !kPro;
+  const unsigned wv = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
   for (int i = 0; i < kALoads; i++) {
-    const unsigned c = tid + i * kThreads, r = c >> 3, ch = c & 7u;
+    const unsigned c = tid + i * kThreads, r = c >> 3, ch = kDma ? swz(r, c & 7u) : (c & 7u);
     const unsigned gm = (m0 + r < M) ? m0 + r : M - 1u;
     if constexpr (kIm2col) {
       const unsigned plane = p.OH * p.OW;
@@ -207,7 +220,7 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   unsigned w_vo[kWLoads], w_dst[kWLoads];
 #pragma unroll
   for (int i = 0; i < kWLoads; i++) {
-    const unsigned c = tid + i * kThreads, r = c >> 3, ch = c & 7u;
+    const unsigned c = tid + i * kThreads, r = c >> 3, ch = kDma ? swz(r, c & 7u) : (c & 7u);
     w_vo[i] = (n0 + r) * krow + ch * 16u;
     w_dst[i] = r * 8u + swz(r, ch);
   }
@@ -218,12 +231,14 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
 
   // One K-tile in registers on its way to LDS.
   struct Stage {
-    u32x4 ra[kALoads], rw[kWLoads];
+    u32x4 ra[kDma ? 1 : kALoads], rw[kDma ? 1 : kWLoads];
     // Prologue parameters: a thread's A chunks all hold channels (tid & 7) * 8 .. + 7 of
     // the K-tile (256 threads cover 8 chunks per row), so one set of 8 per K-tile.
     float ps[kPro ? 8 : 1], pt[kPro ? 8 : 1];
   };
-  auto load_tile = [&](unsigned kt, Stage& st) {
+  // The wave's LDS-DMA destination for piece i of buffer `base`.
+  auto slot = [&](u32x4* base, int i) { return base + wv * 64u + (unsigned)i * kThreads; };
+  auto load_tile = [&](unsigned kt, Stage& st, int b) {
     const unsigned koff = kt * (kBK * 2u);  // bytes along K
     if constexpr (kPro) {
       const unsigned c0 = kt * kBK + (tid & 7u) * 8u;
@@ -247,19 +262,28 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
       }
       const unsigned soff = t_c0 * (kBK * 2u);
 #pragma unroll
-      for (int i = 0; i < kALoads; i++) st.ra[i] = ld16(xr, a_vo[i], soff);
+      for (int i = 0; i < kALoads; i++) {
+        if constexpr (kDma) dma16(xr, slot(a_lds(b), i), a_vo[i], soff);
+        else st.ra[i] = ld16(xr, a_vo[i], soff);
+      }
       if (++t_c0 == cpt) {
         t_c0 = 0;
         if (++t_kw == p.KW) t_kw = 0, t_kh++;
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < kALoads; i++) st.ra[i] = ld16(xr, a_vo[i], koff);
+      for (int i = 0; i < kALoads; i++) {
+        if constexpr (kDma) dma16(xr, slot(a_lds(b), i), a_vo[i], koff);
+        else st.ra[i] = ld16(xr, a_vo[i], koff);
+      }
     }
 #pragma unroll
-    for (int i = 0; i < kWLoads; i++) st.rw[i] = ld16(wr, w_vo[i], koff);
+    for (int i = 0; i < kWLoads; i++) {
+      if constexpr (kDma) dma16(wr, slot(w_lds(b), i), w_vo[i], koff);
+      else st.rw[i] = ld16(wr, w_vo[i], koff);
+    }
   };
-  auto store_tile = [&](int b, Stage& st) {
+  auto store_tile = [&](int b, Stage& st) {  // register path only
     if constexpr (kPro) {
 #pragma unroll
       for (int i = 0; i < kALoads; i++) {
@@ -307,7 +331,7 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
 
   const unsigned nk = K / kBK;
   Stage s0;
-  load_tile(0, s0);
+  load_tile(0, s0, 0);
   // The residual tile does not depend on the GEMM: its loads go out right behind the
   // first K-tile's, so they are in flight together and complete under the MFMAs instead
   // of stalling the epilogue (vmcnt retires loads in order, so the first LDS store only
@@ -325,15 +349,17 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
       rpre[j] = __builtin_nontemporal_load(&R[(size_t)gm * nvec + (n0 >> 3) + cc]);
     }
   }
-  store_tile(0, s0);
+  if constexpr (!kDma) store_tile(0, s0);
   __syncthreads();
-  // One register stage: tile k+1's loads are in flight while tile k feeds the MFMAs. A
-  // second stage (tile k+2 in flight) was measured slower on every ResNet-50 layer: it
-  // needs 32 more VGPRs per stage and drops BN=128 to one wave per SIMD (profiles/r1t).
+  // Tile k+1's loads (LDS-DMA into the other buffer, or into registers) are in flight
+  // while tile k feeds the MFMAs; the barrier's vmcnt(0) retires them. A second register
+  // stage (tile k+2 in flight) was measured slower on every ResNet-50 layer: it needs 32
+  // more VGPRs per stage and drops BN=128 to one wave per SIMD (profiles/r1t).
   for (unsigned kt = 0; kt < nk; kt++) {
-    if (kt + 1 < nk) load_tile(kt + 1, s0);
+    if (kt + 1 < nk) load_tile(kt + 1, s0, (kt & 1) ^ 1);
     compute(kt & 1);
-    if (kt + 1 < nk) store_tile((kt & 1) ^ 1, s0);
+    if constexpr (!kDma)
+      if (kt + 1 < nk) store_tile((kt & 1) ^ 1, s0);
     __syncthreads();
   }
 
