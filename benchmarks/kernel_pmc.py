@@ -2,7 +2,8 @@
 """Workload for per-kernel hardware-counter passes (rocprofv3 --pmc) over the hand-written
 gfx950 kernels at ResNet-V2-50 inference shapes (batch 50, 346x346): the fused stem, a
 stage-1 3x3 conv (implicit GEMM, BN+ReLU epilogue), a stage-1 conv3 (1x1, sum-only
-epilogue) and a stage-1 conv1 with the BN+ReLU prologue. Each runs --iters times.
+epilogue) and a stage-1 conv1 with the BN+ReLU prologue; or (--set conv3x3) the 3x3
+convs of all four stages. Each runs --iters times.
 
     rocprofv3 --pmc <counters> --kernel-trace --output-format csv -d OUT -o p1 -- \\
         python3 benchmarks/kernel_pmc.py
@@ -19,6 +20,8 @@ sys.path.insert(0, REPO)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--set", default="mixed", choices=["mixed", "conv3x3"],
+                    help="conv3x3: the four stages' 3x3 convs (BN+ReLU epilogue) instead")
     a = ap.parse_args()
     import torch
     from amdvgpu.ops.fused import conv_nhwc, stem_pool_bn_act, stem_weight
@@ -34,6 +37,19 @@ def main():
     w33 = (torch.randn(64, 64, 3, 3, device=dev) / 576 ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
     w3 = (torch.randn(256, 64, 1, 1, device=dev) / 8).to(torch.bfloat16).contiguous(memory_format=cl)
     w1 = (torch.randn(64, 256, 1, 1, device=dev) / 16).to(torch.bfloat16).contiguous(memory_format=cl)
+    if a.set == "conv3x3":
+        layers = []
+        for c, hw in ((64, 87), (128, 44), (256, 22), (512, 11)):
+            xi = torch.randn(50, c, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+            wi = (torch.randn(c, c, 3, 3, device=dev) / (9 * c) ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+            layers.append((xi, wi, torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev)))
+        with torch.inference_mode():
+            for _ in range(a.iters):
+                for xi, wi, si, ti in layers:
+                    conv_nhwc(xi, wi, 1, 1, si, ti, act="relu")
+            torch.cuda.synchronize()
+        print("kernel_pmc done", flush=True)
+        return
     with torch.inference_mode():
         for _ in range(a.iters):
             stem_pool_bn_act(x, w192, s64, t64)

@@ -331,36 +331,54 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
 
   const unsigned nk = K / kBK;
   Stage s0;
-  load_tile(0, s0, 0);
-  // The residual tile does not depend on the GEMM: its loads go out right behind the
-  // first K-tile's, so they are in flight together and complete under the MFMAs instead
-  // of stalling the epilogue (vmcnt retires loads in order, so the first LDS store only
-  // waits for the older A/W loads).
+  // The residual tile does not depend on the GEMM: its loads go out with the first
+  // K-tile's, so they are in flight together and complete under the MFMAs instead of
+  // stalling the epilogue.
   constexpr unsigned kChunksPerRow = BN / 8;
   constexpr int kEpiIters = BM * kChunksPerRow / kThreads;
   static_assert(kEpiIters * kThreads == BM * kChunksPerRow, "whole epilogue iterations");
   const size_t nvec = N >> 3;  // output row stride in 16-B chunks
   u32x4 rpre[kEpi >= 2 ? kEpiIters : 1];
-  if constexpr (kEpi >= 2) {
+  auto prefetch_residual = [&]() {
+    if constexpr (kEpi >= 2) {
 #pragma unroll
-    for (int j = 0; j < kEpiIters; j++) {
-      const unsigned c = tid + j * kThreads, r = c / kChunksPerRow, cc = c % kChunksPerRow;
-      const unsigned gm = (m0 + r < M) ? m0 + r : M - 1u;
-      rpre[j] = __builtin_nontemporal_load(&R[(size_t)gm * nvec + (n0 >> 3) + cc]);
+      for (int j = 0; j < kEpiIters; j++) {
+        const unsigned c = tid + j * kThreads, r = c / kChunksPerRow, cc = c % kChunksPerRow;
+        const unsigned gm = (m0 + r < M) ? m0 + r : M - 1u;
+        rpre[j] = __builtin_nontemporal_load(&R[(size_t)gm * nvec + (n0 >> 3) + cc]);
+      }
     }
-  }
-  if constexpr (!kDma) store_tile(0, s0);
-  __syncthreads();
-  // Tile k+1's loads (LDS-DMA into the other buffer, or into registers) are in flight
-  // while tile k feeds the MFMAs; the barrier's vmcnt(0) retires them. A second register
-  // stage (tile k+2 in flight) was measured slower on every ResNet-50 layer: it needs 32
-  // more VGPRs per stage and drops BN=128 to one wave per SIMD (profiles/r1t).
-  for (unsigned kt = 0; kt < nk; kt++) {
-    if (kt + 1 < nk) load_tile(kt + 1, s0, (kt & 1) ^ 1);
-    compute(kt & 1);
-    if constexpr (!kDma)
-      if (kt + 1 < nk) store_tile((kt & 1) ^ 1, s0);
+  };
+  if constexpr (kDma) {
+    // Step kt: barrier (its vmcnt(0) retires tile kt's LDS-DMA), start tile kt + 1's
+    // LDS-DMA into the buffer step kt - 1 read, compute tile kt. A 3-deep ring (two tiles
+    // in flight, counted vmcnt + bare s_barrier) was slower on 19 of 23 ResNet-50 layers:
+    // it costs a block per CU of LDS (profiles/r1al). So was a transposed product with
+    // the epilogue on the accumulators (4 channels of a pixel per lane, no LDS round
+    // trip): its 8-byte residual loads and output stores made the memory-bound layers up
+    // to 1.6x slower (profiles/r1am).
+    prefetch_residual();
+    load_tile(0, s0, 0);
+    for (unsigned kt = 0; kt < nk; kt++) {
+      __syncthreads();
+      if (kt + 1 < nk) load_tile(kt + 1, s0, (kt & 1) ^ 1);
+      compute(kt & 1);
+    }
+    __syncthreads();  // every wave's last fragment reads before the epilogue reuses LDS
+  } else {
+    load_tile(0, s0, 0);
+    prefetch_residual();
+    store_tile(0, s0);
     __syncthreads();
+    // One register stage: tile k+1's loads are in flight while tile k feeds the MFMAs. A
+    // second register stage was measured slower on every ResNet-50 layer: it needs 32
+    // more VGPRs per stage and drops BN=128 to one wave per SIMD (profiles/r1t).
+    for (unsigned kt = 0; kt < nk; kt++) {
+      if (kt + 1 < nk) load_tile(kt + 1, s0, 0);
+      compute(kt & 1);
+      if (kt + 1 < nk) store_tile((kt & 1) ^ 1, s0);
+      __syncthreads();
+    }
   }
 
   // Accumulators -> LDS (fp32, row-major [128][BN + 4]); C/D map of 16x16x32:
