@@ -41,6 +41,8 @@ def _ops():
         L.vgpu_conv1x1_bf16.restype = C.c_int
         L.vgpu_conv_nhwc_bf16.argtypes = [C.c_void_p] * 9 + [C.c_int] * 12 + [C.c_void_p]
         L.vgpu_conv_nhwc_bf16.restype = C.c_int
+        L.vgpu_conv_dual_bf16.argtypes = [C.c_void_p] * 7 + [C.c_int] * 12 + [C.c_void_p]
+        L.vgpu_conv_dual_bf16.restype = C.c_int
         L.vgpu_stem_bf16.argtypes = [C.c_void_p] * 5 + [C.c_int] * 3 + [C.c_void_p]
         L.vgpu_stem_bf16.restype = C.c_int
         L.vgpu_lstm_seq_bf16.argtypes = [C.c_void_p] * 6 + [C.c_int] * 3 + [C.c_void_p]
@@ -294,6 +296,59 @@ def conv_nhwc(x, w, stride=1, padding=0, scale=None, shift=None, residual=None, 
     return (y, s) if write_sum else y
 
 
+def conv_dual_reference(x, w1, x2, w2, stride2=1, scale=None, shift=None, act="relu"):
+    """fp32 reference of :func:`conv_dual`: returns (y, acc)."""
+    acc = F.conv2d(x.float(), w1.float()) + F.conv2d(x2.float(), w2.float(), stride=stride2)
+    if scale is None:
+        return acc, acc
+    shape = [1, -1, 1, 1]
+    return _act_torch(acc * scale.float().view(shape) + shift.float().view(shape), act), acc
+
+
+def conv_dual_weight(w1, w2):
+    """[Cout, C + C2] weight of :func:`conv_dual` from two 1x1 conv weights."""
+    return torch.cat([conv_weight_2d(w1), conv_weight_2d(w2)], dim=1).contiguous()
+
+
+def conv_dual(x, x2, wcat, stride2=1, scale=None, shift=None, act="relu", write_sum=False, max_blocks=None):
+    """One MFMA GEMM for a projection block's conv3 and its shortcut conv
+    (``conv_nhwc_mfma.hip``, dual source): acc = conv1x1(x, w1) + conv1x1(x2, w2,
+    stride2), ``wcat`` = :func:`conv_dual_weight` (w1 | w2 along K). Returns acc, or
+    act(acc * scale + shift) (and acc too with ``write_sum``). The shortcut output is
+    never written to HBM and read back as a residual."""
+    for t in (x, x2):
+        if t.dtype != torch.bfloat16 or not t.is_cuda or t.dim() != 4 or \
+                not t.is_contiguous(memory_format=torch.channels_last):
+            raise TypeError("conv_dual needs 4-D bf16 channels_last CUDA tensors")
+    N, Cin, H, W = x.shape
+    N2, C2, H2, W2 = x2.shape
+    cout = wcat.shape[0]
+    if N2 != N or (H2 - 1) // stride2 + 1 != H or (W2 - 1) // stride2 + 1 != W:
+        raise ValueError(f"x2 {tuple(x2.shape)} with stride {stride2} does not map onto x {tuple(x.shape)}")
+    if tuple(wcat.shape) != (cout, Cin + C2) or wcat.dtype != torch.bfloat16 or not wcat.is_contiguous():
+        raise ValueError("wcat must be the contiguous bf16 [Cout, C + C2] weight")
+    if Cin % 64 or C2 % 64 or cout % 64:
+        raise ValueError("conv_dual needs channel counts that are multiples of 64")
+    if (scale is None) != (shift is None) or (write_sum and scale is None):
+        raise ValueError("write_sum needs scale and shift")
+    for v in (scale, shift):
+        if v is not None and (v.dtype != torch.float32 or v.numel() != cout or not v.is_contiguous()):
+            raise ValueError("scale/shift must be contiguous fp32 vectors of Cout")
+    y = torch.empty((N, cout, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    s = torch.empty_like(y) if write_sum else None
+    epi = 0 if scale is None else 6 if write_sum else 1
+    _same_device(x, x2, wcat, scale, shift)
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    if max_blocks is None:
+        max_blocks = grid_cap(cout, x.device)
+    rc = _ops().vgpu_conv_dual_bf16(_ptr(x), _ptr(x2), _ptr(wcat), _ptr(scale), _ptr(shift), _ptr(y), _ptr(s), N, H,
+                                    W, Cin, C2, H2, W2, stride2, cout, epi, ACT[act], int(max_blocks),
+                                    C.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"vgpu_conv_dual_bf16 failed ({rc}) for x {tuple(x.shape)} x2 {tuple(x2.shape)}")
+    return (y, s) if write_sum else y
+
+
 def is_resnet_stem(conv, pool):
     """conv7x7/2 (3 -> 64, pad 3, no bias) followed by maxpool3x3/2 pad 1: the shape
     ``stem_mfma.hip`` fuses."""
@@ -446,6 +501,13 @@ class FusedResNetV2(nn.Module):
         on = self.mfma_mode == "on" or (self.mfma_mode == "auto" and impl == "hip")
         self.prologue = [on and j > 0 and not self.has_sc[j] and is_pointwise(blocks[j].conv1)
                          and self.eligible[j - 1][2] for j in range(len(blocks))]
+        # Projection blocks: conv3 and the 1x1 shortcut conv run as one GEMM over
+        # [y | pre strided] (conv_dual), so the shortcut output never round-trips through
+        # HBM as conv3's residual. Not timed in "auto" either: it removes a full
+        # activation write and read and the shortcut's launch.
+        self.dual = [on and b.shortcut is not None and self.eligible[j][2] and self.eligible[j][3]
+                     and is_pointwise(b.conv3) and b.shortcut.kernel_size == (1, 1) and b.shortcut.padding == (0, 0)
+                     and b.shortcut.stride[0] == b.shortcut.stride[1] for j, b in enumerate(blocks)]
 
     def _w2d(self, conv):
         w = conv.weight
@@ -467,6 +529,23 @@ class FusedResNetV2(nn.Module):
         y, s = conv_reference(x, conv.weight, st, pad, sc, sh, residual, act, prologue=pro)
         y = y.to(x.dtype).contiguous(memory_format=torch.channels_last)
         return (y, s.to(x.dtype).contiguous(memory_format=torch.channels_last)) if write_sum else y
+
+    def _dual(self, i, y, pre, bn=None, write_sum=False):
+        """Block i's conv3(y) + shortcut(pre) as one GEMM, with bn's epilogue (and the
+        pre-BN sum with write_sum)."""
+        c3, scv = self.convs[i][2], self.shortcuts[i]
+        st = scv.stride[0]
+        sc, sh, act = (bn.scale, bn.shift, bn.act) if bn is not None else (None, None, "none")
+        if self.impl == "hip":
+            key = ("dual", i)
+            hit = self._wcache.get(key)
+            tag = (c3.weight.data_ptr(), scv.weight.data_ptr(), c3.weight.dtype)
+            if hit is None or hit[0] != tag:
+                hit = self._wcache[key] = (tag, conv_dual_weight(c3.weight.detach(), scv.weight.detach()))
+            return conv_dual(y, pre, hit[1], st, sc, sh, act, write_sum)
+        out, acc = conv_dual_reference(y, c3.weight, pre, scv.weight, st, sc, sh, act)
+        out = out.to(y.dtype).contiguous(memory_format=torch.channels_last)
+        return (out, acc.to(y.dtype).contiguous(memory_format=torch.channels_last)) if write_sum else out
 
     def _use(self, key, fused, unfused):
         if self.mfma_mode != "auto" or self.impl != "hip":
@@ -504,7 +583,9 @@ class FusedResNetV2(nn.Module):
             # pre is None when the previous conv3 wrote only x: this block's conv1 then
             # applies its pre-activation BN + ReLU (bn_in) while loading x.
             bn_in = self.entry if i == 0 else self.boundary[i - 1]
-            if not self.has_sc[i]:
+            if self.dual[i]:
+                sc = None  # folded into conv3 (conv_dual)
+            elif not self.has_sc[i]:
                 sc = x
             elif esc and self._use((i, 0, tuple(pre.shape)), lambda: self._conv(pre, self.shortcuts[i]),
                                    lambda: self.shortcuts[i](pre)):
@@ -521,7 +602,14 @@ class FusedResNetV2(nn.Module):
                 y = self._conv(y, c2, bn3)
             else:
                 y = bn3(c2(y))
-            if not last and self.prologue[i + 1]:
+            if self.dual[i]:
+                if not last and self.prologue[i + 1]:
+                    x, pre = self._dual(i, y, pre), None
+                elif last:
+                    pre, x = self._dual(i, y, pre, bnd), None
+                else:
+                    pre, x = self._dual(i, y, pre, bnd, write_sum=True)
+            elif not last and self.prologue[i + 1]:
                 x, pre = self._conv(y, c3, None, sc), None  # next conv1 applies bnd itself
             elif e3 and self._use((i, 3, tuple(y.shape)), lambda: self._conv(y, c3, bnd, sc, not last),
                                   lambda: bnd(c3(y), residual=sc, write_sum=not last)):

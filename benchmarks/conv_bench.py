@@ -121,6 +121,33 @@ def main():
                  "speedup": t_l / t_f, "fused_TBps": 2 * (x.numel() + 50 * 64 * 87 * 87) / t_f / 1e6,
                  "fused_TFLOPs": 2.0 * m * 147 * 64 / t_f / 1e6, "max_abs_diff_vs_library": err})
     print(json.dumps(rows[-1]), flush=True)
+    # Projection blocks: conv3 + the 1x1 shortcut as one dual-source GEMM (conv_dual) vs
+    # the two-kernel form (shortcut conv, then conv3 with the shortcut as its residual).
+    from amdvgpu.ops.fused import conv_dual, conv_dual_weight
+    dual_rows = []
+    for label, n, h2, c1, c2, s2, cout in (("s1 conv3 + shortcut", 50, 87, 64, 64, 1, 256),
+                                           ("s2 conv3 + shortcut/2", 50, 87, 128, 256, 2, 512),
+                                           ("s3 conv3 + shortcut/2", 50, 44, 256, 512, 2, 1024),
+                                           ("s4 conv3 + shortcut/2", 50, 22, 512, 1024, 2, 2048)):
+        h = (h2 - 1) // s2 + 1
+        cl = torch.channels_last
+        y = torch.randn(n, c1, h, h, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+        pre = torch.randn(n, c2, h2, h2, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+        w3 = (torch.randn(cout, c1, 1, 1, device="cuda") / c1 ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+        ws = (torch.randn(cout, c2, 1, 1, device="cuda") / c2 ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+        wcat = conv_dual_weight(w3, ws)
+        w3d, wsd = conv_weight_2d(w3), conv_weight_2d(ws)
+        with torch.inference_mode():
+            dual = lambda: conv_dual(y, pre, wcat, s2)  # noqa: E731
+            two = lambda: conv_nhwc(y, w3, 1, 0, residual=conv_nhwc(pre, ws, s2, 0, w2d=wsd), w2d=w3d)  # noqa: E731
+            t_d, t_2 = timeit(dual, a.iters), timeit(two, a.iters)
+            err = (dual().float() - two().float()).abs().max().item()
+        m = n * h * h
+        nbytes = 2 * (m * c1 + n * h2 * h2 * c2 + cout * (c1 + c2) + m * cout)
+        dual_rows.append({"block": label, "M": m, "K": c1 + c2, "N": cout, "dual_us": t_d, "two_kernels_us": t_2,
+                          "speedup": t_2 / t_d, "dual_TBps": nbytes / t_d / 1e6,
+                          "dual_TFLOPs": 2.0 * m * (c1 + c2) * cout / t_d / 1e6, "max_abs_diff": err})
+        print(json.dumps(dual_rows[-1]), flush=True)
     tot_f = sum(r_["fused_us"] for r_ in rows)
     tot_l = sum(r_["library_conv_plus_epilogue_us"] for r_ in rows)
     md = ["| layer | M | K | N | epilogue | fused MFMA us | library conv + epilogue us | conv alone us | speedup "
@@ -131,6 +158,14 @@ def main():
                   f"{r_['speedup']:.2f}x | {r_['fused_TBps']:.2f} | {r_['fused_TFLOPs']:.0f} | "
                   f"{r_['max_abs_diff_vs_library']:.3g} |")
     md.append(f"| **sum (one of each)** | | | | | {tot_f:.1f} | {tot_l:.1f} | | {tot_l / tot_f:.2f}x | | | |")
+    md += ["", "Projection blocks: conv3 + shortcut as one dual-source GEMM vs shortcut conv + conv3 with residual "
+           "(both MFMA kernels)", "",
+           "| block | M | K | N | dual us | two kernels us | speedup | dual TB/s | dual TFLOP/s | max abs diff |",
+           "|---|---|---|---|---|---|---|---|---|---|"]
+    for r_ in dual_rows:
+        md.append(f"| {r_['block']} | {r_['M']} | {r_['K']} | {r_['N']} | {r_['dual_us']:.1f} | "
+                  f"{r_['two_kernels_us']:.1f} | {r_['speedup']:.2f}x | {r_['dual_TBps']:.2f} | "
+                  f"{r_['dual_TFLOPs']:.0f} | {r_['max_abs_diff']:.3g} |")
     print("\n".join(md))
     if a.json_out:
         json.dump(rows, open(a.json_out, "w"), indent=1)

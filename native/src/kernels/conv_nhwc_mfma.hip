@@ -62,6 +62,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace {
 
@@ -80,6 +81,9 @@ struct ConvGeom {
   unsigned H, W, C, OH, OW, KW, stride, pad;    // geometry (implicit-GEMM path)
   unsigned tiles_n, ntiles;
   unsigned x_bytes, w_bytes;                    // buffer-descriptor ranges (< 2^31, host-checked)
+  // Dual source (kDual): K-tiles past K1 = C read X2 [Nb, H2, W2, C2] at pixel
+  // (oh * stride2, ow * stride2), a strided 1x1 conv accumulated into the same tile.
+  unsigned C2, H2, W2, stride2, x2_bytes;
 };
 
 struct ConvArgs {
@@ -92,6 +96,7 @@ struct ConvArgs {
   void* s;
   const float* pscale;  // prologue (1x1 path): A = relu(X * pscale + pshift), or null
   const float* pshift;
+  const void* x2;       // second A source (dual path), or null
   int max_blocks;       // grid cap (persistent blocks), 0 = one block per tile
   ConvGeom g;
 };
@@ -148,13 +153,18 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned ntiles) {
 }
 
 // kEpi: 0 plain (y = acc), 1 y = act(acc*s+t), 2 x = acc + r; y = act(x*s+t),
-//       3 as 2 and also writes x (bf16) to `s`, 4 y = act(acc*s + t + r), 5 y = acc + r.
+//       3 as 2 and also writes x (bf16) to `s`, 4 y = act(acc*s + t + r), 5 y = acc + r,
+//       6 as 3 without a residual (s = acc; y = act(acc*s+t)).
 // kIm2col: false = 1x1/stride-1 (A is X itself), true = implicit GEMM gather.
 // kPro (1x1 path): the A operand is relu(X * pscale[c] + pshift[c]) (the consumer's
 //       pre-activation BN + ReLU applied while staging, rounded to bf16 as a separate
 //       pass would store it), so the producer never writes that activation to HBM.
-template <int BM, int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro>
-__device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32x4* __restrict__ Wt,
+// kDual (1x1 path): A = [X | strided X2] along K, W = [W1 | W2]: the ResNet projection
+//       block's conv3 and its shortcut conv as one GEMM, so the shortcut output is never
+//       written to HBM and read back as the residual.
+template <int BM, int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro, bool kDual>
+__device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32x4* __restrict__ X2,
+                                          const u32x4* __restrict__ Wt,
                                           const float* __restrict__ scale, const float* __restrict__ shift,
                                           const u32x4* __restrict__ R, u32x4* __restrict__ Y, u32x4* __restrict__ S,
                                           const float* __restrict__ pscale, const float* __restrict__ pshift,
@@ -186,8 +196,11 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   // fixed voffset, the K position as the scalar soffset, so a K-tile's loads cost no
   // vector address arithmetic (the host keeps every launch's tensors below 2 GiB).
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(X, p.x_bytes), wr = make_rsrc(Wt, p.w_bytes);
-  const unsigned krow = K * 2u;  // W row (and 1x1 A row) in bytes
+  const unsigned krow = K * 2u;  // W row in bytes
   unsigned a_vo[kALoads];        // 1x1: row start; im2col: current tap's pixel, or kOOB
+  unsigned a_vo2[kDual ? kALoads : 1];  // dual: the strided source-2 pixel's row start
+  const __amdgpu_buffer_rsrc_t xr2 = make_rsrc(kDual ? static_cast<const void*>(X2) : X, kDual ? p.x2_bytes : 0u);
+  const unsigned nk1 = p.C / kBK;       // K-tiles from source 1
   int a_pix[kALoads], a_ih0[kALoads], a_iw0[kALoads];
   unsigned a_dst[kALoads];
   const unsigned cbytes = p.C * 2u;  // input pixel stride (im2col path)
@@ -212,8 +225,14 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
       a_pix[i] = (int)(((img * p.H) * p.W) * cbytes) + (a_ih0[i] * (int)p.W + a_iw0[i]) * (int)cbytes + (int)(ch * 16u);
       a_vo[i] = kOOB;
     } else {
-      a_vo[i] = gm * krow + ch * 16u;
+      a_vo[i] = gm * cbytes + ch * 16u;
       a_pix[i] = a_ih0[i] = a_iw0[i] = 0;
+      if constexpr (kDual) {
+        const unsigned plane = p.OH * p.OW;
+        const unsigned img = gm / plane, rem = gm - img * plane;
+        const unsigned oh = rem / p.OW, ow = rem - oh * p.OW;
+        a_vo2[i] = ((img * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * (p.C2 * 2u) + ch * 16u;
+      }
     }
     a_dst[i] = r * 8u + swz(r, ch);
   }
@@ -270,6 +289,10 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
         t_c0 = 0;
         if (++t_kw == p.KW) t_kw = 0, t_kh++;
       }
+    } else if (kDual && kt >= nk1) {
+      const unsigned koff2 = (kt - nk1) * (kBK * 2u);
+#pragma unroll
+      for (int i = 0; i < kALoads; i++) dma16(xr2, slot(a_lds(b), i), a_vo2[i], koff2);
     } else {
 #pragma unroll
       for (int i = 0; i < kALoads; i++) {
@@ -338,9 +361,10 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   constexpr int kEpiIters = BM * kChunksPerRow / kThreads;
   static_assert(kEpiIters * kThreads == BM * kChunksPerRow, "whole epilogue iterations");
   const size_t nvec = N >> 3;  // output row stride in 16-B chunks
-  u32x4 rpre[kEpi >= 2 ? kEpiIters : 1];
+  constexpr bool kRes = kEpi >= 2 && kEpi <= 5;  // epilogue reads the residual
+  u32x4 rpre[kRes ? kEpiIters : 1];
   auto prefetch_residual = [&]() {
-    if constexpr (kEpi >= 2) {
+    if constexpr (kRes) {
 #pragma unroll
       for (int j = 0; j < kEpiIters; j++) {
         const unsigned c = tid + j * kThreads, r = c / kChunksPerRow, cc = c % kChunksPerRow;
@@ -405,7 +429,7 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
     const unsigned n = n0 + cc * 8u;
     const size_t o = (size_t)gm * nvec + (n >> 3);
     float rr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (kEpi >= 2) {
+    if constexpr (kRes) {
       const u32x4 rv = rpre[j];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -413,17 +437,17 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
         rr[2 * k + 1] = bf_hi(rv[k]);
       }
     }
-    if constexpr (kEpi == 2 || kEpi == 3 || kEpi == 5) {
+    if constexpr (kEpi == 2 || kEpi == 3 || kEpi == 5 || kEpi == 6) {
 #pragma unroll
       for (int k = 0; k < 8; k++) v[k] += rr[k];
-      if constexpr (kEpi == 3) {
+      if constexpr (kEpi == 3 || kEpi == 6) {
         u32x4 sv;
 #pragma unroll
         for (int k = 0; k < 4; k++) sv[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
         S[o] = sv;
       }
     }
-    if constexpr (kEpi >= 1 && kEpi <= 4) {
+    if constexpr ((kEpi >= 1 && kEpi <= 4) || kEpi == 6) {
       const float4 s0 = *reinterpret_cast<const float4*>(scale + n);
       const float4 s1 = *reinterpret_cast<const float4*>(scale + n + 4);
       const float4 t0 = *reinterpret_cast<const float4*>(shift + n);
@@ -449,14 +473,15 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
 // one round and this tenant's dispatch never waits for room on its slice while holding
 // up the other tenants' dispatches (profiles/r1z). The grid is a multiple of 8 when
 // capped, so every tile a block visits keeps the block's XCD in xcd_remap.
-template <int BM, int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro>
-__global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict__ X, const u32x4* __restrict__ Wt,
+template <int BM, int BN, int WM, int WN, int kEpi, int kAct, bool kIm2col, bool kPro, bool kDual>
+__global__ void __launch_bounds__(kThreads) conv_kernel(const u32x4* __restrict__ X, const u32x4* __restrict__ X2,
+                                                       const u32x4* __restrict__ Wt,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        const u32x4* __restrict__ R, u32x4* __restrict__ Y,
                                                        u32x4* __restrict__ S, const float* __restrict__ pscale,
                                                        const float* __restrict__ pshift, const ConvGeom p) {
   for (unsigned t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
-    conv_tile<BM, BN, WM, WN, kEpi, kAct, kIm2col, kPro>(X, Wt, scale, shift, R, Y, S, pscale, pshift, p,
+    conv_tile<BM, BN, WM, WN, kEpi, kAct, kIm2col, kPro, kDual>(X, X2, Wt, scale, shift, R, Y, S, pscale, pshift, p,
                                                       xcd_remap(t, p.ntiles));
     __syncthreads();  // the next tile's staging overwrites this tile's epilogue image in LDS
   }
@@ -467,18 +492,25 @@ int launch(ConvArgs a, bool im2col, hipStream_t stream) {
   ConvGeom g = a.g;
   g.tiles_n = g.N / BN;
   g.ntiles = (g.M + BM - 1) / BM * g.tiles_n;
-  auto kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, false, false>;
-  if (im2col) {
-    kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, true, false>;
+  auto kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, false, false, false>;
+  if (a.x2) {
+    // The dual source exists for the projection conv3 + shortcut (no residual epilogue).
+    if constexpr (kEpi == 0 || kEpi == 1 || kEpi == 6) kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, false, false, true>;
+    else return -1;
+  } else if (im2col) {
+    kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, true, false, false>;
   } else if (a.pscale) {
     // The prologue exists for the ResNet-V2 conv1 (BN + ReLU epilogue) only.
-    if constexpr (kEpi == 1 && kAct == 1) kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, false, true>;
+    if constexpr (kEpi == 1 && kAct == 1) kern = conv_kernel<BM, BN, WM, WN, kEpi, kAct, false, true, false>;
     else return -1;
   }
+  if constexpr (kEpi == 6)
+    if (!a.x2) return -1;
   unsigned grid = g.ntiles;
   if (a.max_blocks > 0 && (unsigned)a.max_blocks < grid) grid = a.max_blocks < 8 ? 8u : (unsigned)a.max_blocks / 8u * 8u;
   if (grid > g.ntiles) grid = g.ntiles;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, stream, static_cast<const u32x4*>(a.x),
+                     static_cast<const u32x4*>(a.x2),
                      static_cast<const u32x4*>(a.w), a.scale, a.shift, static_cast<const u32x4*>(a.r),
                      static_cast<u32x4*>(a.y), static_cast<u32x4*>(a.s), a.pscale, a.pshift, g);
   return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -493,6 +525,7 @@ int by_epi(int epi, const ConvArgs& a, bool im2col, hipStream_t st) {
     case 3: return launch<BM, BN, WM, WN, 3, kAct>(a, im2col, st);
     case 4: return launch<BM, BN, WM, WN, 4, kAct>(a, im2col, st);
     case 5: return launch<BM, BN, WM, WN, 5, 0>(a, im2col, st);
+    case 6: return launch<BM, BN, WM, WN, 6, kAct>(a, im2col, st);
     default: return -1;
   }
 }
@@ -507,43 +540,43 @@ int by_act(int act, int epi, const ConvArgs& a, bool im2col, hipStream_t st) {
   }
 }
 
-}  // namespace
-
-extern "C" {
-
-// y[Nb, OH, OW, Cout] = epilogue(conv(x[Nb, H, W, C], w[Cout, KH, KW, C])), bf16 NHWC,
-// fp32 accumulation, OH = (H + 2 pad - KH) / stride + 1 (same for OW). epi: 0 plain,
-// 1 act(acc*scale+shift), 2 act((acc+r)*scale+shift), 3 as 2 and sum = acc + r,
-// 4 act(acc*scale + shift + r), 5 acc + r. act: 0 none, 1 relu, 2 relu6. scale/shift:
-// fp32[Cout]. pscale/pshift (optional, fp32[C], 1x1 stride-1 with epi 1 + relu only): the
-// input is read as relu(x * pscale + pshift). max_blocks > 0 caps the grid (persistent
-// blocks; rounded down to a multiple of 8). Returns 0 on success, -1 on bad arguments,
-// -2 on launch failure.
-int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const float* shift, const void* r, void* y,
-                        void* sum, const float* pscale, const float* pshift, int nb, int h, int wd, int c, int cout,
-                        int kh, int kw, int stride, int pad, int epi, int act, int max_blocks, void* stream) {
+// The shared host path of both entry points (x2 == nullptr: single source).
+int run_conv(const void* x, const void* w, const float* scale, const float* shift, const void* r, void* y, void* sum,
+             const float* pscale, const float* pshift, const void* x2, int nb, int h, int wd, int c, int cout, int kh,
+             int kw, int stride, int pad, int c2, int h2, int w2, int stride2, int epi, int act, int max_blocks,
+             void* stream) {
   if (!x || !w || !y || nb <= 0 || h <= 0 || wd <= 0 || c <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
       pad < 0 || pad >= kh || pad >= kw)
     return -1;
   if (c % kBK || cout % 64) return -1;
-  if (epi < 0 || epi > 5 || act < 0 || act > 2) return -1;
-  if (epi >= 1 && epi <= 4 && (!scale || !shift)) return -1;
+  if (epi < 0 || epi > 6 || act < 0 || act > 2) return -1;
+  if (((epi >= 1 && epi <= 4) || epi == 6) && (!scale || !shift)) return -1;
   if ((pscale == nullptr) != (pshift == nullptr)) return -1;
   if (pscale && (epi != 1 || act != 1 || kh != 1 || kw != 1 || stride != 1 || pad != 0)) return -1;
-  if (epi >= 2 && !r) return -1;
-  if ((epi == 3) != (sum != nullptr)) return -1;
+  if (epi >= 2 && epi <= 5 && !r) return -1;
+  if ((epi == 3 || epi == 6) != (sum != nullptr)) return -1;
+  if ((epi == 6) && !x2) return -1;
   const int64_t oh = ((int64_t)h + 2 * pad - kh) / stride + 1, ow = ((int64_t)wd + 2 * pad - kw) / stride + 1;
   if (oh <= 0 || ow <= 0 || h + 2 * pad < kh || wd + 2 * pad < kw) return -1;
+  if (x2) {  // [x | x2 strided] . [w1 | w2]^T: 1x1 stride-1 source 1, strided 1x1 source 2
+    if (kh != 1 || kw != 1 || stride != 1 || pad != 0 || pscale || c2 <= 0 || c2 % kBK || h2 <= 0 || w2 <= 0 ||
+        stride2 <= 0 || (h2 - 1) / stride2 + 1 != oh || (w2 - 1) / stride2 + 1 != ow)
+      return -1;
+    if (epi != 0 && epi != 1 && epi != 6) return -1;
+  }
   // Buffer descriptors address with 32-bit offsets below 2^31: the weight must fit, and
   // larger batches run as several launches over groups of whole images.
-  const int64_t k = (int64_t)kh * kw * c, lim = ((int64_t)1 << 31) - 1;
+  const int64_t k = (int64_t)kh * kw * c + (x2 ? c2 : 0), lim = ((int64_t)1 << 31) - 1;
   const int64_t img_x = (int64_t)h * wd * c * 2, img_y = oh * ow * cout * 2;
-  if (k * cout * 2 > lim || img_x > lim || img_y > lim) return -1;
+  const int64_t img_x2 = x2 ? (int64_t)h2 * w2 * c2 * 2 : 0;
+  if (k * cout * 2 > lim || img_x > lim || img_y > lim || img_x2 > lim) return -1;
   auto misaligned = [](const void* q) { return q && (reinterpret_cast<uintptr_t>(q) & 15u); };
   if (misaligned(x) || misaligned(w) || misaligned(y) || misaligned(r) || misaligned(sum) || misaligned(scale) ||
-      misaligned(shift) || misaligned(pscale) || misaligned(pshift))
+      misaligned(shift) || misaligned(pscale) || misaligned(pshift) || misaligned(x2))
     return -1;
-  const int64_t per = lim / (img_x > img_y ? img_x : img_y);  // images per launch
+  int64_t big = img_x > img_y ? img_x : img_y;
+  big = big > img_x2 ? big : img_x2;
+  const int64_t per = lim / big;  // images per launch
   const bool im2col = !(kh == 1 && kw == 1 && stride == 1 && pad == 0);
   hipStream_t st = static_cast<hipStream_t>(stream);
   for (int64_t i0 = 0; i0 < nb; i0 += per) {
@@ -556,6 +589,7 @@ int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const 
     a.pshift = pshift;
     a.max_blocks = max_blocks < 0 ? 0 : max_blocks;
     a.x = at(x, i0 * img_x);
+    a.x2 = at(x2, i0 * img_x2);
     a.w = w;
     a.scale = scale;
     a.shift = shift;
@@ -576,10 +610,22 @@ int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const 
     a.g.pad = (unsigned)pad;
     a.g.x_bytes = (unsigned)(ni * img_x);
     a.g.w_bytes = (unsigned)(k * cout * 2);
+    if (x2) {
+      a.g.C2 = (unsigned)c2;
+      a.g.H2 = (unsigned)h2;
+      a.g.W2 = (unsigned)w2;
+      a.g.stride2 = (unsigned)stride2;
+      a.g.x2_bytes = (unsigned)(ni * img_x2);
+    }
     // Small-M layers (fewer than two 128-row tiles per CU) use 64-row tiles, so the grid
     // still fills the chip (e.g. ResNet stage 4: 6050 rows x 512 -> 192 vs 380 blocks).
     const int64_t bn = cout % 128 == 0 ? 128 : 64;
-    const bool small_m = (m + 127) / 128 * (cout / bn) < 512;
+    // VGPU_CONV_BM=64|128 forces the row-tile height (measurement).
+    static const int force_bm = [] {
+      const char* e = getenv("VGPU_CONV_BM");
+      return e ? atoi(e) : 0;
+    }();
+    const bool small_m = force_bm ? force_bm == 64 : (m + 127) / 128 * (cout / bn) < 512;
     int rc;
     if (bn == 128)
       rc = small_m ? by_act<64, 128, 2, 2>(act, epi, a, im2col, st) : by_act<128, 128, 2, 2>(act, epi, a, im2col, st);
@@ -588,6 +634,38 @@ int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const 
     if (rc) return rc;
   }
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// y[Nb, OH, OW, Cout] = epilogue(conv(x[Nb, H, W, C], w[Cout, KH, KW, C])), bf16 NHWC,
+// fp32 accumulation, OH = (H + 2 pad - KH) / stride + 1 (same for OW). epi: 0 plain,
+// 1 act(acc*scale+shift), 2 act((acc+r)*scale+shift), 3 as 2 and sum = acc + r,
+// 4 act(acc*scale + shift + r), 5 acc + r. act: 0 none, 1 relu, 2 relu6. scale/shift:
+// fp32[Cout]. pscale/pshift (optional, fp32[C], 1x1 stride-1 with epi 1 + relu only): the
+// input is read as relu(x * pscale + pshift). max_blocks > 0 caps the grid (persistent
+// blocks; rounded down to a multiple of 8). Returns 0 on success, -1 on bad arguments,
+// -2 on launch failure.
+int vgpu_conv_nhwc_bf16(const void* x, const void* w, const float* scale, const float* shift, const void* r, void* y,
+                        void* sum, const float* pscale, const float* pshift, int nb, int h, int wd, int c, int cout,
+                        int kh, int kw, int stride, int pad, int epi, int act, int max_blocks, void* stream) {
+  if (epi > 5) return -1;
+  return run_conv(x, w, scale, shift, r, y, sum, pscale, pshift, nullptr, nb, h, wd, c, cout, kh, kw, stride, pad, 0, 0,
+                  0, 0, epi, act, max_blocks, stream);
+}
+
+// Projection block: y[Nb, H, W, Cout] = epilogue(x[Nb, H, W, C] . w1^T + x2[:, ::s2, ::s2, :] . w2^T)
+// with w = [Cout][C + C2] (w1 | w2 along K) and x2 [Nb, H2, W2, C2], (H2 - 1) / s2 + 1 == H
+// (same for W). epi: 0 plain, 1 act(acc*scale+shift), 6 as 1 and sum = acc. Returns as
+// vgpu_conv_nhwc_bf16.
+int vgpu_conv_dual_bf16(const void* x, const void* x2, const void* w, const float* scale, const float* shift, void* y,
+                        void* sum, int nb, int h, int wd, int c, int c2, int h2, int w2, int stride2, int cout, int epi,
+                        int act, int max_blocks, void* stream) {
+  if (!x2) return -1;
+  return run_conv(x, w, scale, shift, nullptr, y, sum, nullptr, nullptr, x2, nb, h, wd, c, cout, 1, 1, 1, 0, c2, h2, w2,
+                  stride2, epi, act, max_blocks, stream);
 }
 
 // 1x1 / stride-1 convolution over M pixels: y[M, N] = epilogue(x[M, K] . w[N, K]^T).

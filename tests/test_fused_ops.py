@@ -6,8 +6,8 @@ import torch.nn as nn
 
 from amdvgpu.models.aibench import ResNetV2, resnet_v2_50
 from amdvgpu.ops.fused import (FusedResNetV2, bn_act, bn_act_reference, bn_scale_shift, conv1x1,
-                                conv1x1_reference, conv_nhwc, conv_reference, grid_cap, stem_pool_bn_act,
-                                stem_reference, stem_weight)
+                                conv1x1_reference, conv_dual, conv_dual_reference, conv_dual_weight, conv_nhwc,
+                                conv_reference, grid_cap, stem_pool_bn_act, stem_reference, stem_weight)
 
 
 def _randomize_bn(model, g):
@@ -127,6 +127,47 @@ def test_conv_nhwc_kernel_numerics(geom, epi):
     torch.testing.assert_close(y.float(), y_ref, rtol=2e-2, atol=3e-2)
     if epi == "residual_sum":
         torch.testing.assert_close(out[1].float(), s_ref, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("geom", [(2, 64, 9, 11, 64, 1, 256), (2, 128, 17, 21, 256, 2, 512), (50, 256, 22, 22, 512, 2, 1024),
+                                  (1, 64, 3, 3, 128, 3, 64)])
+@pytest.mark.parametrize("epi", ["plain", "bn_act", "bn_act_sum"])
+@pytest.mark.parametrize("cap", [0, 24])
+def test_conv_dual_kernel_numerics(geom, epi, cap):
+    """Projection block conv3 + strided shortcut as one dual-source GEMM vs fp32 torch."""
+    N, c1, H2, W2, c2, s2, cout = geom
+    H, W = (H2 - 1) // s2 + 1, (W2 - 1) // s2 + 1
+    g = torch.Generator().manual_seed(21)
+    cl = torch.channels_last
+    y = torch.randn(N, c1, H, W, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=cl)
+    pre = torch.randn(N, c2, H2, W2, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=cl)
+    w3 = (torch.randn(cout, c1, 1, 1, generator=g) / c1 ** 0.5).to("cuda", torch.bfloat16)
+    ws = (torch.randn(cout, c2, 1, 1, generator=g) / c2 ** 0.5).to("cuda", torch.bfloat16)
+    sc = (torch.rand(cout, generator=g) + 0.5).cuda()
+    sh = torch.randn(cout, generator=g).cuda()
+    kw = {} if epi == "plain" else dict(scale=sc, shift=sh, write_sum=epi == "bn_act_sum")
+    out = conv_dual(y, pre, conv_dual_weight(w3, ws), s2, act="relu", max_blocks=cap, **kw)
+    y_ref, acc_ref = conv_dual_reference(y, w3, pre, ws, s2, kw.get("scale"), kw.get("shift"), "relu")
+    o = out[0] if epi == "bn_act_sum" else out
+    assert o.shape == y_ref.shape and o.is_contiguous(memory_format=cl)
+    torch.testing.assert_close(o.float(), y_ref, rtol=2e-2, atol=3e-2)
+    if epi == "bn_act_sum":
+        torch.testing.assert_close(out[1].float(), acc_ref, rtol=2e-2, atol=3e-2)
+
+
+def test_conv_dual_reference_is_conv3_plus_shortcut_cpu():
+    g = torch.Generator().manual_seed(22)
+    y, pre = torch.randn(2, 64, 5, 6, generator=g), torch.randn(2, 128, 9, 11, generator=g)
+    w3, ws = torch.randn(256, 64, 1, 1, generator=g), torch.randn(256, 128, 1, 1, generator=g)
+    out, acc = conv_dual_reference(y, w3, pre, ws, 2)
+    ref = torch.nn.functional.conv2d(y, w3) + torch.nn.functional.conv2d(pre, ws, stride=2)
+    torch.testing.assert_close(out, ref)
+    wcat = conv_dual_weight(w3, ws)
+    assert wcat.shape == (256, 192)
+    # the concatenated-K GEMM over [y | pre strided] is the same sum
+    a = torch.cat([y.permute(0, 2, 3, 1), pre[:, :, ::2, ::2].permute(0, 2, 3, 1)], dim=3).reshape(-1, 192)
+    torch.testing.assert_close((a @ wcat.t()).reshape(2, 5, 6, 256).permute(0, 3, 1, 2), ref, rtol=1e-4, atol=1e-4)
 
 
 def test_stem_weight_layout_cpu():

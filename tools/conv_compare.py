@@ -13,7 +13,7 @@ def read(path):
         c = [x.strip() for x in line.split("|")][1:-1]
         if not c or c[0].startswith("---"):
             continue
-        if c[0] == "layer":
+        if c[0] in ("layer", "block"):
             hdr = c
             continue
         rows[c[0]] = dict(zip(hdr, c))
@@ -26,8 +26,8 @@ def main(paths):
           + " | ".join(f"TF ({p.split('/')[-2]})" for p in paths) + " |")
     print("|---" * (1 + 2 * len(paths)) + "|")
     for k in tabs[0]:
-        us = [t.get(k, {}).get("fused MFMA us", "-") for t in tabs]
-        tf = [t.get(k, {}).get("fused TFLOP/s", "") for t in tabs]
+        us = [t.get(k, {}).get("fused MFMA us", t.get(k, {}).get("dual us", "-")) for t in tabs]
+        tf = [t.get(k, {}).get("fused TFLOP/s", t.get(k, {}).get("dual TFLOP/s", "")) for t in tabs]
         print(f"| {k} | " + " | ".join(us) + " | " + " | ".join(tf) + " |")
 
 
