@@ -611,13 +611,16 @@ class FusedResNetV2(nn.Module):
                     pre, x = self._dual(i, y, pre, bnd, write_sum=True)
             elif not last and self.prologue[i + 1]:
                 x, pre = self._conv(y, c3, None, sc), None  # next conv1 applies bnd itself
-            elif e3 and self._use((i, 3, tuple(y.shape)), lambda: self._conv(y, c3, bnd, sc, not last),
-                                  lambda: bnd(c3(y), residual=sc, write_sum=not last)):
-                out = self._conv(y, c3, bnd, sc, not last)
-                pre, x = (out, None) if last else out
             else:
-                out = bnd(c3(y), residual=sc, write_sum=not last)
-                pre, x = (out, None) if last else out
+                # x itself is only read as the next block's identity shortcut: not after the
+                # last block, and not before a dual projection block (which reads pre only).
+                ws = not last and not self.dual[i + 1]
+                if e3 and self._use((i, 3, tuple(y.shape)), lambda: self._conv(y, c3, bnd, sc, ws),
+                                    lambda: bnd(c3(y), residual=sc, write_sum=ws)):
+                    out = self._conv(y, c3, bnd, sc, ws)
+                else:
+                    out = bnd(c3(y), residual=sc, write_sum=ws)
+                pre, x = out if ws else (out, None)
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(pre, 1), 1))
 
 

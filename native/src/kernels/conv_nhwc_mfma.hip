@@ -70,6 +70,14 @@ using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 using f32x4 = float __attribute__((ext_vector_type(4)));
 using bf16x8 = __bf16 __attribute__((ext_vector_type(8)));
 
+// Cache policy of the epilogue's residual loads / output stores (A/B builds).
+#ifndef VGPU_CONV_RES_NT
+#define VGPU_CONV_RES_NT 1
+#endif
+#ifndef VGPU_CONV_Y_NT
+#define VGPU_CONV_Y_NT 0
+#endif
+
 constexpr int kBK = 64;
 constexpr int kThreads = 256;
 
@@ -369,7 +377,11 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
       for (int j = 0; j < kEpiIters; j++) {
         const unsigned c = tid + j * kThreads, r = c / kChunksPerRow, cc = c % kChunksPerRow;
         const unsigned gm = (m0 + r < M) ? m0 + r : M - 1u;
+#if VGPU_CONV_RES_NT
         rpre[j] = __builtin_nontemporal_load(&R[(size_t)gm * nvec + (n0 >> 3) + cc]);
+#else
+        rpre[j] = R[(size_t)gm * nvec + (n0 >> 3) + cc];
+#endif
       }
     }
   };
@@ -444,7 +456,11 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
         u32x4 sv;
 #pragma unroll
         for (int k = 0; k < 4; k++) sv[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
+#if VGPU_CONV_Y_NT
+        __builtin_nontemporal_store(sv, &S[o]);
+#else
         S[o] = sv;
+#endif
       }
     }
     if constexpr ((kEpi >= 1 && kEpi <= 4) || kEpi == 6) {
@@ -464,7 +480,11 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
     u32x4 yv;
 #pragma unroll
     for (int k = 0; k < 4; k++) yv[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
+#if VGPU_CONV_Y_NT
+    __builtin_nontemporal_store(yv, &Y[o]);
+#else
     Y[o] = yv;
+#endif
   }
 }
 
