@@ -496,17 +496,15 @@ class FusedResNetV2(nn.Module):
         self.stem_fusable = is_resnet_stem(model.stem, model.pool) and self.has_sc[0]
         # Block j's conv1 reads x and applies bn1_j + ReLU itself (the previous conv3 then
         # writes only x) when pre_j has no other reader (identity shortcut) and both convs
-        # run on the MFMA kernel. It removes a full activation write and read, but the
-        # prologue's VALU transform rides on conv1's staging: it is free while conv1 is
-        # memory-bound (Cout <= 128: 2 Cout FLOP per 2-byte input element, below the
-        # chip's ~300 FLOP/byte ridge) and doubles a compute-bound conv1 (stages 3-4 of
-        # ResNet-50: 19 -> 39 us vs an 8 us saved write; profiles/r1ap, r1as).
-        # VGPU_PROLOGUE=on|off|auto overrides the rule. Not timed in "auto".
+        # run on the MFMA kernel: one full activation write and read fewer per block. Not
+        # timed in "auto". The prologue is applied to conv1's A fragments as they leave LDS
+        # (profiles/r1at: 23700 -> 24353 img/s over a rule that kept compute-bound conv1s
+        # plain, which the earlier register-staged prologue had doubled; r1as).
+        # VGPU_PROLOGUE=off disables it (measurement).
         on = self.mfma_mode == "on" or (self.mfma_mode == "auto" and impl == "hip")
-        pmode = os.environ.get("VGPU_PROLOGUE", "auto")
+        pmode = os.environ.get("VGPU_PROLOGUE", "on")
         self.prologue = [on and pmode != "off" and j > 0 and not self.has_sc[j] and is_pointwise(blocks[j].conv1)
-                         and self.eligible[j - 1][2] and (pmode == "on" or blocks[j].conv1.out_channels <= 128)
-                         for j in range(len(blocks))]
+                         and self.eligible[j - 1][2] for j in range(len(blocks))]
         # Projection blocks: conv3 and the 1x1 shortcut conv run as one GEMM over
         # [y | pre strided] (conv_dual), so the shortcut output never round-trips through
         # HBM as conv3's residual. Not timed in "auto" either: it removes a full

@@ -126,10 +126,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsig
 // (the implicit GEMM's padding taps, without a select after the load).
 constexpr unsigned kOOB = 0x80000000u;
 
-__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
-}
-
 // LDS-DMA: 16 B per lane from the buffer straight into LDS at lds + 16 * lane (`lds` is
 // wave-uniform), no VGPR destination and no ds_write.
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, u32x4* lds, unsigned voff, unsigned soff) {
@@ -140,10 +136,11 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, u32x4* lds, unsi
 __device__ __forceinline__ float bf_lo(unsigned v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float bf_hi(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
 
+// Two floats -> packed bf16 pair (round to nearest even) in one v_cvt_pk_bf16_f32.
 __device__ __forceinline__ unsigned pack_bf16(float lo, float hi) {
-  __hip_bfloat16 a = __float2bfloat16(lo);
-  __hip_bfloat16 b = __float2bfloat16(hi);
-  return (unsigned)__bfloat16_as_ushort(a) | ((unsigned)__bfloat16_as_ushort(b) << 16);
+  using f32x2_t = float __attribute__((ext_vector_type(2)));
+  using bf16x2_t = __bf16 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 
 template <int kAct>
@@ -165,8 +162,9 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned ntiles) {
 //       6 as 3 without a residual (s = acc; y = act(acc*s+t)).
 // kIm2col: false = 1x1/stride-1 (A is X itself), true = implicit GEMM gather.
 // kPro (1x1 path): the A operand is relu(X * pscale[c] + pshift[c]) (the consumer's
-//       pre-activation BN + ReLU applied while staging, rounded to bf16 as a separate
-//       pass would store it), so the producer never writes that activation to HBM.
+//       pre-activation BN + ReLU applied to the A fragments as they leave LDS, rounded to
+//       bf16 as a separate pass would store it), so the producer never writes that
+//       activation to HBM.
 // kDual (1x1 path): A = [X | strided X2] along K, W = [W1 | W2]: the ResNet projection
 //       block's conv3 and its shortcut conv as one GEMM, so the shortcut output is never
 //       written to HBM and read back as the residual.
@@ -186,7 +184,9 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   constexpr int kStage = 2 * (kAStage + kWStage);
   constexpr int kCStride = BN + 4;  // fp32 epilogue tile row stride (16-B multiple)
   constexpr int kEpiBytes = BM * kCStride * 4;
-  constexpr int kLds = kStage > kEpiBytes ? kStage : kEpiBytes;
+  constexpr int kLdsMain = kStage > kEpiBytes ? kStage : kEpiBytes;
+  constexpr int kParam = kPro ? 512 : 0;  // prologue scale | shift of one K-tile (fp32 x 64 x 2)
+  constexpr int kLds = kLdsMain + 2 * kParam;
   constexpr int kALoads = BM * 8 / kThreads;  // 16-B chunks per thread per K-tile
   constexpr int kWLoads = BN * 8 / kThreads;
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLds];
@@ -199,6 +199,7 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   // would be a static initializer, which the AMDGPU backend cannot emit).
   auto a_lds = [&](int b) { return reinterpret_cast<u32x4*>(smem + b * kAStage); };
   auto w_lds = [&](int b) { return reinterpret_cast<u32x4*>(smem + 2 * kAStage + b * kWStage); };
+  auto p_lds = [&](int b) { return reinterpret_cast<u32x4*>(smem + kLdsMain + b * kParam); };
 
   // Operands are read through buffer descriptors with 32-bit byte offsets: per thread a
   // fixed voffset, the K position as the scalar soffset, so a K-tile's loads cost no
@@ -210,17 +211,14 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   const __amdgpu_buffer_rsrc_t xr2 = make_rsrc(kDual ? static_cast<const void*>(X2) : X, kDual ? p.x2_bytes : 0u);
   const unsigned nk1 = p.C / kBK;       // K-tiles from source 1
   int a_pix[kALoads], a_ih0[kALoads], a_iw0[kALoads];
-  unsigned a_dst[kALoads];
   const unsigned cbytes = p.C * 2u;  // input pixel stride (im2col path)
-  // Staging: LDS-DMA except on the prologue path (it transforms A in registers). An
-  // LDS-DMA image is lane-linear (lane l of piece i fills 16-B slot (tid + 256 i) of the
-  // buffer), so the XOR swizzle moves to the source: slot (row r, chunk ch) is loaded
-  // from logical chunk swz(r, ch) (the swizzle is an involution).
-  constexpr bool kDma = !kPro;
+  // Staging is LDS-DMA. Its image is lane-linear (lane l of piece i fills 16-B slot
+  // tid + 256 i of the buffer), so the XOR swizzle moves to the source: slot (row r,
+  // chunk ch) is loaded from logical chunk swz(r, ch) (the swizzle is an involution).
   const unsigned wv = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
   for (int i = 0; i < kALoads; i++) {
-    const unsigned c = tid + i * kThreads, r = c >> 3, ch = kDma ? swz(r, c & 7u) : (c & 7u);
+    const unsigned c = tid + i * kThreads, r = c >> 3, ch = swz(r, c & 7u);
     const unsigned gm = (m0 + r < M) ? m0 + r : M - 1u;
     if constexpr (kIm2col) {
       const unsigned plane = p.OH * p.OW;
@@ -242,41 +240,31 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
         a_vo2[i] = ((img * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * (p.C2 * 2u) + ch * 16u;
       }
     }
-    a_dst[i] = r * 8u + swz(r, ch);
   }
-  unsigned w_vo[kWLoads], w_dst[kWLoads];
+  unsigned w_vo[kWLoads];
 #pragma unroll
   for (int i = 0; i < kWLoads; i++) {
-    const unsigned c = tid + i * kThreads, r = c >> 3, ch = kDma ? swz(r, c & 7u) : (c & 7u);
+    const unsigned c = tid + i * kThreads, r = c >> 3, ch = swz(r, c & 7u);
     w_vo[i] = (n0 + r) * krow + ch * 16u;
-    w_dst[i] = r * 8u + swz(r, ch);
   }
+  // Prologue parameters ride along with each K-tile: lanes 0-15 of wave 0 DMA the tile's
+  // 64 scales, then its 64 shifts, into the buffer's parameter slot.
+  const __amdgpu_buffer_rsrc_t psr = make_rsrc(kPro ? static_cast<const void*>(pscale) : X, kPro ? K * 4u : 0u);
+  const __amdgpu_buffer_rsrc_t ptr_ = make_rsrc(kPro ? static_cast<const void*>(pshift) : X, kPro ? K * 4u : 0u);
   // im2col: the K-tile's (kh, kw) tap and channel block, advanced one K-tile per load
   // (wave-uniform scalars). A tap's bounds checks run once per tap, not per K-tile.
   const unsigned cpt = p.C / kBK;
   unsigned t_c0 = 0, t_kw = 0, t_kh = 0;
 
-  // One K-tile in registers on its way to LDS.
-  struct Stage {
-    u32x4 ra[kDma ? 1 : kALoads], rw[kDma ? 1 : kWLoads];
-    // Prologue parameters: a thread's A chunks all hold channels (tid & 7) * 8 .. + 7 of
-    // the K-tile (256 threads cover 8 chunks per row), so one set of 8 per K-tile.
-    float ps[kPro ? 8 : 1], pt[kPro ? 8 : 1];
-  };
   // The wave's LDS-DMA destination for piece i of buffer `base`.
   auto slot = [&](u32x4* base, int i) { return base + wv * 64u + (unsigned)i * kThreads; };
-  auto load_tile = [&](unsigned kt, Stage& st, int b) {
+  auto load_tile = [&](unsigned kt, int b) {
     const unsigned koff = kt * (kBK * 2u);  // bytes along K
     if constexpr (kPro) {
-      const unsigned c0 = kt * kBK + (tid & 7u) * 8u;
-      const float4 s0 = *reinterpret_cast<const float4*>(pscale + c0);
-      const float4 s1 = *reinterpret_cast<const float4*>(pscale + c0 + 4);
-      const float4 t0 = *reinterpret_cast<const float4*>(pshift + c0);
-      const float4 t1 = *reinterpret_cast<const float4*>(pshift + c0 + 4);
-      st.ps[0] = s0.x; st.ps[1] = s0.y; st.ps[2] = s0.z; st.ps[3] = s0.w;
-      st.ps[4] = s1.x; st.ps[5] = s1.y; st.ps[6] = s1.z; st.ps[7] = s1.w;
-      st.pt[0] = t0.x; st.pt[1] = t0.y; st.pt[2] = t0.z; st.pt[3] = t0.w;
-      st.pt[4] = t1.x; st.pt[5] = t1.y; st.pt[6] = t1.z; st.pt[7] = t1.w;
+      if (wv == 0 && lane < 16u) {
+        dma16(psr, p_lds(b), lane * 16u, kt * (kBK * 4u));
+        dma16(ptr_, p_lds(b) + 16, lane * 16u, kt * (kBK * 4u));
+      }
     }
     if constexpr (kIm2col) {
       if (t_c0 == 0) {  // first K-tile of a new tap
@@ -289,10 +277,7 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
       }
       const unsigned soff = t_c0 * (kBK * 2u);
 #pragma unroll
-      for (int i = 0; i < kALoads; i++) {
-        if constexpr (kDma) dma16(xr, slot(a_lds(b), i), a_vo[i], soff);
-        else st.ra[i] = ld16(xr, a_vo[i], soff);
-      }
+      for (int i = 0; i < kALoads; i++) dma16(xr, slot(a_lds(b), i), a_vo[i], soff);
       if (++t_c0 == cpt) {
         t_c0 = 0;
         if (++t_kw == p.KW) t_kw = 0, t_kh++;
@@ -303,31 +288,10 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
       for (int i = 0; i < kALoads; i++) dma16(xr2, slot(a_lds(b), i), a_vo2[i], koff2);
     } else {
 #pragma unroll
-      for (int i = 0; i < kALoads; i++) {
-        if constexpr (kDma) dma16(xr, slot(a_lds(b), i), a_vo[i], koff);
-        else st.ra[i] = ld16(xr, a_vo[i], koff);
-      }
+      for (int i = 0; i < kALoads; i++) dma16(xr, slot(a_lds(b), i), a_vo[i], koff);
     }
 #pragma unroll
-    for (int i = 0; i < kWLoads; i++) {
-      if constexpr (kDma) dma16(wr, slot(w_lds(b), i), w_vo[i], koff);
-      else st.rw[i] = ld16(wr, w_vo[i], koff);
-    }
-  };
-  auto store_tile = [&](int b, Stage& st) {  // register path only
-    if constexpr (kPro) {
-#pragma unroll
-      for (int i = 0; i < kALoads; i++) {
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          st.ra[i][k] = pack_bf16(fmaxf(fmaf(bf_lo(st.ra[i][k]), st.ps[2 * k], st.pt[2 * k]), 0.f),
-                                  fmaxf(fmaf(bf_hi(st.ra[i][k]), st.ps[2 * k + 1], st.pt[2 * k + 1]), 0.f));
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < kALoads; i++) a_lds(b)[a_dst[i]] = st.ra[i];
-#pragma unroll
-    for (int i = 0; i < kWLoads; i++) w_lds(b)[w_dst[i]] = st.rw[i];
+    for (int i = 0; i < kWLoads; i++) dma16(wr, slot(w_lds(b), i), w_vo[i], koff);
   };
 
   const unsigned wm = wave / WN, wn = wave % WN;
@@ -343,10 +307,26 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
     for (int kk = 0; kk < kBK / 32; kk++) {
       const unsigned chunk = kk * 4u + (lane >> 4);
       bf16x8 af[FM], bfr[FN];
+      // Prologue: this lane's fragments hold channels 8 * chunk .. + 7 of the K-tile.
+      float ps[kPro ? 8 : 1], pt[kPro ? 8 : 1];
+      if constexpr (kPro) {
+        const float4* pp = reinterpret_cast<const float4*>(p_lds(b));
+        const float4 s0 = pp[2 * chunk], s1 = pp[2 * chunk + 1], t0 = pp[16 + 2 * chunk], t1 = pp[17 + 2 * chunk];
+        ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w; ps[4] = s1.x; ps[5] = s1.y; ps[6] = s1.z; ps[7] = s1.w;
+        pt[0] = t0.x; pt[1] = t0.y; pt[2] = t0.z; pt[3] = t0.w; pt[4] = t1.x; pt[5] = t1.y; pt[6] = t1.z; pt[7] = t1.w;
+      }
 #pragma unroll
       for (int i = 0; i < FM; i++) {
         const unsigned r = row_base + i * 16u + (lane & 15u);
-        af[i] = __builtin_bit_cast(bf16x8, a_lds(b)[r * 8u + swz(r, chunk)]);
+        u32x4 v = a_lds(b)[r * 8u + swz(r, chunk)];
+        if constexpr (kPro) {
+          // relu(x * scale + shift), rounded to bf16 as a separate pass would store it.
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            v[k] = pack_bf16(fmaxf(fmaf(bf_lo(v[k]), ps[2 * k], pt[2 * k]), 0.f),
+                             fmaxf(fmaf(bf_hi(v[k]), ps[2 * k + 1], pt[2 * k + 1]), 0.f));
+        }
+        af[i] = __builtin_bit_cast(bf16x8, v);
       }
 #pragma unroll
       for (int j = 0; j < FN; j++) {
@@ -361,7 +341,6 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
   };
 
   const unsigned nk = K / kBK;
-  Stage s0;
   // The residual tile does not depend on the GEMM: its loads go out with the first
   // K-tile's, so they are in flight together and complete under the MFMAs instead of
   // stalling the epilogue.
@@ -385,37 +364,21 @@ __device__ __forceinline__ void conv_tile(const u32x4* __restrict__ X, const u32
       }
     }
   };
-  if constexpr (kDma) {
-    // Step kt: barrier (its vmcnt(0) retires tile kt's LDS-DMA), start tile kt + 1's
-    // LDS-DMA into the buffer step kt - 1 read, compute tile kt. A 3-deep ring (two tiles
-    // in flight, counted vmcnt + bare s_barrier) was slower on 19 of 23 ResNet-50 layers:
-    // it costs a block per CU of LDS (profiles/r1al). So was a transposed product with
-    // the epilogue on the accumulators (4 channels of a pixel per lane, no LDS round
-    // trip): its 8-byte residual loads and output stores made the memory-bound layers up
-    // to 1.6x slower (profiles/r1am).
-    prefetch_residual();
-    load_tile(0, s0, 0);
-    for (unsigned kt = 0; kt < nk; kt++) {
-      __syncthreads();
-      if (kt + 1 < nk) load_tile(kt + 1, s0, (kt & 1) ^ 1);
-      compute(kt & 1);
-    }
-    __syncthreads();  // every wave's last fragment reads before the epilogue reuses LDS
-  } else {
-    load_tile(0, s0, 0);
-    prefetch_residual();
-    store_tile(0, s0);
+  // Step kt: barrier (its vmcnt(0) retires tile kt's LDS-DMA), start tile kt + 1's LDS-DMA
+  // into the buffer step kt - 1 read, compute tile kt. A 3-deep ring (two tiles in
+  // flight, counted vmcnt + bare s_barrier) was slower on 19 of 23 ResNet-50 layers: it
+  // costs a block per CU of LDS (profiles/r1al). So was a transposed product with the
+  // epilogue on the accumulators (4 channels of a pixel per lane, no LDS round trip): its
+  // 8-byte residual loads and output stores made the memory-bound layers up to 1.6x
+  // slower (profiles/r1am).
+  prefetch_residual();
+  load_tile(0, 0);
+  for (unsigned kt = 0; kt < nk; kt++) {
     __syncthreads();
-    // One register stage: tile k+1's loads are in flight while tile k feeds the MFMAs. A
-    // second register stage was measured slower on every ResNet-50 layer: it needs 32
-    // more VGPRs per stage and drops BN=128 to one wave per SIMD (profiles/r1t).
-    for (unsigned kt = 0; kt < nk; kt++) {
-      if (kt + 1 < nk) load_tile(kt + 1, s0, 0);
-      compute(kt & 1);
-      if (kt + 1 < nk) store_tile((kt & 1) ^ 1, s0);
-      __syncthreads();
-    }
+    if (kt + 1 < nk) load_tile(kt + 1, (kt & 1) ^ 1);
+    compute(kt & 1);
   }
+  __syncthreads();  // every wave's last fragment reads before the epilogue reuses LDS
 
   // Accumulators -> LDS (fp32, row-major [128][BN + 4]); C/D map of 16x16x32:
   // col = lane & 15, row = 4 * (lane >> 4) + reg.

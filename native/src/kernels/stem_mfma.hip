@@ -57,10 +57,11 @@ constexpr int kThreads = 256;
 __device__ __forceinline__ float bf_lo(unsigned v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float bf_hi(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
 
+// Two floats -> packed bf16 pair (round to nearest even) in one v_cvt_pk_bf16_f32.
 __device__ __forceinline__ unsigned pack_bf16(float lo, float hi) {
-  __hip_bfloat16 a = __float2bfloat16(lo);
-  __hip_bfloat16 b = __float2bfloat16(hi);
-  return (unsigned)__bfloat16_as_ushort(a) | ((unsigned)__bfloat16_as_ushort(b) << 16);
+  using f32x2_t = float __attribute__((ext_vector_type(2)));
+  using bf16x2_t = __bf16 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 
 __device__ __forceinline__ void stem_tile(const unsigned short* __restrict__ X, const u32x4* __restrict__ Wk,
