@@ -296,6 +296,11 @@ class Runner:
         self.y = y.to(self.device)
         if case.train:
             model.train()
+            if fuse and isinstance(model, LSTMSentiment) and dtype == torch.bfloat16 and self.device.type == "cuda":
+                # Forward and backward recurrences in whole-sequence HIP kernels
+                # (ops/fused.py::FusedLSTMTrainLast): graph-capturable, unlike MIOpen's RNN.
+                from ..ops.fused import FusedLSTMTrainLast
+                model.last = FusedLSTMTrainLast(model.lstm)
             self.opt = torch.optim.SGD(model.parameters(), lr=1e-3, momentum=0.9)
         else:
             model.eval()
@@ -324,8 +329,10 @@ class Runner:
                 model = model.to(dtype)
             self.x = self.x.to(dtype)
             self.opt = None
-        self.fused = fuse and not case.train and (type(model).__name__ == "FusedResNetV2" or any(
-            type(m).__name__ in ("ConvBNAct", "ConvBiasAct", "FusedLSTMLast") for m in model.modules()))
+        self.fused = fuse and (not case.train or isinstance(model, LSTMSentiment)) and (
+            type(model).__name__ == "FusedResNetV2" or any(
+                type(m).__name__ in ("ConvBNAct", "ConvBiasAct", "FusedLSTMLast") or getattr(m, "fused", False) is True
+                for m in model.modules()))
         self.model = model
 
     def capture(self, warmup=3):
@@ -337,7 +344,7 @@ class Runner:
         autotuning and optimizer-state creation happen outside the capture."""
         if self.device.type != "cuda":
             raise ValueError("graph capture needs a GPU")
-        if self.case.train and self.case.kind == "sequence":
+        if self.case.train and self.case.kind == "sequence" and not self.fused:
             # Measured on MI355X (ROCm 7.2, PyTorch 2.10): capturing the MIOpen RNN
             # backward kills the process, so recurrent training always runs eagerly.
             raise NotImplementedError("MIOpen RNN training is not HIP-graph capturable")

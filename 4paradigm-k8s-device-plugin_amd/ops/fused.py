@@ -47,6 +47,10 @@ def _ops():
         L.vgpu_stem_bf16.restype = C.c_int
         L.vgpu_lstm_seq_bf16.argtypes = [C.c_void_p] * 6 + [C.c_int] * 3 + [C.c_void_p]
         L.vgpu_lstm_seq_bf16.restype = C.c_int
+        L.vgpu_lstm_seq_train_bf16.argtypes = [C.c_void_p] * 9 + [C.c_int] * 3 + [C.c_void_p]
+        L.vgpu_lstm_seq_train_bf16.restype = C.c_int
+        L.vgpu_lstm_seq_bwd_bf16.argtypes = [C.c_void_p] * 9 + [C.c_int] * 3 + [C.c_void_p]
+        L.vgpu_lstm_seq_bwd_bf16.restype = C.c_int
         L.vgpu_stem_set_block_cap.argtypes = [C.c_int]
         L.vgpu_bn_act_set_block_cap.argtypes = [C.c_int]
         # Inside a CU-masked vGPU every kernel's grid is capped to one dispatch round on
@@ -767,6 +771,149 @@ class FusedLSTMLast(nn.Module):
                 return self._fused(x)
             d = self.plan[key] = _time_us(lambda: self._fused(x)) <= _time_us(lambda: self._library(x))
         return self._fused(x) if d else self._library(x)
+
+
+def lstm_input_projection(x, w_ih, b_ih, b_hh, dtype):
+    """gx [B, T, 128, 4] = x . W_ih^T + b_ih + b_hh with W_ih's rows permuted so the four
+    gates (i, f, g, o) of one hidden unit are adjacent, the layout of ``lstm_mfma.hip``."""
+    B, T, Fin = x.shape
+    H = w_ih.shape[0] // 4
+    w = w_ih.view(4, H, Fin).permute(1, 0, 2).reshape(4 * H, Fin).to(dtype)
+    b = (b_ih.float() + b_hh.float()).view(4, H).t().reshape(4 * H).to(dtype)
+    return torch.addmm(b, x.reshape(B * T, Fin).to(dtype), w.t()).view(B, T, H, 4)
+
+
+def lstm_train_forward_reference(gx, w_hh, h0=None, c0=None):
+    """Plain-PyTorch mirror of ``vgpu_lstm_seq_train_bf16`` (fp32 math, h rounded to the
+    dtype of ``w_hh`` each step like the kernel's MFMA operand): returns hT, cT and the
+    stash act [B, T, H, 4] (sigmoid i, sigmoid f, tanh g, sigmoid o), cs [B, T, H], hs."""
+    B, T, H, _ = gx.shape
+    dev = gx.device
+    h = torch.zeros(B, H, device=dev) if h0 is None else h0.float()
+    c = torch.zeros(B, H, device=dev) if c0 is None else c0.float()
+    w = w_hh.float()
+    act = torch.empty(B, T, H, 4, device=dev)
+    cs = torch.empty(B, T, H, device=dev)
+    hs = torch.empty(B, T, H, device=dev, dtype=w_hh.dtype)
+    hq = h.to(w_hh.dtype).float()
+    for t in range(T):
+        z = gx[:, t].float() + (hq @ w.t()).view(B, 4, H).transpose(1, 2)
+        i, f, g, o = torch.sigmoid(z[..., 0]), torch.sigmoid(z[..., 1]), torch.tanh(z[..., 2]), torch.sigmoid(z[..., 3])
+        c = f * c + i * g
+        h = o * torch.tanh(c)
+        act[:, t] = torch.stack([i, f, g, o], -1)
+        cs[:, t] = c
+        hs[:, t] = h.to(w_hh.dtype)
+        hq = hs[:, t].float()
+    return h, c, act, cs, hs
+
+
+def lstm_bwd_reference(w_hh, act, cs, dhT, c0=None, dcT=None):
+    """Plain-PyTorch mirror of ``vgpu_lstm_seq_bwd_bf16``: BPTT of a loss on h_T over the
+    forward's stash. Returns dz [B, T, 4H] (pre-activation gate gradients, columns
+    i|f|g|o like PyTorch's weight rows, rounded to the dtype of ``w_hh`` like the kernel's
+    MFMA operand), dh0, dc0."""
+    B, T, H, _ = act.shape
+    w = w_hh.float()
+    dh = dhT.float()
+    dc = torch.zeros_like(dh) if dcT is None else dcT.float()
+    dz = torch.empty(B, T, 4 * H, device=act.device, dtype=w_hh.dtype)
+    for t in range(T - 1, -1, -1):
+        i, f, g, o = act[:, t].unbind(-1)
+        tc = torch.tanh(cs[:, t])
+        cp = cs[:, t - 1] if t > 0 else (torch.zeros_like(dh) if c0 is None else c0.float())
+        dct = dc + dh * o * (1 - tc * tc)
+        z = torch.cat([dct * g * i * (1 - i), dct * cp * f * (1 - f), dct * i * (1 - g * g), dh * tc * o * (1 - o)], 1)
+        dc = dct * f
+        dz[:, t] = z.to(w_hh.dtype)
+        dh = dz[:, t].float() @ w
+    return dz, dh, dc
+
+
+def lstm_weight_grads(dz, x, hs, h0=None):
+    """The library half of the backward: dW_ih = dz^T x, dW_hh = dz^T h_{t-1}, db = sum dz
+    (one GEMM each over all B*T steps)."""
+    B, T, G = dz.shape
+    H = hs.shape[-1]
+    first = torch.zeros(B, 1, H, device=hs.device, dtype=hs.dtype) if h0 is None else h0.to(hs.dtype).unsqueeze(1)
+    hprev = torch.cat([first, hs[:, :-1]], 1).reshape(B * T, H)
+    dzf = dz.reshape(B * T, G)
+    dw_ih = dzf.t().mm(x.reshape(B * T, -1).to(dz.dtype))
+    dw_hh = dzf.t().mm(hprev.to(dz.dtype))
+    db = dzf.float().sum(0)
+    return dw_ih, dw_hh, db
+
+
+class _LSTMLastFn(torch.autograd.Function):
+    """h_T of a 1-layer, 128-unit LSTM with zero initial state, forward and backward on the
+    whole-sequence HIP kernels (``lstm_mfma.hip``): input projection (library GEMM) →
+    stashing recurrence kernel; backward recurrence kernel → three library GEMMs for the
+    weight gradients. Every piece runs on the current stream, so the training step is
+    HIP-graph capturable (MIOpen's RNN backward is not)."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh):
+        dt = torch.bfloat16
+        gx = lstm_input_projection(x, w_ih, b_ih, b_hh, dt).contiguous()
+        whh = w_hh.to(dt).contiguous()
+        B, T = x.shape[:2]
+        H = 128
+        hT = torch.empty(B, H, dtype=torch.float32, device=x.device)
+        act = torch.empty(B, T, H, 4, dtype=torch.float32, device=x.device)
+        cs = torch.empty(B, T, H, dtype=torch.float32, device=x.device)
+        hs = torch.empty(B, T, H, dtype=dt, device=x.device)
+        _same_device(x, whh, gx)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        rc = _ops().vgpu_lstm_seq_train_bf16(_ptr(gx), _ptr(whh), None, None, _ptr(hT), None, _ptr(act), _ptr(cs),
+                                             _ptr(hs), B, T, H, C.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"vgpu_lstm_seq_train_bf16 failed ({rc}) for x {tuple(x.shape)}")
+        ctx.save_for_backward(x, w_ih, whh, act, cs, hs)
+        return hT.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dhT):
+        x, w_ih, whh, act, cs, hs = ctx.saved_tensors
+        B, T = x.shape[:2]
+        H = 128
+        whhT = whh.t().contiguous()
+        dh = dhT.float().contiguous()
+        dz = torch.empty(B, T, 4 * H, dtype=torch.bfloat16, device=x.device)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        rc = _ops().vgpu_lstm_seq_bwd_bf16(_ptr(whhT), _ptr(act), _ptr(cs), None, _ptr(dh), None, _ptr(dz), None,
+                                           None, B, T, H, C.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"vgpu_lstm_seq_bwd_bf16 failed ({rc}) for x {tuple(x.shape)}")
+        dw_ih, dw_hh, db = lstm_weight_grads(dz, x, hs)
+        dx = dz.reshape(B * T, 4 * H).mm(w_ih.to(dz.dtype)).view_as(x).to(x.dtype) if ctx.needs_input_grad[0] else None
+        return (dx, dw_ih.to(w_ih.dtype), dw_hh.to(w_ih.dtype), db.to(w_ih.dtype), db.to(w_ih.dtype))
+
+
+class FusedLSTMTrainLast(nn.Module):
+    """Training form of ``FusedLSTMLast`` (the sentiment model's LSTM, only h_T used):
+    forward and backward through ``_LSTMLastFn`` on the live parameters of the wrapped
+    ``nn.LSTM`` (fp32 master weights, bf16 compute; gradients land in the LSTM's
+    ``.grad`` like the library path's). ``VGPU_MFMA_CONV=off`` selects the library LSTM."""
+
+    def __init__(self, lstm, mode=None):
+        super().__init__()
+        if (lstm.num_layers != 1 or lstm.bidirectional or not lstm.batch_first or lstm.hidden_size != 128
+                or not lstm.bias or getattr(lstm, "proj_size", 0)):
+            raise ValueError("FusedLSTMTrainLast needs a 1-layer, unidirectional, batch-first LSTM with 128 units")
+        self.lstm = lstm
+        self.mode = mode or os.environ.get("VGPU_MFMA_CONV", os.environ.get("VGPU_CONV1X1", "auto"))
+
+    @property
+    def fused(self):
+        return self.mode != "off"
+
+    def forward(self, x):
+        if not self.fused or not x.is_cuda:
+            out, _ = self.lstm(x)
+            return out[:, -1]
+        l = self.lstm
+        with torch.autocast(x.device.type, enabled=False):
+            return _LSTMLastFn.apply(x.to(torch.bfloat16), l.weight_ih_l0, l.weight_hh_l0, l.bias_ih_l0, l.bias_hh_l0)
 
 
 class ConvBNAct(nn.Module):

@@ -490,3 +490,117 @@ def test_lstm_recurrence_numerics(B, T):
         got = FusedLSTMLast(lstm, impl="hip", mode="on")(x).float()
     assert got.shape == ref.shape
     torch.testing.assert_close(got, ref, rtol=0, atol=3e-2)
+
+
+def _lstm_autograd_grads(lstm, x):
+    """dL/d(params) of L = sum(h_T * v) through PyTorch's own LSTM (fp32)."""
+    v = torch.linspace(-1, 1, 128, device=x.device)
+    lstm.zero_grad()
+    out, _ = lstm(x)
+    (out[:, -1] * v).sum().backward()
+    return v, out[:, -1].detach(), {n: p_.grad.clone() for n, p_ in lstm.named_parameters()}
+
+
+def test_lstm_training_reference_matches_autograd_cpu():
+    """The math the training kernels implement (forward stash, BPTT over the stash, the
+    three weight-gradient GEMMs), mirrored in PyTorch, equals autograd through nn.LSTM
+    (fp32 throughout, so no operand rounding)."""
+    from amdvgpu.ops.fused import (lstm_bwd_reference, lstm_input_projection, lstm_train_forward_reference,
+                                   lstm_weight_grads)
+    torch.manual_seed(0)
+    lstm = nn.LSTM(20, 128, batch_first=True)
+    x = torch.randn(3, 9, 20)
+    v, href, g = _lstm_autograd_grads(lstm, x)
+    gx = lstm_input_projection(x, lstm.weight_ih_l0, lstm.bias_ih_l0, lstm.bias_hh_l0, torch.float32)
+    hT, _, act, cs, hs = lstm_train_forward_reference(gx, lstm.weight_hh_l0.detach())
+    torch.testing.assert_close(hT, href, rtol=1e-5, atol=1e-5)
+    dz, _, _ = lstm_bwd_reference(lstm.weight_hh_l0.detach(), act, cs, v.expand(3, 128))
+    dw_ih, dw_hh, db = lstm_weight_grads(dz, x, hs)
+    torch.testing.assert_close(dw_ih, g["weight_ih_l0"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dw_hh, g["weight_hh_l0"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(db, g["bias_ih_l0"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(db, g["bias_hh_l0"], rtol=1e-4, atol=1e-5)
+
+
+def test_lstm_train_module_cpu_is_library_path():
+    """Off the GPU FusedLSTMTrainLast is the library LSTM's last step (same gradients)."""
+    from amdvgpu.ops.fused import FusedLSTMTrainLast
+    torch.manual_seed(0)
+    lstm = nn.LSTM(12, 128, batch_first=True)
+    x = torch.randn(2, 4, 12)
+    f = FusedLSTMTrainLast(lstm)
+    out, _ = lstm(x)
+    torch.testing.assert_close(f(x), out[:, -1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T", [(10, 1024), (20, 64), (3, 7)])
+def test_lstm_training_kernels_numerics(B, T):
+    """HIP training forward (stash) and backward recurrence kernels vs (a) their PyTorch
+    mirror on identical bf16 operands and (b) autograd through PyTorch's fp32 LSTM on the
+    same bf16-rounded weights. B=20 leaves a partial 16-row workgroup."""
+    from amdvgpu.ops.fused import (_ops, _ptr, lstm_bwd_reference, lstm_input_projection,
+                                   lstm_train_forward_reference, FusedLSTMTrainLast)
+    import ctypes as C
+    torch.manual_seed(2)
+    lstm = nn.LSTM(300, 128, batch_first=True).cuda()
+    with torch.no_grad():
+        for p_ in lstm.parameters():
+            p_.copy_(p_.to(torch.bfloat16).float())
+    x = torch.randn(B, T, 300, device="cuda").to(torch.bfloat16)
+    # (a) kernels vs the mirror, step for step
+    gx = lstm_input_projection(x, lstm.weight_ih_l0.detach(), lstm.bias_ih_l0.detach(), lstm.bias_hh_l0.detach(),
+                               torch.bfloat16).contiguous()
+    whh = lstm.weight_hh_l0.detach().to(torch.bfloat16).contiguous()
+    hT = torch.empty(B, 128, device="cuda")
+    act = torch.empty(B, T, 128, 4, device="cuda")
+    cs = torch.empty(B, T, 128, device="cuda")
+    hs = torch.empty(B, T, 128, device="cuda", dtype=torch.bfloat16)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert _ops().vgpu_lstm_seq_train_bf16(_ptr(gx), _ptr(whh), None, None, _ptr(hT), None, _ptr(act), _ptr(cs),
+                                           _ptr(hs), B, T, 128, st) == 0
+    v = torch.linspace(-1, 1, 128, device="cuda")
+    dhT = v.expand(B, 128).contiguous()
+    dz = torch.empty(B, T, 512, device="cuda", dtype=torch.bfloat16)
+    dh0 = torch.empty(B, 128, device="cuda")
+    whhT = whh.t().contiguous()
+    assert _ops().vgpu_lstm_seq_bwd_bf16(_ptr(whhT), _ptr(act), _ptr(cs), None, _ptr(dhT), None, _ptr(dz),
+                                         _ptr(dh0), None, B, T, 128, st) == 0
+    torch.cuda.synchronize()
+    if T <= 64:
+        rh, _, ract, rcs, _ = lstm_train_forward_reference(gx, whh)
+        torch.testing.assert_close(hT, rh, rtol=0, atol=2e-2)
+        torch.testing.assert_close(act, ract, rtol=0, atol=3e-2)
+        rdz, rdh0, _ = lstm_bwd_reference(whh, act, cs, dhT)  # on the kernel's own stash
+        torch.testing.assert_close(dz.float(), rdz.float(), rtol=2e-2, atol=2e-3)
+        torch.testing.assert_close(dh0, rdh0, rtol=2e-2, atol=2e-3)
+    # (b) the autograd Function vs fp32 autograd through nn.LSTM
+    _, href, g = _lstm_autograd_grads(lstm, x.float())
+    lstm.zero_grad()
+    h = FusedLSTMTrainLast(lstm, mode="on")(x)
+    (h.float() * v).sum().backward()
+    torch.testing.assert_close(h.float(), href, rtol=0, atol=3e-2)
+    for n in ("weight_ih_l0", "weight_hh_l0", "bias_ih_l0"):
+        got, ref = getattr(lstm, n).grad, g[n]
+        cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0)
+        rel = (got - ref).norm() / ref.norm()
+        assert cos > 0.995 and rel < 0.1, (n, float(cos), float(rel))
+
+
+@pytest.mark.gpu
+def test_lstm_training_step_graph_capturable():
+    """The fused LSTM training step (forward, loss, backward, SGD) replays from a HIP graph:
+    every replay updates the weights (the captured loss changes) and stays finite."""
+    from amdvgpu.models.aibench import Runner, get_case
+    r = Runner(get_case("lstm-train"), "cuda:0", batch=10)
+    assert r.fused
+    r.x = r.x[:, :128].contiguous()
+    w0 = r.model.lstm.weight_hh_l0.detach().clone()
+    assert torch.isfinite(r.step()).item()
+    r.capture(warmup=2)
+    losses = []
+    for _ in range(3):
+        losses.append(float(r.step()))
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(torch.tensor(losses))) and len(set(losses)) == 3, losses
+    assert not torch.equal(w0, r.model.lstm.weight_hh_l0.detach())
