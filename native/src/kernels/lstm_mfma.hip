@@ -43,8 +43,29 @@ constexpr int kThreads = kWaves * 64;
 __device__ __forceinline__ float bf_lo(unsigned v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float bf_hi(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
 __device__ __forceinline__ unsigned short to_bf16(float f) { return __bfloat16_as_ushort(__float2bfloat16(f)); }
-__device__ __forceinline__ float sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// Raw v_exp_f32 + v_rcp_f32 (1 ulp): an IEEE division here expanded to ~10 VALU
+// instructions per gate and made the serial step VALU-bound (profiles/r1ax).
+__device__ __forceinline__ float sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
 __device__ __forceinline__ float tanh_fast(float x) { return 2.0f * sigmoid(2.0f * x) - 1.0f; }
+
+// Raw buffer descriptor over [p, p + bytes) (bytes < 2^31, checked on the host). Per-step
+// traffic goes through these: a lane's voffset is fixed for the whole sequence and the
+// step is the wave-uniform soffset, so there is no 64-bit address arithmetic in the serial
+// loop, and a row past the batch gets voffset kOOB: its stores are dropped by the range
+// check instead of branched around.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr unsigned kOOB = 0x80000000u;
+// A per-step soffset made provably wave-uniform (else the buffer op is wrapped in a
+// readfirstlane waterfall loop).
+__device__ __forceinline__ unsigned uni(unsigned v) { return (unsigned)__builtin_amdgcn_readfirstlane((int)v); }
 
 // gx: [B, T, 128, 4] bf16 (gate order i, f, g, o), whh: [512, 128] bf16 (PyTorch
 // weight_hh_l0, rows i|f|g|o), h0/c0: [B, 128] fp32 or null (zeros), hT/cT: [B, 128] fp32
@@ -57,6 +78,11 @@ __global__ void __launch_bounds__(kThreads) lstm_kernel(const u32x2* __restrict_
                                                        float* __restrict__ hT, float* __restrict__ cT,
                                                        float4* __restrict__ act, float* __restrict__ cs,
                                                        unsigned short* __restrict__ hs, unsigned B, unsigned T) {
+  const unsigned cells = B * T * kH;  // < 2^27 (host check): every byte range below < 2^31
+  const __amdgpu_buffer_rsrc_t gxr = make_rsrc(gx, cells * 8u);
+  const __amdgpu_buffer_rsrc_t actr = make_rsrc(kStash ? static_cast<const void*>(act) : gx, kStash ? cells * 16u : 0u);
+  const __amdgpu_buffer_rsrc_t csr = make_rsrc(kStash ? static_cast<const void*>(cs) : gx, kStash ? cells * 4u : 0u);
+  const __amdgpu_buffer_rsrc_t hsr = make_rsrc(kStash ? static_cast<const void*>(hs) : gx, kStash ? cells * 2u : 0u);
   __shared__ __attribute__((aligned(16))) unsigned short hbuf[2][kRows][kH];
   const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const unsigned l16 = lane & 15u, q4 = lane >> 4;  // q4: k-quarter for A/B, row group for C/D
@@ -84,22 +110,26 @@ __global__ void __launch_bounds__(kThreads) lstm_kernel(const u32x2* __restrict_
       h[jj][r] = (ok && h0) ? h0[(size_t)b * kH + u] : 0.f;
       hbuf[0][4u * q4 + r][u] = to_bf16(h[jj][r]);
     }
-  // Gate-input addresses (row clamped to a valid one past the batch; never stored).
-  const u32x2* gsrc[2][4];
+  // Cell index of (row, unit) at step 0 (+ t * kH per step); gate inputs of a row past the
+  // batch are read from a clamped valid row (never stored), its stash stores are dropped.
+  unsigned e_ld[2][4], e_st[2][4];
 #pragma unroll
   for (int jj = 0; jj < 2; jj++)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      unsigned b = b0 + 4u * q4 + r;
-      b = b < B ? b : B - 1u;
-      const unsigned u = wave * kUnitsPerWave + 16u * jj + l16;
-      gsrc[jj][r] = gx + (size_t)b * T * kH + u;  // + t * kH per step
+      const unsigned b = b0 + 4u * q4 + r, u = wave * kUnitsPerWave + 16u * jj + l16;
+      e_ld[jj][r] = ((b < B ? b : B - 1u) * T) * kH + u;
+      e_st[jj][r] = b < B ? (b * T) * kH + u : kOOB;
     }
+  auto ld_gx = [&](int jj, int r, unsigned t) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(gxr, e_ld[jj][r] * 8u, uni(t * (kH * 8u)), 0);
+    return u32x2{v[0], v[1]};
+  };
   u32x2 gcur[2][4];
 #pragma unroll
   for (int jj = 0; jj < 2; jj++)
 #pragma unroll
-    for (int r = 0; r < 4; r++) gcur[jj][r] = gsrc[jj][r][0];
+    for (int r = 0; r < 4; r++) gcur[jj][r] = ld_gx(jj, r, 0);
   __syncthreads();
 
   for (unsigned t = 0; t < T; t++) {
@@ -110,7 +140,7 @@ __global__ void __launch_bounds__(kThreads) lstm_kernel(const u32x2* __restrict_
 #pragma unroll
     for (int jj = 0; jj < 2; jj++)
 #pragma unroll
-      for (int r = 0; r < 4; r++) gnext[jj][r] = gsrc[jj][r][(size_t)tn * kH];
+      for (int r = 0; r < 4; r++) gnext[jj][r] = ld_gx(jj, r, tn);
 
     f32x4 acc[8];
 #pragma unroll
@@ -138,13 +168,12 @@ __global__ void __launch_bounds__(kThreads) lstm_kernel(const u32x2* __restrict_
         const unsigned short hb = to_bf16(h[jj][r]);
         hbuf[cur ^ 1u][4u * q4 + r][wave * kUnitsPerWave + 16u * jj + l16] = hb;
         if constexpr (kStash) {
-          const unsigned b = b0 + 4u * q4 + r;
-          if (b < B) {
-            const size_t o = ((size_t)b * T + t) * kH + wave * kUnitsPerWave + 16u * jj + l16;
-            act[o] = make_float4(si, sf, tg, so);
-            cs[o] = cn;
-            hs[o] = hb;
-          }
+          const unsigned e = e_st[jj][r];  // kOOB (dropped) past the batch
+          using u32x4_t = unsigned int __attribute__((ext_vector_type(4)));
+          const u32x4_t a4 = {__float_as_uint(si), __float_as_uint(sf), __float_as_uint(tg), __float_as_uint(so)};
+          __builtin_amdgcn_raw_buffer_store_b128(a4, actr, e == kOOB ? kOOB : e * 16u, uni(t * (kH * 16u)), 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cn), csr, e == kOOB ? kOOB : e * 4u, uni(t * (kH * 4u)), 0);
+          __builtin_amdgcn_raw_buffer_store_b16(hb, hsr, e == kOOB ? kOOB : e * 2u, uni(t * (kH * 2u)), 0);
         }
       }
 #pragma unroll
@@ -176,6 +205,9 @@ __global__ void __launch_bounds__(kThreads) lstm_kernel(const u32x2* __restrict_
 // double-buffered LDS image (rows padded by 16 B: conflict-free fragment reads).
 // dz is also written out ([B, T, 512] bf16, columns gate-major i|f|g|o like PyTorch's
 // weight rows) for the weight-gradient GEMMs. dh0/dc0: gradients of the initial state.
+// Its per-step traffic stays on plain global pointers: moving it to buffer descriptors
+// like the forward's pushed the kernel to 256 VGPRs, the compiler then serialised the
+// next step's loads (vmcnt(0) after each) and the kernel ran 2x slower (profiles/r1ay).
 constexpr int kG = 4 * kH;       // gate columns
 constexpr int kZStride = kG + 8;  // bf16 per LDS row of dz
 
@@ -309,7 +341,7 @@ extern "C" {
 int vgpu_lstm_seq_bf16(const void* gx, const void* whh, const float* h0, const float* c0, float* hT, float* cT,
                        int batch, int steps, int hidden, void* stream) {
   if (!gx || !whh || !hT || batch <= 0 || steps <= 0 || hidden != kH) return -1;
-  if ((int64_t)batch * steps * kH * 4 >= ((int64_t)1 << 34)) return -1;
+  if ((int64_t)batch * steps * kH * 8 >= ((int64_t)1 << 31)) return -1;  // buffer-descriptor range
   auto misaligned = [](const void* p, uintptr_t a) { return p && (reinterpret_cast<uintptr_t>(p) & (a - 1)); };
   if (misaligned(gx, 8) || misaligned(whh, 16) || misaligned(h0, 4) || misaligned(c0, 4) || misaligned(hT, 4) ||
       misaligned(cT, 4))
@@ -328,7 +360,7 @@ int vgpu_lstm_seq_train_bf16(const void* gx, const void* whh, const float* h0, c
                              float* cT, float* act, float* cs, void* hs, int batch, int steps, int hidden,
                              void* stream) {
   if (!gx || !whh || !hT || !act || !cs || !hs || batch <= 0 || steps <= 0 || hidden != kH) return -1;
-  if ((int64_t)batch * steps * kH * 16 >= ((int64_t)1 << 40)) return -1;
+  if ((int64_t)batch * steps * kH * 16 >= ((int64_t)1 << 31)) return -1;  // buffer-descriptor ranges
   auto misaligned = [](const void* p, uintptr_t a) { return p && (reinterpret_cast<uintptr_t>(p) & (a - 1)); };
   if (misaligned(gx, 8) || misaligned(whh, 16) || misaligned(h0, 4) || misaligned(c0, 4) || misaligned(hT, 4) ||
       misaligned(cT, 4) || misaligned(act, 16) || misaligned(cs, 4) || misaligned(hs, 2))
@@ -349,7 +381,7 @@ int vgpu_lstm_seq_bwd_bf16(const void* whhT, const float* act, const float* cs, 
                            const float* dcT, void* dz, float* dh0, float* dc0, int batch, int steps, int hidden,
                            void* stream) {
   if (!whhT || !act || !cs || !dhT || !dz || batch <= 0 || steps <= 0 || hidden != kH) return -1;
-  if ((int64_t)batch * steps * kH * 16 >= ((int64_t)1 << 40)) return -1;
+  if ((int64_t)batch * steps * kH * 16 >= ((int64_t)1 << 31)) return -1;  // buffer-descriptor ranges
   auto misaligned = [](const void* p, uintptr_t a) { return p && (reinterpret_cast<uintptr_t>(p) & (a - 1)); };
   if (misaligned(whhT, 16) || misaligned(act, 16) || misaligned(cs, 4) || misaligned(c0, 4) || misaligned(dhT, 4) ||
       misaligned(dcT, 4) || misaligned(dz, 2) || misaligned(dh0, 4) || misaligned(dc0, 4))
