@@ -20,7 +20,7 @@ def _run(argv):
     ap.add_argument("--hbm", default=None, help="HBM-resident share (with --oversubscribe)")
     ap.add_argument("--cu", type=int, default=None, help="CU share in percent")
     ap.add_argument("--cu-range", default=None, help="logical CU range b-e")
-    ap.add_argument("--cu-mode", default=None, choices=["spatial", "temporal", "both", "off"])
+    ap.add_argument("--cu-mode", default=None, choices=["auto", "spatial", "temporal", "both", "off"])
     ap.add_argument("--oversubscribe", action="store_true")
     ap.add_argument("--region", default=None, help="shared region file (default: a fresh /tmp file)")
     ap.add_argument("--keep-region", action="store_true")

@@ -13,7 +13,7 @@ from dataclasses import dataclass, field
 PARTITION_NONE, PARTITION_SINGLE, PARTITION_MIXED = "none", "single", "mixed"
 LIST_ENVVAR, LIST_AMD_RUNTIME, LIST_VOLUME_MOUNTS = "envvar", "amd-container-runtime", "volume-mounts"
 ID_UUID, ID_INDEX = "uuid", "index"
-CU_MODES = ("spatial", "temporal", "both", "off")
+CU_MODES = ("auto", "spatial", "temporal", "both", "off")
 DEFAULT_RESOURCE = "amd.com/gpu"
 DEFAULT_PLUGIN_DIR = "/var/lib/kubelet/device-plugins/"
 DEFAULT_VGPU_DIR = "/usr/local/vgpu"
@@ -39,7 +39,7 @@ class PluginConfig:
     enable_legacy_preferred: bool = False
     verbose: int = 0
     # MI355X additions
-    cu_mode: str = "spatial"
+    cu_mode: str = "auto"
     backend: str = "auto"
     fake_devices: str = ""
     resource_name: str = DEFAULT_RESOURCE
@@ -96,7 +96,8 @@ _FLAGS = [
     ("--enable-legacy-preferred", "enable_legacy_preferred", "bool", ["ENABLE_LEGACY_PREFERRED"],
      "preferred allocation for kubelets without GetPreferredAllocation"),
     ("--verbose", "verbose", int, ["VERBOSE"], "log verbosity"),
-    ("--cu-mode", "cu_mode", str, ["CU_MODE"], "CU limit enforcement: spatial | temporal | both | off"),
+    ("--cu-mode", "cu_mode", str, ["CU_MODE"], "CU limit enforcement: auto (spatial for shares >= 50 %, temporal below) | spatial | "
+     "temporal | both | off"),
     ("--backend", "backend", str, ["DEVICE_BACKEND"], "device backend: auto | amdsmi | sysfs | fake"),
     ("--fake-devices", "fake_devices", str, ["FAKE_DEVICES"], "JSON spec (or file) for the fake backend"),
     ("--resource-name", "resource_name", str, ["RESOURCE_NAME"], "extended resource name"),

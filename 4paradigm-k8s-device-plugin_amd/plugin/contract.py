@@ -35,8 +35,41 @@ CONTAINER_PCIINFO = "/usr/local/vgpu/pciinfo.vgpu"
 CONTAINER_VALIDATOR = "/usr/bin/vgpu-validate"
 CONTAINER_ALLOWLIST_DIR = "/vgpu"
 SHARED_HOST_DIR = "shared"
+# Host-PID discovery lock shared by every vGPU container of the node (the reference's
+# "unified lock" /tmp/vgpulock/lock, utils.c:30-36, which only serialised one container):
+# processes of different containers that start together take turns probing KFD.
+LOCK_HOST_DIR = "lock"
+CONTAINER_LOCK_DIR = "/usr/local/vgpu/lock"
 ANN_REQUEST = "amd-vgpu/request"
 ANN_USING = "amd-vgpu/using"
+
+
+ALLOWLIST_HOST_DIR = "allowlist"
+ALLOWLIST_MAX_AGE_S = 7 * 24 * 3600
+
+
+def write_allowlist(vgpu_dir, name, uuids):
+    """Writes <vgpu_dir>/allowlist/containers/<name>.list with ``uuids``; returns its path,
+    or None if the host directory is not writable. Lists older than a week are removed
+    (containers that old have long since started; the shim reads the list once)."""
+    d = os.path.join(vgpu_dir, ALLOWLIST_HOST_DIR, "containers")
+    try:
+        os.makedirs(d, exist_ok=True)
+        path = os.path.join(d, name + ".list")
+        with open(path, "w") as f:
+            f.write("".join(u + "\n" for u in uuids))
+    except OSError:
+        return None
+    try:
+        import time
+        now = time.time()
+        for fn in os.listdir(d):
+            fp = os.path.join(d, fn)
+            if fn.endswith(".list") and now - os.path.getmtime(fp) > ALLOWLIST_MAX_AGE_S:
+                os.unlink(fp)
+    except OSError:
+        pass
+    return path
 
 
 def device_ids(cfg, devices_by_uuid, uuids):
@@ -97,8 +130,8 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
                 resp.envs[f"VGPU_DEVICE_CU_RANGE_{i}"] = f"{v.cu_range[0]}-{v.cu_range[1]}"
         dmap.append(f"{i}:{v.uuid}")
     resp.envs["VGPU_DEVICE_MAP"] = " ".join(dmap)
-    if cfg.cu_mode != "spatial":
-        resp.envs["VGPU_CU_MODE"] = cfg.cu_mode
+    # Always explicit, so a container never depends on the shim's built-in default.
+    resp.envs["VGPU_CU_MODE"] = cfg.cu_mode
 
     cache_name = f"{_uuid.uuid4()}.cache"
     if cfg.monitor_mode and pod_tag:
@@ -110,18 +143,29 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         resp.envs["VGPU_SHARED_CACHE"] = os.path.join(cfg.shared_cache_dir, cache_name)
     if cfg.device_memory_scaling > 1:
         resp.envs["VGPU_OVERSUBSCRIBE"] = "true"
-    # Device authorisation against the node's allow-list (mounted below at /vgpu).
+    # Device authorisation (reference: vgpuvalidator against the licensed device pool):
+    # every container gets its own allow-list holding exactly the GPUs it was allocated,
+    # so a process that widens ROCR_VISIBLE_DEVICES inside the container gets no memory
+    # on any other GPU. Falls back to the node-wide list when the host dir is read-only.
     resp.envs["VGPU_ALLOWLIST"] = CONTAINER_ALLOWLIST_DIR + "/allowlist"
-
     vdir = cfg.vgpu_dir
+    own_list = write_allowlist(vdir, cache_name.rsplit(".", 1)[0], uuids)
+
     resp.mounts.add(container_path=CONTAINER_SHIM, host_path=os.path.join(vdir, "libvgpu_hip.so"), read_only=True)
     resp.mounts.add(container_path=CONTAINER_PRELOAD, host_path=os.path.join(vdir, "ld.so.preload"), read_only=True)
     if cfg.pcibus_file and os.path.exists(cfg.pcibus_file):
         resp.mounts.add(container_path=CONTAINER_PCIINFO, host_path=cfg.pcibus_file, read_only=True)
     resp.mounts.add(container_path=CONTAINER_VALIDATOR, host_path=os.path.join(vdir, "vgpu-validate"),
                     read_only=True)
-    resp.mounts.add(container_path=CONTAINER_ALLOWLIST_DIR, host_path=os.path.join(vdir, "allowlist"),
-                    read_only=True)
+    if own_list:
+        resp.mounts.add(container_path=CONTAINER_ALLOWLIST_DIR + "/allowlist", host_path=own_list, read_only=True)
+    else:
+        resp.mounts.add(container_path=CONTAINER_ALLOWLIST_DIR, host_path=os.path.join(vdir, "allowlist"),
+                        read_only=True)
+    lock_dir = os.path.join(vdir, LOCK_HOST_DIR)
+    if os.path.isdir(lock_dir):
+        resp.mounts.add(container_path=CONTAINER_LOCK_DIR, host_path=lock_dir, read_only=False)
+        resp.envs["VGPU_LOCK_FILE"] = CONTAINER_LOCK_DIR + "/hostpid.lock"
     return resp
 
 

@@ -127,8 +127,83 @@ class StubKubelet:
         self.allocated.update(ids)
         return ids, resp.container_responses[0]
 
+    def allocate_ids(self, resource, ids):
+        """Allocate exactly ``ids`` (a pod pinned to given vGPUs, e.g. a benchmark rank's
+        own GPU). Returns the ContainerAllocateResponse."""
+        stub = self.stub_for(resource)
+        devs = self.wait_devices(resource)
+        missing = [i for i in ids if i not in devs]
+        if missing:
+            raise RuntimeError(f"unknown {resource} devices {missing}")
+        resp = stub.Allocate(api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(
+            devicesIDs=list(ids))]))
+        self.allocated.update(ids)
+        return resp.container_responses[0]
+
     def release(self, ids):
         self.allocated.difference_update(ids)
+
+
+class NodeHarness:
+    """A device plugin (``main.Supervisor``) registered with a stub kubelet in a private
+    directory: the node side of a pod's life, for benchmarks and GPU tests. ``pod(ids)``
+    returns the (envs, mounts) the kubelet would hand to the container runtime for a
+    container holding vGPUs ``ids``; ``launcher.apply_contract`` turns them into a
+    process environment.
+
+        with NodeHarness(SysfsBackend(), device_split_count=4) as node:
+            envs, mounts = node.pod([f"{uuid}-0"])
+    """
+
+    def __init__(self, backend, resource="amd.com/gpu", workdir=None, **cfg_kw):
+        import tempfile
+        self.backend = backend
+        self.resource = resource
+        self._own_dir = workdir is None
+        self.dir = workdir or tempfile.mkdtemp(prefix="vgpu-node-")
+        self.cfg_kw = cfg_kw
+        self.kubelet = None
+        self._sup = None
+        self._stop = None
+        self._thread = None
+
+    def __enter__(self):
+        from .config import PluginConfig
+        from .main import Supervisor
+        pdir = os.path.join(self.dir, "device-plugins")
+        os.makedirs(pdir, exist_ok=True)
+        kw = dict(device_plugin_path=pdir + "/", shared_cache_dir=self.dir, vgpu_dir=os.path.join(self.dir, "vgpu"),
+                  resource_name=self.resource)
+        kw.update(self.cfg_kw)
+        cfg = PluginConfig(**kw).validate()
+        self.kubelet = StubKubelet(pdir).start()
+        self._sup = Supervisor(cfg, backend=self.backend, install_signals=False)
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._sup.run, args=(self._stop,), daemon=True)
+        self._thread.start()
+        self.kubelet.wait_registered(self.resource, timeout=30)
+        self.kubelet.wait_devices(self.resource, timeout=30)
+        return self
+
+    def __exit__(self, *exc):
+        if self._stop:
+            self._stop.set()
+        if self._thread:
+            self._thread.join(10)
+        if self.kubelet:
+            self.kubelet.stop()
+        if self._own_dir:
+            import shutil
+            shutil.rmtree(self.dir, ignore_errors=True)
+
+    def vgpu_ids(self, uuid):
+        """The advertised vGPU IDs of physical GPU ``uuid``, in slot order."""
+        ids = [i for i in self.kubelet.devices.get(self.resource, {}) if i.rsplit("-", 1)[0] == uuid]
+        return sorted(ids, key=lambda i: int(i.rsplit("-", 1)[1]))
+
+    def pod(self, ids):
+        from .contract import response_to_env
+        return response_to_env(self.kubelet.allocate_ids(self.resource, ids))
 
 
 def run_pod(kubelet, resource, count, cmd, **kw):

@@ -92,8 +92,12 @@ def render_metrics(root):
                          lb, d["monitor_used"])
                 w.metric("vgpu_cu_limit_percent", "gauge", "CU share (0 = unlimited)", lb, d["cu_limit_pct"])
                 w.metric("vgpu_cu_mask_count", "gauge", "CUs in the spatial mask", lb, d["cu_mask_count"])
-                w.metric("vgpu_utilization_percent", "gauge", "last sampled utilisation", lb, d["util_pct"])
-                w.metric("vgpu_tokens", "gauge", "temporal-limiter bucket (workgroups)", lb, d["tokens"])
+                w.metric("vgpu_utilization_percent", "gauge", "smoothed GPU-time share charged to the container",
+                         lb, d["util_pct"])
+                w.metric("vgpu_compute_credit_seconds", "gauge", "temporal limiter: remaining GPU-time credit", lb,
+                         d["credit_ns"] / 1e9)
+                w.metric("vgpu_compute_charged_seconds_total", "counter", "GPU time charged to the container", lb,
+                         d["charged_ns"] / 1e9)
             for p in snap["procs"]:
                 lp = dict(base, pid=p["pid"], hostpid=p["hostpid"])
                 w.metric("vgpu_process_launches_total", "counter", "kernel launches through the gates", lp,

@@ -269,15 +269,24 @@ class DevicePluginServer:
                 tags = self.pod_matcher.match([len(r.devicesIDs) for r in request.container_requests])
             except Exception as e:
                 log.warning("monitor mode: pod match failed: %s", e)
-        if self.legacy is not None:
-            self.legacy.update_from_checkpoint()
+        if self.legacy is not None and not self.legacy.update_from_checkpoint():
+            # Reference server.go:410-412: without the checkpoint the controller cannot know
+            # which vGPUs other containers hold, so it refuses instead of double-booking.
+            self._fail(context, f"legacy preferred allocation for '{self.resource_name}': "
+                                "cannot read the kubelet checkpoint")
         for i, req in enumerate(request.container_requests):
             requested = list(req.devicesIDs)
             using = requested
             if self.legacy is not None:
                 self.legacy.release_by_request(requested)
                 avail = self.legacy.available([v.id for v in self.vdevices])
-                using = allocate_vdevices(self.vdevices, avail, [], len(requested)) or requested
+                using = allocate_vdevices(self.vdevices, avail, [], len(requested)) if len(avail) >= len(
+                    requested) else []
+                if len(using) < len(requested):
+                    # Reference server.go:436-439 ("no enough devices"): never fall back to
+                    # the kubelet's IDs, which may belong to another container's vGPUs.
+                    self._fail(context, f"no enough devices for '{self.resource_name}': requested "
+                                        f"{len(requested)}, {len(avail)} free")
                 self.legacy.acquire(requested, using)
             try:
                 vds = vdevices_by_ids(self.vdevices, using)

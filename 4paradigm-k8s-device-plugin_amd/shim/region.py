@@ -27,13 +27,16 @@ class ProcInfo(C.Structure):
     ]
 
 
+CU_MODES = {0: "off", 1: "spatial", 2: "temporal", 3: "both"}
+
+
 class DeviceInfo(C.Structure):
     _fields_ = [
         ("uuid", C.c_char * 64), ("mem_limit", C.c_uint64), ("phys_total", C.c_uint64), ("used", C.c_uint64),
         ("spilled", C.c_uint64), ("monitor_used", C.c_uint64), ("cu_limit_pct", C.c_int32),
         ("cu_count", C.c_int32), ("num_xcc", C.c_int32), ("cu_mask_count", C.c_int32),
-        ("cu_mask", C.c_uint32 * 8), ("tokens", C.c_int64), ("share", C.c_int64), ("util_pct", C.c_int32),
-        ("gpu_id", C.c_uint32), ("bdf", C.c_uint32), ("domain", C.c_uint32), ("configured", C.c_uint32),
+        ("cu_mask", C.c_uint32 * 8), ("credit_ns", C.c_int64), ("charged_ns", C.c_uint64),
+        ("wall_ns", C.c_uint64), ("util_pct", C.c_int32), ("cu_mode", C.c_int32), ("gpu_id", C.c_uint32), ("bdf", C.c_uint32), ("domain", C.c_uint32), ("configured", C.c_uint32),
         ("hbm_limit", C.c_uint64),
     ]
 
@@ -140,8 +143,9 @@ class Region:
             "index": dev, "uuid": d.uuid.decode(errors="replace"), "mem_limit": d.mem_limit,
             "phys_total": d.phys_total, "used": d.used, "spilled": d.spilled, "monitor_used": d.monitor_used,
             "cu_limit_pct": d.cu_limit_pct, "cu_count": d.cu_count, "num_xcc": d.num_xcc,
-            "cu_mask_count": d.cu_mask_count, "cu_mask": mask, "tokens": d.tokens, "share": d.share,
-            "util_pct": d.util_pct, "gpu_id": d.gpu_id, "bdf": d.bdf, "domain": d.domain,
+            "cu_mask_count": d.cu_mask_count, "cu_mask": mask, "credit_ns": d.credit_ns,
+            "charged_ns": d.charged_ns, "wall_ns": d.wall_ns, "util_pct": d.util_pct,
+            "cu_mode": CU_MODES.get(d.cu_mode, str(d.cu_mode)), "gpu_id": d.gpu_id, "bdf": d.bdf, "domain": d.domain,
             "configured": bool(d.configured), "hbm_limit": d.hbm_limit,
         }
 

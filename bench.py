@@ -1,21 +1,38 @@
 #!/usr/bin/env python3
-"""Headline benchmark: ai-benchmark ResNet-V2-50 inference (test 1.1) inside a vGPU.
+"""Headline benchmark: stock PyTorch-ROCm ResNet-V2-50 inference (ai-benchmark test 1.1,
+batch 50, 346², fp32) inside a vGPU of one MI355X, as the device plugin allocates it.
 
-Mirrors the reference's published measurement (README.md:38-72): the same
-workload run natively and inside a vGPU container, reporting the vGPU's throughput and
-its ms/batch overhead versus native. Here the vGPU is a 4-way split of one MI355X
-(72 GiB HBM quota, BASELINE.json config 2) enforced by the in-tree interception shim
-(libvgpu_hip.so), applied to the worker exactly as the container runtime would apply the
-plugin's Allocate response (env contract + preload).
+BASELINE.json config 2 (split 4, 72 GiB quota per pod) with the reference's metric: the
+ms/batch cost of the vGPU versus native, and how many vGPUs one GPU sustains.
 
-Process layout (one rank per GPU under torch.distributed.run): the rank process never
-touches the GPU; it starts one worker child per mode (native, then vgpu), each of which
-initialises RCCL, runs W untimed warmup steps, then times exactly K steps bracketed by
-barrier + synchronize on both sides, and reduces the MAX step time over ranks. Rank 0
-prints one JSON line. ``value`` is the whole-job vGPU throughput (sum over GPUs).
+Every vGPU contract comes from a real ``Allocate`` call: the plugin (``main.Supervisor``
+on the sysfs device backend) registers with a stub kubelet, the rank's GPU is allocated,
+and the returned envs + mounts are applied to the worker process exactly as a container
+runtime would (``shim/launcher.py``), so the workload runs under the interception shim
+(``libvgpu_hip.so``) with the limits a pod would get. The workload is stock PyTorch
+(MIOpen / hipBLASLt kernels, no custom fused ops) in fp32, the reference's precision.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--case resnet50-inf]
-                    [--modes native,vgpu] [--split 4] [--cu-limit 0]
+Modes, one fresh worker process each (the rank process itself never touches the GPU):
+
+* native   no shim; the GPU made visible as the official plugin would.
+* vgpu     the split-4 pod: 72 GiB quota, 25 % compute share (auto mode: the GPU-time
+           limiter, since CU masks serve at most two tenants per GPU).   → ``value``
+* quota    the same pod with the compute limit disabled (VGPU_CU_POLICY=disable): the
+           shim's own overhead on stock PyTorch, the number the reference's vGPU column
+           measured (its 50 % SM limit did not bind on TF).
+* parity   the reference's benchmark configuration: split 2, memory scaling 1.8
+           (server.go:492,505-507): 50 % compute (CU mask), 259 GiB oversubscribed quota.
+* sweep    N = 1, 2, 4, 8 pods of a split-N plugin run concurrently on one GPU (default
+           deployment config). ``max_vgpus_per_gpu`` is the largest N whose aggregate
+           stays >= 0.9x one whole-GPU pod and whose slowest pod gets >= 0.9x its 1/N
+           entitlement. Only on single-GPU runs unless --sweep on.
+
+Timed region (native / vgpu / quota / parity): W untimed warmup steps, then exactly K
+steps bracketed by barrier + synchronize on both sides; MAX step time over ranks (one
+rank per GPU under torch.distributed.run, RCCL). ``value`` is the whole-job vGPU
+throughput (sum over GPUs).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--case resnet50-inf] [--sweep auto|on|off]
 """
 import argparse
 import json
@@ -28,8 +45,10 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-MI355X_HBM_BYTES = 309220868096  # 288 GiB as reported by ROCr on the box (gpurun_out probe)
-METRIC = "ai-benchmark ResNet-V2-50 inference throughput inside a vGPU (images/s); ms/batch overhead vs native"
+METRIC = ("ai-benchmark ResNet-50 ms/batch overhead vs native plugin; max vGPUs per MI355X "
+          "(value: ResNet-V2-50 b=50 346² fp32 inference throughput inside a split-4 vGPU, images/s)")
+SWEEP_MIN_AGGREGATE = 0.9
+SWEEP_MIN_TENANT = 0.9
 
 
 def parse(argv=None):
@@ -38,23 +57,24 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--case", default="resnet50-inf")
-    ap.add_argument("--modes", default="native,vgpu")
-    ap.add_argument("--split", type=int, default=4, help="vGPUs per physical GPU (quota = HBM / split)")
-    ap.add_argument("--memory-scaling", type=float, default=1.0)
-    ap.add_argument("--cu-limit", type=int, default=0, help="CU share %% of the vGPU (0 = quota only)")
-    ap.add_argument("--cu-mode", default="spatial", choices=["spatial", "temporal", "both", "off"])
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--no-fuse", action="store_true", help="eager PyTorch epilogues (no fused HIP BN+ReLU)")
-    ap.add_argument("--tune", type=int, default=1, choices=[0, 1],
-                    help="MIOpen find-mode conv autotuning during warmup (torch.backends.cudnn.benchmark); "
-                         "the reference's TensorFlow autotunes convolutions too")
+    ap.add_argument("--modes", default="native,vgpu,quota,parity")
+    ap.add_argument("--split", type=int, default=4, help="vGPUs per GPU of the headline pod (BASELINE config 2)")
+    ap.add_argument("--cu-mode", default="auto", choices=["auto", "spatial", "temporal", "both", "off"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--fuse", action="store_true", help="round-1 hand-written bf16 kernels (not the stock workload)")
+    ap.add_argument("--sweep", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--sweep-tenants", default="1,2,4,8")
+    ap.add_argument("--sweep-seconds", type=float, default=6.0)
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     # worker-only
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--mode", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--result-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--port", type=int, default=0, help=argparse.SUPPRESS)
-    # CPU rehearsal of the multi-rank orchestration (gloo, tiny batch); not a measurement
+    ap.add_argument("--dist", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--seconds", type=float, default=0.0, help=argparse.SUPPRESS)
+    ap.add_argument("--go", default=None, help=argparse.SUPPRESS)
+    # CPU rehearsal of the multi-rank orchestration (gloo, fake devices, tiny input); not a measurement
     ap.add_argument("--cpu-rehearsal", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -69,61 +89,71 @@ def worker(args):
     from amdvgpu.models.aibench import Runner, get_case
 
     rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1)) if args.dist else 1
     cpu = args.cpu_rehearsal
-    if cpu:
-        device = torch.device("cpu")
-    else:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+    # The pod sees exactly its own GPU (ROCR_VISIBLE_DEVICES from the contract): cuda:0.
+    device = torch.device("cpu") if cpu else torch.device("cuda", 0)
+    if not cpu:
+        torch.cuda.set_device(device)
     if world > 1:
         init = f"tcp://{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{args.port}"
         if cpu:
             dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
         else:
             dist.init_process_group("nccl", init_method=init, rank=rank, world_size=world, device_id=device)
-
     sync = (lambda: None) if cpu else (lambda: torch.cuda.synchronize(device))
     free0, total = torch.cuda.mem_get_info(device) if not cpu else (0, 0)
-    if args.mode == "vgpu" and not cpu:
-        quota = int(os.environ["VGPU_DEVICE_MEMORY_LIMIT"].rstrip("m")) << 20
-        if total != min(quota, MI355X_HBM_BYTES) and not os.environ.get("VGPU_OVERSUBSCRIBE"):
-            raise SystemExit(f"vGPU shim not in effect: mem_get_info total {total} != quota {quota}")
+    quota = int(os.environ.get("VGPU_DEVICE_MEMORY_LIMIT_0", "0").rstrip("m") or 0) << 20
+    if quota and not cpu and total != quota:
+        raise SystemExit(f"vGPU shim not in effect: mem_get_info total {total} != quota {quota}")
 
-    torch.backends.cudnn.benchmark = bool(args.tune)
+    torch.backends.cudnn.benchmark = True  # MIOpen find mode (the reference's TF autotunes too)
     case = get_case(args.case)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     if cpu:
         runner = Runner(case, device, dtype=torch.float32, batch=2, channels_last=False, fuse=False)
         runner.x = runner.x[..., :64, :64].contiguous() if runner.x.dim() == 4 else runner.x[:, :16].contiguous()
     else:
-        runner = Runner(case, device, dtype=dtype, fuse=not args.no_fuse)
+        runner = Runner(case, device, dtype=dtype, fuse=args.fuse)
     for _ in range(args.warmup):
         runner.step()
     sync()
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local]) if not cpu else dist.barrier()
+            dist.barrier(device_ids=[0]) if not cpu else dist.barrier()
         sync()
 
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        runner.step()
-    sync()
-    barrier()
-    dt = time.perf_counter() - t0
-    ms = torch.tensor([dt * 1000.0 / args.steps], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-    res = {
-        "mode": args.mode, "ms_per_step": ms.item(), "items_per_step": runner.items_per_step,
-        "mem_total": total, "world": world,
-        "peak_allocated": torch.cuda.max_memory_allocated(device) if not cpu else 0,
-    }
-    if rank == 0 and args.result_file:
+    if args.go:  # concurrent tenants: start together, run for a fixed wall time
+        open(args.result_file + ".ready", "w").close()
+        while not os.path.exists(args.go):
+            time.sleep(0.002)
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.seconds:
+            runner.step()
+            n += 1
+            if n % 4 == 0:
+                sync()
+        sync()
+        dt = time.perf_counter() - t0
+        res = {"mode": args.mode, "ms_per_step": dt * 1000.0 / n, "items_per_step": runner.items_per_step,
+               "steps": n, "t0": t0, "t1": t0 + dt}
+    else:
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            runner.step()
+        sync()
+        barrier()
+        dt = time.perf_counter() - t0
+        ms = torch.tensor([dt * 1000.0 / args.steps], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        res = {"mode": args.mode, "ms_per_step": ms.item(), "items_per_step": runner.items_per_step,
+               "steps": args.steps, "mem_total": total,
+               "peak_allocated": torch.cuda.max_memory_allocated(device) if not cpu else 0}
+    if args.result_file and (rank == 0 or world == 1):
         with open(args.result_file, "w") as f:
             json.dump(res, f)
     if world > 1:
@@ -135,63 +165,160 @@ def worker(args):
 # ----------------------------------------------------------------------------- parent
 
 
-def run_mode(args, mode, port):
-    from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
+def worker_cmd(args, mode, result, port, dist=1, seconds=0.0, go=None):
+    cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--mode", mode, "--result-file", result,
+           "--port", str(port), "--dist", str(dist), "--case", args.case, "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--dtype", args.dtype]
+    if args.fuse:
+        cmd.append("--fuse")
+    if args.cpu_rehearsal:
+        cmd.append("--cpu-rehearsal")
+    if go:
+        cmd += ["--seconds", str(seconds), "--go", go]
+    return cmd
 
-    rank = int(os.environ.get("RANK", 0))
+
+def pod_env(node, ids, extra=None):
+    """(process env, contract envs) for a container holding vGPUs ``ids``."""
+    from amdvgpu.shim.launcher import apply_contract
+    envs, mounts = node.pod(ids)
+    env = apply_contract(envs, mounts)
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    if extra:
+        env.update(extra)
+    return env, envs
+
+
+def native_env(uuid, cpu):
+    env = dict(os.environ)
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    if not cpu:
+        env["ROCR_VISIBLE_DEVICES"] = uuid  # the official plugin exposes the GPU the same way
+    return env
+
+
+def run_one(args, mode, env, port):
+    """One timed worker (all ranks take part in its process group). Rank 0 returns the
+    result dict, other ranks None."""
     fd, result = tempfile.mkstemp(prefix=f"bench-{mode}-", suffix=".json")
     os.close(fd)
-    cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--mode", mode, "--result-file", result,
-           "--port", str(port), "--case", args.case, "--steps", str(args.steps), "--warmup", str(args.warmup),
-           "--dtype", args.dtype, "--tune", str(args.tune)] + (["--no-fuse"] if args.no_fuse else []) + \
-        (["--cpu-rehearsal"] if args.cpu_rehearsal else [])
-    contract = {}
-    if mode == "vgpu":
-        quota = int(MI355X_HBM_BYTES * args.memory_scaling / args.split)
-        contract = vgpu_env(mem_limit=quota, cu_limit=args.cu_limit or None, cu_mode=args.cu_mode,
-                            oversubscribe=args.memory_scaling > 1,
-                            shared_cache=os.path.join(tempfile.gettempdir(), f"vgpu-bench-{os.getpid()}-{rank}.cache"))
-        env = apply_contract(contract)
-    else:
-        env = dict(os.environ)
-    # The worker hosts its own rendezvous store on `port` (rank 0); under
-    # torch.distributed.run the agent's store flag would make every worker a client of a
-    # store that does not exist on that port.
-    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
     try:
-        rc = subprocess.call(cmd, env=env)
+        rc = subprocess.call(worker_cmd(args, mode, result, port), env=env)
         if rc != 0:
             raise SystemExit(f"bench worker ({mode}) failed with exit code {rc}")
-        if rank != 0:
+        if int(os.environ.get("RANK", 0)) != 0:
             return None
         with open(result) as f:
             return json.load(f)
     finally:
         os.unlink(result)
-        if contract:
-            cleanup_region(contract)
+
+
+def run_concurrent(args, envs, label):
+    """Starts one tenant per env, releases them together, returns their results."""
+    tmp = tempfile.mkdtemp(prefix=f"bench-{label}-")
+    go = os.path.join(tmp, "go")
+    procs, outs = [], []
+    for i, env in enumerate(envs):
+        out = os.path.join(tmp, f"t{i}.json")
+        procs.append(subprocess.Popen(worker_cmd(args, label, out, 0, dist=0, seconds=args.sweep_seconds, go=go),
+                                      env=env))
+        outs.append(out)
+    try:
+        deadline = time.time() + 900
+        while not all(os.path.exists(o + ".ready") for o in outs):
+            if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
+                raise SystemExit(f"a {label} tenant failed before the start barrier")
+            time.sleep(0.05)
+        open(go, "w").close()
+        for p in procs:
+            if p.wait(timeout=900) != 0:
+                raise SystemExit(f"a {label} tenant failed")
+        return [json.load(open(o)) for o in outs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+
+
+def sweep(args, backend, uuid, tenants):
+    from amdvgpu.plugin.kubelet_stub import NodeHarness
+    rows = []
+    for n in tenants:
+        with NodeHarness(backend, device_split_count=n, cu_mode=args.cu_mode) as node:
+            ids = node.vgpu_ids(uuid)[:n]
+            pods = [pod_env(node, [i]) for i in ids]
+            res = run_concurrent(args, [e for e, _ in pods], f"sweep{n}")
+            c0 = pods[0][1]
+        tput = [r["items_per_step"] * r["steps"] / (r["t1"] - r["t0"]) for r in res]
+        span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
+        agg = sum(r["items_per_step"] * r["steps"] for r in res) / span
+        rows.append({"tenants": n, "aggregate": round(agg, 2), "per_tenant": [round(t, 2) for t in tput],
+                     "cu_limit_pct": int(c0.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0),
+                     "cu_mode": c0.get("VGPU_CU_MODE"), "quota_mib": int(c0["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m"))})
+        print(f"[bench] sweep {n} tenants: aggregate {agg:.1f}, per tenant {min(tput):.1f}..{max(tput):.1f}",
+              file=sys.stderr, flush=True)
+    base = next((r["aggregate"] for r in rows if r["tenants"] == 1), None)
+    best = 0
+    for r in rows:
+        if not base:
+            break
+        r["aggregate_vs_one"] = round(r["aggregate"] / base, 3)
+        r["min_tenant_vs_entitlement"] = round(min(r["per_tenant"]) / (base / r["tenants"]), 3)
+        r["ok"] = r["aggregate_vs_one"] >= SWEEP_MIN_AGGREGATE and r["min_tenant_vs_entitlement"] >= SWEEP_MIN_TENANT
+        if r["ok"]:
+            best = max(best, r["tenants"])
+    return rows, best
 
 
 def main(argv=None):
     args = parse(argv)
     if args.worker:
         return worker(args)
+    from amdvgpu.models.aibench import get_case
+    from amdvgpu.plugin.devices import FakeBackend, SysfsBackend
+    from amdvgpu.plugin.kubelet_stub import NodeHarness
+
     world = int(os.environ.get("WORLD_SIZE", 1))
+    rank = int(os.environ.get("RANK", 0))
+    local = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    cpu = args.cpu_rehearsal
+    backend = FakeBackend(n=max(world, 1)) if cpu else SysfsBackend()
+    devices = backend.devices()
+    if local >= len(devices):
+        raise SystemExit(f"LOCAL_RANK {local} but only {len(devices)} GPUs")
+    uuid = devices[local].uuid
     base_port = int(os.environ.get("MASTER_PORT", 29500))
     modes = [m for m in args.modes.split(",") if m]
-    results = {}
-    for i, mode in enumerate(modes):
-        results[mode] = run_mode(args, mode, base_port + 1 + i)
-    if int(os.environ.get("RANK", 0)) != 0:
+    results, contracts = {}, {}
+    port = base_port + 1
+    for mode in modes:
+        if mode == "native":
+            results[mode] = run_one(args, mode, native_env(uuid, cpu), port)
+        else:
+            split, scaling, extra = {"vgpu": (args.split, 1.0, None), "quota": (args.split, 1.0, {
+                "VGPU_CU_POLICY": "disable"}), "parity": (2, 1.8, None)}[mode]
+            with NodeHarness(backend, device_split_count=split, device_memory_scaling=scaling,
+                             cu_mode=args.cu_mode) as node:
+                env, contracts[mode] = pod_env(node, node.vgpu_ids(uuid)[:1], extra)
+                results[mode] = run_one(args, mode, env, port)
+        port += 1
+    do_sweep = args.sweep == "on" or (args.sweep == "auto" and world == 1 and not cpu)
+    sweep_rows, max_vgpus = ([], None)
+    if do_sweep:
+        sweep_rows, max_vgpus = sweep(args, backend, uuid, [int(x) for x in args.sweep_tenants.split(",")])
+    if rank != 0:
         return 0
 
-    from amdvgpu.models.aibench import get_case
     case = get_case(args.case)
-    head = results.get("vgpu") or results[modes[-1]]
+    head_mode = "vgpu" if "vgpu" in results else modes[-1]
+    head = results[head_mode]
     ms = head["ms_per_step"]
     value = world * head["items_per_step"] * 1000.0 / ms
+    c = contracts.get("vgpu", {})
+    cu_pct = int(c.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0)
     line = {
         "metric": METRIC if args.case == "resnet50-inf" else f"ai-benchmark {case.model} "
                   f"{'training' if case.train else 'inference'} throughput inside a vGPU ({case.unit})",
@@ -210,23 +337,49 @@ def main(argv=None):
             "model": case.model, "test": case.test_id, "mode": "training" if case.train else "inference",
             "global_batch": case.batch * world, "per_gpu_batch": case.batch,
             "input_shape": list(case.input_shape), "seq_len": None,
-            "parallelism": f"dp{world} (one independent vGPU replica per GPU)",
-            "fused_epilogues": not args.no_fuse,
-            "conv_autotune": bool(args.tune),
-            "vgpu": {"split": args.split, "quota_bytes": int(MI355X_HBM_BYTES * args.memory_scaling / args.split),
-                     # CU-mask granularity is one CU per XCD (8 CUs): 256 / 8 disjoint slices
-                     "max_vgpus_per_gpu_spatial": 32,
-                     "cu_limit_pct": args.cu_limit, "cu_mode": args.cu_mode,
-                     "memory_scaling": args.memory_scaling},
+            "parallelism": f"dp{world} (one independent split-{args.split} vGPU pod per GPU)",
+            "workload": "stock PyTorch-ROCm (MIOpen/hipBLASLt), no custom kernels" if not args.fuse else
+                        "round-1 fused bf16 HIP kernels",
+            "fused_epilogues": bool(args.fuse),
+            "vgpu": {"split": args.split, "source": "Allocate response of the plugin (sysfs backend, stub kubelet)",
+                     "envs": {k: v for k, v in sorted(c.items()) if k.startswith("VGPU_") and k != "VGPU_SHARED_CACHE"},
+                     "quota_bytes": int(c.get("VGPU_DEVICE_MEMORY_LIMIT_0", "0").rstrip("m") or 0) << 20,
+                     "cu_limit_pct": cu_pct, "cu_mode": c.get("VGPU_CU_MODE")},
         },
     }
-    if "native" in results and "vgpu" in results:
-        nat = results["native"]["ms_per_step"]
+    nat = results.get("native", {}).get("ms_per_step") if results.get("native") else None
+    if nat:
         line["ms_per_batch_native"] = round(nat, 4)
-        line["ms_per_batch_vgpu"] = round(ms, 4)
-        line["overhead_pct_vs_native"] = round((ms - nat) / nat * 100.0, 3)
+        if "vgpu" in results:
+            line["ms_per_batch_vgpu"] = round(ms, 4)
+            share = cu_pct / 100.0 if 0 < cu_pct < 100 else 1.0
+            # The pod's throughput over what its compute share entitles it to (native x share).
+            line["entitlement_ratio"] = round(nat / (ms * share), 3)
+            line["overhead_pct_vs_native_x_share"] = round((ms * share - nat) / nat * 100.0, 3)
+        if "quota" in results:
+            q = results["quota"]["ms_per_step"]
+            line["ms_per_batch_quota_only"] = round(q, 4)
+            line["overhead_pct_quota_only"] = round((q - nat) / nat * 100.0, 3)
+        if "parity" in results:
+            p = results["parity"]["ms_per_step"]
+            pc = contracts["parity"]
+            pct = int(pc.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0)
+            line["parity_split2_mem1.8"] = {
+                "ms_per_batch": round(p, 4),
+                "throughput": round(world * results["parity"]["items_per_step"] * 1000 / p, 3),
+                "cu_limit_pct": pct, "cu_mode": pc.get("VGPU_CU_MODE"),
+                "oversubscribe": pc.get("VGPU_OVERSUBSCRIBE") == "true",
+                "quota_bytes": int(pc["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m")) << 20,
+                "hbm_limit_bytes": int(pc.get("VGPU_DEVICE_HBM_LIMIT_0", "0").rstrip("m") or 0) << 20,
+                "entitlement_ratio": round(nat / (p * (pct / 100.0 if 0 < pct < 100 else 1.0)), 3)}
         # Reference's own vGPU overhead on this case (2xV100, BASELINE.md "Derived ms/batch").
         line["reference_overhead_pct"] = round((case.baseline_native / case.baseline_vgpu - 1) * 100.0, 2)
+    if do_sweep:
+        line["max_vgpus_per_gpu"] = max_vgpus
+        line["max_vgpus_criterion"] = (f"largest N with aggregate >= {SWEEP_MIN_AGGREGATE}x one whole-GPU pod and "
+                                       f"slowest pod >= {SWEEP_MIN_TENANT}x its 1/N entitlement "
+                                       f"(tested N = {args.sweep_tenants})")
+        line["sweep"] = sweep_rows
     line["baseline_vgpu_v100"] = case.baseline_vgpu
     out = json.dumps(line)
     print(out, flush=True)

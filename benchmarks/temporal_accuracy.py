@@ -1,13 +1,20 @@
 #!/usr/bin/env python3
-"""Temporal (reference-parity) compute limit: achieved share vs configured limit.
+"""Temporal compute limit: achieved share vs configured limit, on stock workloads.
 
-A saturating workload (single-wave workgroups spinning a fixed time, a full chip wave
-per launch) runs natively and inside a vGPU with VGPU_CU_MODE=temporal at several
-limits; the achieved share is native_time / limited_time over a fixed amount of work.
-The reference's token bucket has no published accuracy; its grid-block tokens refill
-every 120 ms from NVML utilisation.
+Each tenant is a separate process (its own vGPU region, as separate containers would
+be) running a stock PyTorch-ROCm workload for a fixed wall time; the achieved share is
+its throughput divided by the same workload's native (unlimited, alone) throughput.
+Measured for one tenant alone and for two identical tenants running concurrently (each
+in its own vGPU with the same limit). The reference publishes no accuracy for its
+token bucket; round 1 measured 29/44/62 % for 25/50/75 %
+(profiles/r1l/temporal.md).
 
-    python benchmarks/temporal_accuracy.py [--limits 25,50,75] [--seconds 3]
+Workloads: ``resnet50`` (ai-benchmark 1.1: ResNet-V2-50 inference, batch 50, 346², fp32,
+stock PyTorch/MIOpen), ``spin`` (calibration kernel: 2048 single-wave workgroups of
+500 µs — a GPU-bound launch stream with no host gaps).
+
+    python benchmarks/temporal_accuracy.py [--workload resnet50] [--limits 10,25,50,75,90]
+                                           [--tenants 1,2] [--seconds 4]
 """
 import argparse
 import json
@@ -21,60 +28,105 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def worker(launches, spin_us, out):
+def worker(workload, seconds, sync_every, out, go):
     import torch
-    from amdvgpu.ops import spin
-    spin(256 * 32, 100)
+    if workload == "resnet50":
+        from amdvgpu.models.aibench import Runner, get_case
+        torch.backends.cudnn.benchmark = True
+        r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False)
+        step, items = r.step, 50
+    else:
+        from amdvgpu.ops import spin
+        step, items = (lambda: spin(2048, 500)), 1
+    for _ in range(5):
+        step()
     torch.cuda.synchronize()
+    open(out + ".ready", "w").close()
+    while go and not os.path.exists(go):
+        time.sleep(0.002)
+    n = 0
     t0 = time.perf_counter()
-    for i in range(launches):
-        spin(256 * 32, spin_us)
-        if i % 64 == 0:
+    while time.perf_counter() - t0 < seconds:
+        step()
+        n += 1
+        if n % sync_every == 0:
             torch.cuda.synchronize()
     torch.cuda.synchronize()
-    json.dump({"t": time.perf_counter() - t0}, open(out, "w"))
+    dt = time.perf_counter() - t0
+    json.dump({"steps": n, "seconds": dt, "throughput": n * items / dt}, open(out, "w"))
 
 
-def run(launches, spin_us, contract):
+def run_tenants(workload, contracts, seconds, sync_every):
+    """Starts len(contracts) tenants (None = native), releases them together, returns
+    each one's throughput."""
     from amdvgpu.shim.launcher import apply_contract, cleanup_region
-    fd, out = tempfile.mkstemp(suffix=".json")
-    os.close(fd)
-    env = apply_contract(contract) if contract else dict(os.environ)
+    tmp = tempfile.mkdtemp(prefix="tacc-")
+    go = os.path.join(tmp, "go")
+    procs, outs = [], []
+    for i, c in enumerate(contracts):
+        out = os.path.join(tmp, f"t{i}.json")
+        env = apply_contract(c) if c else dict(os.environ)
+        cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--workload", workload, "--seconds",
+               str(seconds), "--sync-every", str(sync_every), "--out", out, "--go", go]
+        procs.append(subprocess.Popen(cmd, env=env))
+        outs.append(out)
     try:
-        subprocess.check_call([sys.executable, os.path.abspath(__file__), "--worker", "--launches", str(launches),
-                               "--spin-us", str(spin_us), "--out", out], env=env)
-        return json.load(open(out))["t"]
+        deadline = time.time() + 600
+        while not all(os.path.exists(o + ".ready") for o in outs):
+            if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
+                raise SystemExit("a tenant failed before the start barrier")
+            time.sleep(0.02)
+        open(go, "w").close()
+        for p in procs:
+            if p.wait(timeout=600) != 0:
+                raise SystemExit("a tenant failed")
+        return [json.load(open(o))["throughput"] for o in outs]
     finally:
-        os.unlink(out)
-        if contract:
-            cleanup_region(contract)
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for c in contracts:
+            if c:
+                cleanup_region(c)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--limits", default="25,50,75")
-    ap.add_argument("--seconds", type=float, default=3.0)
-    ap.add_argument("--spin-us", type=int, default=500)
+    ap.add_argument("--workload", default="resnet50", choices=["resnet50", "spin"])
+    ap.add_argument("--limits", default="10,25,50,75,90")
+    ap.add_argument("--tenants", default="1,2")
+    ap.add_argument("--seconds", type=float, default=4.0)
+    ap.add_argument("--sync-every", type=int, default=8)
+    ap.add_argument("--extra", default="", help="extra contract env, K=V[,K=V] (e.g. VGPU_LIMITER_WINDOW_MS=120)")
     ap.add_argument("--worker", action="store_true")
-    ap.add_argument("--launches", type=int, default=0)
     ap.add_argument("--out")
+    ap.add_argument("--go")
+    ap.add_argument("--json-out")
     ap.add_argument("--md-out")
     a = ap.parse_args()
     if a.worker:
-        return worker(a.launches, a.spin_us, a.out)
+        return worker(a.workload, a.seconds, a.sync_every, a.out, a.go)
     from amdvgpu.shim.launcher import vgpu_env
-    probe = run(200, a.spin_us, None)
-    launches = max(200, int(200 * a.seconds / probe))
-    base = run(launches, a.spin_us, None)
+    native = run_tenants(a.workload, [None], a.seconds, a.sync_every)[0]
+    print(json.dumps({"native": native}), flush=True)
     rows = []
-    for lim in [int(x) for x in a.limits.split(",")]:
-        t = run(launches, a.spin_us, vgpu_env(cu_limit=lim, cu_mode="temporal"))
-        rows.append({"limit_pct": lim, "native_s": base, "limited_s": t, "achieved_pct": 100.0 * base / t})
-        print(json.dumps(rows[-1]), flush=True)
-    md = ["| limit % | native s | limited s | achieved % |", "|---|---|---|---|"]
-    md += [f"| {r['limit_pct']} | {r['native_s']:.2f} | {r['limited_s']:.2f} | {r['achieved_pct']:.1f} |"
-           for r in rows]
+    for n in [int(x) for x in a.tenants.split(",")]:
+        for lim in [int(x) for x in a.limits.split(",")]:
+            extra = dict(kv.split("=", 1) for kv in a.extra.split(",") if kv)
+            cs = [vgpu_env(cu_limit=lim, cu_mode="temporal", mem_limit=64 << 30, extra=extra) for _ in range(n)]
+            got = run_tenants(a.workload, cs, a.seconds, a.sync_every)
+            ach = [100.0 * g / native for g in got]
+            rows.append({"tenants": n, "limit_pct": lim, "throughput": got, "achieved_pct": ach,
+                         "max_error_pts": max(abs(x - lim) for x in ach)})
+            print(json.dumps(rows[-1]), flush=True)
+    md = [f"# temporal limit accuracy — {a.workload} (native {native:.1f}/s, {a.seconds:.0f} s per point)", "",
+          "| tenants | limit % | achieved % (per tenant) | max error (pts) |", "|---|---|---|---|"]
+    for r in rows:
+        md.append(f"| {r['tenants']} | {r['limit_pct']} | {' / '.join(f'{x:.1f}' for x in r['achieved_pct'])} | "
+                  f"{r['max_error_pts']:.1f} |")
     print("\n".join(md))
+    if a.json_out:
+        json.dump({"workload": a.workload, "native": native, "rows": rows}, open(a.json_out, "w"), indent=1)
     if a.md_out:
         open(a.md_out, "w").write("\n".join(md) + "\n")
 

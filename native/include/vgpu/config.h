@@ -23,9 +23,17 @@ constexpr int kCuMaskWords = kMaxCUs / 32;
 enum class CuMode : int {
   kOff = 0,       // no compute limit
   kSpatial = 1,   // per-queue CU mask (hsa_amd_queue_cu_set_mask): default on MI355X
-  kTemporal = 2,  // reference-parity token bucket at kernel launch
+  kTemporal = 2,  // GPU-time credit checked at kernel launch (ratelimit.h)
   kBoth = 3,
+  kAuto = 4,      // spatial for shares >= 50 % (at most two tenants per GPU), temporal below
 };
+
+// Spatial masks serve at most two co-resident tenants well: beyond that the tenants'
+// dispatches contend in the shared front end (profiles/r1z), so smaller shares are
+// enforced in time instead (profiles/r2*/scaling.md).
+constexpr int kAutoSpatialMinPct = 50;
+// The mode a device actually uses for share `pct` under configured mode `m`.
+CuMode effective_cu_mode(CuMode m, int pct);
 
 // GPU_CORE_UTILIZATION_POLICY analogue.
 enum class CuPolicy : int { kDefault = 0, kForce = 1, kDisable = 2 };
@@ -46,13 +54,16 @@ struct Config {
   std::string shared_cache = "/tmp/vgpushr.cache";
   bool oversubscribe = false;            // VGPU_OVERSUBSCRIBE
   int priority = 1;                      // VGPU_TASK_PRIORITY
-  CuMode cu_mode = CuMode::kSpatial;     // VGPU_CU_MODE
+  CuMode cu_mode = CuMode::kAuto;        // VGPU_CU_MODE
   CuPolicy cu_policy = CuPolicy::kDefault;
   bool active_oom_killer = false;        // VGPU_ACTIVE_OOM_KILLER
   bool memory_override = false;          // VGPU_MEMORY_OVERRIDE
   bool signal_control = false;           // VGPU_SIGNAL_CONTROL: also honour SIGUSR1/2
   bool hook_smi = true;                  // VGPU_HOOK_SMI: virtualise amd-smi/rocm-smi
-  int util_period_ms = 120;              // feedback period (reference: 120 ms)
+  int util_period_ms = 120;              // monitor / OOM-killer / accounting period (reference: 120 ms)
+  int util_sample_us = 1000;             // temporal-mode occupancy sampling interval
+  int limiter_window_ms = 40;            // temporal-mode credit window (ratelimit.h)
+  std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
 
   bool any_memory_limit() const;

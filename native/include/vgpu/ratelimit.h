@@ -1,20 +1,33 @@
-// Temporal compute limiter (reference-parity mode).
+// Temporal compute limiter: a GPU-time credit per container and device.
 //
 // Reference: libvgpu.so src/multiprocess/multiprocess_utilization_watcher.c
 //   rate_limiter [53-72]  tokens = grid blocks; spin while recent_kernel < 0;
 //                         CAS tokens -= grids; while tokens < 0 sleep 10 ms
 //   delta@0x46712         proportional controller on |limit - util|
-//   utilization_watcher   every 120 ms: sample util, share = delta(...),
+//   utilization_watcher   every 120 ms: sample NVML SM util, share = delta(...),
 //                         tokens = min(tokens + share, total)
 //
-// Differences: the bucket lives in the shared region (one budget per container and
-// device, not one per process) and one elected process runs the watcher. The
-// reference's controller steps by a chip-size constant (sm^2 * maxThreads * diff /
-// 2560) into a bucket of sm * maxThreads * 32 tokens, so a tenant runs unthrottled
-// until millions of workgroups have drained the initial bucket and then oscillates.
-// Here the refill `share` is adjusted relative to itself (proportional decrease to
-// limit/util, multiplicative increase by the headroom) and the bucket holds two
-// periods' worth, so the duty cycle converges within a few 120 ms periods.
+// The reference prices a launch in grid blocks and steers the refill from a 120 ms
+// utilisation sample, so the achieved share depends on kernel shapes (a workgroup of a
+// 2 µs kernel costs the same as one of a 2 ms kernel) and the loop oscillates. Round 1
+// kept that structure and measured 29/44/62 % for 25/50/75 % limits.
+//
+// MI355X design: the currency is GPU time itself.
+//   * A sampler (one elected process per container) reads KFD's per-process
+//     cu_occupancy for the container's host PIDs and for every other process on the
+//     same GPU every ~1 ms (a read costs ~29 µs, profiles/r2a/occ_probe.json). While the
+//     container has resident waves it is charged the wall time of the interval,
+//     weighted by its share of all resident waves on the GPU (processor-sharing: when
+//     k tenants run concurrently each gets about 1/k of the throughput, and is charged
+//     1/k of the time). Alone on the GPU it is charged exactly its busy time.
+//   * Each interval also grants limit% of the wall time. credit = grants − charges,
+//     clamped to [-debt, +burst].
+//   * The launch gate (every kernel / graph launch) passes while credit > 0 and sleeps
+//     otherwise. Work already queued on the GPU keeps running and keeps being charged,
+//     so the credit goes into debt and the gate stays closed until the debt is repaid:
+//     the long-run busy fraction converges to limit% regardless of launch granularity
+//     or queue depth.
+// No tokens are priced per launch; the launch path is one relaxed load.
 #pragma once
 
 #include <cstdint>
@@ -23,30 +36,55 @@
 
 namespace vgpu {
 
-struct LimiterSpec {
-  int cu_count = 256;
-  int max_threads_per_cu = 2048;  // 32 waves x 64 lanes
-  // Upper bound of the per-period share (the reference's g_total_cuda_cores).
-  int64_t total() const { return (int64_t)cu_count * max_threads_per_cu * 32; }
-  // One full wave of single-wave workgroups on the chip.
-  int64_t wave() const { return (int64_t)cu_count * (max_threads_per_cu / 64); }
-  // Minimum share: one workgroup per CU per period, so a tenant is never starved.
-  int64_t floor() const { return cu_count > 0 ? cu_count : 1; }
+struct TimeShareParams {
+  int limit_pct = 100;       // 0 or >= 100 = unlimited
+  int64_t burst_ns = 0;      // positive credit cap
+  int64_t debt_ns = 0;       // negative credit floor (as a positive number)
+  int64_t reopen_ns = 0;     // a closed gate re-opens once the credit reaches this
 };
 
-// Starting share (and bucket) for a limit: limit% of one chip wave.
-int64_t limiter_initial_share(const LimiterSpec& spec, int limit_pct);
+// Default clamps for a limit: burst = max(4 ms, limit% of `window_ms`, default 40 ms),
+// re-open threshold burst / 2, debt = 2 s. The hysteresis makes on/off periods several milliseconds
+// long instead of one sample: every restart after an idle gap costs the tenant some
+// throughput (clocks and caches ramp up again), so fewer, longer periods track the
+// limit more closely (profiles/r2b vs r2c).
+TimeShareParams timeshare_params(int limit_pct, int window_ms = 40);
 
-// One controller step: returns the new per-period refill `share`.
-int64_t limiter_delta(const LimiterSpec& spec, int limit_pct, int util_pct, int64_t share);
+// Gate state after a sample: an open gate stays open while credit > 0; a closed gate
+// re-opens once credit >= reopen_ns.
+inline bool timeshare_gate(bool open, int64_t credit, const TimeShareParams& p) {
+  return open ? credit > 0 : credit >= p.reopen_ns;
+}
 
-// Periodic refill after a utilisation sample: share = delta(...), cap = 2 * share,
-// tokens = min(tokens + share, cap).
-void limiter_refill(DeviceState& d, const LimiterSpec& spec, int limit_pct, int util_pct);
+// Charge for `dt_ns` of wall time in which the container held `mine` of the `total`
+// resident waves (CUs' worth) on the device. mine <= 0 → 0; total < mine → total = mine.
+int64_t timeshare_charge(int64_t dt_ns, int64_t mine, int64_t total);
 
-// Blocking token acquisition for a launch of `workgroups` on device state `d`.
-// Returns nanoseconds spent waiting. `sleep_ns` is the back-off (reference: 10 ms).
-uint64_t limiter_acquire(RegionHeader& h, DeviceState& d, int64_t workgroups, int64_t sleep_ns = 10'000'000);
+// GPU time of an interval estimated from the charge fractions (per mille, 0..1000) at
+// its two end samples: trapezoid rule, except that an interval which began with the
+// gate re-opening (credit crossed above zero at the previous sample, so the container's
+// work resumed right after it) and started idle is charged at the end-point rate. The
+// plain end-point rule misses half an interval at every busy→idle edge; the trapezoid
+// alone misses half of one at every gate-triggered start (simulated in core_tests.cpp).
+int64_t timeshare_interval(int64_t dt_ns, int prev_pm, int now_pm, bool gate_opened_at_prev);
+
+// One accounting step: credit + dt*limit/100 − charge, clamped. Pure.
+int64_t timeshare_step(int64_t credit, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns);
+
+// Applies one step to the region's device state (credit, gate, cumulative charged time
+// and the smoothed utilisation shown by vgpuctl / the monitor).
+void timeshare_apply(DeviceState& d, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns);
+
+// Launch-side gate. Blocks while the region's launch block is set (recent_kernel < 0,
+// every cu mode) and, when `limited`, while the device's credit is exhausted and the
+// sampler is alive. Returns nanoseconds spent blocked. `poll_ns` is the back-off.
+uint64_t limiter_acquire(RegionHeader& h, DeviceState& d, bool limited, int64_t poll_ns = 200'000);
+
+// True if the launch block or an exhausted credit would make limiter_acquire wait.
+inline bool limiter_would_block(const RegionHeader& h, const DeviceState& d, bool limited) {
+  return h.recent_kernel.load(std::memory_order_relaxed) < 0 ||
+         (limited && !d.gate_open.load(std::memory_order_relaxed));
+}
 
 uint64_t now_ns();
 

@@ -37,7 +37,7 @@
 namespace vgpu {
 
 constexpr uint32_t kRegionMagic = 0x56475055u;  // "VGPU"
-constexpr uint32_t kRegionVersion = 2;
+constexpr uint32_t kRegionVersion = 3;
 
 enum ProcStatus : int32_t { kProcFree = 0, kProcRunning = 1, kProcSuspended = 2 };
 
@@ -77,10 +77,15 @@ struct alignas(64) DeviceState {
   std::atomic<uint64_t> used;             // aggregate bytes charged (all live slots)
   std::atomic<uint64_t> spilled;          // portion of `used` served from host memory
   std::atomic<uint64_t> monitor_used;     // sampled physical usage of the region's PIDs
-  std::atomic<int64_t> tokens;            // temporal mode bucket (workgroups)
-  std::atomic<int64_t> token_cap;
-  std::atomic<int64_t> share;             // refill per period
-  std::atomic<int32_t> util_pct;          // last sampled utilisation (0..100)
+  std::atomic<int64_t> credit_ns;         // temporal mode: GPU-time credit (ratelimit.h)
+  std::atomic<uint64_t> charged_ns;       // GPU time charged to the container so far
+  std::atomic<uint64_t> wall_ns;          // wall time the sampler has accounted
+  std::atomic<int32_t> util_pm;           // smoothed utilisation, per mille
+  std::atomic<int32_t> gate_open;         // temporal mode: launches may proceed
+  int32_t num_se;                         // shader engines per XCC (mask layout)
+  int32_t cu_range_begin;                 // logical CU range of the vGPU (-1 = from pct)
+  int32_t cu_range_end;
+  std::atomic<int32_t> cu_mode;           // effective CuMode of this device
   uint32_t gpu_id;                        // KFD gpu_id (stats_<gpu_id> in sysfs)
   uint32_t bdf;                           // PCI bus/device/function (HSA BDFID)
   uint32_t domain;                        // PCI domain
@@ -104,6 +109,7 @@ struct RegionHeader {
   uint32_t flags;                           // RegionFlags
   uint32_t pad0;
   std::atomic<uint64_t> generation;         // bumped on any limit change
+  std::atomic<uint64_t> samples;            // sampler ticks (temporal mode)
 };
 
 enum RegionFlags : uint32_t { kFlagOversubscribe = 1u, kFlagActiveOomKiller = 2u };
@@ -165,6 +171,9 @@ class SharedRegion {
   // set_current_device_sm_limit_scale, suspend_all, resume_all, priority,
   // recent_kernel).
   void set_limit(int dev, uint64_t bytes);
+  // Changes the CU share of a device: the CU mask is recomputed here (every process of
+  // the container re-applies it to its queues when it sees the generation change) and,
+  // in auto mode, the enforcement mode follows the new share.
   void set_cu_limit(int dev, int pct);
   void suspend_all();
   void resume_all();

@@ -44,9 +44,11 @@ typedef struct {
   int32_t num_xcc;
   int32_t cu_mask_count;
   uint32_t cu_mask[8];
-  int64_t tokens;
-  int64_t share;
-  int32_t util_pct;
+  int64_t credit_ns;   /* temporal mode: remaining GPU-time credit */
+  uint64_t charged_ns; /* GPU time charged to the container */
+  uint64_t wall_ns;    /* wall time accounted by the sampler */
+  int32_t util_pct;    /* smoothed utilisation (charged / wall), percent */
+  int32_t cu_mode;     /* effective mode: 0 off, 1 spatial, 2 temporal, 3 both */
   uint32_t gpu_id;
   uint32_t bdf;
   uint32_t domain;

@@ -36,6 +36,12 @@ bool parse_int(const char* s, long lo, long hi, long* out) {
 }
 }  // namespace
 
+CuMode effective_cu_mode(CuMode m, int pct) {
+  if (m != CuMode::kAuto) return m;
+  if (pct <= 0 || pct >= 100) return CuMode::kSpatial;  // unlimited: no mask is applied anyway
+  return pct >= kAutoSpatialMinPct ? CuMode::kSpatial : CuMode::kTemporal;
+}
+
 bool Config::any_memory_limit() const {
   for (int i = 0; i < kMaxDevices; i++)
     if (dev[i].mem_limit) return true;
@@ -221,7 +227,8 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
     else if (!strcasecmp(s, "temporal")) cfg->cu_mode = CuMode::kTemporal;
     else if (!strcasecmp(s, "both")) cfg->cu_mode = CuMode::kBoth;
     else if (!strcasecmp(s, "off") || !strcasecmp(s, "none")) cfg->cu_mode = CuMode::kOff;
-    else VLOG_WARN("invalid VGPU_CU_MODE=%s, using spatial", s);
+    else if (!strcasecmp(s, "auto")) cfg->cu_mode = CuMode::kAuto;
+    else VLOG_WARN("invalid VGPU_CU_MODE=%s, using auto", s);
   }
   if (const char* s = getenv_fn("VGPU_CU_POLICY")) {
     if (!strcasecmp(s, "force")) cfg->cu_policy = CuPolicy::kForce;
@@ -233,6 +240,13 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   cfg->hook_smi = parse_bool(getenv_fn("VGPU_HOOK_SMI"), true);
   long period = 120;
   if (parse_int(getenv_fn("VGPU_UTIL_PERIOD_MS"), 10, 10000, &period)) cfg->util_period_ms = (int)period;
+  long sample = 1000;
+  if (parse_int(getenv_fn("VGPU_UTIL_SAMPLE_US"), 200, 100000, &sample)) cfg->util_sample_us = (int)sample;
+  long window = 40;
+  if (parse_int(getenv_fn("VGPU_LIMITER_WINDOW_MS"), 5, 2000, &window)) cfg->limiter_window_ms = (int)window;
+  if (const char* s = getenv_fn("VGPU_LOCK_FILE")) {
+    if (*s) cfg->lock_file = s;
+  }
   long merge = 1;
   if (parse_int(getenv_fn("VGPU_DUPLICATE_MERGE"), 0, 1, &merge)) cfg->duplicate_merge = (int)merge;
 }

@@ -3,7 +3,6 @@
 #include <time.h>
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace vgpu {
 
@@ -13,67 +12,72 @@ uint64_t now_ns() {
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
-int64_t limiter_delta(const LimiterSpec& spec, int limit_pct, int util_pct, int64_t share) {
-  const int64_t floor = spec.floor();
-  const int64_t ceil = spec.total();
-  if (share < floor) share = floor;
-  if (util_pct > limit_pct) {
-    // Proportional decrease toward limit/util, at most halving per period.
-    int64_t num = std::max(limit_pct, util_pct / 2);
-    share = std::max(floor, share * num / std::max(util_pct, 1));
-  } else if (util_pct < limit_pct) {
-    // Proportional increase toward limit/util (at most 4x per period), so a saturating
-    // tenant reaches its share in a handful of 120 ms periods instead of ramping +50 %
-    // at a time; an idle tenant (util 0) grows 1.5x plus one wave.
-    if (util_pct > 0) {
-      int64_t num = std::min<int64_t>(limit_pct, 4 * (int64_t)util_pct);
-      share = std::min(ceil, std::max(share + floor, share * num / util_pct));
-    } else {
-      share = std::min(ceil, share + share / 2 + floor);
-    }
+TimeShareParams timeshare_params(int limit_pct, int window_ms) {
+  TimeShareParams p;
+  p.limit_pct = limit_pct;
+  int pct = limit_pct > 0 && limit_pct < 100 ? limit_pct : 100;
+  if (window_ms <= 0) window_ms = 40;
+  p.burst_ns = std::max<int64_t>(4'000'000, (int64_t)window_ms * 1'000'000ll * pct / 100);
+  p.reopen_ns = p.burst_ns / 2;
+  p.debt_ns = 2'000'000'000ll;
+  return p;
+}
+
+int64_t timeshare_charge(int64_t dt_ns, int64_t mine, int64_t total) {
+  if (dt_ns <= 0 || mine <= 0) return 0;
+  if (total < mine) total = mine;
+  // 128-bit free: dt (< 2^40 for any sane interval) * mine (<= a few thousand waves).
+  return dt_ns * mine / total;
+}
+
+int64_t timeshare_interval(int64_t dt_ns, int prev_pm, int now_pm, bool gate_opened_at_prev) {
+  if (dt_ns <= 0) return 0;
+  if (gate_opened_at_prev && prev_pm == 0) return dt_ns * now_pm / 1000;
+  return dt_ns * (prev_pm + now_pm) / 2000;
+}
+
+int64_t timeshare_step(int64_t credit, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns) {
+  if (dt_ns < 0) dt_ns = 0;
+  int pct = p.limit_pct > 0 && p.limit_pct < 100 ? p.limit_pct : 100;
+  credit += dt_ns * pct / 100 - charge_ns;
+  if (credit > p.burst_ns) credit = p.burst_ns;
+  if (credit < -p.debt_ns) credit = -p.debt_ns;
+  return credit;
+}
+
+void timeshare_apply(DeviceState& d, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns) {
+  // Single writer (the sampler lease holder); launch gates only read the credit.
+  int64_t c = timeshare_step(d.credit_ns.load(std::memory_order_relaxed), p, dt_ns, charge_ns);
+  d.credit_ns.store(c, std::memory_order_release);
+  d.gate_open.store(timeshare_gate(d.gate_open.load(std::memory_order_relaxed) != 0, c, p) ? 1 : 0,
+                    std::memory_order_release);
+  d.charged_ns.fetch_add((uint64_t)std::max<int64_t>(0, charge_ns), std::memory_order_relaxed);
+  d.wall_ns.fetch_add((uint64_t)std::max<int64_t>(0, dt_ns), std::memory_order_relaxed);
+  // Utilisation over roughly the last 100 ms (EWMA of the charged fraction, per mille).
+  if (dt_ns > 0) {
+    int64_t frac = std::min<int64_t>(1000, charge_ns * 1000 / dt_ns);
+    int64_t prev = d.util_pm.load(std::memory_order_relaxed);
+    int64_t alpha = std::min<int64_t>(1000, dt_ns / 100'000);  // dt / 100 ms, per mille
+    d.util_pm.store((int32_t)(prev + (frac - prev) * alpha / 1000), std::memory_order_relaxed);
   }
-  return share;
 }
 
-int64_t limiter_initial_share(const LimiterSpec& spec, int limit_pct) {
-  int64_t pct = limit_pct > 0 && limit_pct < 100 ? limit_pct : 100;
-  return std::max(spec.floor(), spec.wave() * pct / 100);
-}
-
-void limiter_refill(DeviceState& d, const LimiterSpec& spec, int limit_pct, int util_pct) {
-  int64_t share = limiter_delta(spec, limit_pct, util_pct, d.share.load());
-  // Burst capacity of two periods: small enough that a saturating tenant is throttled
-  // within ~2 periods of exceeding its share; grids larger than the bucket simply
-  // wait for several refills (tokens go negative, never deadlock).
-  int64_t cap = 2 * share;
-  d.share.store(share);
-  d.token_cap.store(cap);
-  d.util_pct.store(util_pct);
-  int64_t cur = d.tokens.load();
-  while (!d.tokens.compare_exchange_weak(cur, std::min(cur + share, cap))) {
-  }
-}
-
-uint64_t limiter_acquire(RegionHeader& h, DeviceState& d, int64_t workgroups, int64_t sleep_ns) {
-  uint64_t waited = 0;
+uint64_t limiter_acquire(RegionHeader& h, DeviceState& d, bool limited, int64_t poll_ns) {
   uint64_t t0 = 0;
-  struct timespec ts = {(time_t)(sleep_ns / 1000000000), (long)(sleep_ns % 1000000000)};
-  // External launch block (reference: recent_kernel < 0).
+  struct timespec ts = {(time_t)(poll_ns / 1000000000), (long)(poll_ns % 1000000000)};
+  // External launch block (reference: recent_kernel < 0), honoured in every cu mode.
   while (h.recent_kernel.load(std::memory_order_relaxed) < 0) {
     if (!t0) t0 = now_ns();
     nanosleep(&ts, nullptr);
   }
-  if (h.recent_kernel.load(std::memory_order_relaxed) != 2) h.recent_kernel.store(2, std::memory_order_relaxed);
-  d.tokens.fetch_sub(workgroups, std::memory_order_acq_rel);
-  while (d.tokens.load(std::memory_order_acquire) < 0) {
+  while (limited && !d.gate_open.load(std::memory_order_acquire)) {
     if (!t0) t0 = now_ns();
-    // If no watcher refills (it died and nobody took over yet) do not block forever.
+    // Without a live sampler nobody repays the debt: never block forever.
     uint64_t hb = h.watcher_heartbeat.load(std::memory_order_relaxed);
-    if (hb && now_ns() - hb > 2'000'000'000ull) break;
+    if (!hb || now_ns() - hb > 1'000'000'000ull) break;
     nanosleep(&ts, nullptr);
   }
-  if (t0) waited = now_ns() - t0;
-  return waited;
+  return t0 ? now_ns() - t0 : 0;
 }
 
 }  // namespace vgpu

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "vgpu/cumask.h"
 #include "vgpu/log.h"
 
 namespace vgpu {
@@ -153,10 +154,14 @@ void SharedRegion::init_fresh(const Config* cfg) {
       d.mem_limit = cfg->dev[i].mem_limit;
       d.hbm_limit = cfg->dev[i].hbm_limit;
       d.cu_limit_pct = cfg->dev[i].cu_limit_pct;
+      d.cu_range_begin = cfg->dev[i].cu_range_begin;
+      d.cu_range_end = cfg->dev[i].cu_range_end;
       memcpy(d.uuid, cfg->dev[i].uuid, sizeof(d.uuid));
       d.uuid[sizeof(d.uuid) - 1] = 0;
     }
     n = cfg->num_devices;
+  } else {
+    for (int i = 0; i < kMaxDevices; i++) r_->dev[i].cu_range_begin = r_->dev[i].cu_range_end = -1;
   }
   r_->hdr.num_devices = n;
   r_->hdr.initialized.store(1);
@@ -298,7 +303,7 @@ Charge SharedRegion::charge(int slot, int dev, uint64_t bytes, MemKind kind) {
     uint64_t cur = d.used.load(std::memory_order_relaxed);
     bool admitted = false;
     while (true) {
-      if (lim && cur + bytes > lim) break;
+      if (lim && (bytes > lim || cur > lim - bytes)) break;  // overflow-safe cur + bytes > lim
       if (d.used.compare_exchange_weak(cur, cur + bytes, std::memory_order_acq_rel)) {
         admitted = true;
         break;
@@ -369,8 +374,22 @@ void SharedRegion::set_limit(int dev, uint64_t bytes) {
 }
 
 void SharedRegion::set_cu_limit(int dev, int pct) {
-  r_->dev[dev].cu_limit_pct = pct;
+  DeviceState& d = r_->dev[dev];
+  bool locked = lock();
+  d.cu_limit_pct = pct;
+  if (d.configured && d.cu_count > 0) {
+    // Keep the vGPU's anchor (the start of the slice the plugin assigned) and resize the
+    // slice to the new share, shifted left when it would run past the last CU.
+    const int xcc = d.num_xcc > 0 ? d.num_xcc : 1;
+    int want = cu_share_count(d.cu_count, xcc, pct);
+    int b = d.cu_range_begin >= 0 ? d.cu_range_begin / xcc * xcc : 0;
+    if (b + want > d.cu_count) b = (d.cu_count - want) / xcc * xcc;
+    CuMask m = cu_mask_range(d.cu_count, xcc, b, b + want, d.num_se > 0 ? d.num_se : 1);
+    memcpy(d.cu_mask, m.words, sizeof(d.cu_mask));
+    d.cu_mask_bits = m.nbits;
+  }
   if (dev >= r_->hdr.num_devices) r_->hdr.num_devices = dev + 1;
+  if (locked) unlock();
   r_->hdr.generation.fetch_add(1);
 }
 

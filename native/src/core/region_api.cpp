@@ -53,9 +53,11 @@ int vgpu_region_device_info(vgpu_region* r, int dev, vgpu_device_info* out) {
   m.nbits = d.cu_mask_bits;
   out->cu_mask_count = m.count();
   memcpy(out->cu_mask, d.cu_mask, sizeof(out->cu_mask));
-  out->tokens = d.tokens.load();
-  out->share = d.share.load();
-  out->util_pct = d.util_pct.load();
+  out->credit_ns = d.credit_ns.load();
+  out->charged_ns = d.charged_ns.load();
+  out->wall_ns = d.wall_ns.load();
+  out->util_pct = (d.util_pm.load() + 5) / 10;
+  out->cu_mode = d.cu_mode.load();
   out->gpu_id = d.gpu_id;
   out->bdf = d.bdf;
   out->domain = d.domain;

@@ -12,6 +12,10 @@
 //                     same holding dynamic LDS (few workgroups per CU at a time).
 //  * vgpu_stream_copy 16-byte-per-lane grid-stride copy; with the source in spilled
 //                     host memory it measures the oversubscription path's bandwidth.
+//  * vgpu_scratch_hog a kernel with a 16 KiB-per-lane private segment (dynamically
+//                     indexed, so it lives in scratch): makes ROCr allocate a large
+//                     scratch backing store behind the allocation hooks' back, which the
+//                     shim's context accounting has to pick up from KFD.
 //
 // C ABI, loaded with ctypes; pointers are device pointers (e.g. torch data_ptr()) and
 // `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream).
@@ -54,6 +58,18 @@ __global__ void __launch_bounds__(64) spin_lds_kernel(uint64_t spin_ticks) {
   if (threadIdx.x == 0) dyn_lds[0] = 1;
 }
 
+constexpr int kScratchWords = 4096;  // 16 KiB of private memory per lane
+
+__global__ void __launch_bounds__(64) scratch_kernel(uint32_t* out, uint32_t stride) {
+  uint32_t buf[kScratchWords];
+  const uint32_t lane = threadIdx.x;
+  // Data-dependent indices keep the array out of registers (stride comes from the host).
+  for (int i = 0; i < kScratchWords; i++) buf[(i * stride + lane) % kScratchWords] = i ^ lane;
+  uint32_t acc = 0;
+  for (int i = 0; i < kScratchWords; i += 7) acc += buf[(i * stride) % kScratchWords];
+  out[blockIdx.x * 64 + lane] = acc;
+}
+
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(256) copy_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src, size_t n) {
@@ -86,6 +102,14 @@ int vgpu_spin_lds(int nblocks, int spin_us, int lds_bytes, void* stream) {
   if (nblocks <= 0 || lds_bytes < 1 || lds_bytes > 160 * 1024) return -1;
   hipLaunchKernelGGL(spin_lds_kernel, dim3(nblocks), dim3(64), (size_t)lds_bytes, (hipStream_t)stream,
                      (uint64_t)spin_us * 100);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// `nblocks` single-wave workgroups, each lane with a 16 KiB private array; out holds
+// nblocks * 64 uint32. `stride` must be odd (any odd value gives a permutation).
+int vgpu_scratch_hog(uint32_t* out, int nblocks, int stride, void* stream) {
+  if (!out || nblocks <= 0 || !(stride & 1)) return -1;
+  hipLaunchKernelGGL(scratch_kernel, dim3(nblocks), dim3(64), 0, (hipStream_t)stream, out, (uint32_t)stride);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

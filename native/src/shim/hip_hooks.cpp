@@ -6,9 +6,10 @@
 // plain passthrough there [graph.c:224-225], so graph replays escape the throttle;
 // here graph launches are charged with the workgroups of their kernel nodes.
 //
-// Hot-path budget: with no temporal limit configured a launch pays one predictable
-// branch on process-local state plus two relaxed loads of region words
-// (suspend flags). The device lookup (hipGetDevice) only happens in temporal mode.
+// Hot-path budget: a launch pays one predictable branch on process-local state, a
+// relaxed increment of its own slot's launch counter, and relaxed loads of region words
+// (generation, suspend flags, launch block, and in temporal mode the device's credit).
+// The device lookup (hipGetDevice) only happens with several agents in temporal mode.
 #define __HIP_PLATFORM_AMD__ 1
 #include <hip/hip_runtime_api.h>
 
@@ -42,82 +43,44 @@ using ExtLaunchKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, size_t
 namespace {
 
 // VGPU_HOOK_LAUNCH=0: launch hooks become pure pass-throughs (diagnostics; disables the
-// suspend gate and the temporal limiter at launch). Read once at load time.
+// suspend gate, the launch block and the temporal limiter at launch). Read once at load.
 bool g_launch_hooks_on = true;
 __attribute__((constructor)) void launch_hook_ctor() {
   const char* s = getenv("VGPU_HOOK_LAUNCH");
   if (s && *s == '0') g_launch_hooks_on = false;
 }
 
-std::atomic<int> g_temporal_any{-1};  // -1 unknown, 0 no agent gated, 1 some agent gated
-std::mutex g_graph_mu;
-std::unordered_map<uintptr_t, int64_t> g_graph_wgs;  // hipGraphExec_t → workgroups per launch
-
-int temporal_any() {
-  int v = g_temporal_any.load(std::memory_order_relaxed);
-  if (__builtin_expect(v >= 0, 1)) return v;
-  ShimState& s = shim();
-  if (s.phase.load(std::memory_order_acquire) != 2) return 0;
-  int any = 0;
-  for (int i = 0; i < s.n_agents; i++) any |= s.agents[i].temporal_active ? 1 : 0;
-  g_temporal_any.store(any);
-  return any;
-}
-
-inline void launch_gate(int64_t workgroups) {
+inline void launch_gate() {
   VGPU_STAT(kStatLaunch);
   if (__builtin_expect(!g_launch_hooks_on, 0)) return;
-  ShimState& s = shim();
-  if (__builtin_expect(!s.active, 1)) return;
-  gate_suspend();
-  if (__builtin_expect(temporal_any(), 0)) gate_launch(workgroups, -1);
-}
-
-int64_t graph_workgroups(hipGraph_t graph) {
-  VGPU_REAL_HIP(hipGraphGetNodes);
-  VGPU_REAL_HIP(hipGraphNodeGetType);
-  VGPU_REAL_HIP(hipGraphKernelNodeGetParams);
-  if (!real_hipGraphGetNodes || !real_hipGraphNodeGetType || !real_hipGraphKernelNodeGetParams) return 0;
-  size_t n = 0;
-  if (real_hipGraphGetNodes(graph, nullptr, &n) != hipSuccess || n == 0) return 0;
-  std::vector<hipGraphNode_t> nodes(n);
-  if (real_hipGraphGetNodes(graph, nodes.data(), &n) != hipSuccess) return 0;
-  int64_t total = 0;
-  for (size_t i = 0; i < n; i++) {
-    hipGraphNodeType t;
-    if (real_hipGraphNodeGetType(nodes[i], &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
-    hipKernelNodeParams p{};
-    if (real_hipGraphKernelNodeGetParams(nodes[i], &p) != hipSuccess) continue;
-    total += (int64_t)p.gridDim.x * p.gridDim.y * p.gridDim.z;
-  }
-  return total;
-}
-
-void remember_graph(hipGraphExec_t exec, hipGraph_t graph) {
-  if (!shim().active || !temporal_any()) return;
-  int64_t wgs = graph_workgroups(graph);
-  std::lock_guard<std::mutex> g(g_graph_mu);
-  g_graph_wgs[reinterpret_cast<uintptr_t>(exec)] = wgs;
+  if (__builtin_expect(!shim().active, 1)) return;
+  gate_launch(-1);
 }
 
 }  // namespace
 
 namespace vgpu {
 
-void gate_launch(int64_t workgroups, int dev) {
+void gate_launch(int dev) {
   ShimState& s = shim();
+  Region* r = s.region.raw();
+  if (s.slot >= 0) r->procs[s.slot].launches.fetch_add(1, std::memory_order_relaxed);
+  check_live_config();
+  gate_suspend();
   if (dev < 0) {
-    if (s.n_agents == 1) {
-      dev = 0;
-    } else {
+    dev = 0;
+    if (s.n_agents > 1) {
+      bool any = false;
+      for (int i = 0; i < s.n_agents; i++) any |= s.agents[i].temporal_active.load(std::memory_order_relaxed);
       VGPU_REAL_HIP(hipGetDevice);
-      if (!real_hipGetDevice || real_hipGetDevice(&dev) != hipSuccess) dev = 0;
+      if (any && (!real_hipGetDevice || real_hipGetDevice(&dev) != hipSuccess)) dev = 0;
     }
   }
-  if (dev < 0 || dev >= s.n_agents || !s.agents[dev].temporal_active) return;
-  Region* r = s.region.raw();
-  if (!r->hdr.utilization_switch.load(std::memory_order_relaxed) && config().cu_policy != CuPolicy::kForce) return;
-  uint64_t waited = limiter_acquire(r->hdr, r->dev[dev], workgroups);
+  if (dev < 0 || dev >= s.n_agents) dev = 0;
+  bool limited = s.agents[dev].temporal_active.load(std::memory_order_relaxed) &&
+                 (r->hdr.utilization_switch.load(std::memory_order_relaxed) || config().cu_policy == CuPolicy::kForce);
+  if (__builtin_expect(!limiter_would_block(r->hdr, r->dev[dev], limited), 1)) return;
+  uint64_t waited = limiter_acquire(r->hdr, r->dev[dev], limited);
   if (waited && s.slot >= 0) r->procs[s.slot].throttle_ns.fetch_add(waited, std::memory_order_relaxed);
 }
 
@@ -128,7 +91,7 @@ extern "C" {
 hipError_t hipLaunchKernel(const void* function_address, dim3 numBlocks, dim3 dimBlocks, void** args,
                            size_t sharedMemBytes, hipStream_t stream) {
   VGPU_REAL_HIP_T(hipLaunchKernel, LaunchKernelFn);
-  launch_gate((int64_t)numBlocks.x * numBlocks.y * numBlocks.z);
+  launch_gate();
   return real_hipLaunchKernel(function_address, numBlocks, dimBlocks, args, sharedMemBytes, stream);
 }
 
@@ -136,7 +99,7 @@ hipError_t hipExtLaunchKernel(const void* function_address, dim3 numBlocks, dim3
                               size_t sharedMemBytes, hipStream_t stream, hipEvent_t startEvent, hipEvent_t stopEvent,
                               int flags) {
   VGPU_REAL_HIP_T(hipExtLaunchKernel, ExtLaunchKernelFn);
-  launch_gate((int64_t)numBlocks.x * numBlocks.y * numBlocks.z);
+  launch_gate();
   return real_hipExtLaunchKernel(function_address, numBlocks, dimBlocks, args, sharedMemBytes, stream, startEvent,
                                  stopEvent, flags);
 }
@@ -145,7 +108,7 @@ hipError_t hipModuleLaunchKernel(hipFunction_t f, unsigned int gridDimX, unsigne
                                  unsigned int blockDimX, unsigned int blockDimY, unsigned int blockDimZ,
                                  unsigned int sharedMemBytes, hipStream_t stream, void** kernelParams, void** extra) {
   VGPU_REAL_HIP(hipModuleLaunchKernel);
-  launch_gate((int64_t)gridDimX * gridDimY * gridDimZ);
+  launch_gate();
   return real_hipModuleLaunchKernel(f, gridDimX, gridDimY, gridDimZ, blockDimX, blockDimY, blockDimZ, sharedMemBytes,
                                     stream, kernelParams, extra);
 }
@@ -156,9 +119,7 @@ hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t globalWorkSizeX, u
                                     void** kernelParams, void** extra, hipEvent_t startEvent, hipEvent_t stopEvent,
                                     uint32_t flags) {
   VGPU_REAL_HIP(hipExtModuleLaunchKernel);
-  auto wg = [](uint32_t g, uint32_t l) -> int64_t { return l ? (g + l - 1) / l : g; };
-  launch_gate(wg(globalWorkSizeX, localWorkSizeX) * wg(globalWorkSizeY, localWorkSizeY) *
-              wg(globalWorkSizeZ, localWorkSizeZ));
+  launch_gate();
   return real_hipExtModuleLaunchKernel(f, globalWorkSizeX, globalWorkSizeY, globalWorkSizeZ, localWorkSizeX,
                                        localWorkSizeY, localWorkSizeZ, sharedMemBytes, hStream, kernelParams, extra,
                                        startEvent, stopEvent, flags);
@@ -167,7 +128,7 @@ hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t globalWorkSizeX, u
 hipError_t hipLaunchCooperativeKernel(const void* f, dim3 gridDim, dim3 blockDimX, void** kernelParams,
                                       unsigned int sharedMemBytes, hipStream_t stream) {
   VGPU_REAL_HIP_T(hipLaunchCooperativeKernel, CoopKernelFn);
-  launch_gate((int64_t)gridDim.x * gridDim.y * gridDim.z);
+  launch_gate();
   return real_hipLaunchCooperativeKernel(f, gridDim, blockDimX, kernelParams, sharedMemBytes, stream);
 }
 
@@ -176,55 +137,19 @@ hipError_t hipModuleLaunchCooperativeKernel(hipFunction_t f, unsigned int gridDi
                                             unsigned int blockDimZ, unsigned int sharedMemBytes, hipStream_t stream,
                                             void** kernelParams) {
   VGPU_REAL_HIP(hipModuleLaunchCooperativeKernel);
-  launch_gate((int64_t)gridDimX * gridDimY * gridDimZ);
+  launch_gate();
   return real_hipModuleLaunchCooperativeKernel(f, gridDimX, gridDimY, gridDimZ, blockDimX, blockDimY, blockDimZ,
                                                sharedMemBytes, stream, kernelParams);
-}
-
-hipError_t hipGraphInstantiate(hipGraphExec_t* pGraphExec, hipGraph_t graph, hipGraphNode_t* pErrorNode,
-                               char* pLogBuffer, size_t bufferSize) {
-  VGPU_REAL_HIP(hipGraphInstantiate);
-  hipError_t e = real_hipGraphInstantiate(pGraphExec, graph, pErrorNode, pLogBuffer, bufferSize);
-  if (e == hipSuccess && pGraphExec) remember_graph(*pGraphExec, graph);
-  return e;
-}
-
-hipError_t hipGraphInstantiateWithFlags(hipGraphExec_t* pGraphExec, hipGraph_t graph, unsigned long long flags) {
-  VGPU_REAL_HIP(hipGraphInstantiateWithFlags);
-  hipError_t e = real_hipGraphInstantiateWithFlags(pGraphExec, graph, flags);
-  if (e == hipSuccess && pGraphExec) remember_graph(*pGraphExec, graph);
-  return e;
 }
 
 hipError_t hipGraphLaunch(hipGraphExec_t graphExec, hipStream_t stream) {
   VGPU_REAL_HIP(hipGraphLaunch);
   VGPU_STAT(kStatGraphLaunch);
-  ShimState& s = shim();
-  if (__builtin_expect(s.active, 0)) {
-    gate_suspend();
-    if (temporal_any()) {
-      int64_t wgs = 0;
-      {
-        std::lock_guard<std::mutex> g(g_graph_mu);
-        auto it = g_graph_wgs.find(reinterpret_cast<uintptr_t>(graphExec));
-        if (it != g_graph_wgs.end()) wgs = it->second;
-      }
-      // Unknown graphs (instantiated before the shim was active) cost one full wave
-      // of the device so they are never free.
-      if (wgs <= 0) wgs = s.n_agents ? s.agents[0].cu_count : 256;
-      gate_launch(wgs, -1);
-    }
-  }
+  // A graph replay is one launch for the gates: the temporal limiter charges GPU time,
+  // not launches, so a graph costs what its kernels run (the reference's cuGraphLaunch
+  // bypassed the throttle entirely, [graph.c:224-225]).
+  launch_gate();
   return real_hipGraphLaunch(graphExec, stream);
-}
-
-hipError_t hipGraphExecDestroy(hipGraphExec_t graphExec) {
-  VGPU_REAL_HIP(hipGraphExecDestroy);
-  {
-    std::lock_guard<std::mutex> g(g_graph_mu);
-    g_graph_wgs.erase(reinterpret_cast<uintptr_t>(graphExec));
-  }
-  return real_hipGraphExecDestroy(graphExec);
 }
 
 // Managed memory (reference: cuMemAllocManaged is an accounted allocation, class (a) in

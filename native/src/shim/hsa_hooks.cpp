@@ -11,7 +11,7 @@
 //   cuMemFree_v2  → remove_chunk → rm usage                              (free)
 //   cuMemGetInfo_v2 / cuDeviceTotalMem_v2 → limit-based answers          (info hooks)
 //   CUDA_OVERSUBSCRIBE → managed memory                                  (host spill)
-//   cuIpc* pass-through without double charge                            (not hooked)
+//   cuIpc* pass-through without double charge    (suspend-gated, charged to the exporter)
 // MI355X-only: hsa_queue_create applies the vGPU's CU mask to every HW queue and
 // hsa_amd_queue_cu_set_mask cannot widen it.
 #include <unistd.h>
@@ -76,23 +76,6 @@ inline bool ready() {
     ph = s.phase.load(std::memory_order_acquire);
   }
   return ph == 2 && s.active && !s.exiting.load(std::memory_order_relaxed);
-}
-
-void charge_context_once(int dev) {
-  // Per-process runtime overhead (queues, scratch, code objects) is allocated by
-  // ROCr internally and bypasses the pool hooks. Charge it once as "context" memory
-  // from KFD's own per-process VRAM counter (reference: primary context size).
-  ShimState& s = shim();
-  AgentInfo& a = s.agents[dev];
-  if (a.context_charged || !s.hostpid || !a.gpu_id) return;
-  a.context_charged = true;
-  int64_t vram = kfd_vram_usage(s.hostpid, a.gpu_id);
-  if (vram <= 0) return;
-  uint64_t mine = s.region.proc_usage(s.slot, dev);
-  if ((uint64_t)vram > mine) {
-    uint64_t ctx = (uint64_t)vram - mine;
-    if (ctx < (1ull << 30)) s.region.force_charge(s.slot, dev, ctx, kMemContext);
-  }
 }
 
 }  // namespace
@@ -278,7 +261,7 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
     std::lock_guard<std::mutex> g(s.alloc_mu);
     s.queues[reinterpret_cast<uintptr_t>(*queue)] = dev;
   }
-  if (a.mask_active) {
+  if (a.mask_active.load()) {
     VGPU_REAL_HSA(hsa_amd_queue_cu_set_mask);
     uint32_t nbits = (uint32_t)((a.cu_count + 31) / 32 * 32);
     hsa_status_t ms = real_hsa_amd_queue_cu_set_mask(*queue, nbits, a.mask.words);
@@ -299,7 +282,9 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
     else
       VLOG_INFO("device %d: queue %p priority %s", dev, (void*)*queue, prio <= 0 ? "high" : "low");
   }
-  charge_context_once(dev);
+  // Queue creation is where ROCr allocates the process's ring buffers, scratch and
+  // trap handlers: account them right away (the maintenance thread keeps it in sync).
+  resync_context_charge();
   return st;
 }
 
@@ -315,7 +300,8 @@ hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* queue, uint32_t num_cu
     auto it = s.queues.find(reinterpret_cast<uintptr_t>(queue));
     if (it != s.queues.end()) dev = it->second;
   }
-  if (dev < 0 || !s.agents[dev].mask_active) return real_hsa_amd_queue_cu_set_mask(queue, num_cu_mask_count, cu_mask);
+  if (dev < 0 || !s.agents[dev].mask_active.load())
+    return real_hsa_amd_queue_cu_set_mask(queue, num_cu_mask_count, cu_mask);
   AgentInfo& a = s.agents[dev];
   // A user mask (hipExtStreamCreateWithCUMask, ROC_GLOBAL_CU_MASK) may only narrow
   // the vGPU's partition, never widen it; count 0 means "all CUs" → the vGPU mask.
@@ -341,6 +327,44 @@ hsa_status_t hsa_queue_destroy(hsa_queue_t* queue) {
     s.queues.erase(reinterpret_cast<uintptr_t>(queue));
   }
   return real_hsa_queue_destroy(queue);
+}
+
+// IPC (reference: cuIpcOpenMemHandle/CloseMemHandle are suspend-gated pass-throughs,
+// [memory.c:374-388]). The exporting process already holds the charge for the buffer
+// and KFD does not count the import in the importer's VRAM, so the importer is never
+// charged; the mapping is recorded for diagnostics (VGPU_LOG_LEVEL=4, ipc_bytes).
+hsa_status_t hsa_amd_ipc_memory_attach(const hsa_amd_ipc_memory_t* handle, size_t len, uint32_t num_agents,
+                                       const hsa_agent_t* mapping_agents, void** mapped_ptr) {
+  VGPU_REAL_HSA(hsa_amd_ipc_memory_attach);
+  if (!real_hsa_amd_ipc_memory_attach) return HSA_STATUS_ERROR;
+  gate_suspend();
+  hsa_status_t st = real_hsa_amd_ipc_memory_attach(handle, len, num_agents, mapping_agents, mapped_ptr);
+  if (st != HSA_STATUS_SUCCESS || !mapped_ptr || !*mapped_ptr || !ready()) return st;
+  ShimState& s = shim();
+  int dev = num_agents && mapping_agents ? agent_ordinal(mapping_agents[0]) : 0;
+  if (dev < 0) dev = 0;
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    s.ipc[reinterpret_cast<uintptr_t>(*mapped_ptr)] = AllocRec{len, dev, kMemData};
+  }
+  s.ipc_bytes[dev].fetch_add((int64_t)len);
+  VLOG_DEBUG("ipc attach %zu bytes at %p on device %d (charged to the exporter)", len, *mapped_ptr, dev);
+  return st;
+}
+
+hsa_status_t hsa_amd_ipc_memory_detach(void* mapped_ptr) {
+  VGPU_REAL_HSA(hsa_amd_ipc_memory_detach);
+  if (!real_hsa_amd_ipc_memory_detach) return HSA_STATUS_ERROR;
+  ShimState& s = shim();
+  if (mapped_ptr && s.phase.load(std::memory_order_relaxed) == 2) {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    auto it = s.ipc.find(reinterpret_cast<uintptr_t>(mapped_ptr));
+    if (it != s.ipc.end()) {
+      s.ipc_bytes[it->second.dev].fetch_sub((int64_t)it->second.size);
+      s.ipc.erase(it);
+    }
+  }
+  return real_hsa_amd_ipc_memory_detach(mapped_ptr);
 }
 
 }  // extern "C"

@@ -70,7 +70,12 @@ hsa_status_t pool_cb(hsa_amd_memory_pool_t pool, void* data) {
   uint32_t flags = 0;
   real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SIZE, &sz);
   real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
-  if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && sz > a->phys_total) a->phys_total = sz;
+  if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && sz > a->phys_total) {
+    a->phys_total = sz;
+    bool alloc_ok = false;
+    real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc_ok);
+    if (alloc_ok) a->vram_pool = pool;
+  }
   return HSA_STATUS_SUCCESS;
 }
 
@@ -149,7 +154,10 @@ void atfork_child() {
   s.allocs.clear();
   s.vmem.clear();
   s.managed.clear();
+  s.ipc.clear();
+  for (auto& b : s.ipc_bytes) b.store(0);
   s.queues.clear();
+  s.hostpid = 0;
   s.watcher_started.store(false);
   s.phase.store(0);
   s.pid = getpid();
@@ -280,11 +288,9 @@ void shim_init_after_hsa() {
   for (int i = 0; i < kMaxDevices; i++) resolved.dev[i] = i < s.n_agents ? per_agent[i] : DeviceConfig();
   resolved.num_devices = s.n_agents;
 
-  // Host PID: sysfs is not PID-namespaced; outside a container it equals getpid().
-  if (!s.hostpid) {
-    std::vector<int> pids = kfd_list_pids();
-    if (std::binary_search(pids.begin(), pids.end(), (int)s.pid)) s.hostpid = s.pid;
-  }
+  // Host PID: sysfs is not PID-namespaced; outside a container it equals getpid(),
+  // inside one the VRAM signature resolves it (the maintenance thread retries).
+  if (!s.hostpid) s.hostpid = resolve_hostpid(2000);
 
   int rc = s.region.attach(cfg.shared_cache.c_str(), &resolved, true);
   if (rc != 0) {
@@ -314,30 +320,23 @@ void shim_init_after_hsa() {
       if (!d.mem_limit && per_agent[i].mem_limit) d.mem_limit = per_agent[i].mem_limit;
       if (!d.hbm_limit && per_agent[i].hbm_limit) d.hbm_limit = per_agent[i].hbm_limit;
       if (!d.cu_limit_pct && per_agent[i].cu_limit_pct) d.cu_limit_pct = per_agent[i].cu_limit_pct;
+      if (d.cu_range_begin < 0 && per_agent[i].cu_range_begin >= 0) {
+        d.cu_range_begin = per_agent[i].cu_range_begin;
+        d.cu_range_end = per_agent[i].cu_range_end;
+      }
       const char* layout = getenv("VGPU_CU_LAYOUT");  // "se" (default) | "interleave"
-      int se = (layout && !strcasecmp(layout, "interleave")) ? 1 : a.num_se;
-      CuMask m = cu_mask_for(a.cu_count, a.num_xcc, d.cu_limit_pct, per_agent[i].cu_range_begin,
-                             per_agent[i].cu_range_end, se);
+      d.num_se = (layout && !strcasecmp(layout, "interleave")) ? 1 : a.num_se;
+      CuMask m = cu_mask_for(a.cu_count, a.num_xcc, d.cu_limit_pct, d.cu_range_begin, d.cu_range_end, d.num_se);
       memcpy(d.cu_mask, m.words, sizeof(d.cu_mask));
       d.cu_mask_bits = m.nbits;
-      LimiterSpec spec{a.cu_count, a.max_waves_per_cu * 64};
-      int64_t share0 = limiter_initial_share(spec, d.cu_limit_pct);
-      d.share.store(share0);
-      d.tokens.store(share0);
-      d.token_cap.store(2 * share0);
+      d.credit_ns.store(timeshare_params(d.cu_limit_pct, config().limiter_window_ms).burst_ns);
+      d.gate_open.store(1);
       d.configured = 1;
     }
-    memcpy(a.mask.words, d.cu_mask, sizeof(a.mask.words));
-    a.mask.nbits = d.cu_mask_bits ? d.cu_mask_bits : a.cu_count;
-    bool limited = d.cu_limit_pct > 0 && d.cu_limit_pct < 100;
-    bool spatial = cfg.cu_mode == CuMode::kSpatial || cfg.cu_mode == CuMode::kBoth;
-    bool temporal = cfg.cu_mode == CuMode::kTemporal || cfg.cu_mode == CuMode::kBoth;
-    bool force = cfg.cu_policy == CuPolicy::kForce, off = cfg.cu_policy == CuPolicy::kDisable;
-    a.mask_active = !off && spatial && (limited || per_agent[i].cu_range_begin >= 0) &&
-                    a.mask.count() < a.cu_count && a.mask.count() > 0;
-    a.temporal_active = !off && temporal && (limited || force);
   }
   s.region.unlock();
+  s.seen_generation.store(r->hdr.generation.load() - 1);  // forces the first apply below
+  apply_live_config();
 
   s.slot = s.region.register_process(s.pid, s.hostpid, cfg.priority);
   s.active = s.slot >= 0;
@@ -352,13 +351,130 @@ void shim_init_after_hsa() {
   });
   for (int i = 0; i < s.n_agents; i++) {
     const DeviceState& d = r->dev[i];
-    VLOG_INFO("device %d uuid=%s gpu_id=%u cus=%d xcc=%d limit=%lu MiB cu_limit=%d%% mask=%d CUs%s%s", i, d.uuid,
-              s.agents[i].gpu_id, s.agents[i].cu_count, s.agents[i].num_xcc, (unsigned long)(d.mem_limit >> 20),
-              d.cu_limit_pct, s.agents[i].mask.count(), s.agents[i].mask_active ? " [spatial]" : "",
-              s.agents[i].temporal_active ? " [temporal]" : "");
+    VLOG_INFO("device %d uuid=%s gpu_id=%u cus=%d xcc=%d limit=%lu MiB cu_limit=%d%% mask=%d CUs%s%s hostpid=%d", i,
+              d.uuid, s.agents[i].gpu_id, s.agents[i].cu_count, s.agents[i].num_xcc,
+              (unsigned long)(d.mem_limit >> 20), d.cu_limit_pct, s.agents[i].mask.count(),
+              s.agents[i].mask_active ? " [spatial]" : "", s.agents[i].temporal_active ? " [temporal]" : "",
+              (int)s.hostpid);
   }
   s.phase.store(2);
   start_watcher_if_needed();
+}
+
+namespace {
+
+bool probe_vram(void* ctx, uint64_t bytes, bool alloc) {
+  // One probe buffer at a time (kfd_resolve_hostpid allocates, reads sysfs, frees).
+  static void* ptr = nullptr;
+  AgentInfo* a = static_cast<AgentInfo*>(ctx);
+  if (alloc) {
+    VGPU_REAL_HSA(hsa_amd_memory_pool_allocate);
+    ptr = nullptr;
+    return real_hsa_amd_memory_pool_allocate(a->vram_pool, bytes, 0, &ptr) == HSA_STATUS_SUCCESS && ptr;
+  }
+  VGPU_REAL_HSA(hsa_amd_memory_pool_free);
+  if (ptr) real_hsa_amd_memory_pool_free(ptr);
+  ptr = nullptr;
+  return true;
+}
+
+}  // namespace
+
+pid_t resolve_hostpid(int lock_timeout_ms) {
+  ShimState& s = shim();
+  for (int i = 0; i < s.n_agents; i++) {
+    AgentInfo& a = s.agents[i];
+    if (!a.gpu_id || !a.vram_pool.handle) continue;
+    return kfd_resolve_hostpid(a.gpu_id, probe_vram, &a, config().lock_file.c_str(), lock_timeout_ms,
+                               (unsigned)(now_ns() ^ (uint64_t)getpid() << 20));
+  }
+  std::vector<int> pids = kfd_list_pids();
+  return std::binary_search(pids.begin(), pids.end(), (int)getpid()) ? getpid() : 0;
+}
+
+void apply_live_config() {
+  ShimState& s = shim();
+  std::lock_guard<std::mutex> g(s.live_mu);
+  Region* r = s.region.raw();
+  const uint64_t gen = r->hdr.generation.load(std::memory_order_acquire);
+  if (gen == s.seen_generation.load()) return;
+  const Config& cfg = config();
+  const bool force = cfg.cu_policy == CuPolicy::kForce, off = cfg.cu_policy == CuPolicy::kDisable;
+  for (int i = 0; i < s.n_agents; i++) {
+    AgentInfo& a = s.agents[i];
+    DeviceState& d = r->dev[i];
+    s.region.lock();
+    CuMask m;
+    memcpy(m.words, d.cu_mask, sizeof(m.words));
+    m.nbits = d.cu_mask_bits ? d.cu_mask_bits : a.cu_count;
+    const int pct = d.cu_limit_pct;
+    const bool ranged = d.cu_range_begin >= 0;
+    s.region.unlock();
+    const bool limited = pct > 0 && pct < 100;
+    const CuMode mode = effective_cu_mode(cfg.cu_mode, pct);
+    const bool spatial = mode == CuMode::kSpatial || mode == CuMode::kBoth;
+    const bool temporal = mode == CuMode::kTemporal || mode == CuMode::kBoth;
+    const bool mask_on = !off && spatial && (limited || ranged) && m.count() < a.cu_count && m.count() > 0;
+    const bool temp_on = !off && temporal && (limited || force);
+    const bool mask_changed = mask_on != a.mask_active.load() || memcmp(m.words, a.mask.words, sizeof(m.words)) != 0;
+    if (temp_on && !a.temporal_active.load() && !d.gate_open.load()) {
+      d.credit_ns.store(timeshare_params(pct, cfg.limiter_window_ms).burst_ns);
+      d.gate_open.store(1);
+    }
+    a.mask = m;
+    a.mode = mode;
+    a.temporal_active.store(temp_on);
+    int flags = (mask_on ? 1 : 0) | (temp_on ? 2 : 0);
+    d.cu_mode.store(flags);
+    if (mask_changed) {
+      a.mask_active.store(mask_on);
+      // Re-apply to every queue this process already owns (they were created with the
+      // old mask); new queues pick the mask up in hsa_queue_create.
+      std::vector<hsa_queue_t*> qs;
+      {
+        std::lock_guard<std::mutex> q(s.alloc_mu);
+        for (auto& kv : s.queues)
+          if (kv.second == i) qs.push_back(reinterpret_cast<hsa_queue_t*>(kv.first));
+      }
+      VGPU_REAL_HSA(hsa_amd_queue_cu_set_mask);
+      CuMask all;
+      for (int b = 0; b < a.cu_count && b < kMaxCUs; b++) all.set(b);
+      const CuMask& eff = mask_on ? m : all;
+      uint32_t nbits = (uint32_t)((a.cu_count + 31) / 32 * 32);
+      for (hsa_queue_t* q : qs) {
+        hsa_status_t st = real_hsa_amd_queue_cu_set_mask(q, nbits, eff.words);
+        if (st != HSA_STATUS_SUCCESS && (int)st != (int)HSA_STATUS_CU_MASK_REDUCED)
+          VLOG_ERROR("device %d: cannot re-apply CU mask to queue %p (status %d)", i, (void*)q, (int)st);
+      }
+      if (!qs.empty())
+        VLOG_INFO("device %d: CU limit %d%% -> %d CUs re-applied to %zu queue(s)", i, pct,
+                  mask_on ? m.count() : a.cu_count, qs.size());
+    }
+  }
+  s.seen_generation.store(gen);
+  if (s.phase.load() == 2) start_watcher_if_needed();
+}
+
+void resync_context_charge() {
+  ShimState& s = shim();
+  if (!s.active || s.slot < 0 || !s.hostpid || s.exiting.load()) return;
+  Region* r = s.region.raw();
+  for (int i = 0; i < s.n_agents; i++) {
+    const AgentInfo& a = s.agents[i];
+    if (!a.gpu_id) continue;
+    int64_t vram = kfd_vram_usage(s.hostpid, a.gpu_id);
+    if (vram < 0) continue;
+    DeviceUsage& u = r->procs[s.slot].used[i];
+    int64_t tracked = (int64_t)u.kind[kMemData].load();
+    // IPC imports are not in the importer's vram_<gpu_id> (measured on MI355X: a 1 GiB
+    // import left the consumer's counter at its ~0.5 GiB runtime footprint,
+    // profiles/r2e), so nothing is subtracted for them: the exporter alone holds the charge.
+    int64_t ctx_now = vram - tracked;
+    if (ctx_now < 0) ctx_now = 0;
+    int64_t ctx_had = (int64_t)u.kind[kMemContext].load();
+    if (ctx_now > ctx_had) s.region.force_charge(s.slot, i, (uint64_t)(ctx_now - ctx_had), kMemContext);
+    else if (ctx_now < ctx_had) s.region.uncharge(s.slot, i, (uint64_t)(ctx_had - ctx_now), kMemContext);
+  }
 }
 
 void gate_suspend_slow() {

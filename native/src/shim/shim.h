@@ -32,12 +32,13 @@ struct AgentInfo {
   int num_se = 1;                    // shader engines per XCC (mask layout)
   int max_waves_per_cu = 32;
   uint64_t phys_total = 0;
-  bool mask_active = false;          // spatial mask applied to its queues
-  bool authorised = true;            // listed in VGPU_ALLOWLIST (when one is configured)
-  bool temporal_active = false;      // token bucket gates its launches
-  bool context_charged = false;
+  std::atomic<bool> mask_active{false};      // spatial mask applied to its queues
+  bool authorised = true;                    // listed in VGPU_ALLOWLIST (when one is configured)
+  std::atomic<bool> temporal_active{false};  // GPU-time credit gates its launches
+  CuMode mode = CuMode::kOff;                // effective enforcement mode
   CuMask mask;
   hsa_amd_memory_pool_t pools[8]{};  // GPU-local pools of this agent
+  hsa_amd_memory_pool_t vram_pool{0};  // coarse-grained VRAM pool (host-PID probe allocations)
   int n_pools = 0;
 };
 
@@ -60,9 +61,13 @@ struct ShimState {
   std::unordered_map<uintptr_t, AllocRec> allocs;   // device pointer → record
   std::unordered_map<uint64_t, AllocRec> vmem;      // vmem handle → record
   std::unordered_map<uintptr_t, AllocRec> managed;  // hipMallocManaged pointers charged at HIP level
+  std::unordered_map<uintptr_t, AllocRec> ipc;      // IPC-attached pointers (owned by another process)
   std::unordered_map<uintptr_t, int> queues;        // hsa_queue_t* → ordinal
   std::atomic<bool> exiting{false};
   std::atomic<bool> watcher_started{false};
+  std::atomic<uint64_t> seen_generation{0};         // region generation the queues reflect
+  std::atomic<int64_t> ipc_bytes[kMaxDevices] = {};  // IPC-attached bytes per device
+  std::mutex live_mu;                               // serialises live reconfiguration
 };
 
 ShimState& shim();
@@ -103,11 +108,35 @@ inline void gate_suspend() {
   if (__builtin_expect(gate_needed(), 0)) gate_suspend_slow();
 }
 
-// Kernel-launch gate: suspend check + temporal token bucket for device `dev`
-// (dev < 0 = current HIP device).
-void gate_launch(int64_t workgroups, int dev);
+// Kernel-launch gate: launch counter, live reconfiguration, suspend check, external
+// launch block and the temporal GPU-time credit of device `dev` (dev < 0 = current HIP
+// device).
+void gate_launch(int dev);
 
-// Utilisation watcher (temporal mode, monitor-based OOM killer, memory override).
+// Re-reads limits the controller changed in the region (generation bump): CU masks are
+// re-applied to every tracked queue and the enforcement mode follows the new share.
+void apply_live_config();
+inline void check_live_config() {
+  ShimState& s = shim();
+  if (__builtin_expect(s.region.raw()->hdr.generation.load(std::memory_order_relaxed) !=
+                           s.seen_generation.load(std::memory_order_relaxed),
+                       0))
+    apply_live_config();
+}
+
+// Per-process maintenance thread: host-PID discovery retries, continuous context
+// accounting, and (for the process holding the container's sampler lease) the
+// temporal-mode occupancy sampler, monitor-based usage and the active OOM killer.
 void start_watcher_if_needed();
+
+// Host PID of this process via the VRAM signature (kfd.h); 0 if still unknown.
+pid_t resolve_hostpid(int lock_timeout_ms);
+
+// Re-syncs this process's "context" charge on every device with KFD's view of its VRAM:
+// context = vram_<gpu_id> − (tracked HBM allocations). Covers the
+// runtime's internal allocations (queues, scratch / private segments, code objects)
+// that never pass the pool hooks (reference: per-context and per-module charges,
+// [context.c:49-86], [export_table.c:85-113]).
+void resync_context_charge();
 
 }  // namespace vgpu

@@ -1,23 +1,29 @@
-// Utilisation watcher: the feedback loop of the temporal limiter, plus the
-// monitor-based memory accounting and the active OOM killer.
+// Maintenance thread of every GPU process in a vGPU container, and the container's
+// temporal-mode sampler.
 //
 // Reference: utilization_watcher@0x471a7 [multiprocess_utilization_watcher.c:195-216]
-// samples NVML per-process SM utilisation every 120 ms, sums it over the region's
-// host PIDs, refills the token bucket through delta(), and feeds
-// set_gpu_device_memory_monitor → active_oom_killer (SIGKILL every region process).
+// retries the host-PID lookup while it is unknown, samples NVML per-process SM
+// utilisation every 120 ms, sums it over the region's host PIDs, refills the token
+// bucket through delta(), and feeds set_gpu_device_memory_monitor → active_oom_killer
+// (SIGKILL every region process).
 //
-// MI355X: the signal is KFD's per-process cu_occupancy (CUs' worth of resident
-// waves), sampled several times per period and averaged; fallback is the device's
-// gpu_busy_percent. One process per region holds the watcher lease (watcher_pid +
-// heartbeat) so the container has a single controller and a single bucket. The OOM
-// killer terminates the largest consumer instead of every process.
+// MI355X: every process runs this thread for its own bookkeeping (host-PID discovery
+// retries, continuous context accounting from KFD's vram counter, live limit changes).
+// One process per region holds the sampler lease (watcher_pid + heartbeat) and does the
+// container-wide work: in temporal mode it samples KFD cu_occupancy of the container's
+// processes and of every other process on the GPU about every millisecond and turns it
+// into the GPU-time credit of ratelimit.h; every period it updates monitor-based usage
+// and runs the OOM killer, which terminates the largest consumer instead of every
+// process.
 #include <dirent.h>
 #include <pthread.h>
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "shim.h"
 #include "vgpu/kfd.h"
@@ -28,7 +34,8 @@ namespace vgpu {
 
 namespace {
 
-// Device-wide busy percent for KFD gpu_id via the topology's render minor.
+// Device-wide busy percent for KFD gpu_id via the topology's render minor (fallback
+// signal when none of the container's host PIDs is known yet).
 int device_busy_percent(uint32_t gpu_id) {
   static char cached_path[kMaxDevices][128];
   static uint32_t cached_id[kMaxDevices];
@@ -91,86 +98,159 @@ bool take_lease(Region* r, pid_t me) {
   return r->hdr.watcher_pid.compare_exchange_strong(cur, me);
 }
 
+bool any_temporal() {
+  ShimState& s = shim();
+  for (int i = 0; i < s.n_agents; i++)
+    if (s.agents[i].temporal_active.load(std::memory_order_relaxed)) return true;
+  return false;
+}
+
+// Occupancy sampler state (lease holder only).
+struct Sampler {
+  uint64_t last_ns = 0;
+  uint64_t others_at_ns = 0;
+  std::vector<int> mine;                  // host PIDs of the container's processes
+  int unknown = 0;                        // container processes whose host PID is unknown
+  std::vector<int> others[kMaxDevices];   // other processes on each GPU
+  int prev_pm[kMaxDevices] = {};          // charge fraction at the previous sample
+  bool opened[kMaxDevices] = {};          // the previous sample re-opened the gate
+};
+
+void collect_region_pids(Region* r, Sampler& sm) {
+  sm.mine.clear();
+  sm.unknown = 0;
+  for (int i = 0; i < kMaxProcs; i++) {
+    if (!r->procs[i].pid.load(std::memory_order_relaxed)) continue;
+    int32_t hp = r->procs[i].hostpid.load(std::memory_order_relaxed);
+    if (hp) sm.mine.push_back(hp);
+    else sm.unknown++;
+  }
+}
+
+void sample_tick(Region* r, Sampler& sm) {
+  ShimState& s = shim();
+  const uint64_t now = now_ns();
+  const int64_t dt = sm.last_ns ? (int64_t)std::min<uint64_t>(now - sm.last_ns, 1'000'000'000ull) : 0;
+  sm.last_ns = now;
+  collect_region_pids(r, sm);
+  const bool refresh = now - sm.others_at_ns > 100'000'000ull;
+  if (refresh) sm.others_at_ns = now;
+  for (int d = 0; d < s.n_agents; d++) {
+    AgentInfo& a = s.agents[d];
+    if (!a.temporal_active.load(std::memory_order_relaxed) || !a.gpu_id) continue;
+    DeviceState& ds = r->dev[d];
+    if (refresh) {
+      std::vector<int> on = kfd_pids_on_gpu(a.gpu_id);
+      sm.others[d].clear();
+      for (int p : on)
+        if (std::find(sm.mine.begin(), sm.mine.end(), p) == sm.mine.end()) sm.others[d].push_back(p);
+    }
+    int pm = 0;  // the container's share of the GPU at this instant, per mille
+    if (!sm.mine.empty()) {
+      int64_t mine = 0;
+      for (int hp : sm.mine) mine += std::max<int64_t>(0, kfd_cu_occupancy(hp, a.gpu_id));
+      int64_t total = mine;
+      // Split the instant with whoever else has waves resident on this GPU (other
+      // containers, unlimited processes): only read when the container is busy.
+      if (mine > 0)
+        for (int p : sm.others[d]) total += std::max<int64_t>(0, kfd_cu_occupancy(p, a.gpu_id));
+      pm = (int)timeshare_charge(1000, mine, total);
+    } else if (sm.unknown) {
+      // No host PID known yet: fall back to device-wide busy time (conservative).
+      int busy = device_busy_percent(a.gpu_id);
+      pm = busy > 0 ? std::min(busy, 100) * 10 : 0;
+    }
+    const int64_t charge = timeshare_interval(dt, sm.prev_pm[d], pm, sm.opened[d]);
+    const bool was_closed = !ds.gate_open.load(std::memory_order_relaxed);
+    timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, config().limiter_window_ms), dt, charge);
+    sm.opened[d] = was_closed && ds.gate_open.load(std::memory_order_relaxed);
+    sm.prev_pm[d] = pm;
+  }
+  r->hdr.samples.fetch_add(1, std::memory_order_relaxed);
+  r->hdr.watcher_heartbeat.store(now);
+}
+
+// Monitor-based usage (reference set_gpu_device_memory_monitor) and the active OOM killer.
+void monitor_tick(Region* r) {
+  ShimState& s = shim();
+  for (int d = 0; d < s.n_agents; d++) {
+    AgentInfo& a = s.agents[d];
+    DeviceState& ds = r->dev[d];
+    uint64_t mon = 0;
+    int32_t worst_pid = 0;
+    int64_t worst = -1;
+    for (int i = 0; i < kMaxProcs; i++) {
+      if (!r->procs[i].pid.load(std::memory_order_relaxed)) continue;
+      int32_t hp = r->procs[i].hostpid.load(std::memory_order_relaxed);
+      if (!hp || !a.gpu_id) continue;
+      int64_t v = kfd_vram_usage(hp, a.gpu_id);
+      if (v > 0) {
+        mon += (uint64_t)v;
+        if (v > worst) {
+          worst = v;
+          worst_pid = r->procs[i].pid.load();
+        }
+      }
+    }
+    ds.monitor_used.store(mon);
+    if ((r->hdr.flags & kFlagActiveOomKiller) && ds.mem_limit && mon > ds.mem_limit && worst_pid > 0) {
+      VLOG_ERROR("device %d: measured usage %lu exceeds limit %lu; killing largest consumer pid %d", d,
+                 (unsigned long)mon, (unsigned long)ds.mem_limit, worst_pid);
+      kill(worst_pid, SIGKILL);
+    }
+  }
+}
+
 void* watcher_main(void*) {
   ShimState& s = shim();
   Region* r = s.region.raw();
   const Config& cfg = config();
-  const int period_ms = cfg.util_period_ms;
-  const int samples = 6;
-  struct timespec tick = {0, (long)period_ms * 1000000L / samples};
-  pid_t me = getpid();
+  const pid_t me = getpid();
+  const uint64_t period_ns = (uint64_t)cfg.util_period_ms * 1'000'000ull;
+  Sampler sm;
+  uint64_t next_slow = 0;
+  int pid_attempts = 0;
+  unsigned rng = (unsigned)me * 2654435761u;
   while (!s.exiting.load() && s.pid == me) {
-    if (!take_lease(r, me)) {
-      struct timespec ts = {0, (long)period_ms * 1000000L};
-      nanosleep(&ts, nullptr);
-      continue;
+    const uint64_t now = now_ns();
+    const bool lease = take_lease(r, me);
+    const bool temporal = any_temporal();
+    if (lease && temporal) {
+      sample_tick(r, sm);
+    } else {
+      sm.last_ns = 0;
     }
-    int64_t occ_sum[kMaxDevices] = {0};
-    int occ_ok[kMaxDevices] = {0};
-    for (int k = 0; k < samples; k++) {
-      for (int d = 0; d < s.n_agents; d++) {
-        if (!s.agents[d].gpu_id) continue;
-        int64_t sum = 0;
-        bool any = false;
-        for (int i = 0; i < kMaxProcs; i++) {
-          if (!r->procs[i].pid.load(std::memory_order_relaxed)) continue;
-          int32_t hp = r->procs[i].hostpid.load(std::memory_order_relaxed);
-          if (!hp) continue;
-          int64_t v = kfd_cu_occupancy(hp, s.agents[d].gpu_id);
-          if (v >= 0) {
-            sum += v;
-            any = true;
-          }
-        }
-        if (any) {
-          occ_sum[d] += sum;
-          occ_ok[d]++;
+    if (now >= next_slow) {
+      next_slow = now + period_ns;
+      check_live_config();
+      // Host-PID retries: every period for the first ~10 s, then every ~5 s.
+      if (!s.hostpid && (pid_attempts < 80 || pid_attempts % 40 == 0)) {
+        pid_t hp = resolve_hostpid(50);
+        if (hp && s.slot >= 0) {
+          s.hostpid = hp;
+          r->procs[s.slot].hostpid.store(hp);
+          VLOG_INFO("host PID %d resolved by the maintenance thread after %d attempt(s)", (int)hp, pid_attempts + 1);
         }
       }
-      nanosleep(&tick, nullptr);
-    }
-    r->hdr.watcher_heartbeat.store(now_ns());
-    for (int d = 0; d < s.n_agents; d++) {
-      AgentInfo& a = s.agents[d];
-      DeviceState& ds = r->dev[d];
-      int util;
-      if (occ_ok[d]) {
-        int64_t avg = occ_sum[d] / occ_ok[d];
-        util = a.cu_count ? (int)(avg * 100 / a.cu_count) : 0;
-      } else {
-        util = device_busy_percent(a.gpu_id);
-        if (util < 0) util = 0;
-      }
-      if (util > 100) util = 100;
-      ds.util_pct.store(util);
-      if (a.temporal_active) {
-        LimiterSpec spec{a.cu_count, a.max_waves_per_cu * 64};
-        limiter_refill(ds, spec, ds.cu_limit_pct, util);
-      }
-      // Monitor-based usage (reference set_gpu_device_memory_monitor).
-      uint64_t mon = 0;
-      int32_t worst_pid = 0;
-      int64_t worst = -1;
-      for (int i = 0; i < kMaxProcs; i++) {
-        if (!r->procs[i].pid.load(std::memory_order_relaxed)) continue;
-        int32_t hp = r->procs[i].hostpid.load(std::memory_order_relaxed);
-        if (!hp || !a.gpu_id) continue;
-        int64_t v = kfd_vram_usage(hp, a.gpu_id);
-        if (v > 0) {
-          mon += (uint64_t)v;
-          if (v > worst) {
-            worst = v;
-            worst_pid = r->procs[i].pid.load();
-          }
-        }
-      }
-      ds.monitor_used.store(mon);
-      if ((r->hdr.flags & kFlagActiveOomKiller) && ds.mem_limit && mon > ds.mem_limit && worst_pid > 0) {
-        VLOG_ERROR("device %d: measured usage %lu exceeds limit %lu; killing largest consumer pid %d", d,
-                   (unsigned long)mon, (unsigned long)ds.mem_limit, worst_pid);
-        kill(worst_pid, SIGKILL);
+      if (!s.hostpid) pid_attempts++;
+      resync_context_charge();
+      if (lease) {
+        monitor_tick(r);
+        if (!temporal) r->hdr.watcher_heartbeat.store(now_ns());
       }
     }
+    // Sampling cadence with ±25 % jitter so the samples never phase-lock to the gate.
+    int64_t sleep_ns;
+    if (lease && temporal) {
+      rng = rng * 1103515245u + 12345u;
+      int64_t base = (int64_t)cfg.util_sample_us * 1000;
+      sleep_ns = base * 3 / 4 + (int64_t)((rng >> 8) % (uint32_t)(base / 2 + 1));
+    } else {
+      sleep_ns = (int64_t)std::min<uint64_t>(period_ns, next_slow > now_ns() ? next_slow - now_ns() : 0);
+      if (sleep_ns < 1'000'000) sleep_ns = 1'000'000;
+    }
+    struct timespec ts = {(time_t)(sleep_ns / 1000000000), (long)(sleep_ns % 1000000000)};
+    nanosleep(&ts, nullptr);
   }
   int32_t me32 = me;
   r->hdr.watcher_pid.compare_exchange_strong(me32, 0);
@@ -183,8 +263,7 @@ void start_watcher_if_needed() {
   ShimState& s = shim();
   if (!s.active) return;
   const Config& cfg = config();
-  bool need = cfg.active_oom_killer || cfg.memory_override;
-  for (int i = 0; i < s.n_agents; i++) need |= s.agents[i].temporal_active;
+  bool need = cfg.active_oom_killer || cfg.memory_override || cfg.any_memory_limit() || !s.hostpid || any_temporal();
   if (!need) return;
   bool expected = false;
   if (!s.watcher_started.compare_exchange_strong(expected, true)) return;
@@ -193,7 +272,7 @@ void start_watcher_if_needed() {
   pthread_attr_init(&attr);
   pthread_attr_setdetachstate(&attr, PTHREAD_CREATE_DETACHED);
   if (pthread_create(&th, &attr, watcher_main, nullptr) != 0) {
-    VLOG_ERROR("cannot start utilisation watcher");
+    VLOG_ERROR("cannot start the maintenance thread");
     s.watcher_started.store(false);
   }
   pthread_attr_destroy(&attr);

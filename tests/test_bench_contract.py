@@ -36,4 +36,5 @@ def test_bench_two_ranks_cpu_rehearsal():
         assert k in r, k
     assert r["n_gpus"] == 2 and r["steps"] == 2 and r["warmup"] == 1
     assert r["config"]["global_batch"] == 100 and r["config"]["model"] == "ResNet-V2-50"
-    assert "overhead_pct_vs_native" in r
+    assert "overhead_pct_quota_only" in r and "entitlement_ratio" in r and "parity_split2_mem1.8" in r
+    assert r["dtype"] == "fp32" and r["config"]["vgpu"]["cu_limit_pct"] == 25

@@ -61,13 +61,14 @@ def plugin(tmp_path):
 
 
 def test_slice_resnet50_in_allocated_vgpu(plugin):
-    """4-way split: quota = HBM/4 (72 GiB), kernels confined to 64 CUs, model runs."""
+    """4-way split: quota = HBM/4 (72 GiB), 25 % compute share enforced in time (auto mode:
+    masks serve at most two tenants per GPU), stock fp32 model runs."""
     code = CHILD_PRELUDE + """
 import torch
 from amdvgpu.models.aibench import Runner, get_case
 from amdvgpu.ops import cu_census
 free, total = torch.cuda.mem_get_info(0)
-r = Runner(get_case("resnet50-inf"), "cuda:0")
+r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False)
 for _ in range(3): r.step()
 torch.cuda.synchronize()
 t0 = time.time()
@@ -75,7 +76,8 @@ for _ in range(10): r.step()
 torch.cuda.synchronize()
 dt = (time.time() - t0) / 10
 ncu = len(cu_census(nblocks=8192, spin_us=300))
-emit(total=total, ms=dt * 1000, ips=50 / dt, ncu=ncu)
+from amdvgpu.shim.region import Region
+emit(total=total, ms=dt * 1000, ips=50 / dt, ncu=ncu, mode=Region(os.environ["VGPU_SHARED_CACHE"]).device(0)["cu_mode"])
 """
     import sys
     ids, envs, proc = run_pod(plugin, "amd.com/gpu", 1, [sys.executable, "-c", code], capture_output=True,
@@ -85,9 +87,10 @@ emit(total=total, ms=dt * 1000, ips=50 / dt, ncu=ncu)
     r = [json.loads(l[7:]) for l in proc.stdout.splitlines() if l.startswith("RESULT ")][0]
     quota = int(envs["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m")) * MiB
     assert r["total"] == quota and 70 * GiB <= quota <= 73 * GiB
-    assert r["ncu"] == 64
+    assert envs["VGPU_CU_MODE"] == "auto" and envs["VGPU_DEVICE_CU_LIMIT_0"] == "25"
+    assert r["ncu"] == 256 and r["mode"] == "temporal", r
     assert envs["VGPU_DEVICE_CU_RANGE_0"] in ("0-64", "64-128", "128-192", "192-256")
-    print(f"slice: ResNet-V2-50 b=50 inference in a 1/4 vGPU (64 CUs): {r['ips']:.1f} img/s")
+    print(f"slice: ResNet-V2-50 b=50 fp32 inference in a 1/4 vGPU (25 % GPU time): {r['ips']:.1f} img/s")
 
 
 def test_oversubscription_spills_past_hbm_share(tmp_region):
