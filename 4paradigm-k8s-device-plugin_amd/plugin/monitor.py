@@ -17,6 +17,8 @@ That monitor is not part of the reference; this is the in-tree one.
     python -m amdvgpu.plugin.monitor --root /usr/local/vgpu/shared --port 9394
 """
 import argparse
+import hmac
+import ipaddress
 import glob
 import json
 import logging
@@ -144,7 +146,13 @@ def control(root, tag, action, params):
     return done
 
 
-def make_handler(root):
+def make_handler(root, control_enabled=False, token=None):
+    """HTTP handler. The metrics side (GET /metrics, /regions, /healthz) is read-only and
+    meant for Prometheus on the pod IP. The control side (POST /regions/<tag>/<action>)
+    changes tenants' quotas, CU shares and run state, so it is only served by a handler
+    built with ``control_enabled`` (the control server, loopback by default) and, when a
+    ``token`` is configured, only to requests carrying ``Authorization: Bearer <token>``."""
+
     class Handler(BaseHTTPRequestHandler):
         def _send(self, code, body, ctype="text/plain; version=0.0.4"):
             data = body.encode()
@@ -174,6 +182,12 @@ def make_handler(root):
             return self._send(404, "not found\n")
 
         def do_POST(self):
+            if not control_enabled:
+                return self._send(403, "control endpoints are served on the control address only\n")
+            if token is not None:
+                got = self.headers.get("Authorization", "")
+                if not hmac.compare_digest(got.encode(), f"Bearer {token}".encode()):
+                    return self._send(401, "unauthorized\n")
             u = urllib.parse.urlparse(self.path)
             parts = u.path.strip("/").split("/")
             if len(parts) != 3 or parts[0] != "regions":
@@ -185,6 +199,7 @@ def make_handler(root):
                 return self._send(404, "unknown container\n")
             except (ValueError, TypeError) as e:
                 return self._send(400, f"bad request: {e}\n")
+            log.info("control %s %s %s by %s", parts[1], parts[2], params, self.client_address[0])
             return self._send(200, json.dumps({"regions": n}), "application/json")
 
         def log_message(self, fmt, *args):
@@ -193,8 +208,18 @@ def make_handler(root):
     return Handler
 
 
-def serve(root, host="0.0.0.0", port=9394):
-    srv = ThreadingHTTPServer((host, port), make_handler(root))
+def _is_loopback(host):
+    try:
+        return ipaddress.ip_address(host).is_loopback
+    except ValueError:
+        return host == "localhost"
+
+
+def serve(root, host="0.0.0.0", port=9394, control_enabled=False, token=None):
+    """Starts a server thread. A control server on a non-loopback address needs a token."""
+    if control_enabled and token is None and not _is_loopback(host):
+        raise ValueError("the control server listens beyond loopback only with a token (--control-token-file)")
+    srv = ThreadingHTTPServer((host, port), make_handler(root, control_enabled, token))
     th = threading.Thread(target=srv.serve_forever, daemon=True)
     th.start()
     return srv
@@ -203,9 +228,18 @@ def serve(root, host="0.0.0.0", port=9394):
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--root", default="/usr/local/vgpu/shared")
-    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--host", default="0.0.0.0", help="metrics address (read-only endpoints)")
     ap.add_argument("--port", type=int, default=9394)
+    ap.add_argument("--enable-control", action="store_true",
+                    help="serve the mutating control endpoints (off by default)")
+    ap.add_argument("--control-host", default="127.0.0.1", help="control address (loopback unless a token is set)")
+    ap.add_argument("--control-port", type=int, default=9395)
+    ap.add_argument("--control-token-file", default=None, help="file holding the bearer token for control calls")
     a = ap.parse_args(argv)
+    token = open(a.control_token_file).read().strip() if a.control_token_file else None
+    if a.enable_control:
+        serve(a.root, a.control_host, a.control_port, control_enabled=True, token=token)
+        log.info("control endpoints on %s:%d%s", a.control_host, a.control_port, " (token)" if token else "")
     srv = ThreadingHTTPServer((a.host, a.port), make_handler(a.root))
     srv.serve_forever()
 

@@ -137,3 +137,53 @@ def test_monitor_pod_matcher():
     assert m.match([1]) == ["new_main"]
     with pytest.raises(LookupError):
         m.match([2])
+
+
+def _legacy_server(tmp_path, split=2):
+    from amdvgpu.plugin.server import AllocationError, DevicePluginServer
+    cfg = PluginConfig(device_plugin_path=str(tmp_path) + "/", device_split_count=split,
+                       enable_legacy_preferred=True, vgpu_dir=str(tmp_path / "vgpu")).validate()
+    devs = FakeBackend(n=1).devices()
+    ids = [f"{devs[0].uuid}-{i}" for i in range(split)]
+    srv = DevicePluginServer(cfg, "amd.com/gpu", "amd-gpu.sock", devs,
+                             legacy=LegacyController(ids, "amd.com/gpu", str(tmp_path)))
+    srv.initialize()
+    return srv, ids, AllocationError
+
+
+def _alloc_req(ids):
+    return api.AllocateRequest(container_requests=[api.ContainerAllocateRequest(devicesIDs=ids)])
+
+
+def test_legacy_allocate_refuses_when_pool_exhausted(tmp_path):
+    """Reference server.go:436-439 ("no enough devices"): when the legacy pool has fewer
+    free vGPUs than requested, Allocate fails instead of reusing the kubelet's IDs (which
+    may belong to another container) or handing out fewer GPUs than asked for."""
+    srv, ids, AllocationError = _legacy_server(tmp_path, split=3)
+    _checkpoint(tmp_path, [])
+    r1 = srv.Allocate(_alloc_req([ids[0]]), None)
+    r2 = srv.Allocate(_alloc_req([ids[1]]), None)
+    used = [dict(r.container_responses[0].annotations)[ANN_USING] for r in (r1, r2)]
+    assert len(set(used)) == 2                       # no double booking
+    # Live pods in the checkpoint hold every vGPU under other request IDs: a request for a
+    # vGPU the kubelet believes free must be refused, not served with its own (taken) ID.
+    entries = [{"PodUID": f"p{i}", "ContainerName": "c", "ResourceName": "amd.com/gpu", "DeviceIDs": [f"x-{i}"],
+                "AllocResp": _alloc_resp([f"x-{i}"], [v])} for i, v in enumerate(ids)]
+    _checkpoint(tmp_path, entries)
+    srv2, ids2, _ = _legacy_server(tmp_path, split=3)
+    srv2.legacy.pod_lister = lambda: [{"uid": f"p{i}", "phase": "Running"} for i in range(3)]
+    with pytest.raises(AllocationError):
+        srv2.Allocate(_alloc_req([ids2[0]]), None)
+    # One of them ends: one vGPU free, two requested -> refused, never a short allocation.
+    srv2.legacy.pod_lister = lambda: [{"uid": f"p{i}", "phase": "Running" if i else "Succeeded"} for i in range(3)]
+    with pytest.raises(AllocationError):
+        srv2.Allocate(_alloc_req(ids2[:2]), None)
+    r = srv2.Allocate(_alloc_req([ids2[1]]), None)
+    assert dict(r.container_responses[0].annotations)[ANN_USING] == ids2[0]
+
+
+def test_legacy_allocate_refuses_without_checkpoint(tmp_path):
+    """Reference server.go:410-412: an unreadable checkpoint fails the allocation."""
+    srv, ids, AllocationError = _legacy_server(tmp_path)
+    with pytest.raises(AllocationError):
+        srv.Allocate(_alloc_req([ids[0]]), None)

@@ -2,7 +2,10 @@
 admission path the shim uses)."""
 import json
 import os
+import urllib.error
 import urllib.request
+
+import pytest
 
 from amdvgpu.plugin.monitor import control, discover, render_metrics, serve
 from amdvgpu.shim.region import Region
@@ -47,15 +50,41 @@ def test_http_endpoints(tmp_path):
     root = str(tmp_path)
     r, slot = make_region(root, "pod2_c")
     srv = serve(root, "127.0.0.1", 0)
-    port = srv.server_address[1]
+    ctl = serve(root, "127.0.0.1", 0, control_enabled=True)
+    port, cport = srv.server_address[1], ctl.server_address[1]
     try:
         body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics").read().decode()
         assert "vgpu_container_processes" in body
         snap = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{port}/regions").read())
         assert snap["pod2_c"][0]["devices"][0]["used"] == 3 << 30
+        # the metrics server never mutates a tenant
         req = urllib.request.Request(f"http://127.0.0.1:{port}/regions/pod2_c/suspend", method="POST", data=b"")
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(req)
+        assert e.value.code == 403 and not r.suspended
+        req = urllib.request.Request(f"http://127.0.0.1:{cport}/regions/pod2_c/suspend", method="POST", data=b"")
         assert json.loads(urllib.request.urlopen(req).read())["regions"] == 1
         assert r.suspended
     finally:
         srv.shutdown()
+        ctl.shutdown()
+        r.close()
+
+
+def test_control_token_and_bind_policy(tmp_path):
+    root = str(tmp_path)
+    r, slot = make_region(root, "pod3_c")
+    with pytest.raises(ValueError):
+        serve(root, "0.0.0.0", 0, control_enabled=True)          # beyond loopback without a token
+    ctl = serve(root, "127.0.0.1", 0, control_enabled=True, token="s3cret")
+    url = f"http://127.0.0.1:{ctl.server_address[1]}/regions/pod3_c/block"
+    try:
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(urllib.request.Request(url, method="POST", data=b""))
+        assert e.value.code == 401 and r.recent_kernel >= 0
+        req = urllib.request.Request(url, method="POST", data=b"", headers={"Authorization": "Bearer s3cret"})
+        assert json.loads(urllib.request.urlopen(req).read())["regions"] == 1
+        assert r.recent_kernel < 0
+    finally:
+        ctl.shutdown()
         r.close()

@@ -41,7 +41,9 @@ def _worker(path, seed, hold_event, stop_event, over_flag):
 def test_concurrent_quota_with_kills(region_path):
     r = Region(region_path, create=True)
     r.set_memory_limit(0, LIMIT)
-    ctx = mp.get_context("fork")
+    # spawn, not fork: the pytest process runs gRPC servers in other tests, and forking a
+    # process with live gRPC threads can deadlock the child in gRPC's atfork handlers.
+    ctx = mp.get_context("spawn")
     stop, hold = ctx.Event(), ctx.Event()
     over = ctx.Value("i", 0)
     procs = [ctx.Process(target=_worker, args=(region_path, i, hold, stop, over)) for i in range(12)]
