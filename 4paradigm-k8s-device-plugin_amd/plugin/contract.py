@@ -130,6 +130,11 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
                 resp.envs[f"VGPU_DEVICE_CU_RANGE_{i}"] = f"{v.cu_range[0]}-{v.cu_range[1]}"
         dmap.append(f"{i}:{v.uuid}")
     resp.envs["VGPU_DEVICE_MAP"] = " ".join(dmap)
+    # PCI addresses of the container's GPUs: in-container amd-smi lists only these
+    # (reference: nvmlDeviceGetCount / GetHandleByIndex remapping, nvml/hook.c:438-527).
+    bdfs = [devices_by_uuid[u].bdf for u in uuids if u in devices_by_uuid and devices_by_uuid[u].bdf]
+    if bdfs:
+        resp.envs["VGPU_DEVICE_BDFS"] = ",".join(bdfs)
     # Always explicit, so a container never depends on the shim's built-in default.
     resp.envs["VGPU_CU_MODE"] = cfg.cu_mode
 

@@ -1,24 +1,37 @@
 #!/usr/bin/env python3
-"""The reference's ten ai-benchmark cases, native vs inside a vGPU, on one MI355X.
+"""The reference's ten ai-benchmark cases on one MI355X: native, inside a vGPU, and two
+concurrent vGPUs (the "virtual device memory" column), with repeat statistics.
 
-Reference numbers: BASELINE.md (2xV100, TF 2.4.1; native = official plugin, vGPU = split
-2 / memScaling 1.8 with the temporal SM limit). Columns measured here:
+Reference (2xV100, TF 2.4.1): native = official plugin; vGPU = this plugin
+with split 2 / memScaling 1.8 (50 % SM limit + CUDA_OVERSUBSCRIBE, server.go:492,505-507);
+vGPU+VDM = 4 such containers on the 2 GPUs at once ("high load", README_cn.md:52).
 
-* native        no shim
-* vgpu          1 vGPU of a 2-way split: quota = HBM/2, no CU limit (the interception
-                overhead the reference's "vGPU" column measures)
-* vgpu-cu50     same, plus a 50 % spatial CU mask (128 of 256 CUs) — what a tenant of a
-                2-way split with --device-cores-scaling=1 gets
-* vgpu-t50      same share enforced temporally (reference-parity token bucket)
+Every vGPU contract here comes from a real Allocate of the plugin (NodeHarness, sysfs
+backend) configured like the reference's benchmark DaemonSet: --device-split-count=2
+--device-memory-scaling=1.8 (default --cu-mode=auto → a 50 % spatial CU mask). The
+workloads are stock PyTorch-ROCm in fp32 (MIOpen / hipBLASLt kernels, no custom ops).
 
-One worker process per column runs every case (warmup W, then K timed steps bracketed by
-synchronize). Output: JSON + a markdown table with ms/batch, throughput and overhead.
+Columns:
+* native     no shim, the GPU visible as the official plugin would expose it
+* vgpu       the pod's contract with the compute limit disabled (VGPU_CU_POLICY=disable):
+             the interception overhead alone — what the reference's vGPU column measured,
+             whose 50 % SM limit did not bind (its vGPU numbers match native)
+* vgpu-cu50  the contract exactly as emitted: 259 GiB oversubscribed quota (144 GiB of it
+             HBM-resident), 128 of 256 CUs
+* vdm        two pods of that plugin on one GPU running the same case concurrently
+             (aggregate throughput; one GPU here, so 2 pods = the reference's 4 on 2 GPUs)
 
-    python benchmarks/aibench_suite.py [--cases all] [--modes native,vgpu,vgpu-cu50] [--steps 20]
+Statistics: --repeats R runs of native / vgpu / vgpu-cu50 in alternating (ABBA) order;
+per case the overhead is the median over repeats of the paired ms/batch ratio, with a
+95 % confidence interval (t-interval on the paired log-ratios).
+
+    python benchmarks/aibench_suite.py [--cases all] [--repeats 5] [--steps 10] [--json-out F] [--md-out F]
 """
 import argparse
 import json
+import math
 import os
+import statistics
 import subprocess
 import sys
 import tempfile
@@ -26,130 +39,152 @@ import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-HBM = 309220868096
 
-MODES = {
-    "native": None,
-    "vgpu": dict(mem_limit=HBM // 2),
-    "vgpu-cu50": dict(mem_limit=HBM // 2, cu_limit=50),
-    "vgpu-t50": dict(mem_limit=HBM // 2, cu_limit=50, cu_mode="temporal"),
-    # every step replayed from a captured HIP graph (forward, or forward+backward+optimizer)
-    "vgpu-graph": dict(mem_limit=HBM // 2, extra={"VGPU_BENCH_GRAPH": "1"}),
-    "native-graph": {"extra": {"VGPU_BENCH_GRAPH": "1"}, "native": True},
-    # diagnostics: launch hooks as pure pass-throughs / per-hook call counters
-    "vgpu-nolaunch": dict(mem_limit=HBM // 2, extra={"VGPU_HOOK_LAUNCH": "0"}),
-    "vgpu-stats": dict(mem_limit=HBM // 2, extra={"VGPU_STATS": "1"}),
-}
+T95 = {1: 12.71, 2: 4.30, 3: 3.18, 4: 2.78, 5: 2.57, 6: 2.45, 7: 2.36, 8: 2.31, 9: 2.26, 10: 2.23}
 
 
-def worker(cases, steps, warmup, out):
+def worker(cases, steps, warmup, out, seconds=0.0, sync_dir=None, tag="0", peers=1):
     import torch
     from amdvgpu.models.aibench import Runner, get_case
-    torch.backends.cudnn.benchmark = os.environ.get("VGPU_BENCH_TUNE", "1") == "1"  # MIOpen find mode
+    torch.backends.cudnn.benchmark = True  # MIOpen find mode (TF autotunes too)
     res = {}
     for name in cases:
         case = get_case(name)
-        r = Runner(case, "cuda:0")
+        r = Runner(case, "cuda:0", dtype=torch.float32, fuse=False)
         for _ in range(warmup):
             r.step()
-        method = "eager"
-        if os.environ.get("VGPU_BENCH_GRAPH") == "1":
-            try:
-                r.capture()
-                method = "graph"
-            except Exception as e:  # recorded: the case is then measured eagerly
-                print(f"  {name}: graph capture failed ({type(e).__name__}: {str(e)[:120]}); eager", flush=True)
-                torch.cuda.synchronize()
-                r = Runner(case, "cuda:0")
-                for _ in range(warmup):
-                    r.step()
         torch.cuda.synchronize()
+        if sync_dir:  # concurrent pods: every pod ready on this case, then go together
+            open(os.path.join(sync_dir, f"{name}.{tag}"), "w").close()
+            while len([f for f in os.listdir(sync_dir) if f.startswith(name + ".")]) < peers:
+                time.sleep(0.002)
+        n = 0
         t0 = time.perf_counter()
-        for _ in range(steps):
+        while (n < steps) if not seconds else (time.perf_counter() - t0 < seconds):
             r.step()
+            n += 1
+            if seconds and n % 4 == 0:
+                torch.cuda.synchronize()
         torch.cuda.synchronize()
-        ms = (time.perf_counter() - t0) * 1000 / steps
-        res[name] = {"ms_per_batch": ms, "throughput": case.batch * 1000 / ms, "batch": case.batch, "method": method}
-        print(f"  {name}: {ms:.3f} ms/batch, {case.batch * 1000 / ms:.1f} {case.unit}", flush=True)
+        dt = time.perf_counter() - t0
+        res[name] = {"ms_per_batch": dt * 1000 / n, "throughput": case.batch * n / dt, "batch": case.batch,
+                     "steps": n}
+        print(f"  [{tag}] {name}: {dt * 1000 / n:.3f} ms/batch", flush=True)
         del r
         torch.cuda.empty_cache()
     with open(out, "w") as f:
         json.dump(res, f)
 
 
-def run_mode(mode, cases, steps, warmup):
-    from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
+def _cmd(cases, steps, warmup, out, extra=()):
+    return [sys.executable, os.path.abspath(__file__), "--worker", "--cases", ",".join(cases), "--steps", str(steps),
+            "--warmup", str(warmup), "--out", out, *extra]
+
+
+def run_mode(mode, node, uuid, cases, steps, warmup):
+    from amdvgpu.shim.launcher import apply_contract
     fd, out = tempfile.mkstemp(suffix=".json")
     os.close(fd)
-    spec = dict(MODES[mode] or {})
-    native = spec.pop("native", False) or not MODES[mode]
-    if native:
-        contract = {}
-        env = dict(os.environ, **spec.get("extra", {}))
+    if mode == "native":
+        env = dict(os.environ, ROCR_VISIBLE_DEVICES=uuid)
     else:
-        contract = vgpu_env(**spec)
-        env = apply_contract(contract)
-    cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--cases", ",".join(cases), "--steps", str(steps),
-           "--warmup", str(warmup), "--out", out]
+        envs, mounts = node.pod(node.vgpu_ids(uuid)[:1])
+        env = apply_contract(envs, mounts)
+        if mode == "vgpu":
+            env["VGPU_CU_POLICY"] = "disable"
     print(f"[{mode}]", flush=True)
     try:
-        rc = subprocess.call(cmd, env=env)
-        if rc:
-            raise SystemExit(f"{mode} worker failed ({rc})")
+        if subprocess.call(_cmd(cases, steps, warmup, out), env=env):
+            raise SystemExit(f"{mode} worker failed")
         return json.load(open(out))
     finally:
         os.unlink(out)
-        cleanup_region(contract)
 
 
-def _pair(modes):
-    """(native mode, vGPU mode) to compare: plain or graph-replayed."""
-    for nat, vg in (("native", "vgpu"), ("native-graph", "vgpu-graph")):
-        if nat in modes and vg in modes:
-            return nat, vg
-    return None, None
+def run_vdm(node, uuid, cases, warmup, seconds, pods=2):
+    from amdvgpu.shim.launcher import apply_contract
+    sync = tempfile.mkdtemp(prefix="vdm-")
+    procs, outs = [], []
+    for i, vid in enumerate(node.vgpu_ids(uuid)[:pods]):
+        envs, mounts = node.pod([vid])
+        out = os.path.join(sync, f"res{i}.json")
+        procs.append(subprocess.Popen(_cmd(cases, 0, warmup, out, ["--seconds", str(seconds), "--sync-dir", sync,
+                                                                   "--tag", str(i), "--peers", str(pods)]),
+                                      env=apply_contract(envs, mounts)))
+        outs.append(out)
+    print(f"[vdm x{pods}]", flush=True)
+    for p in procs:
+        if p.wait(timeout=3600):
+            raise SystemExit("vdm pod failed")
+    per = [json.load(open(o)) for o in outs]
+    return {c: {"throughput": sum(p[c]["throughput"] for p in per), "per_pod": [p[c]["throughput"] for p in per]}
+            for c in cases}
 
 
-def table(results, modes):
-    from amdvgpu.models.aibench import CASES
-    nat_m, vg_m = _pair(modes)
-    lines = ["| test | case | batch | " + " | ".join(f"{m} ms/batch" for m in modes) +
-             f" | {vg_m or 'vgpu'} overhead | reference vGPU overhead (V100) | throughput | V100 vGPU throughput | x |",
-             "|" + "---|" * (8 + len(modes))]
-    ovs = []
-    for c in CASES:
-        if c.name not in results[modes[0]]:
-            continue
-        row = [c.test_id, c.name, str(c.batch)] + [f"{results[m][c.name]['ms_per_batch']:.2f}" for m in modes]
-        ov = ""
-        if nat_m:
-            n, v = results[nat_m][c.name]["ms_per_batch"], results[vg_m][c.name]["ms_per_batch"]
-            ovs.append((v - n) / n * 100)
-            ov = f"{ovs[-1]:+.2f} %"
+def ci_ratio(nat, vg):
+    """Median paired ratio and 95 % CI (t-interval on log-ratios), as overhead percents."""
+    lr = [math.log(v / n) for n, v in zip(nat, vg)]
+    med = (math.exp(statistics.median(lr)) - 1) * 100
+    if len(lr) < 2:
+        return med, med, med
+    m, sd = statistics.mean(lr), statistics.stdev(lr)
+    h = T95.get(len(lr) - 1, 2.0) * sd / math.sqrt(len(lr))
+    return med, (math.exp(m - h) - 1) * 100, (math.exp(m + h) - 1) * 100
+
+
+def table(runs, vdm, cases):
+    from amdvgpu.models.aibench import get_case
+    lines = ["| test | case | batch | native ms/batch | vgpu ms/batch | vgpu overhead (median, 95 % CI) | "
+             "reference vGPU overhead | vgpu-cu50 ms/batch | vdm (2 pods) throughput | V100 vGPU / vGPU+VDM |",
+             "|---|---|---|---|---|---|---|---|---|---|"]
+    summary = []
+    for name in cases:
+        c = get_case(name)
+        nat = [r["native"][name]["ms_per_batch"] for r in runs]
+        vg = [r["vgpu"][name]["ms_per_batch"] for r in runs]
+        cu = [r["vgpu-cu50"][name]["ms_per_batch"] for r in runs if "vgpu-cu50" in r]
+        med, lo, hi = ci_ratio(nat, vg)
         ref = (c.baseline_native / c.baseline_vgpu - 1) * 100
-        tp = results.get(vg_m or "vgpu", results[modes[-1]])[c.name]["throughput"]
-        row += [ov, f"{ref:+.1f} %", f"{tp:.1f} {c.unit}", f"{c.baseline_vgpu}", f"{tp / c.baseline_vgpu:.1f}"]
-        lines.append("| " + " | ".join(row) + " |")
+        summary.append({"case": name, "test": c.test_id, "native_ms": statistics.median(nat),
+                        "vgpu_ms": statistics.median(vg), "overhead_pct": med, "ci95": [lo, hi],
+                        "reference_overhead_pct": ref, "vgpu_cu50_ms": statistics.median(cu) if cu else None,
+                        "vdm_throughput": vdm.get(name, {}).get("throughput") if vdm else None,
+                        "repeats": len(nat)})
+        vdm_s = f"{vdm[name]['throughput']:.1f} {c.unit}" if vdm and name in vdm else "-"
+        cu_s = f"{statistics.median(cu):.2f}" if cu else "-"
+        lines.append(f"| {c.test_id} | {name} | {c.batch} | {statistics.median(nat):.2f} | {statistics.median(vg):.2f} | "
+                     f"{med:+.2f} % [{lo:+.2f}, {hi:+.2f}] | {ref:+.1f} % | {cu_s} | {vdm_s} | "
+                     f"{c.baseline_vgpu} / {vdm_baseline(c)} |")
+    ovs = sorted(s["overhead_pct"] for s in summary)
     if ovs:
-        s = sorted(ovs)
-        med = s[len(s) // 2] if len(s) % 2 else (s[len(s) // 2 - 1] + s[len(s) // 2]) / 2
-        lines.append("")
-        lines.append(f"vGPU overhead ({vg_m} vs {nat_m}): median {med:+.2f} %, range {min(ovs):+.2f} % .. "
-                     f"{max(ovs):+.2f} % (reference: median +2.5 %, range -3.8 % .. +17.7 %)")
-    return "\n".join(lines)
+        lines += ["", f"vGPU interception overhead over {len(runs)} ABBA repeats: median "
+                      f"{statistics.median(ovs):+.2f} %, range {ovs[0]:+.2f} % .. {ovs[-1]:+.2f} % "
+                      "(reference: median +2.5 %, range -3.8 % .. +17.7 %)"]
+    return "\n".join(lines), summary
+
+
+VDM_V100 = {"1.1": 207.9, "1.2": 79.84, "2.1": 211.3, "2.2": 45.14, "3.1": 179.77, "3.2": 14.87, "4.1": 11.1,
+            "4.2": 7.69, "5.1": 23.02, "5.2": 6.95}
+
+
+def vdm_baseline(c):
+    return VDM_V100.get(c.test_id, "-")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default="all")
     ap.add_argument("--modes", default="native,vgpu,vgpu-cu50")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--repeats", type=int, default=1,
-                    help="run the modes this many times in alternating order; keep each mode's best")
+    ap.add_argument("--repeats", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--vdm", type=int, default=1, help="also run the two-pod virtual-device-memory column")
+    ap.add_argument("--vdm-seconds", type=float, default=3.0)
     ap.add_argument("--worker", action="store_true")
-    ap.add_argument("--in-process", action="store_true",
-                    help="run every case in this process (inside a pod whose shim is already preloaded)")
+    ap.add_argument("--seconds", type=float, default=0.0)
+    ap.add_argument("--sync-dir", default=None)
+    ap.add_argument("--tag", default="0")
+    ap.add_argument("--peers", type=int, default=1)
     ap.add_argument("--out", default=None)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--md-out", default=None)
@@ -157,26 +192,24 @@ def main():
     from amdvgpu.models.aibench import CASES
     cases = [c.name for c in CASES] if a.cases == "all" else a.cases.split(",")
     if a.worker:
-        return worker(cases, a.steps, a.warmup, a.out)
-    if a.in_process:
-        out = a.json_out or os.path.join(tempfile.gettempdir(), "aibench.json")
-        return worker(cases, a.steps, a.warmup, out)
+        return worker(cases, a.steps, a.warmup, a.out, a.seconds, a.sync_dir, a.tag, a.peers)
+    from amdvgpu.plugin.devices import SysfsBackend
+    from amdvgpu.plugin.kubelet_stub import NodeHarness
+    backend = SysfsBackend()
+    uuid = backend.devices()[0].uuid
     modes = a.modes.split(",")
-    results = {}
-    for rep in range(a.repeats):
-        order = modes if rep % 2 == 0 else modes[::-1]  # ABBA: cancels drift between runs
-        for m in order:
-            r = run_mode(m, cases, a.steps, a.warmup)
-            if m not in results:
-                results[m] = r
-            else:
-                for k, v in r.items():
-                    if v["ms_per_batch"] < results[m][k]["ms_per_batch"]:
-                        results[m][k] = v
-    md = table(results, modes)
+    runs, vdm = [], {}
+    with NodeHarness(backend, device_split_count=2, device_memory_scaling=1.8) as node:
+        for rep in range(a.repeats):
+            order = modes if rep % 2 == 0 else modes[::-1]  # ABBA: cancels drift between runs
+            runs.append({m: run_mode(m, node, uuid, cases, a.steps, a.warmup) for m in order})
+        if a.vdm:
+            vdm = run_vdm(node, uuid, cases, a.warmup, a.vdm_seconds)
+    md, summary = table(runs, vdm, cases)
     print(md)
     if a.json_out:
-        json.dump({"steps": a.steps, "warmup": a.warmup, "results": results}, open(a.json_out, "w"), indent=1)
+        json.dump({"steps": a.steps, "warmup": a.warmup, "repeats": a.repeats, "summary": summary, "runs": runs,
+                   "vdm": vdm}, open(a.json_out, "w"), indent=1)
     if a.md_out:
         open(a.md_out, "w").write(md + "\n")
 

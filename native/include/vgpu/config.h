@@ -35,6 +35,12 @@ constexpr int kAutoSpatialMinPct = 50;
 // The mode a device actually uses for share `pct` under configured mode `m`.
 CuMode effective_cu_mode(CuMode m, int pct);
 
+// Where oversubscribed allocations live (VGPU_SPILL_POLICY).
+enum class SpillPolicy : int {
+  kFirstCome = 0,   // HBM until the tenant's HBM share is used up, then host memory
+  kLargeFirst = 1,  // large allocations spill first; a reserve of the share stays for small ones
+};
+
 // GPU_CORE_UTILIZATION_POLICY analogue.
 enum class CuPolicy : int { kDefault = 0, kForce = 1, kDisable = 2 };
 
@@ -45,6 +51,7 @@ struct DeviceConfig {
   int cu_range_begin = -1;     // explicit logical CU range [begin, end) or -1 = derive
   int cu_range_end = -1;
   char uuid[64] = {0};         // physical UUID from VGPU_DEVICE_MAP (may be empty)
+  bool unmapped = false;       // agent absent from a non-empty VGPU_DEVICE_MAP: not this container's
 };
 
 struct Config {
@@ -53,6 +60,9 @@ struct Config {
   DeviceConfig dev[kMaxDevices];
   std::string shared_cache = "/tmp/vgpushr.cache";
   bool oversubscribe = false;            // VGPU_OVERSUBSCRIBE
+  SpillPolicy spill_policy = SpillPolicy::kLargeFirst;  // VGPU_SPILL_POLICY
+  uint64_t spill_large_bytes = 256ull << 20;  // VGPU_SPILL_LARGE: "large" allocation threshold
+  uint64_t spill_reserve_bytes = 0;      // VGPU_SPILL_RESERVE: HBM kept for small ones (0 = auto)
   int priority = 1;                      // VGPU_TASK_PRIORITY
   CuMode cu_mode = CuMode::kAuto;        // VGPU_CU_MODE
   CuPolicy cu_policy = CuPolicy::kDefault;
@@ -69,6 +79,10 @@ struct Config {
   bool any_memory_limit() const;
   bool any_cu_limit() const;
 };
+
+// HBM reserve for small allocations under large-first spilling: the configured value, or
+// max(min(2 GiB, hbm_share / 4), hbm_share / 16) — 18 GiB of a 288 GiB share, 512 MiB of 2 GiB.
+uint64_t spill_reserve(const Config& cfg, uint64_t hbm_share);
 
 // Parses "NNN[KkMmGg][iB|B]" into bytes. Returns false on syntax error or overflow.
 // Bare numbers are bytes; "m"/"M" is MiB, as in the reference ("<MiB>m").

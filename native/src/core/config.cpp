@@ -1,6 +1,7 @@
 // Env contract parser (see vgpu/config.h for the reference mapping).
 #include "vgpu/config.h"
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -40,6 +41,12 @@ CuMode effective_cu_mode(CuMode m, int pct) {
   if (m != CuMode::kAuto) return m;
   if (pct <= 0 || pct >= 100) return CuMode::kSpatial;  // unlimited: no mask is applied anyway
   return pct >= kAutoSpatialMinPct ? CuMode::kSpatial : CuMode::kTemporal;
+}
+
+uint64_t spill_reserve(const Config& cfg, uint64_t hbm_share) {
+  if (cfg.spill_reserve_bytes) return cfg.spill_reserve_bytes;
+  const uint64_t floor = std::min<uint64_t>(2ull << 30, hbm_share / 4);
+  return std::max<uint64_t>(floor, hbm_share / 16);
 }
 
 bool Config::any_memory_limit() const {
@@ -219,6 +226,17 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
     if (*s) cfg->shared_cache = s;
   }
   cfg->oversubscribe = parse_bool(getenv_fn("VGPU_OVERSUBSCRIBE"), false);
+  if (const char* s = getenv_fn("VGPU_SPILL_POLICY")) {
+    if (!strcasecmp(s, "first-come") || !strcasecmp(s, "fifo")) cfg->spill_policy = SpillPolicy::kFirstCome;
+    else if (!strcasecmp(s, "large-first")) cfg->spill_policy = SpillPolicy::kLargeFirst;
+    else VLOG_WARN("invalid VGPU_SPILL_POLICY=%s, using large-first", s);
+  }
+  if (const char* s = getenv_fn("VGPU_SPILL_LARGE")) {
+    if (!parse_size(s, &cfg->spill_large_bytes)) VLOG_WARN("invalid VGPU_SPILL_LARGE=%s ignored", s);
+  }
+  if (const char* s = getenv_fn("VGPU_SPILL_RESERVE")) {
+    if (!parse_size(s, &cfg->spill_reserve_bytes)) VLOG_WARN("invalid VGPU_SPILL_RESERVE=%s ignored", s);
+  }
   long prio = 1;
   if (parse_int(getenv_fn("VGPU_TASK_PRIORITY"), -1000, 1000, &prio)) cfg->priority = (int)prio;
 

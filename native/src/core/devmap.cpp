@@ -97,7 +97,10 @@ int resolve_devices(const Config& cfg, const DeviceMap& map, const char* const* 
         }
       }
     }
-    if (!matched) out[k] = cfg.dev[k];  // positional fallback
+    // No map: positional. With a map, an agent it does not name is not one of the
+    // container's vGPUs (only reachable if visibility was widened inside the container).
+    if (!matched && map.n == 0) out[k] = cfg.dev[k];
+    if (!matched && map.n > 0) out[k].unmapped = true;
     if (agent_uuids && agent_uuids[k]) snprintf(out[k].uuid, sizeof(out[k].uuid), "%s", agent_uuids[k]);
   }
   return n_agents;

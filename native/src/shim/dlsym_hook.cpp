@@ -26,6 +26,8 @@ extern "C" {
 amdsmi_status_t amdsmi_get_gpu_memory_total(amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*);
 amdsmi_status_t amdsmi_get_gpu_memory_usage(amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*);
 amdsmi_status_t amdsmi_get_gpu_vram_usage(amdsmi_processor_handle, amdsmi_vram_usage_t*);
+amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle, uint32_t*, amdsmi_processor_handle*);
+amdsmi_status_t amdsmi_get_gpu_process_list(amdsmi_processor_handle, uint32_t*, amdsmi_proc_info_t*);
 rsmi_status_t rsmi_dev_memory_total_get(uint32_t, rsmi_memory_type_t, uint64_t*);
 rsmi_status_t rsmi_dev_memory_usage_get(uint32_t, rsmi_memory_type_t, uint64_t*);
 }
@@ -62,6 +64,8 @@ const Hook kHooks[] = {
     {"amdsmi_get_gpu_memory_total", reinterpret_cast<void*>(&amdsmi_get_gpu_memory_total)},
     {"amdsmi_get_gpu_memory_usage", reinterpret_cast<void*>(&amdsmi_get_gpu_memory_usage)},
     {"amdsmi_get_gpu_vram_usage", reinterpret_cast<void*>(&amdsmi_get_gpu_vram_usage)},
+    {"amdsmi_get_processor_handles", reinterpret_cast<void*>(&amdsmi_get_processor_handles)},
+    {"amdsmi_get_gpu_process_list", reinterpret_cast<void*>(&amdsmi_get_gpu_process_list)},
     {"rsmi_dev_memory_total_get", reinterpret_cast<void*>(&rsmi_dev_memory_total_get)},
     {"rsmi_dev_memory_usage_get", reinterpret_cast<void*>(&rsmi_dev_memory_usage_get)},
 };

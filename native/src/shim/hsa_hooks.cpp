@@ -66,6 +66,31 @@ hsa_status_t spill_allocate(int dev, size_t size, void** ptr) {
   return HSA_STATUS_SUCCESS;
 }
 
+// Placement of an allocation of a tenant with virtual device memory: true = host memory.
+// First-come keeps HBM until the tenant's HBM share is used up. Large-first (default)
+// sends large allocations (datasets, caches: bulk data touched a slice at a time) to host
+// memory once they would eat into a reserve of the share, so the small, hot allocations
+// that come later (weights, activations, workspaces) still find HBM; a large allocation
+// also spills when the physical HBM (shared with other tenants) lacks size + reserve.
+bool should_spill(int dev, size_t size) {
+  ShimState& s = shim();
+  const Config& cfg = config();
+  const uint64_t hbm = s.region.hbm_limit(dev);
+  if (!cfg.oversubscribe || !hbm) return false;
+  const uint64_t resident = s.region.resident(dev);
+  const bool large = cfg.spill_policy == SpillPolicy::kLargeFirst && size >= cfg.spill_large_bytes;
+  if (!large) return resident + size > hbm;
+  const uint64_t reserve = spill_reserve(cfg, hbm);
+  if (resident + size + reserve > hbm) return true;
+  VGPU_REAL_HSA(hsa_agent_get_info);
+  uint64_t avail = 0;
+  if (real_hsa_agent_get_info(s.agents[dev].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &avail) ==
+          HSA_STATUS_SUCCESS &&
+      avail < size + reserve)
+    return true;
+  return false;
+}
+
 inline bool ready() {
   ShimState& s = shim();
   int ph = s.phase.load(std::memory_order_acquire);
@@ -121,8 +146,7 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   // Virtual device memory: past the tenant's HBM-resident share the quota is served
   // from host memory (VGPU_DEVICE_HBM_LIMIT_<i>, emitted by the plugin when
   // --device-memory-scaling > 1), so one tenant cannot crowd the others out of HBM.
-  uint64_t hbm = config().oversubscribe ? s.region.hbm_limit(dev) : 0;
-  if (hbm && s.region.resident(dev) > hbm) {
+  if (should_spill(dev, size)) {
     st = spill_allocate(dev, size, ptr);
     if (st == HSA_STATUS_SUCCESS) {
       s.region.uncharge(s.slot, dev, size, kMemData);

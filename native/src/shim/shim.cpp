@@ -175,6 +175,9 @@ void on_exit() {
 
 void load_env_config() {
   log_init_from_env();
+  // Alternate KFD process tree (the CPU-only fake runtime of the test suite).
+  if (const char* k = getenv("VGPU_KFD_ROOT"))
+    if (*k) g_kfd_proc_root = strdup(k);
   const char* ovr = getenv("VGPU_OVERRIDE_ENV_FILE");
   int n = apply_override_env_file(ovr && *ovr ? ovr : "/vgpu/override.env");
   if (n) log_init_from_env();
@@ -285,6 +288,11 @@ void shim_init_after_hsa() {
   Config resolved = cfg;
   DeviceConfig per_agent[kMaxDevices];
   resolve_devices(cfg, map, uuid_ptrs, s.n_agents, per_agent);
+  for (int i = 0; i < s.n_agents; i++) {
+    if (!per_agent[i].unmapped) continue;
+    s.agents[i].authorised = false;
+    VLOG_ERROR("device %d (%s) is not in VGPU_DEVICE_MAP: no device memory for it in this container", i, uuids[i]);
+  }
   for (int i = 0; i < kMaxDevices; i++) resolved.dev[i] = i < s.n_agents ? per_agent[i] : DeviceConfig();
   resolved.num_devices = s.n_agents;
 

@@ -1,14 +1,29 @@
-// amd-smi / rocm-smi memory virtualisation (in-container tools show the vGPU quota).
+// amd-smi / rocm-smi virtualisation: in-container tools see the container's GPUs, its
+// processes and the vGPU quota.
 //
 // Reference: src/nvml/hook.c nvmlDeviceGetMemoryInfo(_v2) [327-361] reports
 // total = limit, used = region usage (or the monitor value under MEMORY_OVERRIDE),
-// free = limit - used. The MI355X equivalents are amdsmi_get_gpu_memory_total/usage,
-// amdsmi_get_gpu_vram_usage and the rocm_smi rsmi_dev_memory_total/usage_get calls.
-// These run in processes that usually never initialise ROCr (amd-smi itself), so
-// the region is attached read-mostly and devices are matched by PCI BDF, which the
-// first GPU process of the container recorded in the region.
+// free = limit - used; nvmlDeviceGetCount / GetHandleByIndex / ByPciBusId / ByUUID
+// [438-527] remap the device list to the container's virtual devices.
+//
+// MI355X equivalents:
+//  * memory: amdsmi_get_gpu_memory_total/usage, amdsmi_get_gpu_vram_usage and the
+//    rocm_smi rsmi_dev_memory_total/usage_get calls;
+//  * devices: amdsmi is handle based, so filtering amdsmi_get_processor_handles to the
+//    container's GPUs (the plugin's VGPU_DEVICE_BDFS, else the BDFs the container's GPU
+//    processes recorded in the region) virtualises every later per-device query without
+//    per-function index remapping (rocm_smi's index-based API is left as is);
+//  * processes: amdsmi_get_gpu_process_list keeps only the container's processes (the
+//    region's host PIDs), so tenants cannot see each other's workloads.
+// These run in processes that usually never initialise ROCr (amd-smi itself), so the
+// region is attached read-mostly and devices are matched by PCI BDF.
 #include <amd_smi/amdsmi.h>
 #include <rocm_smi/rocm_smi.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
 
 #include "real.h"
 #include "shim.h"
@@ -49,6 +64,50 @@ int amdsmi_dev(amdsmi_processor_handle h) {
   b.as_uint = 0;
   if (real_amdsmi_get_gpu_device_bdf(h, &b) != AMDSMI_STATUS_SUCCESS) return -1;
   return device_by_bdf(b.as_uint >> 16, (uint32_t)(b.as_uint & 0xffff));
+}
+
+// The container's GPUs as (domain, bdfid) pairs: VGPU_DEVICE_BDFS from the plugin
+// ("dddd:bb:dd.f,..."), else the region's recorded devices. Empty = no filtering.
+struct Bdf {
+  uint64_t domain;
+  uint32_t bdfid;
+};
+
+std::vector<Bdf> visible_bdfs() {
+  std::vector<Bdf> out;
+  if (!config().hook_smi) return out;
+  if (const char* s = getenv("VGPU_DEVICE_BDFS")) {
+    const char* p = s;
+    while (*p) {
+      unsigned dom = 0, bus = 0, dev = 0, fn = 0;
+      int used = 0;
+      if (sscanf(p, "%x:%x:%x.%x%n", &dom, &bus, &dev, &fn, &used) == 4) {
+        out.push_back({dom, (bus << 8) | (dev << 3) | fn});
+        p += used;
+      } else {
+        VLOG_WARN("invalid VGPU_DEVICE_BDFS=%s: device list not filtered", s);
+        return {};
+      }
+      while (*p == ',' || *p == ' ') p++;
+    }
+    return out;
+  }
+  if (!shim_attach_region_only()) return out;
+  const Region* r = shim().region.raw();
+  for (int i = 0; i < kMaxDevices; i++)
+    if (r->dev[i].configured) out.push_back({r->dev[i].domain, r->dev[i].bdf});
+  return out;
+}
+
+bool amdsmi_visible(amdsmi_processor_handle h, const std::vector<Bdf>& vis) {
+  VGPU_REAL_IMPL(amdsmi_get_gpu_device_bdf, "libamd_smi", nullptr);
+  if (!real_amdsmi_get_gpu_device_bdf) return true;
+  amdsmi_bdf_t b;
+  b.as_uint = 0;
+  if (real_amdsmi_get_gpu_device_bdf(h, &b) != AMDSMI_STATUS_SUCCESS) return true;  // not a GPU: keep
+  for (const Bdf& v : vis)
+    if (v.domain == (b.as_uint >> 16) && v.bdfid == (uint32_t)(b.as_uint & 0xffff)) return true;
+  return false;
 }
 
 int rsmi_dev(uint32_t idx) {
@@ -114,6 +173,70 @@ rsmi_status_t rsmi_dev_memory_usage_get(uint32_t dv_ind, rsmi_memory_type_t type
   int dev = rsmi_dev(dv_ind);
   if (dev >= 0 && shim().region.limit(dev)) *used = virt_used(dev);
   return st;
+}
+
+amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle socket, uint32_t* count,
+                                             amdsmi_processor_handle* handles) {
+  VGPU_REAL_IMPL(amdsmi_get_processor_handles, "libamd_smi", nullptr);
+  if (!real_amdsmi_get_processor_handles) return AMDSMI_STATUS_NOT_SUPPORTED;
+  std::vector<Bdf> vis = visible_bdfs();
+  if (vis.empty() || !count) return real_amdsmi_get_processor_handles(socket, count, handles);
+  uint32_t n = 0;
+  amdsmi_status_t st = real_amdsmi_get_processor_handles(socket, &n, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS) return st;
+  std::vector<amdsmi_processor_handle> all(n);
+  if (n && (st = real_amdsmi_get_processor_handles(socket, &n, all.data())) != AMDSMI_STATUS_SUCCESS) return st;
+  std::vector<amdsmi_processor_handle> mine;
+  for (uint32_t i = 0; i < n && i < all.size(); i++)
+    if (amdsmi_visible(all[i], vis)) mine.push_back(all[i]);
+  if (!handles) {
+    *count = (uint32_t)mine.size();
+    return AMDSMI_STATUS_SUCCESS;
+  }
+  uint32_t cap = *count, w = 0;
+  for (; w < cap && w < mine.size(); w++) handles[w] = mine[w];
+  *count = cap < mine.size() ? (uint32_t)mine.size() : w;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_process_list(amdsmi_processor_handle h, uint32_t* max_processes,
+                                            amdsmi_proc_info_t* list) {
+  VGPU_REAL_IMPL(amdsmi_get_gpu_process_list, "libamd_smi", nullptr);
+  if (!real_amdsmi_get_gpu_process_list) return AMDSMI_STATUS_NOT_SUPPORTED;
+  if (!config().hook_smi || !max_processes || !shim_attach_region_only())
+    return real_amdsmi_get_gpu_process_list(h, max_processes, list);
+  // The full list (host PIDs), then only this container's processes.
+  std::vector<amdsmi_proc_info_t> all(64);
+  amdsmi_status_t st;
+  for (;;) {
+    uint32_t n = (uint32_t)all.size();
+    st = real_amdsmi_get_gpu_process_list(h, &n, all.data());
+    if (st == AMDSMI_STATUS_OUT_OF_RESOURCES && n > all.size() && n < 65536) {
+      all.resize(n);
+      continue;
+    }
+    if (st != AMDSMI_STATUS_SUCCESS) return st;
+    all.resize(n);
+    break;
+  }
+  const Region* r = shim().region.raw();
+  std::vector<amdsmi_proc_info_t> mine;
+  for (const amdsmi_proc_info_t& p : all) {
+    for (int i = 0; i < kMaxProcs; i++) {
+      int32_t pid = r->procs[i].pid.load(std::memory_order_relaxed);
+      if (!pid) continue;
+      int32_t hp = r->procs[i].hostpid.load(std::memory_order_relaxed);
+      if ((uint32_t)(hp ? hp : pid) == (uint32_t)p.pid) {
+        mine.push_back(p);
+        break;
+      }
+    }
+  }
+  const uint32_t cap = *max_processes;
+  *max_processes = (uint32_t)mine.size();
+  if (cap == 0 || !list) return AMDSMI_STATUS_SUCCESS;
+  for (uint32_t i = 0; i < cap && i < mine.size(); i++) list[i] = mine[i];
+  return cap < mine.size() ? AMDSMI_STATUS_OUT_OF_RESOURCES : AMDSMI_STATUS_SUCCESS;
 }
 
 }  // extern "C"

@@ -120,6 +120,26 @@ static void test_config() {
   CHECK(c.cu_mode == CuMode::kAuto);
 }
 
+static void test_spill_config() {
+  g_env.clear();
+  Config c;
+  load_config(&c, fake_getenv);
+  CHECK(c.spill_policy == SpillPolicy::kLargeFirst);
+  CHECK_EQ(c.spill_large_bytes, 256ull << 20);
+  CHECK_EQ(spill_reserve(c, 288ull << 30), 18ull << 30);
+  CHECK_EQ(spill_reserve(c, 2ull << 30), 512ull << 20);
+  CHECK_EQ(spill_reserve(c, 64ull << 30), 4ull << 30);
+  g_env["VGPU_SPILL_POLICY"] = "first-come";
+  g_env["VGPU_SPILL_LARGE"] = "1g";
+  g_env["VGPU_SPILL_RESERVE"] = "3g";
+  Config d;
+  load_config(&d, fake_getenv);
+  CHECK(d.spill_policy == SpillPolicy::kFirstCome);
+  CHECK_EQ(d.spill_large_bytes, 1ull << 30);
+  CHECK_EQ(spill_reserve(d, 288ull << 30), 3ull << 30);
+  g_env.clear();
+}
+
 static const char* legacy_env(const char* k) {
   static const std::map<std::string, std::string> m = {
       {"CUDA_DEVICE_MEMORY_LIMIT", "4g"}, {"CUDA_DEVICE_MEMORY_LIMIT_1", "2048m"},
@@ -793,6 +813,7 @@ int main(int argc, char** argv) {
       {"parse_range", test_parse_range},
       {"config", test_config},
       {"legacy_env_names", test_legacy_env_names},
+      {"spill_config", test_spill_config},
       {"override_file", test_override_file},
       {"region_basic", test_region_basic},
       {"region_kinds", test_region_unlimited_and_kinds},

@@ -1,0 +1,217 @@
+// A fake libamdhip64.so over the fake ROCr (fake_hsa.cpp) for CPU-only shim tests.
+//
+// Implements the slice of the HIP API the shim interposes or calls: devices, hipMalloc /
+// hipFree / hipMemGetInfo (through the HSA pool and agent-info entry points, as CLR does),
+// streams (one HSA queue each, so the shim's CU masks land on them), and kernel launches
+// executed by a per-device "GPU" thread that sleeps for the kernel's duration while
+// reporting resident waves in the fake KFD cu_occupancy file. A kernel is a pointer to a
+// uint32 duration in microseconds (the `function_address` argument of hipLaunchKernel;
+// the graph-exec handle of hipGraphLaunch).
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+
+extern "C" int fake_rocr_set_occupancy(int dev, int cus);
+
+namespace {
+
+struct Device {
+  hsa_agent_t agent{0};
+  hsa_amd_memory_pool_t pool{0};
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<uint32_t> work;  // kernel durations (µs)
+  bool running = false;
+  uint64_t busy_us = 0;
+  uint64_t kernels = 0;
+  std::thread th;
+};
+
+std::mutex g_mu;
+bool g_inited = false;
+int g_n = 0;
+// Never destroyed: the per-device GPU threads wait on these until the process ends.
+Device* const g_dev = new Device[16];
+thread_local int t_dev = 0;
+
+void gpu_loop(int d) {
+  Device& D = g_dev[d];
+  for (;;) {
+    uint32_t us;
+    {
+      std::unique_lock<std::mutex> l(D.mu);
+      D.cv.wait(l, [&] { return !D.work.empty(); });
+      us = D.work.front();
+      if (!D.running) fake_rocr_set_occupancy(d, 64);
+      D.running = true;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    std::this_thread::sleep_for(std::chrono::microseconds(us));
+    uint64_t took = (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+                        std::chrono::steady_clock::now() - t0).count();
+    std::lock_guard<std::mutex> l(D.mu);
+    D.work.pop_front();
+    D.busy_us += took;  // the time the "GPU" was really busy (sleeps overshoot)
+    D.kernels++;
+    if (D.work.empty()) {
+      D.running = false;
+      fake_rocr_set_occupancy(d, 0);
+      D.cv.notify_all();
+    }
+  }
+}
+
+hsa_status_t agent_cb(hsa_agent_t a, void*) {
+  hsa_device_type_t t;
+  hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+  if (t == HSA_DEVICE_TYPE_GPU && g_n < 16) g_dev[g_n++].agent = a;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t pool_cb(hsa_amd_memory_pool_t p, void* data) {
+  *static_cast<hsa_amd_memory_pool_t*>(data) = p;
+  return HSA_STATUS_SUCCESS;
+}
+
+void init() {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_inited) return;
+  hsa_init();  // the shim's hsa_init hook runs here, as inside CLR
+  hsa_iterate_agents(agent_cb, nullptr);
+  for (int i = 0; i < g_n; i++) {
+    hsa_amd_agent_iterate_memory_pools(g_dev[i].agent, pool_cb, &g_dev[i].pool);
+    g_dev[i].th = std::thread(gpu_loop, i);
+    g_dev[i].th.detach();
+  }
+  g_inited = true;
+}
+
+struct FakeStream {
+  hsa_queue_t* q;
+  int dev;
+};
+
+int dev_of(hipStream_t s) { return s ? reinterpret_cast<FakeStream*>(s)->dev : t_dev; }
+
+void submit(int d, uint32_t us) {
+  Device& D = g_dev[d];
+  std::lock_guard<std::mutex> l(D.mu);
+  D.work.push_back(us);
+  D.cv.notify_all();
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t hipInit(unsigned int) {
+  init();
+  return hipSuccess;
+}
+
+hipError_t hipGetDeviceCount(int* n) {
+  init();
+  *n = g_n;
+  return hipSuccess;
+}
+
+hipError_t hipSetDevice(int d) {
+  init();
+  if (d < 0 || d >= g_n) return hipErrorInvalidDevice;
+  t_dev = d;
+  return hipSuccess;
+}
+
+hipError_t hipGetDevice(int* d) {
+  init();
+  *d = t_dev;
+  return hipSuccess;
+}
+
+hipError_t hipMalloc(void** ptr, size_t size) {
+  init();
+  hsa_status_t s = hsa_amd_memory_pool_allocate(g_dev[t_dev].pool, size, 0, ptr);
+  return s == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorOutOfMemory;
+}
+
+hipError_t hipFree(void* ptr) {
+  if (!ptr) return hipSuccess;
+  return hsa_amd_memory_pool_free(ptr) == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorInvalidValue;
+}
+
+hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
+  init();
+  uint64_t avail = 0;
+  size_t total = 0;
+  hsa_agent_get_info(g_dev[t_dev].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &avail);
+  hsa_amd_memory_pool_get_info(g_dev[t_dev].pool, HSA_AMD_MEMORY_POOL_INFO_SIZE, &total);
+  *free_b = avail;
+  *total_b = total;
+  return hipSuccess;
+}
+
+hipError_t hipStreamCreate(hipStream_t* stream) {
+  init();
+  FakeStream* s = new FakeStream{nullptr, t_dev};
+  if (hsa_queue_create(g_dev[t_dev].agent, 4096, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &s->q) !=
+      HSA_STATUS_SUCCESS) {
+    delete s;
+    return hipErrorOutOfMemory;
+  }
+  *stream = reinterpret_cast<hipStream_t>(s);
+  return hipSuccess;
+}
+
+hipError_t hipStreamDestroy(hipStream_t stream) {
+  FakeStream* s = reinterpret_cast<FakeStream*>(stream);
+  hsa_queue_destroy(s->q);
+  delete s;
+  return hipSuccess;
+}
+
+hipError_t hipLaunchKernel(const void* function_address, dim3, dim3, void**, size_t, hipStream_t stream) {
+  init();
+  submit(dev_of(stream), *static_cast<const uint32_t*>(function_address));
+  return hipSuccess;
+}
+
+hipError_t hipGraphLaunch(hipGraphExec_t graphExec, hipStream_t stream) {
+  init();
+  submit(dev_of(stream), *reinterpret_cast<const uint32_t*>(graphExec));
+  return hipSuccess;
+}
+
+hipError_t hipDeviceSynchronize() {
+  init();
+  Device& D = g_dev[t_dev];
+  std::unique_lock<std::mutex> l(D.mu);
+  D.cv.wait(l, [&] { return D.work.empty(); });
+  return hipSuccess;
+}
+
+hipError_t hipStreamSynchronize(hipStream_t stream) {
+  int d = dev_of(stream);
+  Device& D = g_dev[d];
+  std::unique_lock<std::mutex> l(D.mu);
+  D.cv.wait(l, [&] { return D.work.empty(); });
+  return hipSuccess;
+}
+
+// Test introspection: GPU time executed on `dev` so far, and its kernel count.
+uint64_t fake_hip_busy_us(int dev, uint64_t* kernels) {
+  if (dev < 0 || dev >= g_n) return 0;
+  std::lock_guard<std::mutex> l(g_dev[dev].mu);
+  if (kernels) *kernels = g_dev[dev].kernels;
+  return g_dev[dev].busy_us;
+}
+
+hsa_queue_t* fake_hip_stream_queue(hipStream_t stream) { return reinterpret_cast<FakeStream*>(stream)->q; }
+
+}  // extern "C"

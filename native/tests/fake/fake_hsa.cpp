@@ -1,0 +1,374 @@
+// A fake ROCr (libhsa-runtime64.so.1) for testing the interception shim on a CPU-only
+// machine: N GPU agents with configurable UUIDs, HBM sizes and CU layout, memory pools
+// backed by reserved-but-never-touched address space, queues that record the CU masks
+// and priorities applied to them, and a fake KFD process tree (vram_<gpu_id>,
+// stats_<gpu_id>/cu_occupancy) under $FAKE_KFD_ROOT for the process's fake host PID
+// (getpid() + $FAKE_KFD_PID_OFFSET, so the shim's host-PID discovery has to work as in a
+// PID namespace).
+//
+// Exported with the ROCR_1 symbol version like the real runtime, so the shim's
+// interposition and real-symbol resolution (real.cpp) behave exactly as with libamdhip64
+// and the real ROCr. Environment:
+//   FAKE_ROCR_GPUS      number of GPU agents (default 2)
+//   FAKE_ROCR_HBM       bytes of HBM per GPU (default 8 GiB)
+//   FAKE_ROCR_CUS / FAKE_ROCR_XCC / FAKE_ROCR_SE   CU layout (256 / 8 / 32 per agent)
+//   FAKE_ROCR_UUIDS     comma-separated agent UUIDs (default GPU-fa4e00000000000<i>)
+//   FAKE_KFD_ROOT       fake /sys/class/kfd/kfd/proc (unset: no KFD tree)
+//   FAKE_KFD_PID_OFFSET host-PID offset (default 100000)
+// Test-only introspection: fake_rocr_* functions below.
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr uint64_t kCpuAgent = 100;
+constexpr uint64_t kGpuPoolBase = 1000;
+constexpr uint64_t kCpuPool = 2000;
+
+struct FakeGpu {
+  std::string uuid;
+  uint64_t hbm = 8ull << 30;
+  std::atomic<uint64_t> used{0};
+  uint32_t gpu_id = 0;
+};
+
+struct FakeQueue {
+  hsa_queue_t q;
+  int dev;
+  uint32_t mask[8];
+  int mask_bits;
+  int mask_sets;
+  int priority;
+};
+
+struct State {
+  int n = 2;
+  int cus = 256, xcc = 8, se = 32;
+  FakeGpu gpus[16];
+  std::mutex mu;
+  std::map<uintptr_t, std::pair<int, uint64_t>> allocs;  // ptr -> (dev or -1 for host, size)
+  std::map<uintptr_t, FakeQueue*> queues;
+  char* arena = nullptr;
+  uint64_t arena_size = 0, arena_next = 0;
+  std::string kfd;  // fake KFD process dir of this process ("" = none)
+  bool inited = false;
+  int init_count = 0;
+};
+
+State& st() {
+  static State* s = new State();
+  return *s;
+}
+
+uint64_t env_u64(const char* k, uint64_t d) {
+  const char* v = getenv(k);
+  return v && *v ? strtoull(v, nullptr, 0) : d;
+}
+
+void write_file(const std::string& path, uint64_t v) {
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) return;
+  fprintf(f, "%llu\n", (unsigned long long)v);
+  fclose(f);
+}
+
+void kfd_update_vram(int dev) {
+  State& s = st();
+  if (s.kfd.empty() || dev < 0) return;
+  write_file(s.kfd + "/vram_" + std::to_string(s.gpus[dev].gpu_id), s.gpus[dev].used.load());
+}
+
+void setup() {
+  State& s = st();
+  if (s.inited) return;
+  s.n = (int)env_u64("FAKE_ROCR_GPUS", 2);
+  if (s.n < 1) s.n = 1;
+  if (s.n > 16) s.n = 16;
+  s.cus = (int)env_u64("FAKE_ROCR_CUS", 256);
+  s.xcc = (int)env_u64("FAKE_ROCR_XCC", 8);
+  s.se = (int)env_u64("FAKE_ROCR_SE", 32);
+  uint64_t hbm = env_u64("FAKE_ROCR_HBM", 8ull << 30);
+  std::vector<std::string> uuids;
+  if (const char* u = getenv("FAKE_ROCR_UUIDS")) {
+    std::string all(u);
+    size_t p = 0;
+    while (p <= all.size()) {
+      size_t c = all.find(',', p);
+      if (c == std::string::npos) c = all.size();
+      if (c > p) uuids.push_back(all.substr(p, c - p));
+      p = c + 1;
+    }
+  }
+  for (int i = 0; i < s.n; i++) {
+    char buf[64];
+    snprintf(buf, sizeof(buf), "GPU-fa4e%012x", i);
+    s.gpus[i].uuid = i < (int)uuids.size() ? uuids[i] : buf;
+    s.gpus[i].hbm = hbm;
+    s.gpus[i].gpu_id = 1000 + i;
+  }
+  s.arena_size = 1ull << 42;  // 4 TiB of address space, never touched
+  void* p = mmap(nullptr, s.arena_size, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  s.arena = p == MAP_FAILED ? nullptr : static_cast<char*>(p);
+  if (const char* root = getenv("FAKE_KFD_ROOT")) {
+    int hp = (int)getpid() + (int)env_u64("FAKE_KFD_PID_OFFSET", 100000);
+    s.kfd = std::string(root) + "/" + std::to_string(hp);
+    mkdir(root, 0777);
+    mkdir(s.kfd.c_str(), 0777);
+    for (int i = 0; i < s.n; i++) {
+      std::string stats = s.kfd + "/stats_" + std::to_string(s.gpus[i].gpu_id);
+      mkdir(stats.c_str(), 0777);
+      write_file(stats + "/cu_occupancy", 0);
+      kfd_update_vram(i);
+    }
+  }
+  s.inited = true;
+}
+
+int gpu_of(hsa_agent_t a) {
+  if (a.handle >= 1 && a.handle <= (uint64_t)st().n) return (int)a.handle - 1;
+  return -1;
+}
+
+void* bump(uint64_t size) {
+  State& s = st();
+  uint64_t sz = (size + 0xFFFF) & ~0xFFFFull;
+  if (!s.arena || s.arena_next + sz > s.arena_size) return nullptr;
+  void* p = s.arena + s.arena_next;
+  s.arena_next += sz + 0x10000;  // guard gap
+  return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+hsa_status_t hsa_init() {
+  std::lock_guard<std::mutex> g(st().mu);
+  setup();
+  st().init_count++;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_shut_down() { return HSA_STATUS_SUCCESS; }
+
+hsa_status_t hsa_iterate_agents(hsa_status_t (*cb)(hsa_agent_t, void*), void* data) {
+  setup();
+  hsa_status_t r = cb(hsa_agent_t{kCpuAgent}, data);
+  if (r != HSA_STATUS_SUCCESS) return r;
+  for (int i = 0; i < st().n; i++) {
+    r = cb(hsa_agent_t{(uint64_t)i + 1}, data);
+    if (r != HSA_STATUS_SUCCESS) return r;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* value) {
+  setup();
+  State& s = st();
+  int d = gpu_of(agent);
+  if ((int)attr == HSA_AGENT_INFO_DEVICE) {
+    *static_cast<hsa_device_type_t*>(value) = d >= 0 ? HSA_DEVICE_TYPE_GPU : HSA_DEVICE_TYPE_CPU;
+    return HSA_STATUS_SUCCESS;
+  }
+  if (d < 0) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  switch ((int)attr) {
+    case HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT: *static_cast<uint32_t*>(value) = s.cus; break;
+    case HSA_AMD_AGENT_INFO_NUM_XCC: *static_cast<uint32_t*>(value) = s.xcc; break;
+    case HSA_AMD_AGENT_INFO_NUM_SHADER_ENGINES: *static_cast<uint32_t*>(value) = s.se; break;
+    case HSA_AMD_AGENT_INFO_DRIVER_UID: *static_cast<uint32_t*>(value) = s.gpus[d].gpu_id; break;
+    case HSA_AMD_AGENT_INFO_MAX_WAVES_PER_CU: *static_cast<uint32_t*>(value) = 32; break;
+    case HSA_AMD_AGENT_INFO_NEAREST_CPU: *static_cast<hsa_agent_t*>(value) = hsa_agent_t{kCpuAgent}; break;
+    case HSA_AMD_AGENT_INFO_UUID: snprintf(static_cast<char*>(value), 64, "%s", s.gpus[d].uuid.c_str()); break;
+    case HSA_AMD_AGENT_INFO_BDFID: *static_cast<uint32_t*>(value) = (uint32_t)(0x05 + 0x10 * d) << 8; break;
+    case HSA_AMD_AGENT_INFO_DOMAIN: *static_cast<uint32_t*>(value) = 0; break;
+    case HSA_AMD_AGENT_INFO_MEMORY_AVAIL: {
+      uint64_t u = s.gpus[d].used.load();
+      *static_cast<uint64_t*>(value) = s.gpus[d].hbm > u ? s.gpus[d].hbm - u : 0;
+      break;
+    }
+    default: return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_amd_agent_iterate_memory_pools(hsa_agent_t agent,
+                                                hsa_status_t (*cb)(hsa_amd_memory_pool_t, void*), void* data) {
+  int d = gpu_of(agent);
+  if (agent.handle == kCpuAgent) return cb(hsa_amd_memory_pool_t{kCpuPool}, data);
+  if (d < 0) return HSA_STATUS_ERROR_INVALID_AGENT;
+  return cb(hsa_amd_memory_pool_t{kGpuPoolBase + (uint64_t)d}, data);
+}
+
+hsa_status_t hsa_amd_memory_pool_get_info(hsa_amd_memory_pool_t pool, hsa_amd_memory_pool_info_t attr, void* value) {
+  setup();
+  State& s = st();
+  int d = pool.handle >= kGpuPoolBase && pool.handle < kGpuPoolBase + (uint64_t)s.n ? (int)(pool.handle - kGpuPoolBase)
+                                                                                     : -1;
+  if (d < 0 && pool.handle != kCpuPool) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  switch ((int)attr) {
+    case HSA_AMD_MEMORY_POOL_INFO_SEGMENT: *static_cast<hsa_amd_segment_t*>(value) = HSA_AMD_SEGMENT_GLOBAL; break;
+    case HSA_AMD_MEMORY_POOL_INFO_SIZE: *static_cast<size_t*>(value) = d >= 0 ? s.gpus[d].hbm : (64ull << 30); break;
+    case HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS:
+      *static_cast<uint32_t*>(value) = HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED;
+      break;
+    case HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED: *static_cast<bool*>(value) = true; break;
+    default: return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t, void** ptr) {
+  setup();
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  int d = pool.handle >= kGpuPoolBase && pool.handle < kGpuPoolBase + (uint64_t)s.n ? (int)(pool.handle - kGpuPoolBase)
+                                                                                     : -1;
+  if (d < 0 && pool.handle != kCpuPool) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  if (d >= 0 && s.gpus[d].used.load() + size > s.gpus[d].hbm) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  void* p = bump(size);
+  if (!p) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  s.allocs[reinterpret_cast<uintptr_t>(p)] = {d, size};
+  if (d >= 0) {
+    s.gpus[d].used.fetch_add(size);
+    kfd_update_vram(d);
+  }
+  *ptr = p;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  auto it = s.allocs.find(reinterpret_cast<uintptr_t>(ptr));
+  if (it == s.allocs.end()) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  int d = it->second.first;
+  if (d >= 0) {
+    s.gpus[d].used.fetch_sub(it->second.second);
+    kfd_update_vram(d);
+  }
+  s.allocs.erase(it);
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_amd_agents_allow_access(uint32_t, const hsa_agent_t*, const uint32_t*, const void*) {
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
+                              void (*)(hsa_status_t, hsa_queue_t*, void*), void*, uint32_t, uint32_t,
+                              hsa_queue_t** queue) {
+  int d = gpu_of(agent);
+  if (d < 0) return HSA_STATUS_ERROR_INVALID_AGENT;
+  FakeQueue* q = new FakeQueue();
+  memset(&q->q, 0, sizeof(q->q));
+  q->q.type = type;
+  q->q.size = size;
+  q->dev = d;
+  memset(q->mask, 0xff, sizeof(q->mask));
+  q->mask_bits = st().cus;
+  q->mask_sets = 0;
+  q->priority = 1;
+  std::lock_guard<std::mutex> g(st().mu);
+  st().queues[reinterpret_cast<uintptr_t>(&q->q)] = q;
+  *queue = &q->q;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_queue_destroy(hsa_queue_t* queue) {
+  std::lock_guard<std::mutex> g(st().mu);
+  auto it = st().queues.find(reinterpret_cast<uintptr_t>(queue));
+  if (it == st().queues.end()) return HSA_STATUS_ERROR_INVALID_QUEUE;
+  delete it->second;
+  st().queues.erase(it);
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* queue, uint32_t num_cu_mask_count, const uint32_t* cu_mask) {
+  std::lock_guard<std::mutex> g(st().mu);
+  auto it = st().queues.find(reinterpret_cast<uintptr_t>(queue));
+  if (it == st().queues.end()) return HSA_STATUS_ERROR_INVALID_QUEUE;
+  FakeQueue* q = it->second;
+  memset(q->mask, 0, sizeof(q->mask));
+  for (uint32_t i = 0; i < num_cu_mask_count && i < 256; i++)
+    if ((cu_mask[i / 32] >> (i % 32)) & 1u) q->mask[i / 32] |= 1u << (i % 32);
+  q->mask_bits = (int)num_cu_mask_count;
+  q->mask_sets++;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_amd_queue_set_priority(hsa_queue_t* queue, hsa_amd_queue_priority_t priority) {
+  std::lock_guard<std::mutex> g(st().mu);
+  auto it = st().queues.find(reinterpret_cast<uintptr_t>(queue));
+  if (it == st().queues.end()) return HSA_STATUS_ERROR_INVALID_QUEUE;
+  it->second->priority = (int)priority;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_amd_vmem_handle_create(hsa_amd_memory_pool_t pool, size_t size, hsa_amd_memory_type_t, uint64_t,
+                                        hsa_amd_vmem_alloc_handle_t* handle) {
+  void* p = nullptr;
+  hsa_status_t r = hsa_amd_memory_pool_allocate(pool, size, 0, &p);
+  if (r == HSA_STATUS_SUCCESS) handle->handle = reinterpret_cast<uint64_t>(p);
+  return r;
+}
+
+hsa_status_t hsa_amd_vmem_handle_release(hsa_amd_vmem_alloc_handle_t handle) {
+  return hsa_amd_memory_pool_free(reinterpret_cast<void*>(handle.handle));
+}
+
+hsa_status_t hsa_amd_ipc_memory_attach(const hsa_amd_ipc_memory_t*, size_t len, uint32_t, const hsa_agent_t*,
+                                       void** mapped_ptr) {
+  std::lock_guard<std::mutex> g(st().mu);
+  *mapped_ptr = bump(len);
+  return *mapped_ptr ? HSA_STATUS_SUCCESS : HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+}
+
+hsa_status_t hsa_amd_ipc_memory_detach(void*) { return HSA_STATUS_SUCCESS; }
+
+// ---------------------------------------------------------------- test introspection
+// CU mask and priority last applied to `queue`; returns the number of mask changes.
+int fake_rocr_queue_state(const hsa_queue_t* queue, uint32_t* mask_words8, int* priority, int* device) {
+  std::lock_guard<std::mutex> g(st().mu);
+  auto it = st().queues.find(reinterpret_cast<uintptr_t>(queue));
+  if (it == st().queues.end()) return -1;
+  memcpy(mask_words8, it->second->mask, sizeof(it->second->mask));
+  if (priority) *priority = it->second->priority;
+  if (device) *device = it->second->dev;
+  return it->second->mask_sets;
+}
+
+// Bytes the fake runtime holds on GPU `dev` (what a real driver would report).
+uint64_t fake_rocr_used(int dev) { return dev >= 0 && dev < st().n ? st().gpus[dev].used.load() : 0; }
+
+// Memory the runtime allocates internally (scratch, code objects): bypasses every
+// allocation entry point, shows up only in KFD's per-process VRAM counter.
+int fake_rocr_internal_alloc(int dev, int64_t bytes) {
+  if (dev < 0 || dev >= st().n) return -1;
+  if (bytes >= 0) st().gpus[dev].used.fetch_add((uint64_t)bytes);
+  else st().gpus[dev].used.fetch_sub((uint64_t)-bytes);
+  kfd_update_vram(dev);
+  return 0;
+}
+
+// Sets the fake cu_occupancy of this process on `dev` (resident waves, CUs' worth).
+int fake_rocr_set_occupancy(int dev, int cus) {
+  if (st().kfd.empty() || dev < 0 || dev >= st().n) return -1;
+  write_file(st().kfd + "/stats_" + std::to_string(st().gpus[dev].gpu_id) + "/cu_occupancy", (uint64_t)cus);
+  return 0;
+}
+
+int fake_rocr_host_pid() { return (int)getpid() + (int)env_u64("FAKE_KFD_PID_OFFSET", 100000); }
+
+}  // extern "C"

@@ -1,0 +1,140 @@
+// Driver for CPU-only shim tests: a "HIP application" linked against the fake HIP/ROCr
+// (fake_hip.cpp, fake_hsa.cpp) and run with libvgpu_hip.so preloaded, exactly like a
+// PyTorch process under the vGPU contract. It executes a small script given on the
+// command line and prints one JSON object per step (tests/test_shim_fake.py):
+//
+//   dev=N            hipSetDevice(N)
+//   malloc=SIZE      hipMalloc (K/M/G suffixes) -> {"malloc": "ok"|"oom"}
+//   free             hipFree of the most recent successful allocation
+//   meminfo          hipMemGetInfo -> {"free": .., "total": ..}
+//   stream           hipStreamCreate on the current device (becomes the current stream)
+//   launch=US,N      N launches of a US-microsecond kernel, then synchronize
+//   run=US,SECS      back-to-back US-microsecond kernels for SECS seconds (sync every 8):
+//                    {"busy_frac": GPU time executed / wall, ...}
+//   graph=US,SECS    like run, with hipGraphLaunch of a US-microsecond "graph"
+//   internal=SIZE    runtime-internal device memory (bypasses every hook; negative frees)
+//   queues           CU-mask bit count, mask changes and priority of every created stream
+//   sleep=SECS
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+#include <hsa/hsa.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+extern "C" {
+uint64_t fake_hip_busy_us(int dev, uint64_t* kernels);
+hsa_queue_t* fake_hip_stream_queue(hipStream_t stream);
+int fake_rocr_queue_state(const hsa_queue_t* queue, uint32_t* mask_words8, int* priority, int* device);
+int fake_rocr_internal_alloc(int dev, int64_t bytes);
+int fake_rocr_host_pid();
+}
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+long long parse_size(const char* s) {
+  char* end = nullptr;
+  long long v = strtoll(s, &end, 10);
+  switch (end && *end ? *end : 0) {
+    case 'k': case 'K': v <<= 10; break;
+    case 'm': case 'M': v <<= 20; break;
+    case 'g': case 'G': v <<= 30; break;
+    default: break;
+  }
+  return v;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  hipInit(0);
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  std::vector<void*> ptrs;
+  std::vector<hipStream_t> streams;
+  static uint32_t kernel_us[64];
+  int kslot = 0;
+  printf("{\"pid\": %d, \"fake_hostpid\": %d}\n", (int)getpid(), fake_rocr_host_pid());
+  for (int i = 1; i < argc; i++) {
+    std::string op(argv[i]);
+    std::string key = op.substr(0, op.find('='));
+    std::string val = op.find('=') == std::string::npos ? "" : op.substr(op.find('=') + 1);
+    if (key == "dev") {
+      dev = atoi(val.c_str());
+      printf("{\"dev\": %d, \"rc\": %d}\n", dev, (int)hipSetDevice(dev));
+      stream = nullptr;
+    } else if (key == "malloc") {
+      void* p = nullptr;
+      hipError_t e = hipMalloc(&p, (size_t)parse_size(val.c_str()));
+      if (e == hipSuccess) ptrs.push_back(p);
+      printf("{\"malloc\": \"%s\", \"bytes\": %lld}\n", e == hipSuccess ? "ok" : "oom", parse_size(val.c_str()));
+    } else if (key == "free") {
+      if (!ptrs.empty()) {
+        hipFree(ptrs.back());
+        ptrs.pop_back();
+      }
+      printf("{\"free\": true}\n");
+    } else if (key == "meminfo") {
+      size_t f = 0, t = 0;
+      hipMemGetInfo(&f, &t);
+      printf("{\"dev\": %d, \"free\": %zu, \"total\": %zu}\n", dev, f, t);
+    } else if (key == "stream") {
+      hipStreamCreate(&stream);
+      streams.push_back(stream);
+      printf("{\"stream\": %zu}\n", streams.size() - 1);
+    } else if (key == "launch" || key == "graph" || key == "run") {
+      unsigned us = (unsigned)atoi(val.c_str());
+      double amount = atof(val.substr(val.find(',') + 1).c_str());
+      uint32_t* k = &kernel_us[kslot++ % 64];
+      *k = us;
+      uint64_t k0 = 0, b0 = fake_hip_busy_us(dev, &k0);
+      double t0 = now_s();
+      long n = 0;
+      for (;; n++) {
+        const bool timed = key != "launch";
+        if (timed ? now_s() - t0 >= amount : n >= (long)amount) break;
+        if (key == "graph") hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(k), stream);
+        else hipLaunchKernel(k, dim3(1), dim3(64), nullptr, 0, stream);
+        if (timed && n % 8 == 7) hipStreamSynchronize(stream);
+      }
+      hipStreamSynchronize(stream);
+      double wall = now_s() - t0;
+      uint64_t k1 = 0, b1 = fake_hip_busy_us(dev, &k1);
+      printf("{\"%s\": %ld, \"wall\": %.6f, \"busy_us\": %llu, \"busy_frac\": %.4f}\n", key.c_str(), n, wall,
+             (unsigned long long)(b1 - b0), (b1 - b0) / 1e6 / wall);
+    } else if (key == "internal") {
+      fake_rocr_internal_alloc(dev, parse_size(val.c_str()));
+      printf("{\"internal\": %lld}\n", parse_size(val.c_str()));
+    } else if (key == "queues") {
+      printf("{\"queues\": [");
+      for (size_t q = 0; q < streams.size(); q++) {
+        uint32_t m[8];
+        int prio = 0, d = 0;
+        int sets = fake_rocr_queue_state(fake_hip_stream_queue(streams[q]), m, &prio, &d);
+        int bits = 0;
+        for (uint32_t w : m) bits += __builtin_popcount(w);
+        printf("%s{\"dev\": %d, \"cus\": %d, \"sets\": %d, \"priority\": %d, \"mask0\": %u}", q ? ", " : "", d, bits,
+               sets, prio, m[0]);
+      }
+      printf("]}\n");
+    } else if (key == "sleep") {
+      std::this_thread::sleep_for(std::chrono::duration<double>(atof(val.c_str())));
+      printf("{\"slept\": %s}\n", val.c_str());
+    } else {
+      fprintf(stderr, "unknown op %s\n", op.c_str());
+      return 2;
+    }
+    fflush(stdout);
+  }
+  return 0;
+}

@@ -3,6 +3,7 @@
 plus oversubscription spill, SMI virtualisation and RCCL through the shim."""
 import os
 import threading
+import time
 
 import pytest
 
@@ -249,3 +250,58 @@ except Exception as e:
     emit(ok=False, err=repr(e)[:300])
 """, None)
     print("amdsmi native:", res[0])
+
+
+HOLD = """
+import torch
+x = torch.ones(256 << 20, dtype=torch.uint8, device="cuda"); torch.cuda.synchronize()
+emit(ok=True)
+time.sleep(40)
+"""
+
+AMDSMI_VIEW = """
+try:
+    import amdsmi
+    amdsmi.amdsmi_init()
+    hs = amdsmi.amdsmi_get_processor_handles()
+    procs = [p["pid"] for h in hs for p in amdsmi.amdsmi_get_gpu_process_list(h)]
+    emit(ok=True, n=len(hs), procs=procs)
+except Exception as e:
+    emit(ok=False, err=repr(e)[:300])
+"""
+
+
+def test_amdsmi_shows_only_the_containers_gpus_and_processes(tmp_region):
+    """In-container amd-smi (amdsmi over ctypes): the process list holds the container's
+    processes only (a GPU process of another tenant on the same GPU is hidden) and the
+    device list is the container's (reference: NVML count/handle remapping, nvml/hook.c
+    :438-527). On the 1-GPU box the device filter is shown by a non-matching BDF list."""
+    from amdvgpu.plugin.devices import SysfsBackend
+    from amdvgpu.shim.region import Region
+    dev = SysfsBackend().devices()[0]
+    c = vgpu_env(mem_limit=24 * GiB, shared_cache=tmp_region, extra={"VGPU_DEVICE_BDFS": dev.bdf})
+    foreign = spawn_child(HOLD, None)
+    holder = spawn_child(HOLD, c)
+    try:
+        assert foreign.stdout.readline().startswith("RESULT")
+        assert holder.stdout.readline().startswith("RESULT")
+        time.sleep(1.0)
+        with Region(tmp_region) as r:
+            mine = {p["hostpid"] for p in r.procs()}
+        native, _ = run_child(AMDSMI_VIEW, None)
+        inside, _ = run_child(AMDSMI_VIEW, c)
+        c_other = dict(c, VGPU_DEVICE_BDFS="0000:ff:1f.7")
+        hidden, _ = run_child(AMDSMI_VIEW, c_other)
+    finally:
+        for p in (foreign, holder):
+            p.kill()
+            p.wait()
+    if not native[0]["ok"]:
+        pytest.skip(f"amdsmi unavailable on this box: {native[0]['err']}")
+    n, i, h = native[0], inside[0], hidden[0]
+    assert i["ok"] and h["ok"], (i, h)
+    print("amdsmi native:", n, "inside:", i, "container hostpids:", mine)
+    assert all(m > 0 for m in mine)
+    assert len(n["procs"]) >= 2                     # both GPU processes are on the GPU
+    assert set(i["procs"]) <= mine and mine & set(i["procs"]), (i, mine)
+    assert i["n"] == n["n"] == 1 and h["n"] == 0

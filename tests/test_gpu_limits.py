@@ -334,3 +334,38 @@ def test_ipc_tensor_is_charged_once(tmp_region, tmp_path):
     # Each process's charge matches KFD's own count of its VRAM (the import is not in it).
     for pr in r["procs"]:
         assert abs(pr["data"] + pr["context"] - pr["kfd_vram"]) < 64 * MiB, pr
+
+
+SPILL = """
+import torch
+from amdvgpu.shim.region import Region
+x = torch.ones(1 << 20, device="cuda"); torch.cuda.synchronize(); time.sleep(0.3)
+r = Region(os.environ["VGPU_SHARED_CACHE"])
+big = [torch.ones(1 << 30, dtype=torch.uint8, device="cuda") for _ in range(8)]     # 8 x 1 GiB ("large")
+torch.cuda.synchronize()
+after_big = r.device(0)["spilled"]
+small = [torch.full((32 << 20,), 7, dtype=torch.uint8, device="cuda") for _ in range(64)]   # 64 x 32 MiB
+torch.cuda.synchronize()
+after_small = r.device(0)["spilled"]
+ok = all(bool(t[:4096].eq(1).all()) for t in big) and all(bool(t[:4096].eq(7).all()) for t in small)
+emit(after_big=after_big, after_small=after_small, ok=ok)
+"""
+
+
+@pytest.mark.parametrize("policy", ["large-first", "first-come"])
+def test_spill_placement_policy(tmp_region, policy):
+    """Virtual device memory with an 8 GiB HBM share: first-come fills HBM with the eight
+    1 GiB buffers and spills the later small (hot) allocations; large-first spills large
+    buffers once they would eat into the share's reserve (3 GiB here), so the 2 GiB of
+    small ones still find HBM."""
+    c = vgpu_env(mem_limit=16 * GiB, shared_cache=tmp_region, oversubscribe=True,
+                 extra={"VGPU_DEVICE_HBM_LIMIT_0": "8192m", "VGPU_SPILL_POLICY": policy,
+                        "VGPU_SPILL_RESERVE": "3g"})
+    res, _ = run_child(SPILL, c)
+    r = res[0]
+    assert r["ok"], r
+    small_spilled = r["after_small"] - r["after_big"]
+    if policy == "large-first":
+        assert r["after_big"] >= 2 * GiB and small_spilled == 0, r
+    else:
+        assert r["after_big"] <= 2 * GiB and small_spilled >= 512 * MiB, r
