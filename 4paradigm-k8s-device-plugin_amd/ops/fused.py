@@ -719,6 +719,17 @@ def lstm_recurrence(gx, whh, h0=None, c0=None):
     return hT, cT
 
 
+# Buffer-descriptor ranges of the LSTM kernels (lstm_mfma.hip host guards): the stash of
+# the training kernel holds B*T*128*16 bytes, the inference input B*T*128*8; both must stay
+# below 2^31. Larger inputs take the library LSTM instead of failing.
+LSTM_TRAIN_MAX_BT = (1 << 31) // (128 * 16)
+LSTM_INFER_MAX_BT = (1 << 31) // (128 * 8)
+
+
+def lstm_fits(x, max_bt):
+    return x.dim() == 3 and x.shape[0] * x.shape[1] < max_bt
+
+
 class FusedLSTMLast(nn.Module):
     """Inference form of a single-layer, unidirectional, batch-first ``nn.LSTM`` with 128
     hidden units whose caller only needs the last hidden state (the sentiment model):
@@ -741,8 +752,29 @@ class FusedLSTMLast(nn.Module):
         self.register_buffer("b_perm", b.contiguous())
         self.plan = {}
         self._cast = None
+        self._src = None
+
+    def _weights_version(self):
+        l = self.lstm
+        return tuple((p.data_ptr(), p._version) for p in (l.weight_ih_l0, l.weight_hh_l0, l.bias_ih_l0, l.bias_hh_l0))
+
+    def _refresh(self):
+        """Re-derives the permuted weights when the wrapped LSTM's parameters changed
+        (load_state_dict, fine-tuning, the library path's in-place .to(dtype))."""
+        v = self._weights_version()
+        if v == self._src:
+            return
+        l, H, Fin = self.lstm, self.lstm.hidden_size, self.lstm.input_size
+        with torch.no_grad():
+            w = l.weight_ih_l0.detach().float().view(4, H, Fin).permute(1, 0, 2).reshape(4 * H, Fin)
+            b = (l.bias_ih_l0.detach().float() + l.bias_hh_l0.detach().float()).view(4, H).t().reshape(4 * H)
+            self.w_ih_perm = w.contiguous().to(self.w_ih_perm.device)
+            self.b_perm = b.contiguous().to(self.b_perm.device)
+        self._cast = None
+        self._src = v
 
     def _fused(self, x):
+        self._refresh()
         if self._cast is None or self._cast[0] != x.dtype:
             self._cast = (x.dtype, self.w_ih_perm.to(x.dtype).t(), self.b_perm.to(x.dtype),
                           self.lstm.weight_hh_l0.detach().to(x.dtype).contiguous())
@@ -759,7 +791,8 @@ class FusedLSTMLast(nn.Module):
         return out[:, -1]
 
     def forward(self, x):
-        ok = self.impl == "hip" and self.mode != "off" and x.is_cuda and x.dtype == torch.bfloat16
+        ok = (self.impl == "hip" and self.mode != "off" and x.is_cuda and x.dtype == torch.bfloat16
+              and lstm_fits(x, LSTM_INFER_MAX_BT))
         if not ok:
             return self._library(x)
         if self.mode == "on":
@@ -908,7 +941,7 @@ class FusedLSTMTrainLast(nn.Module):
         return self.mode != "off"
 
     def forward(self, x):
-        if not self.fused or not x.is_cuda:
+        if not self.fused or not x.is_cuda or not lstm_fits(x, LSTM_TRAIN_MAX_BT):
             out, _ = self.lstm(x)
             return out[:, -1]
         l = self.lstm

@@ -80,7 +80,9 @@ void gate_launch(int dev) {
   bool limited = s.agents[dev].temporal_active.load(std::memory_order_relaxed) &&
                  (r->hdr.utilization_switch.load(std::memory_order_relaxed) || config().cu_policy == CuPolicy::kForce);
   if (__builtin_expect(!limiter_would_block(r->hdr, r->dev[dev], limited), 1)) return;
+  trace_push(limited ? "vgpu:throttle" : "vgpu:blocked");
   uint64_t waited = limiter_acquire(r->hdr, r->dev[dev], limited);
+  trace_pop();
   if (waited && s.slot >= 0) r->procs[s.slot].throttle_ns.fetch_add(waited, std::memory_order_relaxed);
 }
 

@@ -490,6 +490,7 @@ void gate_suspend_slow() {
   uint64_t t0 = now_ns();
   bool logged = false;
   struct timespec ts = {0, 1000000};
+  trace_push("vgpu:suspended");
   while (gate_needed()) {
     if (!logged) {
       VLOG_INFO("process suspended by controller; waiting");
@@ -497,6 +498,7 @@ void gate_suspend_slow() {
     }
     nanosleep(&ts, nullptr);
   }
+  trace_pop();
   if (s.slot >= 0) s.region.raw()->procs[s.slot].suspend_ns.fetch_add(now_ns() - t0);
 }
 

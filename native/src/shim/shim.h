@@ -95,6 +95,10 @@ extern std::atomic<uint64_t> g_stats[kStatCount];
 int agent_ordinal(hsa_agent_t a);
 int pool_ordinal(hsa_amd_memory_pool_t p);
 
+// roctx ranges around blocking waits (trace.cpp; VGPU_TRACE=1).
+void trace_push(const char* name);
+void trace_pop();
+
 // Suspend gate: blocks while the container is suspended (reference wait_status_self).
 void gate_suspend_slow();
 inline bool gate_needed() {

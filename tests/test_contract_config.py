@@ -187,3 +187,23 @@ def test_legacy_allocate_refuses_without_checkpoint(tmp_path):
     srv, ids, AllocationError = _legacy_server(tmp_path)
     with pytest.raises(AllocationError):
         srv.Allocate(_alloc_req([ids[0]]), None)
+
+
+def test_fused_lstm_routes_oversize_inputs_to_the_library():
+    """inputs beyond the kernels' buffer-descriptor range take nn.LSTM."""
+    import torch
+    from amdvgpu.ops.fused import (LSTM_INFER_MAX_BT, LSTM_TRAIN_MAX_BT, FusedLSTMLast, FusedLSTMTrainLast,
+                                   lstm_fits)
+    assert LSTM_TRAIN_MAX_BT == 1 << 20 and LSTM_INFER_MAX_BT == 1 << 21
+    assert lstm_fits(torch.empty(1023, 1024, 1), LSTM_TRAIN_MAX_BT)
+    assert not lstm_fits(torch.empty(1024, 1024, 1), LSTM_TRAIN_MAX_BT)
+    lstm = torch.nn.LSTM(8, 128, batch_first=True)
+    x = torch.randn(2, 5, 8)
+    ref = lstm(x)[0][:, -1]
+    assert torch.allclose(FusedLSTMTrainLast(lstm)(x), ref)      # CPU tensors: library path
+    f = FusedLSTMLast(lstm)
+    assert torch.allclose(f(x), ref)
+    with torch.no_grad():                                         # live weights are tracked
+        lstm.weight_ih_l0.mul_(2)
+    f._refresh()
+    assert torch.allclose(f.w_ih_perm.view(128, 4, 8).permute(1, 0, 2).reshape(512, 8), lstm.weight_ih_l0)

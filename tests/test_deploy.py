@@ -43,3 +43,25 @@ def test_helm_template_flags_exist():
 def test_preload_file_points_at_container_shim():
     from amdvgpu.plugin.contract import CONTAINER_SHIM
     assert open(os.path.join(REPO, "vgpu", "ld.so.preload")).read().strip() == CONTAINER_SHIM
+
+
+def test_image_build_inputs_exist():
+    """Static check of docker/Dockerfile (no container engine in CI's first stage): every
+    COPY source exists, the make targets are real targets, and the entrypoint installs
+    exactly what the build produces."""
+    import re
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    df = open(os.path.join(repo, "docker", "Dockerfile")).read()
+    for src in re.findall(r"^COPY (?!--from)(\S+)", df, re.M):
+        assert os.path.exists(os.path.join(repo, src.rstrip("/"))), src
+    targets = re.findall(r"\.\./4paradigm-k8s-device-plugin_amd/lib/(\S+)", df)
+    assert set(targets) == {"libvgpu_hip.so", "libvgpu_region.so", "vgpuctl", "vgpu-validate"}
+    for t in targets:  # make knows how to build each one (dry run)
+        rc = subprocess.call(["make", "-n", "-C", os.path.join(repo, "native"),
+                              f"../4paradigm-k8s-device-plugin_amd/lib/{t}"], stdout=subprocess.DEVNULL)
+        assert rc == 0, t
+    ep = open(os.path.join(repo, "docker", "entrypoint.sh")).read()
+    installed = re.search(r"for f in ([^;]+);", ep).group(1).split()
+    assert set(installed) == set(targets) | {"ld.so.preload"}
+    assert "lock" in ep and "containers" in ep
