@@ -1,20 +1,19 @@
 #!/usr/bin/env python3
-"""Concurrent-vGPU scaling curve on one MI355X: N tenants (N = 1, 2, 4, 8) each running
-the same workload in its own vGPU, started together; reports per-tenant and aggregate
-throughput. This is the reference's "vGPU+VDM high load" column (4 containers on 2 GPUs,
-BASELINE.md) generalised to the MI355X's tenant counts.
+"""Concurrent-vGPU scaling curve on one MI355X: N pods (N = 1, 2, 4, 8) each running the
+same stock workload (fp32, MIOpen / hipBLASLt) in its own vGPU, started together; reports
+per-pod and aggregate throughput. This is the reference's "vGPU+VDM high load" column
+(4 containers on 2 GPUs) generalised to the MI355X's tenant counts.
 
-Policies:
-* spatial   tenant i of N gets quota HBM/N and the i-th disjoint XCD-balanced CU slice
-            (what the plugin hands out with --device-split-count=N)
-* shared    quota HBM/N, no CU limit: tenants time-share all 256 CUs (hardware
-            scheduling between queues)
-* spatial-interleave  same slices in the plain interleaved mask layout (every tenant
-            on every SE) instead of the default SE-major layout
-* vdm       the reference's "virtual device memory" setting: quota 1.8 x HBM/N with
-            oversubscription (HBM share HBM/N, rest spills), CU limit 100*1/N spatial
+Every pod's contract comes from an Allocate of the plugin (NodeHarness, sysfs backend)
+configured with --device-split-count=N and the policy's --cu-mode:
 
-    python benchmarks/vgpu_scaling.py [--case resnet50-inf] [--tenants 1,2,4,8] [--policy spatial,shared]
+* default   --cu-mode auto (the shipped default): CU masks for 2 pods, the GPU-time
+            limiter for 4 and 8
+* spatial   --cu-mode spatial: disjoint XCD-balanced CU slices at every N
+* temporal  --cu-mode temporal at every N
+* shared    --cu-mode off: quota only, hardware time-sharing of all 256 CUs
+
+    python benchmarks/vgpu_scaling.py [--case resnet50-inf] [--tenants 1,2,4,8] [--policy default,spatial,shared]
 """
 import argparse
 import json
@@ -29,72 +28,66 @@ sys.path.insert(0, REPO)
 HBM = 309220868096
 
 
-def worker(case_name, steps, warmup, out, go_file):
+def worker(case_name, steps, warmup, out, go_file, seconds):
     import torch
     from amdvgpu.models.aibench import Runner, get_case
-    torch.backends.cudnn.benchmark = os.environ.get("VGPU_BENCH_TUNE", "1") == "1"  # MIOpen find mode
+    torch.backends.cudnn.benchmark = True  # MIOpen find mode
     case = get_case(case_name)
-    r = Runner(case, "cuda:0")
+    r = Runner(case, "cuda:0", dtype=torch.float32, fuse=False)
     for _ in range(warmup):
         r.step()
     torch.cuda.synchronize()
     open(out + ".ready", "w").close()
     while not os.path.exists(go_file):
         time.sleep(0.005)
+    n = 0
     t0 = time.perf_counter()
-    for _ in range(steps):
+    while time.perf_counter() - t0 < seconds:
         r.step()
+        n += 1
+        if n % 4 == 0:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    json.dump({"ms_per_batch": (t1 - t0) * 1000 / steps, "t0": t0, "t1": t1, "batch": case.batch,
-               "throughput": case.batch * steps / (t1 - t0)}, open(out, "w"))
+    json.dump({"ms_per_batch": (t1 - t0) * 1000 / n, "t0": t0, "t1": t1, "batch": case.batch, "steps": n,
+               "throughput": case.batch * n / (t1 - t0)}, open(out, "w"))
 
 
-def run_point(case, n, policy, steps, warmup, solo=False):
-    from amdvgpu.plugin.vdevice import cu_partition_range
-    from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
+MODES = {"default": "auto", "spatial": "spatial", "temporal": "temporal", "shared": "off"}
+
+
+def run_point(backend, uuid, case, n, policy, warmup, seconds):
+    from amdvgpu.plugin.kubelet_stub import NodeHarness
+    from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="scal-")
     go = os.path.join(tmp, "go")
-    procs, contracts, outs = [], [], []
-    for i in range(1 if solo else n):
-        kw = dict(mem_limit=HBM // n)
-        if policy == "vdm":
-            kw = dict(mem_limit=int(HBM * 1.8 / n), oversubscribe=True,
-                      extra={"VGPU_DEVICE_HBM_LIMIT_0": f"{HBM // n >> 20}m"})
-        if policy in ("spatial", "spatial-interleave", "spatial-q1", "vdm") and n > 1:
-            b, e = cu_partition_range(256, 8, n, i)
-            kw.update(cu_limit=100 * (e - b) // 256, cu_range=(b, e))
-        if policy == "spatial-q1":
-            kw["extra"] = dict(kw.get("extra") or {}, GPU_MAX_HW_QUEUES="1")
-        if policy == "spatial-interleave":
-            kw["extra"] = dict(kw.get("extra") or {}, VGPU_CU_LAYOUT="interleave")
-        c = vgpu_env(**kw)
-        out = os.path.join(tmp, f"t{i}.json")
-        cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--case", case, "--steps", str(steps),
-               "--warmup", str(warmup), "--out", out, "--go", go]
-        procs.append(subprocess.Popen(cmd, env=apply_contract(c)))
-        contracts.append(c)
-        outs.append(out)
-    try:
-        deadline = time.time() + 600
-        while not all(os.path.exists(o + ".ready") for o in outs):
-            if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
-                raise SystemExit("a tenant failed before the start barrier")
-            time.sleep(0.05)
-        open(go, "w").close()
-        for p in procs:
-            if p.wait(timeout=900) != 0:
-                raise SystemExit("a tenant failed")
-        res = [json.load(open(o)) for o in outs]
-    finally:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
-        for c in contracts:
-            cleanup_region(c)
+    procs, outs = [], []
+    with NodeHarness(backend, device_split_count=n, cu_mode=MODES[policy]) as node:
+        for i, vid in enumerate(node.vgpu_ids(uuid)[:n]):
+            envs, mounts = node.pod([vid])
+            out = os.path.join(tmp, f"t{i}.json")
+            cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--case", case, "--warmup", str(warmup),
+                   "--seconds", str(seconds), "--out", out, "--go", go]
+            procs.append(subprocess.Popen(cmd, env=apply_contract(envs, mounts)))
+            outs.append(out)
+        try:
+            deadline = time.time() + 600
+            while not all(os.path.exists(o + ".ready") for o in outs):
+                if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
+                    raise SystemExit("a tenant failed before the start barrier")
+                time.sleep(0.05)
+            open(go, "w").close()
+            for p in procs:
+                if p.wait(timeout=900) != 0:
+                    raise SystemExit("a tenant failed")
+            res = [json.load(open(o)) for o in outs]
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
     span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
-    agg = sum(r["batch"] * steps for r in res) / span
-    return {"tenants": n, "policy": policy + ("-solo" if solo else ""), "aggregate_throughput": agg,
+    agg = sum(r["batch"] * r["steps"] for r in res) / span
+    return {"tenants": n, "policy": policy, "aggregate_throughput": agg,
             "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res]}
 
 
@@ -102,10 +95,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="resnet50-inf")
     ap.add_argument("--tenants", default="1,2,4,8")
-    ap.add_argument("--policy", default="spatial,shared")
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--policy", default="default,spatial,shared")
+    ap.add_argument("--seconds", type=float, default=6.0)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--solo", action="store_true", help="run only tenant 0 of each N (its slice alone)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--go")
@@ -113,22 +105,26 @@ def main():
     ap.add_argument("--md-out")
     a = ap.parse_args()
     if a.worker:
-        return worker(a.case, a.steps, a.warmup, a.out, a.go)
+        return worker(a.case, 0, a.warmup, a.out, a.go, a.seconds)
+    from amdvgpu.plugin.devices import SysfsBackend
+    backend = SysfsBackend()
+    uuid = backend.devices()[0].uuid
     rows = []
     for pol in a.policy.split(","):
         for n in [int(x) for x in a.tenants.split(",")]:
-            r = run_point(a.case, n, pol, a.steps, a.warmup, solo=a.solo)
+            r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds)
             rows.append(r)
             print(json.dumps(r), flush=True)
     base = {r["policy"]: r["aggregate_throughput"] for r in rows if r["tenants"] == 1}
-    for r in rows:
-        base.setdefault(r["policy"], rows[0]["aggregate_throughput"])
-    md = [f"# concurrent vGPUs on one MI355X — {a.case}", "",
-          "| policy | tenants | aggregate | vs 1 tenant | per-tenant (min..max) |", "|---|---|---|---|---|"]
+    md = [f"# concurrent vGPU pods on one MI355X — {a.case} (stock fp32; contracts from Allocate)", "",
+          "| policy (--cu-mode) | pods | aggregate | vs 1 pod | per pod (min..max) | slowest pod vs 1/N |",
+          "|---|---|---|---|---|---|"]
     for r in rows:
         pt = r["per_tenant"]
-        md.append(f"| {r['policy']} | {r['tenants']} | {r['aggregate_throughput']:.1f} | "
-                  f"{r['aggregate_throughput'] / base[r['policy']]:.2f}x | {min(pt):.1f} .. {max(pt):.1f} |")
+        b = base.get(r["policy"], rows[0]["aggregate_throughput"])
+        md.append(f"| {r['policy']} ({MODES[r['policy']]}) | {r['tenants']} | {r['aggregate_throughput']:.1f} | "
+                  f"{r['aggregate_throughput'] / b:.2f}x | {min(pt):.1f} .. {max(pt):.1f} | "
+                  f"{min(pt) / (b / r['tenants']):.2f} |")
     print("\n".join(md))
     if a.json_out:
         json.dump(rows, open(a.json_out, "w"), indent=1)

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""rocprofv3 evidence for the data plane: the same stock fp32 ResNet-50 tenant profiled
+natively, inside a quota-only vGPU, and inside a 25 % temporal vGPU with the shim's roctx
+ranges on (VGPU_TRACE=1).
+
+    python tools/probe/prof_tenant.py --out gpurun_out/prof [--steps 30]
+
+For every mode: `rocprofv3 --kernel-trace --marker-trace --stats -d <out>/<mode> --
+python3 prof_tenant.py --tenant ...` (the profiled program itself follows `--`), then a
+summary (kernel time per step, top kernels, vgpu:* marker time) in <out>/summary.md.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+
+
+def tenant(steps):
+    import torch
+    from amdvgpu.models.aibench import Runner, get_case
+    torch.backends.cudnn.benchmark = True
+    r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False)
+    for _ in range(5):
+        r.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r.step()
+    torch.cuda.synchronize()
+    print(json.dumps({"ms_per_step": (time.perf_counter() - t0) * 1000 / steps}), flush=True)
+
+
+def find(d, pattern):
+    hits = glob.glob(os.path.join(d, "**", pattern), recursive=True)
+    return hits[0] if hits else None
+
+
+def summarize(d, steps):
+    out = {}
+    ks = find(d, "*kernel_stats.csv")
+    if ks:
+        rows = list(csv.DictReader(open(ks)))
+        total = sum(float(r["TotalDurationNs"]) for r in rows)
+        out["kernel_ms_per_step"] = total / 1e6 / (steps + 5)
+        out["kernels"] = sum(int(r["Calls"]) for r in rows)
+        top = sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:5]
+        out["top"] = [(r["Name"][:70], round(float(r["TotalDurationNs"]) / 1e6, 2), int(r["Calls"])) for r in top]
+    mk = find(d, "*marker_api_trace.csv")
+    if mk:
+        rows = list(csv.DictReader(open(mk)))
+        agg = {}
+        for r in rows:
+            name = r.get("Function") or r.get("Name") or ""
+            if name.startswith("vgpu:"):
+                dur = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+                n, t = agg.get(name, (0, 0.0))
+                agg[name] = (n + 1, t + dur / 1e6)
+        out["markers"] = {k: {"count": n, "ms": round(t, 2)} for k, (n, t) in agg.items()}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="gpurun_out/prof")
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--tenant", action="store_true")
+    a = ap.parse_args()
+    if a.tenant:
+        return tenant(a.steps)
+    from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
+    modes = {
+        "native": None,
+        "vgpu-quota": vgpu_env(mem_limit=72 << 30),
+        "vgpu-t25": vgpu_env(mem_limit=72 << 30, cu_limit=25, cu_mode="temporal", extra={"VGPU_TRACE": "1"}),
+    }
+    res = {}
+    for mode, c in modes.items():
+        env = apply_contract(c) if c else dict(os.environ)
+        d = os.path.join(a.out, mode)
+        cmd = ["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "-d", d, "-o", mode, "--",
+               sys.executable, os.path.abspath(__file__), "--tenant", "--steps", str(a.steps)]
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+        if c:
+            cleanup_region(c)
+        line = [l for l in p.stdout.splitlines() if l.startswith("{")]
+        res[mode] = {"rc": p.returncode, **(json.loads(line[-1]) if line else {}), **summarize(d, a.steps)}
+        print(mode, json.dumps(res[mode]), flush=True)
+        if p.returncode != 0:
+            print(p.stderr[-3000:], file=sys.stderr)
+            break
+    md = ["# rocprofv3: stock fp32 ResNet-50 (b=50, 346²) native vs inside vGPUs", "",
+          "| mode | wall ms/step | GPU kernel ms/step | kernels | vgpu:* roctx ranges |", "|---|---|---|---|---|"]
+    for m, r in res.items():
+        mk = ", ".join(f"{k} x{v['count']} {v['ms']} ms" for k, v in (r.get("markers") or {}).items()) or "-"
+        md.append(f"| {m} | {r.get('ms_per_step', 0):.2f} | {r.get('kernel_ms_per_step', 0):.2f} | "
+                  f"{r.get('kernels', 0)} | {mk} |")
+    md += ["", "Top kernels (native): " + "; ".join(f"{n} {t} ms x{c}" for n, t, c in res["native"].get("top", []))]
+    os.makedirs(a.out, exist_ok=True)
+    open(os.path.join(a.out, "summary.md"), "w").write("\n".join(md) + "\n")
+    json.dump(res, open(os.path.join(a.out, "summary.json"), "w"), indent=1)
+    print("\n".join(md))
+
+
+if __name__ == "__main__":
+    main()
