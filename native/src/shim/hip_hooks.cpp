@@ -53,7 +53,18 @@ __attribute__((constructor)) void launch_hook_ctor() {
 inline void launch_gate() {
   VGPU_STAT(kStatLaunch);
   if (__builtin_expect(!g_launch_hooks_on, 0)) return;
-  if (__builtin_expect(!shim().active, 1)) return;
+  ShimState& s = shim();
+  if (__builtin_expect(!s.active, 1)) return;
+  // Fast path: count (process-local; the maintenance thread publishes it), then three
+  // relaxed loads of region words that only a controller writes.
+  s.launches.fetch_add(1, std::memory_order_relaxed);
+  const Region* r = s.region.raw();
+  if (__builtin_expect(r->hdr.generation.load(std::memory_order_relaxed) ==
+                               s.seen_generation.load(std::memory_order_relaxed) &&
+                           !gate_needed() && r->hdr.recent_kernel.load(std::memory_order_relaxed) >= 0 &&
+                           !s.any_temporal.load(std::memory_order_relaxed),
+                       1))
+    return;
   gate_launch(-1);
 }
 
@@ -64,7 +75,6 @@ namespace vgpu {
 void gate_launch(int dev) {
   ShimState& s = shim();
   Region* r = s.region.raw();
-  if (s.slot >= 0) r->procs[s.slot].launches.fetch_add(1, std::memory_order_relaxed);
   check_live_config();
   gate_suspend();
   if (dev < 0) {

@@ -158,6 +158,7 @@ void atfork_child() {
   for (auto& b : s.ipc_bytes) b.store(0);
   s.queues.clear();
   s.hostpid = 0;
+  s.launches.store(0);
   s.watcher_started.store(false);
   s.phase.store(0);
   s.pid = getpid();
@@ -167,6 +168,7 @@ void on_exit() {
   ShimState& s = shim();
   s.exiting.store(true);
   if (s.slot >= 0 && s.region.attached() && s.pid == getpid()) {
+    s.region.raw()->procs[s.slot].launches.store(s.launches.load());
     // Reference exit_handler [475-494]: release the slot and its charges.
     s.region.unregister_process(s.slot);
     s.slot = -1;
@@ -459,6 +461,9 @@ void apply_live_config() {
                   mask_on ? m.count() : a.cu_count, qs.size());
     }
   }
+  bool any = false;
+  for (int i = 0; i < s.n_agents; i++) any |= s.agents[i].temporal_active.load();
+  s.any_temporal.store(any);
   s.seen_generation.store(gen);
   if (s.phase.load() == 2) start_watcher_if_needed();
 }

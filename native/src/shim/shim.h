@@ -66,6 +66,8 @@ struct ShimState {
   std::atomic<bool> exiting{false};
   std::atomic<bool> watcher_started{false};
   std::atomic<uint64_t> seen_generation{0};         // region generation the queues reflect
+  std::atomic<uint64_t> launches{0};                // published to the region by the maintenance thread
+  std::atomic<bool> any_temporal{false};            // some agent is gated by the GPU-time limiter
   std::atomic<int64_t> ipc_bytes[kMaxDevices] = {};  // IPC-attached bytes per device
   std::mutex live_mu;                               // serialises live reconfiguration
 };

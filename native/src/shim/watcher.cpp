@@ -233,6 +233,7 @@ void* watcher_main(void*) {
         }
       }
       if (!s.hostpid) pid_attempts++;
+      if (s.slot >= 0) r->procs[s.slot].launches.store(s.launches.load(std::memory_order_relaxed));
       resync_context_charge();
       if (lease) {
         monitor_tick(r);
@@ -263,8 +264,9 @@ void start_watcher_if_needed() {
   ShimState& s = shim();
   if (!s.active) return;
   const Config& cfg = config();
-  bool need = cfg.active_oom_killer || cfg.memory_override || cfg.any_memory_limit() || !s.hostpid || any_temporal();
-  if (!need) return;
+  // Always: the thread also publishes the launch counter and applies live limit changes
+  // (it sleeps a whole period, 120 ms, between ticks unless the sampler runs).
+  (void)cfg;
   bool expected = false;
   if (!s.watcher_started.compare_exchange_strong(expected, true)) return;
   pthread_t th;
