@@ -30,6 +30,8 @@ amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle, uint32_t*, am
 amdsmi_status_t amdsmi_get_gpu_process_list(amdsmi_processor_handle, uint32_t*, amdsmi_proc_info_t*);
 rsmi_status_t rsmi_dev_memory_total_get(uint32_t, rsmi_memory_type_t, uint64_t*);
 rsmi_status_t rsmi_dev_memory_usage_get(uint32_t, rsmi_memory_type_t, uint64_t*);
+rsmi_status_t rsmi_compute_process_info_get(rsmi_process_info_t*, uint32_t*);
+rsmi_status_t rsmi_compute_process_info_by_pid_get(uint32_t, rsmi_process_info_t*);
 }
 
 namespace {
@@ -68,6 +70,8 @@ const Hook kHooks[] = {
     {"amdsmi_get_gpu_process_list", reinterpret_cast<void*>(&amdsmi_get_gpu_process_list)},
     {"rsmi_dev_memory_total_get", reinterpret_cast<void*>(&rsmi_dev_memory_total_get)},
     {"rsmi_dev_memory_usage_get", reinterpret_cast<void*>(&rsmi_dev_memory_usage_get)},
+    {"rsmi_compute_process_info_get", reinterpret_cast<void*>(&rsmi_compute_process_info_get)},
+    {"rsmi_compute_process_info_by_pid_get", reinterpret_cast<void*>(&rsmi_compute_process_info_by_pid_get)},
 };
 
 __attribute__((noinline)) void* maybe_hook(void* handle, const char* name, DlsymFn real) {
