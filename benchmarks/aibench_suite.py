@@ -43,10 +43,10 @@ sys.path.insert(0, REPO)
 T95 = {1: 12.71, 2: 4.30, 3: 3.18, 4: 2.78, 5: 2.57, 6: 2.45, 7: 2.36, 8: 2.31, 9: 2.26, 10: 2.23}
 
 
-def worker(cases, steps, warmup, out, seconds=0.0, sync_dir=None, tag="0", peers=1):
+def worker(cases, steps, warmup, out, seconds=0.0, sync_dir=None, tag="0", peers=1, autotune=1):
     import torch
     from amdvgpu.models.aibench import Runner, get_case
-    torch.backends.cudnn.benchmark = True  # MIOpen find mode (TF autotunes too)
+    torch.backends.cudnn.benchmark = bool(autotune)  # MIOpen find mode (TF autotunes too)
     res = {}
     for name in cases:
         case = get_case(name)
@@ -76,9 +76,12 @@ def worker(cases, steps, warmup, out, seconds=0.0, sync_dir=None, tag="0", peers
         json.dump(res, f)
 
 
+AUTOTUNE = 1
+
+
 def _cmd(cases, steps, warmup, out, extra=()):
     return [sys.executable, os.path.abspath(__file__), "--worker", "--cases", ",".join(cases), "--steps", str(steps),
-            "--warmup", str(warmup), "--out", out, *extra]
+            "--warmup", str(warmup), "--out", out, "--autotune", str(AUTOTUNE), *extra]
 
 
 def run_mode(mode, node, uuid, cases, steps, warmup):
@@ -188,11 +191,15 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--md-out", default=None)
+    ap.add_argument("--autotune", type=int, default=1,
+                    help="MIOpen find mode (cudnn.benchmark); 0 = deterministic heuristic solver choice")
     a = ap.parse_args()
+    global AUTOTUNE
+    AUTOTUNE = a.autotune
     from amdvgpu.models.aibench import CASES
     cases = [c.name for c in CASES] if a.cases == "all" else a.cases.split(",")
     if a.worker:
-        return worker(cases, a.steps, a.warmup, a.out, a.seconds, a.sync_dir, a.tag, a.peers)
+        return worker(cases, a.steps, a.warmup, a.out, a.seconds, a.sync_dir, a.tag, a.peers, a.autotune)
     from amdvgpu.plugin.devices import SysfsBackend
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     backend = SysfsBackend()
@@ -208,7 +215,7 @@ def main():
     md, summary = table(runs, vdm, cases)
     print(md)
     if a.json_out:
-        json.dump({"steps": a.steps, "warmup": a.warmup, "repeats": a.repeats, "summary": summary, "runs": runs,
+        json.dump({"steps": a.steps, "warmup": a.warmup, "repeats": a.repeats, "autotune": a.autotune, "summary": summary, "runs": runs,
                    "vdm": vdm}, open(a.json_out, "w"), indent=1)
     if a.md_out:
         open(a.md_out, "w").write(md + "\n")

@@ -3,11 +3,15 @@
 natively, inside a quota-only vGPU, and inside a 25 % temporal vGPU with the shim's roctx
 ranges on (VGPU_TRACE=1).
 
-    python tools/probe/prof_tenant.py --out gpurun_out/prof [--steps 30]
+    python tools/probe/prof_tenant.py --out gpurun_out/prof [--steps 30] [--case resnet50-inf]
+        [--modes native,vgpu-quota,vgpu-t25] [--runs 1] [--autotune 1]
 
-For every mode: `rocprofv3 --kernel-trace --marker-trace --stats -d <out>/<mode> --
-python3 prof_tenant.py --tenant ...` (the profiled program itself follows `--`), then a
-summary (kernel time per step, top kernels, vgpu:* marker time) in <out>/summary.md.
+For every mode (and run): `rocprofv3 --kernel-trace --marker-trace --stats -d
+<out>/<mode>.<run> -- python3 prof_tenant.py --tenant ...` (the profiled program itself
+follows `--`), then a summary (wall and GPU kernel time per step, top kernels, vgpu:*
+marker time) in <out>/summary.md. With --runs > 1 the same mode is profiled in several
+processes, which separates process-to-process variation (e.g. MIOpen picking different
+convolution solvers under autotuning) from the cost of the interception.
 """
 import argparse
 import csv
@@ -22,11 +26,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, REPO)
 
 
-def tenant(steps):
+def tenant(steps, case, autotune):
     import torch
     from amdvgpu.models.aibench import Runner, get_case
-    torch.backends.cudnn.benchmark = True
-    r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False)
+    torch.backends.cudnn.benchmark = bool(autotune)
+    r = Runner(get_case(case), "cuda:0", dtype=torch.float32, fuse=False)
     for _ in range(5):
         r.step()
     torch.cuda.synchronize()
@@ -52,6 +56,7 @@ def summarize(d, steps):
         out["kernels"] = sum(int(r["Calls"]) for r in rows)
         top = sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:5]
         out["top"] = [(r["Name"][:70], round(float(r["TotalDurationNs"]) / 1e6, 2), int(r["Calls"])) for r in top]
+        out["kernel_names"] = len(rows)
     mk = find(d, "*marker_api_trace.csv")
     if mk:
         rows = list(csv.DictReader(open(mk)))
@@ -71,37 +76,47 @@ def main():
     ap.add_argument("--out", default="gpurun_out/prof")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--tenant", action="store_true")
+    ap.add_argument("--case", default="resnet50-inf")
+    ap.add_argument("--modes", default="native,vgpu-quota,vgpu-t25")
+    ap.add_argument("--runs", type=int, default=1)
+    ap.add_argument("--autotune", type=int, default=1)
     a = ap.parse_args()
     if a.tenant:
-        return tenant(a.steps)
+        return tenant(a.steps, a.case, a.autotune)
     from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
-    modes = {
-        "native": None,
-        "vgpu-quota": vgpu_env(mem_limit=72 << 30),
-        "vgpu-t25": vgpu_env(mem_limit=72 << 30, cu_limit=25, cu_mode="temporal", extra={"VGPU_TRACE": "1"}),
+    contracts = {
+        "native": lambda: None,
+        "vgpu-quota": lambda: vgpu_env(mem_limit=72 << 30),
+        "vgpu-t25": lambda: vgpu_env(mem_limit=72 << 30, cu_limit=25, cu_mode="temporal", extra={"VGPU_TRACE": "1"}),
     }
     res = {}
-    for mode, c in modes.items():
-        env = apply_contract(c) if c else dict(os.environ)
-        d = os.path.join(a.out, mode)
-        cmd = ["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "-d", d, "-o", mode, "--",
-               sys.executable, os.path.abspath(__file__), "--tenant", "--steps", str(a.steps)]
-        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
-        if c:
-            cleanup_region(c)
-        line = [l for l in p.stdout.splitlines() if l.startswith("{")]
-        res[mode] = {"rc": p.returncode, **(json.loads(line[-1]) if line else {}), **summarize(d, a.steps)}
-        print(mode, json.dumps(res[mode]), flush=True)
-        if p.returncode != 0:
-            print(p.stderr[-3000:], file=sys.stderr)
-            break
-    md = ["# rocprofv3: stock fp32 ResNet-50 (b=50, 346²) native vs inside vGPUs", "",
-          "| mode | wall ms/step | GPU kernel ms/step | kernels | vgpu:* roctx ranges |", "|---|---|---|---|---|"]
-    for m, r in res.items():
+    for run in range(a.runs):
+        for mode in (a.modes.split(",") if run % 2 == 0 else a.modes.split(",")[::-1]):
+            c = contracts[mode]()
+            env = apply_contract(c) if c else dict(os.environ)
+            key = mode if a.runs == 1 else f"{mode}.{run}"
+            d = os.path.join(a.out, key)
+            cmd = ["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "-d", d, "-o", mode, "--",
+                   sys.executable, os.path.abspath(__file__), "--tenant", "--steps", str(a.steps), "--case", a.case,
+                   "--autotune", str(a.autotune)]
+            p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+            if c:
+                cleanup_region(c)
+            line = [l for l in p.stdout.splitlines() if l.startswith("{")]
+            res[key] = {"rc": p.returncode, **(json.loads(line[-1]) if line else {}), **summarize(d, a.steps)}
+            print(key, json.dumps(res[key]), flush=True)
+            if p.returncode != 0:
+                print(p.stderr[-3000:], file=sys.stderr)
+                raise SystemExit(p.returncode)
+    md = [f"# rocprofv3: stock fp32 {a.case} native vs inside vGPUs (autotune={a.autotune}, {a.steps} steps)", "",
+          "| mode | wall ms/step | GPU kernel ms/step | kernel launches | distinct kernels | vgpu:* roctx ranges |",
+          "|---|---|---|---|---|---|"]
+    for m, r in sorted(res.items()):
         mk = ", ".join(f"{k} x{v['count']} {v['ms']} ms" for k, v in (r.get("markers") or {}).items()) or "-"
         md.append(f"| {m} | {r.get('ms_per_step', 0):.2f} | {r.get('kernel_ms_per_step', 0):.2f} | "
-                  f"{r.get('kernels', 0)} | {mk} |")
-    md += ["", "Top kernels (native): " + "; ".join(f"{n} {t} ms x{c}" for n, t, c in res["native"].get("top", []))]
+                  f"{r.get('kernels', 0)} | {r.get('kernel_names', 0)} | {mk} |")
+    for m, r in sorted(res.items()):
+        md += ["", f"Top kernels ({m}): " + "; ".join(f"{n} {t} ms x{c}" for n, t, c in r.get("top", []))]
     os.makedirs(a.out, exist_ok=True)
     open(os.path.join(a.out, "summary.md"), "w").write("\n".join(md) + "\n")
     json.dump(res, open(os.path.join(a.out, "summary.json"), "w"), indent=1)
