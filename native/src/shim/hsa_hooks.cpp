@@ -77,11 +77,12 @@ bool should_spill(int dev, size_t size) {
   const Config& cfg = config();
   const uint64_t hbm = s.region.hbm_limit(dev);
   if (!cfg.oversubscribe || !hbm) return false;
+  // The caller has already charged `size` as data, so `resident` includes this request.
   const uint64_t resident = s.region.resident(dev);
   const bool large = cfg.spill_policy == SpillPolicy::kLargeFirst && size >= cfg.spill_large_bytes;
-  if (!large) return resident + size > hbm;
+  if (!large) return resident > hbm;
   const uint64_t reserve = spill_reserve(cfg, hbm);
-  if (resident + size + reserve > hbm) return true;
+  if (resident + reserve > hbm) return true;
   VGPU_REAL_HSA(hsa_agent_get_info);
   uint64_t avail = 0;
   if (real_hsa_agent_get_info(s.agents[dev].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &avail) ==

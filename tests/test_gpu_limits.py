@@ -355,7 +355,7 @@ emit(after_big=after_big, after_small=after_small, ok=ok)
 
 @pytest.mark.parametrize("policy", ["large-first", "first-come"])
 def test_spill_placement_policy(tmp_region, policy):
-    """Virtual device memory with an 8 GiB HBM share: first-come fills HBM with the eight
+    """Virtual device memory with an 8 GiB HBM share: first-come fills HBM with seven
     1 GiB buffers and spills the later small (hot) allocations; large-first spills large
     buffers once they would eat into the share's reserve (3 GiB here), so the 2 GiB of
     small ones still find HBM."""

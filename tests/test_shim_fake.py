@@ -185,3 +185,31 @@ def test_launch_block_and_counter(fake):
         assert p.wait(30) == 0
     launch = [o for o in out if "launch" in o][0]
     assert launch["wall"] >= 0.9 and launches_blocked <= 1
+
+
+@pytest.mark.parametrize("policy", ["large-first", "first-come"])
+def test_spill_placement_policy(fake, policy):
+    """Virtual device memory: 16 GiB quota with an 8 GiB HBM share. First-come keeps the
+    first eight 1 GiB buffers in HBM and sends the later small (hot) ones to host memory;
+    large-first spills the large buffers once they would eat into the 3 GiB reserve, so
+    all 2 GiB of small ones stay in HBM. Exact byte counts: the fake has no context."""
+    e = fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="16g", VGPU_DEVICE_HBM_LIMIT_0="8192m",
+             VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY=policy, VGPU_SPILL_RESERVE="3g")
+    ops = ["malloc=1g"] * 10 + ["sleep=1"] + ["malloc=32m"] * 64 + ["sleep=1"]
+    p = subprocess.Popen([HARNESS, *ops], env=e, stdout=subprocess.PIPE, text=True)
+    mallocs, snaps = [], []
+    p.stdout.readline()   # header: the shim is initialised and the region exists
+    with Region(fake.region) as r:
+        for line in iter(p.stdout.readline, ""):
+            o = json.loads(line)
+            if "malloc" in o:
+                mallocs.append(o["malloc"])
+                if len(mallocs) in (10, 74):   # last of a group: the harness now sleeps 1 s
+                    snaps.append(r.device(0)["spilled"])
+    assert p.wait(30) == 0
+    assert mallocs == ["ok"] * 74
+    after_big, after_small = snaps
+    if policy == "large-first":
+        assert after_big == 5 * GiB and after_small == after_big     # 5 resident + 3 GiB reserve
+    else:
+        assert after_big == 2 * GiB and after_small - after_big == 2 * GiB   # HBM full after 8

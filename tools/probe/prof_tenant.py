@@ -96,7 +96,8 @@ def main():
             env = apply_contract(c) if c else dict(os.environ)
             key = mode if a.runs == 1 else f"{mode}.{run}"
             d = os.path.join(a.out, key)
-            cmd = ["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "-d", d, "-o", mode, "--",
+            cmd = ["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "--output-format", "csv", "-d", d, "-o", mode,
+                   "--",
                    sys.executable, os.path.abspath(__file__), "--tenant", "--steps", str(a.steps), "--case", a.case,
                    "--autotune", str(a.autotune)]
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
@@ -104,6 +105,9 @@ def main():
                 cleanup_region(c)
             line = [l for l in p.stdout.splitlines() if l.startswith("{")]
             res[key] = {"rc": p.returncode, **(json.loads(line[-1]) if line else {}), **summarize(d, a.steps)}
+            for f in glob.glob(os.path.join(d, "**", "*"), recursive=True):  # keep the per-kernel stats only
+                if os.path.isfile(f) and not f.endswith("_stats.csv"):
+                    os.unlink(f)
             print(key, json.dumps(res[key]), flush=True)
             if p.returncode != 0:
                 print(p.stderr[-3000:], file=sys.stderr)
