@@ -96,7 +96,7 @@ _FLAGS = [
     ("--enable-legacy-preferred", "enable_legacy_preferred", "bool", ["ENABLE_LEGACY_PREFERRED"],
      "preferred allocation for kubelets without GetPreferredAllocation"),
     ("--verbose", "verbose", int, ["VERBOSE"], "log verbosity"),
-    ("--cu-mode", "cu_mode", str, ["CU_MODE"], "CU limit enforcement: auto (spatial for shares >= 50 %, temporal below) | spatial | "
+    ("--cu-mode", "cu_mode", str, ["CU_MODE"], "CU limit enforcement: auto (spatial for shares >= 50 %%, temporal below) | spatial | "
      "temporal | both | off"),
     ("--backend", "backend", str, ["DEVICE_BACKEND"], "device backend: auto | amdsmi | sysfs | fake"),
     ("--fake-devices", "fake_devices", str, ["FAKE_DEVICES"], "JSON spec (or file) for the fake backend"),

@@ -3,7 +3,8 @@
 Reference: ``vdevice.go`` — ``VDevice{dev, memory}`` (:29-33), ``Device2VDevice``
 (:36-58, memory per vGPU = ``totalMiB * memScaling / split`` at :49, MIG devices get one
 vdevice with memory 0), ``VDevicesByIDs`` (:61-75), ``UniqueDeviceIDs`` (:78-90); and the
-SM limit ``int(100 * coresScaling / split)`` emitted for every vdevice (``server.go:492``).
+SM limit ``int(100 * coresScaling / split)`` emitted for every vdevice (``server.go:492``;
+rounded up here, see ``device_to_vdevices``).
 
 MI355X additions:
 * every vGPU carries its own CU share *and* a logical CU range. Slot ``i`` of a GPU gets
@@ -19,6 +20,7 @@ MI355X additions:
 The CU arithmetic here is the Python twin of ``native/src/core/cumask.cpp``
 (cross-checked by tests/test_vdevice.py).
 """
+import math
 from dataclasses import dataclass
 
 MiB = 1 << 20
@@ -90,7 +92,12 @@ def device_to_vdevices(devices, split, memory_scaling=1.0, cores_scaling=1.0):
         total_mib = d.memory_total // MiB
         mem = int(total_mib * memory_scaling / split) * MiB
         hbm = int(total_mib / split) * MiB if memory_scaling > 1 else 0
-        pct = int(100 * cores_scaling / split)
+        # Rounded up, unlike the reference's int(): the shares of a fully split GPU then
+        # sum to >= 100 %, so N busy temporal tenants (each charged 1/N of the time)
+        # are never throttled below the whole GPU (int() leaves up to N-1 % idle, e.g.
+        # 8 x 12 % = 96 %). Spatial slices are unchanged (cu_share_count rounds down to
+        # whole XCD columns, which fit the partition slice).
+        pct = math.ceil(round(100 * cores_scaling / split, 6))
         if pct >= 100:
             pct = 0
         for i in range(split):

@@ -43,7 +43,32 @@ sys.path.insert(0, REPO)
 T95 = {1: 12.71, 2: 4.30, 3: 3.18, 4: 2.78, 5: 2.57, 6: 2.45, 7: 2.36, 8: 2.31, 9: 2.26, 10: 2.23}
 
 
+def parse_cpulist(text):
+    cpus = set()
+    for part in text.strip().split(","):
+        if "-" in part:
+            lo, hi = part.split("-")
+            cpus.update(range(int(lo), int(hi) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
+
+
+def gpu_local_cpus(bdf):
+    """CPUs of the GPU's NUMA node that this process may run on (empty = do not pin).
+    Launch-bound cases (small batches, thousands of kernels per step) run measurably
+    slower from a remote NUMA node, which otherwise shows up as process-to-process
+    jitter in both columns."""
+    try:
+        local = parse_cpulist(open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read())
+    except (OSError, ValueError):
+        return []
+    return sorted(local & os.sched_getaffinity(0))
+
+
 def worker(cases, steps, warmup, out, seconds=0.0, sync_dir=None, tag="0", peers=1, autotune=1):
+    if os.environ.get("AIBENCH_CPUS"):
+        os.sched_setaffinity(0, parse_cpulist(os.environ["AIBENCH_CPUS"]))
     import torch
     from amdvgpu.models.aibench import Runner, get_case
     torch.backends.cudnn.benchmark = bool(autotune)  # MIOpen find mode (TF autotunes too)
@@ -174,6 +199,29 @@ def vdm_baseline(c):
     return VDM_V100.get(c.test_id, "-")
 
 
+def merge(paths, json_out, md_out):
+    """One table over several suite runs (e.g. the two halves of the ten cases)."""
+    from amdvgpu.models.aibench import CASES
+    parts = [json.load(open(p)) for p in paths]
+    n = min(len(p["runs"]) for p in parts)
+    runs = [{} for _ in range(n)]
+    vdm = {}
+    for p in parts:
+        for i in range(n):
+            for mode, res in p["runs"][i].items():
+                runs[i].setdefault(mode, {}).update(res)
+        vdm.update(p.get("vdm") or {})
+    have = set().union(*(r["native"].keys() for r in runs))
+    cases = [c.name for c in sorted(CASES, key=lambda c: c.test_id) if c.name in have]
+    md, summary = table(runs, vdm, cases)
+    print(md)
+    if json_out:
+        json.dump({"merged": paths, "repeats": n, "summary": summary, "runs": runs, "vdm": vdm}, open(json_out, "w"),
+                  indent=1)
+    if md_out:
+        open(md_out, "w").write(md + "\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default="all")
@@ -191,6 +239,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--md-out", default=None)
+    ap.add_argument("--merge", nargs="+", default=None,
+                    help="render one table from the --json-out files of runs over disjoint case lists")
+    ap.add_argument("--pin", type=int, default=1, help="pin every worker to the GPU's NUMA-local CPUs")
     ap.add_argument("--autotune", type=int, default=1,
                     help="MIOpen find mode (cudnn.benchmark); 0 = deterministic heuristic solver choice")
     a = ap.parse_args()
@@ -200,10 +251,17 @@ def main():
     cases = [c.name for c in CASES] if a.cases == "all" else a.cases.split(",")
     if a.worker:
         return worker(cases, a.steps, a.warmup, a.out, a.seconds, a.sync_dir, a.tag, a.peers, a.autotune)
+    if a.merge:
+        return merge(a.merge, a.json_out, a.md_out)
     from amdvgpu.plugin.devices import SysfsBackend
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     backend = SysfsBackend()
-    uuid = backend.devices()[0].uuid
+    dev = backend.devices()[0]
+    uuid = dev.uuid
+    cpus = gpu_local_cpus(dev.bdf) if a.pin else []
+    if cpus:
+        os.environ["AIBENCH_CPUS"] = ",".join(map(str, cpus))
+    print(f"GPU {dev.bdf}: workers pinned to {len(cpus)} NUMA-local CPUs" if cpus else "workers not pinned", flush=True)
     modes = a.modes.split(",")
     runs, vdm = [], {}
     with NodeHarness(backend, device_split_count=2, device_memory_scaling=1.8) as node:
@@ -215,7 +273,8 @@ def main():
     md, summary = table(runs, vdm, cases)
     print(md)
     if a.json_out:
-        json.dump({"steps": a.steps, "warmup": a.warmup, "repeats": a.repeats, "autotune": a.autotune, "summary": summary, "runs": runs,
+        json.dump({"steps": a.steps, "warmup": a.warmup, "repeats": a.repeats, "autotune": a.autotune,
+                   "pinned_cpus": len(cpus), "summary": summary, "runs": runs,
                    "vdm": vdm}, open(a.json_out, "w"), indent=1)
     if a.md_out:
         open(a.md_out, "w").write(md + "\n")

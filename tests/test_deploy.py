@@ -65,3 +65,16 @@ def test_image_build_inputs_exist():
     installed = re.search(r"for f in ([^;]+);", ep).group(1).split()
     assert set(installed) == set(targets) | {"ld.so.preload"}
     assert "lock" in ep and "containers" in ep
+
+
+def test_image_rehearsal_builds_and_entrypoint_installs(tmp_path):
+    """docker/Dockerfile replayed stage by stage without a container engine
+    (tools/image_rehearsal.py): the build stage compiles the product from the filtered
+    context, the runtime stage's entrypoint installs the data plane and starts the
+    plugin's CLI (--help)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import image_rehearsal
+    stages, final = image_rehearsal.rehearse(str(tmp_path), log=lambda *_: None)
+    out = image_rehearsal.check_runtime(final, str(tmp_path), log=lambda *_: None)
+    assert "--device-split-count" in out and "--cu-mode" in out

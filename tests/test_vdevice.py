@@ -85,3 +85,16 @@ def test_partition_ranges_cover_chip_disjointly():
 
 def test_cu_range_for_clamps():
     assert cu_range_for(256, 8, 4, 3, 50) == (128, 256)
+
+
+@pytest.mark.parametrize("split,pct", [(2, 50), (3, 34), (4, 25), (6, 17), (8, 13), (10, 10)])
+def test_cu_share_rounds_up_so_shares_cover_the_gpu(split, pct):
+    """A fully split GPU's temporal shares sum to >= 100 %, so N busy tenants are never
+    throttled below the whole GPU (the reference's int() gives 8 x 12 % = 96 %)."""
+    dev = FakeBackend(n=1).devices()
+    vds = device_to_vdevices(dev, split)
+    assert {v.cu_pct for v in vds} == {pct}
+    assert sum(v.cu_pct for v in vds) >= 100
+    # spatial slices stay disjoint
+    rngs = sorted(v.cu_range for v in vds)
+    assert all(a[1] <= b[0] for a, b in zip(rngs, rngs[1:]))
