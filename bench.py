@@ -140,19 +140,33 @@ def worker(args):
         res = {"mode": args.mode, "ms_per_step": dt * 1000.0 / n, "items_per_step": runner.items_per_step,
                "steps": n, "t0": t0, "t1": t0 + dt}
     else:
+        # The limiter's own account of the timed window (GPU time charged / wall time), read
+        # from the pod's shared region like vgpuctl would: what the vGPU granted this pod.
+        region = None
+        if not cpu and os.environ.get("VGPU_SHARED_CACHE") and os.path.exists(os.environ["VGPU_SHARED_CACHE"]):
+            from amdvgpu.shim.region import Region
+            region = Region(os.environ["VGPU_SHARED_CACHE"])
         barrier()
+        g0 = region.device(0) if region else None
         t0 = time.perf_counter()
         for _ in range(args.steps):
             runner.step()
         sync()
         barrier()
         dt = time.perf_counter() - t0
+        g1 = region.device(0) if region else None
         ms = torch.tensor([dt * 1000.0 / args.steps], dtype=torch.float64, device=device)
         if world > 1:
             dist.all_reduce(ms, op=dist.ReduceOp.MAX)
         res = {"mode": args.mode, "ms_per_step": ms.item(), "items_per_step": runner.items_per_step,
                "steps": args.steps, "mem_total": total,
                "peak_allocated": torch.cuda.max_memory_allocated(device) if not cpu else 0}
+        if g0 and g1 and g1["wall_ns"] > g0["wall_ns"]:
+            res["limiter_granted_pct"] = round(100.0 * (g1["charged_ns"] - g0["charged_ns"]) /
+                                               (g1["wall_ns"] - g0["wall_ns"]), 2)
+            res["gpu_ms_charged_per_step"] = round((g1["charged_ns"] - g0["charged_ns"]) / 1e6 / args.steps, 3)
+        if region:
+            region.close()
     if args.result_file and (rank == 0 or world == 1):
         with open(args.result_file, "w") as f:
             json.dump(res, f)
@@ -356,6 +370,9 @@ def main(argv=None):
             # The pod's throughput over what its compute share entitles it to (native x share).
             line["entitlement_ratio"] = round(nat / (ms * share), 3)
             line["overhead_pct_vs_native_x_share"] = round((ms * share - nat) / nat * 100.0, 3)
+            for k in ("limiter_granted_pct", "gpu_ms_charged_per_step"):
+                if k in results["vgpu"]:
+                    line[k] = results["vgpu"][k]
         if "quota" in results:
             q = results["quota"]["ms_per_step"]
             line["ms_per_batch_quota_only"] = round(q, 4)
