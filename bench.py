@@ -66,6 +66,7 @@ def parse(argv=None):
     ap.add_argument("--sweep-tenants", default="1,2,4,8")
     ap.add_argument("--sweep-seconds", type=float, default=6.0)
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
+    ap.add_argument("--rccl-probe", type=int, default=1, help="N>1: RCCL all-reduce between the pods afterwards")
     # worker-only
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--mode", default=None, help=argparse.SUPPRESS)
@@ -96,11 +97,14 @@ def worker(args):
     if not cpu:
         torch.cuda.set_device(device)
     if world > 1:
+        # The pods are independent tenants (no gradient exchange): the cross-rank group only
+        # brackets the timed window and takes the max, so it runs on gloo over TCP and the
+        # measurement cannot depend on GPU peer access between pods. RCCL through the shim
+        # is exercised separately (mode "rccl").
         init = f"tcp://{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{args.port}"
-        if cpu:
-            dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
-        else:
-            dist.init_process_group("nccl", init_method=init, rank=rank, world_size=world, device_id=device)
+        dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    if args.mode == "rccl":
+        return rccl_probe(args, device, rank, world)
     sync = (lambda: None) if cpu else (lambda: torch.cuda.synchronize(device))
     free0, total = torch.cuda.mem_get_info(device) if not cpu else (0, 0)
     quota = int(os.environ.get("VGPU_DEVICE_MEMORY_LIMIT_0", "0").rstrip("m") or 0) << 20
@@ -120,9 +124,9 @@ def worker(args):
     sync()
 
     def barrier():
-        if world > 1:
-            dist.barrier(device_ids=[0]) if not cpu else dist.barrier()
         sync()
+        if world > 1:
+            dist.barrier()
 
     if args.go:  # concurrent tenants: start together, run for a fixed wall time
         open(args.result_file + ".ready", "w").close()
@@ -155,7 +159,7 @@ def worker(args):
         barrier()
         dt = time.perf_counter() - t0
         g1 = region.device(0) if region else None
-        ms = torch.tensor([dt * 1000.0 / args.steps], dtype=torch.float64, device=device)
+        ms = torch.tensor([dt * 1000.0 / args.steps], dtype=torch.float64)
         if world > 1:
             dist.all_reduce(ms, op=dist.ReduceOp.MAX)
         res = {"mode": args.mode, "ms_per_step": ms.item(), "items_per_step": runner.items_per_step,
@@ -173,6 +177,37 @@ def worker(args):
     if world > 1:
         barrier()
         dist.destroy_process_group()
+    return 0
+
+
+def rccl_probe(args, device, rank, world):
+    """RCCL all-reduce between the ranks' vGPU pods, through the shim (IPC / peer access
+    must pass untouched and imports must not be charged twice). Reports bus bandwidth;
+    runs after the measurement in its own process, bounded by the parent's timeout."""
+    import torch
+    import torch.distributed as dist
+    cpu = args.cpu_rehearsal
+    pg = dist.new_group(backend="gloo" if cpu else "nccl")
+    sync = (lambda: None) if cpu else (lambda: torch.cuda.synchronize(device))
+    total = torch.cuda.mem_get_info(device)[1] if not cpu else 0
+    n = (1 << 16) if cpu else (64 << 20)  # 64 Mi floats = 256 MiB per rank
+    x = torch.full((n,), float(rank + 1), device=device)
+    dist.all_reduce(x, group=pg)
+    sync()
+    ok = bool(torch.allclose(x[:1024], torch.full((1024,), world * (world + 1) / 2.0, device=device)))
+    iters = 10
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(x, group=pg)
+    sync()
+    dt = (time.perf_counter() - t0) / iters
+    busbw = 2 * (world - 1) / world * n * 4 / dt / 1e9
+    res = {"ok": ok, "backend": "gloo (cpu rehearsal)" if cpu else "nccl (RCCL)", "bytes": n * 4,
+           "ms": round(dt * 1000, 3), "busbw_GBps": round(busbw, 1), "mem_get_info_total": total}
+    if args.result_file and rank == 0:
+        with open(args.result_file, "w") as f:
+            json.dump(res, f)
+    dist.destroy_process_group()
     return 0
 
 
@@ -224,6 +259,31 @@ def run_one(args, mode, env, port):
             return None
         with open(result) as f:
             return json.load(f)
+    finally:
+        os.unlink(result)
+
+
+def probe_rccl(args, env, port, timeout=240):
+    """RCCL all-reduce across the ranks' vGPU pods (never fails the bench: a failure or
+    timeout is reported as such)."""
+    fd, result = tempfile.mkstemp(prefix="bench-rccl-", suffix=".json")
+    os.close(fd)
+    p = subprocess.Popen(worker_cmd(args, "rccl", result, port), env=env)
+    try:
+        rc = p.wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.wait()
+        rc = "timeout"
+    try:
+        if rc != 0:
+            return {"ok": False, "error": f"exit {rc}"}
+        if int(os.environ.get("RANK", 0)) != 0:
+            return None
+        with open(result) as f:
+            return json.load(f)
+    except (OSError, ValueError) as e:
+        return {"ok": False, "error": repr(e)[:200]}
     finally:
         os.unlink(result)
 
@@ -319,6 +379,12 @@ def main(argv=None):
                 env, contracts[mode] = pod_env(node, node.vgpu_ids(uuid)[:1], extra)
                 results[mode] = run_one(args, mode, env, port)
         port += 1
+    rccl = None
+    if world > 1 and args.rccl_probe:
+        with NodeHarness(backend, device_split_count=args.split, cu_mode=args.cu_mode) as node:
+            env, _ = pod_env(node, node.vgpu_ids(uuid)[:1])
+            rccl = probe_rccl(args, env, port)
+        port += 1
     do_sweep = args.sweep == "on" or (args.sweep == "auto" and world == 1 and not cpu)
     sweep_rows, max_vgpus = ([], None)
     if do_sweep:
@@ -391,6 +457,8 @@ def main(argv=None):
                 "entitlement_ratio": round(nat / (p * (pct / 100.0 if 0 < pct < 100 else 1.0)), 3)}
         # Reference's own vGPU overhead on this case (2xV100, BASELINE.md "Derived ms/batch").
         line["reference_overhead_pct"] = round((case.baseline_native / case.baseline_vgpu - 1) * 100.0, 2)
+    if rccl is not None:
+        line["rccl_allreduce_between_pods"] = rccl
     if do_sweep:
         line["max_vgpus_per_gpu"] = max_vgpus
         line["max_vgpus_criterion"] = (f"largest N with aggregate >= {SWEEP_MIN_AGGREGATE}x one whole-GPU pod and "
