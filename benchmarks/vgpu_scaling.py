@@ -56,7 +56,17 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
 MODES = {"default": "auto", "spatial": "spatial", "temporal": "temporal", "shared": "off"}
 
 
-def run_point(backend, uuid, case, n, policy, warmup, seconds):
+def kfd_queue_count():
+    """User-mode queues of every process on the node's GPUs (KFD sysfs), or None."""
+    root = "/sys/class/kfd/kfd/proc"
+    try:
+        return sum(len(os.listdir(os.path.join(root, p, "queues"))) for p in os.listdir(root)
+                   if os.path.isdir(os.path.join(root, p, "queues")))
+    except OSError:
+        return None
+
+
+def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="scal-")
@@ -68,7 +78,10 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds):
             out = os.path.join(tmp, f"t{i}.json")
             cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--case", case, "--warmup", str(warmup),
                    "--seconds", str(seconds), "--out", out, "--go", go]
-            procs.append(subprocess.Popen(cmd, env=apply_contract(envs, mounts)))
+            env = apply_contract(envs, mounts)
+            if hw_queues:
+                env["GPU_MAX_HW_QUEUES"] = str(hw_queues)
+            procs.append(subprocess.Popen(cmd, env=env))
             outs.append(out)
         try:
             deadline = time.time() + 600
@@ -76,6 +89,7 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds):
                 if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
                     raise SystemExit("a tenant failed before the start barrier")
                 time.sleep(0.05)
+            queues = kfd_queue_count()
             open(go, "w").close()
             for p in procs:
                 if p.wait(timeout=900) != 0:
@@ -87,7 +101,8 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds):
                     p.kill()
     span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
     agg = sum(r["batch"] * r["steps"] for r in res) / span
-    return {"tenants": n, "policy": policy, "aggregate_throughput": agg,
+    return {"tenants": n, "policy": policy, "hw_queues": hw_queues or None, "kfd_queues": queues,
+            "aggregate_throughput": agg,
             "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res]}
 
 
@@ -98,6 +113,7 @@ def main():
     ap.add_argument("--policy", default="default,spatial,shared")
     ap.add_argument("--seconds", type=float, default=6.0)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--hw-queues", default="0", help="GPU_MAX_HW_QUEUES per pod (comma list; 0 = HIP default)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--go")
@@ -110,19 +126,22 @@ def main():
     backend = SysfsBackend()
     uuid = backend.devices()[0].uuid
     rows = []
-    for pol in a.policy.split(","):
-        for n in [int(x) for x in a.tenants.split(",")]:
-            r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds)
-            rows.append(r)
-            print(json.dumps(r), flush=True)
+    for hq in [int(x) for x in a.hw_queues.split(",")]:
+        for pol in a.policy.split(","):
+            for n in [int(x) for x in a.tenants.split(",")]:
+                r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq)
+                rows.append(r)
+                print(json.dumps(r), flush=True)
     base = {r["policy"]: r["aggregate_throughput"] for r in rows if r["tenants"] == 1}
     md = [f"# concurrent vGPU pods on one MI355X — {a.case} (stock fp32; contracts from Allocate)", "",
-          "| policy (--cu-mode) | pods | aggregate | vs 1 pod | per pod (min..max) | slowest pod vs 1/N |",
-          "|---|---|---|---|---|---|"]
+          "| policy (--cu-mode) | HW queues/pod | KFD queues | pods | aggregate | vs 1 pod | per pod (min..max) | "
+          "slowest pod vs 1/N |",
+          "|---|---|---|---|---|---|---|---|"]
     for r in rows:
         pt = r["per_tenant"]
         b = base.get(r["policy"], rows[0]["aggregate_throughput"])
-        md.append(f"| {r['policy']} ({MODES[r['policy']]}) | {r['tenants']} | {r['aggregate_throughput']:.1f} | "
+        md.append(f"| {r['policy']} ({MODES[r['policy']]}) | {r['hw_queues'] or 'default'} | {r['kfd_queues']} | "
+                  f"{r['tenants']} | {r['aggregate_throughput']:.1f} | "
                   f"{r['aggregate_throughput'] / b:.2f}x | {min(pt):.1f} .. {max(pt):.1f} | "
                   f"{min(pt) / (b / r['tenants']):.2f} |")
     print("\n".join(md))
