@@ -263,7 +263,7 @@ def run_one(args, mode, env, port):
         os.unlink(result)
 
 
-def probe_rccl(args, env, port, timeout=240):
+def probe_rccl(args, env, port, timeout=120):
     """RCCL all-reduce across the ranks' vGPU pods (never fails the bench: a failure or
     timeout is reported as such)."""
     fd, result = tempfile.mkstemp(prefix="bench-rccl-", suffix=".json")

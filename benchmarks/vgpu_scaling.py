@@ -85,9 +85,14 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0):
             outs.append(out)
         try:
             deadline = time.time() + 600
+            beat = time.time()
             while not all(os.path.exists(o + ".ready") for o in outs):
                 if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
                     raise SystemExit("a tenant failed before the start barrier")
+                if time.time() - beat > 30:
+                    beat = time.time()
+                    print(f"  waiting: {sum(os.path.exists(o + '.ready') for o in outs)}/{n} pods warmed up",
+                          flush=True)
                 time.sleep(0.05)
             queues = kfd_queue_count()
             open(go, "w").close()

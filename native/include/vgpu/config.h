@@ -70,6 +70,7 @@ struct Config {
   bool memory_override = false;          // VGPU_MEMORY_OVERRIDE
   bool signal_control = false;           // VGPU_SIGNAL_CONTROL: also honour SIGUSR1/2
   bool hook_smi = true;                  // VGPU_HOOK_SMI: virtualise amd-smi/rocm-smi
+  bool virtual_cu_count = true;          // VGPU_VIRTUAL_CU_COUNT: report the spatial slice's CUs
   int util_period_ms = 120;              // monitor / OOM-killer / accounting period (reference: 120 ms)
   int util_sample_us = 1000;             // temporal-mode occupancy sampling interval
   int limiter_window_ms = 40;            // temporal-mode credit window (ratelimit.h)

@@ -256,6 +256,7 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   cfg->memory_override = parse_bool(getenv_fn("VGPU_MEMORY_OVERRIDE"), false);
   cfg->signal_control = parse_bool(getenv_fn("VGPU_SIGNAL_CONTROL"), false);
   cfg->hook_smi = parse_bool(getenv_fn("VGPU_HOOK_SMI"), true);
+  cfg->virtual_cu_count = parse_bool(getenv_fn("VGPU_VIRTUAL_CU_COUNT"), true);
   long period = 120;
   if (parse_int(getenv_fn("VGPU_UTIL_PERIOD_MS"), 10, 10000, &period)) cfg->util_period_ms = (int)period;
   long sample = 1000;

@@ -254,6 +254,20 @@ hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* 
   VGPU_STAT(kStatAgentInfo);
   if (!real_hsa_agent_get_info) return HSA_STATUS_ERROR;
   hsa_status_t st = real_hsa_agent_get_info(agent, attr, value);
+  if (((int)attr == HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT ||
+       (int)attr == HSA_AMD_AGENT_INFO_COOPERATIVE_COMPUTE_UNIT_COUNT) && st == HSA_STATUS_SUCCESS) {
+    // Reference: cuDeviceGetAttribute virtualisation [device.c:130-134]. Here the CU
+    // count follows the spatial slice (AgentInfo::visible_cus), read once by CLR at init
+    // (its maxComputeUnits / hipDeviceProp multiProcessorCount come from the cooperative
+    // count, the total CU count from the other attribute).
+    const bool r = ready();
+    int dev = r ? agent_ordinal(agent) : -1;
+    int n = dev >= 0 ? shim().agents[dev].visible_cus.load(std::memory_order_relaxed) : 0;
+    VLOG_DEBUG("agent_info CU count (attr %#x): dev=%d real=%u visible=%d", (unsigned)attr, dev,
+               *static_cast<uint32_t*>(value), n);
+    if (n > 0 && (uint32_t)n < *static_cast<uint32_t*>(value)) *static_cast<uint32_t*>(value) = (uint32_t)n;
+    return st;
+  }
   if (__builtin_expect((int)attr != HSA_AMD_AGENT_INFO_MEMORY_AVAIL, 1) || st != HSA_STATUS_SUCCESS) return st;
   if (!ready()) return st;
   int dev = agent_ordinal(agent);

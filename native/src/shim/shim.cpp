@@ -433,6 +433,10 @@ void apply_live_config() {
     }
     a.mask = m;
     a.mode = mode;
+    // Libraries size grids and pick kernels from the CU count (hipDeviceProp
+    // multiProcessorCount, which CLR reads from the agent): under a spatial mask report
+    // the slice, so stock MIOpen / hipBLASLt / PyTorch launches fit the CUs they get.
+    a.visible_cus.store(mask_on && cfg.virtual_cu_count ? m.count() : 0);
     a.temporal_active.store(temp_on);
     int flags = (mask_on ? 1 : 0) | (temp_on ? 2 : 0);
     d.cu_mode.store(flags);

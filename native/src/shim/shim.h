@@ -33,6 +33,7 @@ struct AgentInfo {
   int max_waves_per_cu = 32;
   uint64_t phys_total = 0;
   std::atomic<bool> mask_active{false};      // spatial mask applied to its queues
+  std::atomic<int> visible_cus{0};           // CU count reported to the runtime (0 = the real one)
   bool authorised = true;                    // listed in VGPU_ALLOWLIST (when one is configured)
   std::atomic<bool> temporal_active{false};  // GPU-time credit gates its launches
   CuMode mode = CuMode::kOff;                // effective enforcement mode

@@ -214,4 +214,14 @@ uint64_t fake_hip_busy_us(int dev, uint64_t* kernels) {
 
 hsa_queue_t* fake_hip_stream_queue(hipStream_t stream) { return reinterpret_cast<FakeStream*>(stream)->q; }
 
+// The CU count as CLR sees it (hipDeviceProp multiProcessorCount): the agent query goes
+// through the preloaded shim like the real runtime's.
+int fake_hip_device_cus(int dev) {
+  init();
+  if (dev < 0 || dev >= g_n) return -1;
+  uint32_t v = 0;
+  hsa_agent_get_info(g_dev[dev].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_COOPERATIVE_COMPUTE_UNIT_COUNT, &v);
+  return (int)v;
+}
+
 }  // extern "C"

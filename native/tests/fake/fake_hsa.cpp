@@ -185,6 +185,7 @@ hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* 
   if (d < 0) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
   switch ((int)attr) {
     case HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT: *static_cast<uint32_t*>(value) = s.cus; break;
+    case HSA_AMD_AGENT_INFO_COOPERATIVE_COMPUTE_UNIT_COUNT: *static_cast<uint32_t*>(value) = s.cus; break;
     case HSA_AMD_AGENT_INFO_NUM_XCC: *static_cast<uint32_t*>(value) = s.xcc; break;
     case HSA_AMD_AGENT_INFO_NUM_SHADER_ENGINES: *static_cast<uint32_t*>(value) = s.se; break;
     case HSA_AMD_AGENT_INFO_DRIVER_UID: *static_cast<uint32_t*>(value) = s.gpus[d].gpu_id; break;

@@ -14,6 +14,7 @@
 //   graph=US,SECS    like run, with hipGraphLaunch of a US-microsecond "graph"
 //   internal=SIZE    runtime-internal device memory (bypasses every hook; negative frees)
 //   queues           CU-mask bit count, mask changes and priority of every created stream
+//   cus              the current device's CU count as the runtime sees it
 //   sleep=SECS
 #define __HIP_PLATFORM_AMD__ 1
 #include <hip/hip_runtime_api.h>
@@ -34,6 +35,7 @@ hsa_queue_t* fake_hip_stream_queue(hipStream_t stream);
 int fake_rocr_queue_state(const hsa_queue_t* queue, uint32_t* mask_words8, int* priority, int* device);
 int fake_rocr_internal_alloc(int dev, int64_t bytes);
 int fake_rocr_host_pid();
+int fake_hip_device_cus(int dev);
 }
 
 namespace {
@@ -127,6 +129,8 @@ int main(int argc, char** argv) {
                sets, prio, m[0]);
       }
       printf("]}\n");
+    } else if (key == "cus") {
+      printf("{\"dev\": %d, \"cus\": %d}\n", dev, fake_hip_device_cus(dev));
     } else if (key == "sleep") {
       std::this_thread::sleep_for(std::chrono::duration<double>(atof(val.c_str())));
       printf("{\"slept\": %s}\n", val.c_str());

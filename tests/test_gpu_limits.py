@@ -370,3 +370,28 @@ def test_spill_placement_policy(tmp_region, policy):
         assert r["after_big"] >= 2 * GiB and small_spilled == 0, r
     else:
         assert small_spilled >= 256 * MiB, r
+
+
+CU_PROPS = """
+import torch
+p = torch.cuda.get_device_properties(0)
+a = torch.randn(2048, 2048, device="cuda"); b = torch.randn(2048, 2048, device="cuda")
+c = a @ b
+conv = torch.nn.Conv2d(64, 64, 3, padding=1).cuda()
+y = conv(torch.randn(8, 64, 56, 56, device="cuda"))
+torch.cuda.synchronize()
+ok = bool(torch.allclose(c[:64, :64].cpu(), (a[:64].cpu() @ b[:, :64].cpu()), atol=1e-2, rtol=1e-3))
+emit(cus=p.multi_processor_count, ok=ok, conv_finite=bool(torch.isfinite(y).all()))
+"""
+
+
+@pytest.mark.parametrize("mode,want", [("spatial", 64), ("temporal", 256)])
+def test_runtime_sees_the_spatial_slice_cu_count(tmp_region, mode, want):
+    """Reference: cuDeviceGetAttribute virtualisation [device.c:130-134]. A 25 % spatial
+    vGPU reports 64 CUs to HIP (multiProcessorCount), so stock libraries size grids for
+    the slice; stock GEMM / conv still compute correctly. Temporal vGPUs keep 256."""
+    c = vgpu_env(mem_limit=24 * GiB, cu_limit=25, cu_mode=mode, shared_cache=tmp_region)
+    res, _ = run_child(CU_PROPS, c)
+    r = res[0]
+    assert r["cus"] == want, r
+    assert r["ok"] and r["conv_finite"], r

@@ -94,7 +94,7 @@ def test_temporal_limit_routed_to_the_current_device(fake):
     e = fake(gpus=2, VGPU_DEVICE_CU_LIMIT_1="20", VGPU_CU_MODE="temporal", VGPU_DEVICE_MEMORY_LIMIT_1="4g")
     out = run(e, "dev=0", "stream", "run=2000,1.5", "dev=1", "stream", "run=2000,3", timeout=120)
     runs = [o for o in out if "run" in o]
-    assert runs[0]["busy_frac"] > 0.9, runs
+    assert runs[0]["busy_frac"] > 0.75, runs   # unlimited (host timing noise aside)
     assert abs(runs[1]["busy_frac"] - 0.20) <= 0.05, runs
     with Region(fake.region) as r:
         d1 = r.device(1)
@@ -213,3 +213,12 @@ def test_spill_placement_policy(fake, policy):
         assert after_big == 5 * GiB and after_small == after_big     # 5 resident + 3 GiB reserve
     else:
         assert after_big == 2 * GiB and after_small - after_big == 2 * GiB   # HBM full after 8
+
+
+@pytest.mark.parametrize("mode,virt,want", [("spatial", "1", 64), ("spatial", "0", 256), ("temporal", "1", 256)])
+def test_cu_count_follows_the_spatial_slice(fake, mode, virt, want):
+    """Under a spatial mask the runtime is told the slice's CU count (what stock
+    libraries size their grids from); temporal vGPUs keep every CU."""
+    e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE=mode, VGPU_VIRTUAL_CU_COUNT=virt)
+    out = run(e, "cus")
+    assert out[-1]["cus"] == want
