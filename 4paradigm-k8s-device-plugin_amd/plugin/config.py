@@ -96,7 +96,8 @@ _FLAGS = [
     ("--enable-legacy-preferred", "enable_legacy_preferred", "bool", ["ENABLE_LEGACY_PREFERRED"],
      "preferred allocation for kubelets without GetPreferredAllocation"),
     ("--verbose", "verbose", int, ["VERBOSE"], "log verbosity"),
-    ("--cu-mode", "cu_mode", str, ["CU_MODE"], "CU limit enforcement: auto (spatial for shares >= 50 %%, temporal below) | spatial | "
+    ("--cu-mode", "cu_mode", str, ["CU_MODE"], "CU limit enforcement: auto (CU masks for shares >= 50 %% and while the GPU is not crowded, "
+     "the GPU-time limiter for smaller shares on a crowded GPU) | spatial | "
      "temporal | both | off"),
     ("--backend", "backend", str, ["DEVICE_BACKEND"], "device backend: auto | amdsmi | sysfs | fake"),
     ("--fake-devices", "fake_devices", str, ["FAKE_DEVICES"], "JSON spec (or file) for the fake backend"),

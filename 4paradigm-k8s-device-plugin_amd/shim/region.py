@@ -37,7 +37,7 @@ class DeviceInfo(C.Structure):
         ("cu_count", C.c_int32), ("num_xcc", C.c_int32), ("cu_mask_count", C.c_int32),
         ("cu_mask", C.c_uint32 * 8), ("credit_ns", C.c_int64), ("charged_ns", C.c_uint64),
         ("wall_ns", C.c_uint64), ("util_pct", C.c_int32), ("cu_mode", C.c_int32), ("gpu_id", C.c_uint32), ("bdf", C.c_uint32), ("domain", C.c_uint32), ("configured", C.c_uint32),
-        ("hbm_limit", C.c_uint64),
+        ("hbm_limit", C.c_uint64), ("crowd", C.c_int32),
     ]
 
 
@@ -146,7 +146,7 @@ class Region:
             "cu_mask_count": d.cu_mask_count, "cu_mask": mask, "credit_ns": d.credit_ns,
             "charged_ns": d.charged_ns, "wall_ns": d.wall_ns, "util_pct": d.util_pct,
             "cu_mode": CU_MODES.get(d.cu_mode, str(d.cu_mode)), "gpu_id": d.gpu_id, "bdf": d.bdf, "domain": d.domain,
-            "configured": bool(d.configured), "hbm_limit": d.hbm_limit,
+            "configured": bool(d.configured), "hbm_limit": d.hbm_limit, "crowd": d.crowd,
         }
 
     def devices(self):

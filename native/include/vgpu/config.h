@@ -32,8 +32,13 @@ enum class CuMode : int {
 // dispatches contend in the shared front end (profiles/r1z), so smaller shares are
 // enforced in time instead (profiles/r2*/scaling.md).
 constexpr int kAutoSpatialMinPct = 50;
+// Auto mode below kAutoSpatialMinPct: CU masks while at most this many other processes
+// keep the GPU busy (masked tenants only stall each other in the dispatchers from about
+// four on), the GPU-time limiter beyond.
+constexpr int kAutoSpatialMaxCrowd = 1;
 // The mode a device actually uses for share `pct` under configured mode `m`.
-CuMode effective_cu_mode(CuMode m, int pct);
+// `crowd`: other busy processes on the GPU (-1 = unknown, treated as crowded).
+CuMode effective_cu_mode(CuMode m, int pct, int crowd = -1);
 
 // Where oversubscribed allocations live (VGPU_SPILL_POLICY).
 enum class SpillPolicy : int {

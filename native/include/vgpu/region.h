@@ -37,7 +37,7 @@
 namespace vgpu {
 
 constexpr uint32_t kRegionMagic = 0x56475055u;  // "VGPU"
-constexpr uint32_t kRegionVersion = 3;
+constexpr uint32_t kRegionVersion = 4;
 
 enum ProcStatus : int32_t { kProcFree = 0, kProcRunning = 1, kProcSuspended = 2 };
 
@@ -90,6 +90,7 @@ struct alignas(64) DeviceState {
   uint32_t bdf;                           // PCI bus/device/function (HSA BDFID)
   uint32_t domain;                        // PCI domain
   uint32_t configured;                    // 1 once a GPU process filled the agent info
+  std::atomic<int32_t> crowd;             // auto mode: other busy processes on the GPU (-1 = unknown)
 };
 
 struct RegionHeader {

@@ -54,6 +54,7 @@ typedef struct {
   uint32_t domain;
   uint32_t configured;
   uint64_t hbm_limit;
+  int32_t crowd;       /* auto mode: other busy processes seen on the GPU (-1 = not assessed) */
 } vgpu_device_info;
 
 /* Returns NULL on failure; *err receives -errno. */

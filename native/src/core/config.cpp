@@ -37,10 +37,11 @@ bool parse_int(const char* s, long lo, long hi, long* out) {
 }
 }  // namespace
 
-CuMode effective_cu_mode(CuMode m, int pct) {
+CuMode effective_cu_mode(CuMode m, int pct, int crowd) {
   if (m != CuMode::kAuto) return m;
   if (pct <= 0 || pct >= 100) return CuMode::kSpatial;  // unlimited: no mask is applied anyway
-  return pct >= kAutoSpatialMinPct ? CuMode::kSpatial : CuMode::kTemporal;
+  if (pct >= kAutoSpatialMinPct) return CuMode::kSpatial;
+  return crowd >= 0 && crowd <= kAutoSpatialMaxCrowd ? CuMode::kSpatial : CuMode::kTemporal;
 }
 
 uint64_t spill_reserve(const Config& cfg, uint64_t hbm_share) {

@@ -158,10 +158,14 @@ void SharedRegion::init_fresh(const Config* cfg) {
       d.cu_range_end = cfg->dev[i].cu_range_end;
       memcpy(d.uuid, cfg->dev[i].uuid, sizeof(d.uuid));
       d.uuid[sizeof(d.uuid) - 1] = 0;
+      d.crowd.store(-1);
     }
     n = cfg->num_devices;
   } else {
-    for (int i = 0; i < kMaxDevices; i++) r_->dev[i].cu_range_begin = r_->dev[i].cu_range_end = -1;
+    for (int i = 0; i < kMaxDevices; i++) {
+      r_->dev[i].cu_range_begin = r_->dev[i].cu_range_end = -1;
+      r_->dev[i].crowd.store(-1);
+    }
   }
   r_->hdr.num_devices = n;
   r_->hdr.initialized.store(1);

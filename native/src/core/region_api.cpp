@@ -63,6 +63,7 @@ int vgpu_region_device_info(vgpu_region* r, int dev, vgpu_device_info* out) {
   out->domain = d.domain;
   out->configured = d.configured;
   out->hbm_limit = d.hbm_limit;
+  out->crowd = d.crowd.load();
   return 0;
 }
 

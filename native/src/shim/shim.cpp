@@ -421,7 +421,7 @@ void apply_live_config() {
     const bool ranged = d.cu_range_begin >= 0;
     s.region.unlock();
     const bool limited = pct > 0 && pct < 100;
-    const CuMode mode = effective_cu_mode(cfg.cu_mode, pct);
+    const CuMode mode = effective_cu_mode(cfg.cu_mode, pct, d.crowd.load(std::memory_order_relaxed));
     const bool spatial = mode == CuMode::kSpatial || mode == CuMode::kBoth;
     const bool temporal = mode == CuMode::kTemporal || mode == CuMode::kBoth;
     const bool mask_on = !off && spatial && (limited || ranged) && m.count() < a.cu_count && m.count() > 0;

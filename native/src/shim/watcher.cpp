@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "shim.h"
@@ -170,6 +171,61 @@ void sample_tick(Region* r, Sampler& sm) {
   r->hdr.watcher_heartbeat.store(now);
 }
 
+// Auto mode below a 50 % share (lease holder, every period): how many other processes
+// keep each GPU busy. A process counts while it had waves resident in the last second.
+// One or none: the container keeps its CU mask (no duty-cycling, its own CUs); more: the
+// masks of several tenants would stall each other in the dispatchers, so every
+// container switches to the GPU-time limiter at once, and back after 2 s of calm.
+struct Crowd {
+  std::map<int, uint64_t> busy_at[kMaxDevices];  // other host PID -> last time with waves
+  uint64_t calm_since[kMaxDevices] = {};
+};
+
+void crowd_tick(Region* r, Sampler& sm, Crowd& c, uint64_t now) {
+  ShimState& s = shim();
+  const Config& cfg = config();
+  if (cfg.cu_mode != CuMode::kAuto) return;
+  bool changed = false;
+  for (int d = 0; d < s.n_agents; d++) {
+    AgentInfo& a = s.agents[d];
+    DeviceState& ds = r->dev[d];
+    const int pct = ds.cu_limit_pct;
+    if (!a.gpu_id || pct <= 0 || pct >= kAutoSpatialMinPct) continue;
+    for (int p : kfd_pids_on_gpu(a.gpu_id)) {
+      if (std::find(sm.mine.begin(), sm.mine.end(), p) != sm.mine.end()) continue;
+      if (kfd_cu_occupancy(p, a.gpu_id) > 0) c.busy_at[d][p] = now;
+    }
+    int busy = 0;
+    for (auto it = c.busy_at[d].begin(); it != c.busy_at[d].end();) {
+      if (now - it->second > 1'000'000'000ull) {
+        it = c.busy_at[d].erase(it);
+      } else {
+        busy++;
+        ++it;
+      }
+    }
+    const int cur = ds.crowd.load(std::memory_order_relaxed);
+    const bool crowded_now = busy > kAutoSpatialMaxCrowd;
+    const bool was_crowded = cur < 0 || cur > kAutoSpatialMaxCrowd;
+    int next = busy;
+    if (crowded_now || cur < 0) {
+      c.calm_since[d] = 0;
+    } else if (was_crowded) {  // calming down: hold the limiter for 2 s first
+      if (!c.calm_since[d]) c.calm_since[d] = now;
+      if (now - c.calm_since[d] < 2'000'000'000ull) next = cur;
+    }
+    if (next != cur) {
+      ds.crowd.store(next, std::memory_order_relaxed);
+      if ((next > kAutoSpatialMaxCrowd) != was_crowded) {
+        changed = true;
+        VLOG_INFO("device %d: %d other busy process(es) on the GPU -> %s", d, busy,
+                  next > kAutoSpatialMaxCrowd ? "GPU-time limiter" : "CU mask");
+      }
+    }
+  }
+  if (changed) r->hdr.generation.fetch_add(1, std::memory_order_acq_rel);  // every process re-applies
+}
+
 // Monitor-based usage (reference set_gpu_device_memory_monitor) and the active OOM killer.
 void monitor_tick(Region* r) {
   ShimState& s = shim();
@@ -208,6 +264,7 @@ void* watcher_main(void*) {
   const pid_t me = getpid();
   const uint64_t period_ns = (uint64_t)cfg.util_period_ms * 1'000'000ull;
   Sampler sm;
+  Crowd crowd;
   uint64_t next_slow = 0;
   int pid_attempts = 0;
   unsigned rng = (unsigned)me * 2654435761u;
@@ -236,6 +293,8 @@ void* watcher_main(void*) {
       if (s.slot >= 0) r->procs[s.slot].launches.store(s.launches.load(std::memory_order_relaxed));
       resync_context_charge();
       if (lease) {
+        collect_region_pids(r, sm);
+        crowd_tick(r, sm, crowd, now);
         monitor_tick(r);
         if (!temporal) r->hdr.watcher_heartbeat.store(now_ns());
       }

@@ -618,8 +618,13 @@ static void test_ratelimit() {
 static void test_auto_mode_and_live_cu() {
   CHECK(effective_cu_mode(CuMode::kAuto, 50) == CuMode::kSpatial);
   CHECK(effective_cu_mode(CuMode::kAuto, 100) == CuMode::kSpatial);
-  CHECK(effective_cu_mode(CuMode::kAuto, 25) == CuMode::kTemporal);
+  CHECK(effective_cu_mode(CuMode::kAuto, 25) == CuMode::kTemporal);      // crowd not assessed yet
   CHECK(effective_cu_mode(CuMode::kAuto, 12) == CuMode::kTemporal);
+  CHECK(effective_cu_mode(CuMode::kAuto, 25, 0) == CuMode::kSpatial);    // alone: keep the CU mask
+  CHECK(effective_cu_mode(CuMode::kAuto, 25, 1) == CuMode::kSpatial);    // one other busy tenant
+  CHECK(effective_cu_mode(CuMode::kAuto, 25, 2) == CuMode::kTemporal);   // crowded: GPU-time limiter
+  CHECK(effective_cu_mode(CuMode::kAuto, 60, 7) == CuMode::kSpatial);    // large shares always masked
+  CHECK(effective_cu_mode(CuMode::kTemporal, 25, 0) == CuMode::kTemporal);
   CHECK(effective_cu_mode(CuMode::kTemporal, 75) == CuMode::kTemporal);
   CHECK(effective_cu_mode(CuMode::kSpatial, 10) == CuMode::kSpatial);
   // set_cu_limit recomputes the mask around the vGPU's anchor and bumps the generation.

@@ -62,8 +62,8 @@ def plugin(tmp_path):
 
 
 def test_slice_resnet50_in_allocated_vgpu(plugin):
-    """4-way split: quota = HBM/4 (72 GiB), 25 % compute share enforced in time (auto mode:
-    masks serve at most two tenants per GPU), stock fp32 model runs."""
+    """4-way split: quota = HBM/4 (72 GiB), 25 % compute share; alone on the GPU the auto
+    mode enforces it with the slot's CU mask (64 CUs), stock fp32 model runs."""
     code = CHILD_PRELUDE + """
 import torch
 from amdvgpu.models.aibench import Runner, get_case
@@ -89,9 +89,9 @@ emit(total=total, ms=dt * 1000, ips=50 / dt, ncu=ncu, mode=Region(os.environ["VG
     quota = int(envs["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m")) * MiB
     assert r["total"] == quota and 70 * GiB <= quota <= 73 * GiB
     assert envs["VGPU_CU_MODE"] == "auto" and envs["VGPU_DEVICE_CU_LIMIT_0"] == "25"
-    assert r["ncu"] == 256 and r["mode"] == "temporal", r
+    assert r["ncu"] == 64 and r["mode"] == "spatial", r
     assert envs["VGPU_DEVICE_CU_RANGE_0"] in ("0-64", "64-128", "128-192", "192-256")
-    print(f"slice: ResNet-V2-50 b=50 fp32 inference in a 1/4 vGPU (25 % GPU time): {r['ips']:.1f} img/s")
+    print(f"slice: ResNet-V2-50 b=50 fp32 inference in a 1/4 vGPU (64 CUs): {r['ips']:.1f} img/s")
 
 
 def test_oversubscription_spills_past_hbm_share(tmp_region):

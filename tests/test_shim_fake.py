@@ -222,3 +222,38 @@ def test_cu_count_follows_the_spatial_slice(fake, mode, virt, want):
     e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE=mode, VGPU_VIRTUAL_CU_COUNT=virt)
     out = run(e, "cus")
     assert out[-1]["cus"] == want
+
+
+def _foreign(kfd, pid, occupancy):
+    d = os.path.join(kfd, str(pid), "stats_1000")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(kfd, str(pid), "vram_1000"), "w") as f:
+        f.write(str(GiB))
+    with open(os.path.join(d, "cu_occupancy"), "w") as f:
+        f.write(str(occupancy))
+
+
+def test_auto_mode_follows_the_crowd(fake):
+    """Auto mode below a 50 % share: the container keeps its CU mask while at most one
+    other process keeps the GPU busy, switches every queue to the GPU-time limiter when
+    two others are busy, and returns to the mask after the GPU calms down."""
+    e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="auto", VGPU_DEVICE_MEMORY_LIMIT="4g")
+    _foreign(fake.kfd, 424250, 40)            # one busy neighbour: still masked
+    p = subprocess.Popen([HARNESS, "stream", "sleep=1.0", "queues", "sleep=2.0", "queues", "sleep=4.0", "queues"],
+                         env=e, stdout=subprocess.PIPE, text=True)
+    lines = [json.loads(p.stdout.readline()) for _ in range(4)]   # header, stream, slept, queues
+    alone = lines[3]["queues"][0]
+    with Region(fake.region) as r:
+        crowd0 = r.device(0)["crowd"]
+        _foreign(fake.kfd, 424251, 40)        # a second busy neighbour: crowded
+        lines += [json.loads(p.stdout.readline()) for _ in range(2)]
+        crowded = lines[5]["queues"][0]
+        d_crowded = r.device(0)
+        for pid in (424250, 424251):          # both go idle
+            _foreign(fake.kfd, pid, 0)
+        rest = [json.loads(l) for l in p.stdout.read().splitlines() if l.startswith("{")]
+    assert p.wait(30) == 0
+    calm = rest[-1]["queues"][0]
+    assert crowd0 == 1 and alone["cus"] == 64, (crowd0, alone)
+    assert d_crowded["crowd"] == 2 and d_crowded["cu_mode"] == "temporal" and crowded["cus"] == 256, (d_crowded, crowded)
+    assert calm["cus"] == 64, calm
