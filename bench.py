@@ -300,10 +300,17 @@ def run_concurrent(args, envs, label):
         outs.append(out)
     try:
         deadline = time.time() + 900
+        t_start = beat = time.time()
         while not all(os.path.exists(o + ".ready") for o in outs):
             if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
                 raise SystemExit(f"a {label} tenant failed before the start barrier")
+            if time.time() - beat > 30:
+                beat = time.time()
+                print(f"[bench] {label}: {sum(os.path.exists(o + '.ready') for o in outs)}/{len(outs)} tenants "
+                      f"warmed up after {beat - t_start:.0f} s", file=sys.stderr, flush=True)
             time.sleep(0.05)
+        print(f"[bench] {label}: all {len(outs)} tenants warmed up after {time.time() - t_start:.0f} s",
+              file=sys.stderr, flush=True)
         open(go, "w").close()
         for p in procs:
             if p.wait(timeout=900) != 0:

@@ -172,7 +172,8 @@ void sample_tick(Region* r, Sampler& sm) {
 }
 
 // Auto mode below a 50 % share (lease holder, every period): how many other processes
-// keep each GPU busy. A process counts while it had waves resident in the last second.
+// keep each GPU busy. A process counts while it had waves resident in the last 5 s (long
+// enough to bridge the CPU-bound phases of a busy tenant, e.g. kernel compilation).
 // One or none: the container keeps its CU mask (no duty-cycling, its own CUs); more: the
 // masks of several tenants would stall each other in the dispatchers, so every
 // container switches to the GPU-time limiter at once, and back after 2 s of calm.
@@ -190,14 +191,16 @@ void crowd_tick(Region* r, Sampler& sm, Crowd& c, uint64_t now) {
     AgentInfo& a = s.agents[d];
     DeviceState& ds = r->dev[d];
     const int pct = ds.cu_limit_pct;
-    if (!a.gpu_id || pct <= 0 || pct >= kAutoSpatialMinPct) continue;
+    // Assessed for every limited device (not only below 50 %), so a live change to a
+    // smaller share finds the crowd already known.
+    if (!a.gpu_id || pct <= 0 || pct >= 100) continue;
     for (int p : kfd_pids_on_gpu(a.gpu_id)) {
       if (std::find(sm.mine.begin(), sm.mine.end(), p) != sm.mine.end()) continue;
       if (kfd_cu_occupancy(p, a.gpu_id) > 0) c.busy_at[d][p] = now;
     }
     int busy = 0;
     for (auto it = c.busy_at[d].begin(); it != c.busy_at[d].end();) {
-      if (now - it->second > 1'000'000'000ull) {
+      if (now - it->second > 5'000'000'000ull) {
         it = c.busy_at[d].erase(it);
       } else {
         busy++;

@@ -239,7 +239,7 @@ def test_auto_mode_follows_the_crowd(fake):
     two others are busy, and returns to the mask after the GPU calms down."""
     e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="auto", VGPU_DEVICE_MEMORY_LIMIT="4g")
     _foreign(fake.kfd, 424250, 40)            # one busy neighbour: still masked
-    p = subprocess.Popen([HARNESS, "stream", "sleep=1.0", "queues", "sleep=2.0", "queues", "sleep=4.0", "queues"],
+    p = subprocess.Popen([HARNESS, "stream", "sleep=1.0", "queues", "sleep=2.0", "queues", "sleep=8.5", "queues"],
                          env=e, stdout=subprocess.PIPE, text=True)
     lines = [json.loads(p.stdout.readline()) for _ in range(4)]   # header, stream, slept, queues
     alone = lines[3]["queues"][0]
