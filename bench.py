@@ -165,6 +165,11 @@ def worker(args):
         res = {"mode": args.mode, "ms_per_step": ms.item(), "items_per_step": runner.items_per_step,
                "steps": args.steps, "mem_total": total,
                "peak_allocated": torch.cuda.max_memory_allocated(device) if not cpu else 0}
+        if g1:
+            # The enforcement the pod actually ran under (auto mode: CU mask when the GPU is
+            # not crowded, GPU-time limiter when it is) and the crowd it saw.
+            res["effective_cu_mode"] = g1["cu_mode"]
+            res["crowd"] = g1["crowd"]
         if g0 and g1 and g1["wall_ns"] > g0["wall_ns"]:
             res["limiter_granted_pct"] = round(100.0 * (g1["charged_ns"] - g0["charged_ns"]) /
                                                (g1["wall_ns"] - g0["wall_ns"]), 2)
@@ -443,7 +448,7 @@ def main(argv=None):
             # The pod's throughput over what its compute share entitles it to (native x share).
             line["entitlement_ratio"] = round(nat / (ms * share), 3)
             line["overhead_pct_vs_native_x_share"] = round((ms * share - nat) / nat * 100.0, 3)
-            for k in ("limiter_granted_pct", "gpu_ms_charged_per_step"):
+            for k in ("limiter_granted_pct", "gpu_ms_charged_per_step", "effective_cu_mode", "crowd"):
                 if k in results["vgpu"]:
                     line[k] = results["vgpu"][k]
         if "quota" in results:
