@@ -94,6 +94,10 @@ def render_metrics(root):
                          lb, d["monitor_used"])
                 w.metric("vgpu_cu_limit_percent", "gauge", "CU share (0 = unlimited)", lb, d["cu_limit_pct"])
                 w.metric("vgpu_cu_mask_count", "gauge", "CUs in the spatial mask", lb, d["cu_mask_count"])
+                w.metric("vgpu_cu_mode", "gauge", "effective enforcement: 0 off, 1 CU mask, 2 GPU-time limiter, 3 both",
+                         lb, {"off": 0, "spatial": 1, "temporal": 2, "both": 3}.get(d["cu_mode"], -1))
+                w.metric("vgpu_gpu_crowd", "gauge", "auto mode: other busy processes on the GPU (-1 = not assessed)",
+                         lb, d.get("crowd", -1))
                 w.metric("vgpu_utilization_percent", "gauge", "smoothed GPU-time share charged to the container",
                          lb, d["util_pct"])
                 w.metric("vgpu_compute_credit_seconds", "gauge", "temporal limiter: remaining GPU-time credit", lb,
