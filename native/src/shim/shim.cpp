@@ -316,7 +316,7 @@ void shim_init_after_hsa() {
     AgentInfo& a = s.agents[i];
     DeviceState& d = r->dev[i];
     if (!d.configured) {
-      snprintf(d.uuid, sizeof(d.uuid), "%s", uuids[i]);
+      snprintf(d.uuid, sizeof(d.uuid), "%.63s", uuids[i]);  // UUIDs are "GPU-" + 16 hex digits
       d.phys_total = a.phys_total;
       d.cu_count = a.cu_count;
       d.num_xcc = a.num_xcc;

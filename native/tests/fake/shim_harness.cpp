@@ -59,7 +59,7 @@ long long parse_size(const char* s) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  hipInit(0);
+  if (hipInit(0) != hipSuccess) return 1;
   int dev = 0;
   hipStream_t stream = nullptr;
   std::vector<void*> ptrs;
@@ -82,16 +82,16 @@ int main(int argc, char** argv) {
       printf("{\"malloc\": \"%s\", \"bytes\": %lld}\n", e == hipSuccess ? "ok" : "oom", parse_size(val.c_str()));
     } else if (key == "free") {
       if (!ptrs.empty()) {
-        hipFree(ptrs.back());
+        (void)hipFree(ptrs.back());
         ptrs.pop_back();
       }
       printf("{\"free\": true}\n");
     } else if (key == "meminfo") {
       size_t f = 0, t = 0;
-      hipMemGetInfo(&f, &t);
+      (void)hipMemGetInfo(&f, &t);
       printf("{\"dev\": %d, \"free\": %zu, \"total\": %zu}\n", dev, f, t);
     } else if (key == "stream") {
-      hipStreamCreate(&stream);
+      (void)hipStreamCreate(&stream);
       streams.push_back(stream);
       printf("{\"stream\": %zu}\n", streams.size() - 1);
     } else if (key == "launch" || key == "graph" || key == "run") {
@@ -105,11 +105,11 @@ int main(int argc, char** argv) {
       for (;; n++) {
         const bool timed = key != "launch";
         if (timed ? now_s() - t0 >= amount : n >= (long)amount) break;
-        if (key == "graph") hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(k), stream);
-        else hipLaunchKernel(k, dim3(1), dim3(64), nullptr, 0, stream);
-        if (timed && n % 8 == 7) hipStreamSynchronize(stream);
+        if (key == "graph") (void)hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(k), stream);
+        else (void)hipLaunchKernel(k, dim3(1), dim3(64), nullptr, 0, stream);
+        if (timed && n % 8 == 7) (void)hipStreamSynchronize(stream);
       }
-      hipStreamSynchronize(stream);
+      (void)hipStreamSynchronize(stream);
       double wall = now_s() - t0;
       uint64_t k1 = 0, b1 = fake_hip_busy_us(dev, &k1);
       printf("{\"%s\": %ld, \"wall\": %.6f, \"busy_us\": %llu, \"busy_frac\": %.4f}\n", key.c_str(), n, wall,
