@@ -85,7 +85,11 @@ int SharedRegion::attach(const char* path, const Config* cfg, bool create) {
     close(fd);
     return -e;
   }
-  if ((size_t)st.st_size < sizeof(Region)) {
+  // A file shorter than the layout was never fully initialised or was cut short: its
+  // header may still look valid while the limits behind it read as 0 (= unlimited), so it
+  // is rebuilt from the environment rather than trusted.
+  const bool short_file = (size_t)st.st_size < sizeof(Region);
+  if (short_file) {
     if (!create || ftruncate(fd, sizeof(Region)) != 0) {
       int e = create ? errno : EINVAL;
       flock(fd, LOCK_UN);
@@ -102,7 +106,7 @@ int SharedRegion::attach(const char* path, const Config* cfg, bool create) {
   }
   r_ = static_cast<Region*>(p);
   fd_ = fd;
-  if (r_->hdr.magic != kRegionMagic) {
+  if (r_->hdr.magic != kRegionMagic || short_file) {
     if (!create) {
       munmap(p, sizeof(Region));
       r_ = nullptr;

@@ -1,6 +1,7 @@
 // Native unit tests of the shim core (no GPU). Driven by tests/test_native_core.py;
 // run one case with `vgpu_core_tests <name>` or all with no argument.
 // Built plain and with -fsanitize=thread / address (make SAN=thread|address).
+#include <fcntl.h>
 #include <signal.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -331,6 +332,48 @@ static void test_region_version_guard() {
   }
   SharedRegion r2;
   CHECK(r2.attach(p.c_str(), &c, true) < 0);
+  unlink(p.c_str());
+}
+
+// Fault injection: a region file whose header was overwritten, and one cut short, are
+// re-initialised by a creating attach (the tenant keeps running with its env limits) and
+// refused by a read-only attach (vgpuctl / the monitor never act on garbage).
+static void test_region_corruption() {
+  std::string p = tmp_region("corrupt");
+  Config c = limits_cfg(4096);
+  {
+    SharedRegion r;
+    CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+    int slot = r.register_process(getpid(), 0, 1);
+    CHECK(slot >= 0);
+    CHECK(r.charge(slot, 0, 100, kMemData) == Charge::kOk);
+  }
+  {
+    int fd = open(p.c_str(), O_WRONLY);
+    CHECK(fd >= 0);
+    char junk[256];
+    for (size_t i = 0; i < sizeof(junk); i++) junk[i] = (char)(0x5a ^ i);
+    CHECK(pwrite(fd, junk, sizeof(junk), 0) == (ssize_t)sizeof(junk));
+    close(fd);
+  }
+  {
+    SharedRegion ro;
+    CHECK_EQ(ro.attach(p.c_str(), nullptr, false), -EINVAL);
+    SharedRegion r;
+    CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+    CHECK_EQ(r.limit(0), (uint64_t)4096);
+    CHECK_EQ(r.usage(0), (uint64_t)0);
+    CHECK(r.lock());
+    r.unlock();
+  }
+  CHECK(truncate(p.c_str(), 100) == 0);
+  {
+    SharedRegion ro;
+    CHECK(ro.attach(p.c_str(), nullptr, false) < 0);
+    SharedRegion r;
+    CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+    CHECK_EQ(r.limit(0), (uint64_t)4096);
+  }
   unlink(p.c_str());
 }
 
@@ -826,6 +869,7 @@ int main(int argc, char** argv) {
       {"region_multiprocess", test_region_multiprocess_and_reclaim},
       {"region_robust_lock", test_region_robust_lock},
       {"region_version_guard", test_region_version_guard},
+      {"region_corruption", test_region_corruption},
       {"proc_alive", test_proc_alive},
       {"cumask", test_cumask},
       {"cumask_se_layout", test_cumask_se_layout},
