@@ -393,10 +393,16 @@ def main(argv=None):
         port += 1
     rccl = None
     if world > 1 and args.rccl_probe:
+        # an all-reduce between vGPUs of different GPUs must run at the native
+        # xGMI bandwidth. Same ranks, same size: without the shim, then inside the pods.
+        rccl = {"native": probe_rccl(args, native_env(uuid, cpu), port)}
+        port += 1
         with NodeHarness(backend, device_split_count=args.split, cu_mode=args.cu_mode) as node:
             env, _ = pod_env(node, node.vgpu_ids(uuid)[:1])
-            rccl = probe_rccl(args, env, port)
+            rccl["vgpu"] = probe_rccl(args, env, port)
         port += 1
+        if rank == 0 and all(isinstance(v, dict) and v.get("busbw_GBps") for v in rccl.values()):
+            rccl["vgpu_vs_native_busbw"] = round(rccl["vgpu"]["busbw_GBps"] / rccl["native"]["busbw_GBps"], 3)
     do_sweep = args.sweep == "on" or (args.sweep == "auto" and world == 1 and not cpu)
     sweep_rows, max_vgpus = ([], None)
     if do_sweep:

@@ -434,9 +434,14 @@ void apply_live_config() {
     a.mask = m;
     a.mode = mode;
     // Libraries size grids and pick kernels from the CU count (hipDeviceProp
-    // multiProcessorCount, which CLR reads from the agent): under a spatial mask report
-    // the slice, so stock MIOpen / hipBLASLt / PyTorch launches fit the CUs they get.
-    a.visible_cus.store(mask_on && cfg.virtual_cu_count ? m.count() : 0);
+    // multiProcessorCount, which CLR reads once from the agent): a vGPU with a CU slice
+    // reports the slice, so stock MIOpen / hipBLASLt / PyTorch launches — cooperative and
+    // persistent grids in particular — fit the CUs it may get. In auto mode the slice is
+    // reported whether or not the mask is on at this moment, so every process of the
+    // container sees the same count however crowded the GPU was when it started.
+    const bool may_mask = spatial || cfg.cu_mode == CuMode::kAuto;
+    const bool slice = !off && may_mask && (limited || ranged) && m.count() < a.cu_count && m.count() > 0;
+    a.visible_cus.store(slice && cfg.virtual_cu_count ? m.count() : 0);
     a.temporal_active.store(temp_on);
     int flags = (mask_on ? 1 : 0) | (temp_on ? 2 : 0);
     d.cu_mode.store(flags);

@@ -38,4 +38,5 @@ def test_bench_two_ranks_cpu_rehearsal():
     assert r["config"]["global_batch"] == 100 and r["config"]["model"] == "ResNet-V2-50"
     assert "overhead_pct_quota_only" in r and "entitlement_ratio" in r and "parity_split2_mem1.8" in r
     assert r["dtype"] == "fp32" and r["config"]["vgpu"]["cu_limit_pct"] == 25
-    assert r["rccl_allreduce_between_pods"]["ok"], r["rccl_allreduce_between_pods"]
+    rc = r["rccl_allreduce_between_pods"]
+    assert rc["native"]["ok"] and rc["vgpu"]["ok"] and "vgpu_vs_native_busbw" in rc, rc

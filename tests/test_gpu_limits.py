@@ -413,11 +413,12 @@ emit(cus=p.multi_processor_count, ok=ok, conv_finite=bool(torch.isfinite(y).all(
 """
 
 
-@pytest.mark.parametrize("mode,want", [("spatial", 64), ("temporal", 256)])
+@pytest.mark.parametrize("mode,want", [("spatial", 64), ("temporal", 256), ("auto", 64)])
 def test_runtime_sees_the_spatial_slice_cu_count(tmp_region, mode, want):
-    """Reference: cuDeviceGetAttribute virtualisation [device.c:130-134]. A 25 % spatial
-    vGPU reports 64 CUs to HIP (multiProcessorCount), so stock libraries size grids for
-    the slice; stock GEMM / conv still compute correctly. Temporal vGPUs keep 256."""
+    """Reference: cuDeviceGetAttribute virtualisation [device.c:130-134]. A 25 % vGPU with
+    a CU slice (spatial, or auto whichever enforcement is on) reports 64 CUs to HIP
+    (multiProcessorCount), so stock libraries size grids for the slice; stock GEMM / conv
+    still compute correctly. Explicitly temporal vGPUs keep 256."""
     c = vgpu_env(mem_limit=24 * GiB, cu_limit=25, cu_mode=mode, shared_cache=tmp_region)
     res, _ = run_child(CU_PROPS, c)
     r = res[0]

@@ -215,7 +215,8 @@ def test_spill_placement_policy(fake, policy):
         assert after_big == 2 * GiB and after_small - after_big == 2 * GiB   # HBM full after 8
 
 
-@pytest.mark.parametrize("mode,virt,want", [("spatial", "1", 64), ("spatial", "0", 256), ("temporal", "1", 256)])
+@pytest.mark.parametrize("mode,virt,want", [("spatial", "1", 64), ("spatial", "0", 256), ("temporal", "1", 256),
+                                            ("auto", "1", 64)])
 def test_cu_count_follows_the_spatial_slice(fake, mode, virt, want):
     """Under a spatial mask the runtime is told the slice's CU count (what stock
     libraries size their grids from); temporal vGPUs keep every CU."""
