@@ -66,7 +66,7 @@ def kfd_queue_count():
         return None
 
 
-def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0):
+def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="scal-")
@@ -81,6 +81,7 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0):
             env = apply_contract(envs, mounts)
             if hw_queues:
                 env["GPU_MAX_HW_QUEUES"] = str(hw_queues)
+            env.update(pod_env or {})
             procs.append(subprocess.Popen(cmd, env=env))
             outs.append(out)
         try:
@@ -107,6 +108,7 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0):
     span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
     agg = sum(r["batch"] * r["steps"] for r in res) / span
     return {"tenants": n, "policy": policy, "hw_queues": hw_queues or None, "kfd_queues": queues,
+            "pod_env": pod_env or None,
             "aggregate_throughput": agg,
             "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res]}
 
@@ -119,6 +121,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=6.0)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--hw-queues", default="0", help="GPU_MAX_HW_QUEUES per pod (comma list; 0 = HIP default)")
+    ap.add_argument("--pod-env", action="append", default=[],
+                    help="KEY=V1,V2,...: extra env in every pod, one sweep per value (repeatable)")
+    ap.add_argument("--repeats", type=int, default=1)
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--go")
@@ -131,21 +136,28 @@ def main():
     backend = SysfsBackend()
     uuid = backend.devices()[0].uuid
     rows = []
-    for hq in [int(x) for x in a.hw_queues.split(",")]:
-        for pol in a.policy.split(","):
-            for n in [int(x) for x in a.tenants.split(",")]:
-                r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq)
-                rows.append(r)
-                print(json.dumps(r), flush=True)
+    envs = [{}]
+    for spec in a.pod_env:
+        k, _, vals = spec.partition("=")
+        envs = [dict(e, **{k: v}) for e in envs for v in vals.split(",")]
+    for rep in range(a.repeats):
+        for pe in envs:
+            for hq in [int(x) for x in a.hw_queues.split(",")]:
+                for pol in a.policy.split(","):
+                    for n in [int(x) for x in a.tenants.split(",")]:
+                        r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq, pe)
+                        rows.append(r)
+                        print(json.dumps(r), flush=True)
     base = {r["policy"]: r["aggregate_throughput"] for r in rows if r["tenants"] == 1}
     md = [f"# concurrent vGPU pods on one MI355X — {a.case} (stock fp32; contracts from Allocate)", "",
-          "| policy (--cu-mode) | HW queues/pod | KFD queues | pods | aggregate | vs 1 pod | per pod (min..max) | "
-          "slowest pod vs 1/N |",
-          "|---|---|---|---|---|---|---|---|"]
+          "| policy (--cu-mode) | pod env | HW queues/pod | KFD queues | pods | aggregate | vs 1 pod | "
+          "per pod (min..max) | slowest pod vs 1/N |",
+          "|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         pt = r["per_tenant"]
         b = base.get(r["policy"], rows[0]["aggregate_throughput"])
-        md.append(f"| {r['policy']} ({MODES[r['policy']]}) | {r['hw_queues'] or 'default'} | {r['kfd_queues']} | "
+        pe = " ".join(f"{k}={v}" for k, v in (r["pod_env"] or {}).items()) or "-"
+        md.append(f"| {r['policy']} ({MODES[r['policy']]}) | {pe} | {r['hw_queues'] or 'default'} | {r['kfd_queues']} | "
                   f"{r['tenants']} | {r['aggregate_throughput']:.1f} | "
                   f"{r['aggregate_throughput'] / b:.2f}x | {min(pt):.1f} .. {max(pt):.1f} | "
                   f"{min(pt) / (b / r['tenants']):.2f} |")
