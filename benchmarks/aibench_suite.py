@@ -268,6 +268,9 @@ def main():
         for rep in range(a.repeats):
             order = modes if rep % 2 == 0 else modes[::-1]  # ABBA: cancels drift between runs
             runs.append({m: run_mode(m, node, uuid, cases, a.steps, a.warmup) for m in order})
+            if a.json_out:  # keep what is measured if a later step runs out of time
+                json.dump({"steps": a.steps, "warmup": a.warmup, "repeats": rep + 1, "partial": True, "runs": runs},
+                          open(a.json_out, "w"), indent=1)
         if a.vdm:
             vdm = run_vdm(node, uuid, cases, a.warmup, a.vdm_seconds)
     md, summary = table(runs, vdm, cases)
