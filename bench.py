@@ -15,8 +15,11 @@ runtime would (``shim/launcher.py``), so the workload runs under the interceptio
 Modes, one fresh worker process each (the rank process itself never touches the GPU):
 
 * native   no shim; the GPU made visible as the official plugin would.
-* vgpu     the split-4 pod: 72 GiB quota, 25 % compute share (auto mode: the GPU-time
-           limiter, since CU masks serve at most two tenants per GPU).   → ``value``
+* vgpu     the split-4 pod: 72 GiB quota, 25 % compute share. Auto mode enforces it with
+           the pod's 64-CU mask while the GPU is not crowded (here the pod is alone),
+           and with the GPU-time limiter once two or more other processes keep the GPU
+           busy (the sweep's 4 and 8 pods). The line reports the enforcement used
+           (``effective_cu_mode``, ``crowd``).   → ``value``
 * quota    the same pod with the compute limit disabled (VGPU_CU_POLICY=disable): the
            shim's own overhead on stock PyTorch, the number the reference's vGPU column
            measured (its 50 % SM limit did not bind on TF).
@@ -29,8 +32,10 @@ Modes, one fresh worker process each (the rank process itself never touches the 
 
 Timed region (native / vgpu / quota / parity): W untimed warmup steps, then exactly K
 steps bracketed by barrier + synchronize on both sides; MAX step time over ranks (one
-rank per GPU under torch.distributed.run, RCCL). ``value`` is the whole-job vGPU
-throughput (sum over GPUs).
+rank per GPU under torch.distributed.run; the pods are independent tenants, so the
+cross-rank group is gloo). ``value`` is the whole-job vGPU throughput (sum over GPUs).
+With N > 1 an RCCL all-reduce between the ranks' pods is probed afterwards, natively and
+inside the pods, and its bus bandwidth compared (``rccl_allreduce_between_pods``).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--case resnet50-inf] [--sweep auto|on|off]
 """
