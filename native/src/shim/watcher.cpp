@@ -325,10 +325,8 @@ void* watcher_main(void*) {
 void start_watcher_if_needed() {
   ShimState& s = shim();
   if (!s.active) return;
-  const Config& cfg = config();
   // Always: the thread also publishes the launch counter and applies live limit changes
   // (it sleeps a whole period, 120 ms, between ticks unless the sampler runs).
-  (void)cfg;
   bool expected = false;
   if (!s.watcher_started.compare_exchange_strong(expected, true)) return;
   pthread_t th;
