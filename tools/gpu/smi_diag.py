@@ -1,5 +1,4 @@
 """Diagnose SMI library initialisation under the shim (run on the GPU box)."""
-import json
 import os
 import subprocess
 import sys

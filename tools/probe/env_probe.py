@@ -1,4 +1,4 @@
-import json, os, subprocess, sys, glob
+import json, os, subprocess
 out = {}
 def sh(c):
     try: return subprocess.run(c, shell=True, capture_output=True, text=True, timeout=60).stdout[-4000:]

@@ -1,4 +1,4 @@
-import time, torch, sys
+import time, torch
 print("mem_get_info", torch.cuda.mem_get_info())
 p = torch.cuda.get_device_properties(0)
 print("props", p.name, p.total_memory, p.multi_processor_count, getattr(p, "gcnArchName", ""))
