@@ -7,7 +7,11 @@
 // entry point with dlsym(handle, name), which never consults the preloaded shim. So
 // dlsym is interposed, but narrowly:
 //   * only names starting with "amdsmi_" / "rsmi_" that resolve into an SMI library
-//     and have a virtualising hook are redirected (to smi_hooks.cpp);
+//     and have a virtualising hook are redirected (to smi_hooks.cpp), and only for
+//     callers outside the SMI libraries (libamd_smi embeds and calls rocm_smi itself,
+//     with node indices);
+//   * the rocm_smi hooks are reached only this way (not exported from the shim), so
+//     libamd_smi's internal calls to its own rsmi_* never hit the index remapping;
 //   * every other lookup is a guaranteed tail call ([[clang::musttail]]) into glibc,
 //     so RTLD_NEXT keeps resolving relative to the *original* caller - other
 //     interposers preloaded alongside the shim are unaffected.
@@ -32,6 +36,12 @@ rsmi_status_t rsmi_dev_memory_total_get(uint32_t, rsmi_memory_type_t, uint64_t*)
 rsmi_status_t rsmi_dev_memory_usage_get(uint32_t, rsmi_memory_type_t, uint64_t*);
 rsmi_status_t rsmi_compute_process_info_get(rsmi_process_info_t*, uint32_t*);
 rsmi_status_t rsmi_compute_process_info_by_pid_get(uint32_t, rsmi_process_info_t*);
+rsmi_status_t rsmi_num_monitor_devices(uint32_t*);
+rsmi_status_t rsmi_compute_process_gpus_get(uint32_t, uint32_t*, uint32_t*);
+}
+
+namespace vgpu {
+void* rsmi_remap_hook(const char* name);  // smi_hooks.cpp (generated index remapping)
 }
 
 namespace {
@@ -72,22 +82,27 @@ const Hook kHooks[] = {
     {"rsmi_dev_memory_usage_get", reinterpret_cast<void*>(&rsmi_dev_memory_usage_get)},
     {"rsmi_compute_process_info_get", reinterpret_cast<void*>(&rsmi_compute_process_info_get)},
     {"rsmi_compute_process_info_by_pid_get", reinterpret_cast<void*>(&rsmi_compute_process_info_by_pid_get)},
+    {"rsmi_num_monitor_devices", reinterpret_cast<void*>(&rsmi_num_monitor_devices)},
+    {"rsmi_compute_process_gpus_get", reinterpret_cast<void*>(&rsmi_compute_process_gpus_get)},
 };
 
-__attribute__((noinline)) void* maybe_hook(void* handle, const char* name, DlsymFn real) {
+bool in_smi_library(const void* addr) {
+  Dl_info info;
+  if (!addr || !dladdr(addr, &info) || !info.dli_fname) return false;
+  const char* f = info.dli_fname;
+  return (strstr(f, "amd_smi") || strstr(f, "rocm_smi")) && !strstr(f, "vgpu");
+}
+
+__attribute__((noinline)) void* maybe_hook(void* handle, const char* name, DlsymFn real, const void* caller) {
   if (handle == RTLD_NEXT || handle == RTLD_DEFAULT) return nullptr;
   if (strncmp(name, "amdsmi_", 7) != 0 && strncmp(name, "rsmi_", 5) != 0) return nullptr;
-  for (const Hook& h : kHooks) {
-    if (strcmp(name, h.name) != 0) continue;
-    void* p = real(handle, name);
-    if (!p) return nullptr;
-    Dl_info info;
-    if (!dladdr(p, &info) || !info.dli_fname) return nullptr;
-    const char* f = info.dli_fname;
-    if ((strstr(f, "amd_smi") || strstr(f, "rocm_smi")) && !strstr(f, "vgpu")) return h.fn;
-    return nullptr;
-  }
-  return nullptr;
+  void* hook = nullptr;
+  for (const Hook& h : kHooks)
+    if (strcmp(name, h.name) == 0) hook = h.fn;
+  if (!hook && name[0] == 'r') hook = vgpu::rsmi_remap_hook(name);
+  if (!hook || in_smi_library(caller)) return nullptr;
+  void* p = real(handle, name);
+  return p && in_smi_library(p) ? hook : nullptr;
 }
 
 }  // namespace
@@ -102,7 +117,7 @@ extern "C" {
 __attribute__((visibility("default"))) void* shim_dlsym_v234(void* handle, const char* name) {
   DlsymFn real = load_real(g_real_234, "GLIBC_2.34");
   if (__builtin_expect(g_dlsym_hook_on && name && (name[0] == 'a' || name[0] == 'r'), 0)) {
-    if (void* h = maybe_hook(handle, name, real)) return h;
+    if (void* h = maybe_hook(handle, name, real, __builtin_return_address(0))) return h;
   }
   [[clang::musttail]] return real(handle, name);
 }
@@ -110,7 +125,7 @@ __attribute__((visibility("default"))) void* shim_dlsym_v234(void* handle, const
 __attribute__((visibility("default"))) void* shim_dlsym_v225(void* handle, const char* name) {
   DlsymFn real = load_real(g_real_225, "GLIBC_2.2.5");
   if (__builtin_expect(g_dlsym_hook_on && name && (name[0] == 'a' || name[0] == 'r'), 0)) {
-    if (void* h = maybe_hook(handle, name, real)) return h;
+    if (void* h = maybe_hook(handle, name, real, __builtin_return_address(0))) return h;
   }
   [[clang::musttail]] return real(handle, name);
 }

@@ -269,6 +269,7 @@ except Exception as e:
     emit(ok=False, err=repr(e)[:300])
     raise SystemExit(0)
 rprocs = None
+rn = None
 try:
     import ctypes
     class P(ctypes.Structure):
@@ -282,9 +283,12 @@ try:
         m = ctypes.c_uint32(n.value)
         lib.rsmi_compute_process_info_get(arr, ctypes.byref(m))
         rprocs = [arr[k].process_id for k in range(m.value)]
+        c = ctypes.c_uint32()
+        if lib.rsmi_num_monitor_devices(ctypes.byref(c)) == 0:
+            rn = c.value
 except Exception as e:
     rprocs = repr(e)[:200]
-emit(ok=True, n=len(hs), procs=procs, rprocs=rprocs)
+emit(ok=True, n=len(hs), procs=procs, rprocs=rprocs, rn=rn)
 """
 
 
@@ -324,3 +328,5 @@ def test_amdsmi_shows_only_the_containers_gpus_and_processes(tmp_region):
     assert i["n"] == n["n"] == 1 and h["n"] == 0
     if isinstance(n.get("rprocs"), list) and len(n["rprocs"]) >= 2:   # rocm_smi: same filtering
         assert set(i["rprocs"]) <= mine and mine & set(i["rprocs"]), (i, mine)
+    if n.get("rn") is not None:                                        # rocm_smi device count
+        assert n["rn"] == i["rn"] == 1 and h["rn"] == 0, (n, i, h)
