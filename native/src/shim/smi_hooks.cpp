@@ -141,10 +141,7 @@ RsmiMap& rsmi_map() {
   std::lock_guard<std::mutex> g(m->mu);
   if (m->built) return *m;
   std::vector<Bdf> vis = visible_bdfs();
-  if (vis.empty()) {
-    m->built = true;  // nothing to hide
-    return *m;
-  }
+  if (vis.empty()) return *m;  // nothing to hide (yet: a later GPU process may record its BDF)
   VGPU_REAL_IMPL(rsmi_num_monitor_devices, "librocm_smi64", nullptr);
   VGPU_REAL_IMPL(rsmi_dev_pci_id_get, "librocm_smi64", nullptr);
   uint32_t n = 0;
