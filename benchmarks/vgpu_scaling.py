@@ -49,8 +49,13 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    mode = crowd = None
+    if os.environ.get("VGPU_SHARED_CACHE") and os.path.exists(os.environ["VGPU_SHARED_CACHE"]):
+        from amdvgpu.shim.region import Region
+        with Region(os.environ["VGPU_SHARED_CACHE"]) as r:  # the enforcement the pod ended under
+            mode, crowd = r.device(0)["cu_mode"], r.device(0)["crowd"]
     json.dump({"ms_per_batch": (t1 - t0) * 1000 / n, "t0": t0, "t1": t1, "batch": case.batch, "steps": n,
-               "throughput": case.batch * n / (t1 - t0)}, open(out, "w"))
+               "throughput": case.batch * n / (t1 - t0), "cu_mode": mode, "crowd": crowd}, open(out, "w"))
 
 
 MODES = {"default": "auto", "spatial": "spatial", "temporal": "temporal", "shared": "off"}
@@ -66,13 +71,13 @@ def kfd_queue_count():
         return None
 
 
-def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None):
+def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None, split=0):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="scal-")
     go = os.path.join(tmp, "go")
     procs, outs = [], []
-    with NodeHarness(backend, device_split_count=n, cu_mode=MODES[policy]) as node:
+    with NodeHarness(backend, device_split_count=split or n, cu_mode=MODES[policy]) as node:
         for i, vid in enumerate(node.vgpu_ids(uuid)[:n]):
             envs, mounts = node.pod([vid])
             out = os.path.join(tmp, f"t{i}.json")
@@ -107,8 +112,8 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
                     p.kill()
     span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
     agg = sum(r["batch"] * r["steps"] for r in res) / span
-    return {"tenants": n, "policy": policy, "hw_queues": hw_queues or None, "kfd_queues": queues,
-            "pod_env": pod_env or None,
+    return {"tenants": n, "policy": policy, "split": split or n, "hw_queues": hw_queues or None, "kfd_queues": queues,
+            "pod_env": pod_env or None, "modes": sorted({str(r.get("cu_mode")) for r in res}),
             "aggregate_throughput": agg,
             "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res]}
 
@@ -124,6 +129,7 @@ def main():
     ap.add_argument("--pod-env", action="append", default=[],
                     help="KEY=V1,V2,...: extra env in every pod, one sweep per value (repeatable)")
     ap.add_argument("--repeats", type=int, default=1)
+    ap.add_argument("--split", type=int, default=0, help="vGPUs per GPU (default: one per pod)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--go")
@@ -145,22 +151,23 @@ def main():
             for hq in [int(x) for x in a.hw_queues.split(",")]:
                 for pol in a.policy.split(","):
                     for n in [int(x) for x in a.tenants.split(",")]:
-                        r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq, pe)
+                        r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq, pe, a.split)
                         rows.append(r)
                         print(json.dumps(r), flush=True)
     base = {r["policy"]: r["aggregate_throughput"] for r in rows if r["tenants"] == 1}
     md = [f"# concurrent vGPU pods on one MI355X — {a.case} (stock fp32; contracts from Allocate)", "",
-          "| policy (--cu-mode) | pod env | HW queues/pod | KFD queues | pods | aggregate | vs 1 pod | "
-          "per pod (min..max) | slowest pod vs 1/N |",
-          "|---|---|---|---|---|---|---|---|---|"]
+          "| policy (--cu-mode) | split | enforcement | pod env | HW queues/pod | KFD queues | pods | aggregate | "
+          "vs 1 pod | per pod (min..max) | slowest pod vs 1/N of one pod (fixed --split: vs the lone pod) |",
+          "|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         pt = r["per_tenant"]
         b = base.get(r["policy"], rows[0]["aggregate_throughput"])
         pe = " ".join(f"{k}={v}" for k, v in (r["pod_env"] or {}).items()) or "-"
-        md.append(f"| {r['policy']} ({MODES[r['policy']]}) | {pe} | {r['hw_queues'] or 'default'} | {r['kfd_queues']} | "
+        md.append(f"| {r['policy']} ({MODES[r['policy']]}) | {r['split']} | {'/'.join(r['modes'])} | {pe} | "
+                  f"{r['hw_queues'] or 'default'} | {r['kfd_queues']} | "
                   f"{r['tenants']} | {r['aggregate_throughput']:.1f} | "
                   f"{r['aggregate_throughput'] / b:.2f}x | {min(pt):.1f} .. {max(pt):.1f} | "
-                  f"{min(pt) / (b / r['tenants']):.2f} |")
+                  f"{min(pt) / (b / (r['tenants'] if r['split'] == r['tenants'] else 1)):.2f} |")
     print("\n".join(md))
     if a.json_out:
         json.dump(rows, open(a.json_out, "w"), indent=1)
