@@ -25,7 +25,7 @@ enum class CuMode : int {
   kSpatial = 1,   // per-queue CU mask (hsa_amd_queue_cu_set_mask): default on MI355X
   kTemporal = 2,  // GPU-time credit checked at kernel launch (ratelimit.h)
   kBoth = 3,
-  kAuto = 4,      // spatial for shares >= 50 % (at most two tenants per GPU), temporal below
+  kAuto = 4,      // spatial for shares >= 50 %; below, spatial unless the GPU is crowded (effective_cu_mode)
 };
 
 // Spatial masks serve at most two co-resident tenants well: beyond that the tenants'
