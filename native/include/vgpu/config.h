@@ -78,6 +78,7 @@ struct Config {
   bool virtual_cu_count = true;          // VGPU_VIRTUAL_CU_COUNT: report the spatial slice's CUs
   int util_period_ms = 120;              // monitor / OOM-killer / accounting period (reference: 120 ms)
   int util_sample_us = 1000;             // temporal-mode occupancy sampling interval
+  int sample_read_budget = 32;           // node-wide occupancy reads per interval (ratelimit.h)
   int limiter_window_ms = 40;            // temporal-mode credit window (ratelimit.h)
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU

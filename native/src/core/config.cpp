@@ -262,6 +262,8 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   if (parse_int(getenv_fn("VGPU_UTIL_PERIOD_MS"), 10, 10000, &period)) cfg->util_period_ms = (int)period;
   long sample = 1000;
   if (parse_int(getenv_fn("VGPU_UTIL_SAMPLE_US"), 200, 100000, &sample)) cfg->util_sample_us = (int)sample;
+  long budget = 32;
+  if (parse_int(getenv_fn("VGPU_SAMPLE_READ_BUDGET"), 0, 1 << 20, &budget)) cfg->sample_read_budget = (int)budget;
   long window = 40;
   if (parse_int(getenv_fn("VGPU_LIMITER_WINDOW_MS"), 5, 2000, &window)) cfg->limiter_window_ms = (int)window;
   if (const char* s = getenv_fn("VGPU_LOCK_FILE")) {

@@ -115,6 +115,7 @@ struct Sampler {
   std::vector<int> others[kMaxDevices];   // other processes on each GPU
   int prev_pm[kMaxDevices] = {};          // charge fraction at the previous sample
   bool opened[kMaxDevices] = {};          // the previous sample re-opened the gate
+  int procs = 1;                          // processes on the busiest sampled GPU (period)
 };
 
 void collect_region_pids(Region* r, Sampler& sm) {
@@ -135,7 +136,10 @@ void sample_tick(Region* r, Sampler& sm) {
   sm.last_ns = now;
   collect_region_pids(r, sm);
   const bool refresh = now - sm.others_at_ns > 100'000'000ull;
-  if (refresh) sm.others_at_ns = now;
+  if (refresh) {
+    sm.others_at_ns = now;
+    sm.procs = 1;
+  }
   for (int d = 0; d < s.n_agents; d++) {
     AgentInfo& a = s.agents[d];
     if (!a.temporal_active.load(std::memory_order_relaxed) || !a.gpu_id) continue;
@@ -145,6 +149,7 @@ void sample_tick(Region* r, Sampler& sm) {
       sm.others[d].clear();
       for (int p : on)
         if (std::find(sm.mine.begin(), sm.mine.end(), p) == sm.mine.end()) sm.others[d].push_back(p);
+      sm.procs = std::max(sm.procs, (int)(sm.mine.size() + sm.others[d].size()));
     }
     int pm = 0;  // the container's share of the GPU at this instant, per mille
     if (!sm.mine.empty()) {
@@ -302,11 +307,13 @@ void* watcher_main(void*) {
         if (!temporal) r->hdr.watcher_heartbeat.store(now_ns());
       }
     }
-    // Sampling cadence with ±25 % jitter so the samples never phase-lock to the gate.
+    // Sampling cadence with ±25 % jitter so the samples never phase-lock to the gate,
+    // stretched on a crowded GPU so the node's occupancy reads stay bounded.
     int64_t sleep_ns;
     if (lease && temporal) {
       rng = rng * 1103515245u + 12345u;
-      int64_t base = (int64_t)cfg.util_sample_us * 1000;
+      int64_t base = sample_period_ns((int64_t)cfg.util_sample_us * 1000, sm.procs, cfg.sample_read_budget,
+                                      std::max<int64_t>(10'000'000, (int64_t)cfg.util_sample_us * 1000));
       sleep_ns = base * 3 / 4 + (int64_t)((rng >> 8) % (uint32_t)(base / 2 + 1));
     } else {
       sleep_ns = (int64_t)std::min<uint64_t>(period_ns, next_slow > now_ns() ? next_slow - now_ns() : 0);
