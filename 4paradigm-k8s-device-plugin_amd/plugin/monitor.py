@@ -82,6 +82,8 @@ def render_metrics(root):
             w.metric("vgpu_container_priority", "gauge", "task priority", base, snap["priority"])
             w.metric("vgpu_container_processes", "gauge", "processes attached to the region", base,
                      len(snap["procs"]))
+            w.metric("vgpu_sampler_ticks_total", "counter", "temporal limiter: occupancy samples taken", base,
+                     snap["samples"])
             for d in snap["devices"]:
                 if not d["configured"] and not d["mem_limit"]:
                     continue

@@ -69,6 +69,7 @@ def lib():
             "vgpu_region_get_recent_kernel": (C.c_int, [P]),
             "vgpu_region_set_utilization_switch": (C.c_int, [P, C.c_int]),
             "vgpu_region_reclaim": (C.c_int, [P]),
+            "vgpu_region_samples": (C.c_uint64, [P]),
             "vgpu_region_register": (C.c_int, [P, C.c_int32, C.c_int32]),
             "vgpu_region_unregister": (None, [P, C.c_int]),
             "vgpu_region_charge": (C.c_int, [P, C.c_int, C.c_int, C.c_uint64, C.c_int]),
@@ -172,7 +173,8 @@ class Region:
     def snapshot(self):
         return {
             "path": self.path, "version": lib().vgpu_region_version(), "suspended": self.suspended,
-            "priority": self.priority, "recent_kernel": self.recent_kernel, "devices": self.devices(),
+            "priority": self.priority, "recent_kernel": self.recent_kernel, "samples": self.samples,
+            "devices": self.devices(),
             "procs": self.procs(),
         }
 
@@ -208,6 +210,11 @@ class Region:
     @recent_kernel.setter
     def recent_kernel(self, v):
         lib().vgpu_region_set_recent_kernel(self._h, int(v))
+
+    @property
+    def samples(self):
+        """Occupancy-sampler ticks so far (temporal mode)."""
+        return lib().vgpu_region_samples(self._h)
 
     def set_utilization_switch(self, v):
         return lib().vgpu_region_set_utilization_switch(self._h, int(v))

@@ -125,6 +125,8 @@ int vgpu_region_set_recent_kernel(vgpu_region* r, int v) {
   return 0;
 }
 int vgpu_region_get_recent_kernel(vgpu_region* r) { return r->r.raw()->hdr.recent_kernel.load(); }
+
+uint64_t vgpu_region_samples(vgpu_region* r) { return r->r.raw()->hdr.samples.load(); }
 int vgpu_region_set_utilization_switch(vgpu_region* r, int v) {
   r->r.raw()->hdr.utilization_switch.store(v);
   return 0;

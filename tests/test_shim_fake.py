@@ -258,3 +258,26 @@ def test_auto_mode_follows_the_crowd(fake):
     assert crowd0 == 1 and alone["cus"] == 64, (crowd0, alone)
     assert d_crowded["crowd"] == 2 and d_crowded["cu_mode"] == "temporal" and crowded["cus"] == 256, (d_crowded, crowded)
     assert calm["cus"] == 64, calm
+
+
+def test_sampler_period_stretches_on_a_crowded_gpu(fake):
+    """Eleven other busy processes share the GPU, so every limited container would read
+    twelve cu_occupancy files per tick: the sampler stretches its period to ~4.5 ms
+    (profiles/r2ae: 1 ms ticks cost 12 pods 14 % of the GPU). VGPU_SAMPLE_READ_BUDGET=0
+    keeps the fixed ~1 ms period."""
+    for pid in range(424300, 424311):
+        _foreign(fake.kfd, pid, 40)
+    rates = {}
+    for budget in ("32", "0"):
+        if os.path.exists(fake.region):
+            os.unlink(fake.region)
+        e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="50", VGPU_CU_MODE="temporal", VGPU_SAMPLE_READ_BUDGET=budget)
+        t0 = time.monotonic()
+        out = run(e, "stream", "run=1000,2", timeout=120)
+        wall = time.monotonic() - t0
+        with Region(fake.region) as r:
+            rates[budget] = r.samples / wall
+            d = r.device(0)
+        assert d["cu_mode"] == "temporal" and d["charged_ns"] > 0 and [o for o in out if "run" in o], d
+    assert rates["32"] < 300, rates                   # ~220 Hz at 4.5 ms +- 25 % jitter
+    assert rates["0"] > 2.5 * rates["32"], rates      # ~1 kHz
