@@ -213,7 +213,7 @@ def rccl_probe(args, device, rank, world):
     dt = (time.perf_counter() - t0) / iters
     busbw = 2 * (world - 1) / world * n * 4 / dt / 1e9
     res = {"ok": ok, "backend": "gloo (cpu rehearsal)" if cpu else "nccl (RCCL)", "bytes": n * 4,
-           "ms": round(dt * 1000, 3), "busbw_GBps": round(busbw, 1), "mem_get_info_total": total}
+           "ms": round(dt * 1000, 3), "busbw_GBps": round(busbw, 3), "mem_get_info_total": total}
     if args.result_file and rank == 0:
         with open(args.result_file, "w") as f:
             json.dump(res, f)
@@ -406,7 +406,7 @@ def main(argv=None):
             env, _ = pod_env(node, node.vgpu_ids(uuid)[:1])
             rccl["vgpu"] = probe_rccl(args, env, port)
         port += 1
-        if rank == 0 and all(isinstance(v, dict) and v.get("busbw_GBps") for v in rccl.values()):
+        if rank == 0 and all(isinstance(v, dict) and (v.get("busbw_GBps") or 0) > 0 for v in rccl.values()):
             rccl["vgpu_vs_native_busbw"] = round(rccl["vgpu"]["busbw_GBps"] / rccl["native"]["busbw_GBps"], 3)
     do_sweep = args.sweep == "on" or (args.sweep == "auto" and world == 1 and not cpu)
     sweep_rows, max_vgpus = ([], None)
