@@ -84,6 +84,9 @@ def render_metrics(root):
                      len(snap["procs"]))
             w.metric("vgpu_sampler_ticks_total", "counter", "temporal limiter: occupancy samples taken", base,
                      snap["samples"])
+            w.metric("vgpu_sampler_other_refreshes_total", "counter",
+                     "temporal limiter: samples that re-read the other processes' occupancy", base,
+                     snap["other_refreshes"])
             for d in snap["devices"]:
                 if not d["configured"] and not d["mem_limit"]:
                     continue

@@ -70,6 +70,7 @@ def lib():
             "vgpu_region_set_utilization_switch": (C.c_int, [P, C.c_int]),
             "vgpu_region_reclaim": (C.c_int, [P]),
             "vgpu_region_samples": (C.c_uint64, [P]),
+            "vgpu_region_other_refreshes": (C.c_uint64, [P]),
             "vgpu_region_register": (C.c_int, [P, C.c_int32, C.c_int32]),
             "vgpu_region_unregister": (None, [P, C.c_int]),
             "vgpu_region_charge": (C.c_int, [P, C.c_int, C.c_int, C.c_uint64, C.c_int]),
@@ -174,6 +175,7 @@ class Region:
         return {
             "path": self.path, "version": lib().vgpu_region_version(), "suspended": self.suspended,
             "priority": self.priority, "recent_kernel": self.recent_kernel, "samples": self.samples,
+            "other_refreshes": self.other_refreshes,
             "devices": self.devices(),
             "procs": self.procs(),
         }
@@ -215,6 +217,11 @@ class Region:
     def samples(self):
         """Occupancy-sampler ticks so far (temporal mode)."""
         return lib().vgpu_region_samples(self._h)
+
+    @property
+    def other_refreshes(self):
+        """Sampler ticks that re-read the other processes' occupancy."""
+        return lib().vgpu_region_other_refreshes(self._h)
 
     def set_utilization_switch(self, v):
         return lib().vgpu_region_set_utilization_switch(self._h, int(v))

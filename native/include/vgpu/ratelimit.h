@@ -86,16 +86,21 @@ inline bool limiter_would_block(const RegionHeader& h, const DeviceState& d, boo
          (limited && !d.gate_open.load(std::memory_order_relaxed));
 }
 
-// Occupancy sampling period for a sampler that shares its GPU with `procs` processes
-// (its own included). Every limited container samples every process on the GPU, so n
-// processes make the node read ~n² KFD cu_occupancy files per period, and each read
-// walks the GPU's wave slots (~29 µs, profiles/r2a). 12 pods sampling every 1 ms lost
-// 14 % of the GPU (0.86x aggregate); every 4 ms, 2 % (profiles/r2ae). The period
-// stretches so that the node-wide read rate stays within `budget` reads per `base_ns`:
-// base while n² <= budget, then base·n²/budget, at most `max_ns`.
-inline int64_t sample_period_ns(int64_t base_ns, int procs, int budget, int64_t max_ns) {
-  if (budget <= 0 || (int64_t)procs * procs <= budget) return base_ns;
-  int64_t p = base_ns * procs * procs / budget;
+// Occupancy sampling periods on a crowded GPU. Every limited container samples its own
+// processes and every other process on the GPU, and each KFD cu_occupancy read walks the
+// GPU's wave slots (~29 µs, profiles/r2a): with n processes the node reads about n files
+// per tick for the containers' own occupancy and n² for everyone's view of the others.
+// 12 pods reading everything every 1 ms lost 14 % of the GPU (0.86x aggregate); every
+// 4 ms, 2 % (profiles/r2ae). The own reads decide the charge's accuracy (with gating a
+// pod runs in bursts of a few ms, and sparser samples make its charge noisier), so they
+// keep the base period while the others' total, only the denominator of the split, is
+// refreshed less often. A period covering `reads` node-wide reads per base period
+// stretches to base·reads/budget once reads > budget, at most `max_ns`:
+//   tick (own processes)      sample_period_ns(base, n,     budget, max)
+//   others' occupancy refresh sample_period_ns(base, n * n, budget, max)
+inline int64_t sample_period_ns(int64_t base_ns, int64_t reads, int budget, int64_t max_ns) {
+  if (budget <= 0 || reads <= budget) return base_ns;
+  int64_t p = base_ns * reads / budget;
   return p < max_ns ? p : (max_ns > base_ns ? max_ns : base_ns);
 }
 

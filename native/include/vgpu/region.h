@@ -108,7 +108,7 @@ struct RegionHeader {
   std::atomic<int32_t> watcher_pid;         // process that runs the utilisation watcher
   std::atomic<uint64_t> watcher_heartbeat;  // CLOCK_MONOTONIC ns of the last tick
   uint32_t flags;                           // RegionFlags
-  uint32_t pad0;
+  std::atomic<uint32_t> other_refreshes;    // sampler reads of the other processes' occupancy
   std::atomic<uint64_t> generation;         // bumped on any limit change
   std::atomic<uint64_t> samples;            // sampler ticks (temporal mode)
 };

@@ -79,6 +79,8 @@ int vgpu_region_get_recent_kernel(vgpu_region* r);
 int vgpu_region_set_utilization_switch(vgpu_region* r, int v);
 /* Occupancy-sampler ticks so far (temporal mode; the sampling rate over a window). */
 uint64_t vgpu_region_samples(vgpu_region* r);
+/* Of those, the ticks that re-read the other processes' occupancy (crowd-stretched). */
+uint64_t vgpu_region_other_refreshes(vgpu_region* r);
 int vgpu_region_reclaim(vgpu_region* r);
 /* Test hooks: charge/uncharge through the same admission path the shim uses. */
 int vgpu_region_register(vgpu_region* r, int32_t pid, int32_t hostpid);

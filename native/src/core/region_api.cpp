@@ -127,6 +127,8 @@ int vgpu_region_set_recent_kernel(vgpu_region* r, int v) {
 int vgpu_region_get_recent_kernel(vgpu_region* r) { return r->r.raw()->hdr.recent_kernel.load(); }
 
 uint64_t vgpu_region_samples(vgpu_region* r) { return r->r.raw()->hdr.samples.load(); }
+
+uint64_t vgpu_region_other_refreshes(vgpu_region* r) { return r->r.raw()->hdr.other_refreshes.load(); }
 int vgpu_region_set_utilization_switch(vgpu_region* r, int v) {
   r->r.raw()->hdr.utilization_switch.store(v);
   return 0;

@@ -115,7 +115,9 @@ struct Sampler {
   std::vector<int> others[kMaxDevices];   // other processes on each GPU
   int prev_pm[kMaxDevices] = {};          // charge fraction at the previous sample
   bool opened[kMaxDevices] = {};          // the previous sample re-opened the gate
-  int procs = 1;                          // processes on the busiest sampled GPU (period)
+  int procs = 1;                          // processes on the busiest sampled GPU (periods)
+  int64_t others_occ[kMaxDevices] = {};   // the others' resident waves at their last read
+  uint64_t others_read_ns[kMaxDevices] = {};
 };
 
 void collect_region_pids(Region* r, Sampler& sm) {
@@ -155,12 +157,24 @@ void sample_tick(Region* r, Sampler& sm) {
     if (!sm.mine.empty()) {
       int64_t mine = 0;
       for (int hp : sm.mine) mine += std::max<int64_t>(0, kfd_cu_occupancy(hp, a.gpu_id));
-      int64_t total = mine;
       // Split the instant with whoever else has waves resident on this GPU (other
-      // containers, unlimited processes): only read when the container is busy.
-      if (mine > 0)
-        for (int p : sm.others[d]) total += std::max<int64_t>(0, kfd_cu_occupancy(p, a.gpu_id));
-      pm = (int)timeshare_charge(1000, mine, total);
+      // containers, unlimited processes): only needed while the container is busy, and
+      // refreshed at the crowd-stretched period (ratelimit.h, sample_period_ns).
+      if (mine > 0) {
+        const Config& cfg = config();
+        const int64_t base = (int64_t)cfg.util_sample_us * 1000;
+        const int64_t every = sample_period_ns(base, (int64_t)sm.procs * sm.procs, cfg.sample_read_budget,
+                                               std::max<int64_t>(10'000'000, base));
+        // 3/4 of the period: the refresh lands on the first tick after it (ticks jitter).
+        if (now - sm.others_read_ns[d] >= (uint64_t)(every * 3 / 4)) {
+          int64_t others = 0;
+          for (int p : sm.others[d]) others += std::max<int64_t>(0, kfd_cu_occupancy(p, a.gpu_id));
+          sm.others_occ[d] = others;
+          sm.others_read_ns[d] = now;
+          r->hdr.other_refreshes.fetch_add(1, std::memory_order_relaxed);
+        }
+      }
+      pm = (int)timeshare_charge(1000, mine, mine + (mine > 0 ? sm.others_occ[d] : 0));
     } else if (sm.unknown) {
       // No host PID known yet: fall back to device-wide busy time (conservative).
       int busy = device_busy_percent(a.gpu_id);
@@ -308,7 +322,7 @@ void* watcher_main(void*) {
       }
     }
     // Sampling cadence with ±25 % jitter so the samples never phase-lock to the gate,
-    // stretched on a crowded GPU so the node's occupancy reads stay bounded.
+    // stretched only when even the containers' own reads exceed the node's budget.
     int64_t sleep_ns;
     if (lease && temporal) {
       rng = rng * 1103515245u + 12345u;

@@ -25,9 +25,11 @@ static int usage() {
 }
 
 static void show(vgpu_region* r) {
-  printf("{\"version\": %u, \"num_devices\": %d, \"suspended\": %d, \"priority\": %d, \"recent_kernel\": %d,\n",
+  printf("{\"version\": %u, \"num_devices\": %d, \"suspended\": %d, \"priority\": %d, \"recent_kernel\": %d, "
+         "\"samples\": %llu, \"other_refreshes\": %llu,\n",
          vgpu_region_version(), vgpu_region_num_devices(r), vgpu_region_suspended(r), vgpu_region_get_priority(r),
-         vgpu_region_get_recent_kernel(r));
+         vgpu_region_get_recent_kernel(r), (unsigned long long)vgpu_region_samples(r),
+         (unsigned long long)vgpu_region_other_refreshes(r));
   printf(" \"devices\": [");
   int nd = vgpu_region_num_devices(r);
   for (int d = 0; d < nd; d++) {

@@ -583,14 +583,14 @@ static void test_ratelimit() {
   CHECK_EQ(timeshare_step(-p.debt_ns, p, 1000000, 1000000), -p.debt_ns);
   // Unlimited: grants the whole interval.
   CHECK_EQ(timeshare_step(0, timeshare_params(0), 1000000, 1000000), 0);
-  // Sampling period: base up to sqrt(budget) processes, then ~n², capped.
+  // Sampling periods: base while the node-wide reads fit the budget, then proportional.
   CHECK_EQ(sample_period_ns(1000000, 1, 32, 10000000), 1000000);
-  CHECK_EQ(sample_period_ns(1000000, 5, 32, 10000000), 1000000);
-  CHECK_EQ(sample_period_ns(1000000, 8, 32, 10000000), 2000000);
-  CHECK_EQ(sample_period_ns(1000000, 12, 32, 10000000), 4500000);
-  CHECK_EQ(sample_period_ns(1000000, 64, 32, 10000000), 10000000);
-  CHECK_EQ(sample_period_ns(1000000, 64, 0, 10000000), 1000000);  // budget 0: fixed period
-  CHECK_EQ(sample_period_ns(20000000, 64, 32, 10000000), 20000000);  // never below base
+  CHECK_EQ(sample_period_ns(1000000, 12, 32, 10000000), 1000000);      // own reads, 12 pods
+  CHECK_EQ(sample_period_ns(1000000, 8 * 8, 32, 10000000), 2000000);
+  CHECK_EQ(sample_period_ns(1000000, 12 * 12, 32, 10000000), 4500000);  // others, 12 pods
+  CHECK_EQ(sample_period_ns(1000000, 64 * 64, 32, 10000000), 10000000);
+  CHECK_EQ(sample_period_ns(1000000, 64 * 64, 0, 10000000), 1000000);   // budget 0: fixed
+  CHECK_EQ(sample_period_ns(20000000, 64 * 64, 32, 10000000), 20000000);  // never below base
 
   // Closed loop, one tenant: achieved share within 2 points of every limit.
   for (int lim : {10, 25, 50, 75, 90}) {

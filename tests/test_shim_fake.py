@@ -261,23 +261,24 @@ def test_auto_mode_follows_the_crowd(fake):
 
 
 def test_sampler_period_stretches_on_a_crowded_gpu(fake):
-    """Eleven other busy processes share the GPU, so every limited container would read
-    twelve cu_occupancy files per tick: the sampler stretches its period to ~4.5 ms
-    (profiles/r2ae: 1 ms ticks cost 12 pods 14 % of the GPU). VGPU_SAMPLE_READ_BUDGET=0
-    keeps the fixed ~1 ms period."""
+    """Eleven other busy processes share the GPU, so re-reading all of them every tick in
+    every limited container would cost the node ~n² cu_occupancy reads per ms
+    (profiles/r2ae: 12 pods lost 14 % of the GPU). The sampler keeps reading its own
+    processes every ~1 ms and refreshes the others' total every ~4.5 ms;
+    VGPU_SAMPLE_READ_BUDGET=0 re-reads everything every tick."""
     for pid in range(424300, 424311):
         _foreign(fake.kfd, pid, 40)
-    rates = {}
+    got = {}
     for budget in ("32", "0"):
         if os.path.exists(fake.region):
             os.unlink(fake.region)
         e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="50", VGPU_CU_MODE="temporal", VGPU_SAMPLE_READ_BUDGET=budget)
-        t0 = time.monotonic()
         out = run(e, "stream", "run=1000,2", timeout=120)
-        wall = time.monotonic() - t0
         with Region(fake.region) as r:
-            rates[budget] = r.samples / wall
+            got[budget] = (r.samples, r.other_refreshes)
             d = r.device(0)
         assert d["cu_mode"] == "temporal" and d["charged_ns"] > 0 and [o for o in out if "run" in o], d
-    assert rates["32"] < 300, rates                   # ~220 Hz at 4.5 ms +- 25 % jitter
-    assert rates["0"] > 2.5 * rates["32"], rates      # ~1 kHz
+    ticks, refreshes = got["32"]
+    assert ticks > 600 and refreshes < ticks / 2.5, got        # own reads ~1 kHz, others ~4 ms
+    ticks0, refreshes0 = got["0"]
+    assert ticks0 > 600 and refreshes0 > 0.6 * ticks0, got     # everything every tick
