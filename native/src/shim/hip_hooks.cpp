@@ -4,7 +4,8 @@
 // run the suspend gate (wait_status_self) and the token-bucket rate_limiter before
 // the real launch, and 41 copy/alloc hooks run the suspend gate. cuGraphLaunch is a
 // plain passthrough there [graph.c:224-225], so graph replays escape the throttle;
-// here graph launches are charged with the workgroups of their kernel nodes.
+// here a graph launch passes the same gates as a kernel launch, and the GPU-time limiter
+// charges whatever its kernels run (ratelimit.h).
 //
 // Hot-path budget: a launch pays one predictable branch on process-local state, a
 // relaxed increment of its own slot's launch counter, and relaxed loads of region words

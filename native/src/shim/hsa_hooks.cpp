@@ -197,6 +197,7 @@ hsa_status_t hsa_amd_vmem_handle_create(hsa_amd_memory_pool_t pool, size_t size,
   if (dev < 0) return real_hsa_amd_vmem_handle_create(pool, size, type, flags, handle);
   ShimState& s = shim();
   gate_suspend();
+  if (__builtin_expect(!s.agents[dev].authorised, 0)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   if (s.region.charge(s.slot, dev, size, kMemData) != Charge::kOk) {
     VLOG_WARN("device %d OOM (vmem): request %zu bytes, usage %lu of limit %lu", dev, size,
               (unsigned long)s.region.usage(dev), (unsigned long)s.region.limit(dev));
