@@ -30,6 +30,8 @@ def test_metrics_and_control(tmp_path):
     assert 'vgpu_memory_limit_bytes{container="pod1_main",region="abc.cache",device="0"' in text
     assert f"vgpu_memory_used_bytes" in text and str(3 << 30) in text
     assert "vgpu_process_oom_events_total" in text
+    assert 'vgpu_sampler_ticks_total{container="pod1_main",region="abc.cache"} 0' in text
+    assert 'vgpu_sampler_other_refreshes_total{container="pod1_main",region="abc.cache"} 0' in text
     # quota enforcement through the region: a charge past the limit is refused
     assert r.charge(slot, 0, 6 << 30, 0) != 0
     assert control(root, "pod1_main", "suspend", {}) == 1
