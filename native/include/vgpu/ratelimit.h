@@ -86,18 +86,15 @@ inline bool limiter_would_block(const RegionHeader& h, const DeviceState& d, boo
          (limited && !d.gate_open.load(std::memory_order_relaxed));
 }
 
-// Occupancy sampling periods on a crowded GPU. Every limited container samples its own
+// Occupancy sampling period on a crowded GPU. Every limited container samples its own
 // processes and every other process on the GPU, and each KFD cu_occupancy read walks the
-// GPU's wave slots (~29 µs, profiles/r2a): with n processes the node reads about n files
-// per tick for the containers' own occupancy and n² for everyone's view of the others.
-// 12 pods reading everything every 1 ms lost 14 % of the GPU (0.86x aggregate); every
-// 4 ms, 2 % (profiles/r2ae). The own reads decide the charge's accuracy (with gating a
-// pod runs in bursts of a few ms, and sparser samples make its charge noisier), so they
-// keep the base period while the others' total, only the denominator of the split, is
-// refreshed less often. A period covering `reads` node-wide reads per base period
-// stretches to base·reads/budget once reads > budget, at most `max_ns`:
-//   tick (own processes)      sample_period_ns(base, n,     budget, max)
-//   others' occupancy refresh sample_period_ns(base, n * n, budget, max)
+// GPU's wave slots (~29 µs, profiles/r2a): with n processes the node reads about n² files
+// per period. Sampling everything every 1 ms cost 12 pods 14 % of the GPU (0.86x
+// aggregate); every ~4.5 ms, 2-6 % (0.94-0.98x, profiles/r2ae, r2af, r2ag). Re-reading
+// only the pod's own processes every 1 ms and the others every ~4.5 ms measured 0.85x
+// (profiles/r2aj): part of the gain comes from the coarser gate decisions themselves
+// (longer on/off periods, fewer restarts). The period covering `reads` node-wide reads
+// (n² here) stretches to base·reads/budget once reads > budget, at most `max_ns`.
 inline int64_t sample_period_ns(int64_t base_ns, int64_t reads, int budget, int64_t max_ns) {
   if (budget <= 0 || reads <= budget) return base_ns;
   int64_t p = base_ns * reads / budget;

@@ -115,9 +115,7 @@ struct Sampler {
   std::vector<int> others[kMaxDevices];   // other processes on each GPU
   int prev_pm[kMaxDevices] = {};          // charge fraction at the previous sample
   bool opened[kMaxDevices] = {};          // the previous sample re-opened the gate
-  int procs = 1;                          // processes on the busiest sampled GPU (periods)
-  int64_t others_occ[kMaxDevices] = {};   // the others' resident waves at their last read
-  uint64_t others_read_ns[kMaxDevices] = {};
+  int procs = 1;                          // processes on the busiest sampled GPU (period)
 };
 
 void collect_region_pids(Region* r, Sampler& sm) {
@@ -158,23 +156,13 @@ void sample_tick(Region* r, Sampler& sm) {
       int64_t mine = 0;
       for (int hp : sm.mine) mine += std::max<int64_t>(0, kfd_cu_occupancy(hp, a.gpu_id));
       // Split the instant with whoever else has waves resident on this GPU (other
-      // containers, unlimited processes): only needed while the container is busy, and
-      // refreshed at the crowd-stretched period (ratelimit.h, sample_period_ns).
+      // containers, unlimited processes): only read when the container is busy.
+      int64_t total = mine;
       if (mine > 0) {
-        const Config& cfg = config();
-        const int64_t base = (int64_t)cfg.util_sample_us * 1000;
-        const int64_t every = sample_period_ns(base, (int64_t)sm.procs * sm.procs, cfg.sample_read_budget,
-                                               std::max<int64_t>(10'000'000, base));
-        // 3/4 of the period: the refresh lands on the first tick after it (ticks jitter).
-        if (now - sm.others_read_ns[d] >= (uint64_t)(every * 3 / 4)) {
-          int64_t others = 0;
-          for (int p : sm.others[d]) others += std::max<int64_t>(0, kfd_cu_occupancy(p, a.gpu_id));
-          sm.others_occ[d] = others;
-          sm.others_read_ns[d] = now;
-          r->hdr.other_refreshes.fetch_add(1, std::memory_order_relaxed);
-        }
+        for (int p : sm.others[d]) total += std::max<int64_t>(0, kfd_cu_occupancy(p, a.gpu_id));
+        r->hdr.other_refreshes.fetch_add(1, std::memory_order_relaxed);
       }
-      pm = (int)timeshare_charge(1000, mine, mine + (mine > 0 ? sm.others_occ[d] : 0));
+      pm = (int)timeshare_charge(1000, mine, total);
     } else if (sm.unknown) {
       // No host PID known yet: fall back to device-wide busy time (conservative).
       int busy = device_busy_percent(a.gpu_id);
@@ -322,11 +310,12 @@ void* watcher_main(void*) {
       }
     }
     // Sampling cadence with ±25 % jitter so the samples never phase-lock to the gate,
-    // stretched only when even the containers' own reads exceed the node's budget.
+    // stretched on a crowded GPU so the node's occupancy reads stay bounded.
     int64_t sleep_ns;
     if (lease && temporal) {
       rng = rng * 1103515245u + 12345u;
-      int64_t base = sample_period_ns((int64_t)cfg.util_sample_us * 1000, sm.procs, cfg.sample_read_budget,
+      int64_t base = sample_period_ns((int64_t)cfg.util_sample_us * 1000, (int64_t)sm.procs * sm.procs,
+                                      cfg.sample_read_budget,
                                       std::max<int64_t>(10'000'000, (int64_t)cfg.util_sample_us * 1000));
       sleep_ns = base * 3 / 4 + (int64_t)((rng >> 8) % (uint32_t)(base / 2 + 1));
     } else {

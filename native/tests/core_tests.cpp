@@ -585,9 +585,9 @@ static void test_ratelimit() {
   CHECK_EQ(timeshare_step(0, timeshare_params(0), 1000000, 1000000), 0);
   // Sampling periods: base while the node-wide reads fit the budget, then proportional.
   CHECK_EQ(sample_period_ns(1000000, 1, 32, 10000000), 1000000);
-  CHECK_EQ(sample_period_ns(1000000, 12, 32, 10000000), 1000000);      // own reads, 12 pods
+  CHECK_EQ(sample_period_ns(1000000, 5 * 5, 32, 10000000), 1000000);   // 5 processes: base
   CHECK_EQ(sample_period_ns(1000000, 8 * 8, 32, 10000000), 2000000);
-  CHECK_EQ(sample_period_ns(1000000, 12 * 12, 32, 10000000), 4500000);  // others, 12 pods
+  CHECK_EQ(sample_period_ns(1000000, 12 * 12, 32, 10000000), 4500000);  // 12 pods
   CHECK_EQ(sample_period_ns(1000000, 64 * 64, 32, 10000000), 10000000);
   CHECK_EQ(sample_period_ns(1000000, 64 * 64, 0, 10000000), 1000000);   // budget 0: fixed
   CHECK_EQ(sample_period_ns(20000000, 64 * 64, 32, 10000000), 20000000);  // never below base

@@ -261,11 +261,10 @@ def test_auto_mode_follows_the_crowd(fake):
 
 
 def test_sampler_period_stretches_on_a_crowded_gpu(fake):
-    """Eleven other busy processes share the GPU, so re-reading all of them every tick in
-    every limited container would cost the node ~n² cu_occupancy reads per ms
-    (profiles/r2ae: 12 pods lost 14 % of the GPU). The sampler keeps reading its own
-    processes every ~1 ms and refreshes the others' total every ~4.5 ms;
-    VGPU_SAMPLE_READ_BUDGET=0 re-reads everything every tick."""
+    """Eleven other busy processes share the GPU, so every limited container would read
+    twelve cu_occupancy files per tick: the sampler stretches its period to ~4.5 ms
+    (profiles/r2ae: 1 ms ticks cost 12 pods 14 % of the GPU). VGPU_SAMPLE_READ_BUDGET=0
+    keeps the fixed ~1 ms period."""
     for pid in range(424300, 424311):
         _foreign(fake.kfd, pid, 40)
     got = {}
@@ -279,6 +278,6 @@ def test_sampler_period_stretches_on_a_crowded_gpu(fake):
             d = r.device(0)
         assert d["cu_mode"] == "temporal" and d["charged_ns"] > 0 and [o for o in out if "run" in o], d
     ticks, refreshes = got["32"]
-    assert ticks > 600 and refreshes < ticks / 2.5, got        # own reads ~1 kHz, others ~4 ms
     ticks0, refreshes0 = got["0"]
-    assert ticks0 > 600 and refreshes0 > 0.6 * ticks0, got     # everything every tick
+    assert ticks < 600 and ticks0 > 2.5 * ticks, got           # ~220 Hz vs ~1 kHz over 2 s
+    assert 0 < refreshes <= ticks and refreshes0 > 0.6 * ticks0, got  # others read while busy
