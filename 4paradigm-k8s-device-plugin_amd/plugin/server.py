@@ -13,6 +13,7 @@ backend reports recovery (``server.go:262``); ``Register`` and
 legacy-preferred ``acquire`` runs once per container (:456 and :484); monitor mode
 looks only at this node's pending pods and never indexes out of range (:376-392).
 """
+import collections
 import logging
 import os
 import threading
@@ -61,7 +62,9 @@ class DevicePluginServer:
         self.fatal = None            # set when the restart budget is exhausted
         self.watchdog_period_s = WATCHDOG_PERIOD_S
         self.vdevices = []
-        self.allocations = []  # (request ids, using ids) — observability / tests
+        # (request ids, using ids) of recent Allocate calls, for observability; bounded so a
+        # long-lived plugin does not grow with every container start.
+        self.allocations = collections.deque(maxlen=1024)
 
     # ------------------------------------------------------------------ lifecycle
     def initialize(self):
