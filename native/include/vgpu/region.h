@@ -113,6 +113,9 @@ struct RegionHeader {
   std::atomic<uint64_t> samples;            // sampler ticks (temporal mode)
 };
 
+// Wait bound for the region lock on paths that must not hang behind a stopped holder.
+constexpr int kLockTimeoutMs = 500;
+
 enum RegionFlags : uint32_t { kFlagOversubscribe = 1u, kFlagActiveOomKiller = 2u };
 
 struct Region {
@@ -145,6 +148,10 @@ class SharedRegion {
 
   // Robust lock. Returns false only if the mutex is unrecoverable.
   bool lock();
+  // lock() that gives up after `timeout_ms` (false): for paths that must not hang behind
+  // a lock holder that is alive but stopped (SIGSTOP, a debugger, a frozen cgroup). The
+  // reference's lock_shrreg used sem_timedwait for the same reason.
+  bool lock_for(int timeout_ms);
   void unlock();
 
   // Process slots.

@@ -11,6 +11,7 @@
 #include <sys/file.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -212,6 +213,28 @@ bool SharedRegion::lock() {
   return rc == 0;
 }
 
+bool SharedRegion::lock_for(int timeout_ms) {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);  // pthread_mutex_timedlock's clock
+  ts.tv_sec += timeout_ms / 1000;
+  ts.tv_nsec += (long)(timeout_ms % 1000) * 1000000L;
+  if (ts.tv_nsec >= 1000000000L) {
+    ts.tv_sec++;
+    ts.tv_nsec -= 1000000000L;
+  }
+  int rc = pthread_mutex_timedlock(&r_->hdr.mutex, &ts);
+  if (rc == EOWNERDEAD) {
+    VLOG_WARN("shared region lock owner died; recovering");
+    pthread_mutex_consistent(&r_->hdr.mutex);
+    return true;
+  }
+  if (rc == ETIMEDOUT) {
+    VLOG_WARN("shared region lock still held after %d ms (holder stopped?); going on without it", timeout_ms);
+    return false;
+  }
+  return rc == 0;
+}
+
 void SharedRegion::unlock() { pthread_mutex_unlock(&r_->hdr.mutex); }
 
 int SharedRegion::num_devices() const { return r_ ? r_->hdr.num_devices : 0; }
@@ -288,7 +311,9 @@ void SharedRegion::unregister_process(int slot) {
 
 int SharedRegion::reclaim_dead() {
   if (!r_) return 0;
-  if (!lock()) return 0;
+  // Reached from the allocation path (charge over the limit): a stopped lock holder must
+  // turn into an OOM for the caller, not a hang.
+  if (!lock_for(kLockTimeoutMs)) return 0;
   int n = 0;
   for (int i = 0; i < kMaxProcs; i++) {
     ProcSlot& s = r_->procs[i];
@@ -383,7 +408,7 @@ void SharedRegion::set_limit(int dev, uint64_t bytes) {
 
 void SharedRegion::set_cu_limit(int dev, int pct) {
   DeviceState& d = r_->dev[dev];
-  bool locked = lock();
+  bool locked = lock_for(kLockTimeoutMs);  // node tools must not hang behind a stopped tenant
   d.cu_limit_pct = pct;
   if (d.configured && d.cu_count > 0) {
     // Keep the vGPU's anchor (the start of the slice the plugin assigned) and resize the

@@ -413,13 +413,16 @@ void apply_live_config() {
   for (int i = 0; i < s.n_agents; i++) {
     AgentInfo& a = s.agents[i];
     DeviceState& d = r->dev[i];
-    s.region.lock();
+    // Bounded wait: this runs from the launch path, which must not hang behind a region
+    // lock holder that is stopped; without the lock the read may see a half-written mask,
+    // which the writer's generation bump makes every process re-read.
+    const bool locked = s.region.lock_for(kLockTimeoutMs);
     CuMask m;
     memcpy(m.words, d.cu_mask, sizeof(m.words));
     m.nbits = d.cu_mask_bits ? d.cu_mask_bits : a.cu_count;
     const int pct = d.cu_limit_pct;
     const bool ranged = d.cu_range_begin >= 0;
-    s.region.unlock();
+    if (locked) s.region.unlock();
     const bool limited = pct > 0 && pct < 100;
     const CuMode mode = effective_cu_mode(cfg.cu_mode, pct, d.crowd.load(std::memory_order_relaxed));
     const bool spatial = mode == CuMode::kSpatial || mode == CuMode::kBoth;

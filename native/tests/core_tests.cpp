@@ -322,6 +322,48 @@ static void test_region_robust_lock() {
   unlink(p.c_str());
 }
 
+// Fault injection (SURVEY §5 "SIGSTOP the lock owner"): a process stopped while it holds
+// the region lock. Charges under the limit never take the lock; an over-limit charge (its
+// reclaim pass wants the lock) turns into an OOM within the bound instead of hanging, and
+// set_cu_limit (vgpuctl, the monitor) completes too. Once the holder dies the robust
+// mutex recovers.
+static void test_region_stopped_lock_owner() {
+  std::string p = tmp_region("stopped");
+  Config c = limits_cfg(1000);
+  SharedRegion r;
+  CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+  int s = r.register_process(getpid(), getpid(), 1);
+  pid_t pid = fork();
+  if (pid == 0) {
+    SharedRegion rc;
+    if (rc.attach(p.c_str(), nullptr, false) != 0) _exit(2);
+    rc.lock();
+    raise(SIGSTOP);
+    _exit(0);
+  }
+  int st = 0;
+  CHECK_EQ(waitpid(pid, &st, WUNTRACED), pid);
+  CHECK(WIFSTOPPED(st));
+  uint64_t t0 = now_ns();
+  CHECK(r.charge(s, 0, 600, kMemData) == Charge::kOk);         // lock-free admission
+  CHECK(now_ns() - t0 < 100'000'000ull);
+  t0 = now_ns();
+  CHECK(r.charge(s, 0, 600, kMemData) == Charge::kOverLimit);  // reclaim gives up: OOM
+  uint64_t waited = now_ns() - t0;
+  CHECK(waited >= (uint64_t)kLockTimeoutMs * 900000ull && waited < (uint64_t)kLockTimeoutMs * 3000000ull);
+  t0 = now_ns();
+  r.set_cu_limit(0, 25);
+  CHECK(now_ns() - t0 < (uint64_t)kLockTimeoutMs * 3000000ull);
+  CHECK_EQ(r.raw()->dev[0].cu_limit_pct, 25);
+  kill(pid, SIGKILL);
+  waitpid(pid, &st, 0);
+  CHECK(r.lock());  // EOWNERDEAD -> consistent
+  r.unlock();
+  r.uncharge(s, 0, 600, kMemData);
+  r.unregister_process(s);
+  unlink(p.c_str());
+}
+
 static void test_region_version_guard() {
   std::string p = tmp_region("ver");
   Config c = limits_cfg(1);
@@ -883,6 +925,7 @@ int main(int argc, char** argv) {
       {"cumask_se_layout", test_cumask_se_layout},
       {"devmap", test_devmap},
       {"ratelimit", test_ratelimit},
+      {"region_stopped_lock_owner", test_region_stopped_lock_owner},
       {"auto_mode_live_cu", test_auto_mode_and_live_cu},
       {"charge_overflow", test_charge_overflow},
       {"kfd", test_kfd},
