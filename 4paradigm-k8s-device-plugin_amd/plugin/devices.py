@@ -18,6 +18,7 @@ configurable topology for tests and the stub-kubelet config (no GPU).
 import glob
 import json
 import os
+import time
 import threading
 from dataclasses import dataclass, field
 
@@ -123,14 +124,25 @@ def rocr_uuid(unique_id):
     return f"GPU-{unique_id:016x}" if unique_id else ""
 
 
+# A GPU marked unhealthy by uncorrectable RAS errors returns to Healthy only after its
+# UE counter stayed flat this long, or at once on an observed GPU reset (amdsmi
+# POST_RESET): an uncorrectable error usually needs a reset, and flapping back after one
+# flat poll would hand the device to new pods while it is still suspect.
+RAS_RECOVER_S = float(os.environ.get("VGPU_RAS_RECOVER_S", "300"))
+
+
 class SysfsBackend(Backend):
     """KFD-topology + DRM sysfs inventory and RAS-counter health (no root, no GPU context)."""
 
     name = "sysfs"
 
-    def __init__(self, kfd_root="/sys/class/kfd/kfd/topology/nodes", drm_root="/sys/class/drm"):
+    def __init__(self, kfd_root="/sys/class/kfd/kfd/topology/nodes", drm_root="/sys/class/drm",
+                 ras_recover_s=None, clock=time.monotonic):
         self.kfd_root, self.drm_root = kfd_root, drm_root
         self._ras = {}
+        self._ras_bad_at = {}   # uuid -> time of the last UE increase (RAS-unhealthy devices)
+        self.ras_recover_s = RAS_RECOVER_S if ras_recover_s is None else ras_recover_s
+        self._clock = clock
 
     def _drm_dev(self, minor):
         return os.path.join(self.drm_root, f"renderD{minor}", "device")
@@ -199,22 +211,34 @@ class SysfsBackend(Backend):
         return total
 
     def poll_health(self, devices):
-        """Uncorrectable RAS errors -> Unhealthy; device node vanished -> Unhealthy; a device
-        whose node is back and whose UE count stayed flat for one poll -> Healthy again
-        (the reference never recovers, server.go:262)."""
+        """Uncorrectable RAS errors -> Unhealthy; device node vanished -> Unhealthy. Recovery
+        (the reference never recovers, server.go:262): a node that is back, with a flat UE
+        count for one poll, is Healthy again (the driver re-created it); a RAS-unhealthy
+        device once its UE count stayed flat for ``ras_recover_s`` (or at a reset event,
+        AmdSmiBackend)."""
         events = []
+        now = self._clock()
         for d in devices:
             present = os.path.exists(os.path.join(self.kfd_root, str(d.node_id), "gpu_id")) if d.node_id >= 0 else True
             ue = self._ras_ue(d) if present else None
             prev = self._ras.get(d.uuid)
             self._ras[d.uuid] = ue
-            if not present and d.healthy:
+            if present and prev is not None and ue is not None and ue > prev:
+                self._ras_bad_at[d.uuid] = now
+                if d.healthy:
+                    events.append(HealthEvent(d.uuid, False, f"uncorrectable RAS errors {prev}->{ue}"))
+            elif not present and d.healthy:
                 events.append(HealthEvent(d.uuid, False, "device node disappeared"))
-            elif present and prev is not None and ue is not None and ue > prev and d.healthy:
-                events.append(HealthEvent(d.uuid, False, f"uncorrectable RAS errors {prev}->{ue}"))
             elif present and not d.healthy and prev is not None and ue == prev:
-                events.append(HealthEvent(d.uuid, True, "device recovered"))
+                bad_at = self._ras_bad_at.get(d.uuid)
+                if bad_at is None or now - bad_at >= self.ras_recover_s:
+                    self._ras_bad_at.pop(d.uuid, None)
+                    events.append(HealthEvent(d.uuid, True, "device recovered"))
         return events
+
+    def reset_observed(self, uuid):
+        """A GPU reset clears the RAS hold-off: the device may recover at once."""
+        self._ras_bad_at.pop(uuid, None)
 
 
 # ----------------------------------------------------------------------------- amdsmi
@@ -287,6 +311,7 @@ class AmdSmiBackend(SysfsBackend):
             if "PRE_RESET" in kind or "RING_HANG" in kind:
                 events.append(HealthEvent(uuid, False, kind))
             elif "POST_RESET" in kind:
+                self.reset_observed(uuid)
                 events.append(HealthEvent(uuid, True, kind))
         return events
 

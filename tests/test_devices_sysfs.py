@@ -67,16 +67,54 @@ def test_cpx_partitions_get_distinct_uuids(tmp_path):
 
 
 def test_ras_health_and_recovery(tmp_path):
+    """Uncorrectable errors mark the GPU unhealthy; it recovers only after the UE count
+    stayed flat for the hold-off (or at a reset), not after one quiet poll."""
     kfd, drm = make_tree(tmp_path, ngpu=1)
-    be = SysfsBackend(kfd, drm)
+    now = [1000.0]
+    be = SysfsBackend(kfd, drm, ras_recover_s=300, clock=lambda: now[0])
     devs = be.devices()
     assert be.poll_health(devs) == []
-    (tmp_path / "drm" / "renderD129" / "device" / "ras" / "umc_err_count").write_text("ue: 3\nce: 0\n")
+    ras = tmp_path / "drm" / "renderD129" / "device" / "ras" / "umc_err_count"
+    ras.write_text("ue: 3\nce: 0\n")
     ev = be.poll_health(devs)
     assert len(ev) == 1 and not ev[0].healthy
     devs[0].healthy = False
+    now[0] += 5
+    assert be.poll_health(devs) == []          # flat, but inside the hold-off
+    now[0] += 200
+    ras.write_text("ue: 4\nce: 0\n")          # another UE restarts the hold-off
+    assert be.poll_health(devs) == []
+    now[0] += 299
+    assert be.poll_health(devs) == []
+    now[0] += 2
     ev = be.poll_health(devs)
-    assert len(ev) == 1 and ev[0].healthy  # stable UE count -> recovered
+    assert len(ev) == 1 and ev[0].healthy      # 301 s flat -> recovered
+    devs[0].healthy = True
+    ras.write_text("ue: 5\nce: 0\n")
+    ev = be.poll_health(devs)
+    assert len(ev) == 1 and not ev[0].healthy
+    devs[0].healthy = False
+    be.reset_observed(devs[0].uuid)            # a GPU reset clears the hold-off
+    now[0] += 5
+    ev = be.poll_health(devs)
+    assert len(ev) == 1 and ev[0].healthy
+
+
+def test_vanished_node_recovers_when_back(tmp_path):
+    kfd, drm = make_tree(tmp_path, ngpu=1)
+    be = SysfsBackend(kfd, drm)
+    devs = be.devices()
+    gid = os.path.join(kfd, str(devs[0].node_id), "gpu_id")
+    saved = open(gid).read()
+    os.unlink(gid)
+    ev = be.poll_health(devs)
+    assert len(ev) == 1 and not ev[0].healthy
+    devs[0].healthy = False
+    with open(gid, "w") as f:
+        f.write(saved)
+    assert be.poll_health(devs) == []          # back: UE count read again (first poll)
+    ev = be.poll_health(devs)
+    assert len(ev) == 1 and ev[0].healthy
 
 
 def test_bdf_decode():
