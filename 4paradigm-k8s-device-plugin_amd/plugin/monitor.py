@@ -144,9 +144,12 @@ def control(root, tag, action, params):
             elif action == "reclaim":
                 r.reclaim()
             elif action == "limit":
-                r.set_memory_limit(int(params.get("dev", 0)), int(params["bytes"]))
+                nbytes = int(params["bytes"])
+                if nbytes < 0 or r.set_memory_limit(int(params.get("dev", 0)), nbytes) != 0:
+                    raise ValueError(f"invalid device or size: {params}")
             elif action == "cu":
-                r.set_cu_limit(int(params.get("dev", 0)), int(params["pct"]))
+                if r.set_cu_limit(int(params.get("dev", 0)), int(params["pct"])) != 0:
+                    raise ValueError(f"invalid device or CU share (0-100): {params}")
             elif action == "priority":
                 r.priority = int(params["value"])
             else:

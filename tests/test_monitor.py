@@ -43,6 +43,10 @@ def test_metrics_and_control(tmp_path):
     control(root, "pod1_main", "block", {})
     assert r.recent_kernel < 0
     control(root, "pod1_main", "unblock", {})
+    with pytest.raises(ValueError):
+        control(root, "pod1_main", "cu", {"dev": "0", "pct": "150"})
+    with pytest.raises(ValueError):
+        control(root, "pod1_main", "limit", {"dev": "99", "bytes": "1"})
     control(root, "pod1_main", "priority", {"value": "3"})
     assert r.priority == 3
     r.close()
