@@ -53,6 +53,9 @@ class DevicePluginServer:
         self.legacy = legacy
         self.pod_matcher = pod_matcher
         self._cond = threading.Condition()
+        # Allocate runs on the gRPC thread pool; with the legacy controller its
+        # read-available / choose / acquire sequence must not interleave with another call's.
+        self._alloc_mu = threading.Lock()
         self._version = 0
         self._stopped = threading.Event()
         self._server = None
@@ -256,6 +259,12 @@ class DevicePluginServer:
         raise AllocationError(msg)
 
     def Allocate(self, request, context):
+        if self.legacy is None:
+            return self._allocate(request, context)
+        with self._alloc_mu:
+            return self._allocate(request, context)
+
+    def _allocate(self, request, context):
         resp = api.AllocateResponse()
         if self.partition_resource:
             for req in request.container_requests:

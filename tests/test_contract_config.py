@@ -207,3 +207,28 @@ def test_fused_lstm_routes_oversize_inputs_to_the_library():
         lstm.weight_ih_l0.mul_(2)
     f._refresh()
     assert torch.allclose(f.w_ih_perm.view(128, 4, 8).permute(1, 0, 2).reshape(512, 8), lstm.weight_ih_l0)
+
+
+def test_legacy_allocate_concurrent_calls_never_share_a_vgpu(tmp_path):
+    """Allocate runs on the gRPC thread pool: concurrent legacy-mode calls must each get
+    their own vGPUs (the read-available / acquire sequence is serialised)."""
+    import threading
+
+    srv, ids, _ = _legacy_server(tmp_path, split=8)
+    _checkpoint(tmp_path, [])
+    got, errors = [], []
+
+    def one(i):
+        try:
+            resp = srv.Allocate(_alloc_req([ids[i]]), None)
+            got.append(dict(resp.container_responses[0].annotations)[ANN_USING])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    threads = [threading.Thread(target=one, args=(i,)) for i in range(8)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
+    assert len(got) == 8 and len(set(got)) == 8, got
