@@ -128,13 +128,15 @@ class Supervisor:
     def _loop(self, stop_event):
         kubelet_sock = os.path.normpath(self.cfg.kubelet_socket)
         need_restart = True
+        retry_at = 0.0
         while True:
-            if need_restart:
+            # A failed start (kubelet not up yet) is retried every second, but events keep
+            # being read meanwhile, so signals and a stop request still end the plugin.
+            if need_restart and time.monotonic() >= retry_at:
                 need_restart = False
                 if not self.start_plugins():
-                    time.sleep(1.0)
                     need_restart = True
-                    continue
+                    retry_at = time.monotonic() + 1.0
             try:
                 ev = self.events.get(timeout=0.2)
             except queue.Empty:
@@ -148,13 +150,13 @@ class Supervisor:
             if isinstance(ev, tuple) and ev[0] == "signal":
                 if ev[1] == signal.SIGHUP:
                     log.info("received SIGHUP, restarting")
-                    need_restart = True
+                    need_restart, retry_at = True, 0.0
                     continue
                 log.info("received signal %d, shutting down", ev[1])
                 return 0
             if os.path.normpath(ev.name) == kubelet_sock and ev.op == "create":
                 log.info("inotify: %s created, restarting", kubelet_sock)
-                need_restart = True
+                need_restart, retry_at = True, 0.0
 
 
 def main(argv=None):

@@ -213,3 +213,19 @@ def test_grpc_server_watchdog_restarts_and_budget(plugin_dir):
         assert not th.is_alive() and p.fatal
     finally:
         shutdown(k, stop, th)
+
+
+def test_stop_honoured_while_the_kubelet_is_down(plugin_dir):
+    """No kubelet socket: registration keeps failing and is retried every second, but a
+    stop request (or a signal) still ends the supervisor promptly."""
+    cfg = PluginConfig(device_plugin_path=plugin_dir + "/", backend="fake", health_interval_s=0.1,
+                       vgpu_dir="/usr/local/vgpu").validate()
+    sup = Supervisor(cfg, backend=FakeBackend(n=1), install_signals=False)
+    stop = threading.Event()
+    th = threading.Thread(target=sup.run, args=(stop,), daemon=True)
+    th.start()
+    time.sleep(2.5)
+    assert th.is_alive() and sup.restarts == 0   # still retrying
+    stop.set()
+    th.join(timeout=10)   # at most one registration attempt (dial timeouts) in flight
+    assert not th.is_alive()
