@@ -838,11 +838,13 @@ static void test_hostpid_resolution() {
   // and allocate: every one resolves its own host PID (serialised by the lock).
   const int kStarters = 16;
   for (int i = 0; i < kStarters; i++) k.add(1000 + i, (int64_t)(i + 1) << 21);
-  std::atomic<bool> stop{false};
+  // The noise process stops cooperatively (a stop file): killing it could orphan one of
+  // its `mkdir -p` helpers, which then races the final rm -rf.
+  const std::string stop_file = kroot + "/stop";
   pid_t noise = fork();
   if (noise == 0) {
     unsigned rng = 99;
-    for (int it = 0; it < 4000; it++) {
+    for (int it = 0; it < 4000 && access(stop_file.c_str(), F_OK) != 0; it++) {
       rng = rng * 1103515245u + 12345u;
       int p = 5000 + (int)((rng >> 8) % 64);
       if ((rng >> 20) % 3 == 0) k.add(p, 0);
@@ -867,8 +869,8 @@ static void test_hostpid_resolution() {
     waitpid(c, &st, 0);
     ok += WIFEXITED(st) && WEXITSTATUS(st) == 0;
   }
-  stop = true;
-  kill(noise, SIGKILL);
+  FILE* sf = fopen(stop_file.c_str(), "w");
+  if (sf) fclose(sf);
   waitpid(noise, nullptr, 0);
   CHECK_EQ(ok, kStarters);
   CHECK(system(("rm -rf " + kroot).c_str()) == 0);
