@@ -58,7 +58,10 @@ class PodMatcher:
     The kubelet's Allocate carries only device IDs; the reference recovers the pod by
     matching per-container GPU counts against pending pods (server.go:381-405). Matching
     is over containers *with* GPUs, in order; the oldest matching pending pod wins.
-    Returns one "<pod>_<container>" tag per container request.
+    Returns one "<namespace>_<pod>_<container>" tag per container request (the
+    reference's "<pod>_<container>" would give two same-named pods of different namespaces
+    one host directory, so the monitor would control both as one container). Kubernetes
+    names never contain "_", so the tag is unambiguous.
     """
 
     def __init__(self, list_pods):
@@ -70,5 +73,6 @@ class PodMatcher:
         for p in pods:
             gpu_ctrs = [c for c in p["containers"] if c["gpus"] > 0]
             if [c["gpus"] for c in gpu_ctrs] == list(request_sizes):
-                return [f"{p['name']}_{c['name']}" for c in gpu_ctrs]
+                prefix = f"{p['namespace']}_" if p.get("namespace") else ""
+                return [f"{prefix}{p['name']}_{c['name']}" for c in gpu_ctrs]
         raise LookupError(f"no pending pod requests {request_sizes} GPUs per container")

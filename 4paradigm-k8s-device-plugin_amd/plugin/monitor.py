@@ -1,7 +1,7 @@
 """Node-side vGPU monitor: Prometheus metrics + control API over the containers' regions.
 
 Reference: with ``VGPU_MONITOR_MODE`` each container's shared region lives on a host path
-``/usr/local/vgpu/shared/<pod>_<ctr>/<uuid>.cache`` (``server.go:494-501``) so that an
+``/usr/local/vgpu/shared/<ns>_<pod>_<ctr>/<uuid>.cache`` (``server.go:494-501``) so that an
 *external* monitor can mmap it and drive the control API exported by libvgpu.so
 (``suspend_all``, ``resume_all``, ``set_current_device_sm_limit_scale``,
 ``set_current_device_memory_limit``, ``recent_kernel``, ``priority``).
@@ -33,7 +33,7 @@ log = logging.getLogger("amdvgpu.monitor")
 
 
 def discover(root):
-    """{container tag: [region paths]} under ``root/<pod>_<ctr>/*.cache``."""
+    """{container tag: [region paths]} under ``root/<ns>_<pod>_<ctr>/*.cache``."""
     out = {}
     for p in sorted(glob.glob(os.path.join(root, "*", "*.cache"))):
         out.setdefault(os.path.basename(os.path.dirname(p)), []).append(p)

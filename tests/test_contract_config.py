@@ -137,6 +137,12 @@ def test_monitor_pod_matcher():
     assert m.match([1]) == ["new_main"]
     with pytest.raises(LookupError):
         m.match([2])
+    # Same pod name in two namespaces: distinct tags (distinct host dirs for the monitor).
+    twin = [pod_summary({"metadata": {"uid": u, "name": "train", "namespace": ns, "creationTimestamp": t},
+                         "spec": {"containers": [{"name": "main", "resources": {"limits": {"amd.com/gpu": "1"}}}]},
+                         "status": {"phase": "Pending"}}) for u, ns, t in (("a", "team-a", "1"), ("b", "team-b", "2"))]
+    assert PodMatcher(lambda: twin).match([1]) == ["team-a_train_main"]
+    assert PodMatcher(lambda: twin[1:]).match([1]) == ["team-b_train_main"]
 
 
 def _legacy_server(tmp_path, split=2):
