@@ -161,13 +161,14 @@ def main():
           "|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         pt = r["per_tenant"]
-        b = base.get(r["policy"], rows[0]["aggregate_throughput"])
+        b = base.get(r["policy"])  # no 1-pod run of this policy in the sweep: no ratios
         pe = " ".join(f"{k}={v}" for k, v in (r["pod_env"] or {}).items()) or "-"
+        vs_one = f"{r['aggregate_throughput'] / b:.2f}x" if b else "n/a"
+        slowest = f"{min(pt) / (b / (r['tenants'] if r['split'] == r['tenants'] else 1)):.2f}" if b else "n/a"
         md.append(f"| {r['policy']} ({MODES[r['policy']]}) | {r['split']} | {'/'.join(r['modes'])} | {pe} | "
                   f"{r['hw_queues'] or 'default'} | {r['kfd_queues']} | "
                   f"{r['tenants']} | {r['aggregate_throughput']:.1f} | "
-                  f"{r['aggregate_throughput'] / b:.2f}x | {min(pt):.1f} .. {max(pt):.1f} | "
-                  f"{min(pt) / (b / (r['tenants'] if r['split'] == r['tenants'] else 1)):.2f} |")
+                  f"{vs_one} | {min(pt):.1f} .. {max(pt):.1f} | {slowest} |")
     print("\n".join(md))
     if a.json_out:
         json.dump(rows, open(a.json_out, "w"), indent=1)
