@@ -37,9 +37,14 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
     for _ in range(warmup):
         r.step()
     torch.cuda.synchronize()
+    region = None
+    if os.environ.get("VGPU_SHARED_CACHE") and os.path.exists(os.environ["VGPU_SHARED_CACHE"]):
+        from amdvgpu.shim.region import Region
+        region = Region(os.environ["VGPU_SHARED_CACHE"])
     open(out + ".ready", "w").close()
     while not os.path.exists(go_file):
         time.sleep(0.005)
+    g0 = region.device(0) if region else None
     n = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -49,13 +54,19 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    mode = crowd = None
-    if os.environ.get("VGPU_SHARED_CACHE") and os.path.exists(os.environ["VGPU_SHARED_CACHE"]):
-        from amdvgpu.shim.region import Region
-        with Region(os.environ["VGPU_SHARED_CACHE"]) as r:  # the enforcement the pod ended under
-            mode, crowd = r.device(0)["cu_mode"], r.device(0)["crowd"]
-    json.dump({"ms_per_batch": (t1 - t0) * 1000 / n, "t0": t0, "t1": t1, "batch": case.batch, "steps": n,
-               "throughput": case.batch * n / (t1 - t0), "cu_mode": mode, "crowd": crowd}, open(out, "w"))
+    res = {"ms_per_batch": (t1 - t0) * 1000 / n, "t0": t0, "t1": t1, "batch": case.batch, "steps": n,
+           "throughput": case.batch * n / (t1 - t0), "cu_mode": None, "crowd": None}
+    if region:
+        g1 = region.device(0)  # the enforcement the pod ended under, and the GPU time it was charged
+        res.update(cu_mode=g1["cu_mode"], crowd=g1["crowd"])
+        if g1["wall_ns"] > g0["wall_ns"]:
+            charged_ms = (g1["charged_ns"] - g0["charged_ns"]) / 1e6
+            res["gpu_ms_charged"] = round(charged_ms, 2)
+            res["granted_pct"] = round(100.0 * (g1["charged_ns"] - g0["charged_ns"]) / (g1["wall_ns"] - g0["wall_ns"]), 2)
+            if charged_ms > 0:  # throughput per charged GPU-millisecond (profiles/r2ak)
+                res["images_per_gpu_ms"] = round(case.batch * n / charged_ms, 4)
+        region.close()
+    json.dump(res, open(out, "w"))
 
 
 MODES = {"default": "auto", "spatial": "spatial", "temporal": "temporal", "shared": "off"}
@@ -115,7 +126,9 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
     return {"tenants": n, "policy": policy, "split": split or n, "hw_queues": hw_queues or None, "kfd_queues": queues,
             "pod_env": pod_env or None, "modes": sorted({str(r.get("cu_mode")) for r in res}),
             "aggregate_throughput": agg,
-            "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res]}
+            "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res],
+            "per_tenant_granted_pct": [r.get("granted_pct") for r in res],
+            "per_tenant_images_per_gpu_ms": [r.get("images_per_gpu_ms") for r in res]}
 
 
 def main():
