@@ -74,10 +74,9 @@ int64_t kfd_vram_usage(pid_t hostpid, uint32_t gpu_id) {
 std::vector<int> kfd_pids_on_gpu(uint32_t gpu_id) {
   std::vector<int> out;
   char path[256];
-  struct stat st;
   for (int p : kfd_list_pids()) {
     snprintf(path, sizeof(path), "%s/%d/stats_%u", g_kfd_proc_root, p, gpu_id);
-    if (stat(path, &st) == 0) out.push_back(p);
+    if (access(path, F_OK) == 0) out.push_back(p);  // not stat (GLIBC_2.33, glibc_compat.h)
   }
   return out;
 }

@@ -42,3 +42,30 @@ def test_calibration_kernels_target_gfx950():
     """The calibration kernels are a gfx950 code object bundle (hipcc --offload-arch=gfx950)."""
     data = open(os.path.join(LIB_DIR, "libvgpu_kernels.so"), "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_shim_needs_only_old_glibc():
+    """The preloaded shim must load in tenant images older than this build host: no C++
+    runtime dependency (libstdc++/libgcc are static and local) and C library symbol
+    versions no newer than glibc 2.17 (include/vgpu/glibc_compat.h,
+    src/shim/glibc_shims.cpp); libdl/libpthread are linked for glibcs that keep the
+    dl/pthread functions there."""
+    import re
+    import shutil
+    import subprocess
+
+    import pytest
+    from amdvgpu.shim.native import shim_path
+    if not shutil.which("readelf"):
+        pytest.skip("readelf not available")
+    lib = shim_path()
+    dyn = subprocess.run(["readelf", "-d", lib], capture_output=True, text=True).stdout
+    needed = re.findall(r"Shared library: \[([^\]]+)\]", dyn)
+    assert not any(n.startswith(("libstdc++", "libgcc_s")) for n in needed), needed
+    assert "libdl.so.2" in needed and "libpthread.so.0" in needed, needed
+    ver = subprocess.run(["readelf", "-V", lib], capture_output=True, text=True).stdout
+    needs = ver.split("Version needs", 1)[1] if "Version needs" in ver else ""
+    names = re.findall(r"Name: (\S+)", needs)
+    assert not [n for n in names if n.startswith(("GLIBCXX", "CXXABI", "GCC_"))], names
+    glibc = [tuple(int(x) for x in n.split("_", 1)[1].split(".")) for n in names if n.startswith("GLIBC_")]
+    assert glibc and max(glibc) <= (2, 17), sorted(glibc)
