@@ -4,6 +4,7 @@
 #include <pthread.h>
 #include <signal.h>
 #include <strings.h>
+#include <sys/auxv.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -176,6 +177,14 @@ void on_exit() {
 }
 
 void load_env_config() {
+  // Secure-execution mode (setuid/setgid or file capabilities): /etc/ld.so.preload still
+  // loads the shim, but the environment belongs to the less privileged caller, so none
+  // of it (region path, override file, limits) may steer a privileged process. The shim
+  // stays a pass-through there.
+  if (getauxval(AT_SECURE)) {
+    mutable_config().disabled = true;
+    return;
+  }
   log_init_from_env();
   // Alternate KFD process tree (the CPU-only fake runtime of the test suite).
   if (const char* k = getenv("VGPU_KFD_ROOT"))

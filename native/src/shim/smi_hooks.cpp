@@ -82,7 +82,7 @@ struct Bdf {
 std::vector<Bdf> visible_bdfs() {
   std::vector<Bdf> out;
   const bool attached = shim_attach_region_only();  // also loads the env config
-  if (!config().hook_smi) return out;
+  if (!config().hook_smi || config().disabled) return out;
   if (const char* s = getenv("VGPU_DEVICE_BDFS")) {
     const char* p = s;
     while (*p) {
