@@ -87,7 +87,8 @@ _FLAGS = [
     ("--device-list-strategy", "device_list_strategy", str, ["DEVICE_LIST_STRATEGY"],
      "how visible devices reach the container: envvar | amd-container-runtime | volume-mounts"),
     ("--device-id-strategy", "device_id_strategy", str, ["DEVICE_ID_STRATEGY"], "uuid | index"),
-    ("--driver-root", "driver_root", str, ["AMD_DRIVER_ROOT", "DRIVER_ROOT"], "root of the host's /dev tree"),
+    ("--driver-root", "driver_root", str, ["AMD_DRIVER_ROOT", "DRIVER_ROOT", "NVIDIA_DRIVER_ROOT"],
+     "root of the host's /dev tree"),
     ("--device-split-count", "device_split_count", int, ["DEVICE_SPLIT_COUNT"], "vGPUs per physical GPU"),
     ("--device-memory-scaling", "device_memory_scaling", float, ["DEVICE_MEMORY_SCALING"],
      "memory oversubscription ratio (>1 spills to host memory)"),
@@ -116,7 +117,8 @@ def build_parser():
     ap = argparse.ArgumentParser(prog="amd-vgpu-device-plugin",
                                  description="MI355X vGPU device plugin for Kubernetes")
     for flag, dest, typ, envs, help_ in _FLAGS:
-        names = [flag] + (["--mig-strategy"] if dest == "partition_strategy" else [])
+        # The reference's flag names stay accepted, so its manifests work unchanged.
+        names = [flag] + {"partition_strategy": ["--mig-strategy"], "driver_root": ["--nvidia-driver-root"]}.get(dest, [])
         if typ == "bool":
             ap.add_argument(*names, dest=dest, nargs="?", const="true", default=None,
                             help=f"{help_} (env {', '.join(envs)})")

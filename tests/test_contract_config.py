@@ -238,3 +238,13 @@ def test_legacy_allocate_concurrent_calls_never_share_a_vgpu(tmp_path):
         t.join()
     assert not errors, errors
     assert len(got) == 8 and len(set(got)) == 8, got
+
+
+def test_reference_flag_and_env_names_accepted():
+    """The reference's manifests work unchanged: --mig-strategy / MIG_STRATEGY and
+    --nvidia-driver-root / NVIDIA_DRIVER_ROOT map onto the MI355X flags."""
+    from amdvgpu.plugin.config import parse_config
+    c = parse_config(["--nvidia-driver-root=/run/driver", "--mig-strategy=single"], environ={})
+    assert c.driver_root == "/run/driver" and c.partition_strategy == "single"
+    c = parse_config([], environ={"NVIDIA_DRIVER_ROOT": "/x", "MIG_STRATEGY": "mixed"})
+    assert c.driver_root == "/x" and c.partition_strategy == "mixed"
