@@ -150,7 +150,8 @@ class SharedRegion {
   bool lock();
   // lock() that gives up after `timeout_ms` (false): for paths that must not hang behind
   // a lock holder that is alive but stopped (SIGSTOP, a debugger, a frozen cgroup). The
-  // reference's lock_shrreg used sem_timedwait for the same reason.
+  // reference's lock_shrreg uses sem_timedwait for the same reason
+  // (libvgpu.so lock_shrreg@0x4426a [multiprocess_memory_limit.c:516-540]).
   bool lock_for(int timeout_ms);
   void unlock();
 
