@@ -264,9 +264,11 @@ def run_one(args, mode, env, port):
     fd, result = tempfile.mkstemp(prefix=f"bench-{mode}-", suffix=".json")
     os.close(fd)
     try:
+        t0 = time.time()
         rc = subprocess.call(worker_cmd(args, mode, result, port), env=env)
         if rc != 0:
             raise SystemExit(f"bench worker ({mode}) failed with exit code {rc}")
+        print(f"[bench] {mode}: worker done in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
         if int(os.environ.get("RANK", 0)) != 0:
             return None
         with open(result) as f:
@@ -338,6 +340,7 @@ def sweep(args, backend, uuid, tenants):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     rows = []
     for n in tenants:
+        t_point = time.time()
         with NodeHarness(backend, device_split_count=n, cu_mode=args.cu_mode) as node:
             ids = node.vgpu_ids(uuid)[:n]
             pods = [pod_env(node, [i]) for i in ids]
@@ -349,8 +352,8 @@ def sweep(args, backend, uuid, tenants):
         rows.append({"tenants": n, "aggregate": round(agg, 2), "per_tenant": [round(t, 2) for t in tput],
                      "cu_limit_pct": int(c0.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0),
                      "cu_mode": c0.get("VGPU_CU_MODE"), "quota_mib": int(c0["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m"))})
-        print(f"[bench] sweep {n} tenants: aggregate {agg:.1f}, per tenant {min(tput):.1f}..{max(tput):.1f}",
-              file=sys.stderr, flush=True)
+        print(f"[bench] sweep {n} tenants: aggregate {agg:.1f}, per tenant {min(tput):.1f}..{max(tput):.1f} "
+              f"({time.time() - t_point:.0f} s)", file=sys.stderr, flush=True)
     base = next((r["aggregate"] for r in rows if r["tenants"] == 1), None)
     best = 0
     for r in rows:
