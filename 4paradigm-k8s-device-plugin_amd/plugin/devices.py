@@ -128,7 +128,15 @@ def rocr_uuid(unique_id):
 # UE counter stayed flat this long, or at once on an observed GPU reset (amdsmi
 # POST_RESET): an uncorrectable error usually needs a reset, and flapping back after one
 # flat poll would hand the device to new pods while it is still suspect.
-RAS_RECOVER_S = float(os.environ.get("VGPU_RAS_RECOVER_S", "300"))
+def _env_seconds(name, default):
+    try:
+        v = float(os.environ.get(name, default))
+    except ValueError:
+        return float(default)
+    return v if v >= 0 else float(default)
+
+
+RAS_RECOVER_S = _env_seconds("VGPU_RAS_RECOVER_S", 300)
 
 
 class SysfsBackend(Backend):
