@@ -11,6 +11,7 @@
 // relaxed increment of its own slot's launch counter, and relaxed loads of region words
 // (generation, suspend flags, launch block, and in temporal mode the device's credit).
 // The device lookup (hipGetDevice) only happens with several agents in temporal mode.
+
 // hip_runtime_api.h must be told its platform when a host compiler (g++) includes it;
 // AMD is the only platform this code is built for.
 #define __HIP_PLATFORM_AMD__ 1
