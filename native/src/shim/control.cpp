@@ -6,6 +6,7 @@
 //   cuVGPUViewAllocator (debug dump)        → vgpu_view_allocator
 // Names are prefixed: the shim is preloaded into arbitrary programs and must not
 // collide with their symbols.
+
 // hip_runtime_api.h must be told its platform when a host compiler (g++) includes it;
 // AMD is the only platform this code is built for.
 #define __HIP_PLATFORM_AMD__ 1
