@@ -30,6 +30,7 @@
 #include <sys/types.h>
 
 #include <atomic>
+#include <cstddef>
 #include <cstdint>
 
 #include "vgpu/config.h"
@@ -61,8 +62,11 @@ struct alignas(64) ProcSlot {
   std::atomic<uint64_t> throttle_ns;      // time spent blocked in the rate limiter
   std::atomic<uint64_t> suspend_ns;       // time spent blocked by suspend
   std::atomic<uint64_t> oom_events;
+  uint64_t pidns;                         // inode of the PID namespace `pid` lives in (0 = unknown)
   DeviceUsage used[kMaxDevices];
 };
+// pidns sits in what was alignment padding in layout v4: the layout is unchanged.
+static_assert(offsetof(ProcSlot, used) == 64, "ProcSlot layout changed");
 
 struct alignas(64) DeviceState {
   char uuid[64];
@@ -204,5 +208,9 @@ class SharedRegion {
 uint64_t proc_start_time(pid_t pid);
 // True if `pid` is alive and (when start_time != 0) is the same process.
 bool proc_alive(pid_t pid, uint64_t start_time);
+// Inode of the calling process's PID namespace (/proc/self/ns/pid), 0 if unreadable.
+uint64_t self_pidns();
+// The initial (host) PID namespace's inode (PROC_PID_INIT_INO).
+constexpr uint64_t kInitPidNs = 0xEFFFFFFCull;
 
 }  // namespace vgpu

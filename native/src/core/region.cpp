@@ -55,6 +55,37 @@ bool proc_alive(pid_t pid, uint64_t start_time) {
   return true;
 }
 
+uint64_t self_pidns() {
+  static const uint64_t ns = [] {
+    char buf[64];
+    ssize_t n = readlink("/proc/self/ns/pid", buf, sizeof(buf) - 1);
+    if (n <= 0) return (uint64_t)0;
+    buf[n] = 0;
+    const char* p = strchr(buf, '[');
+    return p ? (uint64_t)strtoull(p + 1, nullptr, 10) : (uint64_t)0;
+  }();
+  return ns;
+}
+
+namespace {
+
+// Whether a slot's process has exited, judged from the caller's PID namespace. A slot
+// records the PID in its own (container) namespace; a caller in another namespace (the
+// node monitor, vgpuctl on the host) must not look that PID up in its own /proc, where
+// it names an unrelated process or none (the slot of a live tenant would be freed and
+// its charges dropped). From the host namespace the slot's host PID is checked; from any
+// other namespace the slot is kept.
+bool slot_exited(const ProcSlot& s) {
+  const int32_t pid = s.pid.load();
+  const uint64_t me = self_pidns();
+  if (!s.pidns || !me || s.pidns == me) return !proc_alive(pid, s.start_time);
+  const int32_t hp = s.hostpid.load();
+  if (me == kInitPidNs && hp > 0) return !proc_alive(hp, s.start_time);  // start time is namespace-independent
+  return false;
+}
+
+}  // namespace
+
 SharedRegion::~SharedRegion() { detach(); }
 
 void SharedRegion::init_mutex(pthread_mutex_t* m) {
@@ -277,6 +308,7 @@ int SharedRegion::register_process(pid_t pid, pid_t hostpid, int priority) {
     s.oom_events.store(0);
     s.priority = priority;
     s.start_time = proc_start_time(pid);
+    s.pidns = pid == getpid() ? self_pidns() : 0;  // registered by someone else: unknown
     s.hostpid.store(hostpid);
     s.status.store(r_->hdr.suspend_all.load() ? kProcSuspended : kProcRunning);
     s.pid.store(pid, std::memory_order_release);
@@ -321,7 +353,7 @@ int SharedRegion::reclaim_dead() {
     ProcSlot& s = r_->procs[i];
     int32_t pid = s.pid.load();
     if (pid == 0) continue;
-    if (!proc_alive(pid, s.start_time)) {
+    if (slot_exited(s)) {
       VLOG_INFO("reclaiming slot %d of exited pid %d", i, pid);
       clear_slot_locked(i);
       n++;

@@ -364,6 +364,35 @@ static void test_region_stopped_lock_owner() {
   unlink(p.c_str());
 }
 
+// Node-side reclaim (monitor, vgpuctl) runs outside the tenant's PID namespace: a slot
+// whose PID belongs to another namespace is never judged by the caller's /proc.
+static void test_region_reclaim_namespaces() {
+  std::string p = tmp_region("pidns");
+  Config c = limits_cfg(1000);
+  SharedRegion r;
+  CHECK_EQ(r.attach(p.c_str(), &c, true), 0);
+  CHECK(self_pidns() != 0);
+  for (int foreign = 0; foreign < 2; foreign++) {
+    pid_t pid = fork();
+    if (pid == 0) {
+      SharedRegion rc;
+      if (rc.attach(p.c_str(), nullptr, false) != 0) _exit(2);
+      int s = rc.register_process(getpid(), 0, 1);
+      if (s < 0 || rc.raw()->procs[s].pidns != self_pidns()) _exit(3);
+      if (foreign) rc.raw()->procs[s].pidns = 12345;  // as if registered in another namespace
+      rc.charge(s, 0, 100, kMemData);
+      _exit(0);  // dies without unregistering
+    }
+    int st = 0;
+    waitpid(pid, &st, 0);
+    CHECK(WIFEXITED(st) && WEXITSTATUS(st) == 0);
+    CHECK_EQ(r.usage(0), 100u);
+    CHECK_EQ(r.reclaim_dead(), foreign ? 0 : 1);  // same namespace: reclaimed; foreign: kept
+    CHECK_EQ(r.usage(0), foreign ? 100u : 0u);
+  }
+  unlink(p.c_str());
+}
+
 static void test_region_version_guard() {
   std::string p = tmp_region("ver");
   Config c = limits_cfg(1);
@@ -928,6 +957,7 @@ int main(int argc, char** argv) {
       {"devmap", test_devmap},
       {"ratelimit", test_ratelimit},
       {"region_stopped_lock_owner", test_region_stopped_lock_owner},
+      {"region_reclaim_namespaces", test_region_reclaim_namespaces},
       {"auto_mode_live_cu", test_auto_mode_and_live_cu},
       {"charge_overflow", test_charge_overflow},
       {"kfd", test_kfd},
