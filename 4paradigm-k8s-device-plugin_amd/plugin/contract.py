@@ -72,6 +72,53 @@ def write_allowlist(vgpu_dir, name, uuids):
     return path
 
 
+SHARED_MAX_AGE_S = 24 * 3600
+
+
+def gc_shared_dirs(root, max_age_s=SHARED_MAX_AGE_S, now=None):
+    """Monitor mode leaves one host directory per container under ``root``
+    (<ns>_<pod>_<ctr>/<uuid>.cache); the reference never removes them. A directory is
+    removed once it and every region in it are older than ``max_age_s`` and no region
+    still lists a process (processes unregister when they exit). Returns the removed tags."""
+    import shutil
+    import time
+    from ..shim.region import Region
+    now = time.time() if now is None else now
+    removed = []
+    try:
+        tags = os.listdir(root)
+    except OSError:
+        return removed
+    for tag in tags:
+        d = os.path.join(root, tag)
+        try:
+            if not os.path.isdir(d) or now - os.path.getmtime(d) < max_age_s:
+                continue
+            live = False
+            for fn in os.listdir(d):
+                fp = os.path.join(d, fn)
+                if now - os.path.getmtime(fp) < max_age_s:
+                    live = True
+                    break
+                if fn.endswith(".cache"):
+                    try:
+                        # No reclaim here: slots hold PIDs of the tenant's namespace, which
+                        # the plugin cannot check. A region whose processes were killed keeps
+                        # its slots, so its directory is kept (conservative).
+                        with Region(fp) as r:
+                            live = r.proc_count > 0
+                    except OSError:
+                        pass  # not a region of this layout: age alone decides
+                if live:
+                    break
+            if not live:
+                shutil.rmtree(d, ignore_errors=True)
+                removed.append(tag)
+        except OSError:
+            continue
+    return removed
+
+
 def device_ids(cfg, devices_by_uuid, uuids):
     if cfg.device_id_strategy == ID_INDEX:
         return [str(devices_by_uuid[u].index) for u in uuids if u in devices_by_uuid]
@@ -140,6 +187,7 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
 
     cache_name = f"{_uuid.uuid4()}.cache"
     if cfg.monitor_mode and pod_tag:
+        gc_shared_dirs(os.path.join(cfg.vgpu_dir, SHARED_HOST_DIR))
         host_dir = os.path.join(cfg.vgpu_dir, SHARED_HOST_DIR, pod_tag)
         os.makedirs(host_dir, exist_ok=True)
         resp.mounts.add(container_path=f"/{pod_tag}", host_path=host_dir, read_only=False)

@@ -16,6 +16,7 @@
 // and runs the OOM killer, which terminates the largest consumer instead of every
 // process.
 #include <dirent.h>
+#include <errno.h>
 #include <pthread.h>
 #include <signal.h>
 #include <unistd.h>
@@ -94,7 +95,8 @@ bool take_lease(Region* r, pid_t me) {
   int32_t cur = r->hdr.watcher_pid.load();
   if (cur == me) return true;
   uint64_t hb = r->hdr.watcher_heartbeat.load();
-  bool stale = cur == 0 || kill(cur, 0) != 0 || (hb && now_ns() - hb > 1'000'000'000ull);
+  // EPERM means the holder exists (another user's process in the container): not stale.
+  bool stale = cur == 0 || (kill(cur, 0) != 0 && errno == ESRCH) || (hb && now_ns() - hb > 1'000'000'000ull);
   if (!stale) return false;
   return r->hdr.watcher_pid.compare_exchange_strong(cur, me);
 }

@@ -248,3 +248,26 @@ def test_reference_flag_and_env_names_accepted():
     assert c.driver_root == "/run/driver" and c.partition_strategy == "single"
     c = parse_config([], environ={"NVIDIA_DRIVER_ROOT": "/x", "MIG_STRATEGY": "mixed"})
     assert c.driver_root == "/x" and c.partition_strategy == "mixed"
+
+
+def test_monitor_mode_shared_dirs_are_collected(tmp_path):
+    """Old monitor-mode container dirs are removed once no process holds their region;
+    a region with a live process, or a recent dir, is kept."""
+    import time
+
+    from amdvgpu.plugin.contract import gc_shared_dirs
+    from amdvgpu.shim.region import Region
+    root = tmp_path / "shared"
+    now = time.time()
+    old = now - 3 * 24 * 3600
+    for tag in ("ns_done_main", "ns_running_main", "ns_fresh_main"):
+        (root / tag).mkdir(parents=True)
+        r = Region(str(root / tag / "a.cache"), create=True)
+        if tag == "ns_running_main":
+            r.register(os.getpid())
+        r.close()
+    for tag in ("ns_done_main", "ns_running_main"):
+        os.utime(root / tag / "a.cache", (old, old))
+        os.utime(root / tag, (old, old))
+    assert gc_shared_dirs(str(root), now=now) == ["ns_done_main"]
+    assert sorted(os.listdir(root)) == ["ns_fresh_main", "ns_running_main"]
