@@ -25,7 +25,7 @@ int current_device() {
   if (s.n_agents <= 1) return 0;
   VGPU_REAL_HIP(hipGetDevice);
   int d = 0;
-  if (!real_hipGetDevice || real_hipGetDevice(&d) != hipSuccess) d = 0;
+  if (!real_hipGetDevice || real_hipGetDevice(&d) != hipSuccess || d < 0 || d >= s.n_agents) d = 0;
   return d;
 }
 bool ok() { return shim_attach_region_only(); }
