@@ -5,6 +5,8 @@
 #include <signal.h>
 #include <strings.h>
 #include <sys/auxv.h>
+
+#include <new>
 #include <unistd.h>
 
 #include <algorithm>
@@ -145,11 +147,20 @@ void on_signal_resume(int) {
   if (s.slot >= 0 && s.region.attached()) s.region.raw()->procs[s.slot].status.store(kProcRunning);
 }
 
+// fork() while another thread is inside an allocation hook: the allocation table must
+// not be copied half-updated, and the child (which has only the forking thread) must not
+// inherit a lock that thread can never release. The table's lock is taken around the
+// fork; in the child both locks are re-created unlocked.
+void atfork_prepare() { shim().alloc_mu.lock(); }
+void atfork_parent() { shim().alloc_mu.unlock(); }
+
 void atfork_child() {
   // A forked child is a different process: it must not inherit the parent's slot
   // or allocation records (reference: child_reinit_flag). ROCr state does not
   // survive fork either, so the child re-initialises if it calls hsa_init again.
   ShimState& s = shim();
+  new (&s.alloc_mu) std::mutex();  // held by this thread since atfork_prepare
+  new (&s.live_mu) std::mutex();   // may be held by a parent thread that does not exist here
   s.slot = -1;
   s.active = false;
   s.allocs.clear();
@@ -365,7 +376,7 @@ void shim_init_after_hsa() {
   }
   static std::once_flag hooks_once;
   std::call_once(hooks_once, [] {
-    pthread_atfork(nullptr, nullptr, atfork_child);
+    pthread_atfork(atfork_prepare, atfork_parent, atfork_child);
     atexit(on_exit);
   });
   for (int i = 0; i < s.n_agents; i++) {

@@ -16,10 +16,17 @@
 //   queues           CU-mask bit count, mask changes and priority of every created stream
 //   cus              the current device's CU count as the runtime sees it
 //   sleep=SECS
+//   forkmalloc=SIZE  fork; the child hipMallocs SIZE and exits normally:
+//                    {"child_malloc": "ok"|"oom"|"crash"}
+//   forkstorm=N      while a second thread allocates and frees 1 MiB in a loop, fork N
+//                    CPU-only children that exit normally: {"forkstorm": ok_children}
 #define __HIP_PLATFORM_AMD__ 1
 #include <hip/hip_runtime_api.h>
 #include <hsa/hsa.h>
+#include <sys/wait.h>
 #include <unistd.h>
+
+#include <atomic>
 
 #include <chrono>
 #include <cstdio>
@@ -131,6 +138,38 @@ int main(int argc, char** argv) {
       printf("]}\n");
     } else if (key == "cus") {
       printf("{\"dev\": %d, \"cus\": %d}\n", dev, fake_hip_device_cus(dev));
+    } else if (key == "forkmalloc") {
+      fflush(stdout);
+      pid_t c = fork();
+      if (c == 0) {
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, (size_t)parse_size(val.c_str()));
+        exit(e == hipSuccess ? 0 : 3);  // normal exit: the shim's exit handler releases the slot
+      }
+      int st = 0;
+      waitpid(c, &st, 0);
+      const char* r = WIFEXITED(st) ? (WEXITSTATUS(st) == 0 ? "ok" : "oom") : "crash";
+      printf("{\"child_malloc\": \"%s\"}\n", r);
+    } else if (key == "forkstorm") {
+      std::atomic<bool> stop{false};
+      std::thread churn([&] {
+        while (!stop.load()) {
+          void* p = nullptr;
+          if (hipMalloc(&p, 1 << 20) == hipSuccess) (void)hipFree(p);
+        }
+      });
+      int ok = 0, n = atoi(val.c_str());
+      fflush(stdout);
+      for (int k = 0; k < n; k++) {
+        pid_t c = fork();
+        if (c == 0) exit(0);  // CPU-only child, like a DataLoader worker (HIP is not fork-safe)
+        int st = 0;
+        waitpid(c, &st, 0);
+        ok += WIFEXITED(st) && WEXITSTATUS(st) == 0;
+      }
+      stop = true;
+      churn.join();
+      printf("{\"forkstorm\": %d}\n", ok);
     } else if (key == "sleep") {
       std::this_thread::sleep_for(std::chrono::duration<double>(atof(val.c_str())));
       printf("{\"slept\": %s}\n", val.c_str());

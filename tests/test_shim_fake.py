@@ -281,3 +281,26 @@ def test_sampler_period_stretches_on_a_crowded_gpu(fake):
     ticks0, refreshes0 = got["0"]
     assert ticks < 600 and ticks0 > 2.5 * ticks, got           # ~220 Hz vs ~1 kHz over 2 s
     assert 0 < refreshes <= ticks and refreshes0 > 0.6 * ticks0, got  # others read while busy
+
+
+def test_fork_children_get_their_own_slot(fake):
+    """A forked child (DataLoader workers, multiprocessing) is a new process: it registers
+    its own slot, is charged against the same container quota, and its charge goes away
+    when it exits; the parent's records are untouched."""
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="2g")
+    out = run(e, "malloc=1g", "forkmalloc=512m", "forkmalloc=1536m", "malloc=1g", "malloc=1m")
+    child = [o["child_malloc"] for o in out if "child_malloc" in o]
+    mallocs = [o["malloc"] for o in out if "malloc" in o]
+    assert child == ["ok", "oom"], out           # 1g + 0.5g fits; 1g + 1.5g does not
+    assert mallocs == ["ok", "ok", "oom"], out   # the child's 0.5g was released at its exit
+
+
+def test_fork_while_another_thread_allocates(fake):
+    """Forking while another thread of the process is inside the allocation hooks (the
+    DataLoader-worker pattern): every child exits cleanly (it inherits no half-updated
+    allocation table) without releasing the parent's slot, and the parent's accounting is
+    intact afterwards."""
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="4g")
+    out = run(e, "malloc=1g", "forkstorm=40", "malloc=3g", "malloc=1m", timeout=120)
+    assert [o["forkstorm"] for o in out if "forkstorm" in o] == [40], out
+    assert [o["malloc"] for o in out if "malloc" in o] == ["ok", "ok", "oom"], out  # 1g + 3g = the quota
