@@ -20,14 +20,7 @@
 using namespace vgpu;
 
 namespace {
-int current_device() {
-  ShimState& s = shim();
-  if (s.n_agents <= 1) return 0;
-  VGPU_REAL_HIP(hipGetDevice);
-  int d = 0;
-  if (!real_hipGetDevice || real_hipGetDevice(&d) != hipSuccess || d < 0 || d >= s.n_agents) d = 0;
-  return d;
-}
+int current_device() { return current_hip_agent(); }
 bool ok() { return shim_attach_region_only(); }
 }  // namespace
 

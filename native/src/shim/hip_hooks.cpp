@@ -21,6 +21,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include "vgpu/region.h"
+
 #include "real.h"
 #include "shim.h"
 #include "vgpu/log.h"
@@ -76,6 +78,52 @@ inline void launch_gate() {
 
 namespace vgpu {
 
+int hip_device_agent(int hipdev) {
+  ShimState& s = shim();
+  if (s.n_agents <= 1 || hipdev < 0) return 0;
+  static std::once_flag once;
+  static int map[kMaxDevices];
+  std::call_once(once, [&s] {
+    for (int i = 0; i < kMaxDevices; i++) map[i] = i;
+    VGPU_REAL_HIP(hipGetDeviceCount);
+    VGPU_REAL_HIP(hipDeviceGetAttribute);
+    int count = 0;
+    if (!real_hipGetDeviceCount || !real_hipDeviceGetAttribute || real_hipGetDeviceCount(&count) != hipSuccess)
+      return;
+    const Region* r = s.region.raw();
+    int found[kMaxDevices];
+    for (int h = 0; h < count && h < kMaxDevices; h++) {
+      int bus = -1, dev = -1, dom = -1;
+      if (real_hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, h) != hipSuccess ||
+          real_hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, h) != hipSuccess ||
+          real_hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainId, h) != hipSuccess)
+        return;
+      int match = -1, n = 0;
+      for (int a = 0; a < s.n_agents; a++) {
+        const DeviceState& d = r->dev[a];
+        if ((d.bdf >> 3) == ((uint32_t)bus << 5 | (uint32_t)dev) && d.domain == (uint32_t)dom) {
+          match = a;
+          n++;
+        }
+      }
+      if (n != 1) return;  // unknown or shared address (compute partitions): keep the identity
+      found[h] = match;
+    }
+    for (int h = 0; h < count && h < kMaxDevices; h++) map[h] = found[h];
+    VLOG_DEBUG("HIP device -> agent map built for %d device(s)", count);
+  });
+  return hipdev < kMaxDevices && map[hipdev] < s.n_agents ? map[hipdev] : 0;
+}
+
+int current_hip_agent() {
+  ShimState& s = shim();
+  if (s.n_agents <= 1) return 0;
+  VGPU_REAL_HIP(hipGetDevice);
+  int d = 0;
+  if (!real_hipGetDevice || real_hipGetDevice(&d) != hipSuccess) return 0;
+  return hip_device_agent(d);
+}
+
 void gate_launch(int dev) {
   ShimState& s = shim();
   Region* r = s.region.raw();
@@ -86,8 +134,7 @@ void gate_launch(int dev) {
     if (s.n_agents > 1) {
       bool any = false;
       for (int i = 0; i < s.n_agents; i++) any |= s.agents[i].temporal_active.load(std::memory_order_relaxed);
-      VGPU_REAL_HIP(hipGetDevice);
-      if (any && (!real_hipGetDevice || real_hipGetDevice(&dev) != hipSuccess)) dev = 0;
+      if (any) dev = current_hip_agent();
     }
   }
   if (dev < 0 || dev >= s.n_agents) dev = 0;
@@ -189,11 +236,7 @@ hipError_t hipMallocManaged(void** dev_ptr, size_t size, unsigned int flags) {
     VLOG_DEBUG("hipMallocManaged(%zu) -> %p (%s)", size, *dev_ptr, pooled ? "charged by the pool hook" : "charging");
     if (pooled) return e;  // already charged by hsa_amd_memory_pool_allocate
   }
-  int dev = 0;
-  if (s.n_agents > 1) {
-    VGPU_REAL_HIP(hipGetDevice);
-    if (!real_hipGetDevice || real_hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= s.n_agents) dev = 0;
-  }
+  const int dev = current_hip_agent();
   if (s.region.charge(s.slot, dev, size, kMemData) != Charge::kOk) {
     (void)real_hipFree(*dev_ptr);
     *dev_ptr = nullptr;
@@ -220,17 +263,18 @@ constexpr uint64_t kPoolSlack = 64ull << 20;
 bool async_admissible(hipMemPool_t pool, size_t size) {
   ShimState& s = shim();
   if (!s.active || size == 0) return true;
-  int dev = 0;
+  int hipdev = 0;
   if (s.n_agents > 1) {
     VGPU_REAL_HIP(hipGetDevice);
-    if (!real_hipGetDevice || real_hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= s.n_agents) dev = 0;
+    if (!real_hipGetDevice || real_hipGetDevice(&hipdev) != hipSuccess) hipdev = 0;
   }
+  const int dev = hip_device_agent(hipdev);  // the region's device (agent) for the HIP device
   const uint64_t lim = s.region.limit(dev);
   if (!lim || config().oversubscribe) return true;
   if (s.region.usage(dev) + size + kPoolSlack <= lim) return true;
   if (!pool) {
     VGPU_REAL_HIP(hipDeviceGetMemPool);
-    if (!real_hipDeviceGetMemPool || real_hipDeviceGetMemPool(&pool, dev) != hipSuccess) pool = nullptr;
+    if (!real_hipDeviceGetMemPool || real_hipDeviceGetMemPool(&pool, hipdev) != hipSuccess) pool = nullptr;
   }
   if (pool) {
     VGPU_REAL_HIP(hipMemPoolGetAttribute);

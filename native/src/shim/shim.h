@@ -146,4 +146,11 @@ pid_t resolve_hostpid(int lock_timeout_ms);
 // [context.c:49-86], [export_table.c:85-113]).
 void resync_context_charge();
 
+// The agent ordinal of HIP device `hipdev` (hipGetDevice / hipSetDevice numbering),
+// matched by PCI address: HIP_VISIBLE_DEVICES inside the container may reorder or hide
+// devices. Identity with one agent, or when the addresses are ambiguous (partitions).
+int hip_device_agent(int hipdev);
+// hip_device_agent of the calling thread's current HIP device (0 when unknown).
+int current_hip_agent();
+
 }  // namespace vgpu

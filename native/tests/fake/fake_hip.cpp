@@ -13,6 +13,7 @@
 #include <hsa/hsa_ext_amd.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -24,6 +25,7 @@ namespace {
 
 struct Device {
   hsa_agent_t agent{0};
+  int rocr = 0;  // index among the fake ROCr's GPU agents (HIP_VISIBLE_DEVICES may reorder)
   hsa_amd_memory_pool_t pool{0};
   std::mutex mu;
   std::condition_variable cv;
@@ -49,7 +51,7 @@ void gpu_loop(int d) {
       std::unique_lock<std::mutex> l(D.mu);
       D.cv.wait(l, [&] { return !D.work.empty(); });
       us = D.work.front();
-      if (!D.running) fake_rocr_set_occupancy(d, 64);
+      if (!D.running) fake_rocr_set_occupancy(D.rocr, 64);
       D.running = true;
     }
     auto t0 = std::chrono::steady_clock::now();
@@ -62,17 +64,35 @@ void gpu_loop(int d) {
     D.kernels++;
     if (D.work.empty()) {
       D.running = false;
-      fake_rocr_set_occupancy(d, 0);
+      fake_rocr_set_occupancy(D.rocr, 0);
       D.cv.notify_all();
     }
   }
 }
 
+hsa_agent_t g_all[16];
+int g_nall = 0;
+
 hsa_status_t agent_cb(hsa_agent_t a, void*) {
   hsa_device_type_t t;
   hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
-  if (t == HSA_DEVICE_TYPE_GPU && g_n < 16) g_dev[g_n++].agent = a;
+  if (t == HSA_DEVICE_TYPE_GPU && g_nall < 16) g_all[g_nall++] = a;
   return HSA_STATUS_SUCCESS;
+}
+
+// HIP devices over the ROCr agents, in HIP_VISIBLE_DEVICES order when it is set (as CLR).
+void map_devices() {
+  const char* v = getenv("HIP_VISIBLE_DEVICES");
+  if (!v || !*v) {
+    for (int i = 0; i < g_nall; i++) g_dev[g_n].rocr = i, g_dev[g_n++].agent = g_all[i];
+    return;
+  }
+  for (const char* p = v; *p && g_n < 16;) {
+    int i = atoi(p);
+    if (i >= 0 && i < g_nall) g_dev[g_n].rocr = i, g_dev[g_n++].agent = g_all[i];
+    while (*p && *p != ',') p++;
+    if (*p == ',') p++;
+  }
 }
 
 hsa_status_t pool_cb(hsa_amd_memory_pool_t p, void* data) {
@@ -85,6 +105,7 @@ void init() {
   if (g_inited) return;
   hsa_init();  // the shim's hsa_init hook runs here, as inside CLR
   hsa_iterate_agents(agent_cb, nullptr);
+  map_devices();
   for (int i = 0; i < g_n; i++) {
     hsa_amd_agent_iterate_memory_pools(g_dev[i].agent, pool_cb, &g_dev[i].pool);
     g_dev[i].th = std::thread(gpu_loop, i);
@@ -133,6 +154,20 @@ hipError_t hipGetDevice(int* d) {
   init();
   *d = t_dev;
   return hipSuccess;
+}
+
+hipError_t hipDeviceGetAttribute(int* value, hipDeviceAttribute_t attr, int d) {
+  init();
+  if (!value || d < 0 || d >= g_n) return hipErrorInvalidDevice;
+  uint32_t bdf = 0, dom = 0;
+  hsa_agent_get_info(g_dev[d].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+  hsa_agent_get_info(g_dev[d].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+  switch (attr) {
+    case hipDeviceAttributePciBusId: *value = (int)(bdf >> 8); return hipSuccess;
+    case hipDeviceAttributePciDeviceId: *value = (int)((bdf >> 3) & 0x1f); return hipSuccess;
+    case hipDeviceAttributePciDomainId: *value = (int)dom; return hipSuccess;
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t hipMalloc(void** ptr, size_t size) {

@@ -304,3 +304,15 @@ def test_fork_while_another_thread_allocates(fake):
     out = run(e, "malloc=1g", "forkstorm=40", "malloc=3g", "malloc=1m", timeout=120)
     assert [o["forkstorm"] for o in out if "forkstorm" in o] == [40], out
     assert [o["malloc"] for o in out if "malloc" in o] == ["ok", "ok", "oom"], out  # 1g + 3g = the quota
+
+
+def test_hip_device_order_differs_from_agent_order(fake):
+    """HIP_VISIBLE_DEVICES reorders HIP's devices inside the container: HIP device 0 is
+    ROCr agent 1. Launch-time limiting must follow the agent (by PCI address), not the
+    HIP index: the limited agent's work runs at ~20 %, the other at full speed."""
+    e = fake(gpus=2, VGPU_DEVICE_CU_LIMIT_1="20", VGPU_CU_MODE="temporal", VGPU_DEVICE_MEMORY_LIMIT_1="4g",
+             HIP_VISIBLE_DEVICES="1,0")
+    out = run(e, "dev=0", "stream", "run=2000,3", "dev=1", "stream", "run=2000,1.5", timeout=120)
+    runs = [o for o in out if "run" in o]
+    assert abs(runs[0]["busy_frac"] - 0.20) <= 0.05, runs   # HIP 0 = agent 1 (limited)
+    assert runs[1]["busy_frac"] > 0.75, runs                # HIP 1 = agent 0 (unlimited)
