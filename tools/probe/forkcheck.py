@@ -10,9 +10,10 @@ if pid == 0:
     os._exit(0 if sum(range(10)) == 45 else 1)
 _, st = os.waitpid(pid, 0)
 b = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+k = torch.ones(1 << 20, device="cuda").sum().item()  # kernel launches through the gates
 torch.cuda.synchronize()
 free, total = torch.cuda.mem_get_info()
-print("forkcheck", os.WEXITSTATUS(st), total == (4 << 30), flush=True)
+print("forkcheck", os.WEXITSTATUS(st), total == (4 << 30), k == float(1 << 20), flush=True)
 """
 r = subprocess.run([sys.executable, "-c", code], env=apply_contract(c), capture_output=True, text=True, timeout=60)
 cleanup_region(c)
