@@ -80,7 +80,7 @@ namespace vgpu {
 
 int hip_device_agent(int hipdev) {
   ShimState& s = shim();
-  if (s.n_agents <= 1 || hipdev < 0) return 0;
+  if (s.n_agents <= 1 || hipdev < 0 || !s.region.attached()) return 0;
   static std::once_flag once;
   static int map[kMaxDevices];
   std::call_once(once, [&s] {
