@@ -276,9 +276,13 @@ class Runner:
     Inference: forward only under ``torch.inference_mode``. Training: forward, loss,
     backward and optimizer step. Synthetic inputs/labels are generated once on the
     device (the reference's ai-benchmark also feeds a fixed random batch).
+
+    Defaults are the product's tenant: stock PyTorch at fp32 (the reference's TF
+    precision). ``dtype=torch.bfloat16, fuse=True`` selects the optional gfx950 contrib
+    kernels (``ops/fused.py``, ``-m kernels`` tests).
     """
 
-    def __init__(self, case, device, dtype=torch.bfloat16, batch=None, channels_last=True, seed=0, fuse=True):
+    def __init__(self, case, device, dtype=torch.float32, batch=None, channels_last=True, seed=0, fuse=False):
         self.case, self.device, self.dtype = case, torch.device(device), dtype
         self.batch = batch or case.batch
         g = torch.Generator(device="cpu").manual_seed(seed)

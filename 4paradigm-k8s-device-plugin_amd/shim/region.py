@@ -23,7 +23,7 @@ class ProcInfo(C.Structure):
         ("pid", C.c_int32), ("hostpid", C.c_int32), ("status", C.c_int32), ("priority", C.c_int32),
         ("launches", C.c_uint64), ("throttle_ns", C.c_uint64), ("suspend_ns", C.c_uint64),
         ("oom_events", C.c_uint64), ("used", C.c_uint64 * 16), ("used_kind", (C.c_uint64 * 4) * 16),
-        ("peak", C.c_uint64 * 16),
+        ("peak", C.c_uint64 * 16), ("host_used", C.c_uint64), ("host_peak", C.c_uint64),
     ]
 
 
@@ -69,6 +69,10 @@ def lib():
             "vgpu_region_get_recent_kernel": (C.c_int, [P]),
             "vgpu_region_set_utilization_switch": (C.c_int, [P, C.c_int]),
             "vgpu_region_reclaim": (C.c_int, [P]),
+            "vgpu_region_host_info": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+            "vgpu_region_set_host_limit": (C.c_int, [P, C.c_uint64]),
+            "vgpu_region_charge_host": (C.c_int, [P, C.c_int, C.c_uint64]),
+            "vgpu_region_uncharge_host": (None, [P, C.c_int, C.c_uint64]),
             "vgpu_region_samples": (C.c_uint64, [P]),
             "vgpu_region_other_refreshes": (C.c_uint64, [P]),
             "vgpu_region_register": (C.c_int, [P, C.c_int32, C.c_int32]),
@@ -164,8 +168,15 @@ class Region:
                 "launches": p.launches, "throttle_ns": p.throttle_ns, "suspend_ns": p.suspend_ns,
                 "oom_events": p.oom_events, "used": list(p.used),
                 "used_kind": [dict(zip(MEM_KINDS, list(k))) for k in p.used_kind], "peak": list(p.peak),
+                "host_used": p.host_used, "host_peak": p.host_peak,
             })
         return out
+
+    def host(self):
+        """Pinned host memory of the container: {"limit": bytes (0 = unlimited), "used": bytes}."""
+        lim, used = C.c_uint64(), C.c_uint64()
+        lib().vgpu_region_host_info(self._h, C.byref(lim), C.byref(used))
+        return {"limit": lim.value, "used": used.value}
 
     @property
     def proc_count(self):
@@ -175,7 +186,7 @@ class Region:
         return {
             "path": self.path, "version": lib().vgpu_region_version(), "suspended": self.suspended,
             "priority": self.priority, "recent_kernel": self.recent_kernel, "samples": self.samples,
-            "other_refreshes": self.other_refreshes,
+            "other_refreshes": self.other_refreshes, "host": self.host(),
             "devices": self.devices(),
             "procs": self.procs(),
         }
@@ -183,6 +194,9 @@ class Region:
     # --- control API ---------------------------------------------------------
     def set_memory_limit(self, dev, nbytes):
         return lib().vgpu_region_set_memory_limit(self._h, dev, int(nbytes))
+
+    def set_host_limit(self, nbytes):
+        return lib().vgpu_region_set_host_limit(self._h, int(nbytes))
 
     def set_cu_limit(self, dev, pct):
         return lib().vgpu_region_set_cu_limit(self._h, dev, int(pct))
@@ -241,3 +255,9 @@ class Region:
 
     def uncharge(self, slot, dev, nbytes, kind=0):
         lib().vgpu_region_uncharge(self._h, slot, dev, int(nbytes), kind)
+
+    def charge_host(self, slot, nbytes):
+        return lib().vgpu_region_charge_host(self._h, slot, int(nbytes))
+
+    def uncharge_host(self, slot, nbytes):
+        lib().vgpu_region_uncharge_host(self._h, slot, int(nbytes))

@@ -38,7 +38,7 @@ def worker(a):
     if "resnet" in a.workload:
         from amdvgpu.models.aibench import Runner, get_case
         torch.backends.cudnn.benchmark = False
-        r = Runner(get_case("resnet50-inf"), "cuda")
+        r = Runner(get_case("resnet50-inf"), "cuda")  # stock fp32 tenant
         for _ in range(a.iters):
             r.step()
         torch.cuda.synchronize()

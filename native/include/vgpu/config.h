@@ -82,6 +82,7 @@ struct Config {
   int limiter_window_ms = 40;            // temporal-mode credit window (ratelimit.h)
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
+  uint64_t host_mem_limit = 0;           // VGPU_HOST_MEMORY_LIMIT: pinned host memory, 0 = unlimited
 
   bool any_memory_limit() const;
   bool any_cu_limit() const;

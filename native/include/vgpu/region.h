@@ -38,7 +38,7 @@
 namespace vgpu {
 
 constexpr uint32_t kRegionMagic = 0x56475055u;  // "VGPU"
-constexpr uint32_t kRegionVersion = 4;
+constexpr uint32_t kRegionVersion = 5;  // v5: pinned host memory accounting
 
 enum ProcStatus : int32_t { kProcFree = 0, kProcRunning = 1, kProcSuspended = 2 };
 
@@ -64,6 +64,8 @@ struct alignas(64) ProcSlot {
   std::atomic<uint64_t> oom_events;
   uint64_t pidns;                         // inode of the PID namespace `pid` lives in (0 = unknown)
   DeviceUsage used[kMaxDevices];
+  std::atomic<uint64_t> host_used;        // pinned host memory (hipHostMalloc / hipHostRegister)
+  std::atomic<uint64_t> host_peak;
 };
 // pidns sits in what was alignment padding in layout v4: the layout is unchanged.
 static_assert(offsetof(ProcSlot, used) == 64, "ProcSlot layout changed");
@@ -115,6 +117,10 @@ struct RegionHeader {
   std::atomic<uint32_t> other_refreshes;    // sampler reads of the other processes' occupancy
   std::atomic<uint64_t> generation;         // bumped on any limit change
   std::atomic<uint64_t> samples;            // sampler ticks (temporal mode)
+  // Pinned host memory of the container (VGPU_HOST_MEMORY_LIMIT; reference: class (b)
+  // cuMemAllocHost_v2 / cuMemHostAlloc / cuMemHostRegister_v2 OOM checks).
+  uint64_t host_limit;                      // bytes, 0 = unlimited (tracked only)
+  std::atomic<uint64_t> host_used;          // aggregate over live slots
 };
 
 // Wait bound for the region lock on paths that must not hang behind a stopped holder.
@@ -179,6 +185,14 @@ class SharedRegion {
   // Bytes of `dev` resident in HBM (charged minus spilled).
   uint64_t resident(int dev) const;
   uint64_t proc_usage(int slot, int dev) const;
+
+  // Pinned host memory (page-locked RAM is a node-wide resource the host-spill pool
+  // shares): the same CAS admission with reclaim-and-retry as device memory.
+  Charge charge_host(int slot, uint64_t bytes);
+  void uncharge_host(int slot, uint64_t bytes);
+  uint64_t host_usage() const;
+  uint64_t host_limit() const;
+  void set_host_limit(uint64_t bytes);
 
   // External control API (reference: set_current_device_memory_limit,
   // set_current_device_sm_limit_scale, suspend_all, resume_all, priority,

@@ -30,6 +30,8 @@ typedef struct {
   uint64_t used[16];
   uint64_t used_kind[16][4];
   uint64_t peak[16];
+  uint64_t host_used;  /* pinned host memory */
+  uint64_t host_peak;
 } vgpu_proc_info;
 
 typedef struct {
@@ -82,6 +84,11 @@ uint64_t vgpu_region_samples(vgpu_region* r);
 /* Of those, the ticks that re-read the other processes' occupancy (crowd-stretched). */
 uint64_t vgpu_region_other_refreshes(vgpu_region* r);
 int vgpu_region_reclaim(vgpu_region* r);
+/* Pinned host memory of the container: limit (0 = unlimited) and aggregate usage. */
+int vgpu_region_host_info(vgpu_region* r, uint64_t* limit, uint64_t* used);
+int vgpu_region_set_host_limit(vgpu_region* r, uint64_t bytes);
+int vgpu_region_charge_host(vgpu_region* r, int slot, uint64_t bytes);
+void vgpu_region_uncharge_host(vgpu_region* r, int slot, uint64_t bytes);
 /* Test hooks: charge/uncharge through the same admission path the shim uses. */
 int vgpu_region_register(vgpu_region* r, int32_t pid, int32_t hostpid);
 void vgpu_region_unregister(vgpu_region* r, int slot);

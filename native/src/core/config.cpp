@@ -238,6 +238,12 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   if (const char* s = getenv_fn("VGPU_SPILL_RESERVE")) {
     if (!parse_size(s, &cfg->spill_reserve_bytes)) VLOG_WARN("invalid VGPU_SPILL_RESERVE=%s ignored", s);
   }
+  if (const char* s = getenv_fn("VGPU_HOST_MEMORY_LIMIT")) {
+    if (!parse_size(s, &cfg->host_mem_limit)) {
+      VLOG_WARN("invalid VGPU_HOST_MEMORY_LIMIT=%s ignored", s);
+      cfg->host_mem_limit = 0;
+    }
+  }
   long prio = 1;
   if (parse_int(getenv_fn("VGPU_TASK_PRIORITY"), -1000, 1000, &prio)) cfg->priority = (int)prio;
 

@@ -185,6 +185,7 @@ void SharedRegion::init_fresh(const Config* cfg) {
   if (cfg && cfg->oversubscribe) flags |= kFlagOversubscribe;
   if (cfg && cfg->active_oom_killer) flags |= kFlagActiveOomKiller;
   r_->hdr.flags = flags;
+  r_->hdr.host_limit = cfg ? cfg->host_mem_limit : 0;
   int n = 0;
   if (cfg) {
     for (int i = 0; i < kMaxDevices; i++) {
@@ -227,6 +228,9 @@ void SharedRegion::check_consistency(const Config* cfg) {
                 r_->dev[i].cu_limit_pct, cfg->dev[i].cu_limit_pct);
     }
   }
+  if (cfg->host_mem_limit && r_->hdr.host_limit != cfg->host_mem_limit)
+    VLOG_WARN("host memory limit inconsistency: region=%lu env=%lu (region wins)",
+              (unsigned long)r_->hdr.host_limit, (unsigned long)cfg->host_mem_limit);
   if (cfg->num_devices > r_->hdr.num_devices) r_->hdr.num_devices = cfg->num_devices;
 }
 
@@ -302,6 +306,8 @@ int SharedRegion::register_process(pid_t pid, pid_t hostpid, int priority) {
   if (slot >= 0) {
     ProcSlot& s = r_->procs[slot];
     memset(static_cast<void*>(&s.used), 0, sizeof(s.used));
+    s.host_used.store(0);
+    s.host_peak.store(0);
     s.launches.store(0);
     s.throttle_ns.store(0);
     s.suspend_ns.store(0);
@@ -330,6 +336,7 @@ void SharedRegion::clear_slot_locked(int slot) {
     if (t) r_->dev[d].used.fetch_sub(t);
     if (sp) r_->dev[d].spilled.fetch_sub(sp);
   }
+  if (uint64_t h = s.host_used.exchange(0)) r_->hdr.host_used.fetch_sub(h);
   s.status.store(kProcFree);
   s.hostpid.store(0);
   s.pid.store(0, std::memory_order_release);
@@ -433,6 +440,57 @@ uint64_t SharedRegion::resident(int dev) const {
   return u > s ? u - s : 0;
 }
 uint64_t SharedRegion::proc_usage(int slot, int dev) const { return r_->procs[slot].used[dev].total.load(); }
+
+Charge SharedRegion::charge_host(int slot, uint64_t bytes) {
+  RegionHeader& h = r_->hdr;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    const uint64_t lim = h.host_limit;
+    uint64_t cur = h.host_used.load(std::memory_order_relaxed);
+    bool admitted = false;
+    while (true) {
+      if (lim && (bytes > lim || cur > lim - bytes)) break;
+      if (h.host_used.compare_exchange_weak(cur, cur + bytes, std::memory_order_acq_rel)) {
+        admitted = true;
+        break;
+      }
+    }
+    if (admitted) {
+      if (slot >= 0) {
+        ProcSlot& p = r_->procs[slot];
+        uint64_t t = p.host_used.fetch_add(bytes) + bytes;
+        uint64_t pk = p.host_peak.load();
+        while (t > pk && !p.host_peak.compare_exchange_weak(pk, t)) {
+        }
+      }
+      return Charge::kOk;
+    }
+    if (attempt == 0 && reclaim_dead() == 0) break;
+  }
+  if (slot >= 0) r_->procs[slot].oom_events.fetch_add(1);
+  return Charge::kOverLimit;
+}
+
+void SharedRegion::uncharge_host(int slot, uint64_t bytes) {
+  auto sat_sub = [](std::atomic<uint64_t>& a, uint64_t v) {
+    uint64_t cur = a.load(std::memory_order_relaxed);
+    while (!a.compare_exchange_weak(cur, cur > v ? cur - v : 0)) {
+    }
+  };
+  if (slot >= 0) {
+    ProcSlot& p = r_->procs[slot];
+    const uint64_t have = p.host_used.load();
+    if (have < bytes) bytes = have;  // slot already reclaimed/cleared
+    sat_sub(p.host_used, bytes);
+  }
+  sat_sub(r_->hdr.host_used, bytes);
+}
+
+uint64_t SharedRegion::host_usage() const { return r_->hdr.host_used.load(std::memory_order_relaxed); }
+uint64_t SharedRegion::host_limit() const { return r_->hdr.host_limit; }
+void SharedRegion::set_host_limit(uint64_t bytes) {
+  r_->hdr.host_limit = bytes;
+  r_->hdr.generation.fetch_add(1);
+}
 
 void SharedRegion::set_limit(int dev, uint64_t bytes) {
   r_->dev[dev].mem_limit = bytes;

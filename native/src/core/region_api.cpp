@@ -90,6 +90,8 @@ int vgpu_region_procs(vgpu_region* r, vgpu_proc_info* out, int max) {
       o.peak[d] = s.used[d].peak.load();
       for (int k = 0; k < kMemKinds; k++) o.used_kind[d][k] = s.used[d].kind[k].load();
     }
+    o.host_used = s.host_used.load();
+    o.host_peak = s.host_peak.load();
   }
   return n;
 }
@@ -134,6 +136,23 @@ int vgpu_region_set_utilization_switch(vgpu_region* r, int v) {
   return 0;
 }
 int vgpu_region_reclaim(vgpu_region* r) { return r->r.reclaim_dead(); }
+
+int vgpu_region_host_info(vgpu_region* r, uint64_t* limit, uint64_t* used) {
+  if (limit) *limit = r->r.host_limit();
+  if (used) *used = r->r.host_usage();
+  return 0;
+}
+
+int vgpu_region_set_host_limit(vgpu_region* r, uint64_t bytes) {
+  r->r.set_host_limit(bytes);
+  return 0;
+}
+
+int vgpu_region_charge_host(vgpu_region* r, int slot, uint64_t bytes) {
+  return r->r.charge_host(slot, bytes) == Charge::kOk ? 0 : -ENOMEM;
+}
+
+void vgpu_region_uncharge_host(vgpu_region* r, int slot, uint64_t bytes) { r->r.uncharge_host(slot, bytes); }
 int vgpu_region_register(vgpu_region* r, int32_t pid, int32_t hostpid) {
   return r->r.register_process(pid, hostpid, 1);
 }

@@ -1,22 +1,28 @@
-// dlsym interposition for SMI libraries that are dlopen'ed (amd-smi / rocm-smi CLIs).
+// dlsym interposition: lookups made on a library handle never consult the
+// preloaded shim, so hooked names are routed back into it here.
 //
 // Reference: libvgpu.so overrides dlsym [src/libvgpu.c:109-124] so that runtimes that
-// dlopen the driver still reach the hooks. On MI355X the HIP runtime links ROCr
-// directly (no dlsym needed for the HSA/HIP hooks), but the in-container SMI tools
-// are Python (ctypes over libamd_smi.so / librocm_smi64.so): ctypes resolves every
-// entry point with dlsym(handle, name), which never consults the preloaded shim. So
-// dlsym is interposed, but narrowly:
-//   * only names starting with "amdsmi_" / "rsmi_" that resolve into an SMI library
-//     and have a virtualising hook are redirected (to smi_hooks.cpp), and only for
-//     callers outside the SMI libraries (libamd_smi embeds and calls rocm_smi itself,
-//     with node indices);
+// dlopen the driver still reach the hooks. On MI355X two kinds of callers need it:
+//   * HIP runtimes loaded by handle: Triton (every torch.compile tenant) dlopens
+//     libamdhip64 and resolves hipGetProcAddress with dlsym(handle, ...), then its launch
+//     entry points through it. Names starting with "hip" that the shim gates
+//     (hip_gates.def) and that resolve to the very entry point the gate forwards to are
+//     redirected to the shim's definition (gates.cpp: hip_hook_for_name), for callers
+//     outside libamdhip64;
+//   * the in-container SMI tools: Python (ctypes over libamd_smi.so / librocm_smi64.so)
+//     resolves every entry point with dlsym(handle, name). Only names starting with
+//     "amdsmi_" / "rsmi_" that resolve into an SMI library and have a virtualising hook
+//     are redirected (to smi_hooks.cpp), and only for callers outside the SMI libraries
+//     (libamd_smi embeds and calls rocm_smi itself, with node indices);
 //   * the rocm_smi hooks are reached only this way (not exported from the shim), so
 //     libamd_smi's internal calls to its own rsmi_* never hit the index remapping;
 //   * every other lookup is a guaranteed tail call ([[clang::musttail]]) into glibc,
 //     so RTLD_NEXT keeps resolving relative to the *original* caller - other
 //     interposers preloaded alongside the shim are unaffected.
 // Both glibc symbol versions are provided (dlsym@GLIBC_2.2.5 for old binaries,
-// dlsym@@GLIBC_2.34 for current ones). This file is compiled with clang (musttail).
+// dlsym@@GLIBC_2.34 for current ones). dlvsym is not interposed (the shim itself needs
+// glibc's to find the real dlsym, and no HIP consumer resolves entry points with it).
+// This file is compiled with clang (musttail).
 #include <dlfcn.h>
 
 #include <atomic>
@@ -25,6 +31,8 @@
 
 #include <amd_smi/amdsmi.h>
 #include <rocm_smi/rocm_smi.h>
+
+#include "real.h"
 
 extern "C" {
 amdsmi_status_t amdsmi_get_gpu_memory_total(amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*);
@@ -58,6 +66,7 @@ __attribute__((constructor)) void dlsym_hook_ctor() {
 std::atomic<DlsymFn> g_real_234{nullptr};
 std::atomic<DlsymFn> g_real_225{nullptr};
 
+// glibc's dlsym, found with dlvsym (not interposed: the shim routes dlsym lookups only).
 DlsymFn load_real(std::atomic<DlsymFn>& slot, const char* ver) {
   DlsymFn f = slot.load(std::memory_order_acquire);
   if (__builtin_expect(f != nullptr, 1)) return f;
@@ -86,6 +95,28 @@ const Hook kHooks[] = {
     {"rsmi_compute_process_gpus_get", reinterpret_cast<void*>(&rsmi_compute_process_gpus_get)},
 };
 
+bool in_hip_library(const void* addr) {
+  Dl_info info;
+  if (!addr || !dladdr(addr, &info) || !info.dli_fname) return false;
+  return strstr(info.dli_fname, "libamdhip64") && !strstr(info.dli_fname, "vgpu");
+}
+
+bool in_shim(const void* addr) {
+  Dl_info a, self;
+  return addr && dladdr(addr, &a) && dladdr(reinterpret_cast<const void*>(&in_shim), &self) &&
+         a.dli_fbase == self.dli_fbase;
+}
+
+// hip* lookups on a library handle: the shim's gate when the lookup found the runtime's
+// entry point that gate forwards to.
+__attribute__((noinline)) void* maybe_hook_hip(void* handle, const char* name, const char* version, void* found,
+                                               const void* caller) {
+  if (!found || handle == RTLD_NEXT || handle == RTLD_DEFAULT) return nullptr;
+  if (strncmp(name, "hip", 3) != 0 || !in_hip_library(found)) return nullptr;
+  if (in_hip_library(caller) || in_shim(caller)) return nullptr;
+  return vgpu::hip_hook_for_name(name, version, found);
+}
+
 bool in_smi_library(const void* addr) {
   Dl_info info;
   if (!addr || !dladdr(addr, &info) || !info.dli_fname) return false;
@@ -108,29 +139,40 @@ __attribute__((noinline)) void* maybe_hook(void* handle, const char* name, Dlsym
 }  // namespace
 
 namespace vgpu {
-// The shim's own lookups must bypass the interposer (they want the real SMI symbols).
+// The shim's own lookups must bypass the interposer (they want the real symbols).
 void* real_dlsym(void* handle, const char* name) { return load_real(g_real_234, "GLIBC_2.34")(handle, name); }
+void* real_dlvsym(void* handle, const char* name, const char* version) { return dlvsym(handle, name, version); }
 }  // namespace vgpu
 
 extern "C" {
 
-__attribute__((visibility("default"))) void* shim_dlsym_v234(void* handle, const char* name) {
-  DlsymFn real = load_real(g_real_234, "GLIBC_2.34");
-  if (__builtin_expect(g_dlsym_hook_on && name && (name[0] == 'a' || name[0] == 'r'), 0)) {
-    if (void* h = maybe_hook(handle, name, real, __builtin_return_address(0))) return h;
-  }
+// A hip* lookup is resolved first (a plain call: the handle names the library, so the
+// result does not depend on the caller) and replaced by the gate when it is one; every
+// other lookup is a guaranteed tail call so RTLD_NEXT stays relative to the caller.
+#define VGPU_DLSYM_BODY(slot, ver)                                                              \
+  DlsymFn real = load_real(slot, ver);                                                          \
+  if (__builtin_expect(g_dlsym_hook_on && name != nullptr, 1)) {                                \
+    if (name[0] == 'h' && handle != RTLD_NEXT && handle != RTLD_DEFAULT) {                      \
+      void* p = real(handle, name);                                                             \
+      void* h = maybe_hook_hip(handle, name, nullptr, p, __builtin_return_address(0));          \
+      return h ? h : p;                                                                         \
+    }                                                                                           \
+    if (__builtin_expect(name[0] == 'a' || name[0] == 'r', 0)) {                                \
+      if (void* h = maybe_hook(handle, name, real, __builtin_return_address(0))) return h;      \
+    }                                                                                           \
+  }                                                                                             \
   [[clang::musttail]] return real(handle, name);
+
+__attribute__((visibility("default"))) void* shim_dlsym_v234(void* handle, const char* name) {
+  VGPU_DLSYM_BODY(g_real_234, "GLIBC_2.34")
 }
 
 __attribute__((visibility("default"))) void* shim_dlsym_v225(void* handle, const char* name) {
-  DlsymFn real = load_real(g_real_225, "GLIBC_2.2.5");
-  if (__builtin_expect(g_dlsym_hook_on && name && (name[0] == 'a' || name[0] == 'r'), 0)) {
-    if (void* h = maybe_hook(handle, name, real, __builtin_return_address(0))) return h;
-  }
-  [[clang::musttail]] return real(handle, name);
+  VGPU_DLSYM_BODY(g_real_225, "GLIBC_2.2.5")
 }
 
 }  // extern "C"
 
 __asm__(".symver shim_dlsym_v234, dlsym@@GLIBC_2.34");
 __asm__(".symver shim_dlsym_v225, dlsym@GLIBC_2.2.5");
+

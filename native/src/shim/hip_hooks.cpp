@@ -1,11 +1,10 @@
-// HIP-level interposition: kernel-launch and copy gates.
+// HIP-level interposition with semantics: the launch gate's slow path, the HIP device ->
+// agent map, and the device allocations that do not (only) pass the HSA pool hooks.
 //
-// Reference: cuLaunchKernel / cuLaunchCooperativeKernel [src/cuda/memory.c:598-611]
-// run the suspend gate (wait_status_self) and the token-bucket rate_limiter before
-// the real launch, and 41 copy/alloc hooks run the suspend gate. cuGraphLaunch is a
-// plain passthrough there [graph.c:224-225], so graph replays escape the throttle;
-// here a graph launch passes the same gates as a kernel launch, and the GPU-time limiter
-// charges whatever its kernels run (ratelimit.h).
+// The launch / copy / set entry points themselves are generated trampolines (gates.cpp,
+// hip_gates.def). Reference: cuLaunchKernel / cuLaunchCooperativeKernel
+// [src/cuda/memory.c:598-611] run the suspend gate (wait_status_self) and the
+// token-bucket rate_limiter before the real launch.
 //
 // Hot-path budget: a launch pays one predictable branch on process-local state, a
 // relaxed increment of its own slot's launch counter, and relaxed loads of region words
@@ -30,51 +29,9 @@
 
 using namespace vgpu;
 
-// hip_ext.h needs the HIP compiler; declare the one entry point we need from it.
-extern "C" hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t globalWorkSizeX, uint32_t globalWorkSizeY,
-                                               uint32_t globalWorkSizeZ, uint32_t localWorkSizeX,
-                                               uint32_t localWorkSizeY, uint32_t localWorkSizeZ,
-                                               size_t sharedMemBytes, hipStream_t hStream, void** kernelParams,
-                                               void** extra, hipEvent_t startEvent, hipEvent_t stopEvent,
-                                               uint32_t flags);
-
-using LaunchKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t);
-using CoopKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, unsigned int, hipStream_t);
 using MallocManagedFn = hipError_t (*)(void**, size_t, unsigned int);
 using MallocAsyncFn = hipError_t (*)(void**, size_t, hipStream_t);
 using MallocFromPoolAsyncFn = hipError_t (*)(void**, size_t, hipMemPool_t, hipStream_t);
-using ExtLaunchKernelFn = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t, hipEvent_t, hipEvent_t,
-                                         int);
-
-namespace {
-
-// VGPU_HOOK_LAUNCH=0: launch hooks become pure pass-throughs (diagnostics; disables the
-// suspend gate, the launch block and the temporal limiter at launch). Read once at load.
-bool g_launch_hooks_on = true;
-__attribute__((constructor)) void launch_hook_ctor() {
-  const char* s = getenv("VGPU_HOOK_LAUNCH");
-  if (s && *s == '0') g_launch_hooks_on = false;
-}
-
-inline void launch_gate() {
-  VGPU_STAT(kStatLaunch);
-  if (__builtin_expect(!g_launch_hooks_on, 0)) return;
-  ShimState& s = shim();
-  if (__builtin_expect(!s.active, 1)) return;
-  // Fast path: count (process-local; the maintenance thread publishes it), then three
-  // relaxed loads of region words that only a controller writes.
-  s.launches.fetch_add(1, std::memory_order_relaxed);
-  const Region* r = s.region.raw();
-  if (__builtin_expect(r->hdr.generation.load(std::memory_order_relaxed) ==
-                               s.seen_generation.load(std::memory_order_relaxed) &&
-                           !gate_needed() && r->hdr.recent_kernel.load(std::memory_order_relaxed) >= 0 &&
-                           !s.any_temporal.load(std::memory_order_relaxed),
-                       1))
-    return;
-  gate_launch(-1);
-}
-
-}  // namespace
 
 namespace vgpu {
 
@@ -150,70 +107,6 @@ void gate_launch(int dev) {
 }  // namespace vgpu
 
 extern "C" {
-
-hipError_t hipLaunchKernel(const void* function_address, dim3 numBlocks, dim3 dimBlocks, void** args,
-                           size_t sharedMemBytes, hipStream_t stream) {
-  VGPU_REAL_HIP_T(hipLaunchKernel, LaunchKernelFn);
-  launch_gate();
-  return real_hipLaunchKernel(function_address, numBlocks, dimBlocks, args, sharedMemBytes, stream);
-}
-
-hipError_t hipExtLaunchKernel(const void* function_address, dim3 numBlocks, dim3 dimBlocks, void** args,
-                              size_t sharedMemBytes, hipStream_t stream, hipEvent_t startEvent, hipEvent_t stopEvent,
-                              int flags) {
-  VGPU_REAL_HIP_T(hipExtLaunchKernel, ExtLaunchKernelFn);
-  launch_gate();
-  return real_hipExtLaunchKernel(function_address, numBlocks, dimBlocks, args, sharedMemBytes, stream, startEvent,
-                                 stopEvent, flags);
-}
-
-hipError_t hipModuleLaunchKernel(hipFunction_t f, unsigned int gridDimX, unsigned int gridDimY, unsigned int gridDimZ,
-                                 unsigned int blockDimX, unsigned int blockDimY, unsigned int blockDimZ,
-                                 unsigned int sharedMemBytes, hipStream_t stream, void** kernelParams, void** extra) {
-  VGPU_REAL_HIP(hipModuleLaunchKernel);
-  launch_gate();
-  return real_hipModuleLaunchKernel(f, gridDimX, gridDimY, gridDimZ, blockDimX, blockDimY, blockDimZ, sharedMemBytes,
-                                    stream, kernelParams, extra);
-}
-
-hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t globalWorkSizeX, uint32_t globalWorkSizeY,
-                                    uint32_t globalWorkSizeZ, uint32_t localWorkSizeX, uint32_t localWorkSizeY,
-                                    uint32_t localWorkSizeZ, size_t sharedMemBytes, hipStream_t hStream,
-                                    void** kernelParams, void** extra, hipEvent_t startEvent, hipEvent_t stopEvent,
-                                    uint32_t flags) {
-  VGPU_REAL_HIP(hipExtModuleLaunchKernel);
-  launch_gate();
-  return real_hipExtModuleLaunchKernel(f, globalWorkSizeX, globalWorkSizeY, globalWorkSizeZ, localWorkSizeX,
-                                       localWorkSizeY, localWorkSizeZ, sharedMemBytes, hStream, kernelParams, extra,
-                                       startEvent, stopEvent, flags);
-}
-
-hipError_t hipLaunchCooperativeKernel(const void* f, dim3 gridDim, dim3 blockDimX, void** kernelParams,
-                                      unsigned int sharedMemBytes, hipStream_t stream) {
-  VGPU_REAL_HIP_T(hipLaunchCooperativeKernel, CoopKernelFn);
-  launch_gate();
-  return real_hipLaunchCooperativeKernel(f, gridDim, blockDimX, kernelParams, sharedMemBytes, stream);
-}
-
-hipError_t hipModuleLaunchCooperativeKernel(hipFunction_t f, unsigned int gridDimX, unsigned int gridDimY,
-                                            unsigned int gridDimZ, unsigned int blockDimX, unsigned int blockDimY,
-                                            unsigned int blockDimZ, unsigned int sharedMemBytes, hipStream_t stream,
-                                            void** kernelParams) {
-  VGPU_REAL_HIP(hipModuleLaunchCooperativeKernel);
-  launch_gate();
-  return real_hipModuleLaunchCooperativeKernel(f, gridDimX, gridDimY, gridDimZ, blockDimX, blockDimY, blockDimZ,
-                                               sharedMemBytes, stream, kernelParams);
-}
-
-hipError_t hipGraphLaunch(hipGraphExec_t graphExec, hipStream_t stream) {
-  VGPU_REAL_HIP(hipGraphLaunch);
-  VGPU_STAT(kStatGraphLaunch);
-  // A graph replay is one launch for the gates: the temporal limiter charges GPU time,
-  // not launches, so a graph costs what its kernels run (the reference's cuGraphLaunch
-  // bypassed the throttle entirely, [graph.c:224-225]).
-  launch_gate();
-  return real_hipGraphLaunch(graphExec, stream);
-}
 
 // Managed memory (reference: cuMemAllocManaged is an accounted allocation, class (a) in
 // SURVEY.md §2.3). Depending on XNACK/HMM mode CLR may back it with system memory that
@@ -326,57 +219,6 @@ hipError_t hipFree(void* ptr) {
     if (rec.dev >= 0 && s.slot >= 0 && !s.exiting.load()) s.region.uncharge(s.slot, rec.dev, rec.size, kMemData);
   }
   return real_hipFree(ptr);
-}
-
-// Copy/set gates (suspend only), mirroring the reference's wait_status_self set.
-hipError_t hipMemcpy(void* dst, const void* src, size_t sizeBytes, hipMemcpyKind kind) {
-  VGPU_REAL_HIP(hipMemcpy);
-  VGPU_STAT(kStatCopy);
-  gate_suspend();
-  return real_hipMemcpy(dst, src, sizeBytes, kind);
-}
-
-hipError_t hipMemcpyAsync(void* dst, const void* src, size_t sizeBytes, hipMemcpyKind kind, hipStream_t stream) {
-  VGPU_REAL_HIP(hipMemcpyAsync);
-  VGPU_STAT(kStatCopy);
-  gate_suspend();
-  return real_hipMemcpyAsync(dst, src, sizeBytes, kind, stream);
-}
-
-hipError_t hipMemcpyWithStream(void* dst, const void* src, size_t sizeBytes, hipMemcpyKind kind, hipStream_t stream) {
-  VGPU_REAL_HIP(hipMemcpyWithStream);
-  VGPU_STAT(kStatCopy);
-  gate_suspend();
-  return real_hipMemcpyWithStream(dst, src, sizeBytes, kind, stream);
-}
-
-hipError_t hipMemcpyPeerAsync(void* dst, int dstDeviceId, const void* src, int srcDevice, size_t sizeBytes,
-                              hipStream_t stream) {
-  VGPU_REAL_HIP(hipMemcpyPeerAsync);
-  VGPU_STAT(kStatCopy);
-  gate_suspend();
-  return real_hipMemcpyPeerAsync(dst, dstDeviceId, src, srcDevice, sizeBytes, stream);
-}
-
-hipError_t hipMemset(void* dst, int value, size_t sizeBytes) {
-  VGPU_REAL_HIP(hipMemset);
-  VGPU_STAT(kStatSet);
-  gate_suspend();
-  return real_hipMemset(dst, value, sizeBytes);
-}
-
-hipError_t hipMemsetAsync(void* dst, int value, size_t sizeBytes, hipStream_t stream) {
-  VGPU_REAL_HIP(hipMemsetAsync);
-  VGPU_STAT(kStatSet);
-  gate_suspend();
-  return real_hipMemsetAsync(dst, value, sizeBytes, stream);
-}
-
-hipError_t hipMemsetD32Async(hipDeviceptr_t dst, int value, size_t count, hipStream_t stream) {
-  VGPU_REAL_HIP(hipMemsetD32Async);
-  VGPU_STAT(kStatSet);
-  gate_suspend();
-  return real_hipMemsetD32Async(dst, value, count, stream);
 }
 
 }  // extern "C"

@@ -53,7 +53,7 @@ int find_cb(struct dl_phdr_info* info, size_t, void* data) {
 }
 }  // namespace
 
-void* resolve_real(const char* lib_substr, const char* name, const char* ver) {
+void* resolve_real(const char* lib_substr, const char* name, const char* ver, bool quiet) {
   Dl_info self;
   void* self_base = nullptr;
   if (dladdr(reinterpret_cast<void*>(&resolve_real), &self)) self_base = self.dli_fbase;
@@ -63,20 +63,21 @@ void* resolve_real(const char* lib_substr, const char* name, const char* ver) {
   if (f.path) {
     void* h = dlopen(f.path, RTLD_NOLOAD | RTLD_LAZY);
     if (h) {
-      p = ver ? dlvsym(h, name, ver) : nullptr;
+      p = ver ? real_dlvsym(h, name, ver) : nullptr;
       if (!p) p = real_dlsym(h, name);
       // dlopen(RTLD_NOLOAD) took a reference; the object stays loaded regardless.
       dlclose(h);
     }
   }
-  if (!p) p = ver ? dlvsym(RTLD_NEXT, name, ver) : nullptr;
+  if (!p) p = ver ? real_dlvsym(RTLD_NEXT, name, ver) : nullptr;
   if (!p) p = real_dlsym(RTLD_NEXT, name);
   if (!p) {
     FindSym fs{name, self_base, nullptr};
     dl_iterate_phdr(find_sym_cb, &fs);
     p = fs.found;
   }
-  if (!p) VLOG_ERROR("cannot resolve real %s in %s", name, lib_substr);
+  if (!p && !quiet) VLOG_ERROR("cannot resolve real %s in %s", name, lib_substr);
+  else if (!p) VLOG_DEBUG("%s is not defined by the loaded %s", name, lib_substr);
   return p;
 }
 

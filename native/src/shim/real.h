@@ -10,12 +10,20 @@
 
 namespace vgpu {
 
-// glibc's dlsym, bypassing the shim's own dlsym interposer (dlsym_hook.cpp).
+// glibc's dlsym (bypassing the shim's interposer, dlsym_hook.cpp) and dlvsym.
 void* real_dlsym(void* handle, const char* name);
+void* real_dlvsym(void* handle, const char* name, const char* version);
+
+// Routing of runtime lookups (gates.cpp): the shim's hook for the HIP entry point at
+// `real`, or for `name` (with `version`, may be null) when the lookup found `real` - the
+// entry point that hook forwards to. Null when the entry point is not hooked.
+void* hip_hook_for_real(const void* real);
+void* hip_hook_for_name(const char* name, const char* version, const void* real);
 
 // Looks `name` (version `ver`, may be null) up in the first loaded object whose path
-// contains `lib_substr`; falls back to RTLD_NEXT. Returns null when absent.
-void* resolve_real(const char* lib_substr, const char* name, const char* ver);
+// contains `lib_substr`; falls back to RTLD_NEXT. Returns null when absent (logged as an
+// error unless `quiet`: a runtime may lack an entry point the shim knows).
+void* resolve_real(const char* lib_substr, const char* name, const char* ver, bool quiet = false);
 
 }  // namespace vgpu
 

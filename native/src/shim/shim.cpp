@@ -167,6 +167,7 @@ void atfork_child() {
   s.vmem.clear();
   s.managed.clear();
   s.ipc.clear();
+  s.host.clear();
   for (auto& b : s.ipc_bytes) b.store(0);
   s.queues.clear();
   s.hostpid = 0;

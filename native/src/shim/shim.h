@@ -63,6 +63,7 @@ struct ShimState {
   std::unordered_map<uint64_t, AllocRec> vmem;      // vmem handle → record
   std::unordered_map<uintptr_t, AllocRec> managed;  // hipMallocManaged pointers charged at HIP level
   std::unordered_map<uintptr_t, AllocRec> ipc;      // IPC-attached pointers (owned by another process)
+  std::unordered_map<uintptr_t, uint64_t> host;     // pinned host memory (host_hooks.cpp) → bytes
   std::unordered_map<uintptr_t, int> queues;        // hsa_queue_t* → ordinal
   std::atomic<bool> exiting{false};
   std::atomic<bool> watcher_started{false};

@@ -20,7 +20,19 @@
 //                    {"child_malloc": "ok"|"oom"|"crash"}
 //   forkstorm=N      while a second thread allocates and frees 1 MiB in a loop, fork N
 //                    CPU-only children that exit normally: {"forkstorm": ok_children}
+//   gates=MODE       for every name in $FAKE_GATE_NAMES (comma-separated): resolve it as
+//                    an application would - MODE direct (the global scope, i.e. a linked
+//                    call), dlsym (dlsym on a libamdhip64 handle), procaddr (dlsym of
+//                    hipGetProcAddress on that handle, then hipGetProcAddress: Triton's
+//                    way) - and call it while the container is suspended (resumed after
+//                    40 ms by a second thread): {"unrouted": names whose pointer is not the
+//                    shim's, "ungated": names that did not block, "unreached": names whose
+//                    call never reached the runtime}
+//   hostmalloc=SIZE  hipHostMalloc -> {"hostmalloc": "ok"|"oom"}; hostfree frees the last one
+//   hostregister=SIZE  hipHostRegister of a fresh heap buffer -> {"hostregister": "ok"|"oom"};
+//                    hostunregister unregisters (and frees) the last one
 #define __HIP_PLATFORM_AMD__ 1
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <hsa/hsa.h>
 #include <sys/wait.h>
@@ -43,6 +55,7 @@ int fake_rocr_queue_state(const hsa_queue_t* queue, uint32_t* mask_words8, int* 
 int fake_rocr_internal_alloc(int dev, int64_t bytes);
 int fake_rocr_host_pid();
 int fake_hip_device_cus(int dev);
+const char* fake_hip_last_call();
 }
 
 namespace {
@@ -63,6 +76,67 @@ long long parse_size(const char* s) {
   return v;
 }
 
+std::vector<std::string> split_names(const char* s) {
+  std::vector<std::string> out;
+  std::string cur;
+  for (const char* p = s ? s : ""; ; p++) {
+    if (*p == ',' || *p == 0) {
+      if (!cur.empty()) out.push_back(cur);
+      cur.clear();
+      if (!*p) break;
+    } else {
+      cur += *p;
+    }
+  }
+  return out;
+}
+
+void json_list(const char* key, const std::vector<std::string>& v, bool last) {
+  printf("\"%s\": [", key);
+  for (size_t i = 0; i < v.size(); i++) printf("%s\"%s\"", i ? ", " : "", v[i].c_str());
+  printf("]%s", last ? "" : ", ");
+}
+
+void gates(const std::string& mode) {
+  using Ctl = int (*)();
+  using ProcAddr = hipError_t (*)(const char*, void**, int, uint64_t, hipDriverProcAddressQueryResult*);
+  auto suspend = reinterpret_cast<Ctl>(dlsym(RTLD_DEFAULT, "vgpu_suspend_all"));
+  auto resume = reinterpret_cast<Ctl>(dlsym(RTLD_DEFAULT, "vgpu_resume_all"));
+  void* h = dlopen("libamdhip64.so", RTLD_NOLOAD | RTLD_LAZY);
+  ProcAddr gpa = h ? reinterpret_cast<ProcAddr>(dlsym(h, "hipGetProcAddress")) : nullptr;
+  std::vector<std::string> names = split_names(getenv("FAKE_GATE_NAMES")), unrouted, ungated, unreached;
+  for (const std::string& n : names) {
+    void* shim_fn = dlsym(RTLD_DEFAULT, n.c_str());
+    void* p = nullptr;
+    if (mode == "direct") p = shim_fn;
+    else if (mode == "dlsym") p = h ? dlsym(h, n.c_str()) : nullptr;
+    else if (gpa) (void)gpa(n.c_str(), &p, 0, 0, nullptr);
+    if (!p || p != shim_fn) {
+      unrouted.push_back(n);
+      if (!p) continue;
+    }
+    if (!suspend || !resume || suspend() != 0) {
+      ungated.push_back(n);
+      continue;
+    }
+    std::thread t([&] {
+      std::this_thread::sleep_for(std::chrono::milliseconds(40));
+      resume();
+    });
+    double t0 = now_s();
+    (void)reinterpret_cast<int (*)()>(p)();
+    double dt = now_s() - t0;
+    t.join();
+    if (dt < 0.030) ungated.push_back(n);
+    if (n != fake_hip_last_call()) unreached.push_back(n);
+  }
+  printf("{\"gates\": \"%s\", \"n\": %zu, ", mode.c_str(), names.size());
+  json_list("unrouted", unrouted, false);
+  json_list("ungated", ungated, false);
+  json_list("unreached", unreached, true);
+  printf("}\n");
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -71,6 +145,7 @@ int main(int argc, char** argv) {
   hipStream_t stream = nullptr;
   std::vector<void*> ptrs;
   std::vector<hipStream_t> streams;
+  std::vector<void*> host_ptrs, registered;
   static uint32_t kernel_us[64];
   int kslot = 0;
   printf("{\"pid\": %d, \"fake_hostpid\": %d}\n", (int)getpid(), fake_rocr_host_pid());
@@ -170,6 +245,33 @@ int main(int argc, char** argv) {
       stop = true;
       churn.join();
       printf("{\"forkstorm\": %d}\n", ok);
+    } else if (key == "gates") {
+      gates(val);
+    } else if (key == "hostmalloc") {
+      void* p = nullptr;
+      hipError_t e = hipHostMalloc(&p, (size_t)parse_size(val.c_str()), 0);
+      if (e == hipSuccess) host_ptrs.push_back(p);
+      printf("{\"hostmalloc\": \"%s\"}\n", e == hipSuccess ? "ok" : "oom");
+    } else if (key == "hostfree") {
+      if (!host_ptrs.empty()) {
+        (void)hipHostFree(host_ptrs.back());
+        host_ptrs.pop_back();
+      }
+      printf("{\"hostfree\": true}\n");
+    } else if (key == "hostregister") {
+      size_t n = (size_t)parse_size(val.c_str());
+      void* p = malloc(n ? n : 1);
+      hipError_t e = hipHostRegister(p, n, 0);
+      if (e == hipSuccess) registered.push_back(p);
+      else free(p);
+      printf("{\"hostregister\": \"%s\"}\n", e == hipSuccess ? "ok" : "oom");
+    } else if (key == "hostunregister") {
+      if (!registered.empty()) {
+        (void)hipHostUnregister(registered.back());
+        free(registered.back());
+        registered.pop_back();
+      }
+      printf("{\"hostunregister\": true}\n");
     } else if (key == "sleep") {
       std::this_thread::sleep_for(std::chrono::duration<double>(atof(val.c_str())));
       printf("{\"slept\": %s}\n", val.c_str());

@@ -55,7 +55,7 @@ def test_conv1x1_reference_matches_conv2d_cpu():
                                rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("nhw,k,n", [((2, 7, 9), 64, 64), ((1, 11, 11), 2048, 512), ((50, 22, 22), 256, 1024),
                                       ((3, 5, 5), 128, 192), ((4, 16, 16), 512, 128), ((1, 1, 3), 64, 256)])
 @pytest.mark.parametrize("epi", ["plain", "bn_act", "residual", "residual_sum"])
@@ -99,7 +99,7 @@ def test_conv_reference_epilogues_cpu():
     torch.testing.assert_close(y, torch.nn.functional.relu6(conv * v(sc) + v(sh) + r))
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("geom", [(2, 64, 9, 11, 64, 3, 1, 1), (3, 128, 22, 22, 128, 3, 2, 1), (1, 64, 5, 5, 192, 3, 1, 1),
                                   (2, 256, 44, 44, 512, 1, 2, 0), (50, 64, 22, 22, 64, 3, 1, 1),
                                   (1, 64, 3, 2, 64, 3, 1, 1), (2, 128, 7, 7, 128, 3, 1, 0)])
@@ -129,7 +129,7 @@ def test_conv_nhwc_kernel_numerics(geom, epi):
         torch.testing.assert_close(out[1].float(), s_ref, rtol=2e-2, atol=3e-2)
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("geom", [(2, 64, 9, 11, 64, 1, 256), (2, 128, 17, 21, 256, 2, 512), (50, 256, 22, 22, 512, 2, 1024),
                                   (1, 64, 3, 3, 128, 3, 64)])
 @pytest.mark.parametrize("epi", ["plain", "bn_act", "bn_act_sum"])
@@ -187,7 +187,7 @@ def F_conv_valid(x, w):
     return torch.nn.functional.conv2d(x, w).reshape(-1)
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("shape", [(2, 346, 346), (1, 64, 48), (3, 31, 29), (1, 7, 7)])
 def test_stem_kernel_numerics(shape):
     """Fused conv7x7/2 + maxpool3x3/2 + BN + ReLU vs fp32 PyTorch (odd sizes exercise the
@@ -204,7 +204,7 @@ def test_stem_kernel_numerics(shape):
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("nhw,k,n", [((2, 7, 9), 64, 64), ((50, 22, 22), 1024, 256), ((3, 5, 5), 256, 192)])
 def test_conv_prologue_and_sum_only_numerics(nhw, k, n):
     """1x1 conv reading relu(x * s + t) (the consumer-side BN + ReLU prologue) with a
@@ -239,7 +239,7 @@ def test_grid_cap_follows_the_vgpu_cu_share(monkeypatch):
     assert grid_cap(256, 0) == 0                       # no CU mask in temporal mode
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("cap", [8, 24, 130])
 def test_conv_persistent_grid_numerics(cap):
     """Capped (persistent) grids: every block loops over several tiles."""
@@ -258,7 +258,7 @@ def test_conv_persistent_grid_numerics(cap):
         torch.testing.assert_close(s.float(), s_ref, rtol=2e-2, atol=3e-2)
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 def test_capped_stem_and_elementwise_grids():
     """Persistent stem and capped elementwise grids (as inside a CU-masked vGPU) give the
     same results as the uncapped launches."""
@@ -285,7 +285,7 @@ def test_capped_stem_and_elementwise_grids():
     torch.testing.assert_close(got_bn[1], ref_bn[1], rtol=0, atol=0)
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 def test_kernels_reject_host_tensors():
     """A CPU parameter tensor must raise before any launch (its pointer would fault the GPU)."""
     x = torch.zeros(1, 64, 4, 4, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -296,14 +296,14 @@ def test_kernels_reject_host_tensors():
         bn_act(x, torch.ones(64), torch.zeros(64, device="cuda"))
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 def test_conv1x1_rejects_unsupported_shapes():
     x = torch.zeros(1, 96, 4, 4, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     with pytest.raises(ValueError):
         conv1x1(x, torch.zeros(64, 96, device="cuda", dtype=torch.bfloat16))
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("shape", [(2, 64, 17, 17), (3, 256, 9, 7), (1, 2048, 11, 11), (50, 64, 87, 87),
                                    (2, 96, 9, 9), (1, 8, 3, 5)])
 @pytest.mark.parametrize("mode", ["plain", "residual", "residual_sum", "residual_post"])
@@ -326,7 +326,7 @@ def test_bn_act_kernel_numerics(shape, mode, act):
         torch.testing.assert_close(out[1].float(), s_ref, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("mfma_mode", ["off", "on", "auto"])
 def test_fused_resnet50_matches_eager_bf16(mfma_mode):
     torch.manual_seed(0)
@@ -346,12 +346,12 @@ def test_fused_resnet50_matches_eager_bf16(mfma_mode):
     assert cos > 0.995, cos
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("case", ["resnet50-train", "deeplab-inf", "lstm-inf"])
 def test_graph_capture_steps(case):
     """Whole-step HIP-graph capture (forward, or forward+backward+SGD) replays correctly."""
     from amdvgpu.models.aibench import Runner, get_case
-    r = Runner(get_case(case), "cuda:0", batch=2)
+    r = Runner(get_case(case), "cuda:0", batch=2, dtype=torch.bfloat16, fuse=True)
     if r.x.dim() == 4:
         r.x = r.x[..., :128, :128].contiguous(memory_format=torch.channels_last)
     r.step()
@@ -387,7 +387,7 @@ def test_fused_deeplab_graph_equals_original_fp32_cpu():
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 def test_fused_deeplab_matches_eager_bf16():
     import copy
     from amdvgpu.models.aibench import DeepLabV3Plus
@@ -438,7 +438,7 @@ def test_fuse_conv_relu_rewrites_vgg_cpu():
     torch.testing.assert_close(got, ref)
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("mode", ["on", "auto"])
 def test_vgg16_fused_matches_eager_bf16(mode):
     from amdvgpu.models.aibench import VGG16
@@ -473,7 +473,7 @@ def test_lstm_gate_permutation_cpu():
         torch.testing.assert_close(f(x), out[:, -1])  # torch impl: the library path
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("B,T", [(20, 64), (100, 1024), (3, 7)])
 def test_lstm_recurrence_numerics(B, T):
     """Whole-sequence HIP LSTM vs PyTorch's fp32 LSTM on the same (bf16-rounded) weights
@@ -533,7 +533,7 @@ def test_lstm_train_module_cpu_is_library_path():
     torch.testing.assert_close(f(x), out[:, -1])
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 @pytest.mark.parametrize("B,T", [(10, 1024), (20, 64), (3, 7)])
 def test_lstm_training_kernels_numerics(B, T):
     """HIP training forward (stash) and backward recurrence kernels vs (a) their PyTorch
@@ -587,12 +587,12 @@ def test_lstm_training_kernels_numerics(B, T):
         assert cos > 0.995 and rel < 0.1, (n, float(cos), float(rel))
 
 
-@pytest.mark.gpu
+@pytest.mark.kernels
 def test_lstm_training_step_graph_capturable():
     """The fused LSTM training step (forward, loss, backward, SGD) replays from a HIP graph:
     every replay updates the weights (the captured loss changes) and stays finite."""
     from amdvgpu.models.aibench import Runner, get_case
-    r = Runner(get_case("lstm-train"), "cuda:0", batch=10)
+    r = Runner(get_case("lstm-train"), "cuda:0", batch=10, dtype=torch.bfloat16, fuse=True)
     assert r.fused
     r.x = r.x[:, :128].contiguous()
     w0 = r.model.lstm.weight_hh_l0.detach().clone()
