@@ -116,40 +116,99 @@ def best_effort(available, required, size):
     return [items[i] for i in chosen]
 
 
-def allocate_vdevices(vdevices, available_ids, must_include_ids, size):
+PLACEMENT_SPREAD, PLACEMENT_BINPACK = "spread", "binpack"
+PLACEMENTS = (PLACEMENT_SPREAD, PLACEMENT_BINPACK)
+
+
+def _placement_key(placement, free, order):
+    """Sort key of a physical GPU for ``placement``: spread prefers the GPU with the most
+    free vGPUs (tenants land on idle GPUs first, so each keeps its spatial CU slice and
+    the node's 8 GPUs fill evenly); binpack the one with the fewest (whole GPUs stay free
+    for large jobs). Ties keep the kubelet's order."""
+    return (-free if placement == PLACEMENT_SPREAD else free, order)
+
+
+def allocate_vdevices(vdevices, available_ids, must_include_ids, size, placement=PLACEMENT_SPREAD):
     """GetPreferredAllocation for vGPU ids (reference ``server.go:271-326``).
 
-    Maps the available vGPU ids onto their physical GPUs, runs the best-effort policy
-    on the physical set, and maps each chosen GPU back to one of its available vGPUs —
-    a must-include vGPU when there is one (the reference always takes the first
-    available vGPU of the GPU, ignoring must-include). Falls back to the first ``size``
-    available ids (must-include first) when the policy has no answer, e.g. when more
-    vGPUs than distinct GPUs are requested.
+    Maps the available vGPU ids onto their physical GPUs and picks ``size`` distinct GPUs:
+    the best-effort topology policy decides first (for multi-GPU requests), and among
+    GPU sets of equal topology score the ``placement`` policy decides, with the number of
+    free vGPUs per GPU taken from the kubelet's own ``available`` list. Each chosen GPU is
+    mapped back to one of its available vGPUs - a must-include vGPU when there is one (the
+    reference always takes the first available vGPU of the GPU, ignoring must-include).
+
+    The reference's fallback (the first ``size`` available ids, ``server.go:305-310``) may
+    return two vGPUs of one GPU while other GPUs have free slots. Here two vGPUs of one GPU
+    are only returned when fewer than ``size`` distinct GPUs have a free vGPU (and then
+    ``Allocate`` decides, see ``--duplicate-vgpus``), and a 1-vGPU request goes to the GPU
+    the placement policy picks instead of the first available one.
     """
     by_id = {v.id: v for v in vdevices}
     avail = [by_id[i] for i in available_ids if i in by_id]
     must = [by_id[i] for i in must_include_ids if i in by_id]
-    phys, seen = [], set()
+    free, order, phys = {}, {}, []
     for v in avail:
-        if v.uuid not in seen:
-            seen.add(v.uuid)
+        free[v.uuid] = free.get(v.uuid, 0) + 1
+        if v.uuid not in order:
+            order[v.uuid] = len(order)
             phys.append(v.dev)
     req_phys, rseen = [], set()
     for v in must:
         if v.uuid not in rseen:
             rseen.add(v.uuid)
-            req_phys.append(next(p for p in phys if p.uuid == v.uuid))
-    chosen = best_effort(phys, req_phys, size) if len(req_phys) == len(must) else []
+            p = next((p for p in phys if p.uuid == v.uuid), None)
+            if p is not None:
+                req_phys.append(p)
+    key = lambda p: _placement_key(placement, free.get(p.uuid, 0), order.get(p.uuid, 0))  # noqa: E731
+    chosen = []
+    if len(req_phys) == len(rseen) == len(must) and len(phys) >= size:
+        if size == 1:
+            chosen = req_phys[:1] or [min(phys, key=key)]
+        else:
+            best = best_effort(phys, req_phys, size)
+            if best:
+                chosen = _placement_among_ties(phys, req_phys, size, set_score(best), key) or best
     if chosen:
         out = []
         for p in chosen:
             pick = next((v for v in must if v.uuid == p.uuid), None) or next(v for v in avail if v.uuid == p.uuid)
             out.append(pick.id)
         return out
+    # Fewer distinct GPUs than requested (or must-includes that are not available): every
+    # must-include, then one vGPU of each other GPU in placement order, and only then
+    # second vGPUs of GPUs already chosen.
     out = [v.id for v in must]
+    used = {by_id[i].uuid for i in out}
+    for p in sorted(phys, key=key):
+        if len(out) >= size:
+            break
+        if p.uuid not in used:
+            out.append(next(v.id for v in avail if v.uuid == p.uuid))
+            used.add(p.uuid)
     for v in avail:
         if len(out) >= size:
             break
         if v.id not in out:
             out.append(v.id)
     return out[:size]
+
+
+def _placement_among_ties(phys, required, size, score, key, limit=20000):
+    """Among the GPU sets of ``size`` holding ``required`` whose topology score equals
+    ``score`` (the best-effort answer's), the one the placement key prefers (summed over
+    the set). Bounded enumeration: None when there are too many sets to look at."""
+    from math import comb
+    others = [p for p in phys if p not in required]
+    k = size - len(required)
+    if k < 0 or comb(len(others), k) > limit:
+        return None
+    best, best_key = None, None
+    for c in combinations(sorted(others, key=key), k):
+        s = list(required) + list(c)
+        if set_score(s) != score:
+            continue
+        kk = tuple(sum(x) for x in zip(*(key(p) for p in s)))
+        if best is None or kk < best_key:
+            best, best_key = s, kk
+    return best

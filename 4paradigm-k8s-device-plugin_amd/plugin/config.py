@@ -14,6 +14,8 @@ PARTITION_NONE, PARTITION_SINGLE, PARTITION_MIXED = "none", "single", "mixed"
 LIST_ENVVAR, LIST_AMD_RUNTIME, LIST_VOLUME_MOUNTS = "envvar", "amd-container-runtime", "volume-mounts"
 ID_UUID, ID_INDEX = "uuid", "index"
 CU_MODES = ("auto", "spatial", "temporal", "both", "off")
+PLACEMENTS = ("spread", "binpack")
+DUPLICATE_POLICIES = ("reject", "merge")
 DEFAULT_RESOURCE = "amd.com/gpu"
 DEFAULT_PLUGIN_DIR = "/var/lib/kubelet/device-plugins/"
 DEFAULT_VGPU_DIR = "/usr/local/vgpu"
@@ -51,6 +53,9 @@ class PluginConfig:
     health_interval_s: float = 5.0
     node_name: str = ""
     shared_cache_dir: str = "/tmp"
+    placement: str = "spread"               # which GPU a 1-vGPU pod lands on (GetPreferredAllocation)
+    duplicate_vgpus: str = "reject"         # Allocate of two vGPUs of one GPU: reject | merge
+    host_memory_per_vgpu: str = "0"         # pinned host memory budget per vGPU (0 = unlimited)
     version_requested: bool = False
     extra: dict = field(default_factory=dict)
 
@@ -73,7 +78,21 @@ class PluginConfig:
             raise ValueError(f"invalid --device-cores-scaling option: {self.device_cores_scaling}")
         if self.cu_mode not in CU_MODES:
             raise ValueError(f"invalid --cu-mode option: {self.cu_mode}")
+        if self.placement not in PLACEMENTS:
+            raise ValueError(f"invalid --placement option: {self.placement}")
+        if self.duplicate_vgpus not in DUPLICATE_POLICIES:
+            raise ValueError(f"invalid --duplicate-vgpus option: {self.duplicate_vgpus}")
+        from ..utils.sizes import parse_size
+        try:
+            parse_size(self.host_memory_per_vgpu)
+        except ValueError:
+            raise ValueError(f"invalid --host-memory-per-vgpu option: {self.host_memory_per_vgpu}") from None
         return self
+
+    @property
+    def host_memory_per_vgpu_bytes(self):
+        from ..utils.sizes import parse_size
+        return parse_size(self.host_memory_per_vgpu)
 
 
 # (flag, dest, type, env vars, help)
@@ -110,6 +129,13 @@ _FLAGS = [
     ("--pcibus-file", "pcibus_file", str, ["VGPU_PCIBUS_FILE", "PCIBUSFILE"], "write the GPU BDF list here"),
     ("--health-interval", "health_interval_s", float, ["HEALTH_INTERVAL"], "health poll period (s)"),
     ("--node-name", "node_name", str, ["NODE_NAME"], "this node (legacy-preferred / monitor mode)"),
+    ("--placement", "placement", str, ["PLACEMENT_POLICY"],
+     "GPU choice for a new pod: spread (the GPU with the most free vGPUs) | binpack (the fullest GPU with room)"),
+    ("--duplicate-vgpus", "duplicate_vgpus", str, ["DUPLICATE_VGPUS"],
+     "a container given two vGPUs of one GPU: reject (fail Allocate) | merge (one device with the summed "
+     "quota and CU share; VGPU_DUPLICATE_MERGED tells the container)"),
+    ("--host-memory-per-vgpu", "host_memory_per_vgpu", str, ["HOST_MEMORY_PER_VGPU"],
+     "pinned host memory (hipHostMalloc / hipHostRegister) per vGPU, e.g. 64g; 0 = unlimited (tracked only)"),
 ]
 
 

@@ -42,6 +42,7 @@ LOCK_HOST_DIR = "lock"
 CONTAINER_LOCK_DIR = "/usr/local/vgpu/lock"
 ANN_REQUEST = "amd-vgpu/request"
 ANN_USING = "amd-vgpu/using"
+ANN_DUPLICATES = "amd-vgpu/merged-duplicates"
 
 
 ALLOWLIST_HOST_DIR = "allowlist"
@@ -119,6 +120,17 @@ def gc_shared_dirs(root, max_age_s=SHARED_MAX_AGE_S, now=None):
     return removed
 
 
+def duplicate_gpus(vdevs):
+    """UUIDs of the physical GPUs that back more than one of ``vdevs`` (reference
+    duplicate_devices, [nvml/util.c] "device index %d and %d are the same physical device")."""
+    seen, dups = set(), []
+    for v in vdevs:
+        if v.uuid in seen and v.uuid not in dups:
+            dups.append(v.uuid)
+        seen.add(v.uuid)
+    return dups
+
+
 def device_ids(cfg, devices_by_uuid, uuids):
     if cfg.device_id_strategy == ID_INDEX:
         return [str(devices_by_uuid[u].index) for u in uuids if u in devices_by_uuid]
@@ -177,6 +189,18 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
                 resp.envs[f"VGPU_DEVICE_CU_RANGE_{i}"] = f"{v.cu_range[0]}-{v.cu_range[1]}"
         dmap.append(f"{i}:{v.uuid}")
     resp.envs["VGPU_DEVICE_MAP"] = " ".join(dmap)
+    dups = duplicate_gpus(vdevs)
+    if dups:
+        # --duplicate-vgpus=merge: the shim merges the vGPUs of one GPU into that device
+        # (quotas and CU shares add up); the container is told, since it sees fewer
+        # devices than it requested (docs/ABI.md "Duplicate vGPUs").
+        resp.envs["VGPU_DUPLICATE_MERGED"] = ",".join(dups)
+        resp.annotations[ANN_DUPLICATES] = ",".join(dups)
+    host_per = cfg.host_memory_per_vgpu_bytes if hasattr(cfg, "host_memory_per_vgpu_bytes") else 0
+    if host_per:
+        # Pinned host memory of the container (hipHostMalloc / hipHostRegister): one
+        # budget per vGPU, summed (reference: class (b) host-alloc OOM checks).
+        resp.envs["VGPU_HOST_MEMORY_LIMIT"] = format_mib(host_per * len(vdevs))
     # PCI addresses of the container's GPUs: in-container amd-smi lists only these
     # (reference: nvmlDeviceGetCount / GetHandleByIndex remapping, nvml/hook.c:438-527).
     bdfs = [devices_by_uuid[u].bdf for u in uuids if u in devices_by_uuid and devices_by_uuid[u].bdf]

@@ -24,7 +24,7 @@ import grpc
 
 from ..parallel.topology import allocate_vdevices
 from . import api
-from .contract import build_container_response, build_partition_response
+from .contract import duplicate_gpus, build_container_response, build_partition_response
 from .vdevice import device_to_vdevices, vdevices_by_ids
 
 log = logging.getLogger("amdvgpu.plugin")
@@ -249,7 +249,7 @@ class DevicePluginServer:
         resp = api.PreferredAllocationResponse()
         for req in request.container_requests:
             ids = allocate_vdevices(self.vdevices, list(req.available_deviceIDs), list(req.must_include_deviceIDs),
-                                    req.allocation_size)
+                                    req.allocation_size, placement=self.cfg.placement)
             resp.container_responses.add(deviceIDs=ids)
         return resp
 
@@ -292,8 +292,8 @@ class DevicePluginServer:
             if self.legacy is not None:
                 self.legacy.release_by_request(requested)
                 avail = self.legacy.available([v.id for v in self.vdevices])
-                using = allocate_vdevices(self.vdevices, avail, [], len(requested)) if len(avail) >= len(
-                    requested) else []
+                using = allocate_vdevices(self.vdevices, avail, [], len(requested),
+                                          placement=self.cfg.placement) if len(avail) >= len(requested) else []
                 if len(using) < len(requested):
                     # Reference server.go:436-439 ("no enough devices"): never fall back to
                     # the kubelet's IDs, which may belong to another container's vGPUs.
@@ -304,6 +304,15 @@ class DevicePluginServer:
                 vds = vdevices_by_ids(self.vdevices, using)
             except KeyError as e:
                 self._fail(context, f"invalid allocation request for '{self.resource_name}': {e}")
+            dups = duplicate_gpus(vds)
+            if dups and self.cfg.duplicate_vgpus == "reject":
+                # Reference [device.c:81-155] keeps duplicates as separate virtual devices
+                # (virtual PCI ids, cooperative launch off). A ROCm process cannot be shown two
+                # devices backed by one agent, so the container would silently see one GPU
+                # with the summed share: refused instead (--duplicate-vgpus=merge keeps it).
+                self._fail(context, f"allocation for '{self.resource_name}' holds several vGPUs of one GPU "
+                                    f"({', '.join(dups)}); a container sees one device per physical GPU "
+                                    f"(plugin flag --duplicate-vgpus=merge accepts this as one merged device)")
             unhealthy = [v.id for v in vds if not v.dev.healthy]
             if unhealthy:
                 log.warning("allocating unhealthy vGPUs %s", unhealthy)

@@ -271,3 +271,18 @@ def test_monitor_mode_shared_dirs_are_collected(tmp_path):
         os.utime(root / tag, (old, old))
     assert gc_shared_dirs(str(root), now=now) == ["ns_done_main"]
     assert sorted(os.listdir(root)) == ["ns_fresh_main", "ns_running_main"]
+
+
+def test_placement_duplicate_and_host_memory_flags():
+    from amdvgpu.plugin.config import parse_config
+    cfg = parse_config(["--placement", "binpack", "--duplicate-vgpus", "merge", "--host-memory-per-vgpu", "8g"],
+                       environ={})
+    assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("binpack", "merge", 8 << 30)
+    cfg = parse_config([], environ={"PLACEMENT_POLICY": "binpack", "DUPLICATE_VGPUS": "merge",
+                                    "HOST_MEMORY_PER_VGPU": "512m"})
+    assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("binpack", "merge", 512 << 20)
+    cfg = parse_config([], environ={})
+    assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("spread", "reject", 0)
+    for bad in (["--placement", "random"], ["--duplicate-vgpus", "allow"], ["--host-memory-per-vgpu", "lots"]):
+        with pytest.raises(ValueError):
+            parse_config(bad, environ={})

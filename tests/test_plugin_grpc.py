@@ -229,3 +229,67 @@ def test_stop_honoured_while_the_kubelet_is_down(plugin_dir):
     stop.set()
     th.join(timeout=10)   # at most one registration attempt (dial timeouts) in flight
     assert not th.is_alive()
+
+
+def test_duplicate_vgpus_rejected_by_default(plugin_dir):
+    """Two vGPUs of one GPU in one container: Allocate fails with a clear error (the
+    container would otherwise see one device with the summed share)."""
+    import grpc
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=4, backend=FakeBackend(n=1))
+    try:
+        k.wait_registered("amd.com/gpu")
+        devs = k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
+        ids = sorted(devs)[:2]
+        with pytest.raises(grpc.RpcError) as e:
+            k.allocate_ids("amd.com/gpu", ids)
+        assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        assert "several vGPUs of one GPU" in e.value.details() and "--duplicate-vgpus=merge" in e.value.details()
+    finally:
+        shutdown(k, stop, th)
+
+
+def test_duplicate_vgpus_merged_on_request(plugin_dir):
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=4, backend=FakeBackend(n=1),
+                                  duplicate_vgpus="merge")
+    try:
+        k.wait_registered("amd.com/gpu")
+        devs = k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
+        ids = sorted(devs)[:2]
+        resp = k.allocate_ids("amd.com/gpu", ids)
+        envs = dict(resp.envs)
+        uuid = ids[0].rsplit("-", 1)[0]
+        assert envs["VGPU_DUPLICATE_MERGED"] == uuid
+        assert dict(resp.annotations)["amd-vgpu/merged-duplicates"] == uuid
+        assert envs["ROCR_VISIBLE_DEVICES"] == uuid  # one device in the container
+        assert envs["VGPU_DEVICE_MAP"] == f"0:{uuid} 1:{uuid}"
+    finally:
+        shutdown(k, stop, th)
+
+
+def test_placement_spread_over_the_kubelet(plugin_dir):
+    """Sequential 1-vGPU pods through the kubelet flow land on distinct GPUs (spread),
+    or fill one GPU first (binpack)."""
+    for placement, want in (("spread", 4), ("binpack", 1)):
+        d = os.path.join(plugin_dir, placement)
+        os.makedirs(d)
+        cfg, k, sup, stop, th = start(d, device_split_count=4, backend=FakeBackend(n=4, topology="xgmi"),
+                                      placement=placement)
+        try:
+            k.wait_registered("amd.com/gpu")
+            k.wait_devices("amd.com/gpu", predicate=lambda x: len(x) == 16)
+            gpus = {k.allocate("amd.com/gpu", 1)[0][0].rsplit("-", 1)[0] for _ in range(4)}
+            assert len(gpus) == want, (placement, gpus)
+        finally:
+            shutdown(k, stop, th)
+
+
+def test_host_memory_budget_per_vgpu(plugin_dir):
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=2, backend=FakeBackend(n=2),
+                                  host_memory_per_vgpu="16g")
+    try:
+        k.wait_registered("amd.com/gpu")
+        k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
+        _ids, resp = k.allocate("amd.com/gpu", 2)
+        assert dict(resp.envs)["VGPU_HOST_MEMORY_LIMIT"] == f"{32 << 10}m"
+    finally:
+        shutdown(k, stop, th)

@@ -117,3 +117,66 @@ def test_vgpu_fallback_when_more_vgpus_than_gpus():
     vds = device_to_vdevices(FakeBackend(n=1).devices(), 4)
     ids = allocate_vdevices(vds, [v.id for v in vds], [], 3)
     assert ids == [v.id for v in vds[:3]]
+
+
+def _sequential_pods(placement, pods, size=1, n=8, split=4):
+    """The kubelet's view: each pod's GetPreferredAllocation sees the vGPUs still free."""
+    vds = device_to_vdevices(FakeBackend(n=n, topology="xgmi").devices(), split)
+    free = [v.id for v in vds]
+    got = []
+    for _ in range(pods):
+        ids = allocate_vdevices(vds, free, [], size, placement=placement)
+        assert len(ids) == size and all(i in free for i in ids)
+        free = [i for i in free if i not in ids]
+        got.append(ids)
+    return got
+
+
+def _gpu(vid):
+    return vid.rsplit("-", 1)[0]
+
+
+def test_spread_places_sequential_pods_on_distinct_gpus():
+    pods = _sequential_pods("spread", 8)
+    assert len({_gpu(p[0]) for p in pods}) == 8
+    # a second round then fills every GPU's second slot before any third one
+    more = _sequential_pods("spread", 16)
+    per_gpu = {}
+    for p in more:
+        per_gpu[_gpu(p[0])] = per_gpu.get(_gpu(p[0]), 0) + 1
+    assert sorted(per_gpu.values()) == [2] * 8
+
+
+def test_binpack_fills_gpus_before_opening_new_ones():
+    pods = _sequential_pods("binpack", 8)
+    assert len({_gpu(p[0]) for p in pods}) == 2
+
+
+def test_multi_vgpu_requests_keep_the_topology_score():
+    """2-vGPU pods on a PCIe node (pairs score by NUMA node): every pod gets two distinct
+    GPUs of one NUMA node, under both placements."""
+    devs = FakeBackend(n=8, topology="pcie", numa_split=4).devices()
+    by_uuid = {d.uuid: d for d in devs}
+    for placement in ("spread", "binpack"):
+        vds = device_to_vdevices(devs, 4)
+        free = [v.id for v in vds]
+        for _ in range(4):
+            ids = allocate_vdevices(vds, free, [], 2, placement=placement)
+            free = [i for i in free if i not in ids]
+            g = [by_uuid[_gpu(i)] for i in ids]
+            assert g[0] is not g[1] and g[0].numa_node == g[1].numa_node
+
+
+def test_no_duplicate_gpu_while_another_gpu_is_free():
+    """Two slots of one GPU are only preferred when fewer distinct GPUs are free."""
+    vds = device_to_vdevices(FakeBackend(n=3, topology="xgmi").devices(), 4)
+    # GPU 0 has all four slots free, GPUs 1 and 2 one slot each
+    free = [v.id for v in vds if v.dev.index == 0] + [vds[4].id, vds[8].id]
+    for placement in ("spread", "binpack"):
+        ids = allocate_vdevices(vds, free, [], 3, placement=placement)
+        assert len({_gpu(i) for i in ids}) == 3
+    ids = allocate_vdevices(vds, free, [], 4)
+    assert len(ids) == 4 and len({_gpu(i) for i in ids}) == 3  # one duplicate is unavoidable
+    # two must-include vGPUs of one GPU are both kept
+    ids = allocate_vdevices(vds, free, [vds[0].id, vds[1].id], 3)
+    assert vds[0].id in ids and vds[1].id in ids and len(ids) == 3
