@@ -37,9 +37,26 @@ CONTAINER_ALLOWLIST_DIR = "/vgpu"
 SHARED_HOST_DIR = "shared"
 # Host-PID discovery lock shared by every vGPU container of the node (the reference's
 # "unified lock" /tmp/vgpulock/lock, utils.c:30-36, which only serialised one container):
-# processes of different containers that start together take turns probing KFD.
+# processes of different containers that start together take turns probing KFD. The
+# plugin creates the file (root-owned, 0644) and every container gets it read-only: a
+# tenant can take the lock (flock works on a read-only descriptor) but cannot unlink or
+# replace it, and the shim probes unlocked once its wait times out, so holding it forever
+# only delays neighbours (native/src/core/kfd.cpp).
 LOCK_HOST_DIR = "lock"
+LOCK_FILE = "hostpid.lock"
 CONTAINER_LOCK_DIR = "/usr/local/vgpu/lock"
+
+
+def ensure_lock_file(vgpu_dir):
+    """Creates <vgpu_dir>/lock/hostpid.lock (0644) if missing; returns its path."""
+    d = os.path.join(vgpu_dir, LOCK_HOST_DIR)
+    os.makedirs(d, mode=0o755, exist_ok=True)
+    path = os.path.join(d, LOCK_FILE)
+    if not os.path.exists(path):
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+        os.close(fd)
+    os.chmod(path, 0o644)
+    return path
 ANN_REQUEST = "amd-vgpu/request"
 ANN_USING = "amd-vgpu/using"
 ANN_DUPLICATES = "amd-vgpu/merged-duplicates"
@@ -239,10 +256,10 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
     else:
         resp.mounts.add(container_path=CONTAINER_ALLOWLIST_DIR, host_path=os.path.join(vdir, "allowlist"),
                         read_only=True)
-    lock_dir = os.path.join(vdir, LOCK_HOST_DIR)
-    if os.path.isdir(lock_dir):
-        resp.mounts.add(container_path=CONTAINER_LOCK_DIR, host_path=lock_dir, read_only=False)
-        resp.envs["VGPU_LOCK_FILE"] = CONTAINER_LOCK_DIR + "/hostpid.lock"
+    lock_file = os.path.join(vdir, LOCK_HOST_DIR, LOCK_FILE)
+    if os.path.isfile(lock_file):
+        resp.mounts.add(container_path=f"{CONTAINER_LOCK_DIR}/{LOCK_FILE}", host_path=lock_file, read_only=True)
+        resp.envs["VGPU_LOCK_FILE"] = f"{CONTAINER_LOCK_DIR}/{LOCK_FILE}"
     return resp
 
 

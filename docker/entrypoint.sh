@@ -5,7 +5,11 @@ set -euo pipefail
 SRC=${VGPU_LIB_DIR:-/opt/amd-vgpu/4paradigm-k8s-device-plugin_amd/lib}
 DEST=${VGPU_DIR:-/usr/local/vgpu}
 mkdir -p "$DEST" "$DEST/shared" "$DEST/allowlist/containers" "$DEST/lock"
-chmod 0777 "$DEST/lock"   # every container's processes take the host-PID discovery lock here
+# Host-PID discovery lock: root-owned and mounted read-only into every container (flock
+# works on a read-only descriptor; tenants cannot unlink or replace it).
+[ -e "$DEST/lock/hostpid.lock" ] || : > "$DEST/lock/hostpid.lock"
+chmod 0755 "$DEST/lock"
+chmod 0644 "$DEST/lock/hostpid.lock"
 # Atomic replace: containers that already mapped the old shim keep their inode.
 for f in libvgpu_hip.so libvgpu_region.so vgpu-validate vgpuctl ld.so.preload; do
   install -m 0755 "$SRC/$f" "$DEST/.$f.new" && mv -f "$DEST/.$f.new" "$DEST/$f"

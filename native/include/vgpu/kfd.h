@@ -50,8 +50,12 @@ using VramProbe = bool (*)(void* ctx, uint64_t bytes, bool alloc);
 pid_t kfd_resolve_hostpid(uint32_t gpu_id, VramProbe probe, void* ctx, const char* lock_path,
                           int lock_timeout_ms, unsigned seed);
 
-// Exclusive flock on `path` (parent directory created), polling up to timeout_ms.
-// Returns the fd (release with kfd_unlock) or -1.
+// Exclusive flock on `path`, polling up to timeout_ms. An existing file is opened
+// read-only (the plugin mounts it so); a missing one is created, world-accessible.
+// Returns the fd (release with kfd_unlock), kLockBusy when another holder kept it for the
+// whole wait, or kLockUnavailable when the file cannot be opened.
+constexpr int kLockBusy = -2;
+constexpr int kLockUnavailable = -1;
 int kfd_lock(const char* path, int timeout_ms);
 void kfd_unlock(int fd);
 

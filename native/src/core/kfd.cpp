@@ -82,19 +82,25 @@ std::vector<int> kfd_pids_on_gpu(uint32_t gpu_id) {
 }
 
 int kfd_lock(const char* path, int timeout_ms) {
-  if (!path || !*path) return -1;
-  std::string dir(path);
-  size_t slash = dir.rfind('/');
-  if (slash != std::string::npos && slash > 0) {
-    dir.resize(slash);
-    mode_t old = umask(0);
-    mkdir(dir.c_str(), 0777);  // EEXIST is fine
-    umask(old);
+  if (!path || !*path) return kLockUnavailable;
+  // In a pod the plugin bind-mounts a lock file it created, read-only: tenants can take
+  // the lock (flock works on a read-only descriptor) but cannot unlink or replace it.
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    // Outside a pod: create it, world-accessible (processes of one container may run as
+    // different users). The process umask is left alone - it is shared with the
+    // application's threads - and the modes are set explicitly on what this call created.
+    std::string dir(path);
+    size_t slash = dir.rfind('/');
+    if (slash != std::string::npos && slash > 0) {
+      dir.resize(slash);
+      if (mkdir(dir.c_str(), 0700) == 0) chmod(dir.c_str(), 01777);
+    }
+    fd = open(path, O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0600);
+    if (fd >= 0) fchmod(fd, 0666);
+    else fd = open(path, O_RDONLY | O_CLOEXEC);  // created by someone else meanwhile
   }
-  mode_t old = umask(0);
-  int fd = open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0666);
-  umask(old);
-  if (fd < 0) return -1;
+  if (fd < 0) return kLockUnavailable;
   // flock is released by the kernel when the holder dies: no expiry heuristic needed
   // (the reference's lock file carries a timestamp and is broken after a timeout).
   for (int waited = 0;; waited++) {
@@ -104,7 +110,7 @@ int kfd_lock(const char* path, int timeout_ms) {
     nanosleep(&ts, nullptr);
   }
   close(fd);
-  return -1;
+  return kLockBusy;
 }
 
 void kfd_unlock(int fd) {
@@ -119,14 +125,14 @@ pid_t kfd_resolve_hostpid(uint32_t gpu_id, VramProbe probe, void* ctx, const cha
   std::vector<int> pids = kfd_list_pids();
   if (std::binary_search(pids.begin(), pids.end(), (int)self)) return self;
   if (!probe || !gpu_id) return 0;
-  int lock = -1;
-  if (lock_path && *lock_path) {
-    lock = kfd_lock(lock_path, lock_timeout_ms);
-    if (lock < 0) {
-      VLOG_INFO("host-PID discovery: lock %s busy, retrying later", lock_path);
-      return 0;
-    }
-  }
+  // The lock only keeps concurrent probes from blurring each other's signatures; a
+  // holder that never lets go (any tenant can flock the node-wide file) must not stop
+  // this process from resolving its host PID, so after the wait the search runs
+  // unlocked: each candidate must match two different random sizes, which another
+  // process's concurrent probe does not.
+  int lock = lock_path && *lock_path ? kfd_lock(lock_path, lock_timeout_ms) : kLockUnavailable;
+  if (lock == kLockBusy) VLOG_INFO("host-PID discovery: lock %s still busy after %d ms, probing unlocked", lock_path,
+                                   lock_timeout_ms);
   std::vector<int> cand;
   for (int p : pids)
     if (kfd_vram_usage(p, gpu_id) >= 0) cand.push_back(p);

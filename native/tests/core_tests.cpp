@@ -3,6 +3,7 @@
 // Built plain and with -fsanitize=thread / address (make SAN=thread|address).
 #include <fcntl.h>
 #include <signal.h>
+#include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -855,13 +856,25 @@ static void test_hostpid_resolution() {
   k.add(getpid(), 0);
   CHECK_EQ(kfd_resolve_hostpid(k.gid, nullptr, nullptr, nullptr, 0, 1), getpid());
   CHECK(system(("rm -rf " + kroot + "/" + std::to_string(getpid())).c_str()) == 0);
-  // A held lock makes the attempt give up quickly (retried later by the caller).
+  // A lock somebody holds forever (any tenant can flock the node-wide file) delays the
+  // search by the wait only: it then runs unlocked and still resolves. Creating the lock
+  // leaves the process umask alone.
+  const mode_t um = umask(022);
   int held = kfd_lock(lock.c_str(), 0);
   CHECK(held >= 0);
+  CHECK_EQ((int)umask(022), 022);
+  umask(um);
+  CHECK_EQ(kfd_lock(lock.c_str(), 5), kLockBusy);
   ProbeCtx c2{&k, 400};
-  CHECK_EQ(kfd_resolve_hostpid(k.gid, fake_probe, &c2, lock.c_str(), 20, 7), 0);
+  CHECK_EQ(kfd_resolve_hostpid(k.gid, fake_probe, &c2, lock.c_str(), 20, 7), 400);
   kfd_unlock(held);
   CHECK_EQ(kfd_resolve_hostpid(k.gid, fake_probe, &c2, lock.c_str(), 20, 7), 400);
+  // The plugin's lock is a read-only file: flock works on it all the same.
+  CHECK(chmod(lock.c_str(), 0444) == 0);
+  int ro = kfd_lock(lock.c_str(), 0);
+  CHECK(ro >= 0);
+  kfd_unlock(ro);
+  CHECK_EQ(kfd_lock((kroot + "/no/such/dir/lock").c_str(), 0), kLockUnavailable);
 
   // 16 processes of one container start together while foreign processes come and go
   // and allocate: every one resolves its own host PID (serialised by the lock).

@@ -286,3 +286,21 @@ def test_placement_duplicate_and_host_memory_flags():
     for bad in (["--placement", "random"], ["--duplicate-vgpus", "allow"], ["--host-memory-per-vgpu", "lots"]):
         with pytest.raises(ValueError):
             parse_config(bad, environ={})
+
+
+def test_host_pid_lock_is_a_read_only_file_mount(tmp_path):
+    """The node-wide host-PID lock is a plugin-created file mounted read-only (tenants can
+    flock it but not unlink or replace it)."""
+    from amdvgpu.plugin.contract import build_container_response, ensure_lock_file
+    from amdvgpu.plugin.devices import FakeBackend
+    from amdvgpu.plugin.vdevice import device_to_vdevices
+    vdir = str(tmp_path / "vgpu")
+    path = ensure_lock_file(vdir)
+    assert os.stat(path).st_mode & 0o777 == 0o644
+    assert os.stat(os.path.dirname(path)).st_mode & 0o777 == 0o755
+    devs = FakeBackend(n=1).devices()
+    cfg = PluginConfig(vgpu_dir=vdir).validate()
+    resp = build_container_response(cfg, device_to_vdevices(devs, 2)[:1], {d.uuid: d for d in devs})
+    mounts = {m.container_path: (m.host_path, m.read_only) for m in resp.mounts}
+    assert mounts["/usr/local/vgpu/lock/hostpid.lock"] == (path, True)
+    assert dict(resp.envs)["VGPU_LOCK_FILE"] == "/usr/local/vgpu/lock/hostpid.lock"

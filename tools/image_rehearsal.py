@@ -168,6 +168,9 @@ def check_runtime(final, work, log=print):
     for d in ("shared", "lock", "allowlist/containers"):
         if not os.path.isdir(os.path.join(dest, d)):
             raise RuntimeError(f"entrypoint did not create {d}/")
+    lock = os.path.join(dest, "lock", "hostpid.lock")
+    if not os.path.isfile(lock) or os.stat(lock).st_mode & 0o777 != 0o644:
+        raise RuntimeError("entrypoint did not create the read-only host-PID lock file (0644)")
     # The installed shim is a loadable ELF exporting the interposed entry points.
     nm = subprocess.run(["nm", "-D", "--defined-only", os.path.join(dest, "libvgpu_hip.so")], capture_output=True,
                         text=True)
