@@ -90,18 +90,34 @@ def write_allowlist(vgpu_dir, name, uuids):
     return path
 
 
-SHARED_MAX_AGE_S = 24 * 3600
+SHARED_GRACE_S = 300
 
 
-def gc_shared_dirs(root, max_age_s=SHARED_MAX_AGE_S, now=None):
-    """Monitor mode leaves one host directory per container under ``root``
-    (<ns>_<pod>_<ctr>/<uuid>.cache); the reference never removes them. A directory is
-    removed once it and every region in it are older than ``max_age_s`` and no region
-    still lists a process (processes unregister when they exit). Returns the removed tags."""
+def gc_shared_dirs(root, pods, grace_s=SHARED_GRACE_S, now=None):
+    """Removes the monitor-mode host directories (<ns>_<pod>_<ctr>/<uuid>.cache) of pods
+    that no longer exist on this node; the reference never removes them.
+
+    Liveness comes from the pod list (``pods``: ``k8s.pod_summary`` dicts of this node),
+    never from a directory's age or its region's process count: an idle notebook pod or a
+    batch pod between runs keeps its directory however long it sleeps (its container's bind
+    mount points there, and a missing directory would leave the next process of the
+    container without its region). A directory is kept when a pod that is not Succeeded /
+    Failed owns its tag - same namespace, name and container, and the UID in the
+    ``.pod-uid`` marker when there is one (a re-created pod of the same name gets a fresh
+    directory, so the old one goes). ``pods=None`` (no pod list) removes nothing; a
+    directory younger than ``grace_s`` is never removed. Returns the removed tags."""
     import shutil
     import time
-    from ..shim.region import Region
+    from .k8s import POD_MARKER, TERMINAL_PHASES, pod_tag
+    if pods is None:
+        return []
     now = time.time() if now is None else now
+    live = {}
+    for p in pods:
+        if p.get("phase") in TERMINAL_PHASES:
+            continue
+        for c in p.get("containers", []):
+            live.setdefault(pod_tag(p, c["name"]), set()).add(p.get("uid", ""))
     removed = []
     try:
         tags = os.listdir(root)
@@ -110,28 +126,19 @@ def gc_shared_dirs(root, max_age_s=SHARED_MAX_AGE_S, now=None):
     for tag in tags:
         d = os.path.join(root, tag)
         try:
-            if not os.path.isdir(d) or now - os.path.getmtime(d) < max_age_s:
+            if not os.path.isdir(d) or now - os.path.getmtime(d) < grace_s:
                 continue
-            live = False
-            for fn in os.listdir(d):
-                fp = os.path.join(d, fn)
-                if now - os.path.getmtime(fp) < max_age_s:
-                    live = True
-                    break
-                if fn.endswith(".cache"):
-                    try:
-                        # No reclaim here: slots hold PIDs of the tenant's namespace, which
-                        # the plugin cannot check. A region whose processes were killed keeps
-                        # its slots, so its directory is kept (conservative).
-                        with Region(fp) as r:
-                            live = r.proc_count > 0
-                    except OSError:
-                        pass  # not a region of this layout: age alone decides
-                if live:
-                    break
-            if not live:
-                shutil.rmtree(d, ignore_errors=True)
-                removed.append(tag)
+            uids = live.get(tag)
+            if uids:
+                try:
+                    with open(os.path.join(d, POD_MARKER)) as f:
+                        marker = f.read().strip()
+                except OSError:
+                    marker = ""
+                if not marker or marker in uids:
+                    continue
+            shutil.rmtree(d, ignore_errors=True)
+            removed.append(tag)
         except OSError:
             continue
     return removed
@@ -175,7 +182,8 @@ def visible_envs(cfg, ids):
     return {AMD_RUNTIME_ENV: VOLUME_MOUNTS_ROOT}
 
 
-def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, using_ids=None, pod_tag=None):
+def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, using_ids=None, pod_tag=None,
+                             pod_uid=None):
     """ContainerAllocateResponse for one container holding vGPUs ``vdevs``."""
     resp = api.ContainerAllocateResponse()
     uuids = []
@@ -223,14 +231,22 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
     bdfs = [devices_by_uuid[u].bdf for u in uuids if u in devices_by_uuid and devices_by_uuid[u].bdf]
     if bdfs:
         resp.envs["VGPU_DEVICE_BDFS"] = ",".join(bdfs)
+        # KFD gpu_ids of the same devices: compute partitions exposed as GPUs share a PCI
+        # address, and amd-smi inside the container must list only this container's.
+        gids = [str(devices_by_uuid[u].gpu_id or 0) for u in uuids if u in devices_by_uuid and devices_by_uuid[u].bdf]
+        if any(g != "0" for g in gids):
+            resp.envs["VGPU_DEVICE_GPU_IDS"] = ",".join(gids)
     # Always explicit, so a container never depends on the shim's built-in default.
     resp.envs["VGPU_CU_MODE"] = cfg.cu_mode
 
     cache_name = f"{_uuid.uuid4()}.cache"
     if cfg.monitor_mode and pod_tag:
-        gc_shared_dirs(os.path.join(cfg.vgpu_dir, SHARED_HOST_DIR))
+        from .k8s import POD_MARKER
         host_dir = os.path.join(cfg.vgpu_dir, SHARED_HOST_DIR, pod_tag)
         os.makedirs(host_dir, exist_ok=True)
+        if pod_uid:
+            with open(os.path.join(host_dir, POD_MARKER), "w") as f:
+                f.write(pod_uid + "\n")
         resp.mounts.add(container_path=f"/{pod_tag}", host_path=host_dir, read_only=False)
         resp.envs["VGPU_SHARED_CACHE"] = f"/{pod_tag}/{cache_name}"
     else:

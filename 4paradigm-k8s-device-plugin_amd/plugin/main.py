@@ -73,7 +73,7 @@ class Supervisor:
         matcher = None
         if self.cfg.monitor_mode and self.pod_lister is not None:
             from .k8s import PodMatcher
-            matcher = PodMatcher(self.pod_lister)
+            matcher = PodMatcher(self.pod_lister, shared_root=os.path.join(self.cfg.vgpu_dir, "shared"))
         self.plugins = plugins_for(self.cfg, devices, self.backend, self._legacy_factory, matcher)
         started = 0
         for p in self.plugins:

@@ -24,7 +24,8 @@ import grpc
 
 from ..parallel.topology import allocate_vdevices
 from . import api
-from .contract import duplicate_gpus, build_container_response, build_partition_response
+from .contract import (SHARED_HOST_DIR, build_container_response, build_partition_response, duplicate_gpus,
+                       gc_shared_dirs)
 from .vdevice import device_to_vdevices, vdevices_by_ids
 
 log = logging.getLogger("amdvgpu.plugin")
@@ -281,6 +282,8 @@ class DevicePluginServer:
                 tags = self.pod_matcher.match([len(r.devicesIDs) for r in request.container_requests])
             except Exception as e:
                 log.warning("monitor mode: pod match failed: %s", e)
+            # Directories of pods that are gone, judged from the pod list just fetched.
+            gc_shared_dirs(os.path.join(self.cfg.vgpu_dir, SHARED_HOST_DIR), getattr(self.pod_matcher, "last_pods", None))
         if self.legacy is not None and not self.legacy.update_from_checkpoint():
             # Reference server.go:410-412: without the checkpoint the controller cannot know
             # which vGPUs other containers hold, so it refuses instead of double-booking.
@@ -318,7 +321,9 @@ class DevicePluginServer:
                 log.warning("allocating unhealthy vGPUs %s", unhealthy)
             cr = build_container_response(self.cfg, vds, self._by_uuid,
                                           request_ids=requested if self.legacy is not None else None,
-                                          using_ids=using, pod_tag=tags[i] if i < len(tags) else None)
+                                          using_ids=using, pod_tag=tags[i] if i < len(tags) else None,
+                                          pod_uid=self.pod_matcher.owner(tags[i]) if (
+                                              self.pod_matcher is not None and i < len(tags) and tags[i]) else None)
             resp.container_responses.append(cr)
             self.allocations.append((requested, using))
             if self.cfg.verbose > 5:

@@ -83,6 +83,7 @@ struct Config {
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
   uint64_t host_mem_limit = 0;           // VGPU_HOST_MEMORY_LIMIT: pinned host memory, 0 = unlimited
+  bool fail_open = false;                // VGPU_FAIL_OPEN: run unlimited when the region cannot be attached
 
   bool any_memory_limit() const;
   bool any_cu_limit() const;

@@ -262,6 +262,7 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   cfg->active_oom_killer = parse_bool(getenv_fn("VGPU_ACTIVE_OOM_KILLER"), false);
   cfg->memory_override = parse_bool(getenv_fn("VGPU_MEMORY_OVERRIDE"), false);
   cfg->signal_control = parse_bool(getenv_fn("VGPU_SIGNAL_CONTROL"), false);
+  cfg->fail_open = parse_bool(getenv_fn("VGPU_FAIL_OPEN"), false);
   cfg->hook_smi = parse_bool(getenv_fn("VGPU_HOOK_SMI"), true);
   cfg->virtual_cu_count = parse_bool(getenv_fn("VGPU_VIRTUAL_CU_COUNT"), true);
   long period = 120;

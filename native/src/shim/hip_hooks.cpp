@@ -16,7 +16,12 @@
 #define __HIP_PLATFORM_AMD__ 1
 #include <hip/hip_runtime_api.h>
 
+#include <strings.h>
+
+#include <atomic>
+#include <cstring>
 #include <mutex>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -35,41 +40,102 @@ using MallocFromPoolAsyncFn = hipError_t (*)(void**, size_t, hipMemPool_t, hipSt
 
 namespace vgpu {
 
-int hip_device_agent(int hipdev) {
-  ShimState& s = shim();
-  if (s.n_agents <= 1 || hipdev < 0 || !s.region.attached()) return 0;
-  static std::once_flag once;
-  static int map[kMaxDevices];
-  std::call_once(once, [&s] {
-    for (int i = 0; i < kMaxDevices; i++) map[i] = i;
-    VGPU_REAL_HIP(hipGetDeviceCount);
-    VGPU_REAL_HIP(hipDeviceGetAttribute);
-    int count = 0;
-    if (!real_hipGetDeviceCount || !real_hipDeviceGetAttribute || real_hipGetDeviceCount(&count) != hipSuccess)
-      return;
-    const Region* r = s.region.raw();
-    int found[kMaxDevices];
-    for (int h = 0; h < count && h < kMaxDevices; h++) {
-      int bus = -1, dev = -1, dom = -1;
-      if (real_hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, h) != hipSuccess ||
-          real_hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, h) != hipSuccess ||
-          real_hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainId, h) != hipSuccess)
-        return;
-      int match = -1, n = 0;
+namespace {
+
+// HIP device ordinal -> agent index as CLR derives it from HIP_VISIBLE_DEVICES
+// (CUDA_VISIBLE_DEVICES when that is unset): each entry is an agent index or an agent
+// UUID, and CLR stops at the first entry that names no device. Returns the number of
+// entries, or -1 when neither variable is set (identity).
+int visible_from_env(const ShimState& s, int* out) {
+  const char* v = getenv("HIP_VISIBLE_DEVICES");
+  if (!v) v = getenv("CUDA_VISIBLE_DEVICES");
+  if (!v) return -1;
+  const Region* r = s.region.raw();
+  int n = 0;
+  for (const char* p = v; *p && n < kMaxDevices;) {
+    const char* e = p;
+    while (*e && *e != ',') e++;
+    std::string tok(p, (size_t)(e - p));
+    int idx = -1;
+    if (!tok.empty() && tok.find_first_not_of("0123456789") == std::string::npos) {
+      idx = atoi(tok.c_str());
+    } else {
+      for (int a = 0; a < s.n_agents && idx < 0; a++)
+        if (!strcasecmp(r->dev[a].uuid, tok.c_str())) idx = a;
+    }
+    if (idx < 0 || idx >= s.n_agents) break;
+    out[n++] = idx;
+    p = *e ? e + 1 : e;
+  }
+  return n;
+}
+
+// Builds the HIP device -> agent map: by PCI address where it is unique (robust to any
+// reordering), by the visible-devices list where several agents share one address
+// (compute partitions exposed as GPUs). False when the runtime cannot answer yet.
+bool build_device_map(ShimState& s, int* map) {
+  VGPU_REAL_HIP(hipGetDeviceCount);
+  VGPU_REAL_HIP(hipDeviceGetAttribute);
+  int count = 0;
+  if (!real_hipGetDeviceCount || real_hipGetDeviceCount(&count) != hipSuccess || count <= 0) return false;
+  int env[kMaxDevices];
+  const int n_env = visible_from_env(s, env);
+  const Region* r = s.region.raw();
+  for (int h = 0; h < kMaxDevices; h++) map[h] = h < s.n_agents ? h : 0;
+  for (int h = 0; h < count && h < kMaxDevices; h++) {
+    int by_env = n_env < 0 ? h : (h < n_env ? env[h] : -1);
+    int by_bdf = -1, bus = -1, dev = -1, dom = -1;
+    if (real_hipDeviceGetAttribute && real_hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, h) == hipSuccess &&
+        real_hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, h) == hipSuccess &&
+        real_hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainId, h) == hipSuccess) {
+      int n = 0;
       for (int a = 0; a < s.n_agents; a++) {
         const DeviceState& d = r->dev[a];
         if ((d.bdf >> 3) == ((uint32_t)bus << 5 | (uint32_t)dev) && d.domain == (uint32_t)dom) {
-          match = a;
+          by_bdf = a;
           n++;
         }
       }
-      if (n != 1) return;  // unknown or shared address (compute partitions): keep the identity
-      found[h] = match;
+      if (n != 1) by_bdf = -1;  // shared address (partitions) or unknown: the list decides
     }
-    for (int h = 0; h < count && h < kMaxDevices; h++) map[h] = found[h];
-    VLOG_DEBUG("HIP device -> agent map built for %d device(s)", count);
-  });
-  return hipdev < kMaxDevices && map[hipdev] < s.n_agents ? map[hipdev] : 0;
+    const int pick = by_bdf >= 0 ? by_bdf : by_env;
+    if (pick < 0 || pick >= s.n_agents) return false;
+    map[h] = pick;
+  }
+  VLOG_DEBUG("HIP device -> agent map built for %d device(s)", count);
+  return true;
+}
+
+}  // namespace
+
+int hip_device_agent(int hipdev) {
+  ShimState& s = shim();
+  if (s.n_agents <= 1 || hipdev < 0 || hipdev >= kMaxDevices || !s.region.attached()) return 0;
+  static std::atomic<bool> built{false};
+  static int map[kMaxDevices];
+  static std::mutex mu;
+  static uint64_t next_try = 0;
+  if (__builtin_expect(!built.load(std::memory_order_acquire), 0)) {
+    // Not cached on failure: a runtime that could not answer yet (or a transient error)
+    // is asked again, at most every 100 ms, instead of pinning the process to a guess.
+    std::lock_guard<std::mutex> g(mu);
+    if (!built.load(std::memory_order_relaxed) && now_ns() >= next_try) {
+      int m[kMaxDevices];
+      if (build_device_map(s, m)) {
+        memcpy(map, m, sizeof(map));
+        built.store(true, std::memory_order_release);
+      } else {
+        next_try = now_ns() + 100'000'000ull;
+      }
+    }
+    if (!built.load(std::memory_order_relaxed)) {
+      int env[kMaxDevices];
+      const int n_env = visible_from_env(s, env);
+      const int guess = n_env < 0 ? hipdev : (hipdev < n_env ? env[hipdev] : 0);
+      return guess < s.n_agents ? guess : 0;
+    }
+  }
+  return map[hipdev] < s.n_agents ? map[hipdev] : 0;
 }
 
 int current_hip_agent() {

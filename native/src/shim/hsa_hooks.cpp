@@ -92,6 +92,12 @@ bool should_spill(int dev, size_t size) {
   return false;
 }
 
+// Limits are configured but the region could not be attached: GPU memory is refused.
+inline bool refused(hsa_amd_memory_pool_t pool) {
+  ShimState& s = shim();
+  return __builtin_expect(s.fail_closed, 0) && pool_ordinal(pool) >= 0;
+}
+
 inline bool ready() {
   ShimState& s = shim();
   int ph = s.phase.load(std::memory_order_acquire);
@@ -131,7 +137,10 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   VGPU_REAL_HSA(hsa_amd_memory_pool_allocate);
   VGPU_STAT(kStatAlloc);
   if (!real_hsa_amd_memory_pool_allocate) return HSA_STATUS_ERROR;
-  if (!ready() || size == 0) return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
+  if (!ready() || size == 0) {
+    if (size && refused(pool)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+    return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
+  }
   int dev = pool_ordinal(pool);
   VLOG_DEBUG("pool_allocate pool=%lx size=%zu flags=%u dev=%d", (unsigned long)pool.handle, size, flags, dev);
   if (dev < 0) return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
@@ -192,7 +201,10 @@ hsa_status_t hsa_amd_vmem_handle_create(hsa_amd_memory_pool_t pool, size_t size,
                                         uint64_t flags, hsa_amd_vmem_alloc_handle_t* handle) {
   VGPU_REAL_HSA(hsa_amd_vmem_handle_create);
   if (!real_hsa_amd_vmem_handle_create) return HSA_STATUS_ERROR;
-  if (!ready() || size == 0) return real_hsa_amd_vmem_handle_create(pool, size, type, flags, handle);
+  if (!ready() || size == 0) {
+    if (size && refused(pool)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+    return real_hsa_amd_vmem_handle_create(pool, size, type, flags, handle);
+  }
   int dev = pool_ordinal(pool);
   if (dev < 0) return real_hsa_amd_vmem_handle_create(pool, size, type, flags, handle);
   ShimState& s = shim();

@@ -5,7 +5,9 @@
 #include <signal.h>
 #include <strings.h>
 #include <sys/auxv.h>
+#include <sys/stat.h>
 
+#include <cerrno>
 #include <new>
 #include <unistd.h>
 
@@ -161,6 +163,7 @@ void atfork_child() {
   ShimState& s = shim();
   new (&s.alloc_mu) std::mutex();  // held by this thread since atfork_prepare
   new (&s.live_mu) std::mutex();   // may be held by a parent thread that does not exist here
+  new (&s.ctx_mu) std::mutex();
   s.slot = -1;
   s.active = false;
   s.allocs.clear();
@@ -324,9 +327,21 @@ void shim_init_after_hsa() {
   if (!s.hostpid) s.hostpid = resolve_hostpid(2000);
 
   int rc = s.region.attach(cfg.shared_cache.c_str(), &resolved, true);
+  if (rc == -ENOENT) {
+    // The region's directory is missing (e.g. a monitor-mode host directory removed under
+    // a running pod): recreate it, so this container keeps one region.
+    std::string dir = cfg.shared_cache.substr(0, cfg.shared_cache.rfind('/'));
+    for (size_t i = 1; i <= dir.size(); i++)
+      if (i == dir.size() || dir[i] == '/') mkdir(dir.substr(0, i).c_str(), 0755);
+    rc = s.region.attach(cfg.shared_cache.c_str(), &resolved, true);
+  }
   if (rc != 0) {
-    VLOG_ERROR("cannot attach shared region %s (%s); limits are NOT enforced", cfg.shared_cache.c_str(),
-               strerror(-rc));
+    // Without the region there is no shared accounting. With limits configured the shim
+    // fails closed - no device memory - rather than letting the container run unlimited
+    // (VGPU_FAIL_OPEN=1 restores the pass-through).
+    s.fail_closed = !cfg.fail_open && (cfg.any_memory_limit() || cfg.any_cu_limit());
+    VLOG_ERROR("cannot attach shared region %s (%s); %s", cfg.shared_cache.c_str(), strerror(-rc),
+               s.fail_closed ? "device memory is refused (fail closed)" : "limits are NOT enforced");
     s.phase.store(3);
     return;
   }
@@ -504,6 +519,9 @@ void apply_live_config() {
 void resync_context_charge() {
   ShimState& s = shim();
   if (!s.active || s.slot < 0 || !s.hostpid || s.exiting.load()) return;
+  // Called from hsa_queue_create and the maintenance thread: both would compute the same
+  // delta from the same ctx_had and charge it twice (a spurious OOM near the quota).
+  std::lock_guard<std::mutex> g(s.ctx_mu);
   Region* r = s.region.raw();
   for (int i = 0; i < s.n_agents; i++) {
     const AgentInfo& a = s.agents[i];

@@ -52,6 +52,7 @@ struct AllocRec {
 struct ShimState {
   std::atomic<int> phase{0};         // 0 = not initialised, 1 = initialising, 2 = ready, 3 = inert
   bool active = false;               // accounting + gates enabled
+  bool fail_closed = false;          // limits configured but no region: device memory refused
   SharedRegion region;
   int slot = -1;
   pid_t pid = 0;
@@ -72,6 +73,7 @@ struct ShimState {
   std::atomic<bool> any_temporal{false};            // some agent is gated by the GPU-time limiter
   std::atomic<int64_t> ipc_bytes[kMaxDevices] = {};  // IPC-attached bytes per device
   std::mutex live_mu;                               // serialises live reconfiguration
+  std::mutex ctx_mu;                                // serialises resync_context_charge
 };
 
 ShimState& shim();

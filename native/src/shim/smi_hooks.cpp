@@ -39,16 +39,35 @@ using namespace vgpu;
 
 namespace {
 
-// Region device index for a PCI (domain, bdfid) pair, or -1.
-int device_by_bdf(uint64_t domain, uint32_t bdfid) {
+constexpr uint64_t kNoGpuId = ~0ull;
+
+// Region device index for a PCI (domain, bdfid) pair, or -1. Compute partitions exposed
+// as GPUs share one PCI address: then the KFD gpu_id (`gpu_id`, kNoGpuId when the SMI
+// library cannot tell) picks the device.
+int device_by_bdf(uint64_t domain, uint32_t bdfid, uint64_t gpu_id = kNoGpuId) {
   if (!shim_attach_region_only()) return -1;
   if (!config().hook_smi) return -1;
   const Region* r = shim().region.raw();
+  int first = -1, unknown = -1;
   for (int i = 0; i < kMaxDevices; i++) {
     const DeviceState& d = r->dev[i];
-    if (d.configured && d.bdf == bdfid && d.domain == (uint32_t)domain) return i;
+    if (!d.configured || d.bdf != bdfid || d.domain != (uint32_t)domain) continue;
+    if (gpu_id != kNoGpuId && d.gpu_id == (uint32_t)gpu_id) return i;
+    if (first < 0) first = i;
+    if (unknown < 0 && !d.gpu_id) unknown = i;
   }
-  return -1;
+  // A partition at this address that is not one of the region's devices is another
+  // container's: no virtualisation for it (unless the region does not know gpu_ids).
+  return gpu_id == kNoGpuId ? first : unknown;
+}
+
+// KFD gpu_id of an amd-smi processor (kNoGpuId when unsupported).
+uint64_t amdsmi_gpu_id(amdsmi_processor_handle h) {
+  VGPU_REAL_IMPL(amdsmi_get_gpu_kfd_info, "libamd_smi", nullptr);
+  amdsmi_kfd_info_t k;
+  memset(&k, 0, sizeof(k));
+  if (!real_amdsmi_get_gpu_kfd_info || real_amdsmi_get_gpu_kfd_info(h, &k) != AMDSMI_STATUS_SUCCESS) return kNoGpuId;
+  return k.kfd_id == 0xFFFFFFFFFFFFFFFFull ? kNoGpuId : k.kfd_id;
 }
 
 uint64_t virt_total(int dev, uint64_t real_total) {
@@ -63,13 +82,25 @@ uint64_t virt_used(int dev) {
   return r->dev[dev].used.load();
 }
 
+// Whether several of the region's devices sit at PCI address `b` (compute partitions).
+bool shared_bdf(amdsmi_bdf_t b) {
+  if (!shim_attach_region_only()) return false;
+  const Region* r = shim().region.raw();
+  int n = 0;
+  for (int i = 0; i < kMaxDevices; i++) {
+    const DeviceState& d = r->dev[i];
+    n += d.configured && d.bdf == (uint32_t)(b.as_uint & 0xffff) && d.domain == (uint32_t)(b.as_uint >> 16);
+  }
+  return n > 1;
+}
+
 int amdsmi_dev(amdsmi_processor_handle h) {
   VGPU_REAL_IMPL(amdsmi_get_gpu_device_bdf, "libamd_smi", nullptr);
   if (!real_amdsmi_get_gpu_device_bdf) return -1;
   amdsmi_bdf_t b;
   b.as_uint = 0;
   if (real_amdsmi_get_gpu_device_bdf(h, &b) != AMDSMI_STATUS_SUCCESS) return -1;
-  return device_by_bdf(b.as_uint >> 16, (uint32_t)(b.as_uint & 0xffff));
+  return device_by_bdf(b.as_uint >> 16, (uint32_t)(b.as_uint & 0xffff), shared_bdf(b) ? amdsmi_gpu_id(h) : kNoGpuId);
 }
 
 // The container's GPUs as (domain, bdfid) pairs: VGPU_DEVICE_BDFS from the plugin
@@ -77,6 +108,7 @@ int amdsmi_dev(amdsmi_processor_handle h) {
 struct Bdf {
   uint64_t domain;
   uint32_t bdfid;
+  uint64_t gpu_id = kNoGpuId;  // KFD gpu_id when known (partitions share an address)
 };
 
 std::vector<Bdf> visible_bdfs() {
@@ -97,12 +129,25 @@ std::vector<Bdf> visible_bdfs() {
       }
       while (*p == ',' || *p == ' ') p++;
     }
+    // VGPU_DEVICE_GPU_IDS: the KFD gpu_ids of the same devices, in the same order.
+    if (const char* g = getenv("VGPU_DEVICE_GPU_IDS")) {
+      size_t i = 0;
+      for (const char* q = g; *q && i < out.size();) {
+        char* end = nullptr;
+        unsigned long long v = strtoull(q, &end, 10);
+        if (end == q) break;
+        out[i++].gpu_id = v;
+        q = end;
+        while (*q == ',' || *q == ' ') q++;
+      }
+    }
     return out;
   }
   if (!attached) return out;
   const Region* r = shim().region.raw();
   for (int i = 0; i < kMaxDevices; i++)
-    if (r->dev[i].configured) out.push_back({r->dev[i].domain, r->dev[i].bdf});
+    if (r->dev[i].configured)
+      out.push_back({r->dev[i].domain, r->dev[i].bdf, r->dev[i].gpu_id ? r->dev[i].gpu_id : kNoGpuId});
   return out;
 }
 
@@ -112,8 +157,17 @@ bool amdsmi_visible(amdsmi_processor_handle h, const std::vector<Bdf>& vis) {
   amdsmi_bdf_t b;
   b.as_uint = 0;
   if (real_amdsmi_get_gpu_device_bdf(h, &b) != AMDSMI_STATUS_SUCCESS) return true;  // not a GPU: keep
-  for (const Bdf& v : vis)
-    if (v.domain == (b.as_uint >> 16) && v.bdfid == (uint32_t)(b.as_uint & 0xffff)) return true;
+  uint64_t gid = kNoGpuId;
+  bool asked = false;
+  for (const Bdf& v : vis) {
+    if (v.domain != (b.as_uint >> 16) || v.bdfid != (uint32_t)(b.as_uint & 0xffff)) continue;
+    if (v.gpu_id == kNoGpuId) return true;
+    if (!asked) {
+      gid = amdsmi_gpu_id(h);
+      asked = true;
+    }
+    if (gid == kNoGpuId || gid == v.gpu_id) return true;  // partition of this container's GPU
+  }
   return false;
 }
 
@@ -122,7 +176,11 @@ int rsmi_dev(uint32_t idx) {
   if (!real_rsmi_dev_pci_id_get) return -1;
   uint64_t id = 0;
   if (real_rsmi_dev_pci_id_get(idx, &id) != RSMI_STATUS_SUCCESS) return -1;
-  return device_by_bdf(id >> 32, (uint32_t)(id & 0xffff));
+  // rocm_smi's "GUID" is the KFD gpu_id: it separates partitions at one PCI address.
+  VGPU_REAL_IMPL(rsmi_dev_guid_get, "librocm_smi64", nullptr);
+  uint64_t guid = kNoGpuId;
+  if (!real_rsmi_dev_guid_get || real_rsmi_dev_guid_get(idx, &guid) != RSMI_STATUS_SUCCESS) guid = kNoGpuId;
+  return device_by_bdf(id >> 32, (uint32_t)(id & 0xffff), guid);
 }
 
 void* rsmi_real(const char* name) { return resolve_real("librocm_smi64", name, nullptr); }
@@ -183,14 +241,17 @@ struct RsmiRemap {
 #include "rsmi_remap_gen.inc"
 
 // Whether `pid` (a host PID, as the SMI libraries report them) is one of this
-// container's GPU processes.
+// container's GPU processes. Only a known host PID is compared; a slot's own PID stands
+// in for it only when that PID lives in the host's namespace (no PID namespace: the two
+// are the same number). Comparing a namespaced PID with host PIDs would let an unrelated
+// process of another tenant that happens to have that number through the filter.
 bool region_has_pid(uint32_t pid) {
   const Region* r = shim().region.raw();
   for (int i = 0; i < kMaxProcs; i++) {
     int32_t p = r->procs[i].pid.load(std::memory_order_relaxed);
     if (!p) continue;
     int32_t hp = r->procs[i].hostpid.load(std::memory_order_relaxed);
-    if ((uint32_t)(hp ? hp : p) == pid) return true;
+    if (hp > 0 ? (uint32_t)hp == pid : (r->procs[i].pidns == kInitPidNs && (uint32_t)p == pid)) return true;
   }
   return false;
 }

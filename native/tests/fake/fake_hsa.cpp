@@ -13,6 +13,8 @@
 //   FAKE_ROCR_HBM       bytes of HBM per GPU (default 8 GiB)
 //   FAKE_ROCR_CUS / FAKE_ROCR_XCC / FAKE_ROCR_SE   CU layout (256 / 8 / 32 per agent)
 //   FAKE_ROCR_UUIDS     comma-separated agent UUIDs (default GPU-fa4e00000000000<i>)
+//   FAKE_ROCR_PARTS     agents per PCI address (default 1; 4 = CPX-style compute
+//                       partitions exposed as GPUs: consecutive agents share a BDF)
 //   FAKE_KFD_ROOT       fake /sys/class/kfd/kfd/proc (unset: no KFD tree)
 //   FAKE_KFD_PID_OFFSET host-PID offset (default 100000)
 // Test-only introspection: fake_rocr_* functions below.
@@ -55,7 +57,7 @@ struct FakeQueue {
 
 struct State {
   int n = 2;
-  int cus = 256, xcc = 8, se = 32;
+  int cus = 256, xcc = 8, se = 32, parts = 1;
   FakeGpu gpus[16];
   std::mutex mu;
   std::map<uintptr_t, std::pair<int, uint64_t>> allocs;  // ptr -> (dev or -1 for host, size)
@@ -97,6 +99,8 @@ void setup() {
   if (s.n < 1) s.n = 1;
   if (s.n > 16) s.n = 16;
   s.cus = (int)env_u64("FAKE_ROCR_CUS", 256);
+  s.parts = (int)env_u64("FAKE_ROCR_PARTS", 1);
+  if (s.parts < 1) s.parts = 1;
   s.xcc = (int)env_u64("FAKE_ROCR_XCC", 8);
   s.se = (int)env_u64("FAKE_ROCR_SE", 32);
   uint64_t hbm = env_u64("FAKE_ROCR_HBM", 8ull << 30);
@@ -192,7 +196,7 @@ hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* 
     case HSA_AMD_AGENT_INFO_MAX_WAVES_PER_CU: *static_cast<uint32_t*>(value) = 32; break;
     case HSA_AMD_AGENT_INFO_NEAREST_CPU: *static_cast<hsa_agent_t*>(value) = hsa_agent_t{kCpuAgent}; break;
     case HSA_AMD_AGENT_INFO_UUID: snprintf(static_cast<char*>(value), 64, "%s", s.gpus[d].uuid.c_str()); break;
-    case HSA_AMD_AGENT_INFO_BDFID: *static_cast<uint32_t*>(value) = (uint32_t)(0x05 + 0x10 * d) << 8; break;
+    case HSA_AMD_AGENT_INFO_BDFID: *static_cast<uint32_t*>(value) = (uint32_t)(0x05 + 0x10 * (d / s.parts)) << 8; break;
     case HSA_AMD_AGENT_INFO_DOMAIN: *static_cast<uint32_t*>(value) = 0; break;
     case HSA_AMD_AGENT_INFO_MEMORY_AVAIL: {
       uint64_t u = s.gpus[d].used.load();

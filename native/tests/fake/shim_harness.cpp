@@ -15,6 +15,8 @@
 //   internal=SIZE    runtime-internal device memory (bypasses every hook; negative frees)
 //   queues           CU-mask bit count, mask changes and priority of every created stream
 //   cus              the current device's CU count as the runtime sees it
+//   curlimit         the shim's vgpu_get_current_device_memory_limit (the current HIP
+//                    device mapped to its agent): {"dev": N, "limit": bytes}
 //   sleep=SECS
 //   forkmalloc=SIZE  fork; the child hipMallocs SIZE and exits normally:
 //                    {"child_malloc": "ok"|"oom"|"crash"}
@@ -245,6 +247,10 @@ int main(int argc, char** argv) {
       stop = true;
       churn.join();
       printf("{\"forkstorm\": %d}\n", ok);
+    } else if (key == "curlimit") {
+      using Lim = uint64_t (*)();
+      auto f = reinterpret_cast<Lim>(dlsym(RTLD_DEFAULT, "vgpu_get_current_device_memory_limit"));
+      printf("{\"dev\": %d, \"limit\": %llu}\n", dev, f ? (unsigned long long)f() : 0ull);
     } else if (key == "gates") {
       gates(val);
     } else if (key == "hostmalloc") {

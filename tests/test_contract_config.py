@@ -250,27 +250,60 @@ def test_reference_flag_and_env_names_accepted():
     assert c.driver_root == "/x" and c.partition_strategy == "mixed"
 
 
-def test_monitor_mode_shared_dirs_are_collected(tmp_path):
-    """Old monitor-mode container dirs are removed once no process holds their region;
-    a region with a live process, or a recent dir, is kept."""
+def _pod(uid, name, ctrs, phase="Pending", ns="ns", created="2024-01-01", init=()):
+    return pod_summary({"metadata": {"uid": uid, "name": name, "namespace": ns, "creationTimestamp": created},
+                        "spec": {"initContainers": [{"name": c, "resources": {"limits": {"amd.com/gpu": str(g)}}}
+                                                    for c, g in init],
+                                 "containers": [{"name": c, "resources": {"limits": {"amd.com/gpu": str(g)}}}
+                                                for c, g in ctrs]},
+                        "status": {"phase": phase}})
+
+
+def test_monitor_matcher_allocates_containers_one_at_a_time(tmp_path):
+    """A kubelet calls Allocate once per container: a pod with two GPU containers (and a
+    GPU init container) is matched container by container, in allocation order; a
+    restarted plugin picks up where the last one stopped through the .pod-uid markers."""
+    root = tmp_path / "shared"
+    pods = [_pod("u1", "two", [("a", 1), ("side", 0), ("b", 2)], init=[("prep", 1)])]
+    m = PodMatcher(lambda: pods, shared_root=str(root))
+    assert m.match([1]) == ["ns_two_prep"] and m.owner("ns_two_prep") == "u1"
+    assert m.match([1]) == ["ns_two_a"]
+    # the plugin restarts after the first two: the markers written by the contract tell
+    (root / "ns_two_prep").mkdir(parents=True)
+    (root / "ns_two_prep" / ".pod-uid").write_text("u1\n")
+    (root / "ns_two_a").mkdir()
+    (root / "ns_two_a" / ".pod-uid").write_text("u1\n")
+    m2 = PodMatcher(lambda: pods, shared_root=str(root))
+    assert m2.match([2]) == ["ns_two_b"]
+    with pytest.raises(LookupError):
+        m2.match([1])
+    # a re-created pod of the same name (new UID) is not confused with the old markers
+    again = [_pod("u2", "two", [("a", 1), ("side", 0), ("b", 2)], init=[("prep", 1)])]
+    assert PodMatcher(lambda: again, shared_root=str(root)).match([1]) == ["ns_two_prep"]
+
+
+def test_monitor_mode_shared_dirs_follow_the_pod_list(tmp_path):
+    """Directories go when their pod is gone (or terminal, or re-created under the same
+    name), never because they are old or their region is idle; no pod list, no GC."""
     import time
 
     from amdvgpu.plugin.contract import gc_shared_dirs
-    from amdvgpu.shim.region import Region
     root = tmp_path / "shared"
     now = time.time()
     old = now - 3 * 24 * 3600
-    for tag in ("ns_done_main", "ns_running_main", "ns_fresh_main"):
+    for tag, uid in (("ns_idle_main", "u-idle"), ("ns_gone_main", "u-gone"), ("ns_done_main", "u-done"),
+                     ("ns_again_main", "u-old"), ("ns_fresh_main", "u-fresh")):
         (root / tag).mkdir(parents=True)
-        r = Region(str(root / tag / "a.cache"), create=True)
-        if tag == "ns_running_main":
-            r.register(os.getpid())
-        r.close()
-    for tag in ("ns_done_main", "ns_running_main"):
-        os.utime(root / tag / "a.cache", (old, old))
-        os.utime(root / tag, (old, old))
-    assert gc_shared_dirs(str(root), now=now) == ["ns_done_main"]
-    assert sorted(os.listdir(root)) == ["ns_fresh_main", "ns_running_main"]
+        (root / tag / ".pod-uid").write_text(uid + "\n")
+        if tag != "ns_fresh_main":
+            os.utime(root / tag, (old, old))
+    pods = [_pod("u-idle", "idle", [("main", 1)], phase="Running"),
+            _pod("u-done", "done", [("main", 1)], phase="Succeeded"),
+            _pod("u-new", "again", [("main", 1)], phase="Running")]
+    assert gc_shared_dirs(str(root), None, now=now) == []
+    removed = gc_shared_dirs(str(root), pods, now=now)
+    assert sorted(removed) == ["ns_again_main", "ns_done_main", "ns_gone_main"]
+    assert sorted(os.listdir(root)) == ["ns_fresh_main", "ns_idle_main"]
 
 
 def test_placement_duplicate_and_host_memory_flags():

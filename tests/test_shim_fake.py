@@ -316,3 +316,50 @@ def test_hip_device_order_differs_from_agent_order(fake):
     runs = [o for o in out if "run" in o]
     assert abs(runs[0]["busy_frac"] - 0.20) <= 0.05, runs   # HIP 0 = agent 1 (limited)
     assert runs[1]["busy_frac"] > 0.75, runs                # HIP 1 = agent 0 (unlimited)
+
+
+def test_missing_region_directory_is_recreated(fake, tmp_path):
+    """A monitor-mode host directory removed under a running pod: the next process
+    recreates it and is still limited."""
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
+    e["VGPU_SHARED_CACHE"] = str(tmp_path / "gone" / "ns_pod_main" / "r.cache")
+    out = run(e, "malloc=512m", "malloc=768m")
+    assert [o["malloc"] for o in out if "malloc" in o] == ["ok", "oom"]
+    assert os.path.exists(e["VGPU_SHARED_CACHE"])
+
+
+@pytest.mark.parametrize("fail_open,want", [(None, ["oom"]), ("1", ["ok"])])
+def test_unattachable_region_fails_closed(fake, fail_open, want):
+    """With limits configured and no region, device memory is refused (the tenant must not
+    run unlimited); VGPU_FAIL_OPEN=1 restores the pass-through."""
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
+    e["VGPU_SHARED_CACHE"] = "/proc/vgpu-no-such-dir/r.cache"
+    if fail_open:
+        e["VGPU_FAIL_OPEN"] = fail_open
+    out = run(e, "malloc=1m")
+    assert [o["malloc"] for o in out if "malloc" in o] == want
+
+
+@pytest.mark.parametrize("parts", [1, 4])
+def test_eight_agents_reordered_by_hip_visible_devices(fake, parts):
+    """An 8-GPU node (or 2 GPUs x 4 compute partitions sharing one PCI address each):
+    HIP_VISIBLE_DEVICES reorders and hides agents, and the shim's HIP device -> agent map
+    follows it - by PCI address when unique, by the visible list when partitions share
+    one - for the per-device control API and the per-device temporal limiter."""
+    limits = {f"VGPU_DEVICE_MEMORY_LIMIT_{i}": f"{i + 1}g" for i in range(8)}
+    e = fake(gpus=8, **limits)
+    e.update(FAKE_ROCR_PARTS=str(parts), HIP_VISIBLE_DEVICES="6,1,3")
+    out = run(e, "dev=0", "curlimit", "dev=1", "curlimit", "dev=2", "curlimit")
+    got = [o["limit"] for o in out if "limit" in o]
+    assert got == [7 * GiB, 2 * GiB, 4 * GiB], got
+
+
+def test_partition_temporal_limit_follows_the_visible_list(fake):
+    """Only agent 5 is limited (20 %, temporal); with CPX-style partitions sharing PCI
+    addresses and HIP_VISIBLE_DEVICES=5,2 the limit lands on HIP device 0 only."""
+    e = fake(gpus=8, VGPU_DEVICE_CU_LIMIT_5="20", VGPU_CU_MODE="temporal", VGPU_DEVICE_MEMORY_LIMIT_5="4g")
+    e.update(FAKE_ROCR_PARTS="4", HIP_VISIBLE_DEVICES="5,2")
+    out = run(e, "dev=1", "stream", "run=2000,1.5", "dev=0", "stream", "run=2000,3", timeout=120)
+    runs = [o for o in out if "run" in o]
+    assert runs[0]["busy_frac"] > 0.75, runs
+    assert abs(runs[1]["busy_frac"] - 0.20) <= 0.05, runs
