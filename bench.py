@@ -388,7 +388,7 @@ def main(argv=None):
     uuid = devices[local].uuid
     base_port = int(os.environ.get("MASTER_PORT", 29500))
     modes = [m for m in args.modes.split(",") if m]
-    results, contracts = {}, {}
+    results, contracts, applied = {}, {}, {}
     port = base_port + 1
     for mode in modes:
         if mode == "native":
@@ -399,8 +399,16 @@ def main(argv=None):
             with NodeHarness(backend, device_split_count=split, device_memory_scaling=scaling,
                              cu_mode=args.cu_mode) as node:
                 env, contracts[mode] = pod_env(node, node.vgpu_ids(uuid)[:1], extra)
+                applied[mode] = {k: env.get(k) for k in ("ROCR_VISIBLE_DEVICES", "VGPU_SHARED_CACHE", "VGPU_ALLOWLIST",
+                                                         "VGPU_LOCK_FILE", "VGPU_DEVICE_MAP")}
+                applied[mode]["node_dir"] = node.dir
                 results[mode] = run_one(args, mode, env, port)
         port += 1
+    if cpu and os.environ.get("VGPU_BENCH_CONTRACT_DIR"):
+        # Rehearsal evidence: every rank's pods, as the container runtime would see them
+        # (tests/test_bench_contract.py checks that the ranks' node harnesses never collide).
+        with open(os.path.join(os.environ["VGPU_BENCH_CONTRACT_DIR"], f"rank{rank}.json"), "w") as f:
+            json.dump({"rank": rank, "local_rank": local, "uuid": uuid, "pods": applied}, f)
     rccl = None
     if world > 1 and args.rccl_probe:
         # an all-reduce between vGPUs of different GPUs must run at the native

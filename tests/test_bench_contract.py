@@ -1,5 +1,7 @@
-"""bench.py's multi-rank orchestration, rehearsed on CPU with gloo (world_size 2): the
-driver launches it under torch.distributed.run exactly like this on an 8-GPU node."""
+"""bench.py's multi-rank orchestration, rehearsed on CPU with gloo (world_size 2, 4 and
+8): the driver launches it under torch.distributed.run exactly like this on an 8-GPU
+node. Each rank runs its own plugin + stub kubelet (NodeHarness) for its GPU; the ranks'
+sockets, region files, allow-lists and lock files must never collide."""
 import json
 import os
 import socket
@@ -20,13 +22,14 @@ def free_port():
 
 
 @pytest.mark.slow
-def test_bench_two_ranks_cpu_rehearsal():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_multi_rank_cpu_rehearsal(world, tmp_path):
     port = free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu-rehearsal"]
-    env = dict(os.environ, OMP_NUM_THREADS="2")
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+           "--gpus", str(world), "--steps", "2", "--warmup", "1", "--cpu-rehearsal"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", VGPU_BENCH_CONTRACT_DIR=str(tmp_path))
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=REPO)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout  # only rank 0 prints
@@ -34,9 +37,21 @@ def test_bench_two_ranks_cpu_rehearsal():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config"):
         assert k in r, k
-    assert r["n_gpus"] == 2 and r["steps"] == 2 and r["warmup"] == 1
-    assert r["config"]["global_batch"] == 100 and r["config"]["model"] == "ResNet-V2-50"
+    assert r["n_gpus"] == world and r["steps"] == 2 and r["warmup"] == 1
+    assert r["config"]["global_batch"] == 50 * world and r["config"]["model"] == "ResNet-V2-50"
     assert "overhead_pct_quota_only" in r and "entitlement_ratio" in r and "parity_split2_mem1.8" in r
     assert r["dtype"] == "fp32" and r["config"]["vgpu"]["cu_limit_pct"] == 25
     rc = r["rccl_allreduce_between_pods"]
     assert rc["native"]["ok"] and rc["vgpu"]["ok"] and "vgpu_vs_native_busbw" in rc, rc
+    ranks = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(world)]
+    assert sorted(x["local_rank"] for x in ranks) == list(range(world))
+    assert len({x["uuid"] for x in ranks}) == world  # one GPU per rank
+    pods = [(x["uuid"], pod) for x in ranks for pod in x["pods"].values()]
+    assert len(pods) == 3 * world  # vgpu, quota, parity
+    for uuid, pod in pods:
+        assert pod["ROCR_VISIBLE_DEVICES"] == uuid and pod["VGPU_DEVICE_MAP"] == f"0:{uuid}"
+    for key in ("VGPU_SHARED_CACHE", "VGPU_ALLOWLIST", "node_dir"):
+        vals = [pod[key] for _u, pod in pods]
+        assert None not in vals and len(set(vals)) == len(vals), key
+    locks = {x["uuid"]: {pod["VGPU_LOCK_FILE"] for pod in x["pods"].values()} for x in ranks}
+    assert len({lf for s in locks.values() for lf in s}) == 3 * world  # one per plugin instance
