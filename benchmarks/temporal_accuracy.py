@@ -28,13 +28,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def worker(workload, seconds, sync_every, out, go):
+def worker(workload, seconds, sync_every, out, go, batch=0):
     import torch
     if workload == "resnet50":
         from amdvgpu.models.aibench import Runner, get_case
         torch.backends.cudnn.benchmark = True
-        r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False)
-        step, items = r.step, 50
+        r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False, batch=batch or None)
+        step, items = r.step, r.batch
     else:
         from amdvgpu.ops import spin
         step, items = (lambda: spin(2048, 500)), 1
@@ -56,7 +56,7 @@ def worker(workload, seconds, sync_every, out, go):
     json.dump({"steps": n, "seconds": dt, "throughput": n * items / dt}, open(out, "w"))
 
 
-def run_tenants(workload, contracts, seconds, sync_every):
+def run_tenants(workload, contracts, seconds, sync_every, batch=0):
     """Starts len(contracts) tenants (None = native), releases them together, returns
     each one's throughput."""
     from amdvgpu.shim.launcher import apply_contract, cleanup_region
@@ -67,7 +67,7 @@ def run_tenants(workload, contracts, seconds, sync_every):
         out = os.path.join(tmp, f"t{i}.json")
         env = apply_contract(c) if c else dict(os.environ)
         cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--workload", workload, "--seconds",
-               str(seconds), "--sync-every", str(sync_every), "--out", out, "--go", go]
+               str(seconds), "--sync-every", str(sync_every), "--out", out, "--go", go, "--batch", str(batch)]
         procs.append(subprocess.Popen(cmd, env=env))
         outs.append(out)
     try:
@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--tenants", default="1,2")
     ap.add_argument("--seconds", type=float, default=4.0)
     ap.add_argument("--sync-every", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=0, help="resnet50 batch (default: the case's 50; small = light tenant)")
     ap.add_argument("--extra", default="", help="extra contract env, K=V[,K=V] (e.g. VGPU_LIMITER_WINDOW_MS=120)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
@@ -105,21 +106,22 @@ def main():
     ap.add_argument("--md-out")
     a = ap.parse_args()
     if a.worker:
-        return worker(a.workload, a.seconds, a.sync_every, a.out, a.go)
+        return worker(a.workload, a.seconds, a.sync_every, a.out, a.go, a.batch)
     from amdvgpu.shim.launcher import vgpu_env
-    native = run_tenants(a.workload, [None], a.seconds, a.sync_every)[0]
+    native = run_tenants(a.workload, [None], a.seconds, a.sync_every, a.batch)[0]
     print(json.dumps({"native": native}), flush=True)
     rows = []
     for n in [int(x) for x in a.tenants.split(",")]:
         for lim in [int(x) for x in a.limits.split(",")]:
             extra = dict(kv.split("=", 1) for kv in a.extra.split(",") if kv)
             cs = [vgpu_env(cu_limit=lim, cu_mode="temporal", mem_limit=64 << 30, extra=extra) for _ in range(n)]
-            got = run_tenants(a.workload, cs, a.seconds, a.sync_every)
+            got = run_tenants(a.workload, cs, a.seconds, a.sync_every, a.batch)
             ach = [100.0 * g / native for g in got]
             rows.append({"tenants": n, "limit_pct": lim, "throughput": got, "achieved_pct": ach,
                          "max_error_pts": max(abs(x - lim) for x in ach)})
             print(json.dumps(rows[-1]), flush=True)
-    md = [f"# temporal limit accuracy — {a.workload} (native {native:.1f}/s, {a.seconds:.0f} s per point)", "",
+    label = a.workload + (f" b={a.batch}" if a.batch else "") + (f" [{a.extra}]" if a.extra else "")
+    md = [f"# temporal limit accuracy — {label} (native {native:.1f}/s, {a.seconds:.0f} s per point)", "",
           "| tenants | limit % | achieved % (per tenant) | max error (pts) |", "|---|---|---|---|"]
     for r in rows:
         md.append(f"| {r['tenants']} | {r['limit_pct']} | {' / '.join(f'{x:.1f}' for x in r['achieved_pct'])} | "

@@ -46,6 +46,13 @@ enum class SpillPolicy : int {
   kLargeFirst = 1,  // large allocations spill first; a reserve of the share stays for small ones
 };
 
+// How the temporal limiter charges a container that shares the GPU (VGPU_CHARGE_MODEL).
+enum class ChargeModel : int {
+  kShare = 0,     // wall time x its share of the resident waves (processor sharing)
+  kProgress = 1,  // at least wall time x its waves relative to its own recent peak: a
+                  // tenant that co-runs without losing occupancy pays what it would alone
+};
+
 // GPU_CORE_UTILIZATION_POLICY analogue.
 enum class CuPolicy : int { kDefault = 0, kForce = 1, kDisable = 2 };
 
@@ -80,6 +87,7 @@ struct Config {
   int util_sample_us = 1000;             // temporal-mode occupancy sampling interval
   int sample_read_budget = 32;           // node-wide occupancy reads per interval (ratelimit.h)
   int limiter_window_ms = 40;            // temporal-mode credit window (ratelimit.h)
+  ChargeModel charge_model = ChargeModel::kShare;  // VGPU_CHARGE_MODEL: share | progress
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
   uint64_t host_mem_limit = 0;           // VGPU_HOST_MEMORY_LIMIT: pinned host memory, 0 = unlimited

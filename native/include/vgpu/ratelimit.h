@@ -60,6 +60,21 @@ inline bool timeshare_gate(bool open, int64_t credit, const TimeShareParams& p) 
 // resident waves (CUs' worth) on the device. mine <= 0 → 0; total < mine → total = mine.
 int64_t timeshare_charge(int64_t dt_ns, int64_t mine, int64_t total);
 
+// Progress-floor charge fraction (per mille) of a sample: the share `share_pm`, raised to
+// the container's occupancy relative to `ref` - its own recent peak occupancy, i.e. what
+// it holds when nothing slows it down. Tenants that co-run without losing occupancy (two
+// light inference pods) then pay what they would pay alone instead of 1/k of it each;
+// tenants that crowd each other out (occupancy drops to ~1/k of the peak) pay their
+// share as before. Alone, the share is already 1000.
+int timeshare_progress_pm(int share_pm, int64_t mine, int64_t ref);
+
+// Decaying peak of a container's occupancy: max(mine, ref - ref/2048) per sample (a
+// half-life of ~1400 samples, seconds at the sampler's rate).
+inline int64_t occupancy_ref_update(int64_t ref, int64_t mine) {
+  const int64_t decayed = ref - (ref >> 11);
+  return mine > decayed ? mine : decayed;
+}
+
 // GPU time of an interval estimated from the charge fractions (per mille, 0..1000) at
 // its two end samples: trapezoid rule, except that an interval which began with the
 // gate re-opening (credit crossed above zero at the previous sample, so the container's

@@ -273,6 +273,11 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   if (parse_int(getenv_fn("VGPU_SAMPLE_READ_BUDGET"), 0, 1 << 20, &budget)) cfg->sample_read_budget = (int)budget;
   long window = 40;
   if (parse_int(getenv_fn("VGPU_LIMITER_WINDOW_MS"), 5, 2000, &window)) cfg->limiter_window_ms = (int)window;
+  if (const char* s = getenv_fn("VGPU_CHARGE_MODEL")) {
+    if (!strcasecmp(s, "share")) cfg->charge_model = ChargeModel::kShare;
+    else if (!strcasecmp(s, "progress")) cfg->charge_model = ChargeModel::kProgress;
+    else VLOG_WARN("invalid VGPU_CHARGE_MODEL=%s ignored", s);
+  }
   if (const char* s = getenv_fn("VGPU_LOCK_FILE")) {
     if (*s) cfg->lock_file = s;
   }

@@ -30,6 +30,12 @@ int64_t timeshare_charge(int64_t dt_ns, int64_t mine, int64_t total) {
   return dt_ns * mine / total;
 }
 
+int timeshare_progress_pm(int share_pm, int64_t mine, int64_t ref) {
+  if (mine <= 0 || ref <= 0) return share_pm;
+  const int64_t rel = mine >= ref ? 1000 : mine * 1000 / ref;
+  return rel > share_pm ? (int)rel : share_pm;
+}
+
 int64_t timeshare_interval(int64_t dt_ns, int prev_pm, int now_pm, bool gate_opened_at_prev) {
   if (dt_ns <= 0) return 0;
   if (gate_opened_at_prev && prev_pm == 0) return dt_ns * now_pm / 1000;

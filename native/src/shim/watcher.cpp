@@ -116,6 +116,7 @@ struct Sampler {
   int unknown = 0;                        // container processes whose host PID is unknown
   std::vector<int> others[kMaxDevices];   // other processes on each GPU
   int prev_pm[kMaxDevices] = {};          // charge fraction at the previous sample
+  int64_t occ_ref[kMaxDevices] = {};      // decaying peak of the container's occupancy
   bool opened[kMaxDevices] = {};          // the previous sample re-opened the gate
   int procs = 1;                          // processes on the busiest sampled GPU (period)
 };
@@ -165,6 +166,8 @@ void sample_tick(Region* r, Sampler& sm) {
         r->hdr.other_refreshes.fetch_add(1, std::memory_order_relaxed);
       }
       pm = (int)timeshare_charge(1000, mine, total);
+      sm.occ_ref[d] = occupancy_ref_update(sm.occ_ref[d], mine);
+      if (config().charge_model == ChargeModel::kProgress) pm = timeshare_progress_pm(pm, mine, sm.occ_ref[d]);
     } else if (sm.unknown) {
       // No host PID known yet: fall back to device-wide busy time (conservative).
       int busy = device_busy_percent(a.gpu_id);

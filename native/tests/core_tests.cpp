@@ -642,6 +642,17 @@ static void test_ratelimit() {
   CHECK_EQ(timeshare_charge(1000000, 64, 64), 1000000);
   CHECK_EQ(timeshare_charge(900000, 10, 30), 300000);
   CHECK_EQ(timeshare_charge(1000000, 50, 10), 1000000);  // total below mine: alone
+  // Progress floor: co-running at full own occupancy pays what it would alone; crowded
+  // down to a third of its peak it pays the share (here larger); no reference: the share.
+  CHECK_EQ(timeshare_progress_pm(500, 40, 40), 1000);
+  CHECK_EQ(timeshare_progress_pm(500, 30, 40), 750);
+  CHECK_EQ(timeshare_progress_pm(400, 10, 30), 400);
+  CHECK_EQ(timeshare_progress_pm(400, 10, 0), 400);
+  CHECK_EQ(timeshare_progress_pm(0, 0, 40), 0);
+  // The occupancy reference follows peaks at once and decays slowly (1/2048 per sample).
+  CHECK_EQ(occupancy_ref_update(0, 64), 64);
+  CHECK_EQ(occupancy_ref_update(4096, 0), 4094);
+  CHECK_EQ(occupancy_ref_update(4096, 5000), 5000);
   // Credit arithmetic and clamps.
   TimeShareParams p = timeshare_params(25);
   CHECK_EQ(p.burst_ns, 10000000);
