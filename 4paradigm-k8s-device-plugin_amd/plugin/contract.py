@@ -47,6 +47,47 @@ LOCK_FILE = "hostpid.lock"
 CONTAINER_LOCK_DIR = "/usr/local/vgpu/lock"
 
 
+# Node-wide board (native/include/vgpu/board.h): every container reads every slot (the
+# directory is mounted read-only) and writes only its own (its slot file is mounted
+# read-write on top). Task-priority classes act on it: a background container yields GPU
+# time to busy containers of higher priority.
+BOARD_HOST_DIR = "board"
+CONTAINER_BOARD_DIR = "/usr/local/vgpu/board"
+BOARD_MAX_AGE_S = 7 * 24 * 3600
+
+
+def ensure_board_dir(vgpu_dir):
+    d = os.path.join(vgpu_dir, BOARD_HOST_DIR)
+    os.makedirs(d, mode=0o755, exist_ok=True)
+    return d
+
+
+def board_slot(vgpu_dir, name):
+    """Creates this container's slot file (world-writable: the container's processes may
+    run as any user; only this container mounts it read-write). Returns its path, or None
+    when there is no board directory. Slots untouched for a week are removed."""
+    d = os.path.join(vgpu_dir, BOARD_HOST_DIR)
+    if not os.path.isdir(d):
+        return None
+    path = os.path.join(d, name + ".slot")
+    try:
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o666)
+        os.close(fd)
+        os.chmod(path, 0o666)
+    except OSError:
+        return None
+    try:
+        import time
+        now = time.time()
+        for fn in os.listdir(d):
+            fp = os.path.join(d, fn)
+            if fn.endswith(".slot") and now - os.path.getmtime(fp) > BOARD_MAX_AGE_S:
+                os.unlink(fp)
+    except OSError:
+        pass
+    return path
+
+
 def ensure_lock_file(vgpu_dir):
     """Creates <vgpu_dir>/lock/hostpid.lock (0644) if missing; returns its path."""
     d = os.path.join(vgpu_dir, LOCK_HOST_DIR)
@@ -272,6 +313,13 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
     else:
         resp.mounts.add(container_path=CONTAINER_ALLOWLIST_DIR, host_path=os.path.join(vdir, "allowlist"),
                         read_only=True)
+    slot = board_slot(vdir, cache_name.rsplit(".", 1)[0])
+    if slot:
+        resp.mounts.add(container_path=CONTAINER_BOARD_DIR, host_path=os.path.dirname(slot), read_only=True)
+        resp.mounts.add(container_path=f"{CONTAINER_BOARD_DIR}/{os.path.basename(slot)}", host_path=slot,
+                        read_only=False)
+        resp.envs["VGPU_BOARD_DIR"] = CONTAINER_BOARD_DIR
+        resp.envs["VGPU_BOARD_SLOT"] = os.path.basename(slot)
     lock_file = os.path.join(vdir, LOCK_HOST_DIR, LOCK_FILE)
     if os.path.isfile(lock_file):
         resp.mounts.add(container_path=f"{CONTAINER_LOCK_DIR}/{LOCK_FILE}", host_path=lock_file, read_only=True)

@@ -22,7 +22,7 @@ import time
 from .. import __version__
 from ..utils.log import get_logger
 from .config import parse_config
-from .contract import ensure_lock_file
+from .contract import ensure_board_dir, ensure_lock_file
 from .devices import FakeBackend, detect_backend
 from .legacy import LegacyController
 from .strategy import plugins_for
@@ -112,8 +112,9 @@ class Supervisor:
         os.makedirs(cfg.device_plugin_path, exist_ok=True)
         try:
             ensure_lock_file(cfg.vgpu_dir)
+            ensure_board_dir(cfg.vgpu_dir)
         except OSError as e:
-            log.warning("cannot create the host-PID lock file under %s: %s", cfg.vgpu_dir, e)
+            log.warning("cannot create the host-PID lock file / board under %s: %s", cfg.vgpu_dir, e)
         self._fs = FSWatcher(cfg.device_plugin_path.rstrip("/"), self.events)
         if self.install_signals and threading.current_thread() is threading.main_thread():
             self._os = OSWatcher(self.events)

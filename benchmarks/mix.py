@@ -6,16 +6,21 @@ share one GPU, each in its own vGPU of a split-N plugin (default --cu-mode auto)
 a real node is shared: a small-batch inference service next to training jobs.
 
 For every pod the benchmark reports
-  * its throughput when alone in its vGPU ("solo at share": the same contract, so the
-    same CU share / quota, with the GPU otherwise idle) and when all pods run together;
-    ``vs_entitlement`` = together / solo-at-share (>= 0.9 means the neighbours did not
-    take what the pod is entitled to);
-  * for latency pods (``:lat``), the P50 / P99 step latency (one synchronised step per
-    request), alone and together.
-Optionally a second concurrent run with task priorities (``--priority``: e.g.
-``resnet50-inf:1:lat=0,vgg16-train=2``) shows what VGPU_TASK_PRIORITY buys the latency pod.
+  * its throughput alone in its vGPU, under both enforcements auto mode uses: "solo
+    spatial" (the GPU otherwise idle: its CU slice, all the time) and "solo temporal"
+    (its share of the GPU's time on all CUs: what it is entitled to on a crowded GPU);
+  * its throughput when all pods run together; ``vs_entitlement`` = together / solo
+    temporal (>= 0.9: the neighbours did not take GPU time that is the pod's);
+  * for latency pods (``:lat``), the P50 / P99 request latency alone and together.
+    Requests arrive as a Poisson stream (``:rate=R`` per second, default 100; latency
+    counts from arrival, queueing included), so the pod idles between bursts as a service
+    does.
+Optionally a further concurrent run with task priorities (``--priority``: e.g.
+``resnet50-inf:1:lat=0,vgg16-train=2``) shows what VGPU_TASK_PRIORITY buys the latency pod:
+priority 0 keeps its CU slice however crowded the GPU, priority >= 2 (background) yields
+GPU time while a higher-priority pod is busy (the node-wide board, vgpu/board.h).
 
-Pods are given as CASE[:BATCH][:lat], e.g. the default
+Pods are given as CASE[:BATCH][:lat][:rate=R], e.g. the default
     resnet50-inf:1:lat vgg16-train lstm-train deeplab-inf
 Every contract comes from an Allocate of the plugin (NodeHarness, sysfs backend).
 
@@ -37,13 +42,15 @@ DEFAULT_PODS = ["resnet50-inf:1:lat", "vgg16-train", "lstm-train", "deeplab-inf"
 
 def parse_pod(spec):
     parts = spec.split(":")
-    case, batch, lat = parts[0], None, False
+    case, batch, lat, rate = parts[0], None, False, 100.0
     for p in parts[1:]:
         if p == "lat":
             lat = True
+        elif p.startswith("rate="):
+            rate = float(p[5:])
         elif p:
             batch = int(p)
-    return {"spec": spec, "case": case, "batch": batch, "latency": lat}
+    return {"spec": spec, "case": case, "batch": batch, "latency": lat, "rate": rate}
 
 
 def worker(a):
@@ -58,18 +65,27 @@ def worker(a):
     open(a.out + ".ready", "w").close()
     while not os.path.exists(a.go):
         time.sleep(0.005)
+    import random
+    rng = random.Random(1234)
     lat = []
     n = 0
     t0 = time.perf_counter()
+    arrival = t0
     while time.perf_counter() - t0 < a.seconds:
-        s = time.perf_counter()
-        r.step()
-        n += 1
         if a.latency:
+            # Poisson arrivals; a request that arrived while the previous one ran waits.
+            arrival += rng.expovariate(a.rate)
+            now = time.perf_counter()
+            if arrival > now:
+                time.sleep(arrival - now)
+            r.step()
             torch.cuda.synchronize()
-            lat.append(time.perf_counter() - s)
-        elif n % 2 == 0:
-            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - arrival)
+        else:
+            r.step()
+            if n % 2 == 1:
+                torch.cuda.synchronize()
+        n += 1
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     res = {"steps": n, "items": r.batch * n, "t0": t0, "t1": t1, "throughput": r.batch * n / (t1 - t0)}
@@ -82,7 +98,7 @@ def worker(a):
     return 0
 
 
-def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None):
+def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=None):
     """Starts one worker per pod (pods[i] in vGPU ids[i]), releases them together."""
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="mix-")
@@ -93,11 +109,12 @@ def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None):
         env = apply_contract(envs, mounts)
         if priorities and priorities.get(pod["spec"]) is not None:
             env["VGPU_TASK_PRIORITY"] = str(priorities[pod["spec"]])
+        env.update(pod_env or {})
         out = os.path.join(tmp, f"p{i}.json")
         cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--case", pod["case"], "--batch",
                str(pod["batch"] or 0), "--seconds", str(seconds), "--warmup", str(warmup), "--out", out, "--go", go]
         if pod["latency"]:
-            cmd.append("--latency")
+            cmd += ["--latency", "--rate", str(pod["rate"])]
         procs.append(subprocess.Popen(cmd, env=env))
         outs.append(out)
     try:
@@ -131,6 +148,7 @@ def main():
     ap.add_argument("--case")
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--latency", action="store_true")
+    ap.add_argument("--rate", type=float, default=100.0)
     ap.add_argument("--out")
     ap.add_argument("--go")
     a = ap.parse_args()
@@ -147,25 +165,30 @@ def main():
         k, _, v = item.rpartition("=")
         prio[k] = int(v)
     out = {"pods": [p["spec"] for p in pods], "split": split, "cu_mode": a.cu_mode, "seconds": a.seconds,
-           "solo": [], "together": None, "together_priority": None, "priorities": prio or None}
+           "solo": [], "solo_spatial": [], "together": None, "together_priority": None, "priorities": prio or None}
     with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode) as node:
         ids = node.vgpu_ids(uuid)[:len(pods)]
         for pod, vid in zip(pods, ids):
             t = time.time()
-            out["solo"].append(run_pods(node, uuid, [pod], [vid], a.seconds, a.warmup)[0])
-            print(f"[mix] solo {pod['spec']}: {out['solo'][-1]['throughput']:.1f}/s ({time.time() - t:.0f} s)",
+            out["solo_spatial"].append(run_pods(node, uuid, [pod], [vid], a.seconds, a.warmup)[0])
+            out["solo"].append(run_pods(node, uuid, [pod], [vid], a.seconds, a.warmup,
+                                        pod_env={"VGPU_CU_MODE": "temporal"})[0])
+            print(f"[mix] solo {pod['spec']}: {out['solo_spatial'][-1]['throughput']:.1f}/s spatial, "
+                  f"{out['solo'][-1]['throughput']:.1f}/s temporal ({time.time() - t:.0f} s)",
                   file=sys.stderr, flush=True)
         out["together"] = run_pods(node, uuid, pods, ids, a.seconds, a.warmup)
         if prio:
             out["together_priority"] = run_pods(node, uuid, pods, ids, a.seconds, a.warmup, prio)
     rows = []
     for i, pod in enumerate(pods):
-        solo, tog = out["solo"][i], out["together"][i]
-        row = {"pod": pod["spec"], "solo": round(solo["throughput"], 2), "together": round(tog["throughput"], 2),
+        solo, tog, sp = out["solo"][i], out["together"][i], out["solo_spatial"][i]
+        row = {"pod": pod["spec"], "solo_spatial": round(sp["throughput"], 2), "solo": round(solo["throughput"], 2),
+               "together": round(tog["throughput"], 2),
                "vs_entitlement": round(tog["throughput"] / solo["throughput"], 3)}
         if pod["latency"]:
-            row.update(solo_p50_ms=round(solo["p50_ms"], 3), solo_p99_ms=round(solo["p99_ms"], 3),
-                       p50_ms=round(tog["p50_ms"], 3), p99_ms=round(tog["p99_ms"], 3))
+            row.update(solo_spatial_p99_ms=round(sp["p99_ms"], 3), solo_p50_ms=round(solo["p50_ms"], 3),
+                       solo_p99_ms=round(solo["p99_ms"], 3), p50_ms=round(tog["p50_ms"], 3),
+                       p99_ms=round(tog["p99_ms"], 3))
         if out["together_priority"]:
             tp = out["together_priority"][i]
             row["prio"] = prio.get(pod["spec"], 1)
@@ -177,13 +200,16 @@ def main():
     out["rows"] = rows
     out["min_vs_entitlement"] = min(r["vs_entitlement"] for r in rows)
     md = [f"# heterogeneous pods on one MI355X (split {split}, --cu-mode {a.cu_mode}, {a.seconds:.0f} s windows)", "",
-          "| pod | solo at share | together | vs entitlement | P50 / P99 ms solo | P50 / P99 ms together |"
+          "| pod | solo spatial | solo temporal (entitlement) | together | vs entitlement | P99 ms solo spatial | "
+          "P50 / P99 ms solo temporal | P50 / P99 ms together |"
           + (" priority | together (prio) | vs entitlement (prio) | P50 / P99 ms (prio) |" if prio else ""),
-          "|---|---|---|---|---|---|" + ("---|---|---|---|" if prio else "")]
+          "|---|---|---|---|---|---|---|---|" + ("---|---|---|---|" if prio else "")]
     for r in rows:
+        lat_sp = f"{r['solo_spatial_p99_ms']:.2f}" if "p50_ms" in r else "-"
         lat_s = f"{r['solo_p50_ms']:.2f} / {r['solo_p99_ms']:.2f}" if "p50_ms" in r else "-"
         lat_t = f"{r['p50_ms']:.2f} / {r['p99_ms']:.2f}" if "p50_ms" in r else "-"
-        line = f"| {r['pod']} | {r['solo']:.1f} | {r['together']:.1f} | {r['vs_entitlement']:.2f} | {lat_s} | {lat_t} |"
+        line = (f"| {r['pod']} | {r['solo_spatial']:.1f} | {r['solo']:.1f} | {r['together']:.1f} | "
+                f"{r['vs_entitlement']:.2f} | {lat_sp} | {lat_s} | {lat_t} |")
         if prio:
             lat_p = f"{r['prio_p50_ms']:.2f} / {r['prio_p99_ms']:.2f}" if "prio_p50_ms" in r else "-"
             line += f" {r['prio']} | {r['together_prio']:.1f} | {r['vs_entitlement_prio']:.2f} | {lat_p} |"

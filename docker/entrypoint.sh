@@ -4,7 +4,8 @@
 set -euo pipefail
 SRC=${VGPU_LIB_DIR:-/opt/amd-vgpu/4paradigm-k8s-device-plugin_amd/lib}
 DEST=${VGPU_DIR:-/usr/local/vgpu}
-mkdir -p "$DEST" "$DEST/shared" "$DEST/allowlist/containers" "$DEST/lock"
+mkdir -p "$DEST" "$DEST/shared" "$DEST/allowlist/containers" "$DEST/lock" "$DEST/board"
+chmod 0755 "$DEST/board"   # node-wide board: each container writes only its own slot
 # Host-PID discovery lock: root-owned and mounted read-only into every container (flock
 # works on a read-only descriptor; tenants cannot unlink or replace it).
 [ -e "$DEST/lock/hostpid.lock" ] || : > "$DEST/lock/hostpid.lock"

@@ -1,0 +1,91 @@
+// Node-wide GPU board: what the vGPU containers of a node tell each other.
+//
+// The reference has no cross-container channel: every container's limiter works alone,
+// and its CUDA_TASK_PRIORITY is stored but never acted on. Scheduling
+// classes need one: a background container must know which busy processes on its GPU
+// belong to higher-priority containers in order to yield to them, and not to its peers.
+//
+// Layout on the node: the plugin creates <vgpu_dir>/board/ (root, 0755) and, per
+// container, one slot file <id>.slot in it. The container gets the directory read-only
+// and its own slot file read-write on top (docs/ABI.md): every container reads every
+// slot, and writes only its own - no tenant can alter what another one publishes. A
+// slot is written by the container's sampler (lease holder) and is only advice to the
+// containers that opt into yielding (background class): a tenant lying in its own slot
+// cannot take anything from a container that does not yield.
+#pragma once
+
+#include <sys/types.h>
+
+#include <atomic>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "vgpu/config.h"
+
+namespace vgpu {
+
+constexpr uint32_t kBoardMagic = 0x56424431u;  // "VBD1"
+constexpr uint32_t kBoardVersion = 1;
+constexpr int kBoardMaxPids = 256;
+
+// Scheduling classes from VGPU_TASK_PRIORITY (0 high, 1 normal, >= 2 low).
+constexpr int kPrioLatency = 0;     // <= 0: never duty-cycled by auto mode; HW queues high
+constexpr int kPrioNormal = 1;
+constexpr int kPrioBackground = 2;  // >= 2: yields GPU time to busy higher-priority tenants
+
+struct alignas(64) BoardSlot {
+  uint32_t magic;
+  uint32_t version;
+  std::atomic<uint64_t> heartbeat_ns;     // CLOCK_MONOTONIC of the last update (0 = left)
+  std::atomic<int32_t> priority;
+  int32_t ndev;
+  uint32_t gpu_id[kMaxDevices];           // KFD gpu_id of the container's devices
+  std::atomic<int32_t> npids;
+  std::atomic<int32_t> hostpids[kBoardMaxPids];
+};
+
+// Slot staleness: a slot whose heartbeat is older than this is ignored.
+constexpr uint64_t kBoardStaleNs = 2'000'000'000ull;
+
+// Another container as read from its slot.
+struct BoardPeer {
+  int priority = kPrioNormal;
+  std::vector<uint32_t> gpu_ids;
+  std::vector<int> hostpids;
+};
+
+// A container's view of the board directory: its own slot (read-write) and the others.
+class Board {
+ public:
+  Board() = default;
+  ~Board();
+  Board(const Board&) = delete;
+  Board& operator=(const Board&) = delete;
+
+  // Maps `dir`/`self_name` read-write (created if missing and the directory allows it).
+  // Returns 0 or -errno; without a board every query answers "no peers".
+  int open(const char* dir, const char* self_name);
+  bool attached() const { return self_ != nullptr; }
+  BoardSlot* self() { return self_; }
+
+  // Publishes this container's state (the sampler calls it every period).
+  void publish(int priority, const uint32_t* gpu_ids, int ndev, const std::vector<int>& hostpids, uint64_t now);
+  void leave();
+
+  // Re-reads the other slots (live ones only). Cheap enough for every 100 ms.
+  const std::vector<BoardPeer>& refresh(uint64_t now);
+  const std::vector<BoardPeer>& peers() const { return peers_; }
+
+  // Priority of the container owning host PID `pid` on GPU `gpu_id` (kPrioNormal for a
+  // process no live slot lists: an unmanaged process counts as a normal tenant).
+  int priority_of(int pid, uint32_t gpu_id) const;
+
+ private:
+  std::string dir_, self_name_;
+  BoardSlot* self_ = nullptr;
+  int fd_ = -1;
+  std::vector<BoardPeer> peers_;
+};
+
+}  // namespace vgpu

@@ -39,6 +39,11 @@ constexpr int kAutoSpatialMaxCrowd = 1;
 // The mode a device actually uses for share `pct` under configured mode `m`.
 // `crowd`: other busy processes on the GPU (-1 = unknown, treated as crowded).
 CuMode effective_cu_mode(CuMode m, int pct, int crowd = -1);
+// Auto mode with the task priority class (VGPU_TASK_PRIORITY, vgpu/board.h): the latency
+// class (<= 0) is never duty-cycled - its share stays a CU mask however crowded the GPU;
+// the background class (>= 2) runs on the GPU-time gate whenever another process keeps
+// the GPU busy (it yields to busier higher-priority tenants there), even without a limit.
+CuMode effective_cu_mode_prio(CuMode m, int pct, int crowd, int priority);
 
 // Where oversubscribed allocations live (VGPU_SPILL_POLICY).
 enum class SpillPolicy : int {
@@ -88,6 +93,8 @@ struct Config {
   int sample_read_budget = 32;           // node-wide occupancy reads per interval (ratelimit.h)
   int limiter_window_ms = 40;            // temporal-mode credit window (ratelimit.h)
   ChargeModel charge_model = ChargeModel::kShare;  // VGPU_CHARGE_MODEL: share | progress
+  std::string board_dir;                 // VGPU_BOARD_DIR: node-wide board (vgpu/board.h), "" = none
+  std::string board_slot;                // VGPU_BOARD_SLOT: this container's slot file in it
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
   uint64_t host_mem_limit = 0;           // VGPU_HOST_MEMORY_LIMIT: pinned host memory, 0 = unlimited

@@ -83,12 +83,16 @@ inline int64_t occupancy_ref_update(int64_t ref, int64_t mine) {
 // alone misses half of one at every gate-triggered start (simulated in core_tests.cpp).
 int64_t timeshare_interval(int64_t dt_ns, int prev_pm, int now_pm, bool gate_opened_at_prev);
 
-// One accounting step: credit + dt*limit/100 − charge, clamped. Pure.
-int64_t timeshare_step(int64_t credit, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns);
+// One accounting step: credit + grant_dt*limit/100 − charge, clamped. Pure. `grant_dt`
+// is the part of the interval that earns credit (dt, or 0 while a background tenant
+// yields; < 0 = dt).
+int64_t timeshare_step(int64_t credit, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns,
+                       int64_t grant_dt_ns = -1);
 
 // Applies one step to the region's device state (credit, gate, cumulative charged time
 // and the smoothed utilisation shown by vgpuctl / the monitor).
-void timeshare_apply(DeviceState& d, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns);
+void timeshare_apply(DeviceState& d, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns,
+                     int64_t grant_dt_ns = -1);
 
 // Launch-side gate. Blocks while the region's launch block is set (recent_kernel < 0,
 // every cu mode) and, when `limited`, while the device's credit is exhausted and the

@@ -1,0 +1,112 @@
+// Node-wide GPU board (see vgpu/board.h).
+#include "vgpu/board.h"
+
+#include <dirent.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "vgpu/log.h"
+
+namespace vgpu {
+
+Board::~Board() {
+  if (self_) munmap(self_, sizeof(BoardSlot));
+  if (fd_ >= 0) close(fd_);
+}
+
+int Board::open(const char* dir, const char* self_name) {
+  if (!dir || !*dir || !self_name || !*self_name || strchr(self_name, '/')) return -EINVAL;
+  dir_ = dir;
+  self_name_ = self_name;
+  const std::string path = dir_ + "/" + self_name_;
+  int fd = ::open(path.c_str(), O_RDWR | O_CLOEXEC);
+  if (fd < 0 && errno == ENOENT) fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+  if (fd < 0) return -errno;
+  // Size by lseek (fstat is GLIBC_2.33, glibc_compat.h); a short slot is extended.
+  const off_t size = lseek(fd, 0, SEEK_END);
+  if (size < (off_t)sizeof(BoardSlot) && ftruncate(fd, sizeof(BoardSlot)) != 0) {
+    int e = errno;
+    ::close(fd);
+    return -e;
+  }
+  void* p = mmap(nullptr, sizeof(BoardSlot), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (p == MAP_FAILED) {
+    int e = errno;
+    ::close(fd);
+    return -e;
+  }
+  self_ = static_cast<BoardSlot*>(p);
+  fd_ = fd;
+  if (self_->magic != kBoardMagic || self_->version != kBoardVersion) {
+    memset(static_cast<void*>(self_), 0, sizeof(BoardSlot));
+    self_->version = kBoardVersion;
+    std::atomic_thread_fence(std::memory_order_release);
+    self_->magic = kBoardMagic;
+  }
+  return 0;
+}
+
+void Board::publish(int priority, const uint32_t* gpu_ids, int ndev, const std::vector<int>& hostpids, uint64_t now) {
+  if (!self_) return;
+  self_->priority.store(priority, std::memory_order_relaxed);
+  ndev = std::max(0, std::min(ndev, kMaxDevices));
+  for (int i = 0; i < ndev; i++) self_->gpu_id[i] = gpu_ids[i];
+  self_->ndev = ndev;
+  const int n = std::min((int)hostpids.size(), kBoardMaxPids);
+  for (int i = 0; i < n; i++) self_->hostpids[i].store(hostpids[i], std::memory_order_relaxed);
+  self_->npids.store(n, std::memory_order_release);
+  self_->heartbeat_ns.store(now, std::memory_order_release);
+}
+
+void Board::leave() {
+  if (self_) self_->heartbeat_ns.store(0, std::memory_order_release);
+}
+
+const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
+  peers_.clear();
+  if (dir_.empty()) return peers_;
+  DIR* d = opendir(dir_.c_str());
+  if (!d) return peers_;
+  while (struct dirent* e = readdir(d)) {
+    const size_t len = strlen(e->d_name);
+    if (len < 6 || strcmp(e->d_name + len - 5, ".slot") != 0 || self_name_ == e->d_name) continue;
+    const std::string path = dir_ + "/" + e->d_name;
+    int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) continue;
+    BoardSlot s;
+    // A plain read of a slot another container keeps rewriting: fields may be torn, so
+    // every value is bounds-checked and the heartbeat decides liveness.
+    const ssize_t got = pread(fd, static_cast<void*>(&s), sizeof(s), 0);
+    ::close(fd);
+    if (got != (ssize_t)sizeof(s) || s.magic != kBoardMagic || s.version != kBoardVersion) continue;
+    const uint64_t hb = s.heartbeat_ns.load(std::memory_order_relaxed);
+    if (!hb || hb > now + kBoardStaleNs || now - hb > kBoardStaleNs) continue;
+    BoardPeer p;
+    p.priority = s.priority.load(std::memory_order_relaxed);
+    const int ndev = std::max(0, std::min(s.ndev, kMaxDevices));
+    p.gpu_ids.assign(s.gpu_id, s.gpu_id + ndev);
+    const int n = std::max(0, std::min(s.npids.load(std::memory_order_relaxed), kBoardMaxPids));
+    for (int i = 0; i < n; i++) {
+      const int pid = s.hostpids[i].load(std::memory_order_relaxed);
+      if (pid > 0) p.hostpids.push_back(pid);
+    }
+    peers_.push_back(std::move(p));
+  }
+  closedir(d);
+  return peers_;
+}
+
+int Board::priority_of(int pid, uint32_t gpu_id) const {
+  for (const BoardPeer& p : peers_) {
+    if (std::find(p.gpu_ids.begin(), p.gpu_ids.end(), gpu_id) == p.gpu_ids.end()) continue;
+    if (std::find(p.hostpids.begin(), p.hostpids.end(), pid) != p.hostpids.end()) return p.priority;
+  }
+  return kPrioNormal;
+}
+
+}  // namespace vgpu

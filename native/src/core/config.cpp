@@ -44,6 +44,14 @@ CuMode effective_cu_mode(CuMode m, int pct, int crowd) {
   return crowd >= 0 && crowd <= kAutoSpatialMaxCrowd ? CuMode::kSpatial : CuMode::kTemporal;
 }
 
+CuMode effective_cu_mode_prio(CuMode m, int pct, int crowd, int priority) {
+  const CuMode base = effective_cu_mode(m, pct, crowd);
+  if (m != CuMode::kAuto) return base;
+  if (priority <= 0) return CuMode::kSpatial;
+  if (priority >= 2 && crowd != 0) return CuMode::kTemporal;
+  return base;
+}
+
 uint64_t spill_reserve(const Config& cfg, uint64_t hbm_share) {
   if (cfg.spill_reserve_bytes) return cfg.spill_reserve_bytes;
   const uint64_t floor = std::min<uint64_t>(2ull << 30, hbm_share / 4);
@@ -278,6 +286,8 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
     else if (!strcasecmp(s, "progress")) cfg->charge_model = ChargeModel::kProgress;
     else VLOG_WARN("invalid VGPU_CHARGE_MODEL=%s ignored", s);
   }
+  if (const char* s = getenv_fn("VGPU_BOARD_DIR")) cfg->board_dir = s;
+  if (const char* s = getenv_fn("VGPU_BOARD_SLOT")) cfg->board_slot = s;
   if (const char* s = getenv_fn("VGPU_LOCK_FILE")) {
     if (*s) cfg->lock_file = s;
   }

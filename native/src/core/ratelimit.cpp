@@ -42,18 +42,21 @@ int64_t timeshare_interval(int64_t dt_ns, int prev_pm, int now_pm, bool gate_ope
   return dt_ns * (prev_pm + now_pm) / 2000;
 }
 
-int64_t timeshare_step(int64_t credit, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns) {
+int64_t timeshare_step(int64_t credit, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns,
+                       int64_t grant_dt_ns) {
   if (dt_ns < 0) dt_ns = 0;
+  if (grant_dt_ns < 0 || grant_dt_ns > dt_ns) grant_dt_ns = dt_ns;
   int pct = p.limit_pct > 0 && p.limit_pct < 100 ? p.limit_pct : 100;
-  credit += dt_ns * pct / 100 - charge_ns;
+  credit += grant_dt_ns * pct / 100 - charge_ns;
   if (credit > p.burst_ns) credit = p.burst_ns;
   if (credit < -p.debt_ns) credit = -p.debt_ns;
   return credit;
 }
 
-void timeshare_apply(DeviceState& d, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns) {
+void timeshare_apply(DeviceState& d, const TimeShareParams& p, int64_t dt_ns, int64_t charge_ns,
+                     int64_t grant_dt_ns) {
   // Single writer (the sampler lease holder); launch gates only read the credit.
-  int64_t c = timeshare_step(d.credit_ns.load(std::memory_order_relaxed), p, dt_ns, charge_ns);
+  int64_t c = timeshare_step(d.credit_ns.load(std::memory_order_relaxed), p, dt_ns, charge_ns, grant_dt_ns);
   d.credit_ns.store(c, std::memory_order_release);
   d.gate_open.store(timeshare_gate(d.gate_open.load(std::memory_order_relaxed) != 0, c, p) ? 1 : 0,
                     std::memory_order_release);

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "real.h"
+#include "vgpu/board.h"
 #include "vgpu/devmap.h"
 #include "vgpu/kfd.h"
 #include "vgpu/log.h"
@@ -460,11 +461,15 @@ void apply_live_config() {
     const bool ranged = d.cu_range_begin >= 0;
     if (locked) s.region.unlock();
     const bool limited = pct > 0 && pct < 100;
-    const CuMode mode = effective_cu_mode(cfg.cu_mode, pct, d.crowd.load(std::memory_order_relaxed));
+    const int prio = r->hdr.priority.load(std::memory_order_relaxed);
+    const CuMode mode = effective_cu_mode_prio(cfg.cu_mode, pct, d.crowd.load(std::memory_order_relaxed), prio);
     const bool spatial = mode == CuMode::kSpatial || mode == CuMode::kBoth;
     const bool temporal = mode == CuMode::kTemporal || mode == CuMode::kBoth;
     const bool mask_on = !off && spatial && (limited || ranged) && m.count() < a.cu_count && m.count() > 0;
-    const bool temp_on = !off && temporal && (limited || force);
+    // A background tenant is gated in time even without a share: it yields to busier
+    // higher-priority tenants (watcher.cpp) and otherwise runs free.
+    const bool yields = prio >= kPrioBackground && cfg.cu_mode == CuMode::kAuto && temporal;
+    const bool temp_on = !off && temporal && (limited || force || yields);
     const bool mask_changed = mask_on != a.mask_active.load() || memcmp(m.words, a.mask.words, sizeof(m.words)) != 0;
     if (temp_on && !a.temporal_active.load() && !d.gate_open.load()) {
       d.credit_ns.store(timeshare_params(pct, cfg.limiter_window_ms).burst_ns);

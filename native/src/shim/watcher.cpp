@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "shim.h"
+#include "vgpu/board.h"
 #include "vgpu/kfd.h"
 #include "vgpu/log.h"
 #include "vgpu/ratelimit.h"
@@ -119,7 +120,33 @@ struct Sampler {
   int64_t occ_ref[kMaxDevices] = {};      // decaying peak of the container's occupancy
   bool opened[kMaxDevices] = {};          // the previous sample re-opened the gate
   int procs = 1;                          // processes on the busiest sampled GPU (period)
+  Board board;                            // node-wide board (VGPU_BOARD_DIR), if any
+  bool board_tried = false;
+  uint64_t yielded_ns[kMaxDevices] = {};  // background class: time spent yielding (diagnostics)
 };
+
+// The container's task priority (live: vgpuctl / the monitor may change it).
+int region_priority(const Region* r) { return r->hdr.priority.load(std::memory_order_relaxed); }
+
+// Publishes the container on the board (lease holder, every period).
+void board_tick(Region* r, Sampler& sm, uint64_t now) {
+  const Config& cfg = config();
+  if (cfg.board_dir.empty()) return;
+  if (!sm.board.attached()) {
+    if (sm.board_tried) return;
+    sm.board_tried = true;
+    int rc = sm.board.open(cfg.board_dir.c_str(), cfg.board_slot.empty() ? "self.slot" : cfg.board_slot.c_str());
+    if (rc != 0) {
+      VLOG_WARN("cannot open board slot %s/%s (%s); priorities act without it", cfg.board_dir.c_str(),
+                cfg.board_slot.c_str(), strerror(-rc));
+      return;
+    }
+  }
+  ShimState& s = shim();
+  uint32_t ids[kMaxDevices];
+  for (int i = 0; i < s.n_agents; i++) ids[i] = s.agents[i].gpu_id;
+  sm.board.publish(region_priority(r), ids, s.n_agents, sm.mine, now);
+}
 
 void collect_region_pids(Region* r, Sampler& sm) {
   sm.mine.clear();
@@ -142,6 +169,7 @@ void sample_tick(Region* r, Sampler& sm) {
   if (refresh) {
     sm.others_at_ns = now;
     sm.procs = 1;
+    if (sm.board.attached() && region_priority(r) >= kPrioBackground) sm.board.refresh(now);
   }
   for (int d = 0; d < s.n_agents; d++) {
     AgentInfo& a = s.agents[d];
@@ -155,14 +183,24 @@ void sample_tick(Region* r, Sampler& sm) {
       sm.procs = std::max(sm.procs, (int)(sm.mine.size() + sm.others[d].size()));
     }
     int pm = 0;  // the container's share of the GPU at this instant, per mille
-    if (!sm.mine.empty()) {
+    // Background class: no credit is earned while a higher-priority tenant (by its board
+    // slot; a process on no slot counts as normal) has waves resident on this GPU.
+    const int prio = region_priority(r);
+    const bool background = prio >= kPrioBackground;
+    bool yield = false;
+    if (!sm.mine.empty() || background) {
       int64_t mine = 0;
       for (int hp : sm.mine) mine += std::max<int64_t>(0, kfd_cu_occupancy(hp, a.gpu_id));
       // Split the instant with whoever else has waves resident on this GPU (other
-      // containers, unlimited processes): only read when the container is busy.
+      // containers, unlimited processes): only read when the container is busy (or
+      // yields by class, which needs to know whether its betters are busy).
       int64_t total = mine;
-      if (mine > 0) {
-        for (int p : sm.others[d]) total += std::max<int64_t>(0, kfd_cu_occupancy(p, a.gpu_id));
+      if (mine > 0 || background) {
+        for (int p : sm.others[d]) {
+          const int64_t occ = std::max<int64_t>(0, kfd_cu_occupancy(p, a.gpu_id));
+          total += occ;
+          if (background && occ > 0 && !yield && sm.board.priority_of(p, a.gpu_id) < prio) yield = true;
+        }
         r->hdr.other_refreshes.fetch_add(1, std::memory_order_relaxed);
       }
       pm = (int)timeshare_charge(1000, mine, total);
@@ -175,7 +213,8 @@ void sample_tick(Region* r, Sampler& sm) {
     }
     const int64_t charge = timeshare_interval(dt, sm.prev_pm[d], pm, sm.opened[d]);
     const bool was_closed = !ds.gate_open.load(std::memory_order_relaxed);
-    timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, config().limiter_window_ms), dt, charge);
+    if (yield) sm.yielded_ns[d] += dt;
+    timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, config().limiter_window_ms), dt, charge, yield ? 0 : dt);
     sm.opened[d] = was_closed && ds.gate_open.load(std::memory_order_relaxed);
     sm.prev_pm[d] = pm;
   }
@@ -204,8 +243,10 @@ void crowd_tick(Region* r, Sampler& sm, Crowd& c, uint64_t now) {
     DeviceState& ds = r->dev[d];
     const int pct = ds.cu_limit_pct;
     // Assessed for every limited device (not only below 50 %), so a live change to a
-    // smaller share finds the crowd already known.
-    if (!a.gpu_id || pct <= 0 || pct >= 100) continue;
+    // smaller share finds the crowd already known; and for every device of a background
+    // tenant, which goes on the GPU-time gate as soon as anyone else is busy.
+    const bool background = region_priority(r) >= kPrioBackground;
+    if (!a.gpu_id || ((pct <= 0 || pct >= 100) && !background)) continue;
     for (int p : kfd_pids_on_gpu(a.gpu_id)) {
       if (std::find(sm.mine.begin(), sm.mine.end(), p) != sm.mine.end()) continue;
       if (kfd_cu_occupancy(p, a.gpu_id) > 0) c.busy_at[d][p] = now;
@@ -220,8 +261,11 @@ void crowd_tick(Region* r, Sampler& sm, Crowd& c, uint64_t now) {
       }
     }
     const int cur = ds.crowd.load(std::memory_order_relaxed);
-    const bool crowded_now = busy > kAutoSpatialMaxCrowd;
-    const bool was_crowded = cur < 0 || cur > kAutoSpatialMaxCrowd;
+    // The count at which the enforcement changes: a background tenant switches to the
+    // GPU-time gate as soon as one other process is busy (effective_cu_mode_prio).
+    const int threshold = background ? 0 : kAutoSpatialMaxCrowd;
+    const bool crowded_now = busy > threshold;
+    const bool was_crowded = cur < 0 || cur > threshold;
     int next = busy;
     if (crowded_now || cur < 0) {
       c.calm_since[d] = 0;
@@ -231,10 +275,10 @@ void crowd_tick(Region* r, Sampler& sm, Crowd& c, uint64_t now) {
     }
     if (next != cur) {
       ds.crowd.store(next, std::memory_order_relaxed);
-      if ((next > kAutoSpatialMaxCrowd) != was_crowded) {
+      if ((next > threshold) != was_crowded) {
         changed = true;
         VLOG_INFO("device %d: %d other busy process(es) on the GPU -> %s", d, busy,
-                  next > kAutoSpatialMaxCrowd ? "GPU-time limiter" : "CU mask");
+                  next > threshold ? "GPU-time limiter" : "CU mask");
       }
     }
   }
@@ -309,6 +353,7 @@ void* watcher_main(void*) {
       resync_context_charge();
       if (lease) {
         collect_region_pids(r, sm);
+        board_tick(r, sm, now);
         crowd_tick(r, sm, crowd, now);
         monitor_tick(r);
         if (!temporal) r->hdr.watcher_heartbeat.store(now_ns());

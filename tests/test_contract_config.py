@@ -337,3 +337,30 @@ def test_host_pid_lock_is_a_read_only_file_mount(tmp_path):
     mounts = {m.container_path: (m.host_path, m.read_only) for m in resp.mounts}
     assert mounts["/usr/local/vgpu/lock/hostpid.lock"] == (path, True)
     assert dict(resp.envs)["VGPU_LOCK_FILE"] == "/usr/local/vgpu/lock/hostpid.lock"
+
+
+def test_board_slot_mounts(tmp_path):
+    """Each container gets the board directory read-only and its own slot read-write."""
+    from amdvgpu.plugin.contract import build_container_response, ensure_board_dir
+    from amdvgpu.plugin.devices import FakeBackend
+    from amdvgpu.plugin.vdevice import device_to_vdevices
+    vdir = str(tmp_path / "vgpu")
+    board = ensure_board_dir(vdir)
+    devs = FakeBackend(n=1).devices()
+    cfg = PluginConfig(vgpu_dir=vdir).validate()
+    r1 = build_container_response(cfg, device_to_vdevices(devs, 2)[:1], {d.uuid: d for d in devs})
+    r2 = build_container_response(cfg, device_to_vdevices(devs, 2)[1:2], {d.uuid: d for d in devs})
+    slots = []
+    for r in (r1, r2):
+        envs = dict(r.envs)
+        mounts = {m.container_path: (m.host_path, m.read_only) for m in r.mounts}
+        assert envs["VGPU_BOARD_DIR"] == "/usr/local/vgpu/board"
+        assert mounts["/usr/local/vgpu/board"] == (board, True)
+        slot = envs["VGPU_BOARD_SLOT"]
+        assert mounts[f"/usr/local/vgpu/board/{slot}"] == (os.path.join(board, slot), False)
+        assert os.stat(os.path.join(board, slot)).st_mode & 0o777 == 0o666
+        slots.append(slot)
+    assert slots[0] != slots[1]
+    # the container-side order matters: the directory is mounted before the file on top
+    paths = [m.container_path for m in r1.mounts]
+    assert paths.index("/usr/local/vgpu/board") < paths.index(f"/usr/local/vgpu/board/{slots[0]}")

@@ -112,13 +112,40 @@ def test_compiled_launch_block(tmp_region):
     assert child_results(out)[0]["max_gap"] >= 1.5
 
 
+RATE_BUSY = COMPILED.format(body="""
+from amdvgpu.shim.region import Region
+r = Region(os.environ["VGPU_SHARED_CACHE"])
+d0 = r.device(0)
+n = 0
+t0 = time.perf_counter()
+while time.perf_counter() - t0 < {secs}:
+    for _ in range(8):
+        cf(x, y)
+    torch.cuda.synchronize()
+    n += 8
+rate = n / (time.perf_counter() - t0)
+d1 = r.device(0)
+emit(rate=rate, busy=(d1["charged_ns"] - d0["charged_ns"]) / max(1, d1["wall_ns"] - d0["wall_ns"]))
+""")
+
+
 def test_compiled_tenant_temporal_limit():
-    """cu_mode=temporal at 25 %: a compiled tenant gets 25 +- 5 % of its solo rate."""
-    native = _run(RATE.format(secs=3.0), None)["rate"]
-    c = vgpu_env(mem_limit=16 * GiB, cu_limit=25, cu_mode="temporal")
+    """cu_mode=temporal at 25 %: a compiled tenant gets 25 % of the GPU's time, i.e. its
+    solo rate x 25 % / (its solo GPU-busy fraction). The limit is on GPU time, as the
+    reference's SM-utilisation limit is: a launch-bound tenant that keeps the GPU busy only
+    80 % of the time alone gets 25/80 of its solo rate. The solo busy fraction is measured
+    by the same sampler with the limiter forced on at 100 % (it never throttles)."""
+    solo = vgpu_env(mem_limit=16 * GiB, cu_mode="temporal", extra={"VGPU_CU_POLICY": "force"})
+    lim = vgpu_env(mem_limit=16 * GiB, cu_limit=25, cu_mode="temporal")
     try:
-        got = _run(RATE.format(secs=4.0), c)["rate"]
+        native = _run(RATE_BUSY.format(secs=3.0), solo)
+        got = _run(RATE_BUSY.format(secs=4.0), lim)
     finally:
-        cleanup_region(c)
-    achieved = 100.0 * got / native
-    assert abs(achieved - 25.0) <= 5.0, f"achieved {achieved:.1f}% (native {native:.0f}/s, limited {got:.0f}/s)"
+        cleanup_region(solo)
+        cleanup_region(lim)
+    assert 0.3 < native["busy"] <= 1.0, native
+    assert abs(100.0 * got["busy"] - 25.0) <= 3.0, got          # GPU time held to the limit
+    achieved = 100.0 * got["rate"] / native["rate"]
+    expected = 25.0 / native["busy"]
+    assert abs(achieved - expected) <= 5.0, (f"achieved {achieved:.1f}% of the solo rate, expected {expected:.1f}% "
+                                             f"(solo busy {native['busy']:.2f}; {native['rate']:.0f} -> {got['rate']:.0f}/s)")

@@ -363,3 +363,35 @@ def test_partition_temporal_limit_follows_the_visible_list(fake):
     runs = [o for o in out if "run" in o]
     assert runs[0]["busy_frac"] > 0.75, runs
     assert abs(runs[1]["busy_frac"] - 0.20) <= 0.05, runs
+
+
+def _board_env(fake, tmp_path, name, **vgpu):
+    e = fake(gpus=1, **vgpu)
+    e["VGPU_SHARED_CACHE"] = str(tmp_path / f"{name}.cache")  # its own container
+    e["VGPU_BOARD_DIR"] = str(tmp_path / "board")
+    e["VGPU_BOARD_SLOT"] = f"{name}.slot"
+    return e
+
+
+@pytest.mark.parametrize("neighbour_prio,yields", [("1", True), ("2", False)])
+def test_background_class_yields_to_busier_betters(fake, tmp_path, neighbour_prio, yields):
+    """VGPU_TASK_PRIORITY >= 2 (background): while a tenant of higher priority (by its
+    board slot) keeps the GPU busy, the background tenant earns no GPU time and its
+    launches wait; next to an equal-priority tenant it runs as usual."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+    busy = _board_env(fake, tmp_path, "svc", VGPU_TASK_PRIORITY=neighbour_prio)
+    bg = _board_env(fake, tmp_path, "batch", VGPU_TASK_PRIORITY="2")
+    a = sp.Popen([HARNESS, "stream", "run=2000,6"], env=busy, stdout=sp.PIPE, text=True)
+    try:
+        time.sleep(1.0)  # the service is busy and on the board
+        out = run(bg, "stream", "run=2000,3", timeout=120)
+    finally:
+        a.wait(timeout=60)
+    frac = [o for o in out if "run" in o][0]["busy_frac"]
+    if yields:
+        assert frac < 0.25, frac
+    else:
+        assert frac > 0.75, frac
+    slots = sorted(os.listdir(tmp_path / "board"))
+    assert slots == ["batch.slot", "svc.slot"]
