@@ -17,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#include "vgpu/board.h"
 #include "vgpu/config.h"
 #include "vgpu/cumask.h"
 #include "vgpu/devmap.h"
@@ -930,6 +931,37 @@ static void test_hostpid_resolution() {
   g_kfd_proc_root = "/sys/class/kfd/kfd/proc";
 }
 
+static void test_board() {
+  char dir[] = "/tmp/vgpu_board_XXXXXX";
+  CHECK(mkdtemp(dir) != nullptr);
+  Board a, b;
+  CHECK_EQ(a.open(dir, "a.slot"), 0);
+  CHECK_EQ(b.open(dir, "b.slot"), 0);
+  CHECK_EQ(a.open(dir, "../escape.slot"), -EINVAL);
+  const uint64_t now = now_ns();
+  const uint32_t gpus_a[2] = {1000, 1001}, gpus_b[1] = {1001};
+  a.publish(kPrioNormal, gpus_a, 2, {4242, 4243}, now);
+  b.publish(kPrioBackground, gpus_b, 1, {5151}, now);
+  // Each sees the other, never itself.
+  CHECK_EQ((int)b.refresh(now).size(), 1);
+  CHECK_EQ(b.priority_of(4243, 1001), kPrioNormal);
+  CHECK_EQ(a.refresh(now).size(), 1u);
+  CHECK_EQ(a.priority_of(5151, 1001), kPrioBackground);
+  CHECK_EQ(a.priority_of(5151, 1000), kPrioNormal);  // not on that GPU: unknown = normal
+  CHECK_EQ(a.priority_of(9999, 1001), kPrioNormal);  // on no slot
+  // A stale heartbeat (the container is gone) or a departed slot is ignored.
+  CHECK_EQ(a.refresh(now + kBoardStaleNs + 1).size(), 0u);
+  b.leave();
+  CHECK_EQ(a.refresh(now).size(), 0u);
+  // Garbage in a slot file (a tenant writing nonsense into its own slot) is ignored.
+  FILE* f = fopen((std::string(dir) + "/junk.slot").c_str(), "w");
+  CHECK(f != nullptr);
+  fputs("not a slot", f);
+  fclose(f);
+  CHECK_EQ(a.refresh(now).size(), 0u);
+  CHECK(system((std::string("rm -rf ") + dir).c_str()) == 0);
+}
+
 static void test_kfd() {
   char dir[] = "/tmp/vgpu_kfd_XXXXXX";
   CHECK(mkdtemp(dir) != nullptr);
@@ -986,6 +1018,7 @@ int main(int argc, char** argv) {
       {"charge_overflow", test_charge_overflow},
       {"kfd", test_kfd},
       {"hostpid_resolution", test_hostpid_resolution},
+      {"board", test_board},
   };
   if (argc > 1 && !strcmp(argv[1], "--list")) {
     for (auto& t : tests) printf("%s\n", t.first);
