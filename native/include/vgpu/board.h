@@ -41,6 +41,7 @@ struct alignas(64) BoardSlot {
   std::atomic<int32_t> priority;
   int32_t ndev;
   uint32_t gpu_id[kMaxDevices];           // KFD gpu_id of the container's devices
+  uint32_t cu_mask[kMaxDevices][kCuMaskWords];  // the spatial mask its queues use (0 = all CUs)
   std::atomic<int32_t> npids;
   std::atomic<int32_t> hostpids[kBoardMaxPids];
 };
@@ -52,6 +53,7 @@ constexpr uint64_t kBoardStaleNs = 2'000'000'000ull;
 struct BoardPeer {
   int priority = kPrioNormal;
   std::vector<uint32_t> gpu_ids;
+  std::vector<std::vector<uint32_t>> masks;  // per device, kCuMaskWords words (all 0 = no mask)
   std::vector<int> hostpids;
 };
 
@@ -70,7 +72,9 @@ class Board {
   BoardSlot* self() { return self_; }
 
   // Publishes this container's state (the sampler calls it every period).
-  void publish(int priority, const uint32_t* gpu_ids, int ndev, const std::vector<int>& hostpids, uint64_t now);
+  // `masks`: ndev x kCuMaskWords words, or null.
+  void publish(int priority, const uint32_t* gpu_ids, int ndev, const std::vector<int>& hostpids, uint64_t now,
+               const uint32_t (*masks)[kCuMaskWords] = nullptr);
   void leave();
 
   // Re-reads the other slots (live ones only). Cheap enough for every 100 ms.
@@ -80,6 +84,10 @@ class Board {
   // Priority of the container owning host PID `pid` on GPU `gpu_id` (kPrioNormal for a
   // process no live slot lists: an unmanaged process counts as a normal tenant).
   int priority_of(int pid, uint32_t gpu_id) const;
+
+  // OR of the CU masks that tenants of priority <= `max_priority` use on GPU `gpu_id`
+  // (the CUs a background tenant leaves to the latency class).
+  void reserved_mask(uint32_t gpu_id, int max_priority, uint32_t* out_words) const;
 
  private:
   std::string dir_, self_name_;

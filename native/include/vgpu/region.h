@@ -97,6 +97,9 @@ struct alignas(64) DeviceState {
   uint32_t domain;                        // PCI domain
   uint32_t configured;                    // 1 once a GPU process filled the agent info
   std::atomic<int32_t> crowd;             // auto mode: other busy processes on the GPU (-1 = unknown)
+  // Background class: CUs held by latency-class tenants on this GPU (their CU slices, from
+  // the board); the container's queues keep off them (0 = none).
+  uint32_t reserved_mask[kCuMaskWords];
 };
 
 struct RegionHeader {

@@ -51,11 +51,15 @@ int Board::open(const char* dir, const char* self_name) {
   return 0;
 }
 
-void Board::publish(int priority, const uint32_t* gpu_ids, int ndev, const std::vector<int>& hostpids, uint64_t now) {
+void Board::publish(int priority, const uint32_t* gpu_ids, int ndev, const std::vector<int>& hostpids, uint64_t now,
+                    const uint32_t (*masks)[kCuMaskWords]) {
   if (!self_) return;
   self_->priority.store(priority, std::memory_order_relaxed);
   ndev = std::max(0, std::min(ndev, kMaxDevices));
-  for (int i = 0; i < ndev; i++) self_->gpu_id[i] = gpu_ids[i];
+  for (int i = 0; i < ndev; i++) {
+    self_->gpu_id[i] = gpu_ids[i];
+    for (int w = 0; w < kCuMaskWords; w++) self_->cu_mask[i][w] = masks ? masks[i][w] : 0;
+  }
   self_->ndev = ndev;
   const int n = std::min((int)hostpids.size(), kBoardMaxPids);
   for (int i = 0; i < n; i++) self_->hostpids[i].store(hostpids[i], std::memory_order_relaxed);
@@ -90,6 +94,7 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
     p.priority = s.priority.load(std::memory_order_relaxed);
     const int ndev = std::max(0, std::min(s.ndev, kMaxDevices));
     p.gpu_ids.assign(s.gpu_id, s.gpu_id + ndev);
+    for (int i = 0; i < ndev; i++) p.masks.emplace_back(s.cu_mask[i], s.cu_mask[i] + kCuMaskWords);
     const int n = std::max(0, std::min(s.npids.load(std::memory_order_relaxed), kBoardMaxPids));
     for (int i = 0; i < n; i++) {
       const int pid = s.hostpids[i].load(std::memory_order_relaxed);
@@ -99,6 +104,16 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
   }
   closedir(d);
   return peers_;
+}
+
+void Board::reserved_mask(uint32_t gpu_id, int max_priority, uint32_t* out_words) const {
+  for (int w = 0; w < kCuMaskWords; w++) out_words[w] = 0;
+  for (const BoardPeer& p : peers_) {
+    if (p.priority > max_priority) continue;
+    for (size_t i = 0; i < p.gpu_ids.size() && i < p.masks.size(); i++)
+      if (p.gpu_ids[i] == gpu_id)
+        for (int w = 0; w < kCuMaskWords; w++) out_words[w] |= p.masks[i][w];
+  }
 }
 
 int Board::priority_of(int pid, uint32_t gpu_id) const {

@@ -470,7 +470,29 @@ void apply_live_config() {
     // higher-priority tenants (watcher.cpp) and otherwise runs free.
     const bool yields = prio >= kPrioBackground && cfg.cu_mode == CuMode::kAuto && temporal;
     const bool temp_on = !off && temporal && (limited || force || yields);
-    const bool mask_changed = mask_on != a.mask_active.load() || memcmp(m.words, a.mask.words, sizeof(m.words)) != 0;
+    // A background tenant keeps its queues off the CUs latency-class tenants hold on this
+    // GPU (their slices from the board, watcher.cpp): its work can then not sit in front
+    // of theirs on a CU, whatever it has queued.
+    bool reserved_on = false;
+    if (!off && prio >= kPrioBackground) {
+      CuMask rsv;
+      memcpy(rsv.words, d.reserved_mask, sizeof(rsv.words));
+      rsv.nbits = a.cu_count;
+      // At most half the GPU can be held this way: the board is written by the tenants,
+      // and one that claims more is ignored rather than allowed to starve this one.
+      if (rsv.count() > 0 && rsv.count() <= a.cu_count / 2) {
+        CuMask left;
+        left.nbits = a.cu_count;
+        for (int b = 0; b < a.cu_count && b < kMaxCUs; b++)
+          if ((mask_on ? m.test(b) : true) && !rsv.test(b)) left.set(b);
+        if (left.count() > 0 && cu_mask_balanced(left, a.num_xcc)) {
+          m = left;
+          reserved_on = true;
+        }
+      }
+    }
+    const bool mask_eff = mask_on || reserved_on;
+    const bool mask_changed = mask_eff != a.mask_active.load() || memcmp(m.words, a.mask.words, sizeof(m.words)) != 0;
     if (temp_on && !a.temporal_active.load() && !d.gate_open.load()) {
       d.credit_ns.store(timeshare_params(pct, cfg.limiter_window_ms).burst_ns);
       d.gate_open.store(1);
@@ -487,10 +509,10 @@ void apply_live_config() {
     const bool slice = !off && may_mask && (limited || ranged) && m.count() < a.cu_count && m.count() > 0;
     a.visible_cus.store(slice && cfg.virtual_cu_count ? m.count() : 0);
     a.temporal_active.store(temp_on);
-    int flags = (mask_on ? 1 : 0) | (temp_on ? 2 : 0);
+    int flags = (mask_eff ? 1 : 0) | (temp_on ? 2 : 0);
     d.cu_mode.store(flags);
     if (mask_changed) {
-      a.mask_active.store(mask_on);
+      a.mask_active.store(mask_eff);
       // Re-apply to every queue this process already owns (they were created with the
       // old mask); new queues pick the mask up in hsa_queue_create.
       std::vector<hsa_queue_t*> qs;
@@ -502,7 +524,7 @@ void apply_live_config() {
       VGPU_REAL_HSA(hsa_amd_queue_cu_set_mask);
       CuMask all;
       for (int b = 0; b < a.cu_count && b < kMaxCUs; b++) all.set(b);
-      const CuMask& eff = mask_on ? m : all;
+      const CuMask& eff = mask_eff ? m : all;
       uint32_t nbits = (uint32_t)((a.cu_count + 31) / 32 * 32);
       for (hsa_queue_t* q : qs) {
         hsa_status_t st = real_hsa_amd_queue_cu_set_mask(q, nbits, eff.words);
@@ -510,8 +532,8 @@ void apply_live_config() {
           VLOG_ERROR("device %d: cannot re-apply CU mask to queue %p (status %d)", i, (void*)q, (int)st);
       }
       if (!qs.empty())
-        VLOG_INFO("device %d: CU limit %d%% -> %d CUs re-applied to %zu queue(s)", i, pct,
-                  mask_on ? m.count() : a.cu_count, qs.size());
+        VLOG_INFO("device %d: CU limit %d%%%s -> %d CUs re-applied to %zu queue(s)", i, pct,
+                  reserved_on ? " (off the latency class's CUs)" : "", mask_eff ? m.count() : a.cu_count, qs.size());
     }
   }
   bool any = false;

@@ -144,8 +144,30 @@ void board_tick(Region* r, Sampler& sm, uint64_t now) {
   }
   ShimState& s = shim();
   uint32_t ids[kMaxDevices];
-  for (int i = 0; i < s.n_agents; i++) ids[i] = s.agents[i].gpu_id;
-  sm.board.publish(region_priority(r), ids, s.n_agents, sm.mine, now);
+  uint32_t masks[kMaxDevices][kCuMaskWords] = {};
+  for (int i = 0; i < s.n_agents; i++) {
+    ids[i] = s.agents[i].gpu_id;
+    // A background tenant's own mask is derived from the reservation: not published, so
+    // masks never feed back into each other.
+    if (s.agents[i].mask_active.load(std::memory_order_relaxed) && region_priority(r) < kPrioBackground)
+      memcpy(masks[i], s.agents[i].mask.words, sizeof(masks[i]));
+  }
+  sm.board.publish(region_priority(r), ids, s.n_agents, sm.mine, now, masks);
+  // Background class: keep off the CU slices of latency-class tenants on the same GPU.
+  // Stored in the region, so every process of the container re-masks its queues.
+  if (region_priority(r) < kPrioBackground) return;
+  sm.board.refresh(now);
+  bool changed = false;
+  for (int i = 0; i < s.n_agents; i++) {
+    uint32_t want[kCuMaskWords];
+    sm.board.reserved_mask(ids[i], kPrioLatency, want);
+    DeviceState& d = r->dev[i];
+    if (memcmp(want, d.reserved_mask, sizeof(want)) != 0) {
+      memcpy(d.reserved_mask, want, sizeof(want));
+      changed = true;
+    }
+  }
+  if (changed) r->hdr.generation.fetch_add(1, std::memory_order_acq_rel);
 }
 
 void collect_region_pids(Region* r, Sampler& sm) {

@@ -395,3 +395,42 @@ def test_background_class_yields_to_busier_betters(fake, tmp_path, neighbour_pri
         assert frac > 0.75, frac
     slots = sorted(os.listdir(tmp_path / "board"))
     assert slots == ["batch.slot", "svc.slot"]
+
+
+def test_background_class_keeps_off_the_latency_class_cus(fake, tmp_path):
+    """A latency-class tenant (priority 0) publishes its CU slice on the board; a
+    background tenant (priority >= 2) on the same GPU re-masks its queues to the rest of
+    the GPU, so its queued work never sits on the latency tenant's CUs."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+    svc = _board_env(fake, tmp_path, "svc", VGPU_TASK_PRIORITY="0", VGPU_DEVICE_CU_LIMIT="25")
+    bg = _board_env(fake, tmp_path, "batch", VGPU_TASK_PRIORITY="2")
+    a = sp.Popen([HARNESS, "stream", "sleep=3", "queues"], env=svc, stdout=sp.PIPE, text=True)
+    try:
+        time.sleep(0.8)  # the service is on the board with its slice
+        out = run(bg, "stream", "queues", "sleep=1.0", "queues")
+        a_out, _ = a.communicate(timeout=60)
+    finally:
+        if a.poll() is None:
+            a.kill()
+    a_q = [json.loads(l) for l in a_out.splitlines() if l.startswith('{"queues"')][0]["queues"][0]
+    first, later = [o["queues"][0] for o in out if "queues" in o]
+    assert a_q["cus"] == 64
+    assert later["cus"] == 192 and later["sets"] >= 1, (first, later)
+    # no overlap with the service's slice (first mask word: XCC-interleaved bits)
+    assert later["mask0"] & a_q["mask0"] == 0
+
+
+def test_board_claims_over_half_the_gpu_are_ignored(fake, tmp_path):
+    """A tenant that claims more than half the GPU as latency class is ignored."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+    greedy = _board_env(fake, tmp_path, "greedy", VGPU_TASK_PRIORITY="0", VGPU_DEVICE_CU_LIMIT="75")
+    bg = _board_env(fake, tmp_path, "batch", VGPU_TASK_PRIORITY="2")
+    a = sp.Popen([HARNESS, "stream", "sleep=2.5"], env=greedy, stdout=sp.PIPE, text=True)
+    try:
+        time.sleep(0.8)
+        out = run(bg, "stream", "sleep=1.0", "queues")
+    finally:
+        a.wait(timeout=60)
+    assert [o["queues"][0] for o in out if "queues" in o][0]["cus"] == 256
