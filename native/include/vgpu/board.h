@@ -42,6 +42,8 @@ struct alignas(64) BoardSlot {
   int32_t ndev;
   uint32_t gpu_id[kMaxDevices];           // KFD gpu_id of the container's devices
   uint32_t cu_mask[kMaxDevices][kCuMaskWords];  // the spatial mask its queues use (0 = all CUs)
+  std::atomic<int32_t> gate[kMaxDevices];       // GPU-time gate open at the last sample
+  std::atomic<uint64_t> want_since[kMaxDevices];  // waiting for admission since (0 = not waiting)
   std::atomic<int32_t> npids;
   std::atomic<int32_t> hostpids[kBoardMaxPids];
 };
@@ -54,6 +56,8 @@ struct BoardPeer {
   int priority = kPrioNormal;
   std::vector<uint32_t> gpu_ids;
   std::vector<std::vector<uint32_t>> masks;  // per device, kCuMaskWords words (all 0 = no mask)
+  std::vector<int> gate;                     // per device
+  std::vector<uint64_t> want_since;          // per device
   std::vector<int> hostpids;
 };
 
@@ -76,6 +80,16 @@ class Board {
   void publish(int priority, const uint32_t* gpu_ids, int ndev, const std::vector<int>& hostpids, uint64_t now,
                const uint32_t (*masks)[kCuMaskWords] = nullptr);
   void leave();
+  // Gate state of device `dev` for the concurrency admission (every sample).
+  void publish_gate(int dev, bool open, uint64_t want_since);
+
+  // Concurrency admission (VGPU_GPU_CONCURRENCY = k): may this container open its gate on
+  // GPU `gpu_id`, given it has wanted to since `want_since`? Yes while fewer than k
+  // peers hold their gates open there and fewer than (k - open) peers have been waiting
+  // longer. Peers as of the last refresh().
+  bool admit(uint32_t gpu_id, int k, uint64_t want_since) const;
+  // Whether a peer on GPU `gpu_id` is waiting for admission.
+  bool waiting(uint32_t gpu_id) const;
 
   // Re-reads the other slots (live ones only). Cheap enough for every 100 ms.
   const std::vector<BoardPeer>& refresh(uint64_t now);

@@ -95,6 +95,9 @@ struct Config {
   ChargeModel charge_model = ChargeModel::kShare;  // VGPU_CHARGE_MODEL: share | progress
   std::string board_dir;                 // VGPU_BOARD_DIR: node-wide board (vgpu/board.h), "" = none
   std::string board_slot;                // VGPU_BOARD_SLOT: this container's slot file in it
+  int gpu_concurrency = 0;               // VGPU_GPU_CONCURRENCY: limited containers whose GPU-time
+                                         // gates may be open together on one GPU (0 = any number)
+  int gpu_slice_ms = 20;                 // VGPU_GPU_SLICE_MS: turn length under that admission
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
   uint64_t host_mem_limit = 0;           // VGPU_HOST_MEMORY_LIMIT: pinned host memory, 0 = unlimited

@@ -71,6 +71,32 @@ void Board::leave() {
   if (self_) self_->heartbeat_ns.store(0, std::memory_order_release);
 }
 
+void Board::publish_gate(int dev, bool open, uint64_t want_since) {
+  if (!self_ || dev < 0 || dev >= kMaxDevices) return;
+  self_->gate[dev].store(open ? 1 : 0, std::memory_order_relaxed);
+  self_->want_since[dev].store(want_since, std::memory_order_relaxed);
+}
+
+bool Board::waiting(uint32_t gpu_id) const {
+  for (const BoardPeer& p : peers_)
+    for (size_t i = 0; i < p.gpu_ids.size() && i < p.want_since.size(); i++)
+      if (p.gpu_ids[i] == gpu_id && p.want_since[i] && !p.gate[i]) return true;
+  return false;
+}
+
+bool Board::admit(uint32_t gpu_id, int k, uint64_t want_since) const {
+  if (k <= 0) return true;
+  int open = 0, ahead = 0;
+  for (const BoardPeer& p : peers_) {
+    for (size_t i = 0; i < p.gpu_ids.size() && i < p.gate.size(); i++) {
+      if (p.gpu_ids[i] != gpu_id) continue;
+      if (p.gate[i]) open++;
+      else if (p.want_since[i] && p.want_since[i] < want_since) ahead++;
+    }
+  }
+  return open < k && ahead < k - open;
+}
+
 const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
   peers_.clear();
   if (dir_.empty()) return peers_;
@@ -94,7 +120,11 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
     p.priority = s.priority.load(std::memory_order_relaxed);
     const int ndev = std::max(0, std::min(s.ndev, kMaxDevices));
     p.gpu_ids.assign(s.gpu_id, s.gpu_id + ndev);
-    for (int i = 0; i < ndev; i++) p.masks.emplace_back(s.cu_mask[i], s.cu_mask[i] + kCuMaskWords);
+    for (int i = 0; i < ndev; i++) {
+      p.masks.emplace_back(s.cu_mask[i], s.cu_mask[i] + kCuMaskWords);
+      p.gate.push_back(s.gate[i].load(std::memory_order_relaxed));
+      p.want_since.push_back(s.want_since[i].load(std::memory_order_relaxed));
+    }
     const int n = std::max(0, std::min(s.npids.load(std::memory_order_relaxed), kBoardMaxPids));
     for (int i = 0; i < n; i++) {
       const int pid = s.hostpids[i].load(std::memory_order_relaxed);

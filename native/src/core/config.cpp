@@ -287,6 +287,10 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
     else VLOG_WARN("invalid VGPU_CHARGE_MODEL=%s ignored", s);
   }
   if (const char* s = getenv_fn("VGPU_BOARD_DIR")) cfg->board_dir = s;
+  long conc = 0;
+  if (parse_int(getenv_fn("VGPU_GPU_CONCURRENCY"), 0, 64, &conc)) cfg->gpu_concurrency = (int)conc;
+  long slice = 20;
+  if (parse_int(getenv_fn("VGPU_GPU_SLICE_MS"), 1, 10000, &slice)) cfg->gpu_slice_ms = (int)slice;
   if (const char* s = getenv_fn("VGPU_BOARD_SLOT")) cfg->board_slot = s;
   if (const char* s = getenv_fn("VGPU_LOCK_FILE")) {
     if (*s) cfg->lock_file = s;

@@ -123,6 +123,9 @@ struct Sampler {
   Board board;                            // node-wide board (VGPU_BOARD_DIR), if any
   bool board_tried = false;
   uint64_t yielded_ns[kMaxDevices] = {};  // background class: time spent yielding (diagnostics)
+  uint64_t want_since[kMaxDevices] = {};  // concurrency admission: waiting since (0 = not)
+  uint64_t open_since[kMaxDevices] = {};  // concurrency admission: holding the GPU since
+  bool admitted[kMaxDevices] = {};
 };
 
 // The container's task priority (live: vgpuctl / the monitor may change it).
@@ -188,11 +191,13 @@ void sample_tick(Region* r, Sampler& sm) {
   sm.last_ns = now;
   collect_region_pids(r, sm);
   const bool refresh = now - sm.others_at_ns > 100'000'000ull;
+  const int conc = sm.board.attached() ? config().gpu_concurrency : 0;
   if (refresh) {
     sm.others_at_ns = now;
     sm.procs = 1;
-    if (sm.board.attached() && region_priority(r) >= kPrioBackground) sm.board.refresh(now);
   }
+  // Peers: every sample for the concurrency admission, every 100 ms for the classes.
+  if (conc > 0 || (refresh && sm.board.attached() && region_priority(r) >= kPrioBackground)) sm.board.refresh(now);
   for (int d = 0; d < s.n_agents; d++) {
     AgentInfo& a = s.agents[d];
     if (!a.temporal_active.load(std::memory_order_relaxed) || !a.gpu_id) continue;
@@ -237,6 +242,36 @@ void sample_tick(Region* r, Sampler& sm) {
     const bool was_closed = !ds.gate_open.load(std::memory_order_relaxed);
     if (yield) sm.yielded_ns[d] += dt;
     timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, config().limiter_window_ms), dt, charge, yield ? 0 : dt);
+    if (conc > 0) {
+      // Concurrency admission, round robin: while its credit allows, a container holds
+      // the GPU for a slice, then yields to the longest-waiting peer; at most `conc`
+      // containers of the GPU hold it at once. The containers take turns in small groups
+      // instead of all overlapping (the credit still caps each one's share).
+      const bool credit_ok = ds.gate_open.load(std::memory_order_relaxed);
+      const int64_t slice = (int64_t)config().gpu_slice_ms * 1'000'000ll;
+      bool hold = false;
+      if (!credit_ok) {
+        sm.admitted[d] = false;
+        sm.want_since[d] = 0;
+      } else if (sm.admitted[d]) {
+        hold = true;
+        if ((int64_t)(now - sm.open_since[d]) >= slice && sm.board.waiting(a.gpu_id)) {
+          sm.admitted[d] = false;  // slice used up and someone waits: to the back of the queue
+          sm.want_since[d] = now;
+          hold = false;
+        }
+      } else {
+        if (!sm.want_since[d]) sm.want_since[d] = now;
+        if (sm.board.admit(a.gpu_id, conc, sm.want_since[d])) {
+          sm.admitted[d] = true;
+          sm.open_since[d] = now;
+          sm.want_since[d] = 0;
+          hold = true;
+        }
+      }
+      if (!hold) ds.gate_open.store(0, std::memory_order_release);
+      sm.board.publish_gate(d, hold, sm.want_since[d]);
+    }
     sm.opened[d] = was_closed && ds.gate_open.load(std::memory_order_relaxed);
     sm.prev_pm[d] = pm;
   }

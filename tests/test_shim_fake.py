@@ -434,3 +434,42 @@ def test_board_claims_over_half_the_gpu_are_ignored(fake, tmp_path):
     finally:
         a.wait(timeout=60)
     assert [o["queues"][0] for o in out if "queues" in o][0]["cus"] == 256
+
+
+@pytest.mark.parametrize("conc,max_sum", [(0, None), (1, 1.15)])
+def test_gpu_concurrency_admission(fake, tmp_path, conc, max_sum):
+    """VGPU_GPU_CONCURRENCY=k: at most k containers hold their GPU-time gates open on a GPU
+    at once, taking turns of VGPU_GPU_SLICE_MS (longest waiter first). The fake GPUs of the
+    three containers do not slow each other, so under the share charge each pays a third
+    of the time it runs and none is throttled (k = 0); with k = 1 they take turns."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+    envs = [_board_env(fake, tmp_path, f"t{i}", VGPU_DEVICE_CU_LIMIT="50", VGPU_CU_MODE="temporal",
+                       VGPU_GPU_CONCURRENCY=str(conc)) for i in range(3)]
+    ps = [sp.Popen([HARNESS, "stream", "sleep=0.5", "run=1000,4"], env=e, stdout=sp.PIPE, text=True) for e in envs]
+    fracs = []
+    for p in ps:
+        out, _ = p.communicate(timeout=120)
+        assert p.returncode == 0
+        fracs.append([json.loads(l) for l in out.splitlines() if '"run"' in l][0]["busy_frac"])
+    if max_sum is None:
+        assert sum(fracs) > 2.4, fracs  # all overlapping
+    else:
+        assert sum(fracs) <= max_sum, fracs
+        assert min(fracs) >= 0.25, fracs  # everybody gets turns
+
+
+def test_progress_charge_for_co_running_light_tenants(fake, tmp_path):
+    """Three tenants that co-run without slowing each other (separate fake GPUs behind one
+    KFD gpu_id) at 50 %: the share charge bills each a third of its running time (each runs
+    ~100 %); the progress charge bills what it would pay alone (each runs ~50 %)."""
+    import subprocess as sp
+    envs = [_board_env(fake, tmp_path, f"t{i}", VGPU_DEVICE_CU_LIMIT="50", VGPU_CU_MODE="temporal",
+                       VGPU_CHARGE_MODEL="progress") for i in range(3)]
+    ps = [sp.Popen([HARNESS, "stream", "sleep=0.5", "run=1000,4"], env=e, stdout=sp.PIPE, text=True) for e in envs]
+    fracs = []
+    for p in ps:
+        out, _ = p.communicate(timeout=120)
+        assert p.returncode == 0
+        fracs.append([json.loads(l) for l in out.splitlines() if '"run"' in l][0]["busy_frac"])
+    assert all(abs(f - 0.5) <= 0.08 for f in fracs), fracs
