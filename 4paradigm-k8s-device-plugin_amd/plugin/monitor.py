@@ -82,6 +82,11 @@ def render_metrics(root):
             w.metric("vgpu_container_priority", "gauge", "task priority", base, snap["priority"])
             w.metric("vgpu_container_processes", "gauge", "processes attached to the region", base,
                      len(snap["procs"]))
+            host = snap.get("host") or {}
+            w.metric("vgpu_host_memory_limit_bytes", "gauge", "pinned host memory budget (0 = unlimited)", base,
+                     host.get("limit", 0))
+            w.metric("vgpu_host_memory_used_bytes", "gauge", "pinned host memory (hipHostMalloc / hipHostRegister)",
+                     base, host.get("used", 0))
             w.metric("vgpu_sampler_ticks_total", "counter", "temporal limiter: occupancy samples taken", base,
                      snap["samples"])
             w.metric("vgpu_sampler_other_refreshes_total", "counter",

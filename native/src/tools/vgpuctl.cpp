@@ -9,6 +9,7 @@
 //   vgpuctl <region> block|unblock        launch block (recent_kernel < 0)
 //   vgpuctl <region> set-limit <dev> <size>
 //   vgpuctl <region> set-cu <dev> <pct>
+//   vgpuctl <region> set-host-limit <size>  pinned host memory budget (0 = unlimited)
 //   vgpuctl <region> priority <n>
 //   vgpuctl <region> reclaim              free slots of exited processes
 #include <cstdio>
@@ -20,16 +21,19 @@
 static int usage() {
   fprintf(stderr,
           "usage: vgpuctl <region-file> show|suspend|resume|block|unblock|reclaim|"
-          "set-limit <dev> <size>|set-cu <dev> <pct>|priority <n>\n");
+          "set-limit <dev> <size>|set-cu <dev> <pct>|set-host-limit <size>|priority <n>\n");
   return 2;
 }
 
 static void show(vgpu_region* r) {
+  uint64_t host_limit = 0, host_used = 0;
+  vgpu_region_host_info(r, &host_limit, &host_used);
   printf("{\"version\": %u, \"num_devices\": %d, \"suspended\": %d, \"priority\": %d, \"recent_kernel\": %d, "
-         "\"samples\": %llu, \"other_refreshes\": %llu,\n",
+         "\"samples\": %llu, \"other_refreshes\": %llu, \"host_limit\": %llu, \"host_used\": %llu,\n",
          vgpu_region_version(), vgpu_region_num_devices(r), vgpu_region_suspended(r), vgpu_region_get_priority(r),
          vgpu_region_get_recent_kernel(r), (unsigned long long)vgpu_region_samples(r),
-         (unsigned long long)vgpu_region_other_refreshes(r));
+         (unsigned long long)vgpu_region_other_refreshes(r), (unsigned long long)host_limit,
+         (unsigned long long)host_used);
   printf(" \"devices\": [");
   int nd = vgpu_region_num_devices(r);
   for (int d = 0; d < nd; d++) {
@@ -50,9 +54,10 @@ static void show(vgpu_region* r) {
   for (int i = 0; i < np; i++) {
     const vgpu_proc_info& p = procs[i];
     printf("%s\n  {\"pid\": %d, \"hostpid\": %d, \"status\": %d, \"launches\": %llu, \"throttle_ns\": %llu, "
-           "\"suspend_ns\": %llu, \"oom_events\": %llu, \"used\": [",
+           "\"suspend_ns\": %llu, \"oom_events\": %llu, \"host_used\": %llu, \"used\": [",
            i ? "," : "", p.pid, p.hostpid, p.status, (unsigned long long)p.launches,
-           (unsigned long long)p.throttle_ns, (unsigned long long)p.suspend_ns, (unsigned long long)p.oom_events);
+           (unsigned long long)p.throttle_ns, (unsigned long long)p.suspend_ns, (unsigned long long)p.oom_events,
+           (unsigned long long)p.host_used);
     for (int d = 0; d < (nd ? nd : 1); d++) printf("%s%llu", d ? ", " : "", (unsigned long long)p.used[d]);
     printf("]}");
   }
@@ -78,7 +83,12 @@ int main(int argc, char** argv) {
   else if (!strcmp(cmd, "set-limit") && argc == 5) {
     int64_t v = vgpu_parse_size(argv[4]);
     rc = v < 0 ? -1 : vgpu_region_set_memory_limit(r, atoi(argv[3]), (uint64_t)v);
-  } else if (!strcmp(cmd, "set-cu") && argc == 5) rc = vgpu_region_set_cu_limit(r, atoi(argv[3]), atoi(argv[4]));
+  } else if (!strcmp(cmd, "set-cu") && argc == 5) {
+    rc = vgpu_region_set_cu_limit(r, atoi(argv[3]), atoi(argv[4]));
+  } else if (!strcmp(cmd, "set-host-limit") && argc == 4) {
+    int64_t v = vgpu_parse_size(argv[3]);
+    rc = v < 0 ? -1 : vgpu_region_set_host_limit(r, (uint64_t)v);
+  }
   else if (!strcmp(cmd, "priority") && argc == 4) rc = vgpu_region_set_priority(r, atoi(argv[3]));
   else rc = usage();
   vgpu_region_close(r);

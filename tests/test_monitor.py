@@ -32,6 +32,12 @@ def test_metrics_and_control(tmp_path):
     assert "vgpu_process_oom_events_total" in text
     assert 'vgpu_sampler_ticks_total{container="pod1_main",region="abc.cache"} 0' in text
     assert 'vgpu_sampler_other_refreshes_total{container="pod1_main",region="abc.cache"} 0' in text
+    # pinned host memory: the budget and what the container's processes hold
+    r.set_host_limit(8 << 30)
+    assert r.charge_host(slot, 1 << 30) == 0 and r.charge_host(slot, 8 << 30) != 0
+    text = render_metrics(root)
+    assert f'vgpu_host_memory_limit_bytes{{container="pod1_main",region="abc.cache"}} {8 << 30}' in text
+    assert f'vgpu_host_memory_used_bytes{{container="pod1_main",region="abc.cache"}} {1 << 30}' in text
     # quota enforcement through the region: a charge past the limit is refused
     assert r.charge(slot, 0, 6 << 30, 0) != 0
     assert control(root, "pod1_main", "suspend", {}) == 1

@@ -30,6 +30,11 @@ def test_vgpuctl_show_and_control(region_path):
     assert vgpuctl(region_path, "block").returncode == 0 and r.recent_kernel < 0
     assert vgpuctl(region_path, "unblock").returncode == 0 and r.recent_kernel == 2
     assert vgpuctl(region_path, "priority", "4").returncode == 0 and r.priority == 4
+    assert vgpuctl(region_path, "set-host-limit", "2g").returncode == 0 and r.host()["limit"] == 2 << 30
+    assert r.charge_host(slot, 1 << 20) == 0
+    snap = json.loads(vgpuctl(region_path, "show").stdout)
+    assert snap["host_limit"] == 2 << 30 and snap["host_used"] == 1 << 20
+    assert snap["processes"][0]["host_used"] == 1 << 20
     assert vgpuctl(region_path, "bogus").returncode != 0
     assert vgpuctl(region_path + ".missing", "show").returncode != 0
     r.close()
