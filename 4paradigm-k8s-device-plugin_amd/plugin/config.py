@@ -56,6 +56,7 @@ class PluginConfig:
     placement: str = "spread"               # which GPU a 1-vGPU pod lands on (GetPreferredAllocation)
     duplicate_vgpus: str = "reject"         # Allocate of two vGPUs of one GPU: reject | merge
     host_memory_per_vgpu: str = "0"         # pinned host memory budget per vGPU (0 = unlimited)
+    gpu_concurrency: int = 0                # limited containers holding a GPU's time at once (0 = any)
     version_requested: bool = False
     extra: dict = field(default_factory=dict)
 
@@ -82,6 +83,8 @@ class PluginConfig:
             raise ValueError(f"invalid --placement option: {self.placement}")
         if self.duplicate_vgpus not in DUPLICATE_POLICIES:
             raise ValueError(f"invalid --duplicate-vgpus option: {self.duplicate_vgpus}")
+        if not 0 <= self.gpu_concurrency <= 64:
+            raise ValueError(f"invalid --gpu-concurrency option: {self.gpu_concurrency}")
         from ..utils.sizes import parse_size
         try:
             parse_size(self.host_memory_per_vgpu)
@@ -136,6 +139,9 @@ _FLAGS = [
      "quota and CU share; VGPU_DUPLICATE_MERGED tells the container)"),
     ("--host-memory-per-vgpu", "host_memory_per_vgpu", str, ["HOST_MEMORY_PER_VGPU"],
      "pinned host memory (hipHostMalloc / hipHostRegister) per vGPU, e.g. 64g; 0 = unlimited (tracked only)"),
+    ("--gpu-concurrency", "gpu_concurrency", int, ["GPU_CONCURRENCY"],
+     "containers on the GPU-time limiter that may hold a GPU at once, taking turns over the node-wide board "
+     "(0 = no admission: every container whose credit allows runs)"),
 ]
 
 
