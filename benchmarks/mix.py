@@ -134,6 +134,50 @@ def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=No
                 p.kill()
 
 
+def ab_compare(a, pods, backend, uuid, split, prio):
+    """ABAB runs of all pods together, without (A) and with (B) the priorities."""
+    from amdvgpu.plugin.kubelet_stub import NodeHarness
+    runs = []
+    with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode) as node:
+        ids = node.vgpu_ids(uuid)[:len(pods)]
+        for i in range(a.ab):
+            for label, pr in (("default", None), ("priority", prio)):
+                res = run_pods(node, uuid, pods, ids, a.seconds, a.warmup, pr)
+                row = {"run": i, "label": label}
+                for pod, r in zip(pods, res):
+                    row[pod["spec"]] = {k: round(v, 3) for k, v in r.items()
+                                        if k in ("throughput", "p50_ms", "p99_ms", "mean_ms")}
+                runs.append(row)
+                print(json.dumps(row), flush=True)
+    md = [f"# default vs priority classes, ABAB x{a.ab} ({a.seconds:.0f} s windows, split {split})", "",
+          "| run | " + " | ".join(p["spec"] + (" P50 / P99 ms" if p["latency"] else " /s") for p in pods) + " |",
+          "|---|" + "---|" * len(pods)]
+    for r in runs:
+        cells = []
+        for p in pods:
+            v = r[p["spec"]]
+            cells.append(f"{v['p50_ms']:.2f} / {v['p99_ms']:.2f}" if p["latency"] else f"{v['throughput']:.1f}")
+        md.append(f"| {r['label']} #{r['run']} | " + " | ".join(cells) + " |")
+    for label in ("default", "priority"):
+        sel = [r for r in runs if r["label"] == label]
+        cells = []
+        for p in pods:
+            if p["latency"]:
+                vals = sorted(r[p["spec"]]["p99_ms"] for r in sel)
+                cells.append(f"median P99 {vals[len(vals) // 2]:.2f}")
+            else:
+                vals = sorted(r[p["spec"]]["throughput"] for r in sel)
+                cells.append(f"median {vals[len(vals) // 2]:.1f}")
+        md.append(f"| **{label}** | " + " | ".join(cells) + " |")
+    text = "\n".join(md)
+    print(text)
+    if a.json_out:
+        json.dump({"pods": [p["spec"] for p in pods], "priorities": prio, "runs": runs}, open(a.json_out, "w"), indent=1)
+    if a.md_out:
+        open(a.md_out, "w").write(text + "\n")
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--pods", nargs="+", default=DEFAULT_PODS)
@@ -142,6 +186,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--priority", default="", help="SPEC=PRIO,...: a second concurrent run with these priorities")
+    ap.add_argument("--ab", type=int, default=0,
+                    help="skip the solo runs; alternate N times between the default and the --priority run "
+                         "(ABAB...) and report each run's latency-pod P50 / P99 and pod throughputs")
     ap.add_argument("--json-out")
     ap.add_argument("--md-out")
     ap.add_argument("--worker", action="store_true")
@@ -166,6 +213,8 @@ def main():
         prio[k] = int(v)
     out = {"pods": [p["spec"] for p in pods], "split": split, "cu_mode": a.cu_mode, "seconds": a.seconds,
            "solo": [], "solo_spatial": [], "together": None, "together_priority": None, "priorities": prio or None}
+    if a.ab:
+        return ab_compare(a, pods, backend, uuid, split, prio)
     with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode) as node:
         ids = node.vgpu_ids(uuid)[:len(pods)]
         for pod, vid in zip(pods, ids):
