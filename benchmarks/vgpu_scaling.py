@@ -29,6 +29,8 @@ HBM = 309220868096
 
 
 def worker(case_name, steps, warmup, out, go_file, seconds):
+    import faulthandler
+    faulthandler.dump_traceback_later(200, exit=False)  # a pod stuck in warm-up shows where
     import torch
     from amdvgpu.models.aibench import Runner, get_case
     torch.backends.cudnn.benchmark = True  # MIOpen find mode
@@ -41,6 +43,7 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
     if os.environ.get("VGPU_SHARED_CACHE") and os.path.exists(os.environ["VGPU_SHARED_CACHE"]):
         from amdvgpu.shim.region import Region
         region = Region(os.environ["VGPU_SHARED_CACHE"])
+    faulthandler.cancel_dump_traceback_later()
     open(out + ".ready", "w").close()
     while not os.path.exists(go_file):
         time.sleep(0.005)
@@ -82,12 +85,45 @@ def kfd_queue_count():
         return None
 
 
+def stuck_report(outs, regions, procs):
+    """Which pods never got ready, and what their regions say (limiter state, gates)."""
+    from amdvgpu.shim.region import Region
+    for o, reg, p in zip(outs, regions, procs):
+        if os.path.exists(o + ".ready"):
+            continue
+        info = {"pod": os.path.basename(o), "pid": p.pid, "exit": p.poll()}
+        try:
+            with Region(reg) as r:
+                snap = r.snapshot()
+            d = snap["devices"][0] if snap["devices"] else {}
+            info.update(suspended=snap["suspended"], recent_kernel=snap["recent_kernel"], samples=snap["samples"],
+                        credit_ms=d.get("credit_ns", 0) / 1e6, cu_mode=d.get("cu_mode"), crowd=d.get("crowd"),
+                        util_pct=d.get("util_pct"), procs=[{k: q[k] for k in ("pid", "hostpid", "launches",
+                                                                            "throttle_ns", "status")}
+                                                           for q in snap["procs"]])
+        except OSError as e:
+            info["region_error"] = str(e)
+        try:
+            with open(f"/proc/{p.pid}/wchan") as f:
+                info["wchan"] = f.read().strip()
+            info["threads"] = {}
+            for t in os.listdir(f"/proc/{p.pid}/task"):
+                with open(f"/proc/{p.pid}/task/{t}/wchan") as f:
+                    w = f.read().strip()
+                with open(f"/proc/{p.pid}/task/{t}/comm") as f:
+                    c = f.read().strip()
+                info["threads"][f"{t}:{c}"] = w
+        except OSError:
+            pass
+        print("STUCK " + json.dumps(info), flush=True)
+
+
 def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None, split=0):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="scal-")
     go = os.path.join(tmp, "go")
-    procs, outs = [], []
+    procs, outs, regions = [], [], []
     with NodeHarness(backend, device_split_count=split or n, cu_mode=MODES[policy]) as node:
         for i, vid in enumerate(node.vgpu_ids(uuid)[:n]):
             envs, mounts = node.pod([vid])
@@ -95,16 +131,18 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
             cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--case", case, "--warmup", str(warmup),
                    "--seconds", str(seconds), "--out", out, "--go", go]
             env = apply_contract(envs, mounts)
+            regions.append(env.get("VGPU_SHARED_CACHE"))
             if hw_queues:
                 env["GPU_MAX_HW_QUEUES"] = str(hw_queues)
             env.update(pod_env or {})
             procs.append(subprocess.Popen(cmd, env=env))
             outs.append(out)
         try:
-            deadline = time.time() + 600
+            deadline = time.time() + 300
             beat = time.time()
             while not all(os.path.exists(o + ".ready") for o in outs):
                 if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
+                    stuck_report(outs, regions, procs)
                     raise SystemExit("a tenant failed before the start barrier")
                 if time.time() - beat > 30:
                     beat = time.time()
