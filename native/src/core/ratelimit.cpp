@@ -81,9 +81,11 @@ uint64_t limiter_acquire(RegionHeader& h, DeviceState& d, bool limited, int64_t 
   }
   while (limited && !d.gate_open.load(std::memory_order_acquire)) {
     if (!t0) t0 = now_ns();
-    // Without a live sampler nobody repays the debt: never block forever.
+    // Without a live sampler nobody repays the debt: never block forever. The same when
+    // the device left the GPU-time limiter while this launch waited (cu_mode bit 2).
     uint64_t hb = h.watcher_heartbeat.load(std::memory_order_relaxed);
     if (!hb || now_ns() - hb > 1'000'000'000ull) break;
+    if (!(d.cu_mode.load(std::memory_order_relaxed) & 2)) break;
     nanosleep(&ts, nullptr);
   }
   return t0 ? now_ns() - t0 : 0;

@@ -516,6 +516,10 @@ void apply_live_config() {
     const bool may_mask = spatial || cfg.cu_mode == CuMode::kAuto;
     const bool slice = !off && may_mask && (limited || ranged) && m.count() < a.cu_count && m.count() > 0;
     a.visible_cus.store(slice && cfg.virtual_cu_count ? m.count() : 0);
+    // Leaving the GPU-time limiter (auto mode: the GPU calmed down; a live share change):
+    // nobody samples this device's credit any more, so a closed gate would never re-open
+    // and a launch blocked on it would wait forever. Open it.
+    if (!temp_on && !d.gate_open.load()) d.gate_open.store(1);
     a.temporal_active.store(temp_on);
     int flags = (mask_eff ? 1 : 0) | (temp_on ? 2 : 0);
     d.cu_mode.store(flags);

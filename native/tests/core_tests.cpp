@@ -708,6 +708,7 @@ static void test_ratelimit() {
   RegionHeader& h = r.raw()->hdr;
   d.credit_ns.store(1000);
   d.gate_open.store(1);
+  d.cu_mode.store(2);  // on the GPU-time limiter
   h.watcher_heartbeat.store(now_ns());
   CHECK(!limiter_would_block(h, d, true));
   CHECK_EQ(limiter_acquire(h, d, true), 0u);
@@ -725,6 +726,27 @@ static void test_ratelimit() {
   uint64_t waited = limiter_acquire(h, d, true);
   refill.join();
   CHECK(waited >= 20000000u);
+  // A launch blocked on the credit is released when the device leaves the GPU-time limiter
+  // (auto mode back on the CU mask): nobody would re-open the gate (profiles/r3g).
+  d.credit_ns.store(-100000);
+  d.gate_open.store(0);
+  std::atomic<bool> stop_hb{false};
+  std::thread hb([&] {
+    while (!stop_hb) {
+      h.watcher_heartbeat.store(now_ns());  // the maintenance thread stays alive
+      usleep(1000);
+    }
+  });
+  std::thread leave([&] {
+    usleep(30000);
+    d.cu_mode.store(1);
+  });
+  waited = limiter_acquire(h, d, true);
+  leave.join();
+  stop_hb = true;
+  hb.join();
+  CHECK(waited >= 20000000u && waited < 500000000u);
+  d.cu_mode.store(2);
   // A dead sampler (stale heartbeat) never blocks launches forever.
   d.credit_ns.store(-100000);
   d.gate_open.store(0);

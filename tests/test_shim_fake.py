@@ -474,3 +474,27 @@ def test_progress_charge_for_co_running_light_tenants(fake, tmp_path):
         assert p.returncode == 0
         fracs.append([json.loads(l) for l in out.splitlines() if '"run"' in l][0]["busy_frac"])
     assert all(abs(f - 0.5) <= 0.08 for f in fracs), fracs
+
+
+def test_blocked_launch_released_when_the_gpu_calms_down(fake, tmp_path):
+    """Auto mode: a pod on the GPU-time limiter (two busy neighbours) whose credit is
+    exhausted waits in the launch gate; when the neighbours stop, the pod goes back to its
+    CU mask - and the waiting launch must go on (nobody re-opens a gate the sampler no
+    longer looks after; profiles/r3g: a pod hung in warm-up this way)."""
+    import subprocess as sp
+    pod = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="25")  # auto mode (default)
+    pod["VGPU_SHARED_CACHE"] = str(tmp_path / "pod.cache")
+    neighbours = []
+    for i in range(2):
+        e = fake(gpus=1)
+        e["VGPU_SHARED_CACHE"] = str(tmp_path / f"n{i}.cache")
+        neighbours.append(sp.Popen([HARNESS, "stream", "run=2000,2.5"], env=e, stdout=sp.PIPE, text=True))
+    try:
+        # busy neighbours count for 5 s after their last waves, then 2 s of calm: the pod is
+        # back on its CU mask ~9.5 s in
+        out = run(pod, "stream", "run=2000,13", timeout=60)
+    finally:
+        for n in neighbours:
+            n.wait(timeout=60)
+    frac = [o for o in out if "run" in o][0]["busy_frac"]
+    assert frac > 0.3, frac  # crowded (25 %), then its own CUs again (~100 %)
