@@ -201,7 +201,14 @@ void sample_tick(Region* r, Sampler& sm) {
   if (conc > 0 || (refresh && sm.board.attached() && region_priority(r) >= kPrioBackground)) sm.board.refresh(now);
   for (int d = 0; d < s.n_agents; d++) {
     AgentInfo& a = s.agents[d];
-    if (!a.temporal_active.load(std::memory_order_relaxed) || !a.gpu_id) continue;
+    if (!a.temporal_active.load(std::memory_order_relaxed) || !a.gpu_id) {
+      if (sm.admitted[d] || sm.want_since[d]) {  // left the limiter: give up the turn
+        sm.admitted[d] = false;
+        sm.want_since[d] = 0;
+        sm.board.publish_gate(d, false, 0);
+      }
+      continue;
+    }
     DeviceState& ds = r->dev[d];
     if (refresh) {
       std::vector<int> on = kfd_pids_on_gpu(a.gpu_id);

@@ -51,12 +51,17 @@ RESNET_RATE = """
 import torch
 from amdvgpu.models.aibench import Runner, get_case
 torch.backends.cudnn.benchmark = True
-r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False)
+r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False, batch={batch})
 for _ in range(5): r.step()
 torch.cuda.synchronize()
 open(os.environ["VGPU_TEST_READY"], "w").close()
 while not os.path.exists(os.environ["VGPU_TEST_GO"]):
     time.sleep(0.002)
+reg = None
+if os.environ.get("VGPU_SHARED_CACHE"):
+    from amdvgpu.shim.region import Region
+    reg = Region(os.environ["VGPU_SHARED_CACHE"])
+    d0 = reg.device(0)
 n = 0
 t0 = time.perf_counter()
 while time.perf_counter() - t0 < {secs}:
@@ -65,7 +70,12 @@ while time.perf_counter() - t0 < {secs}:
     if n % 8 == 0:
         torch.cuda.synchronize()
 torch.cuda.synchronize()
-emit(rate=n / (time.perf_counter() - t0))
+rate = n / (time.perf_counter() - t0)
+busy = None
+if reg is not None:
+    d1 = reg.device(0)
+    busy = (d1["charged_ns"] - d0["charged_ns"]) / max(1, d1["wall_ns"] - d0["wall_ns"])
+emit(rate=rate, busy=busy)
 """
 
 
@@ -80,13 +90,14 @@ def _spin_rates(contracts, secs=3.0):
     return out
 
 
-def _resnet_rates(contracts, tmp_path, secs=4.0):
-    """Stock fp32 ResNet-50 inference tenants, released together after warm-up."""
+def _resnet_rates(contracts, tmp_path, secs=4.0, batch=None, full=False):
+    """Stock fp32 ResNet-50 inference tenants, released together after warm-up. Returns
+    each one's rate, or with ``full`` its result (rate and charged GPU-time fraction)."""
     go = str(tmp_path / "go")
     ps = []
     for i, c in enumerate(contracts):
         ready = str(tmp_path / f"ready{i}")
-        ps.append((spawn_child(RESNET_RATE.format(secs=secs), c,
+        ps.append((spawn_child(RESNET_RATE.format(secs=secs, batch=batch), c,
                                extra_env={"VGPU_TEST_READY": ready, "VGPU_TEST_GO": go}), ready))
     deadline = time.time() + 240
     while not all(os.path.exists(r) for _, r in ps):
@@ -97,7 +108,8 @@ def _resnet_rates(contracts, tmp_path, secs=4.0):
     for p, _ in ps:
         o, e = p.communicate(timeout=300)
         assert p.returncode == 0, e[-3000:]
-        out.append(child_results(o)[0]["rate"])
+        res = child_results(o)[0]
+        out.append(res if full else res["rate"])
     return out
 
 
@@ -133,6 +145,32 @@ def test_temporal_accuracy_two_tenants_stock_resnet(tmp_path):
             cleanup_region(c)
     achieved = [100.0 * g / native for g in got]
     assert all(abs(a - 25) <= 5.0 for a in achieved), achieved
+
+
+def test_temporal_four_light_tenants(tmp_path):
+    """Small-batch inference (ResNet-50 b=4, launch-bound: the GPU idles between kernels)
+    at 25 %, four tenants at once: each is charged 25 +- 5 % of the GPU's time, and each
+    gets within 5 points of what one such tenant gets alone at 25 % - co-running light
+    tenants neither steal from each other nor are over-charged (profiles/r3c)."""
+    for d in ("n", "s", "t"):
+        (tmp_path / d).mkdir()
+    native = _resnet_rates([None], tmp_path / "n", batch=4)[0]
+    solo = vgpu_env(cu_limit=25, cu_mode="temporal", mem_limit=32 * GiB)
+    cs = [vgpu_env(cu_limit=25, cu_mode="temporal", mem_limit=32 * GiB) for _ in range(4)]
+    try:
+        one = _resnet_rates([solo], tmp_path / "s", batch=4, full=True)[0]
+        four = _resnet_rates(cs, tmp_path / "t", batch=4, full=True)
+    finally:
+        for c in [solo] + cs:
+            cleanup_region(c)
+    alone = 100.0 * one["rate"] / native
+    together = [100.0 * r["rate"] / native for r in four]
+    busy = [100.0 * r["busy"] for r in four]
+    print(json.dumps({"native": native, "alone_pct": alone, "together_pct": together, "busy_pct": busy,
+                      "alone_busy_pct": 100.0 * one["busy"]}))
+    assert abs(100.0 * one["busy"] - 25.0) <= 5.0, one
+    assert all(abs(b - 25.0) <= 5.0 for b in busy), busy
+    assert all(abs(t - alone) <= 5.0 for t in together), (alone, together)
 
 
 CENSUS = """
