@@ -98,8 +98,9 @@ def worker(a):
     return 0
 
 
-def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=None):
-    """Starts one worker per pod (pods[i] in vGPU ids[i]), releases them together."""
+def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=None, bg_env=None):
+    """Starts one worker per pod (pods[i] in vGPU ids[i]), releases them together.
+    ``bg_env`` is added to the pods whose priority is background (>= 2)."""
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="mix-")
     go = os.path.join(tmp, "go")
@@ -109,6 +110,8 @@ def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=No
         env = apply_contract(envs, mounts)
         if priorities and priorities.get(pod["spec"]) is not None:
             env["VGPU_TASK_PRIORITY"] = str(priorities[pod["spec"]])
+            if priorities[pod["spec"]] >= 2:
+                env.update(bg_env or {})
         env.update(pod_env or {})
         out = os.path.join(tmp, f"p{i}.json")
         cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--case", pod["case"], "--batch",
@@ -140,16 +143,20 @@ def ab_compare(a, pods, backend, uuid, split, prio):
     runs = []
     with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode) as node:
         ids = node.vgpu_ids(uuid)[:len(pods)]
+        arms = [("default", None, None), ("priority", prio, None)]
+        if a.bg_env:
+            arms.append(("priority+bg-env", prio, a.bg_env))
         for i in range(a.ab):
-            for label, pr in (("default", None), ("priority", prio)):
-                res = run_pods(node, uuid, pods, ids, a.seconds, a.warmup, pr)
+            for label, pr, bg in arms:
+                res = run_pods(node, uuid, pods, ids, a.seconds, a.warmup, pr, bg_env=bg)
                 row = {"run": i, "label": label}
                 for pod, r in zip(pods, res):
                     row[pod["spec"]] = {k: round(v, 3) for k, v in r.items()
                                         if k in ("throughput", "p50_ms", "p99_ms", "mean_ms")}
                 runs.append(row)
                 print(json.dumps(row), flush=True)
-    md = [f"# default vs priority classes, ABAB x{a.ab} ({a.seconds:.0f} s windows, split {split})", "",
+    md = [f"# default vs priority classes, ABAB x{a.ab} ({a.seconds:.0f} s windows, split {split}"
+          + (f"; bg env {a.bg_env}" if a.bg_env else "") + ")", "",
           "| run | " + " | ".join(p["spec"] + (" P50 / P99 ms" if p["latency"] else " /s") for p in pods) + " |",
           "|---|" + "---|" * len(pods)]
     for r in runs:
@@ -158,7 +165,7 @@ def ab_compare(a, pods, backend, uuid, split, prio):
             v = r[p["spec"]]
             cells.append(f"{v['p50_ms']:.2f} / {v['p99_ms']:.2f}" if p["latency"] else f"{v['throughput']:.1f}")
         md.append(f"| {r['label']} #{r['run']} | " + " | ".join(cells) + " |")
-    for label in ("default", "priority"):
+    for label, _, _ in arms:
         sel = [r for r in runs if r["label"] == label]
         cells = []
         for p in pods:
@@ -172,7 +179,7 @@ def ab_compare(a, pods, backend, uuid, split, prio):
     text = "\n".join(md)
     print(text)
     if a.json_out:
-        json.dump({"pods": [p["spec"] for p in pods], "priorities": prio, "runs": runs}, open(a.json_out, "w"), indent=1)
+        json.dump({"pods": [p["spec"] for p in pods], "priorities": prio, "bg_env": a.bg_env, "runs": runs}, open(a.json_out, "w"), indent=1)
     if a.md_out:
         open(a.md_out, "w").write(text + "\n")
     return 0
@@ -189,6 +196,8 @@ def main():
     ap.add_argument("--ab", type=int, default=0,
                     help="skip the solo runs; alternate N times between the default and the --priority run "
                          "(ABAB...) and report each run's latency-pod P50 / P99 and pod throughputs")
+    ap.add_argument("--bg-env", default="", help="K=V,...: with --ab, a third arm where the background pods "
+                                                      "(priority >= 2) also get this env")
     ap.add_argument("--json-out")
     ap.add_argument("--md-out")
     ap.add_argument("--worker", action="store_true")
@@ -199,6 +208,7 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--go")
     a = ap.parse_args()
+    a.bg_env = dict(kv.split("=", 1) for kv in a.bg_env.split(",") if kv)
     if a.worker:
         return worker(a)
     from amdvgpu.plugin.devices import SysfsBackend
