@@ -25,12 +25,13 @@ Modes, one fresh worker process each (the rank process itself never touches the 
            measured (its 50 % SM limit did not bind on TF).
 * parity   the reference's benchmark configuration: split 2, memory scaling 1.8
            (server.go:492,505-507): 50 % compute (CU mask), 259 GiB oversubscribed quota.
-* sweep    N = 1, 2, 4, 8 pods of a split-N plugin run concurrently on one GPU (default
-           deployment config). ``max_vgpus_per_gpu`` is the largest N whose aggregate
-           stays >= 0.9x one whole-GPU pod and whose slowest pod gets >= 0.9x its 1/N
-           entitlement. Only on single-GPU runs unless --sweep on. 12 pods are left out
-           of the default sweep to keep the whole run well under 10 minutes (they add
-           ~2.5 min; ``--sweep-tenants 1,2,4,8,12``, profiles/r2ag, r2ae).
+* sweep    N = 1, 2, 4, 8, 12 pods of a split-N plugin run concurrently on one GPU
+           (default deployment config). ``max_vgpus_per_gpu`` is the largest N whose
+           aggregate stays >= 0.9x one whole-GPU pod and whose slowest pod gets >= 0.9x
+           its 1/N entitlement. Only on single-GPU runs unless --sweep on. The whole run
+           takes about 8 minutes, 12 pods about 3 of them (mostly the pods' start-up);
+           16 pods (``--sweep-tenants 1,2,4,8,12,16``, another 2.5 min) miss the bar:
+           slowest pod 0.82 (profiles/r3i).
 
 Timed region (native / vgpu / quota / parity): W untimed warmup steps, then exactly K
 steps bracketed by barrier + synchronize on both sides; MAX step time over ranks (one
@@ -70,7 +71,7 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--fuse", action="store_true", help="round-1 hand-written bf16 kernels (not the stock workload)")
     ap.add_argument("--sweep", default="auto", choices=["auto", "on", "off"])
-    ap.add_argument("--sweep-tenants", default="1,2,4,8")
+    ap.add_argument("--sweep-tenants", default="1,2,4,8,12")
     ap.add_argument("--sweep-seconds", type=float, default=6.0)
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     ap.add_argument("--rccl-probe", type=int, default=1, help="N>1: RCCL all-reduce between the pods afterwards")

@@ -149,17 +149,19 @@ def test_temporal_accuracy_two_tenants_stock_resnet(tmp_path):
 
 def test_temporal_four_light_tenants(tmp_path):
     """Small-batch inference (ResNet-50 b=4, launch-bound: the GPU idles between kernels)
-    at 25 %, four tenants at once: each is charged 25 +- 5 % of the GPU's time, and each
-    gets within 5 points of what one such tenant gets alone at 25 % - co-running light
-    tenants neither steal from each other nor are over-charged (profiles/r3c)."""
+    at 25 %, four tenants at once: each gets within 5 points of what one such tenant gets
+    alone at 25 % (co-running light tenants neither steal from each other nor are
+    over-charged), and none is charged more than its share of the GPU's time. Alone, the
+    tenant uses its whole 25 %; together the four share the GPU's instants, so each is
+    charged less (18-23 % in profiles/r3i) for about the same progress."""
     for d in ("n", "s", "t"):
         (tmp_path / d).mkdir()
     native = _resnet_rates([None], tmp_path / "n", batch=4)[0]
     solo = vgpu_env(cu_limit=25, cu_mode="temporal", mem_limit=32 * GiB)
     cs = [vgpu_env(cu_limit=25, cu_mode="temporal", mem_limit=32 * GiB) for _ in range(4)]
     try:
-        one = _resnet_rates([solo], tmp_path / "s", batch=4, full=True)[0]
-        four = _resnet_rates(cs, tmp_path / "t", batch=4, full=True)
+        one = _resnet_rates([solo], tmp_path / "s", secs=6.0, batch=4, full=True)[0]
+        four = _resnet_rates(cs, tmp_path / "t", secs=6.0, batch=4, full=True)
     finally:
         for c in [solo] + cs:
             cleanup_region(c)
@@ -169,7 +171,7 @@ def test_temporal_four_light_tenants(tmp_path):
     print(json.dumps({"native": native, "alone_pct": alone, "together_pct": together, "busy_pct": busy,
                       "alone_busy_pct": 100.0 * one["busy"]}))
     assert abs(100.0 * one["busy"] - 25.0) <= 5.0, one
-    assert all(abs(b - 25.0) <= 5.0 for b in busy), busy
+    assert all(b <= 25.0 + 3.0 for b in busy), busy
     assert all(abs(t - alone) <= 5.0 for t in together), (alone, together)
 
 
