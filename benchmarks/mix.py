@@ -98,7 +98,7 @@ def worker(a):
     return 0
 
 
-def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=None, bg_env=None):
+def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=None, bg_env=None, trace=None):
     """Starts one worker per pod (pods[i] in vGPU ids[i]), releases them together.
     ``bg_env`` is added to the pods whose priority is background (>= 2)."""
     from amdvgpu.shim.launcher import apply_contract
@@ -118,6 +118,10 @@ def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=No
                str(pod["batch"] or 0), "--seconds", str(seconds), "--warmup", str(warmup), "--out", out, "--go", go]
         if pod["latency"]:
             cmd += ["--latency", "--rate", str(pod["rate"])]
+            if trace:  # kernel trace of the latency pod (rocprofv3 starts the worker as its child)
+                os.makedirs(trace, exist_ok=True)
+                cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", trace, "-o", "lat",
+                       "--"] + cmd
         procs.append(subprocess.Popen(cmd, env=env))
         outs.append(out)
     try:
@@ -148,7 +152,8 @@ def ab_compare(a, pods, backend, uuid, split, prio):
             arms.append(("priority+bg-env", prio, a.bg_env))
         for i in range(a.ab):
             for label, pr, bg in arms:
-                res = run_pods(node, uuid, pods, ids, a.seconds, a.warmup, pr, bg_env=bg)
+                trace = os.path.join(a.trace_latency, f"{label}_{i}") if a.trace_latency else None
+                res = run_pods(node, uuid, pods, ids, a.seconds, a.warmup, pr, bg_env=bg, trace=trace)
                 row = {"run": i, "label": label}
                 for pod, r in zip(pods, res):
                     row[pod["spec"]] = {k: round(v, 3) for k, v in r.items()
@@ -198,6 +203,8 @@ def main():
                          "(ABAB...) and report each run's latency-pod P50 / P99 and pod throughputs")
     ap.add_argument("--bg-env", default="", help="K=V,...: with --ab, a third arm where the background pods "
                                                       "(priority >= 2) also get this env")
+    ap.add_argument("--trace-latency", default="", help="with --ab: rocprofv3 kernel trace of the latency pods "
+                                                          "under DIR/<arm>_<run>")
     ap.add_argument("--json-out")
     ap.add_argument("--md-out")
     ap.add_argument("--worker", action="store_true")

@@ -175,6 +175,59 @@ def test_temporal_four_light_tenants(tmp_path):
     assert all(abs(t - alone) <= 5.0 for t in together), (alone, together)
 
 
+LATENCY_SPIN = """
+import torch
+from amdvgpu.ops import spin
+spin(2048, 200); torch.cuda.synchronize()
+open(os.environ["VGPU_TEST_READY"], "w").close()
+t0 = time.perf_counter()
+while not os.path.exists(os.environ["VGPU_TEST_GO"]) and time.perf_counter() - t0 < 120:
+    spin(2048, 500)
+    torch.cuda.synchronize()
+emit(ok=True)
+"""
+
+
+def _background_rate_next_to(neighbour_prio, tmp_path):
+    """A background tenant (priority 2, GPU-time limiter at 50 %) spins for 3 s next to a
+    neighbour container of priority `neighbour_prio` that keeps the GPU busy."""
+    board = tmp_path / "board"
+    board.mkdir()
+    ready, stop = str(tmp_path / "ready"), str(tmp_path / "stop")
+    nb = vgpu_env(mem_limit=16 * GiB, extra={"VGPU_BOARD_DIR": str(board), "VGPU_BOARD_SLOT": "svc.slot",
+                                             "VGPU_TASK_PRIORITY": str(neighbour_prio)})
+    bg = vgpu_env(mem_limit=16 * GiB, cu_limit=50, cu_mode="temporal",
+                  extra={"VGPU_BOARD_DIR": str(board), "VGPU_BOARD_SLOT": "batch.slot", "VGPU_TASK_PRIORITY": "2"})
+    svc = spawn_child(LATENCY_SPIN, nb, extra_env={"VGPU_TEST_READY": ready, "VGPU_TEST_GO": stop})
+    try:
+        deadline = time.time() + 240
+        while not os.path.exists(ready):
+            assert time.time() < deadline and svc.poll() is None, "neighbour failed to start"
+            time.sleep(0.05)
+        time.sleep(1.0)  # on the board, busy
+        rate = _spin_rates([bg], secs=3.0)[0]
+    finally:
+        open(stop, "w").close()
+        svc.communicate(timeout=120)
+        cleanup_region(nb)
+        cleanup_region(bg)
+    return rate
+
+
+def test_background_class_yields_to_a_busy_latency_class(tmp_path):
+    """VGPU_TASK_PRIORITY=2 (background) earns no GPU time while a container of a better
+    class keeps the GPU busy (the board, vgpu/board.h), and runs at its share next to an
+    equal-class neighbour. This is what cuts the inference service's P99 next to
+    background trainers (profiles/r3d, r3j)."""
+    (tmp_path / "eq").mkdir()
+    (tmp_path / "lat").mkdir()
+    equal = _background_rate_next_to(2, tmp_path / "eq")
+    behind = _background_rate_next_to(0, tmp_path / "lat")
+    print(json.dumps({"next_to_equal": equal, "next_to_latency": behind}))
+    assert equal > 0, equal
+    assert behind < 0.3 * equal, (equal, behind)
+
+
 CENSUS = """
 import torch
 from amdvgpu.ops import cu_census
