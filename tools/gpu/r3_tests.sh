@@ -3,9 +3,8 @@
 # tests first), then smoke(). Each GPU step has its own time limit; output under $1.
 out=${1:-gpurun_out/r3}
 mkdir -p "$out"
-timeout -k 10 950 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_gpu_compiled.py tests/test_gpu_gates.py tests/test_gpu_shim.py tests/test_gpu_control.py \
-  tests/test_gpu_limits.py tests/test_gpu_e2e.py -p no:cacheprovider > "$out/pytest.log" 2>&1
+timeout -k 10 1000 python -u -m pytest -v -rfE --timeout 300 --timeout-method thread -m gpu tests/ \
+  -p no:cacheprovider > "$out/pytest.log" 2>&1
 rc=$?
 echo "pytest_rc=$rc" >> "$out/pytest.log"
 case $rc in 124|134|137|139) exit $rc ;; esac
