@@ -20,7 +20,8 @@ Optionally a further concurrent run with task priorities (``--priority``: e.g.
 priority 0 keeps its CU slice however crowded the GPU, priority >= 2 (background) yields
 GPU time while a higher-priority pod is busy (the node-wide board, vgpu/board.h).
 
-Pods are given as CASE[:BATCH][:lat][:rate=R], e.g. the default
+Pods are given as CASE[:BATCH][:lat][:rate=R][:nolimit] (nolimit: the pod has no compute
+share, memory quota only), e.g. the default
     resnet50-inf:1:lat vgg16-train lstm-train deeplab-inf
 Every contract comes from an Allocate of the plugin (NodeHarness, sysfs backend).
 
@@ -42,15 +43,17 @@ DEFAULT_PODS = ["resnet50-inf:1:lat", "vgg16-train", "lstm-train", "deeplab-inf"
 
 def parse_pod(spec):
     parts = spec.split(":")
-    case, batch, lat, rate = parts[0], None, False, 100.0
+    case, batch, lat, rate, nolimit = parts[0], None, False, 100.0, False
     for p in parts[1:]:
         if p == "lat":
             lat = True
+        elif p == "nolimit":
+            nolimit = True
         elif p.startswith("rate="):
             rate = float(p[5:])
         elif p:
             batch = int(p)
-    return {"spec": spec, "case": case, "batch": batch, "latency": lat, "rate": rate}
+    return {"spec": spec, "case": case, "batch": batch, "latency": lat, "rate": rate, "nolimit": nolimit}
 
 
 def worker(a):
@@ -108,6 +111,9 @@ def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=No
     for i, (pod, vid) in enumerate(zip(pods, ids)):
         envs, mounts = node.pod([vid])
         env = apply_contract(envs, mounts)
+        if pod["nolimit"]:  # no compute share (memory quota only): the whole GPU, unless a class rule applies
+            for k in [k for k in env if k.startswith("VGPU_DEVICE_CU_LIMIT") or k.startswith("VGPU_DEVICE_CU_RANGE")]:
+                del env[k]
         if priorities and priorities.get(pod["spec"]) is not None:
             env["VGPU_TASK_PRIORITY"] = str(priorities[pod["spec"]])
             if priorities[pod["spec"]] >= 2:

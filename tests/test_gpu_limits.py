@@ -272,6 +272,51 @@ def test_auto_mode_picks_enforcement(tmp_region, tmp_path, pct, neighbours, mode
     assert res[0]["crowd"] == neighbours or pct >= 50, res
 
 
+SLICE_HOLDER = """
+import torch
+from amdvgpu.ops import cu_census
+time.sleep(1.5)
+emit(cus=sorted(cu_census(nblocks=8192, spin_us=300)))
+t0 = time.perf_counter()
+while not os.path.exists(os.environ["VGPU_TEST_GO"]) and time.perf_counter() - t0 < 120:
+    time.sleep(0.05)
+"""
+
+BG_CENSUS = """
+import torch
+from amdvgpu.ops import cu_census
+time.sleep(1.5)   # the lease holder reads the board and re-masks the queues
+emit(cus=sorted(cu_census(nblocks=8192, spin_us=300)))
+"""
+
+
+def test_background_class_keeps_off_the_latency_slice(tmp_path):
+    """A latency-class container (priority 0, 25 %: its 64-CU slice) publishes its slice on
+    the board; a background container (priority 2) on the same GPU runs its kernels on the
+    other 192 CUs only - the real-hardware check of the board's CU reservation."""
+    board = tmp_path / "board"
+    board.mkdir()
+    go = str(tmp_path / "go")
+    lat = vgpu_env(mem_limit=16 * GiB, cu_limit=25, extra={"VGPU_BOARD_DIR": str(board), "VGPU_BOARD_SLOT": "svc.slot",
+                                                           "VGPU_TASK_PRIORITY": "0"})
+    bg = vgpu_env(mem_limit=16 * GiB, extra={"VGPU_BOARD_DIR": str(board), "VGPU_BOARD_SLOT": "batch.slot",
+                                             "VGPU_TASK_PRIORITY": "2"})
+    svc = spawn_child(SLICE_HOLDER, lat, extra_env={"VGPU_TEST_GO": go})
+    try:
+        line = svc.stdout.readline()
+        assert line.startswith("RESULT"), svc.stderr.read()[-3000:]
+        mine = {tuple(c) for c in json.loads(line[7:])["cus"]}
+        res, _ = run_child(BG_CENSUS, bg)
+    finally:
+        open(go, "w").close()
+        svc.communicate(timeout=60)
+        cleanup_region(lat)
+        cleanup_region(bg)
+    theirs = {tuple(c) for c in res[0]["cus"]}
+    assert len(mine) == 64, len(mine)
+    assert len(theirs) == 192 and not (mine & theirs), (len(theirs), sorted(mine & theirs)[:8])
+
+
 LIVE = """
 import torch
 from amdvgpu.ops import cu_census, spin
