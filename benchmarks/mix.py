@@ -70,7 +70,8 @@ def worker(a):
         time.sleep(0.005)
     import random
     rng = random.Random(1234)
-    lat = []
+    lat, gpu = [], []
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     n = 0
     t0 = time.perf_counter()
     arrival = t0
@@ -81,9 +82,12 @@ def worker(a):
             now = time.perf_counter()
             if arrival > now:
                 time.sleep(arrival - now)
+            ev0.record()
             r.step()
+            ev1.record()
             torch.cuda.synchronize()
             lat.append(time.perf_counter() - arrival)
+            gpu.append(ev0.elapsed_time(ev1))  # the request on the GPU: its kernels and the gaps between them
         else:
             r.step()
             if n % 2 == 1:
@@ -97,6 +101,9 @@ def worker(a):
         res["p50_ms"] = 1000 * lat[len(lat) // 2]
         res["p99_ms"] = 1000 * lat[min(len(lat) - 1, int(len(lat) * 0.99))]
         res["mean_ms"] = 1000 * sum(lat) / len(lat)
+        gpu.sort()
+        res["gpu_p50_ms"] = gpu[len(gpu) // 2]
+        res["gpu_p99_ms"] = gpu[min(len(gpu) - 1, int(len(gpu) * 0.99))]
     json.dump(res, open(a.out, "w"))
     return 0
 
@@ -137,8 +144,9 @@ def run_pods(node, uuid, pods, ids, seconds, warmup, priorities=None, pod_env=No
                 raise SystemExit("a pod failed before the start barrier")
             time.sleep(0.05)
         open(go, "w").close()
+        end = time.time() + seconds + 240  # the timed window, then the pods' exit (a profiler may hang there)
         for p in procs:
-            if p.wait(timeout=900) != 0:
+            if p.wait(timeout=max(1.0, end - time.time())) != 0:
                 raise SystemExit("a pod failed")
         return [json.load(open(o)) for o in outs]
     finally:
@@ -168,13 +176,15 @@ def ab_compare(a, pods, backend, uuid, split, prio):
                 print(json.dumps(row), flush=True)
     md = [f"# default vs priority classes, ABAB x{a.ab} ({a.seconds:.0f} s windows, split {split}"
           + (f"; bg env {a.bg_env}" if a.bg_env else "") + ")", "",
-          "| run | " + " | ".join(p["spec"] + (" P50 / P99 ms" if p["latency"] else " /s") for p in pods) + " |",
+          "| run | " + " | ".join(p["spec"] + (" P50 / P99 ms (on the GPU P50 / P99)" if p["latency"] else " /s")
+                                  for p in pods) + " |",
           "|---|" + "---|" * len(pods)]
     for r in runs:
         cells = []
         for p in pods:
             v = r[p["spec"]]
-            cells.append(f"{v['p50_ms']:.2f} / {v['p99_ms']:.2f}" if p["latency"] else f"{v['throughput']:.1f}")
+            cells.append(f"{v['p50_ms']:.2f} / {v['p99_ms']:.2f} ({v.get('gpu_p50_ms', 0):.2f} / {v.get('gpu_p99_ms', 0):.2f})"
+                         if p["latency"] else f"{v['throughput']:.1f}")
         md.append(f"| {r['label']} #{r['run']} | " + " | ".join(cells) + " |")
     for label, _, _ in arms:
         sel = [r for r in runs if r["label"] == label]

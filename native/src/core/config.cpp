@@ -12,7 +12,9 @@
 namespace vgpu {
 
 namespace {
-Config g_config;
+// Never destroyed: the shim's maintenance thread and hooks the runtime calls during its
+// own teardown read the configuration after static destructors have started to run.
+Config& g_config = *new Config();
 
 bool parse_bool(const char* s, bool dflt) {
   if (!s || !*s) return dflt;
