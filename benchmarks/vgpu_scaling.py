@@ -198,11 +198,16 @@ def main():
         k, _, vals = spec.partition("=")
         envs = [dict(e, **{k: v}) for e in envs for v in vals.split(",")]
     for rep in range(a.repeats):
-        for pe in envs:
+        for k, pe in enumerate(envs):
             for hq in [int(x) for x in a.hw_queues.split(",")]:
                 for pol in a.policy.split(","):
                     for n in [int(x) for x in a.tenants.split(",")]:
-                        r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq, pe, a.split)
+                        # The lone pod is the whole-GPU reference point: run once per
+                        # repeat, without the pod env under study.
+                        if n == 1 and k > 0:
+                            continue
+                        r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq,
+                                      pe if n > 1 else None, a.split)
                         rows.append(r)
                         print(json.dumps(r), flush=True)
     base = {r["policy"]: r["aggregate_throughput"] for r in rows if r["tenants"] == 1}
