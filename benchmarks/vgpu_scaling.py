@@ -138,8 +138,8 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
             procs.append(subprocess.Popen(cmd, env=env))
             outs.append(out)
         try:
-            deadline = time.time() + 300
-            beat = time.time()
+            t_start = beat = time.time()
+            deadline = t_start + 300
             while not all(os.path.exists(o + ".ready") for o in outs):
                 if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
                     stuck_report(outs, regions, procs)
@@ -149,6 +149,7 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
                     print(f"  waiting: {sum(os.path.exists(o + '.ready') for o in outs)}/{n} pods warmed up",
                           flush=True)
                 time.sleep(0.05)
+            warm_s = time.time() - t_start
             queues = kfd_queue_count()
             open(go, "w").close()
             for p in procs:
@@ -162,7 +163,7 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
     span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
     agg = sum(r["batch"] * r["steps"] for r in res) / span
     return {"tenants": n, "policy": policy, "split": split or n, "hw_queues": hw_queues or None, "kfd_queues": queues,
-            "pod_env": pod_env or None, "modes": sorted({str(r.get("cu_mode")) for r in res}),
+            "warmup_s": round(warm_s, 1), "pod_env": pod_env or None, "modes": sorted({str(r.get("cu_mode")) for r in res}),
             "aggregate_throughput": agg,
             "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res],
             "per_tenant_granted_pct": [r.get("granted_pct") for r in res],
