@@ -29,9 +29,9 @@ Modes, one fresh worker process each (the rank process itself never touches the 
            (default deployment config). ``max_vgpus_per_gpu`` is the largest N whose
            aggregate stays >= 0.9x one whole-GPU pod and whose slowest pod gets >= 0.9x
            its 1/N entitlement. Only on single-GPU runs unless --sweep on. The whole run
-           takes about 8 minutes, 12 pods about 3 of them (mostly the pods' start-up);
-           16 pods (``--sweep-tenants 1,2,4,8,12,16``, another 2.5 min) miss the bar:
-           slowest pod 0.82 (profiles/r3i).
+           takes about 8 minutes, 12 pods about 3 of them (mostly the pods' start-up).
+           ``--time-budget`` (default 540 s) bounds the run: a point whose estimated
+           duration would overrun it is skipped and listed as such in ``sweep``.
 
 Timed region (native / vgpu / quota / parity): W untimed warmup steps, then exactly K
 steps bracketed by barrier + synchronize on both sides; MAX step time over ranks (one
@@ -50,6 +50,7 @@ import sys
 import tempfile
 import time
 
+T_START = time.time()
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
@@ -73,6 +74,9 @@ def parse(argv=None):
     ap.add_argument("--sweep", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--sweep-tenants", default="1,2,4,8,12")
     ap.add_argument("--sweep-seconds", type=float, default=6.0)
+    ap.add_argument("--time-budget", type=float, default=540.0,
+                    help="wall seconds for the whole run: sweep points that would not finish in time are "
+                         "skipped (and reported as such), so the line is always printed")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     ap.add_argument("--rccl-probe", type=int, default=1, help="N>1: RCCL all-reduce between the pods afterwards")
     # worker-only
@@ -303,8 +307,17 @@ def probe_rccl(args, env, port, timeout=120):
         os.unlink(result)
 
 
-def run_concurrent(args, envs, label):
-    """Starts one tenant per env, releases them together, returns their results."""
+def now():
+    return time.time()
+
+
+class OutOfTime(Exception):
+    pass
+
+
+def run_concurrent(args, envs, label, deadline=None):
+    """Starts one tenant per env, releases them together, returns their results. Raises
+    OutOfTime when the tenants are not all warmed up by ``deadline`` (epoch seconds)."""
     tmp = tempfile.mkdtemp(prefix=f"bench-{label}-")
     go = os.path.join(tmp, "go")
     procs, outs = [], []
@@ -314,11 +327,14 @@ def run_concurrent(args, envs, label):
                                       env=env))
         outs.append(out)
     try:
-        deadline = time.time() + 900
         t_start = beat = time.time()
+        deadline = deadline or t_start + 900
         while not all(os.path.exists(o + ".ready") for o in outs):
-            if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
+            if any(p.poll() not in (None, 0) for p in procs):
                 raise SystemExit(f"a {label} tenant failed before the start barrier")
+            if time.time() > deadline:
+                raise OutOfTime(f"{sum(os.path.exists(o + '.ready') for o in outs)}/{len(outs)} tenants warmed up "
+                                f"after {time.time() - t_start:.0f} s")
             if time.time() - beat > 30:
                 beat = time.time()
                 print(f"[bench] {label}: {sum(os.path.exists(o + '.ready') for o in outs)}/{len(outs)} tenants "
@@ -339,14 +355,31 @@ def run_concurrent(args, envs, label):
 
 def sweep(args, backend, uuid, tenants):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
-    rows = []
+    rows, skipped = [], []
+    end = T_START + args.time_budget
+    last = None  # (pods, seconds) of the last measured point with several pods
     for n in tenants:
-        t_point = time.time()
-        with NodeHarness(backend, device_split_count=n, cu_mode=args.cu_mode) as node:
-            ids = node.vgpu_ids(uuid)[:n]
-            pods = [pod_env(node, [i]) for i in ids]
-            res = run_concurrent(args, [e for e, _ in pods], f"sweep{n}")
-            c0 = pods[0][1]
+        t_point = now()
+        # Start-up dominates a point and grows about linearly with the pods (each warms up,
+        # MIOpen find included, on its share of the GPU): skip what would not finish.
+        est = last[1] * n / last[0] if last else 20.0 + 8.0 * n
+        if t_point + est > end:
+            skipped.append({"tenants": n, "skipped": f"time budget: ~{est:.0f} s needed, {end - t_point:.0f} s left"})
+            print(f"[bench] sweep {n} tenants skipped ({skipped[-1]['skipped']})", file=sys.stderr, flush=True)
+            continue
+        try:
+            with NodeHarness(backend, device_split_count=n, cu_mode=args.cu_mode) as node:
+                ids = node.vgpu_ids(uuid)[:n]
+                pods = [pod_env(node, [i]) for i in ids]
+                res = run_concurrent(args, [e for e, _ in pods], f"sweep{n}",
+                                     deadline=end - args.sweep_seconds - 15.0)
+                c0 = pods[0][1]
+        except OutOfTime as e:
+            skipped.append({"tenants": n, "skipped": f"time budget: {e}"})
+            print(f"[bench] sweep {n} tenants abandoned ({e})", file=sys.stderr, flush=True)
+            continue
+        if n > 1:
+            last = (n, now() - t_point)
         tput = [r["items_per_step"] * r["steps"] / (r["t1"] - r["t0"]) for r in res]
         span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
         agg = sum(r["items_per_step"] * r["steps"] for r in res) / span
@@ -354,7 +387,7 @@ def sweep(args, backend, uuid, tenants):
                      "cu_limit_pct": int(c0.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0),
                      "cu_mode": c0.get("VGPU_CU_MODE"), "quota_mib": int(c0["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m"))})
         print(f"[bench] sweep {n} tenants: aggregate {agg:.1f}, per tenant {min(tput):.1f}..{max(tput):.1f} "
-              f"({time.time() - t_point:.0f} s)", file=sys.stderr, flush=True)
+              f"({now() - t_point:.0f} s)", file=sys.stderr, flush=True)
     base = next((r["aggregate"] for r in rows if r["tenants"] == 1), None)
     best = 0
     for r in rows:
@@ -365,7 +398,7 @@ def sweep(args, backend, uuid, tenants):
         r["ok"] = r["aggregate_vs_one"] >= SWEEP_MIN_AGGREGATE and r["min_tenant_vs_entitlement"] >= SWEEP_MIN_TENANT
         if r["ok"]:
             best = max(best, r["tenants"])
-    return rows, best
+    return rows + skipped, best
 
 
 def main(argv=None):
@@ -500,7 +533,7 @@ def main(argv=None):
         line["max_vgpus_per_gpu"] = max_vgpus
         line["max_vgpus_criterion"] = (f"largest N with aggregate >= {SWEEP_MIN_AGGREGATE}x one whole-GPU pod and "
                                        f"slowest pod >= {SWEEP_MIN_TENANT}x its 1/N entitlement "
-                                       f"(tested N = {args.sweep_tenants})")
+                                       f"(tested N = {','.join(str(r['tenants']) for r in sweep_rows if 'skipped' not in r)})")
         line["sweep"] = sweep_rows
     line["baseline_vgpu_v100"] = case.baseline_vgpu
     out = json.dumps(line)

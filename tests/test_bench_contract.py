@@ -55,3 +55,31 @@ def test_bench_multi_rank_cpu_rehearsal(world, tmp_path):
         assert None not in vals and len(set(vals)) == len(vals), key
     locks = {x["uuid"]: {pod["VGPU_LOCK_FILE"] for pod in x["pods"].values()} for x in ranks}
     assert len({lf for s in locks.values() for lf in s}) == 3 * world  # one per plugin instance
+
+
+def test_sweep_respects_the_time_budget(monkeypatch):
+    """The driver kills bench.py at its own limit: sweep points that would not finish within
+    --time-budget are skipped and reported, and max_vgpus_per_gpu only counts measured points."""
+    sys.path.insert(0, REPO)
+    import bench
+    from amdvgpu.plugin.devices import FakeBackend
+
+    clock = [1000.0]
+    monkeypatch.setattr(bench, "now", lambda: clock[0])
+    monkeypatch.setattr(bench, "T_START", 1000.0)
+
+    def fake_run(args, envs, label, deadline=None):
+        n = len(envs)
+        clock[0] += 10.0 * n  # start-up grows with the pods
+        per = 4000.0 / n
+        return [{"items_per_step": 50, "steps": int(per * 6 / 50), "t0": 0.0, "t1": 6.0} for _ in envs]
+
+    monkeypatch.setattr(bench, "run_concurrent", fake_run)
+    args = bench.parse(["--time-budget", "200", "--sweep-seconds", "6"])
+    backend = FakeBackend(n=1)
+    rows, best = bench.sweep(args, backend, backend.devices()[0].uuid, [1, 2, 4, 8, 12])
+    measured = [r["tenants"] for r in rows if "skipped" not in r]
+    skipped = [r["tenants"] for r in rows if "skipped" in r]
+    # 1 + 2 + 4 pods take 70 s; 8 pods are estimated at 80 s (150 < 200: run), 12 at 120 s.
+    assert measured == [1, 2, 4, 8] and skipped == [12], rows
+    assert best == 8
