@@ -74,6 +74,9 @@ def parse(argv=None):
     ap.add_argument("--sweep", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--sweep-tenants", default="1,2,4,8,12")
     ap.add_argument("--sweep-seconds", type=float, default=6.0)
+    ap.add_argument("--sweep-find-db", default="own", choices=["own", "shared"],
+                    help="shared: the sweep's pods use one MIOpen find-db, filled by the lone pod (as a "
+                         "tenant image with a tuned find-db would ship); own: every pod runs its own find")
     ap.add_argument("--time-budget", type=float, default=540.0,
                     help="wall seconds for the whole run: sweep points that would not finish in time are "
                          "skipped (and reported as such), so the line is always printed")
@@ -354,9 +357,36 @@ def run_concurrent(args, envs, label, deadline=None):
 
 
 def sweep(args, backend, uuid, tenants):
-    from amdvgpu.plugin.kubelet_stub import NodeHarness
+    import shutil
     rows, skipped = [], []
     end = T_START + args.time_budget
+    extra, db = None, None
+    if args.sweep_find_db == "shared":
+        db = tempfile.mkdtemp(prefix="bench-miopen-")
+        extra = {"MIOPEN_USER_DB_PATH": os.path.join(db, "db"), "MIOPEN_CUSTOM_CACHE_DIR": os.path.join(db, "cache")}
+        for d in extra.values():
+            os.makedirs(d)
+    try:
+        rows, skipped = _sweep_points(args, backend, uuid, tenants, end, extra)
+    finally:
+        if db:
+            shutil.rmtree(db, ignore_errors=True)
+    base = next((r["aggregate"] for r in rows if r["tenants"] == 1), None)
+    best = 0
+    for r in rows:
+        if not base:
+            break
+        r["aggregate_vs_one"] = round(r["aggregate"] / base, 3)
+        r["min_tenant_vs_entitlement"] = round(min(r["per_tenant"]) / (base / r["tenants"]), 3)
+        r["ok"] = r["aggregate_vs_one"] >= SWEEP_MIN_AGGREGATE and r["min_tenant_vs_entitlement"] >= SWEEP_MIN_TENANT
+        if r["ok"]:
+            best = max(best, r["tenants"])
+    return rows + skipped, best
+
+
+def _sweep_points(args, backend, uuid, tenants, end, extra):
+    from amdvgpu.plugin.kubelet_stub import NodeHarness
+    rows, skipped = [], []
     last = None  # (pods, seconds) of the last measured point with several pods
     for n in tenants:
         t_point = now()
@@ -370,7 +400,7 @@ def sweep(args, backend, uuid, tenants):
         try:
             with NodeHarness(backend, device_split_count=n, cu_mode=args.cu_mode) as node:
                 ids = node.vgpu_ids(uuid)[:n]
-                pods = [pod_env(node, [i]) for i in ids]
+                pods = [pod_env(node, [i], extra) for i in ids]
                 res = run_concurrent(args, [e for e, _ in pods], f"sweep{n}",
                                      deadline=end - args.sweep_seconds - 15.0)
                 c0 = pods[0][1]
@@ -388,17 +418,7 @@ def sweep(args, backend, uuid, tenants):
                      "cu_mode": c0.get("VGPU_CU_MODE"), "quota_mib": int(c0["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m"))})
         print(f"[bench] sweep {n} tenants: aggregate {agg:.1f}, per tenant {min(tput):.1f}..{max(tput):.1f} "
               f"({now() - t_point:.0f} s)", file=sys.stderr, flush=True)
-    base = next((r["aggregate"] for r in rows if r["tenants"] == 1), None)
-    best = 0
-    for r in rows:
-        if not base:
-            break
-        r["aggregate_vs_one"] = round(r["aggregate"] / base, 3)
-        r["min_tenant_vs_entitlement"] = round(min(r["per_tenant"]) / (base / r["tenants"]), 3)
-        r["ok"] = r["aggregate_vs_one"] >= SWEEP_MIN_AGGREGATE and r["min_tenant_vs_entitlement"] >= SWEEP_MIN_TENANT
-        if r["ok"]:
-            best = max(best, r["tenants"])
-    return rows + skipped, best
+    return rows, skipped
 
 
 def main(argv=None):
@@ -535,6 +555,7 @@ def main(argv=None):
                                        f"slowest pod >= {SWEEP_MIN_TENANT}x its 1/N entitlement "
                                        f"(tested N = {','.join(str(r['tenants']) for r in sweep_rows if 'skipped' not in r)})")
         line["sweep"] = sweep_rows
+        line["sweep_find_db"] = args.sweep_find_db
     line["baseline_vgpu_v100"] = case.baseline_vgpu
     out = json.dumps(line)
     print(out, flush=True)
