@@ -272,6 +272,7 @@ hipError_t hipFree(void* ptr) {
   ShimState& s = shim();
   if (__builtin_expect(s.active && ptr != nullptr, 1)) {
     AllocRec rec{0, -1, 0};
+    bool pinned = false;
     {
       std::lock_guard<std::mutex> g(s.alloc_mu);
       if (!s.managed.empty()) {
@@ -281,8 +282,15 @@ hipError_t hipFree(void* ptr) {
           s.managed.erase(it);
         }
       }
+      pinned = !s.host.empty() && s.host.count(reinterpret_cast<uintptr_t>(ptr));
     }
     if (rec.dev >= 0 && s.slot >= 0 && !s.exiting.load()) s.region.uncharge(s.slot, rec.dev, rec.size, kMemData);
+    if (pinned) {
+      // hipFree also releases pinned host memory (hipHostMalloc): the host budget follows.
+      hipError_t e = real_hipFree(ptr);
+      if (e == hipSuccess) release_host(ptr);
+      return e;
+    }
   }
   return real_hipFree(ptr);
 }

@@ -41,7 +41,11 @@ void record(void* p, size_t size) {
   s.host[reinterpret_cast<uintptr_t>(p)] = size;
 }
 
-void release(void* p) {
+}  // namespace
+
+namespace vgpu {
+
+void release_host(void* p) {
   ShimState& s = shim();
   if (!p || !s.active) return;
   uint64_t size = 0;
@@ -54,6 +58,10 @@ void release(void* p) {
   }
   if (s.slot >= 0 && !s.exiting.load()) s.region.uncharge_host(s.slot, size);
 }
+
+}  // namespace vgpu
+
+namespace {
 
 // Admission around the runtime's allocation. The first HIP call of a process initialises
 // the runtime (and the shim, from the hsa_init hook) inside the real call, so a process
@@ -121,7 +129,7 @@ hipError_t hipHostFree(void* ptr) {
   VGPU_REAL_AS(hipHostFree, FreeFn, "libamdhip64", nullptr);
   if (!real_hipHostFree) return hipErrorNotSupported;
   gate_suspend();
-  release(ptr);
+  release_host(ptr);
   return real_hipHostFree(ptr);
 }
 
@@ -129,7 +137,7 @@ hipError_t hipFreeHost(void* ptr) {
   VGPU_REAL_AS(hipFreeHost, FreeFn, "libamdhip64", nullptr);
   if (!real_hipFreeHost) return hipErrorNotSupported;
   gate_suspend();
-  release(ptr);
+  release_host(ptr);
   return real_hipFreeHost(ptr);
 }
 
@@ -149,7 +157,7 @@ hipError_t hipHostUnregister(void* host_ptr) {
   if (!real_hipHostUnregister) return hipErrorNotSupported;
   gate_suspend();
   hipError_t e = real_hipHostUnregister(host_ptr);
-  if (e == hipSuccess) release(host_ptr);
+  if (e == hipSuccess) release_host(host_ptr);
   return e;
 }
 

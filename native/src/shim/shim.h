@@ -150,6 +150,10 @@ pid_t resolve_hostpid(int lock_timeout_ms);
 // [context.c:49-86], [export_table.c:85-113]).
 void resync_context_charge();
 
+// Drops the pinned host-memory charge of `p` (host_hooks.cpp) if the shim recorded it:
+// called after the runtime freed or unregistered it, through whichever entry point.
+void release_host(void* p);
+
 // The agent ordinal of HIP device `hipdev` (hipGetDevice / hipSetDevice numbering),
 // matched by PCI address: HIP_VISIBLE_DEVICES inside the container may reorder or hide
 // devices. Identity with one agent, or when the addresses are ambiguous (partitions).

@@ -21,6 +21,7 @@
 #include <condition_variable>
 #include <deque>
 #include <mutex>
+#include <set>
 #include <thread>
 
 extern "C" int fake_rocr_set_occupancy(int dev, int cus);
@@ -180,8 +181,18 @@ hipError_t hipMalloc(void** ptr, size_t size) {
   return s == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorOutOfMemory;
 }
 
+static std::mutex g_host_mu;
+static std::set<void*> g_host;  // hipHostMalloc'd pointers (hipFree releases them too, as CLR does)
+
 hipError_t hipFree(void* ptr) {
   if (!ptr) return hipSuccess;
+  {
+    std::lock_guard<std::mutex> l(g_host_mu);
+    if (g_host.erase(ptr)) {
+      free(ptr);
+      return hipSuccess;
+    }
+  }
   return hsa_amd_memory_pool_free(ptr) == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorInvalidValue;
 }
 
@@ -287,10 +298,17 @@ hipError_t hipGetProcAddress(const char* symbol, void** pfn, int, uint64_t, hipD
 hipError_t hipHostMalloc(void** ptr, size_t size, unsigned int) {
   init();
   *ptr = malloc(size ? size : 1);
-  return *ptr ? hipSuccess : hipErrorOutOfMemory;
+  if (!*ptr) return hipErrorOutOfMemory;
+  std::lock_guard<std::mutex> l(g_host_mu);
+  g_host.insert(*ptr);
+  return hipSuccess;
 }
 
 hipError_t hipHostFree(void* ptr) {
+  {
+    std::lock_guard<std::mutex> l(g_host_mu);
+    g_host.erase(ptr);
+  }
   free(ptr);
   return hipSuccess;
 }

@@ -31,6 +31,7 @@
 //                    shim's, "ungated": names that did not block, "unreached": names whose
 //                    call never reached the runtime}
 //   hostmalloc=SIZE  hipHostMalloc -> {"hostmalloc": "ok"|"oom"}; hostfree frees the last one
+//                    (hostfree_hipfree: through hipFree, which releases pinned memory too)
 //   hostregister=SIZE  hipHostRegister of a fresh heap buffer -> {"hostregister": "ok"|"oom"};
 //                    hostunregister unregisters (and frees) the last one
 #define __HIP_PLATFORM_AMD__ 1
@@ -261,6 +262,12 @@ int main(int argc, char** argv) {
     } else if (key == "hostfree") {
       if (!host_ptrs.empty()) {
         (void)hipHostFree(host_ptrs.back());
+        host_ptrs.pop_back();
+      }
+      printf("{\"hostfree\": true}\n");
+    } else if (key == "hostfree_hipfree") {
+      if (!host_ptrs.empty()) {
+        (void)hipFree(host_ptrs.back());
         host_ptrs.pop_back();
       }
       printf("{\"hostfree\": true}\n");

@@ -138,6 +138,14 @@ def test_pinned_host_memory_budget(fake_env):
         assert r.host() == {"limit": 64 << 20, "used": 0}  # the harness exited: its slot was released
 
 
+def test_pinned_host_memory_freed_with_hipfree(fake_env):
+    """hipFree releases hipHostMalloc'd memory too (CLR accepts it): the budget follows, so
+    a tenant freeing pinned buffers that way is not refused later."""
+    fake_env["VGPU_HOST_MEMORY_LIMIT"] = "64m"
+    out = run_harness(fake_env, "hostmalloc=40m", "hostfree_hipfree", "hostmalloc=40m", "hostmalloc=40m")
+    assert [o["hostmalloc"] for o in out if "hostmalloc" in o] == ["ok", "ok", "oom"], out
+
+
 def test_pinned_host_memory_shared_by_the_container(fake_env):
     """Processes of one container share the host budget: the region holds the aggregate."""
     from amdvgpu.shim.region import Region
