@@ -134,7 +134,7 @@ def write_allowlist(vgpu_dir, name, uuids):
 SHARED_GRACE_S = 300
 
 
-def gc_shared_dirs(root, pods, grace_s=SHARED_GRACE_S, now=None):
+def gc_shared_dirs(root, pods, grace_s=SHARED_GRACE_S, now=None, held=None):
     """Removes the monitor-mode host directories (<ns>_<pod>_<ctr>/<uuid>.cache) of pods
     that no longer exist on this node; the reference never removes them.
 
@@ -146,7 +146,9 @@ def gc_shared_dirs(root, pods, grace_s=SHARED_GRACE_S, now=None):
     Failed owns its tag - same namespace, name and container, and the UID in the
     ``.pod-uid`` marker when there is one (a re-created pod of the same name gets a fresh
     directory, so the old one goes). ``pods=None`` (no pod list) removes nothing; a
-    directory younger than ``grace_s`` is never removed. Returns the removed tags."""
+    directory younger than ``grace_s`` is never removed, nor one whose recorded device IDs
+    (``.devices``) a live container holds according to the kubelet's PodResources
+    (``held``: a set of frozensets of device IDs). Returns the removed tags."""
     import shutil
     import time
     from .k8s import POD_MARKER, TERMINAL_PHASES, pod_tag
@@ -169,6 +171,11 @@ def gc_shared_dirs(root, pods, grace_s=SHARED_GRACE_S, now=None):
         try:
             if not os.path.isdir(d) or now - os.path.getmtime(d) < grace_s:
                 continue
+            if held:
+                from .podresources import read_devices
+                ids = read_devices(d)
+                if ids and ids in held:
+                    continue
             uids = live.get(tag)
             if uids:
                 try:
@@ -224,8 +231,10 @@ def visible_envs(cfg, ids):
 
 
 def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, using_ids=None, pod_tag=None,
-                             pod_uid=None):
-    """ContainerAllocateResponse for one container holding vGPUs ``vdevs``."""
+                             pod_uid=None, kubelet_ids=None):
+    """ContainerAllocateResponse for one container holding vGPUs ``vdevs``. ``kubelet_ids``:
+    the device IDs of the kubelet's request (monitor mode records them in the container's
+    host directory, where the PodResources attribution finds them)."""
     resp = api.ContainerAllocateResponse()
     uuids = []
     for v in vdevs:
@@ -288,6 +297,9 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         if pod_uid:
             with open(os.path.join(host_dir, POD_MARKER), "w") as f:
                 f.write(pod_uid + "\n")
+        if kubelet_ids:
+            from .podresources import write_devices
+            write_devices(host_dir, kubelet_ids)
         resp.mounts.add(container_path=f"/{pod_tag}", host_path=host_dir, read_only=False)
         resp.envs["VGPU_SHARED_CACHE"] = f"/{pod_tag}/{cache_name}"
     else:

@@ -11,6 +11,10 @@ That monitor is not part of the reference; this is the in-tree one.
   monitored usage, CU limit/mask width, utilisation, token bucket, per process
   launches / throttle / suspend seconds / OOM events, suspend state;
 * ``GET /regions``  JSON snapshot of every region;
+* ``vgpu_container_info`` names the pod and container a directory belongs to: from the
+  kubelet's PodResources (``--pod-resources-socket``, the device IDs the kubelet gave the
+  container) when reachable, else the tag the plugin chose at Allocate
+  (``plugin/podresources.py``);
 * ``POST /regions/<pod_ctr>/{suspend,resume,block,unblock,reclaim}`` and
   ``POST /regions/<pod_ctr>/limit?dev=0&bytes=N`` / ``cu?dev=0&pct=P`` / ``priority?value=N``.
 
@@ -64,10 +68,26 @@ class MetricsWriter:
         return "\n".join(self.lines) + "\n"
 
 
-def render_metrics(root):
+def owners(root, pod_resources_socket=None, resources=("amd.com/gpu",)):
+    """{tag: owner} (``podresources.attribute``), PodResources consulted when reachable."""
+    from .podresources import attribute, list_pod_resources
+    pods = list_pod_resources(pod_resources_socket, timeout=1.0) if pod_resources_socket else None
+    return attribute(root, pods, set(resources))
+
+
+def render_metrics(root, pod_resources_socket=None, resources=("amd.com/gpu",)):
     w = MetricsWriter()
     regions = discover(root)
     w.metric("vgpu_monitor_regions", "gauge", "container regions found", {}, sum(len(v) for v in regions.values()))
+    who = owners(root, pod_resources_socket, resources)
+    for tag in sorted(regions):
+        o = who.get(tag)
+        if o:
+            w.metric("vgpu_container_info", "gauge",
+                     "pod and container of a container directory (source: podresources = the kubelet's device "
+                     "assignment, allocate = the plugin's Allocate-time match; mismatch = the two disagree)",
+                     {"container": tag, "namespace": o["namespace"], "pod": o["pod"], "pod_container": o["container"],
+                      "source": o["source"], "mismatch": str(bool(o.get("mismatch"))).lower()}, 1)
     for tag, paths in regions.items():
         for path in paths:
             try:
@@ -163,7 +183,7 @@ def control(root, tag, action, params):
     return done
 
 
-def make_handler(root, control_enabled=False, token=None):
+def make_handler(root, control_enabled=False, token=None, pod_resources_socket=None):
     """HTTP handler. The metrics side (GET /metrics, /regions, /healthz) is read-only and
     meant for Prometheus on the pod IP. The control side (POST /regions/<tag>/<action>)
     changes tenants' quotas, CU shares and run state, so it is only served by a handler
@@ -182,7 +202,7 @@ def make_handler(root, control_enabled=False, token=None):
         def do_GET(self):
             u = urllib.parse.urlparse(self.path)
             if u.path == "/metrics":
-                return self._send(200, render_metrics(root))
+                return self._send(200, render_metrics(root, pod_resources_socket))
             if u.path == "/regions":
                 snaps = {}
                 for tag, paths in discover(root).items():
@@ -252,12 +272,14 @@ def main(argv=None):
     ap.add_argument("--control-host", default="127.0.0.1", help="control address (loopback unless a token is set)")
     ap.add_argument("--control-port", type=int, default=9395)
     ap.add_argument("--control-token-file", default=None, help="file holding the bearer token for control calls")
+    ap.add_argument("--pod-resources-socket", default="/var/lib/kubelet/pod-resources/kubelet.sock",
+                    help="kubelet PodResources socket (pod attribution); ignored when absent")
     a = ap.parse_args(argv)
     token = open(a.control_token_file).read().strip() if a.control_token_file else None
     if a.enable_control:
         serve(a.root, a.control_host, a.control_port, control_enabled=True, token=token)
         log.info("control endpoints on %s:%d%s", a.control_host, a.control_port, " (token)" if token else "")
-    srv = ThreadingHTTPServer((a.host, a.port), make_handler(a.root))
+    srv = ThreadingHTTPServer((a.host, a.port), make_handler(a.root, pod_resources_socket=a.pod_resources_socket))
     srv.serve_forever()
 
 

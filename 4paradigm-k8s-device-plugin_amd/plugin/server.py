@@ -265,6 +265,16 @@ class DevicePluginServer:
         with self._alloc_mu:
             return self._allocate(request, context)
 
+    def _held_device_sets(self):
+        """Device-ID sets of this resource that live containers hold (kubelet PodResources),
+        or None when the service cannot be reached."""
+        from .podresources import list_pod_resources
+        pods = list_pod_resources(self.cfg.pod_resources_socket, timeout=1.0)
+        if pods is None:
+            return None
+        return {frozenset(ids) for p in pods for c in p["containers"]
+                for res, ids in c["devices"].items() if res == self.resource_name and ids}
+
     def _allocate(self, request, context):
         resp = api.AllocateResponse()
         if self.partition_resource:
@@ -283,7 +293,8 @@ class DevicePluginServer:
             except Exception as e:
                 log.warning("monitor mode: pod match failed: %s", e)
             # Directories of pods that are gone, judged from the pod list just fetched.
-            gc_shared_dirs(os.path.join(self.cfg.vgpu_dir, SHARED_HOST_DIR), getattr(self.pod_matcher, "last_pods", None))
+            gc_shared_dirs(os.path.join(self.cfg.vgpu_dir, SHARED_HOST_DIR), getattr(self.pod_matcher, "last_pods", None),
+                           held=self._held_device_sets())
         if self.legacy is not None and not self.legacy.update_from_checkpoint():
             # Reference server.go:410-412: without the checkpoint the controller cannot know
             # which vGPUs other containers hold, so it refuses instead of double-booking.
@@ -323,7 +334,8 @@ class DevicePluginServer:
                                           request_ids=requested if self.legacy is not None else None,
                                           using_ids=using, pod_tag=tags[i] if i < len(tags) else None,
                                           pod_uid=self.pod_matcher.owner(tags[i]) if (
-                                              self.pod_matcher is not None and i < len(tags) and tags[i]) else None)
+                                              self.pod_matcher is not None and i < len(tags) and tags[i]) else None,
+                                          kubelet_ids=requested)
             resp.container_responses.append(cr)
             self.allocations.append((requested, using))
             if self.cfg.verbose > 5:
