@@ -32,6 +32,11 @@ Modes, one fresh worker process each (the rank process itself never touches the 
            takes about 8 minutes, 12 pods about 3 of them (mostly the pods' start-up).
            ``--time-budget`` (default 540 s) bounds the run: a point whose estimated
            duration would overrun it is skipped and listed as such in ``sweep``.
+* node     BASELINE config 5: all --split vGPUs of every GPU of the job busy at once
+           (32 vGPUs on an 8-GPU node), released together across the ranks. Reported as
+           ``node``: the aggregate over every vGPU, vs native x GPUs, and the slowest pod
+           vs its 1/split entitlement. Runs on multi-GPU jobs; a single-GPU run takes it
+           from the sweep's --split point.
 
 Timed region (native / vgpu / quota / parity): W untimed warmup steps, then exactly K
 steps bracketed by barrier + synchronize on both sides; MAX step time over ranks (one
@@ -77,6 +82,9 @@ def parse(argv=None):
     ap.add_argument("--sweep-find-db", default="own", choices=["own", "shared"],
                     help="shared: the sweep's pods use one MIOpen find-db, filled by the lone pod (as a "
                          "tenant image with a tuned find-db would ship); own: every pod runs its own find")
+    ap.add_argument("--node", default="auto", choices=["auto", "on", "off"],
+                    help="node point: all --split vGPUs of every GPU of the job busy at once (BASELINE config 5: "
+                         "32 vGPUs on 8 GPUs); auto = on for multi-GPU runs (single-GPU runs take it from the sweep)")
     ap.add_argument("--time-budget", type=float, default=540.0,
                     help="wall seconds for the whole run: sweep points that would not finish in time are "
                          "skipped (and reported as such), so the line is always printed")
@@ -318,9 +326,11 @@ class OutOfTime(Exception):
     pass
 
 
-def run_concurrent(args, envs, label, deadline=None):
+def run_concurrent(args, envs, label, deadline=None, before_go=None):
     """Starts one tenant per env, releases them together, returns their results. Raises
-    OutOfTime when the tenants are not all warmed up by ``deadline`` (epoch seconds)."""
+    OutOfTime when the tenants are not all warmed up by ``deadline`` (epoch seconds).
+    ``before_go`` runs once every tenant is warmed up, right before the release (the node
+    point's cross-rank barrier, so the pods of every GPU run in the same window)."""
     tmp = tempfile.mkdtemp(prefix=f"bench-{label}-")
     go = os.path.join(tmp, "go")
     procs, outs = [], []
@@ -345,6 +355,8 @@ def run_concurrent(args, envs, label, deadline=None):
             time.sleep(0.05)
         print(f"[bench] {label}: all {len(outs)} tenants warmed up after {time.time() - t_start:.0f} s",
               file=sys.stderr, flush=True)
+        if before_go:
+            before_go()
         open(go, "w").close()
         for p in procs:
             if p.wait(timeout=900) != 0:
@@ -421,6 +433,70 @@ def _sweep_points(args, backend, uuid, tenants, end, extra):
     return rows, skipped
 
 
+def node_point(args, backend, uuid, world, rank, port):
+    """BASELINE config 5 on the GPUs of this job: every GPU split ``--split`` ways with all of
+    its vGPUs busy at once (8 GPUs x 4 = 32 vGPUs on a full node). Each rank runs the pods of
+    its own GPU (one plugin per rank, as in the other modes); a gloo barrier between the
+    ranks' parents releases every pod of the node in the same window. Every rank reaches the
+    barrier even when its pods fail, so a failure is reported, never a hang. Returns the
+    per-rank records on rank 0 (None elsewhere)."""
+    import datetime
+
+    import torch.distributed as dist
+    from amdvgpu.plugin.kubelet_stub import NodeHarness
+    if world > 1:
+        # Under torchrun the rank would otherwise look for the agent's store on this port
+        # instead of rank 0 serving it (the workers drop the variable for the same reason).
+        os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+        dist.init_process_group("gloo", init_method=f"tcp://{os.environ.get('MASTER_ADDR', '127.0.0.1')}:{port}",
+                                rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
+    passed = [False]
+
+    def gate():
+        passed[0] = True  # attempted: a barrier that timed out is not entered twice
+        if world > 1:
+            dist.barrier()
+
+    t_point = now()
+    try:
+        with NodeHarness(backend, device_split_count=args.split, cu_mode=args.cu_mode) as node:
+            ids = node.vgpu_ids(uuid)[:args.split]
+            envs = [pod_env(node, [i])[0] for i in ids]
+            res = run_concurrent(args, envs, "node", deadline=T_START + args.time_budget - args.sweep_seconds - 15.0,
+                                 before_go=gate)
+        mine = {"ok": True, "uuid": uuid, "pods": len(res),
+                "per_pod": [round(r["items_per_step"] * r["steps"] / (r["t1"] - r["t0"]), 2) for r in res],
+                "seconds": round(now() - t_point, 1)}
+    except (Exception, SystemExit) as e:  # noqa: BLE001 - reported in the line, never a hang
+        if not passed[0] and world > 1:
+            dist.barrier()
+        mine = {"ok": False, "uuid": uuid, "error": repr(e)[:300]}
+    print(f"[bench] node point (rank {rank}): {mine}", file=sys.stderr, flush=True)
+    if world == 1:
+        return [mine]
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    dist.destroy_process_group()
+    return out if rank == 0 else None
+
+
+def node_summary(records, split, native_per_gpu):
+    """The node point's line entry: aggregate over every vGPU of the job and the slowest
+    pod against its 1/split entitlement of a native GPU."""
+    ok = [r for r in records if r.get("ok")]
+    s = {"pods_per_gpu": split, "vgpus": split * len(records), "gpus_measured": len(ok),
+         "failures": [r for r in records if not r.get("ok")]}
+    if not ok:
+        return s
+    pods = [t for r in ok for t in r["per_pod"]]
+    s["aggregate"] = round(sum(pods), 2)
+    s["per_pod_min"], s["per_pod_max"] = min(pods), max(pods)
+    if native_per_gpu:
+        s["aggregate_vs_native"] = round(s["aggregate"] / (native_per_gpu * len(ok)), 3)
+        s["min_pod_vs_entitlement"] = round(min(pods) / (native_per_gpu / split), 3)
+    return s
+
+
 def main(argv=None):
     args = parse(argv)
     if args.worker:
@@ -475,6 +551,10 @@ def main(argv=None):
         port += 1
         if rank == 0 and all(isinstance(v, dict) and (v.get("busbw_GBps") or 0) > 0 for v in rccl.values()):
             rccl["vgpu_vs_native_busbw"] = round(rccl["vgpu"]["busbw_GBps"] / rccl["native"]["busbw_GBps"], 3)
+    node = None
+    if args.node == "on" or (args.node == "auto" and world > 1):
+        node = node_point(args, backend, uuid, world, rank, port)
+        port += 1
     do_sweep = args.sweep == "on" or (args.sweep == "auto" and world == 1 and not cpu)
     sweep_rows, max_vgpus = ([], None)
     if do_sweep:
@@ -549,6 +629,14 @@ def main(argv=None):
         line["reference_overhead_pct"] = round((case.baseline_native / case.baseline_vgpu - 1) * 100.0, 2)
     if rccl is not None:
         line["rccl_allreduce_between_pods"] = rccl
+    native_per_gpu = results["native"]["items_per_step"] * 1000.0 / nat if nat else None
+    if node is not None:
+        line["node"] = node_summary(node, args.split, native_per_gpu)
+    elif do_sweep:
+        # Single GPU: the sweep's point with --split pods is the node point of a 1-GPU job.
+        row = next((r for r in sweep_rows if r.get("tenants") == args.split and "per_tenant" in r), None)
+        if row:
+            line["node"] = node_summary([{"ok": True, "per_pod": row["per_tenant"]}], args.split, native_per_gpu)
     if do_sweep:
         line["max_vgpus_per_gpu"] = max_vgpus
         line["max_vgpus_criterion"] = (f"largest N with aggregate >= {SWEEP_MIN_AGGREGATE}x one whole-GPU pod and "

@@ -27,7 +27,7 @@ def test_bench_multi_rank_cpu_rehearsal(world, tmp_path):
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
-           "--gpus", str(world), "--steps", "2", "--warmup", "1", "--cpu-rehearsal"]
+           "--gpus", str(world), "--steps", "2", "--warmup", "1", "--sweep-seconds", "1", "--cpu-rehearsal"]
     env = dict(os.environ, OMP_NUM_THREADS="1", VGPU_BENCH_CONTRACT_DIR=str(tmp_path))
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=REPO)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
@@ -43,6 +43,9 @@ def test_bench_multi_rank_cpu_rehearsal(world, tmp_path):
     assert r["dtype"] == "fp32" and r["config"]["vgpu"]["cu_limit_pct"] == 25
     rc = r["rccl_allreduce_between_pods"]
     assert rc["native"]["ok"] and rc["vgpu"]["ok"] and "vgpu_vs_native_busbw" in rc, rc
+    node = r["node"]  # BASELINE config 5: every vGPU of every GPU busy at once
+    assert node["vgpus"] == 4 * world and node["gpus_measured"] == world and not node["failures"], node
+    assert node["aggregate"] > 0 and "min_pod_vs_entitlement" in node and "aggregate_vs_native" in node
     ranks = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(world)]
     assert sorted(x["local_rank"] for x in ranks) == list(range(world))
     assert len({x["uuid"] for x in ranks}) == world  # one GPU per rank
