@@ -37,7 +37,7 @@ class DeviceInfo(C.Structure):
         ("cu_count", C.c_int32), ("num_xcc", C.c_int32), ("cu_mask_count", C.c_int32),
         ("cu_mask", C.c_uint32 * 8), ("credit_ns", C.c_int64), ("charged_ns", C.c_uint64),
         ("wall_ns", C.c_uint64), ("util_pct", C.c_int32), ("cu_mode", C.c_int32), ("gpu_id", C.c_uint32), ("bdf", C.c_uint32), ("domain", C.c_uint32), ("configured", C.c_uint32),
-        ("hbm_limit", C.c_uint64), ("crowd", C.c_int32),
+        ("hbm_limit", C.c_uint64), ("crowd", C.c_int32), ("preempt", C.c_int32), ("depth_cap", C.c_int32),
     ]
 
 
@@ -153,6 +153,7 @@ class Region:
             "charged_ns": d.charged_ns, "wall_ns": d.wall_ns, "util_pct": d.util_pct,
             "cu_mode": CU_MODES.get(d.cu_mode, str(d.cu_mode)), "gpu_id": d.gpu_id, "bdf": d.bdf, "domain": d.domain,
             "configured": bool(d.configured), "hbm_limit": d.hbm_limit, "crowd": d.crowd,
+            "preempt": bool(d.preempt), "depth_cap": d.depth_cap,
         }
 
     def devices(self):

@@ -161,9 +161,9 @@ def ab_compare(a, pods, backend, uuid, split, prio):
     runs = []
     with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode) as node:
         ids = node.vgpu_ids(uuid)[:len(pods)]
-        arms = [("default", None, None), ("priority", prio, None)]
-        if a.bg_env:
-            arms.append(("priority+bg-env", prio, a.bg_env))
+        arms = ([] if a.skip_default else [("default", None, None)]) + [("priority", prio, None)]
+        for bg in a.bg_env:
+            arms.append(("priority+" + " ".join(f"{k}={v}" for k, v in bg.items()), prio, bg))
         for i in range(a.ab):
             for label, pr, bg in arms:
                 trace = os.path.join(a.trace_latency, f"{label}_{i}") if a.trace_latency else None
@@ -175,7 +175,7 @@ def ab_compare(a, pods, backend, uuid, split, prio):
                 runs.append(row)
                 print(json.dumps(row), flush=True)
     md = [f"# default vs priority classes, ABAB x{a.ab} ({a.seconds:.0f} s windows, split {split}"
-          + (f"; bg env {a.bg_env}" if a.bg_env else "") + ")", "",
+          + "".join(f"; bg env {bg}" for bg in a.bg_env) + ")", "",
           "| run | " + " | ".join(p["spec"] + (" P50 / P99 ms (on the GPU P50 / P99)" if p["latency"] else " /s")
                                   for p in pods) + " |",
           "|---|" + "---|" * len(pods)]
@@ -217,8 +217,10 @@ def main():
     ap.add_argument("--ab", type=int, default=0,
                     help="skip the solo runs; alternate N times between the default and the --priority run "
                          "(ABAB...) and report each run's latency-pod P50 / P99 and pod throughputs")
-    ap.add_argument("--bg-env", default="", help="K=V,...: with --ab, a third arm where the background pods "
-                                                      "(priority >= 2) also get this env")
+    ap.add_argument("--bg-env", action="append", default=[],
+                    help="K=V,...: with --ab, one more arm where the background pods (priority >= 2) also get "
+                         "this env (repeatable: one arm each)")
+    ap.add_argument("--skip-default", action="store_true", help="with --ab: no arm without priorities")
     ap.add_argument("--trace-latency", default="", help="with --ab: rocprofv3 kernel trace of the latency pods "
                                                           "under DIR/<arm>_<run>")
     ap.add_argument("--json-out")
@@ -231,7 +233,7 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--go")
     a = ap.parse_args()
-    a.bg_env = dict(kv.split("=", 1) for kv in a.bg_env.split(",") if kv)
+    a.bg_env = [dict(kv.split("=", 1) for kv in spec.split(",") if kv) for spec in a.bg_env]
     if a.worker:
         return worker(a)
     from amdvgpu.plugin.devices import SysfsBackend

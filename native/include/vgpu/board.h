@@ -98,6 +98,8 @@ class Board {
   // Priority of the container owning host PID `pid` on GPU `gpu_id` (kPrioNormal for a
   // process no live slot lists: an unmanaged process counts as a normal tenant).
   int priority_of(int pid, uint32_t gpu_id) const;
+  // Whether a live peer of priority < `priority` has GPU `gpu_id` (as of the last refresh).
+  bool better_on(uint32_t gpu_id, int priority) const;
 
   // OR of the CU masks that tenants of priority <= `max_priority` use on GPU `gpu_id`
   // (the CUs a background tenant leaves to the latency class).

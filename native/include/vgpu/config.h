@@ -98,6 +98,12 @@ struct Config {
   int gpu_concurrency = 0;               // VGPU_GPU_CONCURRENCY: limited containers whose GPU-time
                                          // gates may be open together on one GPU (0 = any number)
   int gpu_slice_ms = 20;                 // VGPU_GPU_SLICE_MS: turn length under that admission
+  int preempt_hold_ms = 0;               // VGPU_PREEMPT_HOLD_MS: background class - launches held while a
+                                         // better class has waves on the GPU and this long after (0 = the
+                                         // soft yield: only no credit is earned)
+  int preempt_depth = 0;                 // VGPU_PREEMPT_DEPTH: background class - at most this many AQL
+                                         // packets in flight per device while a better class shares the
+                                         // GPU (0 = unbounded)
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
   uint64_t host_mem_limit = 0;           // VGPU_HOST_MEMORY_LIMIT: pinned host memory, 0 = unlimited

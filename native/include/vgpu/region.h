@@ -100,7 +100,14 @@ struct alignas(64) DeviceState {
   // Background class: CUs held by latency-class tenants on this GPU (their CU slices, from
   // the board); the container's queues keep off them (0 = none).
   uint32_t reserved_mask[kCuMaskWords];
+  // Background class next to a better class (VGPU_PREEMPT_HOLD_MS / VGPU_PREEMPT_DEPTH):
+  // launches held because a better class is busy, and the cap on the packets each process
+  // of the container keeps in flight on this device (0 = none). Written by the sampler.
+  std::atomic<int32_t> preempt;
+  std::atomic<int32_t> depth_cap;
 };
+// preempt / depth_cap sit in what was tail padding in layout v5: the layout is unchanged.
+static_assert(sizeof(DeviceState) == 320, "DeviceState layout changed");
 
 struct RegionHeader {
   uint32_t magic;

@@ -57,6 +57,8 @@ typedef struct {
   uint32_t configured;
   uint64_t hbm_limit;
   int32_t crowd;       /* auto mode: other busy processes seen on the GPU (-1 = not assessed) */
+  int32_t preempt;     /* background class: launches held, a better class is busy (1) */
+  int32_t depth_cap;   /* background class: packets in flight allowed per process (0 = any) */
 } vgpu_device_info;
 
 /* Returns NULL on failure; *err receives -errno. */

@@ -154,4 +154,11 @@ int Board::priority_of(int pid, uint32_t gpu_id) const {
   return kPrioNormal;
 }
 
+bool Board::better_on(uint32_t gpu_id, int priority) const {
+  for (const BoardPeer& p : peers_)
+    if (p.priority < priority && std::find(p.gpu_ids.begin(), p.gpu_ids.end(), gpu_id) != p.gpu_ids.end())
+      return true;
+  return false;
+}
+
 }  // namespace vgpu

@@ -64,6 +64,8 @@ int vgpu_region_device_info(vgpu_region* r, int dev, vgpu_device_info* out) {
   out->configured = d.configured;
   out->hbm_limit = d.hbm_limit;
   out->crowd = d.crowd.load();
+  out->preempt = d.preempt.load();
+  out->depth_cap = d.depth_cap.load();
   return 0;
 }
 

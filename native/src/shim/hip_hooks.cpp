@@ -163,10 +163,15 @@ void gate_launch(int dev) {
   if (dev < 0 || dev >= s.n_agents) dev = 0;
   bool limited = s.agents[dev].temporal_active.load(std::memory_order_relaxed) &&
                  (r->hdr.utilization_switch.load(std::memory_order_relaxed) || config().cu_policy == CuPolicy::kForce);
-  if (__builtin_expect(!limiter_would_block(r->hdr, r->dev[dev], limited), 1)) return;
-  trace_push(limited ? "vgpu:throttle" : "vgpu:blocked");
-  uint64_t waited = limiter_acquire(r->hdr, r->dev[dev], limited);
-  trace_pop();
+  uint64_t waited = 0;
+  if (__builtin_expect(limiter_would_block(r->hdr, r->dev[dev], limited), 0)) {
+    trace_push(limited ? "vgpu:throttle" : "vgpu:blocked");
+    waited = limiter_acquire(r->hdr, r->dev[dev], limited);
+    trace_pop();
+  }
+  // Background class next to a better one: bounded work in flight (watcher.cpp preempt_tick).
+  const int cap = limited ? r->dev[dev].depth_cap.load(std::memory_order_relaxed) : 0;
+  if (__builtin_expect(cap > 0, 0)) waited += wait_queue_depth(dev, cap);
   if (waited && s.slot >= 0) r->procs[s.slot].throttle_ns.fetch_add(waited, std::memory_order_relaxed);
 }
 

@@ -14,6 +14,7 @@
 //   cuIpc* pass-through without double charge    (suspend-gated, charged to the exporter)
 // MI355X-only: hsa_queue_create applies the vGPU's CU mask to every HW queue and
 // hsa_amd_queue_cu_set_mask cannot widen it.
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -24,6 +25,7 @@
 #include "shim.h"
 #include "vgpu/kfd.h"
 #include "vgpu/log.h"
+#include "vgpu/ratelimit.h"
 
 using namespace vgpu;
 
@@ -369,6 +371,50 @@ hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* queue, uint32_t num_cu
   uint32_t nbits = (uint32_t)((a.cu_count + 31) / 32 * 32);
   return real_hsa_amd_queue_cu_set_mask(queue, nbits, eff.words);
 }
+
+}  // extern "C"
+
+namespace vgpu {
+
+namespace {
+
+// Packets of this process's queues on `dev` the CP has not consumed yet. The queue map's
+// lock keeps hsa_queue_destroy (which erases under it first) from freeing a queue while
+// its indices are read.
+uint64_t queued_packets(int dev) {
+  VGPU_REAL_HSA(hsa_queue_load_write_index_relaxed);
+  VGPU_REAL_HSA(hsa_queue_load_read_index_relaxed);
+  if (!real_hsa_queue_load_write_index_relaxed || !real_hsa_queue_load_read_index_relaxed) return 0;
+  ShimState& s = shim();
+  uint64_t n = 0;
+  std::lock_guard<std::mutex> g(s.alloc_mu);
+  for (const auto& q : s.queues) {
+    if (q.second != dev) continue;
+    const hsa_queue_t* h = reinterpret_cast<const hsa_queue_t*>(q.first);
+    const uint64_t w = real_hsa_queue_load_write_index_relaxed(h), rd = real_hsa_queue_load_read_index_relaxed(h);
+    if (w > rd) n += w - rd;
+  }
+  return n;
+}
+
+}  // namespace
+
+uint64_t wait_queue_depth(int dev, int cap) {
+  // Bounded: a queue can also hold packets that wait on something only this thread would
+  // launch later (a barrier on another stream's event), which must never deadlock.
+  constexpr uint64_t kMaxWaitNs = 20'000'000ull;
+  if (queued_packets(dev) <= (uint64_t)cap) return 0;
+  const uint64_t t0 = now_ns();
+  struct timespec ts = {0, 20'000};
+  trace_push("vgpu:depth");
+  while (queued_packets(dev) > (uint64_t)cap && now_ns() - t0 < kMaxWaitNs) nanosleep(&ts, nullptr);
+  trace_pop();
+  return now_ns() - t0;
+}
+
+}  // namespace vgpu
+
+extern "C" {
 
 hsa_status_t hsa_queue_destroy(hsa_queue_t* queue) {
   VGPU_REAL_HSA(hsa_queue_destroy);

@@ -124,6 +124,11 @@ inline void gate_suspend() {
 // device).
 void gate_launch(int dev);
 
+// Waits (bounded) until this process's HSA queues on device `dev` hold at most `cap`
+// AQL packets not yet consumed by the command processor (write - read index). Returns
+// the nanoseconds waited.
+uint64_t wait_queue_depth(int dev, int cap);
+
 // Re-reads limits the controller changed in the region (generation bump): CU masks are
 // re-applied to every tracked queue and the enforcement mode follows the new share.
 void apply_live_config();

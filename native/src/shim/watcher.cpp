@@ -123,6 +123,7 @@ struct Sampler {
   Board board;                            // node-wide board (VGPU_BOARD_DIR), if any
   bool board_tried = false;
   uint64_t yielded_ns[kMaxDevices] = {};  // background class: time spent yielding (diagnostics)
+  uint64_t preempt_until[kMaxDevices] = {};  // background class: launches held until (strict yield)
   uint64_t want_since[kMaxDevices] = {};  // concurrency admission: waiting since (0 = not)
   uint64_t open_since[kMaxDevices] = {};  // concurrency admission: holding the GPU since
   bool admitted[kMaxDevices] = {};
@@ -185,6 +186,27 @@ void collect_region_pids(Region* r, Sampler& sm) {
   }
 }
 
+// Background class, strict form (VGPU_PREEMPT_HOLD_MS / VGPU_PREEMPT_DEPTH). The soft
+// yield only stops earning credit, so a background tenant keeps launching until its
+// credit runs out while the better class waits behind its kernels on the memory system
+// (profiles/r3k: the service's kernels run ~3x longer next to the trainers). Strict:
+// (1) while a better class has waves resident, and for the hold time after, the gate is
+// closed outright; (2) while a better-class tenant shares the GPU (board), each process
+// keeps at most `depth` AQL packets in flight (gate_launch), so what is queued when the
+// better class wakes up drains in a few kernels. HAMi-style preemption by priority, at
+// launch granularity: running kernels are never interrupted.
+void preempt_tick(Sampler& sm, DeviceState& ds, uint32_t gpu_id, int prio, int d, bool yield, uint64_t now) {
+  const Config& cfg = config();
+  if (cfg.preempt_hold_ms > 0) {
+    if (yield) sm.preempt_until[d] = now + (uint64_t)cfg.preempt_hold_ms * 1'000'000ull;
+    const bool held = now < sm.preempt_until[d];
+    ds.preempt.store(held ? 1 : 0, std::memory_order_relaxed);
+    if (held) ds.gate_open.store(0, std::memory_order_release);
+  }
+  const int cap = cfg.preempt_depth > 0 && sm.board.better_on(gpu_id, prio) ? cfg.preempt_depth : 0;
+  if (ds.depth_cap.load(std::memory_order_relaxed) != cap) ds.depth_cap.store(cap, std::memory_order_relaxed);
+}
+
 void sample_tick(Region* r, Sampler& sm) {
   ShimState& s = shim();
   const uint64_t now = now_ns();
@@ -207,6 +229,9 @@ void sample_tick(Region* r, Sampler& sm) {
         sm.want_since[d] = 0;
         sm.board.publish_gate(d, false, 0);
       }
+      r->dev[d].preempt.store(0, std::memory_order_relaxed);  // and any strict-yield state
+      r->dev[d].depth_cap.store(0, std::memory_order_relaxed);
+      sm.preempt_until[d] = 0;
       continue;
     }
     DeviceState& ds = r->dev[d];
@@ -280,6 +305,7 @@ void sample_tick(Region* r, Sampler& sm) {
       if (!hold) ds.gate_open.store(0, std::memory_order_release);
       sm.board.publish_gate(d, hold, sm.want_since[d]);
     }
+    if (background) preempt_tick(sm, ds, a.gpu_id, prio, d, yield, now);
     sm.opened[d] = was_closed && ds.gate_open.load(std::memory_order_relaxed);
     sm.prev_pm[d] = pm;
   }

@@ -25,6 +25,8 @@
 #include <thread>
 
 extern "C" int fake_rocr_set_occupancy(int dev, int cus);
+extern "C" void fake_rocr_queue_submit(hsa_queue_t* queue);
+extern "C" void fake_rocr_queue_retire(hsa_queue_t* queue);
 
 namespace {
 
@@ -34,7 +36,7 @@ struct Device {
   hsa_amd_memory_pool_t pool{0};
   std::mutex mu;
   std::condition_variable cv;
-  std::deque<uint32_t> work;  // kernel durations (µs)
+  std::deque<std::pair<uint32_t, hsa_queue_t*>> work;  // kernel durations (µs) and their stream's queue
   bool running = false;
   uint64_t busy_us = 0;
   uint64_t kernels = 0;
@@ -52,10 +54,12 @@ void gpu_loop(int d) {
   Device& D = g_dev[d];
   for (;;) {
     uint32_t us;
+    hsa_queue_t* q;
     {
       std::unique_lock<std::mutex> l(D.mu);
       D.cv.wait(l, [&] { return !D.work.empty(); });
-      us = D.work.front();
+      us = D.work.front().first;
+      q = D.work.front().second;
       if (!D.running) fake_rocr_set_occupancy(D.rocr, 64);
       D.running = true;
     }
@@ -64,6 +68,7 @@ void gpu_loop(int d) {
     uint64_t took = (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
                         std::chrono::steady_clock::now() - t0).count();
     std::lock_guard<std::mutex> l(D.mu);
+    if (q) fake_rocr_queue_retire(q);
     D.work.pop_front();
     D.busy_us += took;  // the time the "GPU" was really busy (sleeps overshoot)
     D.kernels++;
@@ -125,11 +130,13 @@ struct FakeStream {
 };
 
 int dev_of(hipStream_t s) { return s ? reinterpret_cast<FakeStream*>(s)->dev : t_dev; }
+hsa_queue_t* queue_of(hipStream_t s) { return s ? reinterpret_cast<FakeStream*>(s)->q : nullptr; }
 
-void submit(int d, uint32_t us) {
+void submit(int d, uint32_t us, hsa_queue_t* q) {
   Device& D = g_dev[d];
   std::lock_guard<std::mutex> l(D.mu);
-  D.work.push_back(us);
+  if (q) fake_rocr_queue_submit(q);
+  D.work.push_back({us, q});
   D.cv.notify_all();
 }
 
@@ -232,7 +239,7 @@ hipError_t hipLaunchKernel(const void* function_address, dim3, dim3, void**, siz
   init();
   fake_hip_record("hipLaunchKernel");
   if (!function_address) return hipErrorInvalidValue;
-  submit(dev_of(stream), *static_cast<const uint32_t*>(function_address));
+  submit(dev_of(stream), *static_cast<const uint32_t*>(function_address), queue_of(stream));
   return hipSuccess;
 }
 
@@ -240,7 +247,7 @@ hipError_t hipGraphLaunch(hipGraphExec_t graphExec, hipStream_t stream) {
   init();
   fake_hip_record("hipGraphLaunch");
   if (!graphExec) return hipErrorInvalidValue;
-  submit(dev_of(stream), *reinterpret_cast<const uint32_t*>(graphExec));
+  submit(dev_of(stream), *reinterpret_cast<const uint32_t*>(graphExec), queue_of(stream));
   return hipSuccess;
 }
 

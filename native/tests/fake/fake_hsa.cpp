@@ -48,6 +48,7 @@ struct FakeGpu {
 
 struct FakeQueue {
   hsa_queue_t q;
+  std::atomic<uint64_t> wr{0}, rd{0};  // AQL write / read dispatch indices (fake_hip moves them)
   int dev;
   uint32_t mask[8];
   int mask_bits;
@@ -290,6 +291,17 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
   *queue = &q->q;
   return HSA_STATUS_SUCCESS;
 }
+
+// The queue's dispatch indices: fake_hip submits (write index) and retires (read index)
+// the kernels it runs on a stream's queue, as the CP would.
+uint64_t hsa_queue_load_write_index_relaxed(const hsa_queue_t* queue) {
+  return reinterpret_cast<const FakeQueue*>(queue)->wr.load();
+}
+uint64_t hsa_queue_load_read_index_relaxed(const hsa_queue_t* queue) {
+  return reinterpret_cast<const FakeQueue*>(queue)->rd.load();
+}
+void fake_rocr_queue_submit(hsa_queue_t* queue) { reinterpret_cast<FakeQueue*>(queue)->wr.fetch_add(1); }
+void fake_rocr_queue_retire(hsa_queue_t* queue) { reinterpret_cast<FakeQueue*>(queue)->rd.fetch_add(1); }
 
 hsa_status_t hsa_queue_destroy(hsa_queue_t* queue) {
   std::lock_guard<std::mutex> g(st().mu);

@@ -17,6 +17,9 @@
 //   cus              the current device's CU count as the runtime sees it
 //   curlimit         the shim's vgpu_get_current_device_memory_limit (the current HIP
 //                    device mapped to its agent): {"dev": N, "limit": bytes}
+//   burst=US,N       N launches of a US-microsecond kernel on the current stream without
+//                    waiting, then synchronize: {"burst": N, "max_depth": most packets seen
+//                    queued on the stream's HSA queue right after a launch, "wall": s}
 //   sleep=SECS
 //   forkmalloc=SIZE  fork; the child hipMallocs SIZE and exits normally:
 //                    {"child_malloc": "ok"|"oom"|"crash"}
@@ -199,6 +202,24 @@ int main(int argc, char** argv) {
       uint64_t k1 = 0, b1 = fake_hip_busy_us(dev, &k1);
       printf("{\"%s\": %ld, \"wall\": %.6f, \"busy_us\": %llu, \"busy_frac\": %.4f}\n", key.c_str(), n, wall,
              (unsigned long long)(b1 - b0), (b1 - b0) / 1e6 / wall);
+    } else if (key == "burst") {
+      unsigned us = (unsigned)atoi(val.c_str());
+      long n = atol(val.substr(val.find(',') + 1).c_str());
+      uint32_t* k = &kernel_us[kslot++ % 64];
+      *k = us;
+      hsa_queue_t* q = stream ? fake_hip_stream_queue(stream) : nullptr;
+      uint64_t max_depth = 0;
+      double t0 = now_s();
+      for (long i = 0; i < n; i++) {
+        (void)hipLaunchKernel(k, dim3(1), dim3(64), nullptr, 0, stream);
+        if (q) {
+          uint64_t d = hsa_queue_load_write_index_relaxed(q) - hsa_queue_load_read_index_relaxed(q);
+          if (d > max_depth) max_depth = d;
+        }
+      }
+      (void)hipStreamSynchronize(stream);
+      printf("{\"burst\": %ld, \"max_depth\": %llu, \"wall\": %.6f}\n", n, (unsigned long long)max_depth,
+             now_s() - t0);
     } else if (key == "internal") {
       fake_rocr_internal_alloc(dev, parse_size(val.c_str()));
       printf("{\"internal\": %lld}\n", parse_size(val.c_str()));

@@ -397,6 +397,62 @@ def test_background_class_yields_to_busier_betters(fake, tmp_path, neighbour_pri
     assert slots == ["batch.slot", "svc.slot"]
 
 
+def test_background_class_strict_hold(fake, tmp_path):
+    """VGPU_PREEMPT_HOLD_MS: a background tenant's launches are held outright while a
+    better class has waves resident (and for the hold after), not merely left to run
+    until its credit is spent; the region shows the hold."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+    svc = _board_env(fake, tmp_path, "svc", VGPU_TASK_PRIORITY="0")
+    bg = _board_env(fake, tmp_path, "batch", VGPU_TASK_PRIORITY="2", VGPU_PREEMPT_HOLD_MS="50")
+    a = sp.Popen([HARNESS, "stream", "run=2000,4"], env=svc, stdout=sp.PIPE, text=True)
+    try:
+        time.sleep(1.0)  # the service is busy and on the board
+        b = sp.Popen([HARNESS, "stream", "run=2000,2.5"], env=bg, stdout=sp.PIPE, text=True)
+        held = False
+        for _ in range(40):
+            time.sleep(0.05)
+            if os.path.exists(bg["VGPU_SHARED_CACHE"]):
+                try:
+                    with Region(bg["VGPU_SHARED_CACHE"]) as r:
+                        held |= r.device(0)["preempt"]
+                except OSError:
+                    pass
+        out, _ = b.communicate(timeout=120)
+    finally:
+        a.wait(timeout=60)
+    frac = [json.loads(l) for l in out.splitlines() if l.startswith('{"run"')][0]["busy_frac"]
+    assert held and frac < 0.1, (held, frac)
+
+
+@pytest.mark.parametrize("depth,bound", [(0, None), (2, 3)])
+def test_background_class_bounded_depth(fake, tmp_path, depth, bound):
+    """VGPU_PREEMPT_DEPTH: while a better-class tenant shares the GPU (on the board, idle
+    here), a crowded background tenant keeps at most `depth` packets queued on its HSA
+    queues (the launch gate waits for the CP's read index), so the work ahead of the
+    better class's next request drains in a few kernels. Without it, a burst queues whole."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+    svc = _board_env(fake, tmp_path, "svc", VGPU_TASK_PRIORITY="0")
+    peer = _board_env(fake, tmp_path, "peer", VGPU_TASK_PRIORITY="2")  # keeps the GPU crowded
+    bg = _board_env(fake, tmp_path, "batch", VGPU_TASK_PRIORITY="2", VGPU_PREEMPT_DEPTH=str(depth))
+    a = sp.Popen([HARNESS, "stream", "sleep=6"], env=svc, stdout=sp.PIPE, text=True)
+    p = sp.Popen([HARNESS, "stream", "run=2000,6"], env=peer, stdout=sp.PIPE, text=True)
+    try:
+        time.sleep(1.0)
+        out = run(bg, "stream", "run=1000,1.5", "burst=2000,40", timeout=120)
+    finally:
+        a.wait(timeout=60)
+        p.wait(timeout=60)
+    burst = [o for o in out if "burst" in o][0]
+    if bound is None:
+        assert burst["max_depth"] >= 30, burst
+    else:
+        assert 1 <= burst["max_depth"] <= bound, burst
+        with Region(bg["VGPU_SHARED_CACHE"]) as r:
+            assert r.device(0)["depth_cap"] in (0, depth)  # 0 once the process left
+
+
 def test_background_class_keeps_off_the_latency_class_cus(fake, tmp_path):
     """A latency-class tenant (priority 0) publishes its CU slice on the board; a
     background tenant (priority >= 2) on the same GPU re-masks its queues to the rest of
