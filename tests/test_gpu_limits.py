@@ -228,6 +228,68 @@ def test_background_class_yields_to_a_busy_latency_class(tmp_path):
     assert behind < 0.3 * equal, (equal, behind)
 
 
+IDLE_ON_BOARD = """
+import torch
+from amdvgpu.ops import spin
+spin(64, 100); torch.cuda.synchronize()
+open(os.environ["VGPU_TEST_READY"], "w").close()
+t0 = time.perf_counter()
+while not os.path.exists(os.environ["VGPU_TEST_GO"]) and time.perf_counter() - t0 < 120:
+    time.sleep(0.05)
+"""
+
+BURST = """
+import torch
+from amdvgpu.ops import spin
+from amdvgpu.shim.region import Region
+spin(64, 100); torch.cuda.synchronize()
+time.sleep(1.5)  # crowd and board assessed by the lease holder
+t0 = time.perf_counter()
+for _ in range(200):
+    spin(64, 500)
+t1 = time.perf_counter()
+torch.cuda.synchronize()
+t2 = time.perf_counter()
+emit(enqueue_s=t1 - t0, total_s=t2 - t0, depth_cap=Region(os.environ["VGPU_SHARED_CACHE"]).device(0)["depth_cap"])
+"""
+
+
+@pytest.mark.parametrize("depth", [0, 2])
+def test_background_depth_bound_next_to_a_latency_class(tmp_path, depth):
+    """VGPU_PREEMPT_DEPTH: with a latency-class container on the board (idle) and the GPU
+    crowded by an equal-class neighbour, a background container's launches wait on its HSA
+    queues' read index - 200 async 0.5 ms kernels take about as long to enqueue as to run.
+    Without the bound they are all queued at once."""
+    board = tmp_path / "board"
+    board.mkdir()
+    ready, go = str(tmp_path / "ready"), str(tmp_path / "go")
+    ex = {"VGPU_BOARD_DIR": str(board)}
+    lat = vgpu_env(mem_limit=8 * GiB, extra=dict(ex, VGPU_BOARD_SLOT="svc.slot", VGPU_TASK_PRIORITY="0"))
+    peer = vgpu_env(mem_limit=8 * GiB, extra=dict(ex, VGPU_BOARD_SLOT="peer.slot", VGPU_TASK_PRIORITY="2"))
+    bg = vgpu_env(mem_limit=8 * GiB, extra=dict(ex, VGPU_BOARD_SLOT="batch.slot", VGPU_TASK_PRIORITY="2",
+                                                   VGPU_PREEMPT_DEPTH=str(depth)))
+    svc = spawn_child(IDLE_ON_BOARD, lat, extra_env={"VGPU_TEST_READY": ready, "VGPU_TEST_GO": go})
+    busy = spawn_child(LATENCY_SPIN, peer, extra_env={"VGPU_TEST_READY": ready + ".peer", "VGPU_TEST_GO": go})
+    try:
+        deadline = time.time() + 240
+        while not (os.path.exists(ready) and os.path.exists(ready + ".peer")):
+            assert time.time() < deadline and svc.poll() is None and busy.poll() is None, "neighbours failed"
+            time.sleep(0.05)
+        res, _ = run_child(BURST, bg, timeout=240)
+    finally:
+        open(go, "w").close()
+        svc.communicate(timeout=120)
+        busy.communicate(timeout=120)
+        for c in (lat, peer, bg):
+            cleanup_region(c)
+    r = res[0]
+    print(json.dumps(r))
+    if depth:
+        assert r["depth_cap"] == depth and r["enqueue_s"] > 0.8 * r["total_s"], r
+    else:
+        assert r["depth_cap"] == 0 and r["enqueue_s"] < 0.3 * r["total_s"], r
+
+
 CENSUS = """
 import torch
 from amdvgpu.ops import cu_census
