@@ -37,6 +37,48 @@ def write_pcibus_file(path, devices):
         f.write("".join(b + "\n" for b in bdfs))
 
 
+class LedgerDaemon:
+    """The node's GPU-time ledger (native/src/tools/vgpu_ledger.cpp, vgpu/ledger.h): one
+    KFD occupancy sampler for every limited container, writing <board>/ledger.<gpu_id>.
+    Restarted if it exits; the containers fall back to sampling by themselves whenever its
+    ledger goes stale, so a missing binary only costs the saving."""
+
+    def __init__(self, board_dir):
+        self.board_dir = board_dir
+        self.proc = None
+        self.starts = 0
+        self._next_try = 0.0
+
+    def poll(self):
+        if self.proc is not None and self.proc.poll() is None:
+            return
+        if time.monotonic() < self._next_try:
+            return
+        self._next_try = time.monotonic() + 5.0
+        import subprocess
+        from ..shim.native import LEDGER, NativeMissing, lib_path
+        try:
+            exe = lib_path(LEDGER)
+        except NativeMissing as e:
+            if self.starts == 0:
+                log.warning("no ledger daemon (%s); containers sample the GPU by themselves", e)
+            self.starts += 1
+            return
+        if self.proc is not None:
+            log.warning("vgpu-ledger exited with %s; restarting", self.proc.returncode)
+        self.proc = subprocess.Popen([exe, "--dir", self.board_dir], stdin=subprocess.DEVNULL)
+        self.starts += 1
+
+    def stop(self):
+        if self.proc is not None and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(timeout=5)
+            except Exception:
+                self.proc.kill()
+        self.proc = None
+
+
 class Supervisor:
     def __init__(self, cfg, backend=None, install_signals=True, pod_lister=None):
         self.cfg = cfg
@@ -49,6 +91,7 @@ class Supervisor:
         self.started = threading.Event()
         self._fs = None
         self._os = None
+        self.ledger = None
 
     def init_backend(self):
         if self.backend is not None:
@@ -112,7 +155,10 @@ class Supervisor:
         os.makedirs(cfg.device_plugin_path, exist_ok=True)
         try:
             ensure_lock_file(cfg.vgpu_dir)
-            ensure_board_dir(cfg.vgpu_dir)
+            board = ensure_board_dir(cfg.vgpu_dir)
+            if cfg.ledger:
+                self.ledger = LedgerDaemon(board)
+                self.ledger.poll()
         except OSError as e:
             log.warning("cannot create the host-PID lock file / board under %s: %s", cfg.vgpu_dir, e)
         self._fs = FSWatcher(cfg.device_plugin_path.rstrip("/"), self.events)
@@ -122,6 +168,8 @@ class Supervisor:
             return self._loop(stop_event)
         finally:
             self.stop()
+            if self.ledger:
+                self.ledger.stop()
             self._fs.close()
             if self._os:
                 self._os.close()
@@ -138,6 +186,8 @@ class Supervisor:
                 if not self.start_plugins():
                     need_restart = True
                     retry_at = time.monotonic() + 1.0
+            if self.ledger:
+                self.ledger.poll()
             try:
                 ev = self.events.get(timeout=0.2)
             except queue.Empty:

@@ -14,6 +14,7 @@ SHIM = "libvgpu_hip.so"
 REGION = "libvgpu_region.so"
 KERNELS = "libvgpu_kernels.so"
 VGPUCTL = "vgpuctl"
+LEDGER = "vgpu-ledger"
 VALIDATE = "vgpu-validate"
 CORE_TESTS = "vgpu_core_tests"
 

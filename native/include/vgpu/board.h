@@ -72,6 +72,8 @@ class Board {
   // Maps `dir`/`self_name` read-write (created if missing and the directory allows it).
   // Returns 0 or -errno; without a board every query answers "no peers".
   int open(const char* dir, const char* self_name);
+  // Reads the directory without a slot of its own (the ledger daemon).
+  int open_readonly(const char* dir);
   bool attached() const { return self_ != nullptr; }
   BoardSlot* self() { return self_; }
 

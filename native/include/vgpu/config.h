@@ -98,10 +98,12 @@ struct Config {
   int gpu_concurrency = 0;               // VGPU_GPU_CONCURRENCY: limited containers whose GPU-time
                                          // gates may be open together on one GPU (0 = any number)
   int gpu_slice_ms = 20;                 // VGPU_GPU_SLICE_MS: turn length under that admission
-  int preempt_hold_ms = 0;               // VGPU_PREEMPT_HOLD_MS: background class - launches held while a
+  bool use_ledger = true;                // VGPU_LEDGER: take charges from the node's GPU-time ledger
+                                         // (vgpu/ledger.h) when its daemon keeps it fresh
+  int preempt_hold_ms = 3;               // VGPU_PREEMPT_HOLD_MS: background class - launches held while a
                                          // better class has waves on the GPU and this long after (0 = the
-                                         // soft yield: only no credit is earned)
-  int preempt_depth = 0;                 // VGPU_PREEMPT_DEPTH: background class - at most this many AQL
+                                         // soft yield: only no credit is earned; profiles/r3s, r3t)
+  int preempt_depth = 4;                 // VGPU_PREEMPT_DEPTH: background class - at most this many AQL
                                          // packets in flight per device while a better class shares the
                                          // GPU (0 = unbounded)
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)

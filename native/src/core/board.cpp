@@ -51,6 +51,13 @@ int Board::open(const char* dir, const char* self_name) {
   return 0;
 }
 
+int Board::open_readonly(const char* dir) {
+  if (!dir || !*dir) return -EINVAL;
+  dir_ = dir;
+  self_name_.clear();
+  return 0;
+}
+
 void Board::publish(int priority, const uint32_t* gpu_ids, int ndev, const std::vector<int>& hostpids, uint64_t now,
                     const uint32_t (*masks)[kCuMaskWords]) {
   if (!self_) return;

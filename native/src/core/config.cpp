@@ -294,9 +294,10 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   long slice = 20;
   if (parse_int(getenv_fn("VGPU_GPU_SLICE_MS"), 1, 10000, &slice)) cfg->gpu_slice_ms = (int)slice;
   if (const char* s = getenv_fn("VGPU_BOARD_SLOT")) cfg->board_slot = s;
-  long hold = 0;
+  if (const char* s = getenv_fn("VGPU_LEDGER")) cfg->use_ledger = !(s[0] == '0' && !s[1]);
+  long hold = 3;
   if (parse_int(getenv_fn("VGPU_PREEMPT_HOLD_MS"), 0, 10000, &hold)) cfg->preempt_hold_ms = (int)hold;
-  long depth = 0;
+  long depth = 4;
   if (parse_int(getenv_fn("VGPU_PREEMPT_DEPTH"), 0, 4096, &depth)) cfg->preempt_depth = (int)depth;
   if (const char* s = getenv_fn("VGPU_LOCK_FILE")) {
     if (*s) cfg->lock_file = s;

@@ -30,6 +30,7 @@
 #include "shim.h"
 #include "vgpu/board.h"
 #include "vgpu/kfd.h"
+#include "vgpu/ledger.h"
 #include "vgpu/log.h"
 #include "vgpu/ratelimit.h"
 
@@ -127,7 +128,47 @@ struct Sampler {
   uint64_t want_since[kMaxDevices] = {};  // concurrency admission: waiting since (0 = not)
   uint64_t open_since[kMaxDevices] = {};  // concurrency admission: holding the GPU since
   bool admitted[kMaxDevices] = {};
+  // Node ledger (vgpu/ledger.h): per device, the mapped file and this container's last
+  // seen cumulative charge of each of its host PIDs.
+  LedgerReader ledger[kMaxDevices];
+  std::map<int, uint64_t> ledger_seen[kMaxDevices];
+  uint64_t ledger_retry_ns[kMaxDevices] = {};
 };
+
+// The node ledger of device `d` when the daemon keeps it fresh (re-mapped at most every
+// 100 ms while absent), else null: the container then samples KFD by itself.
+const LedgerReader* fresh_ledger(Sampler& sm, int d, uint32_t gpu_id, uint64_t now) {
+  const Config& cfg = config();
+  if (cfg.board_dir.empty() || !cfg.use_ledger || !gpu_id) return nullptr;
+  LedgerReader& l = sm.ledger[d];
+  if (!l.attached()) {
+    if (now < sm.ledger_retry_ns[d]) return nullptr;
+    sm.ledger_retry_ns[d] = now + 100'000'000ull;
+    if (!l.open(cfg.board_dir, gpu_id)) return nullptr;
+  }
+  return l.fresh(now) ? &l : nullptr;
+}
+
+// Charge of the interval from the ledger: the growth of the cumulative charges of the
+// container's processes since the last tick (a process seen for the first time starts
+// from its current value).
+int64_t ledger_charge(const LedgerReader& l, std::map<int, uint64_t>& seen, const std::vector<int>& mine,
+                      int64_t* occ_out) {
+  int64_t charge = 0, occ = 0;
+  std::map<int, uint64_t> next;
+  for (int hp : mine) {
+    const LedgerEntry* e = l.find(hp);
+    if (!e) continue;
+    const uint64_t c = e->charged_ns.load(std::memory_order_relaxed);
+    auto it = seen.find(hp);
+    if (it != seen.end() && c >= it->second) charge += (int64_t)(c - it->second);
+    next[hp] = c;
+    occ += std::max(0, e->occ.load(std::memory_order_relaxed));
+  }
+  seen.swap(next);
+  *occ_out = occ;
+  return charge;
+}
 
 // The container's task priority (live: vgpuctl / the monitor may change it).
 int region_priority(const Region* r) { return r->hdr.priority.load(std::memory_order_relaxed); }
@@ -235,11 +276,17 @@ void sample_tick(Region* r, Sampler& sm) {
       continue;
     }
     DeviceState& ds = r->dev[d];
+    const LedgerReader* led =
+        config().charge_model == ChargeModel::kShare ? fresh_ledger(sm, d, a.gpu_id, now) : nullptr;
     if (refresh) {
       std::vector<int> on = kfd_pids_on_gpu(a.gpu_id);
       sm.others[d].clear();
       for (int p : on)
         if (std::find(sm.mine.begin(), sm.mine.end(), p) == sm.mine.end()) sm.others[d].push_back(p);
+      // The tick stretches with the processes on the GPU, ledger or not: with the ledger the
+      // container reads nothing, but longer on/off periods of the gate are part of what
+      // keeps a crowded GPU efficient (profiles/r2aj); the ledger's charge is integrated at
+      // its own period whatever the tick.
       sm.procs = std::max(sm.procs, (int)(sm.mine.size() + sm.others[d].size()));
     }
     int pm = 0;  // the container's share of the GPU at this instant, per mille
@@ -248,7 +295,23 @@ void sample_tick(Region* r, Sampler& sm) {
     const int prio = region_priority(r);
     const bool background = prio >= kPrioBackground;
     bool yield = false;
-    if (!sm.mine.empty() || background) {
+    int64_t led_charge = -1;
+    if (led) {
+      // The node ledger holds every process's charge from one snapshot per period: no
+      // occupancy reads here at all.
+      int64_t mine = 0;
+      led_charge = ledger_charge(*led, sm.ledger_seen[d], sm.mine, &mine);
+      const int64_t total = std::max<int64_t>(mine, led->file()->total_occ.load(std::memory_order_relaxed));
+      pm = (int)timeshare_charge(1000, mine, total);
+      if (background)
+        for (int p : sm.others[d]) {
+          const LedgerEntry* e = led->find(p);
+          if (e && e->occ.load(std::memory_order_relaxed) > 0 && sm.board.priority_of(p, a.gpu_id) < prio) {
+            yield = true;
+            break;
+          }
+        }
+    } else if (!sm.mine.empty() || background) {
       int64_t mine = 0;
       for (int hp : sm.mine) mine += std::max<int64_t>(0, kfd_cu_occupancy(hp, a.gpu_id));
       // Split the instant with whoever else has waves resident on this GPU (other
@@ -271,7 +334,7 @@ void sample_tick(Region* r, Sampler& sm) {
       int busy = device_busy_percent(a.gpu_id);
       pm = busy > 0 ? std::min(busy, 100) * 10 : 0;
     }
-    const int64_t charge = timeshare_interval(dt, sm.prev_pm[d], pm, sm.opened[d]);
+    const int64_t charge = led_charge >= 0 ? led_charge : timeshare_interval(dt, sm.prev_pm[d], pm, sm.opened[d]);
     const bool was_closed = !ds.gate_open.load(std::memory_order_relaxed);
     if (yield) sm.yielded_ns[d] += dt;
     timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, config().limiter_window_ms), dt, charge, yield ? 0 : dt);
@@ -338,8 +401,17 @@ void crowd_tick(Region* r, Sampler& sm, Crowd& c, uint64_t now) {
     // tenant, which goes on the GPU-time gate as soon as anyone else is busy.
     const bool background = region_priority(r) >= kPrioBackground;
     if (!a.gpu_id || ((pct <= 0 || pct >= 100) && !background)) continue;
+    // From the node ledger when it is fresh: busy means waves resident at any of its
+    // samples since the last tick, not only at this instant.
+    const LedgerReader* led = fresh_ledger(sm, d, a.gpu_id, now);
     for (int p : kfd_pids_on_gpu(a.gpu_id)) {
       if (std::find(sm.mine.begin(), sm.mine.end(), p) != sm.mine.end()) continue;
+      if (led) {
+        const LedgerEntry* e = led->find(p);
+        const uint64_t b = e ? e->busy_ns.load(std::memory_order_relaxed) : 0;
+        if (b && (b > now || now - b < 150'000'000ull)) c.busy_at[d][p] = std::min(b, now);
+        continue;
+      }
       if (kfd_cu_occupancy(p, a.gpu_id) > 0) c.busy_at[d][p] = now;
     }
     int busy = 0;

@@ -373,28 +373,82 @@ def _board_env(fake, tmp_path, name, **vgpu):
     return e
 
 
-@pytest.mark.parametrize("neighbour_prio,yields", [("1", True), ("2", False)])
-def test_background_class_yields_to_busier_betters(fake, tmp_path, neighbour_prio, yields):
+@pytest.mark.parametrize("neighbour_prio,yields,ledger", [("1", True, False), ("2", False, False), ("1", True, True)])
+def test_background_class_yields_to_busier_betters(fake, tmp_path, neighbour_prio, yields, ledger):
     """VGPU_TASK_PRIORITY >= 2 (background): while a tenant of higher priority (by its
     board slot) keeps the GPU busy, the background tenant earns no GPU time and its
-    launches wait; next to an equal-priority tenant it runs as usual."""
+    launches wait; next to an equal-priority tenant it runs as usual. The same decision
+    taken from the node ledger's occupancies (vgpu-ledger running)."""
     import subprocess as sp
     (tmp_path / "board").mkdir()
     busy = _board_env(fake, tmp_path, "svc", VGPU_TASK_PRIORITY=neighbour_prio)
     bg = _board_env(fake, tmp_path, "batch", VGPU_TASK_PRIORITY="2")
+    d = _ledger_daemon(fake, tmp_path / "board") if ledger else None
     a = sp.Popen([HARNESS, "stream", "run=2000,6"], env=busy, stdout=sp.PIPE, text=True)
     try:
         time.sleep(1.0)  # the service is busy and on the board
         out = run(bg, "stream", "run=2000,3", timeout=120)
     finally:
         a.wait(timeout=60)
+        if d:
+            d.terminate()
+            d.wait(timeout=10)
     frac = [o for o in out if "run" in o][0]["busy_frac"]
     if yields:
         assert frac < 0.25, frac
     else:
         assert frac > 0.75, frac
-    slots = sorted(os.listdir(tmp_path / "board"))
+    slots = sorted(f for f in os.listdir(tmp_path / "board") if f.endswith(".slot"))
     assert slots == ["batch.slot", "svc.slot"]
+    if ledger:
+        with Region(bg["VGPU_SHARED_CACHE"]) as r:
+            assert r.other_refreshes < 0.2 * r.samples, (r.other_refreshes, r.samples)
+
+
+def _ledger_daemon(fake, board, period_us=1000):
+    import subprocess as sp
+    from amdvgpu.shim.native import LEDGER, lib_path
+    env = dict(os.environ, VGPU_KFD_ROOT=fake.kfd)
+    return sp.Popen([lib_path(LEDGER), "--dir", str(board), "--period-us", str(period_us)], env=env)
+
+
+@pytest.mark.parametrize("ledger", [True, False])
+def test_temporal_limit_through_the_node_ledger(fake, tmp_path, ledger):
+    """With the node's ledger daemon running (vgpu-ledger, one occupancy sampler for the
+    node), a container's GPU-time limiter charges itself from the ledger - no occupancy
+    reads of its own - and still holds its limit; the ledger's cumulative charge of its
+    process matches what the region accounted. Without the daemon it samples by itself."""
+    import subprocess as sp
+    board = tmp_path / "board"
+    board.mkdir()
+    e = _board_env(fake, tmp_path, "lim", VGPU_DEVICE_CU_LIMIT="30", VGPU_CU_MODE="temporal")
+    d = _ledger_daemon(fake, board) if ledger else None
+    try:
+        out = run(e, "stream", "run=2000,3", timeout=120)
+    finally:
+        if d:
+            d.terminate()
+            d.wait(timeout=10)
+    frac = [o for o in out if "run" in o][0]["busy_frac"]
+    pid = out[0]["fake_hostpid"]
+    assert abs(frac - 0.30) <= 0.06, frac
+    with Region(e["VGPU_SHARED_CACHE"]) as r:
+        refreshes, samples, charged = r.other_refreshes, r.samples, r.device(0)["charged_ns"]
+    if not ledger:
+        assert refreshes > 0.1 * samples and not [f for f in os.listdir(board) if f.startswith("ledger.")]
+        return
+    # Every charge after the start (the container's board slot, then the ledger's first
+    # samples: a few hundred ms) came from the ledger.
+    assert refreshes < 0.1 * samples, (refreshes, samples)
+    ledgers = [f for f in os.listdir(board) if f.startswith("ledger.")]
+    assert len(ledgers) == 1, ledgers
+    raw = open(board / ledgers[0], "rb").read()
+    import struct
+    n = struct.unpack_from("<i", raw, 12)[0]
+    entries = {struct.unpack_from("<i", raw, 128 + 32 * i)[0]: struct.unpack_from("<Q", raw, 128 + 32 * i + 8)[0]
+               for i in range(n)}
+    assert pid in entries, (pid, entries)
+    assert entries[pid] >= 0.9 * charged > 0, (entries[pid], charged)
 
 
 def test_background_class_strict_hold(fake, tmp_path):
