@@ -11,6 +11,8 @@ That monitor is not part of the reference; this is the in-tree one.
   monitored usage, CU limit/mask width, utilisation, token bucket, per process
   launches / throttle / suspend seconds / OOM events, suspend state;
 * ``GET /regions``  JSON snapshot of every region;
+* the node GPU-time ledger (``<root>/../board/ledger.<gpu_id>``, ``plugin/ledger.py``):
+  snapshots, reads, period and age per GPU, GPU time charged per host process;
 * ``vgpu_container_info`` names the pod and container a directory belongs to: from the
   kubelet's PodResources (``--pod-resources-socket``, the device IDs the kubelet gave the
   container) when reachable, else the tag the plugin chose at Allocate
@@ -75,8 +77,29 @@ def owners(root, pod_resources_socket=None, resources=("amd.com/gpu",)):
     return attribute(root, pods, set(resources))
 
 
-def render_metrics(root, pod_resources_socket=None, resources=("amd.com/gpu",)):
+def ledger_metrics(w, board_dir):
+    """The node GPU-time ledger (``plugin/ledger.py``): per GPU the daemon's sampling and
+    per process the GPU time it charged."""
+    from .ledger import monotonic_ns, read_board
+    now = monotonic_ns()
+    for gpu_id, led in sorted(read_board(board_dir).items()):
+        lb = {"gpu_id": gpu_id}
+        w.metric("vgpu_ledger_samples_total", "counter", "node ledger: occupancy snapshots of the GPU", lb,
+                 led["samples"])
+        w.metric("vgpu_ledger_reads_total", "counter", "node ledger: KFD cu_occupancy reads", lb, led["reads"])
+        w.metric("vgpu_ledger_period_seconds", "gauge", "node ledger: current sampling period", lb,
+                 led["period_ns"] / 1e9)
+        w.metric("vgpu_ledger_age_seconds", "gauge", "node ledger: time since the last snapshot (stale past 0.05)",
+                 lb, max(0, now - led["heartbeat_ns"]) / 1e9)
+        for p in led["procs"]:
+            w.metric("vgpu_ledger_process_charged_seconds_total", "counter",
+                     "node ledger: processor-sharing GPU time charged to a host process", dict(lb, hostpid=p["pid"]),
+                     p["charged_ns"] / 1e9)
+
+
+def render_metrics(root, pod_resources_socket=None, resources=("amd.com/gpu",), board_dir=None):
     w = MetricsWriter()
+    ledger_metrics(w, board_dir or os.path.join(os.path.dirname(os.path.normpath(root)), "board"))
     regions = discover(root)
     w.metric("vgpu_monitor_regions", "gauge", "container regions found", {}, sum(len(v) for v in regions.values()))
     who = owners(root, pod_resources_socket, resources)

@@ -451,6 +451,33 @@ def test_temporal_limit_through_the_node_ledger(fake, tmp_path, ledger):
     assert entries[pid] >= 0.9 * charged > 0, (entries[pid], charged)
 
 
+def test_ledger_reader_and_monitor_metrics(fake, tmp_path):
+    """The Python reader (plugin/ledger.py) parses the daemon's file - layout and all - and
+    the node monitor exports it: snapshots, reads and each host process's charged time."""
+    from amdvgpu.plugin.ledger import read_board
+    from amdvgpu.plugin.monitor import render_metrics
+    board = tmp_path / "board"
+    board.mkdir()
+    (tmp_path / "shared").mkdir()
+    e = _board_env(fake, tmp_path, "lim", VGPU_DEVICE_CU_LIMIT="50", VGPU_CU_MODE="temporal")
+    d = _ledger_daemon(fake, board)
+    try:
+        out = run(e, "stream", "run=2000,1.5", timeout=120)
+        leds = read_board(str(board))
+        text = render_metrics(str(tmp_path / "shared"))
+    finally:
+        d.terminate()
+        d.wait(timeout=10)
+    pid = out[0]["fake_hostpid"]
+    assert len(leds) == 1, leds
+    led = next(iter(leds.values()))
+    assert led["samples"] > 100 and led["reads"] >= led["samples"] // 2 and led["period_ns"] == 1_000_000, led
+    mine = [p for p in led["procs"] if p["pid"] == pid]
+    assert mine and 0.3e9 < mine[0]["charged_ns"] < 1.2e9, led["procs"]   # ~50 % of ~1.5 s busy
+    assert f'vgpu_ledger_process_charged_seconds_total{{gpu_id="{led["gpu_id"]}",hostpid="{pid}"}}' in text
+    assert "vgpu_ledger_samples_total" in text and "vgpu_ledger_age_seconds" in text
+
+
 def test_background_class_strict_hold(fake, tmp_path):
     """VGPU_PREEMPT_HOLD_MS: a background tenant's launches are held outright while a
     better class has waves resident (and for the hold after), not merely left to run
