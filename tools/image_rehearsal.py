@@ -151,7 +151,7 @@ def rehearse(work, log=print):
 
 def check_runtime(final, work, log=print):
     lib = final.path("/opt/amd-vgpu/4paradigm-k8s-device-plugin_amd/lib")
-    for f in ("libvgpu_hip.so", "libvgpu_region.so", "vgpuctl", "vgpu-validate", "ld.so.preload"):
+    for f in ("libvgpu_hip.so", "libvgpu_region.so", "vgpuctl", "vgpu-ledger", "vgpu-validate", "ld.so.preload"):
         if not os.path.exists(os.path.join(lib, f)):
             raise RuntimeError(f"image lacks {f}")
     dest = os.path.join(work, "host-usr-local-vgpu")
