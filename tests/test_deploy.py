@@ -56,7 +56,7 @@ def test_image_build_inputs_exist():
     for src in re.findall(r"^COPY (?!--from)(\S+)", df, re.M):
         assert os.path.exists(os.path.join(repo, src.rstrip("/"))), src
     targets = re.findall(r"\.\./4paradigm-k8s-device-plugin_amd/lib/(\S+)", df)
-    assert set(targets) == {"libvgpu_hip.so", "libvgpu_region.so", "vgpuctl", "vgpu-validate"}
+    assert set(targets) == {"libvgpu_hip.so", "libvgpu_region.so", "vgpuctl", "vgpu-ledger", "vgpu-validate"}
     for t in targets:  # make knows how to build each one (dry run)
         rc = subprocess.call(["make", "-n", "-C", os.path.join(repo, "native"),
                               f"../4paradigm-k8s-device-plugin_amd/lib/{t}"], stdout=subprocess.DEVNULL)
