@@ -70,6 +70,7 @@ class LedgerReader {
   // (Re)maps the file; false when it is absent or foreign. Cheap to call again.
   bool open(const std::string& dir, uint32_t gpu_id);
   bool attached() const { return f_ != nullptr; }
+  void close();
   // Attached and sampled within kLedgerStaleNs of `now`.
   bool fresh(uint64_t now) const;
   const LedgerFile* file() const { return f_; }

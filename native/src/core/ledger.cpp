@@ -12,8 +12,11 @@ std::string ledger_path(const std::string& dir, uint32_t gpu_id) {
   return dir + "/ledger." + std::to_string(gpu_id);
 }
 
-LedgerReader::~LedgerReader() {
+LedgerReader::~LedgerReader() { close(); }
+
+void LedgerReader::close() {
   if (f_) munmap(const_cast<LedgerFile*>(f_), sizeof(LedgerFile));
+  f_ = nullptr;
 }
 
 bool LedgerReader::open(const std::string& dir, uint32_t gpu_id) {

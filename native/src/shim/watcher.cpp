@@ -141,12 +141,15 @@ const LedgerReader* fresh_ledger(Sampler& sm, int d, uint32_t gpu_id, uint64_t n
   const Config& cfg = config();
   if (cfg.board_dir.empty() || !cfg.use_ledger || !gpu_id) return nullptr;
   LedgerReader& l = sm.ledger[d];
-  if (!l.attached()) {
-    if (now < sm.ledger_retry_ns[d]) return nullptr;
-    sm.ledger_retry_ns[d] = now + 100'000'000ull;
-    if (!l.open(cfg.board_dir, gpu_id)) return nullptr;
-  }
-  return l.fresh(now) ? &l : nullptr;
+  if (l.attached() && l.fresh(now)) return &l;
+  // Absent, or stale: a restarted daemon writes a new file under the same name, so a
+  // stale mapping is dropped and the name opened again.
+  if (now < sm.ledger_retry_ns[d]) return nullptr;
+  sm.ledger_retry_ns[d] = now + 100'000'000ull;
+  l.close();
+  if (!l.open(cfg.board_dir, gpu_id) || !l.fresh(now)) return nullptr;
+  sm.ledger_seen[d].clear();  // another file: cumulative charges start over
+  return &l;
 }
 
 // Charge of the interval from the ledger: the growth of the cumulative charges of the
