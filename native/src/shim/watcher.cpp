@@ -276,6 +276,9 @@ void sample_tick(Region* r, Sampler& sm) {
       r->dev[d].preempt.store(0, std::memory_order_relaxed);  // and any strict-yield state
       r->dev[d].depth_cap.store(0, std::memory_order_relaxed);
       sm.preempt_until[d] = 0;
+      // Off the limiter nothing is charged: the ledger's growth meanwhile must not be
+      // charged on the way back either.
+      sm.ledger_seen[d].clear();
       continue;
     }
     DeviceState& ds = r->dev[d];
@@ -303,7 +306,10 @@ void sample_tick(Region* r, Sampler& sm) {
       // The node ledger holds every process's charge from one snapshot per period: no
       // occupancy reads here at all.
       int64_t mine = 0;
-      led_charge = ledger_charge(*led, sm.ledger_seen[d], sm.mine, &mine);
+      // At most the interval's wall time (the processes' shares of one snapshot add up to
+      // at most 1), plus one ledger period of misalignment between the two clocks.
+      led_charge = std::min<int64_t>(ledger_charge(*led, sm.ledger_seen[d], sm.mine, &mine),
+                                     dt + (int64_t)led->file()->period_ns.load(std::memory_order_relaxed));
       const int64_t total = std::max<int64_t>(mine, led->file()->total_occ.load(std::memory_order_relaxed));
       pm = (int)timeshare_charge(1000, mine, total);
       if (background)
@@ -501,6 +507,7 @@ void* watcher_main(void*) {
       sample_tick(r, sm);
     } else {
       sm.last_ns = 0;
+      for (auto& seen : sm.ledger_seen) seen.clear();  // nothing charged meanwhile (sample_tick)
     }
     if (now >= next_slow) {
       next_slow = now + period_ns;

@@ -451,6 +451,33 @@ def test_temporal_limit_through_the_node_ledger(fake, tmp_path, ledger):
     assert entries[pid] >= 0.9 * charged > 0, (entries[pid], charged)
 
 
+def test_ledger_charge_not_carried_across_limiter_exit(fake, tmp_path):
+    """A container that leaves the GPU-time limiter (its share lifted live) and comes back
+    is not charged for what its processes ran in between: the ledger's cumulative charge
+    grew meanwhile, and charging that growth on the way back would bury the container in
+    debt (profiles/r3u: one of 16 pods at 14 img/s)."""
+    board = tmp_path / "board"
+    board.mkdir()
+    e = _board_env(fake, tmp_path, "lim", VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="temporal")
+    d = _ledger_daemon(fake, board)
+    p = subprocess.Popen([HARNESS, "stream", "run=2000,1.0", "run=2000,1.5", "run=2000,2.0"], env=e,
+                         stdout=subprocess.PIPE, text=True)
+    try:
+        lines = [json.loads(p.stdout.readline()) for _ in range(3)]  # pid, stream, first run done
+        with Region(e["VGPU_SHARED_CACHE"]) as r:
+            r.set_cu_limit(0, 100)   # off the limiter: runs flat out, the ledger keeps counting
+            lines.append(json.loads(p.stdout.readline()))
+            r.set_cu_limit(0, 25)    # back on it
+        rest = [json.loads(l) for l in p.stdout.read().splitlines() if l.startswith("{")]
+        assert p.wait(60) == 0
+    finally:
+        d.terminate()
+        d.wait(timeout=10)
+    runs = [o for o in lines + rest if "run" in o]
+    assert runs[1]["busy_frac"] > 0.7, runs           # unlimited in between
+    assert 0.12 < runs[2]["busy_frac"] < 0.4, runs    # back at ~25 %, not starved by carried debt
+
+
 def test_ledger_reader_and_monitor_metrics(fake, tmp_path):
     """The Python reader (plugin/ledger.py) parses the daemon's file - layout and all - and
     the node monitor exports it: snapshots, reads and each host process's charged time."""
