@@ -129,6 +129,37 @@ def test_temporal_accuracy_single_tenant(native_spin_rate, limit):
     assert abs(achieved - limit) <= 5.0, f"limit {limit}%: achieved {achieved:.1f}%"
 
 
+def test_temporal_accuracy_through_the_node_ledger(native_spin_rate, tmp_path):
+    """The node ledger on real KFD: with vgpu-ledger running over the board, two spinning
+    tenants at 25 % (temporal) charge themselves from the ledger - almost no occupancy reads
+    of their own - and together hold 2 x 25 % of the GPU."""
+    import subprocess as sp
+    from amdvgpu.plugin.ledger import read_board
+    from amdvgpu.shim.native import LEDGER, lib_path
+    board = tmp_path / "board"
+    board.mkdir()
+    cs = [vgpu_env(cu_limit=25, cu_mode="temporal", extra={"VGPU_BOARD_DIR": str(board),
+                                                          "VGPU_BOARD_SLOT": f"t{i}.slot"}) for i in range(2)]
+    d = sp.Popen([lib_path(LEDGER), "--dir", str(board)])
+    try:
+        got = _spin_rates(cs, secs=4.0)
+        leds = read_board(str(board))
+        stats = []
+        for c in cs:
+            with Region(c["VGPU_SHARED_CACHE"]) as r:
+                stats.append((r.samples, r.other_refreshes))
+    finally:
+        d.terminate()
+        d.wait(timeout=10)
+        for c in cs:
+            cleanup_region(c)
+    achieved = [100.0 * g / native_spin_rate for g in got]
+    print(json.dumps({"achieved_pct": achieved, "sampler": stats, "ledgers": {k: v["samples"] for k, v in leds.items()}}))
+    assert len(leds) == 1 and next(iter(leds.values()))["samples"] > 500, leds
+    assert all(refr < 0.2 * smp for smp, refr in stats), stats
+    assert abs(sum(achieved) - 50.0) <= 8.0 and all(a >= 15.0 for a in achieved), achieved
+
+
 def test_temporal_accuracy_two_tenants_stock_resnet(tmp_path):
     """Two stock fp32 ResNet-50 tenants at 25 % each, concurrently: each gets 25 % of the
     GPU's solo throughput (charged by its share of the resident waves while they overlap).
