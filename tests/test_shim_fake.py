@@ -478,6 +478,37 @@ def test_ledger_charge_not_carried_across_limiter_exit(fake, tmp_path):
     assert 0.12 < runs[2]["busy_frac"] < 0.4, runs    # back at ~25 %, not starved by carried debt
 
 
+def test_ledger_daemon_restart(fake, tmp_path):
+    """The plugin restarts a ledger daemon that died; the new one writes a new file under
+    the same name, which the container maps again (cumulative charges start over) - the
+    limit holds across the switch, and the container is back on the ledger afterwards."""
+    board = tmp_path / "board"
+    board.mkdir()
+    e = _board_env(fake, tmp_path, "lim", VGPU_DEVICE_CU_LIMIT="30", VGPU_CU_MODE="temporal")
+    d = _ledger_daemon(fake, board)
+    p = subprocess.Popen([HARNESS, "stream", "run=2000,1.5", "run=2000,2.5"], env=e, stdout=subprocess.PIPE,
+                         text=True)
+    try:
+        lines = [json.loads(p.stdout.readline()) for _ in range(3)]
+        d.kill()
+        d.wait(timeout=10)
+        time.sleep(0.3)  # stale: the container samples by itself meanwhile
+        d = _ledger_daemon(fake, board)
+        time.sleep(0.5)
+        with Region(e["VGPU_SHARED_CACHE"]) as r:
+            before = r.other_refreshes
+        rest = [json.loads(l) for l in p.stdout.read().splitlines() if l.startswith("{")]
+        assert p.wait(60) == 0
+        with Region(e["VGPU_SHARED_CACHE"]) as r:
+            after, samples = r.other_refreshes, r.samples
+    finally:
+        d.terminate()
+        d.wait(timeout=10)
+    runs = [o for o in lines + rest if "run" in o]
+    assert all(abs(x["busy_frac"] - 0.30) <= 0.07 for x in runs), runs
+    assert after - before < 0.1 * samples, (before, after, samples)   # back on the new ledger
+
+
 def test_ledger_reader_and_monitor_metrics(fake, tmp_path):
     """The Python reader (plugin/ledger.py) parses the daemon's file - layout and all - and
     the node monitor exports it: snapshots, reads and each host process's charged time."""
