@@ -57,7 +57,7 @@ class PluginConfig:
     duplicate_vgpus: str = "reject"         # Allocate of two vGPUs of one GPU: reject | merge
     host_memory_per_vgpu: str = "0"         # pinned host memory budget per vGPU (0 = unlimited)
     gpu_concurrency: int = 0                # limited containers holding a GPU's time at once (0 = any)
-    ledger: bool = True                     # run the node's GPU-time ledger daemon (vgpu-ledger)
+    ledger: bool = False                    # run the node's GPU-time ledger daemon (vgpu-ledger; profiles/r3v)
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"  # kubelet PodResources v1
     version_requested: bool = False
     extra: dict = field(default_factory=dict)
@@ -146,7 +146,9 @@ _FLAGS = [
      "(0 = no admission: every container whose credit allows runs)"),
     ("--ledger", "ledger", "bool", ["VGPU_NODE_LEDGER"],
      "run the node GPU-time ledger (vgpu-ledger): one KFD occupancy sampler for every limited container of the "
-     "node instead of one per container (n reads per period instead of n^2, one consistent snapshot)"),
+     "node instead of one per container (n reads per period instead of n^2, one consistent snapshot); "
+     "off by default: with the rounded-up shares of a fully split GPU its exact charges leave the limiter "
+     "slack and the pods' spread widens (profiles/r3v)"),
     ("--pod-resources-socket", "pod_resources_socket", str, ["POD_RESOURCES_SOCKET"],
      "kubelet PodResources socket: monitor mode attributes container directories to the pods holding their "
      "vGPUs through it (missing socket: the Allocate-time pod match stands)"),

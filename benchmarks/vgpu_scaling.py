@@ -118,13 +118,13 @@ def stuck_report(outs, regions, procs):
         print("STUCK " + json.dumps(info), flush=True)
 
 
-def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None, split=0):
+def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None, split=0, ledger=False):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="scal-")
     go = os.path.join(tmp, "go")
     procs, outs, regions = [], [], []
-    with NodeHarness(backend, device_split_count=split or n, cu_mode=MODES[policy]) as node:
+    with NodeHarness(backend, device_split_count=split or n, cu_mode=MODES[policy], ledger=ledger) as node:
         for i, vid in enumerate(node.vgpu_ids(uuid)[:n]):
             envs, mounts = node.pod([vid])
             out = os.path.join(tmp, f"t{i}.json")
@@ -182,6 +182,7 @@ def main():
                     help="KEY=V1,V2,...: extra env in every pod, one sweep per value (repeatable)")
     ap.add_argument("--repeats", type=int, default=1)
     ap.add_argument("--split", type=int, default=0, help="vGPUs per GPU (default: one per pod)")
+    ap.add_argument("--node-ledger", action="store_true", help="the plugin runs the node GPU-time ledger (vgpu-ledger)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--go")
@@ -208,7 +209,7 @@ def main():
                         if n == 1 and k > 0:
                             continue
                         r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq,
-                                      pe if n > 1 else None, a.split)
+                                      pe if n > 1 else None, a.split, ledger=a.node_ledger)
                         rows.append(r)
                         print(json.dumps(r), flush=True)
     base = {r["policy"]: r["aggregate_throughput"] for r in rows if r["tenants"] == 1}

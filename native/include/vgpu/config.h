@@ -99,7 +99,8 @@ struct Config {
                                          // gates may be open together on one GPU (0 = any number)
   int gpu_slice_ms = 20;                 // VGPU_GPU_SLICE_MS: turn length under that admission
   bool use_ledger = true;                // VGPU_LEDGER: take charges from the node's GPU-time ledger
-                                         // (vgpu/ledger.h) when its daemon keeps it fresh
+                                         // (vgpu/ledger.h) when its daemon keeps it fresh (the plugin
+                                         // runs the daemon only with --ledger: profiles/r3v)
   int preempt_hold_ms = 3;               // VGPU_PREEMPT_HOLD_MS: background class - launches held while a
                                          // better class has waves on the GPU and this long after (0 = the
                                          // soft yield: only no credit is earned; profiles/r3s, r3t)
