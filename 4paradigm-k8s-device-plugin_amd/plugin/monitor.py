@@ -157,6 +157,11 @@ def render_metrics(root, pod_resources_socket=None, resources=("amd.com/gpu",), 
                          d["credit_ns"] / 1e9)
                 w.metric("vgpu_compute_charged_seconds_total", "counter", "GPU time charged to the container", lb,
                          d["charged_ns"] / 1e9)
+                w.metric("vgpu_preempted", "gauge", "background class: launches held while a better class is busy",
+                         lb, int(d.get("preempt", False)))
+                w.metric("vgpu_inflight_cap", "gauge",
+                         "background class: AQL packets in flight allowed per process (0 = unbounded)", lb,
+                         d.get("depth_cap", 0))
             for p in snap["procs"]:
                 lp = dict(base, pid=p["pid"], hostpid=p["hostpid"])
                 w.metric("vgpu_process_launches_total", "counter", "kernel launches through the gates", lp,

@@ -42,11 +42,11 @@ static void show(vgpu_region* r) {
     printf("%s\n  {\"index\": %d, \"uuid\": \"%s\", \"mem_limit\": %llu, \"phys_total\": %llu, \"used\": %llu, "
            "\"spilled\": %llu, \"monitor_used\": %llu, \"cu_limit_pct\": %d, \"cu_count\": %d, \"cu_mask_count\": %d, "
            "\"util_pct\": %d, \"cu_mode\": %d, \"crowd\": %d, \"credit_ns\": %lld, \"charged_ns\": %llu, "
-           "\"wall_ns\": %llu}",
+           "\"wall_ns\": %llu, \"preempt\": %d, \"depth_cap\": %d}",
            d ? "," : "", d, di.uuid, (unsigned long long)di.mem_limit, (unsigned long long)di.phys_total,
            (unsigned long long)di.used, (unsigned long long)di.spilled, (unsigned long long)di.monitor_used,
            di.cu_limit_pct, di.cu_count, di.cu_mask_count, di.util_pct, di.cu_mode, di.crowd, (long long)di.credit_ns,
-           (unsigned long long)di.charged_ns, (unsigned long long)di.wall_ns);
+           (unsigned long long)di.charged_ns, (unsigned long long)di.wall_ns, di.preempt, di.depth_cap);
   }
   printf("],\n \"processes\": [");
   static vgpu_proc_info procs[1024];
