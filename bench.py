@@ -128,6 +128,8 @@ def worker(args):
         dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     if args.mode == "rccl":
         return rccl_probe(args, device, rank, world)
+    if cpu and args.mode == "node" and os.environ.get("VGPU_BENCH_FAIL_NODE_RANK") == str(rank):
+        raise SystemExit("rehearsal: this rank's node pods fail")  # tests/test_bench_contract.py
     sync = (lambda: None) if cpu else (lambda: torch.cuda.synchronize(device))
     free0, total = torch.cuda.mem_get_info(device) if not cpu else (0, 0)
     quota = int(os.environ.get("VGPU_DEVICE_MEMORY_LIMIT_0", "0").rstrip("m") or 0) << 20

@@ -60,6 +60,24 @@ def test_bench_multi_rank_cpu_rehearsal(world, tmp_path):
     assert len({lf for s in locks.values() for lf in s}) == 3 * world  # one per plugin instance
 
 
+@pytest.mark.slow
+def test_node_point_survives_a_failing_rank(tmp_path):
+    """A rank whose pods fail in the node point reaches the cross-rank barrier anyway: the
+    job completes, rank 0 prints its line, and the node entry lists the failure instead of
+    the whole run hanging until the driver's limit."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--sweep-seconds", "1", "--modes", "native",
+           "--rccl-probe", "0", "--cpu-rehearsal"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", VGPU_BENCH_FAIL_NODE_RANK="1")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    r = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    node = r["node"]
+    assert node["gpus_measured"] == 1 and len(node["failures"]) == 1 and node["vgpus"] == 8, node
+
+
 def test_sweep_respects_the_time_budget(monkeypatch):
     """The driver kills bench.py at its own limit: sweep points that would not finish within
     --time-budget are skipped and reported, and max_vgpus_per_gpu only counts measured points."""
