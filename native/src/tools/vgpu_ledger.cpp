@@ -8,8 +8,9 @@
 // nothing; the period stretches when the node-wide reads per base period exceed the
 // read budget, as the containers' own samplers do (ratelimit.h sample_period_ns).
 //
-//   vgpu-ledger --dir <board dir> [--period-us 1000] [--read-budget 32] [--samples N]
+//   vgpu-ledger --dir <board dir> [--period-us 1000] [--read-budget 32] [--samples N] [--gpu ID]...
 //
+// --gpu samples that KFD gpu_id whether or not a container lists it (tests, operators).
 // VGPU_KFD_ROOT points it at a fake KFD tree (tests). It exits with its parent.
 #include <fcntl.h>
 #include <signal.h>
@@ -164,7 +165,8 @@ const char* arg_str(int argc, char** argv, const char* name) {
 int main(int argc, char** argv) {
   const char* dir = arg_str(argc, argv, "--dir");
   if (!dir) {
-    fprintf(stderr, "usage: vgpu-ledger --dir <board dir> [--period-us 1000] [--read-budget 32] [--samples N]\n");
+    fprintf(stderr, "usage: vgpu-ledger --dir <board dir> [--period-us 1000] [--read-budget 32] [--samples N] "
+                    "[--gpu ID]...\n");
     return 2;
   }
   const int64_t base_ns = std::max(100L, arg_long(argc, argv, "--period-us", 1000)) * 1000;
@@ -176,6 +178,9 @@ int main(int argc, char** argv) {
   signal(SIGTERM, on_signal);
   signal(SIGINT, on_signal);
 
+  std::set<uint32_t> always;
+  for (int i = 1; i + 1 < argc; i++)
+    if (!strcmp(argv[i], "--gpu")) always.insert((uint32_t)strtoul(argv[i + 1], nullptr, 10));
   Board board;
   board.open_readonly(dir);
   std::map<uint32_t, Gpu> gpus;
@@ -185,7 +190,7 @@ int main(int argc, char** argv) {
     const uint64_t now = now_ns();
     if (now >= next_refresh) {
       next_refresh = now + 100'000'000ull;
-      std::set<uint32_t> active;
+      std::set<uint32_t> active = always;
       for (const BoardPeer& p : board.refresh(now))
         for (uint32_t id : p.gpu_ids)
           if (id) active.insert(id);

@@ -509,6 +509,33 @@ def test_ledger_daemon_restart(fake, tmp_path):
     assert after - before < 0.1 * samples, (before, after, samples)   # back on the new ledger
 
 
+def test_ledger_processor_sharing_math(tmp_path):
+    """The daemon's integral on a fixed KFD picture: processes holding 30, 10 and 0 of the
+    GPU's resident waves are charged 3/4, 1/4 and none of the elapsed time, and the charges
+    add up to the time the daemon has been sampling."""
+    import subprocess as sp
+    from amdvgpu.plugin.ledger import read_board
+    from amdvgpu.shim.native import LEDGER, lib_path
+    kfd, board = tmp_path / "kfd", tmp_path / "board"
+    board.mkdir()
+    for pid, occ in ((4101, 30), (4102, 10), (4103, 0)):
+        d = kfd / str(pid) / "stats_777"
+        d.mkdir(parents=True)
+        (d / "cu_occupancy").write_text(str(occ))
+    env = dict(os.environ, VGPU_KFD_ROOT=str(kfd))
+    p = sp.Popen([lib_path(LEDGER), "--dir", str(board), "--gpu", "777", "--period-us", "500"], env=env)
+    try:
+        time.sleep(1.5)
+        led = read_board(str(board))[777]
+    finally:
+        p.terminate()
+        p.wait(timeout=10)
+    c = {e["pid"]: e["charged_ns"] for e in led["procs"]}
+    total = sum(c.values())
+    assert led["total_occ"] == 40 and 1.0e9 < total < 1.6e9, (led["total_occ"], total)
+    assert abs(c[4101] / total - 0.75) < 0.01 and abs(c[4102] / total - 0.25) < 0.01 and c[4103] == 0, c
+
+
 def test_ledger_reader_and_monitor_metrics(fake, tmp_path):
     """The Python reader (plugin/ledger.py) parses the daemon's file - layout and all - and
     the node monitor exports it: snapshots, reads and each host process's charged time."""
