@@ -282,8 +282,10 @@ void sample_tick(Region* r, Sampler& sm) {
       continue;
     }
     DeviceState& ds = r->dev[d];
-    const LedgerReader* led =
-        config().charge_model == ChargeModel::kShare ? fresh_ledger(sm, d, a.gpu_id, now) : nullptr;
+    // (No host PID known yet: the device-wide fallback below, as without a ledger.)
+    const LedgerReader* led = config().charge_model == ChargeModel::kShare && !(sm.mine.empty() && sm.unknown)
+                                  ? fresh_ledger(sm, d, a.gpu_id, now)
+                                  : nullptr;
     if (refresh) {
       std::vector<int> on = kfd_pids_on_gpu(a.gpu_id);
       sm.others[d].clear();
