@@ -132,9 +132,10 @@ def test_temporal_accuracy_single_tenant(native_spin_rate, limit):
 def test_temporal_limit_through_the_node_ledger(native_spin_rate, tmp_path):
     """The node ledger on real KFD (opt-in, `--ledger`): with vgpu-ledger running over the
     board, two spinning tenants at 25 % (temporal) charge themselves from the ledger -
-    almost no occupancy reads of their own - and are held well below their solo rate. The
-    ledger's charges run ~25 % below the containers' own sampling here (32.6 % each for
-    25 %, profiles/r3x): the bound is the limit binding, not its accuracy."""
+    almost no occupancy reads of their own - and are held well below their solo rate. Two
+    spin kernels co-run without slowing each other, so a processor-sharing charge gives
+    each more than its share (32.6 % for 25 %, profiles/r3x): the bound is the limit
+    binding, not its accuracy (test_temporal_accuracy_two_tenants_stock_resnet)."""
     import subprocess as sp
     from amdvgpu.plugin.ledger import read_board
     from amdvgpu.shim.native import LEDGER, lib_path
