@@ -260,6 +260,11 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
             resp.envs[f"VGPU_DEVICE_HBM_LIMIT_{i}"] = format_mib(v.hbm_limit)
         if v.cu_pct:
             resp.envs[f"VGPU_DEVICE_CU_LIMIT_{i}"] = str(v.cu_pct)
+            # With the node ledger the limiter's charges are exact (one snapshot, adding up
+            # to at most the GPU's busy time), so its grants take the exact share instead of
+            # the rounded-up percent (profiles/r3v, r3w).
+            if getattr(cfg, "ledger", False) and v.cu_share and v.cu_share != v.cu_pct:
+                resp.envs[f"VGPU_DEVICE_CU_SHARE_{i}"] = f"{v.cu_share:g}"
             if v.cu_range:
                 resp.envs[f"VGPU_DEVICE_CU_RANGE_{i}"] = f"{v.cu_range[0]}-{v.cu_range[1]}"
         dmap.append(f"{i}:{v.uuid}")

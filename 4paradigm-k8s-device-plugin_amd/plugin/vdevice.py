@@ -72,6 +72,7 @@ class VDevice:
     hbm_limit: int         # HBM-resident cap in bytes (0 = same as quota)
     cu_pct: int            # 0 = unlimited
     cu_range: tuple        # (begin, end) logical CUs, or None
+    cu_share: float = 0.0  # exact share in percent (100 * cores_scaling / split); 0 = unlimited
 
     @property
     def uuid(self):
@@ -100,9 +101,10 @@ def device_to_vdevices(devices, split, memory_scaling=1.0, cores_scaling=1.0):
         pct = math.ceil(round(100 * cores_scaling / split, 6))
         if pct >= 100:
             pct = 0
+        share = round(100 * cores_scaling / split, 4) if pct else 0.0
         for i in range(split):
             rng = cu_range_for(d.cu_count, d.num_xcc, split, i, pct) if pct else None
-            out.append(VDevice(f"{d.uuid}-{i}", d, i, mem, hbm, pct, rng))
+            out.append(VDevice(f"{d.uuid}-{i}", d, i, mem, hbm, pct, rng, share))
     return out
 
 

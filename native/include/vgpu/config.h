@@ -65,6 +65,8 @@ struct DeviceConfig {
   uint64_t mem_limit = 0;      // bytes, 0 = unlimited
   uint64_t hbm_limit = 0;      // HBM-resident cap (oversubscription), 0 = mem_limit
   int cu_limit_pct = 0;        // 0 or >= 100 = unlimited
+  int cu_share_bp = 0;         // VGPU_DEVICE_CU_SHARE_<i>: exact GPU-time share in basis points for the
+                               // limiter's grants (0 = cu_limit_pct); the plugin sends it with --ledger
   int cu_range_begin = -1;     // explicit logical CU range [begin, end) or -1 = derive
   int cu_range_end = -1;
   char uuid[64] = {0};         // physical UUID from VGPU_DEVICE_MAP (may be empty)

@@ -38,6 +38,7 @@ namespace vgpu {
 
 struct TimeShareParams {
   int limit_pct = 100;       // 0 or >= 100 = unlimited
+  int limit_bp = 0;          // exact share in basis points (0 = limit_pct)
   int64_t burst_ns = 0;      // positive credit cap
   int64_t debt_ns = 0;       // negative credit floor (as a positive number)
   int64_t reopen_ns = 0;     // a closed gate re-opens once the credit reaches this
@@ -48,7 +49,7 @@ struct TimeShareParams {
 // long instead of one sample: every restart after an idle gap costs the tenant some
 // throughput (clocks and caches ramp up again), so fewer, longer periods track the
 // limit more closely (profiles/r2b vs r2c).
-TimeShareParams timeshare_params(int limit_pct, int window_ms = 40);
+TimeShareParams timeshare_params(int limit_pct, int window_ms = 40, int limit_bp = 0);
 
 // Gate state after a sample: an open gate stays open while credit > 0; a closed gate
 // re-opens once credit >= reopen_ns.

@@ -105,8 +105,12 @@ struct alignas(64) DeviceState {
   // of the container keeps in flight on this device (0 = none). Written by the sampler.
   std::atomic<int32_t> preempt;
   std::atomic<int32_t> depth_cap;
+  // Exact GPU-time share of the limiter's grants, basis points (0 = cu_limit_pct): the
+  // plugin's CU limit is a whole percent rounded up, so a split-16 vGPU's 6.25 % is 7 %.
+  int32_t cu_share_bp;
 };
-// preempt / depth_cap sit in what was tail padding in layout v5: the layout is unchanged.
+// preempt / depth_cap / cu_share_bp sit in what was tail padding in layout v5: the layout
+// is unchanged.
 static_assert(sizeof(DeviceState) == 320, "DeviceState layout changed");
 
 struct RegionHeader {

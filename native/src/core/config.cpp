@@ -223,6 +223,14 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
         VLOG_WARN("invalid %s=%s ignored", key, s);
       }
     }
+    snprintf(key, sizeof(key), "VGPU_DEVICE_CU_SHARE_%d", i);
+    if (const char* s = getenv_fn(key)) {
+      // A decimal percent ("6.25"): the exact share of a vGPU whose CU limit was rounded up.
+      char* end = nullptr;
+      const double v = strtod(s, &end);
+      if (end != s && !*end && v > 0.0 && v <= 100.0) d.cu_share_bp = (int)(v * 100.0 + 0.5);
+      else VLOG_WARN("invalid %s=%s ignored", key, s);
+    }
     snprintf(key, sizeof(key), "VGPU_DEVICE_CU_RANGE_%d", i);
     if (const char* s = getenv_fn(key)) {
       if (!parse_range(s, &d.cu_range_begin, &d.cu_range_end)) {

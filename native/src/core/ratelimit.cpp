@@ -12,12 +12,14 @@ uint64_t now_ns() {
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
-TimeShareParams timeshare_params(int limit_pct, int window_ms) {
+TimeShareParams timeshare_params(int limit_pct, int window_ms, int limit_bp) {
   TimeShareParams p;
   p.limit_pct = limit_pct;
-  int pct = limit_pct > 0 && limit_pct < 100 ? limit_pct : 100;
+  const bool limited = limit_pct > 0 && limit_pct < 100;
+  p.limit_bp = limited && limit_bp > 0 && limit_bp < 10000 ? limit_bp : 0;
+  const int64_t bp = p.limit_bp ? p.limit_bp : (limited ? limit_pct : 100) * 100;
   if (window_ms <= 0) window_ms = 40;
-  p.burst_ns = std::max<int64_t>(4'000'000, (int64_t)window_ms * 1'000'000ll * pct / 100);
+  p.burst_ns = std::max<int64_t>(4'000'000, (int64_t)window_ms * 1'000'000ll * bp / 10000);
   p.reopen_ns = p.burst_ns / 2;
   p.debt_ns = 2'000'000'000ll;
   return p;
@@ -46,8 +48,8 @@ int64_t timeshare_step(int64_t credit, const TimeShareParams& p, int64_t dt_ns, 
                        int64_t grant_dt_ns) {
   if (dt_ns < 0) dt_ns = 0;
   if (grant_dt_ns < 0 || grant_dt_ns > dt_ns) grant_dt_ns = dt_ns;
-  int pct = p.limit_pct > 0 && p.limit_pct < 100 ? p.limit_pct : 100;
-  credit += grant_dt_ns * pct / 100 - charge_ns;
+  const int64_t bp = p.limit_bp > 0 ? p.limit_bp : (p.limit_pct > 0 && p.limit_pct < 100 ? p.limit_pct : 100) * 100;
+  credit += grant_dt_ns * bp / 10000 - charge_ns;
   if (credit > p.burst_ns) credit = p.burst_ns;
   if (credit < -p.debt_ns) credit = -p.debt_ns;
   return credit;

@@ -193,6 +193,7 @@ void SharedRegion::init_fresh(const Config* cfg) {
       d.mem_limit = cfg->dev[i].mem_limit;
       d.hbm_limit = cfg->dev[i].hbm_limit;
       d.cu_limit_pct = cfg->dev[i].cu_limit_pct;
+      d.cu_share_bp = cfg->dev[i].cu_share_bp;
       d.cu_range_begin = cfg->dev[i].cu_range_begin;
       d.cu_range_end = cfg->dev[i].cu_range_end;
       memcpy(d.uuid, cfg->dev[i].uuid, sizeof(d.uuid));
@@ -502,6 +503,7 @@ void SharedRegion::set_cu_limit(int dev, int pct) {
   DeviceState& d = r_->dev[dev];
   bool locked = lock_for(kLockTimeoutMs);  // node tools must not hang behind a stopped tenant
   d.cu_limit_pct = pct;
+  d.cu_share_bp = 0;  // a live share is a whole percent
   if (d.configured && d.cu_count > 0) {
     // Keep the vGPU's anchor (the start of the slice the plugin assigned) and resize the
     // slice to the new share, shifted left when it would run past the last CU.

@@ -667,6 +667,12 @@ static void test_ratelimit() {
   CHECK_EQ(timeshare_step(-p.debt_ns, p, 1000000, 1000000), -p.debt_ns);
   // Unlimited: grants the whole interval.
   CHECK_EQ(timeshare_step(0, timeshare_params(0), 1000000, 1000000), 0);
+  // Exact share (basis points) next to the rounded-up whole percent: split 16 = 6.25 %.
+  TimeShareParams q = timeshare_params(7, 40, 625);
+  CHECK_EQ(q.limit_bp, 625);
+  CHECK_EQ(timeshare_step(0, q, 1000000, 0), 62500);
+  CHECK_EQ(timeshare_step(0, timeshare_params(7), 1000000, 0), 70000);
+  CHECK_EQ(timeshare_params(0, 40, 625).limit_bp, 0);  // unlimited stays unlimited
   // Sampling periods: base while the node-wide reads fit the budget, then proportional.
   CHECK_EQ(sample_period_ns(1000000, 1, 32, 10000000), 1000000);
   CHECK_EQ(sample_period_ns(1000000, 5 * 5, 32, 10000000), 1000000);   // 5 processes: base

@@ -112,6 +112,16 @@ def test_temporal_limiter_closed_loop(fake, limit):
     assert abs(got - limit) <= 5.0, got
 
 
+def test_exact_share_drives_the_grants(fake):
+    """VGPU_DEVICE_CU_SHARE (the exact share the plugin sends with the node ledger) sets the
+    limiter's grants; the whole-percent VGPU_DEVICE_CU_LIMIT still decides that the vGPU
+    is limited (and its CU slice)."""
+    e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="40", VGPU_DEVICE_CU_SHARE_0="25", VGPU_CU_MODE="temporal")
+    out = run(e, "stream", "run=1000,3", timeout=120)
+    got = [o for o in out if "run" in o][0]["busy_frac"]
+    assert abs(got - 0.25) <= 0.05, got
+
+
 def test_graph_launches_are_limited(fake):
     e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="temporal")
     out = run(e, "stream", "graph=5000,3", timeout=120)

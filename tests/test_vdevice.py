@@ -98,3 +98,19 @@ def test_cu_share_rounds_up_so_shares_cover_the_gpu(split, pct):
     # spatial slices stay disjoint
     rngs = sorted(v.cu_range for v in vds)
     assert all(a[1] <= b[0] for a, b in zip(rngs, rngs[1:]))
+
+
+def test_exact_share_sent_only_with_the_ledger():
+    """A split-16 vGPU's CU limit is a whole percent rounded up (7); with the node ledger the
+    plugin also sends the exact share (6.25) for the limiter's grants."""
+    from amdvgpu.plugin.devices import FakeBackend
+    from amdvgpu.plugin.kubelet_stub import NodeHarness
+    b = FakeBackend(n=1)
+    u = b.devices()[0].uuid
+    for ledger, share in ((False, None), (True, "6.25")):
+        with NodeHarness(b, device_split_count=16, ledger=ledger) as node:
+            envs, _ = node.pod(node.vgpu_ids(u)[:1])
+        assert envs["VGPU_DEVICE_CU_LIMIT_0"] == "7" and envs.get("VGPU_DEVICE_CU_SHARE_0") == share
+    with NodeHarness(b, device_split_count=4, ledger=True) as node:   # 25 % is exact already
+        envs, _ = node.pod(node.vgpu_ids(u)[:1])
+    assert envs["VGPU_DEVICE_CU_LIMIT_0"] == "25" and "VGPU_DEVICE_CU_SHARE_0" not in envs
