@@ -88,6 +88,9 @@ def parse(argv=None):
     ap.add_argument("--time-budget", type=float, default=540.0,
                     help="wall seconds for the whole run: sweep points that would not finish in time are "
                          "skipped (and reported as such), so the line is always printed")
+    ap.add_argument("--ledger", action=argparse.BooleanOptionalAction, default=None,
+                    help="the plugin runs the node GPU-time ledger (exact charges and shares; default: the "
+                         "plugin's own default)")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     ap.add_argument("--rccl-probe", type=int, default=1, help="N>1: RCCL all-reduce between the pods afterwards")
     # worker-only
@@ -257,6 +260,11 @@ def worker_cmd(args, mode, result, port, dist=1, seconds=0.0, go=None):
     return cmd
 
 
+def ledger_kw(args):
+    """NodeHarness keyword for --ledger / --no-ledger (none: the plugin's default)."""
+    return {} if args.ledger is None else {"ledger": args.ledger}
+
+
 def pod_env(node, ids, extra=None):
     """(process env, contract envs) for a container holding vGPUs ``ids``."""
     from amdvgpu.shim.launcher import apply_contract
@@ -412,7 +420,7 @@ def _sweep_points(args, backend, uuid, tenants, end, extra):
             print(f"[bench] sweep {n} tenants skipped ({skipped[-1]['skipped']})", file=sys.stderr, flush=True)
             continue
         try:
-            with NodeHarness(backend, device_split_count=n, cu_mode=args.cu_mode) as node:
+            with NodeHarness(backend, device_split_count=n, cu_mode=args.cu_mode, **ledger_kw(args)) as node:
                 ids = node.vgpu_ids(uuid)[:n]
                 pods = [pod_env(node, [i], extra) for i in ids]
                 res = run_concurrent(args, [e for e, _ in pods], f"sweep{n}",
@@ -461,7 +469,7 @@ def node_point(args, backend, uuid, world, rank, port):
 
     t_point = now()
     try:
-        with NodeHarness(backend, device_split_count=args.split, cu_mode=args.cu_mode) as node:
+        with NodeHarness(backend, device_split_count=args.split, cu_mode=args.cu_mode, **ledger_kw(args)) as node:
             ids = node.vgpu_ids(uuid)[:args.split]
             envs = [pod_env(node, [i])[0] for i in ids]
             res = run_concurrent(args, envs, "node", deadline=T_START + args.time_budget - args.sweep_seconds - 15.0,
@@ -528,7 +536,7 @@ def main(argv=None):
         else:
             split, scaling, extra = {"vgpu": (args.split, 1.0, None), "quota": (args.split, 1.0, {
                 "VGPU_CU_POLICY": "disable"}), "parity": (2, 1.8, None)}[mode]
-            with NodeHarness(backend, device_split_count=split, device_memory_scaling=scaling,
+            with NodeHarness(backend, device_split_count=split, device_memory_scaling=scaling, **ledger_kw(args),
                              cu_mode=args.cu_mode) as node:
                 env, contracts[mode] = pod_env(node, node.vgpu_ids(uuid)[:1], extra)
                 applied[mode] = {k: env.get(k) for k in ("ROCR_VISIBLE_DEVICES", "VGPU_SHARED_CACHE", "VGPU_ALLOWLIST",
@@ -547,7 +555,7 @@ def main(argv=None):
         # xGMI bandwidth. Same ranks, same size: without the shim, then inside the pods.
         rccl = {"native": probe_rccl(args, native_env(uuid, cpu), port)}
         port += 1
-        with NodeHarness(backend, device_split_count=args.split, cu_mode=args.cu_mode) as node:
+        with NodeHarness(backend, device_split_count=args.split, cu_mode=args.cu_mode, **ledger_kw(args)) as node:
             env, _ = pod_env(node, node.vgpu_ids(uuid)[:1])
             rccl["vgpu"] = probe_rccl(args, env, port)
         port += 1
