@@ -604,7 +604,8 @@ def main(argv=None):
             "vgpu": {"split": args.split, "source": "Allocate response of the plugin (sysfs backend, stub kubelet)",
                      "envs": {k: v for k, v in sorted(c.items()) if k.startswith("VGPU_") and k != "VGPU_SHARED_CACHE"},
                      "quota_bytes": int(c.get("VGPU_DEVICE_MEMORY_LIMIT_0", "0").rstrip("m") or 0) << 20,
-                     "cu_limit_pct": cu_pct, "cu_mode": c.get("VGPU_CU_MODE")},
+                     "cu_limit_pct": cu_pct, "cu_mode": c.get("VGPU_CU_MODE"),
+                     "node_ledger": bool(args.ledger)},
         },
     }
     nat = results.get("native", {}).get("ms_per_step") if results.get("native") else None
