@@ -260,6 +260,11 @@ def worker_cmd(args, mode, result, port, dist=1, seconds=0.0, go=None):
     return cmd
 
 
+def plugin_default_ledger():
+    from amdvgpu.plugin.config import PluginConfig
+    return PluginConfig().ledger
+
+
 def ledger_kw(args):
     """NodeHarness keyword for --ledger / --no-ledger (none: the plugin's default)."""
     return {} if args.ledger is None else {"ledger": args.ledger}
@@ -605,7 +610,7 @@ def main(argv=None):
                      "envs": {k: v for k, v in sorted(c.items()) if k.startswith("VGPU_") and k != "VGPU_SHARED_CACHE"},
                      "quota_bytes": int(c.get("VGPU_DEVICE_MEMORY_LIMIT_0", "0").rstrip("m") or 0) << 20,
                      "cu_limit_pct": cu_pct, "cu_mode": c.get("VGPU_CU_MODE"),
-                     "node_ledger": bool(args.ledger)},
+                     "node_ledger": bool(args.ledger if args.ledger is not None else plugin_default_ledger())},
         },
     }
     nat = results.get("native", {}).get("ms_per_step") if results.get("native") else None
