@@ -8,7 +8,7 @@
 // own, unsynchronised snapshots. The reference samples NVML per container too
 // (utilization_watcher [multiprocess_utilization_watcher.c:195-216]).
 //
-// The ledger daemon (vgpu-ledger, started by the device plugin as root) reads each
+// The ledger daemon (vgpu-ledger, started by the device plugin as root with --ledger) reads each
 // process on a GPU once per period - n reads for n processes - and integrates, from one
 // consistent snapshot per period, each process's processor-sharing charge
 //     charged_ns += dt · occ(pid) / Σ occ          (trapezoid over the period)

@@ -1,6 +1,6 @@
 // vgpu-ledger: the node's GPU-time ledger daemon (see vgpu/ledger.h).
 //
-// Started by the device plugin (plugin/main.py) next to the board directory it creates.
+// Started by the device plugin with --ledger (plugin/main.py) next to the board directory.
 // Every period it reads KFD cu_occupancy once for each process on each GPU that a live
 // vGPU container has on the board, and integrates each process's processor-sharing
 // charge from that one snapshot into <board>/ledger.<gpu_id> (root-owned, 0644: the
