@@ -12,16 +12,62 @@
 //   vgpuctl <region> set-host-limit <size>  pinned host memory budget (0 = unlimited)
 //   vgpuctl <region> priority <n>
 //   vgpuctl <region> reclaim              free slots of exited processes
+//   vgpuctl ledger <board-dir>            the node GPU-time ledgers (vgpu/ledger.h), JSON
+#include <dirent.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 
+#include "vgpu/ledger.h"
+#include "vgpu/ratelimit.h"
 #include "vgpu/region_api.h"
+
+// Every <board>/ledger.<gpu_id>: sampling state and each process's charged GPU time.
+static int show_ledgers(const char* dir) {
+  DIR* d = opendir(dir);
+  if (!d) {
+    fprintf(stderr, "vgpuctl: cannot open %s\n", dir);
+    return 1;
+  }
+  printf("{\"ledgers\": [");
+  int n = 0;
+  const uint64_t now = vgpu::now_ns();
+  while (struct dirent* e = readdir(d)) {
+    if (strncmp(e->d_name, "ledger.", 7) != 0) continue;
+    char* end = nullptr;
+    const unsigned long id = strtoul(e->d_name + 7, &end, 10);
+    if (end == e->d_name + 7 || *end) continue;
+    vgpu::LedgerReader l;
+    if (!l.open(dir, (uint32_t)id)) continue;
+    const vgpu::LedgerFile* f = l.file();
+    const uint64_t hb = f->heartbeat_ns.load();
+    printf("%s\n  {\"gpu_id\": %lu, \"fresh\": %s, \"age_ms\": %.1f, \"samples\": %llu, \"reads\": %llu, "
+           "\"period_us\": %llu, \"total_occ\": %lld, \"procs\": [",
+           n++ ? "," : "", id, l.fresh(now) ? "true" : "false", hb && now > hb ? (now - hb) / 1e6 : 0.0,
+           (unsigned long long)f->samples.load(), (unsigned long long)f->reads.load(),
+           (unsigned long long)f->period_ns.load() / 1000, (long long)f->total_occ.load());
+    int m = 0;
+    const int k = f->n.load() < vgpu::kLedgerMaxPids ? f->n.load() : vgpu::kLedgerMaxPids;
+    for (int i = 0; i < k; i++) {
+      const int pid = f->e[i].pid.load();
+      if (pid <= 0) continue;
+      printf("%s{\"hostpid\": %d, \"occ\": %d, \"charged_ms\": %.3f}", m++ ? ", " : "", pid, f->e[i].occ.load(),
+             f->e[i].charged_ns.load() / 1e6);
+    }
+    printf("]}");
+  }
+  closedir(d);
+  printf("]}\n");
+  return 0;
+}
 
 static int usage() {
   fprintf(stderr,
           "usage: vgpuctl <region-file> show|suspend|resume|block|unblock|reclaim|"
-          "set-limit <dev> <size>|set-cu <dev> <pct>|set-host-limit <size>|priority <n>\n");
+          "set-limit <dev> <size>|set-cu <dev> <pct>|set-host-limit <size>|priority <n>\n"
+          "       vgpuctl ledger <board-dir>\n");
   return 2;
 }
 
@@ -66,6 +112,7 @@ static void show(vgpu_region* r) {
 
 int main(int argc, char** argv) {
   if (argc < 3) return usage();
+  if (!strcmp(argv[1], "ledger")) return show_ledgers(argv[2]);
   int err = 0;
   vgpu_region* r = vgpu_region_open(argv[1], 0, &err);
   if (!r) {

@@ -537,6 +537,9 @@ def test_ledger_processor_sharing_math(tmp_path):
     try:
         time.sleep(1.5)
         led = read_board(str(board))[777]
+        from amdvgpu.shim.native import VGPUCTL
+        ctl = json.loads(sp.run([lib_path(VGPUCTL), "ledger", str(board)], capture_output=True, text=True,
+                                check=True).stdout)
     finally:
         p.terminate()
         p.wait(timeout=10)
@@ -544,6 +547,9 @@ def test_ledger_processor_sharing_math(tmp_path):
     total = sum(c.values())
     assert led["total_occ"] == 40 and 1.0e9 < total < 1.6e9, (led["total_occ"], total)
     assert abs(c[4101] / total - 0.75) < 0.01 and abs(c[4102] / total - 0.25) < 0.01 and c[4103] == 0, c
+    (g,) = ctl["ledgers"]   # vgpuctl ledger: the same file for operators
+    assert g["gpu_id"] == 777 and g["fresh"] and g["total_occ"] == 40
+    assert {q["hostpid"] for q in g["procs"]} == {4101, 4102, 4103}
 
 
 def test_ledger_reader_and_monitor_metrics(fake, tmp_path):
