@@ -13,12 +13,30 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def free_port(span=16):
+    """A free MASTER_PORT whose next `span` ports are free too: bench.py puts its workers'
+    process groups (one per mode, the node point, the RCCL probes) on MASTER_PORT+1, +2, ..."""
+    for _ in range(200):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        if p + span >= 65536:
+            continue
+        ok = True
+        for q in range(p + 1, p + span + 1):
+            t = socket.socket()
+            try:
+                t.bind(("127.0.0.1", q))
+            except OSError:
+                ok = False
+            finally:
+                t.close()
+            if not ok:
+                break
+        if ok:
+            return p
+    raise RuntimeError("no free port range")
 
 
 @pytest.mark.slow
