@@ -217,11 +217,8 @@ class LSTMSentiment(nn.Module):
         super().__init__()
         self.lstm = nn.LSTM(features, hidden, batch_first=True)
         self.fc = nn.Linear(hidden, num_classes)
-        self.last = None  # inference: ops.fused.FusedLSTMLast (the last hidden state only)
 
     def forward(self, x):
-        if self.last is not None:
-            return self.fc(self.last(x))
         out, _ = self.lstm(x)
         return self.fc(out[:, -1])
 
@@ -278,11 +275,11 @@ class Runner:
     device (the reference's ai-benchmark also feeds a fixed random batch).
 
     Defaults are the product's tenant: stock PyTorch at fp32 (the reference's TF
-    precision). ``dtype=torch.bfloat16, fuse=True`` selects the optional gfx950 contrib
-    kernels (``ops/fused.py``, ``-m kernels`` tests).
+    precision). The tenant is always stock PyTorch-ROCm (MIOpen / hipBLASLt kernels), as
+    the reference's benchmark pods run stock TensorFlow.
     """
 
-    def __init__(self, case, device, dtype=torch.float32, batch=None, channels_last=True, seed=0, fuse=False):
+    def __init__(self, case, device, dtype=torch.float32, batch=None, channels_last=True, seed=0):
         self.case, self.device, self.dtype = case, torch.device(device), dtype
         self.batch = batch or case.batch
         g = torch.Generator(device="cpu").manual_seed(seed)
@@ -300,43 +297,12 @@ class Runner:
         self.y = y.to(self.device)
         if case.train:
             model.train()
-            if fuse and isinstance(model, LSTMSentiment) and dtype == torch.bfloat16 and self.device.type == "cuda":
-                # Forward and backward recurrences in whole-sequence HIP kernels
-                # (ops/fused.py::FusedLSTMTrainLast): graph-capturable, unlike MIOpen's RNN.
-                from ..ops.fused import FusedLSTMTrainLast
-                model.last = FusedLSTMTrainLast(model.lstm)
             self.opt = torch.optim.SGD(model.parameters(), lr=1e-3, momentum=0.9)
         else:
             model.eval()
-            if fuse and isinstance(model, LSTMSentiment) and dtype == torch.bfloat16 and self.device.type == "cuda":
-                # Whole-sequence recurrence in one HIP kernel (ops/fused.py::FusedLSTMLast).
-                from ..ops.fused import FusedLSTMLast
-                model.last = FusedLSTMLast(model.lstm)
-                model.fc.to(dtype)
-            elif fuse and isinstance(model, (ResNetV2, DeepLabV3Plus, VGG16)) and dtype == torch.bfloat16 \
-                    and channels_last:
-                # Inference epilogues fused into the producing conv or one HIP pass each
-                # (ops/fused.py); BN scale/shift and conv biases are taken in fp32 before
-                # the weights are cast.
-                from ..ops.fused import fuse_conv_bn_act, fuse_conv_relu, fuse_resnet_v2
-                impl = "hip" if self.device.type == "cuda" else "torch"
-                if isinstance(model, ResNetV2):
-                    model = fuse_resnet_v2(model, impl=impl)
-                elif isinstance(model, VGG16):
-                    model = fuse_conv_relu(model, impl=impl)
-                else:
-                    model = fuse_conv_bn_act(model, impl=impl)
-                for m in model.modules():
-                    if isinstance(m, (nn.Conv2d, nn.Linear, nn.BatchNorm2d)):
-                        m.to(dtype)
-            else:
-                model = model.to(dtype)
+            model = model.to(dtype)
             self.x = self.x.to(dtype)
             self.opt = None
-        self.fused = fuse and (not case.train or isinstance(model, LSTMSentiment)) and (
-            type(model).__name__ == "FusedResNetV2" or any(
-                type(m).__name__ in ("ConvBNAct", "ConvBiasAct", "FusedLSTMLast") or getattr(m, "fused", False) is True
-                for m in model.modules()))
         self.model = model
 
     def capture(self, warmup=3):
@@ -348,7 +314,7 @@ class Runner:
         autotuning and optimizer-state creation happen outside the capture."""
         if self.device.type != "cuda":
             raise ValueError("graph capture needs a GPU")
-        if self.case.train and self.case.kind == "sequence" and not self.fused:
+        if self.case.train and self.case.kind == "sequence":
             # Measured on MI355X (ROCm 7.2, PyTorch 2.10): capturing the MIOpen RNN
             # backward kills the process, so recurrent training always runs eagerly.
             raise NotImplementedError("MIOpen RNN training is not HIP-graph capturable")

@@ -53,7 +53,9 @@ CONTAINER_LOCK_DIR = "/usr/local/vgpu/lock"
 # time to busy containers of higher priority.
 BOARD_HOST_DIR = "board"
 CONTAINER_BOARD_DIR = "/usr/local/vgpu/board"
-BOARD_MAX_AGE_S = 7 * 24 * 3600
+# A publishing container touches its slot's mtime every 10 s (board.h kBoardTouchS), so a
+# slot untouched for an hour belongs to a container with no GPU process for that long.
+BOARD_MAX_AGE_S = 3600
 
 
 def ensure_board_dir(vgpu_dir):
@@ -65,7 +67,9 @@ def ensure_board_dir(vgpu_dir):
 def board_slot(vgpu_dir, name):
     """Creates this container's slot file (world-writable: the container's processes may
     run as any user; only this container mounts it read-write). Returns its path, or None
-    when there is no board directory. Slots untouched for a week are removed."""
+    when there is no board directory. Slots untouched for an hour are removed: their
+    containers have had no GPU process for that long (a live one touches its slot every
+    10 s), and every reader otherwise keeps stat-ing them."""
     d = os.path.join(vgpu_dir, BOARD_HOST_DIR)
     if not os.path.isdir(d):
         return None

@@ -75,7 +75,6 @@ def parse(argv=None):
     ap.add_argument("--split", type=int, default=4, help="vGPUs per GPU of the headline pod (BASELINE config 2)")
     ap.add_argument("--cu-mode", default="auto", choices=["auto", "spatial", "temporal", "both", "off"])
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--fuse", action="store_true", help="round-1 hand-written bf16 kernels (not the stock workload)")
     ap.add_argument("--sweep", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--sweep-tenants", default="1,2,4,8,12")
     ap.add_argument("--sweep-seconds", type=float, default=6.0)
@@ -143,10 +142,10 @@ def worker(args):
     case = get_case(args.case)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     if cpu:
-        runner = Runner(case, device, dtype=torch.float32, batch=2, channels_last=False, fuse=False)
+        runner = Runner(case, device, dtype=torch.float32, batch=2, channels_last=False)
         runner.x = runner.x[..., :64, :64].contiguous() if runner.x.dim() == 4 else runner.x[:, :16].contiguous()
     else:
-        runner = Runner(case, device, dtype=dtype, fuse=args.fuse)
+        runner = Runner(case, device, dtype=dtype)
     for _ in range(args.warmup):
         runner.step()
     sync()
@@ -251,8 +250,6 @@ def worker_cmd(args, mode, result, port, dist=1, seconds=0.0, go=None):
     cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--mode", mode, "--result-file", result,
            "--port", str(port), "--dist", str(dist), "--case", args.case, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--dtype", args.dtype]
-    if args.fuse:
-        cmd.append("--fuse")
     if args.cpu_rehearsal:
         cmd.append("--cpu-rehearsal")
     if go:
@@ -603,9 +600,7 @@ def main(argv=None):
             "global_batch": case.batch * world, "per_gpu_batch": case.batch,
             "input_shape": list(case.input_shape), "seq_len": None,
             "parallelism": f"dp{world} (one independent split-{args.split} vGPU pod per GPU)",
-            "workload": "stock PyTorch-ROCm (MIOpen/hipBLASLt), no custom kernels" if not args.fuse else
-                        "round-1 fused bf16 HIP kernels",
-            "fused_epilogues": bool(args.fuse),
+            "workload": "stock PyTorch-ROCm (MIOpen/hipBLASLt), no custom kernels",
             "vgpu": {"split": args.split, "source": "Allocate response of the plugin (sysfs backend, stub kubelet)",
                      "envs": {k: v for k, v in sorted(c.items()) if k.startswith("VGPU_") and k != "VGPU_SHARED_CACHE"},
                      "quota_bytes": int(c.get("VGPU_DEVICE_MEMORY_LIMIT_0", "0").rstrip("m") or 0) << 20,

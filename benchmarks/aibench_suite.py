@@ -75,7 +75,7 @@ def worker(cases, steps, warmup, out, seconds=0.0, sync_dir=None, tag="0", peers
     res = {}
     for name in cases:
         case = get_case(name)
-        r = Runner(case, "cuda:0", dtype=torch.float32, fuse=False)
+        r = Runner(case, "cuda:0", dtype=torch.float32)
         for _ in range(warmup):
             r.step()
         torch.cuda.synchronize()

@@ -7,8 +7,8 @@ Runs one workload as a "container" under a vGPU contract (or natively) so that
 
 * ``spin``    single-wave workgroups, 8 per CU of the whole chip, each spinning a fixed
               time: a kernel that would keep every CU busy if it could reach them.
-* ``resnet``  ResNet-V2-50 inference (ai-benchmark 1.1 shape, bf16, fused epilogues), a
-              real workload: its conv/epilogue kernels size their grids for the whole GPU.
+* ``resnet``  ResNet-V2-50 inference (ai-benchmark 1.1 shape, stock fp32 PyTorch), a real
+              workload: its MIOpen / hipBLASLt kernels size their grids for the whole GPU.
 
 The parent never touches the GPU; it starts the worker with the contract applied
 (``shim/launcher.py``), so under ``rocprofv3 -- python3 benchmarks/cu_occupancy.py ...``

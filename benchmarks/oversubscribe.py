@@ -44,7 +44,7 @@ def worker(case, dataset_gib, steps, warmup, out):
         chunks.append(torch.empty(GiB // 4, dtype=torch.float32, device="cuda").normal_())
     torch.cuda.synchronize()
     fill_s = time.perf_counter() - t0
-    r = Runner(get_case(case), "cuda:0", dtype=torch.float32, fuse=False)
+    r = Runner(get_case(case), "cuda:0", dtype=torch.float32)
     per = r.x.numel()
     per_chunk = (GiB // 4) // per
 

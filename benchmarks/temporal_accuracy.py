@@ -33,7 +33,7 @@ def worker(workload, seconds, sync_every, out, go, batch=0):
     if workload == "resnet50":
         from amdvgpu.models.aibench import Runner, get_case
         torch.backends.cudnn.benchmark = True
-        r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False, batch=batch or None)
+        r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, batch=batch or None)
         step, items = r.step, r.batch
     else:
         from amdvgpu.ops import spin
@@ -44,6 +44,7 @@ def worker(workload, seconds, sync_every, out, go, batch=0):
     open(out + ".ready", "w").close()
     while go and not os.path.exists(go):
         time.sleep(0.002)
+    stats0 = _region_stats()
     n = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -53,19 +54,45 @@ def worker(workload, seconds, sync_every, out, go, batch=0):
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    json.dump({"steps": n, "seconds": dt, "throughput": n * items / dt}, open(out, "w"))
+    res = {"steps": n, "seconds": dt, "throughput": n * items / dt}
+    stats1 = _region_stats()
+    if stats0 and stats1:
+        # The container's charged share of the GPU's time over the run, and the time its
+        # launches spent blocked at the GPU-time gate (this process's slot).
+        res["charged_pct"] = 100.0 * (stats1["charged_ns"] - stats0["charged_ns"]) / max(
+            1, stats1["wall_ns"] - stats0["wall_ns"])
+        res["throttle_pct"] = 100.0 * (stats1["throttle_ns"] - stats0["throttle_ns"]) / (dt * 1e9)
+    json.dump(res, open(out, "w"))
 
 
-def run_tenants(workload, contracts, seconds, sync_every, batch=0):
+def _region_stats():
+    """charged_ns / wall_ns of device 0 and this process's throttle_ns, from the region of
+    the container the worker runs in (None outside a vGPU or with a foreign layout)."""
+    path = os.environ.get("VGPU_SHARED_CACHE")
+    if not path:
+        return None
+    try:
+        from amdvgpu.shim.region import Region
+        with Region(path) as r:
+            d = r.device(0)
+            mine = [p for p in r.procs() if p["pid"] == os.getpid()]
+            return {"charged_ns": d["charged_ns"], "wall_ns": d["wall_ns"],
+                    "throttle_ns": mine[0]["throttle_ns"] if mine else 0}
+    except Exception:
+        return None
+
+
+def run_tenants(workload, contracts, seconds, sync_every, batch=0, shim=None, full=False):
     """Starts len(contracts) tenants (None = native), releases them together, returns
-    each one's throughput."""
+    each one's throughput (with ``full``, each one's result: throughput and, in a vGPU,
+    charged_pct / throttle_pct). ``shim`` preloads another build of the shim (A/B runs)."""
     from amdvgpu.shim.launcher import apply_contract, cleanup_region
     tmp = tempfile.mkdtemp(prefix="tacc-")
     go = os.path.join(tmp, "go")
     procs, outs = [], []
     for i, c in enumerate(contracts):
         out = os.path.join(tmp, f"t{i}.json")
-        env = apply_contract(c) if c else dict(os.environ)
+        env = apply_contract(c, shim=shim) if c else dict(os.environ)
         cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--workload", workload, "--seconds",
                str(seconds), "--sync-every", str(sync_every), "--out", out, "--go", go, "--batch", str(batch)]
         procs.append(subprocess.Popen(cmd, env=env))
@@ -80,7 +107,8 @@ def run_tenants(workload, contracts, seconds, sync_every, batch=0):
         for p in procs:
             if p.wait(timeout=600) != 0:
                 raise SystemExit("a tenant failed")
-        return [json.load(open(o))["throughput"] for o in outs]
+        res = [json.load(open(o)) for o in outs]
+        return res if full else [r["throughput"] for r in res]
     finally:
         for p in procs:
             if p.poll() is None:

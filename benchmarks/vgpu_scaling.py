@@ -35,7 +35,7 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
     from amdvgpu.models.aibench import Runner, get_case
     torch.backends.cudnn.benchmark = True  # MIOpen find mode
     case = get_case(case_name)
-    r = Runner(case, "cuda:0", dtype=torch.float32, fuse=False)
+    r = Runner(case, "cuda:0", dtype=torch.float32)
     for _ in range(warmup):
         r.step()
     torch.cuda.synchronize()

@@ -50,6 +50,11 @@ struct alignas(64) BoardSlot {
 
 // Slot staleness: a slot whose heartbeat is older than this is ignored.
 constexpr uint64_t kBoardStaleNs = 2'000'000'000ull;
+// A publishing container touches its slot file's mtime every kBoardTouchS; readers skip,
+// without opening them, slots untouched for kBoardSkipAgeS (the plugin removes slots
+// untouched for an hour: contract.py BOARD_MAX_AGE_S).
+constexpr int64_t kBoardTouchS = 10;
+constexpr int64_t kBoardSkipAgeS = 60;
 
 // Another container as read from its slot.
 struct BoardPeer {
@@ -111,6 +116,7 @@ class Board {
   std::string dir_, self_name_;
   BoardSlot* self_ = nullptr;
   int fd_ = -1;
+  int64_t touched_s_ = 0;  // CLOCK_REALTIME seconds of the last mtime touch
   std::vector<BoardPeer> peers_;
 };
 

@@ -31,8 +31,10 @@ namespace vgpu {
 constexpr uint32_t kLedgerMagic = 0x56474c31u;  // "VGL1"
 constexpr uint32_t kLedgerVersion = 1;
 constexpr int kLedgerMaxPids = 1024;
-// A ledger whose heartbeat is older than this is ignored (containers sample by themselves).
+// A ledger whose heartbeat is older than max(kLedgerStaleNs, kLedgerStalePeriods x its own
+// sampling period) is ignored (containers sample by themselves).
 constexpr uint64_t kLedgerStaleNs = 50'000'000ull;
+constexpr uint64_t kLedgerStalePeriods = 4;
 
 struct alignas(32) LedgerEntry {
   std::atomic<int32_t> pid;          // host PID, 0 = free entry

@@ -5,6 +5,9 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -13,6 +16,25 @@
 #include "vgpu/log.h"
 
 namespace vgpu {
+
+namespace {
+
+// Modification time of `path` in seconds (CLOCK_REALTIME), -1 if unknown. By system call:
+// stat/fstat are GLIBC_2.33 symbols, which the preloaded shim must not need (glibc_compat.h);
+// on x86-64 the kernel's struct stat is glibc's.
+int64_t file_mtime(const char* path) {
+  struct stat st;
+  if (syscall(SYS_newfstatat, AT_FDCWD, path, &st, 0) != 0) return -1;
+  return (int64_t)st.st_mtim.tv_sec;
+}
+
+int64_t wall_seconds() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return (int64_t)ts.tv_sec;
+}
+
+}  // namespace
 
 Board::~Board() {
   if (self_) munmap(self_, sizeof(BoardSlot));
@@ -72,6 +94,11 @@ void Board::publish(int priority, const uint32_t* gpu_ids, int ndev, const std::
   for (int i = 0; i < n; i++) self_->hostpids[i].store(hostpids[i], std::memory_order_relaxed);
   self_->npids.store(n, std::memory_order_release);
   self_->heartbeat_ns.store(now, std::memory_order_release);
+  // Writes through the mapping need not touch the file's mtime (tmpfs never does): it is
+  // touched explicitly, so readers - and the plugin's clean-up of departed containers'
+  // slots - can tell a live slot from a dead one without reading it.
+  const int64_t wall = wall_seconds();
+  if (wall - touched_s_ >= kBoardTouchS && futimens(fd_, nullptr) == 0) touched_s_ = wall;
 }
 
 void Board::leave() {
@@ -109,10 +136,16 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
   if (dir_.empty()) return peers_;
   DIR* d = opendir(dir_.c_str());
   if (!d) return peers_;
+  const int64_t wall = wall_seconds();
   while (struct dirent* e = readdir(d)) {
     const size_t len = strlen(e->d_name);
     if (len < 6 || strcmp(e->d_name + len - 5, ".slot") != 0 || self_name_ == e->d_name) continue;
     const std::string path = dir_ + "/" + e->d_name;
+    // A slot nobody has touched for a while belongs to a container without a live GPU
+    // process (or one long gone): skipped without opening it, so departed containers'
+    // slots cost one stat each until the plugin removes them.
+    const int64_t mt = file_mtime(path.c_str());
+    if (mt >= 0 && wall - mt > kBoardSkipAgeS) continue;
     int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
     if (fd < 0) continue;
     BoardSlot s;

@@ -47,7 +47,11 @@ bool LedgerReader::open(const std::string& dir, uint32_t gpu_id) {
 bool LedgerReader::fresh(uint64_t now) const {
   if (!f_) return false;
   const uint64_t hb = f_->heartbeat_ns.load(std::memory_order_acquire);
-  return hb && hb <= now + kLedgerStaleNs && now - hb <= kLedgerStaleNs;
+  // A few of the daemon's own periods (it reads every GPU of the node in turn, so its
+  // period stretches with the processes on the node), never less than kLedgerStaleNs.
+  const uint64_t period = f_->period_ns.load(std::memory_order_relaxed);
+  const uint64_t stale = period < kLedgerStaleNs / kLedgerStalePeriods ? kLedgerStaleNs : period * kLedgerStalePeriods;
+  return hb && hb <= now + stale && now - hb <= stale;
 }
 
 const LedgerEntry* LedgerReader::find(int pid) const {

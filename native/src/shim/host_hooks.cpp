@@ -129,16 +129,22 @@ hipError_t hipHostFree(void* ptr) {
   VGPU_REAL_AS(hipHostFree, FreeFn, "libamdhip64", nullptr);
   if (!real_hipHostFree) return hipErrorNotSupported;
   gate_suspend();
-  release_host(ptr);
-  return real_hipHostFree(ptr);
+  // Released only once the runtime has let go of the memory: a failed free leaves it
+  // pinned, and so charged (as hipHostUnregister below).
+  hipError_t e = real_hipHostFree(ptr);
+  if (e == hipSuccess) release_host(ptr);
+  return e;
 }
 
 hipError_t hipFreeHost(void* ptr) {
   VGPU_REAL_AS(hipFreeHost, FreeFn, "libamdhip64", nullptr);
   if (!real_hipFreeHost) return hipErrorNotSupported;
   gate_suspend();
-  release_host(ptr);
-  return real_hipFreeHost(ptr);
+  // Released only once the runtime has let go of the memory: a failed free leaves it
+  // pinned, and so charged (as hipHostUnregister below).
+  hipError_t e = real_hipFreeHost(ptr);
+  if (e == hipSuccess) release_host(ptr);
+  return e;
 }
 
 hipError_t hipHostRegister(void* host_ptr, size_t size, unsigned int flags) {

@@ -384,7 +384,7 @@ void shim_init_after_hsa() {
       CuMask m = cu_mask_for(a.cu_count, a.num_xcc, d.cu_limit_pct, d.cu_range_begin, d.cu_range_end, d.num_se);
       memcpy(d.cu_mask, m.words, sizeof(d.cu_mask));
       d.cu_mask_bits = m.nbits;
-      d.credit_ns.store(timeshare_params(d.cu_limit_pct, config().limiter_window_ms).burst_ns);
+      d.credit_ns.store(timeshare_params(d.cu_limit_pct, config().limiter_window_ms, d.cu_share_bp).burst_ns);
       d.gate_open.store(1);
       d.configured = 1;
     }
@@ -502,7 +502,7 @@ void apply_live_config() {
     const bool mask_eff = mask_on || reserved_on;
     const bool mask_changed = mask_eff != a.mask_active.load() || memcmp(m.words, a.mask.words, sizeof(m.words)) != 0;
     if (temp_on && !a.temporal_active.load() && !d.gate_open.load()) {
-      d.credit_ns.store(timeshare_params(pct, cfg.limiter_window_ms).burst_ns);
+      d.credit_ns.store(timeshare_params(pct, cfg.limiter_window_ms, d.cu_share_bp).burst_ns);
       d.gate_open.store(1);
     }
     a.mask = m;

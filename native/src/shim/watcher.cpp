@@ -348,8 +348,12 @@ void sample_tick(Region* r, Sampler& sm) {
     const int64_t charge = led_charge >= 0 ? led_charge : timeshare_interval(dt, sm.prev_pm[d], pm, sm.opened[d]);
     const bool was_closed = !ds.gate_open.load(std::memory_order_relaxed);
     if (yield) sm.yielded_ns[d] += dt;
-    timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, config().limiter_window_ms, ds.cu_share_bp), dt, charge,
-                    yield ? 0 : dt);
+    // The exact share (e.g. 6.25 % for split 16) only with the ledger's exact charges: the
+    // container's own sampling over-charges on a crowded GPU (its charges add up to ~107 %
+    // of the wall time at 16 pods), so it keeps the rounded-up whole percent, which leaves
+    // room for that (the plugin emits the percent rounded up for this reason).
+    timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, config().limiter_window_ms, led ? ds.cu_share_bp : 0), dt,
+                    charge, yield ? 0 : dt);
     if (conc > 0) {
       // Concurrency admission, round robin: while its credit allows, a container holds
       // the GPU for a slice, then yields to the longest-waiting peer; at most `conc`

@@ -22,6 +22,7 @@
 #include "vgpu/cumask.h"
 #include "vgpu/devmap.h"
 #include "vgpu/kfd.h"
+#include "vgpu/ledger.h"
 #include "vgpu/ratelimit.h"
 #include "vgpu/region.h"
 
@@ -977,6 +978,18 @@ static void test_board() {
   CHECK_EQ(a.priority_of(5151, 1001), kPrioBackground);
   CHECK_EQ(a.priority_of(5151, 1000), kPrioNormal);  // not on that GPU: unknown = normal
   CHECK_EQ(a.priority_of(9999, 1001), kPrioNormal);  // on no slot
+  // A slot file untouched for longer than kBoardSkipAgeS is skipped unread (its container
+  // has no live publisher), whatever its heartbeat says; publishing touches it again.
+  {
+    const std::string bpath = std::string(dir) + "/b.slot";
+    struct timespec old[2] = {{time(nullptr) - kBoardSkipAgeS - 5, 0}, {time(nullptr) - kBoardSkipAgeS - 5, 0}};
+    CHECK_EQ(utimensat(AT_FDCWD, bpath.c_str(), old, 0), 0);
+    CHECK_EQ(a.refresh(now).size(), 0u);
+    Board b2;
+    CHECK_EQ(b2.open(dir, "b.slot"), 0);
+    b2.publish(kPrioBackground, gpus_b, 1, {5151}, now);
+    CHECK_EQ(a.refresh(now).size(), 1u);
+  }
   // A stale heartbeat (the container is gone) or a departed slot is ignored.
   CHECK_EQ(a.refresh(now + kBoardStaleNs + 1).size(), 0u);
   b.leave();
@@ -987,6 +1000,40 @@ static void test_board() {
   fputs("not a slot", f);
   fclose(f);
   CHECK_EQ(a.refresh(now).size(), 0u);
+  CHECK(system((std::string("rm -rf ") + dir).c_str()) == 0);
+}
+
+static void test_ledger_fresh() {
+  char dir[] = "/tmp/vgpu_ledger_XXXXXX";
+  CHECK(mkdtemp(dir) != nullptr);
+  const uint32_t gid = 4242;
+  LedgerFile* lf = new LedgerFile();
+  memset(static_cast<void*>(lf), 0, sizeof(LedgerFile));
+  lf->magic = kLedgerMagic;
+  lf->version = kLedgerVersion;
+  lf->gpu_id = gid;
+  const uint64_t now = now_ns();
+  lf->heartbeat_ns.store(now);
+  lf->period_ns.store(1'000'000);
+  std::string path = ledger_path(dir, gid);
+  FILE* f = fopen(path.c_str(), "w");
+  CHECK(f != nullptr);
+  CHECK_EQ(fwrite(lf, sizeof(LedgerFile), 1, f), 1u);
+  fclose(f);
+  LedgerReader r;
+  CHECK(r.open(dir, gid));
+  CHECK(r.fresh(now + 10'000'000));
+  CHECK(!r.fresh(now + kLedgerStaleNs + 1));       // short period: the fixed floor applies
+  // A daemon whose period stretched (every GPU of a busy node read in turn): stale only after
+  // a few of its own periods, not after the fixed 50 ms.
+  int fd = open(path.c_str(), O_WRONLY);
+  CHECK(fd >= 0);
+  const uint64_t period = 40'000'000;
+  CHECK_EQ(pwrite(fd, &period, sizeof(period), offsetof(LedgerFile, period_ns)), (ssize_t)sizeof(period));
+  close(fd);
+  CHECK(r.fresh(now + 100'000'000));
+  CHECK(!r.fresh(now + kLedgerStalePeriods * period + 1));
+  delete lf;
   CHECK(system((std::string("rm -rf ") + dir).c_str()) == 0);
 }
 
@@ -1047,6 +1094,7 @@ int main(int argc, char** argv) {
       {"kfd", test_kfd},
       {"hostpid_resolution", test_hostpid_resolution},
       {"board", test_board},
+      {"ledger_fresh", test_ledger_fresh},
   };
   if (argc > 1 && !strcmp(argv[1], "--list")) {
     for (auto& t : tests) printf("%s\n", t.first);

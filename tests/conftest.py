@@ -15,24 +15,6 @@ if REPO not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the gpurun box)")
     config.addinivalue_line("markers", "slow: takes more than a few seconds")
-    config.addinivalue_line("markers", "kernels: optional gfx950 contrib kernels of the benchmark workloads "
-                            "(need a GPU; not part of the product's -m gpu tier, run with -m kernels)")
-
-
-def pytest_collection_modifyitems(config, items):
-    """`kernels` tests need a GPU but are not in the `gpu` tier: skip them without one."""
-    kern = [i for i in items if i.get_closest_marker("kernels")]
-    if not kern:
-        return
-    try:
-        import torch
-        have_gpu = torch.cuda.is_available()
-    except Exception:
-        have_gpu = False
-    if not have_gpu:
-        skip = pytest.mark.skip(reason="kernels tier needs a GPU")
-        for i in kern:
-            i.add_marker(skip)
 
 
 def native_built():

@@ -195,26 +195,6 @@ def test_legacy_allocate_refuses_without_checkpoint(tmp_path):
         srv.Allocate(_alloc_req([ids[0]]), None)
 
 
-def test_fused_lstm_routes_oversize_inputs_to_the_library():
-    """inputs beyond the kernels' buffer-descriptor range take nn.LSTM."""
-    import torch
-    from amdvgpu.ops.fused import (LSTM_INFER_MAX_BT, LSTM_TRAIN_MAX_BT, FusedLSTMLast, FusedLSTMTrainLast,
-                                   lstm_fits)
-    assert LSTM_TRAIN_MAX_BT == 1 << 20 and LSTM_INFER_MAX_BT == 1 << 21
-    assert lstm_fits(torch.empty(1023, 1024, 1), LSTM_TRAIN_MAX_BT)
-    assert not lstm_fits(torch.empty(1024, 1024, 1), LSTM_TRAIN_MAX_BT)
-    lstm = torch.nn.LSTM(8, 128, batch_first=True)
-    x = torch.randn(2, 5, 8)
-    ref = lstm(x)[0][:, -1]
-    assert torch.allclose(FusedLSTMTrainLast(lstm)(x), ref)      # CPU tensors: library path
-    f = FusedLSTMLast(lstm)
-    assert torch.allclose(f(x), ref)
-    with torch.no_grad():                                         # live weights are tracked
-        lstm.weight_ih_l0.mul_(2)
-    f._refresh()
-    assert torch.allclose(f.w_ih_perm.view(128, 4, 8).permute(1, 0, 2).reshape(512, 8), lstm.weight_ih_l0)
-
-
 def test_legacy_allocate_concurrent_calls_never_share_a_vgpu(tmp_path):
     """Allocate runs on the gRPC thread pool: concurrent legacy-mode calls must each get
     their own vGPUs (the read-available / acquire sequence is serialised)."""
@@ -364,3 +344,20 @@ def test_board_slot_mounts(tmp_path):
     # the container-side order matters: the directory is mounted before the file on top
     paths = [m.container_path for m in r1.mounts]
     assert paths.index("/usr/local/vgpu/board") < paths.index(f"/usr/local/vgpu/board/{slots[0]}")
+
+
+def test_departed_board_slots_are_removed(tmp_path):
+    """A slot untouched for an hour (its container has had no publishing GPU process for
+    that long: a live one touches its slot every 10 s) is removed at the next Allocate;
+    younger ones stay."""
+    import time
+    from amdvgpu.plugin.contract import BOARD_MAX_AGE_S, board_slot, ensure_board_dir
+    board = ensure_board_dir(str(tmp_path / "vgpu"))
+    old, young = os.path.join(board, "old.slot"), os.path.join(board, "young.slot")
+    for p in (old, young):
+        open(p, "w").close()
+    t = time.time() - BOARD_MAX_AGE_S - 60
+    os.utime(old, (t, t))
+    assert BOARD_MAX_AGE_S <= 3600
+    new = board_slot(str(tmp_path / "vgpu"), "new")
+    assert os.path.exists(new) and os.path.exists(young) and not os.path.exists(old)

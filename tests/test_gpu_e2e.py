@@ -69,7 +69,7 @@ import torch
 from amdvgpu.models.aibench import Runner, get_case
 from amdvgpu.ops import cu_census
 free, total = torch.cuda.mem_get_info(0)
-r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False)
+r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32)
 for _ in range(3): r.step()
 torch.cuda.synchronize()
 t0 = time.time()

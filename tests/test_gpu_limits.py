@@ -51,17 +51,20 @@ RESNET_RATE = """
 import torch
 from amdvgpu.models.aibench import Runner, get_case
 torch.backends.cudnn.benchmark = True
-r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False, batch={batch})
+r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, batch={batch})
 for _ in range(5): r.step()
 torch.cuda.synchronize()
 open(os.environ["VGPU_TEST_READY"], "w").close()
 while not os.path.exists(os.environ["VGPU_TEST_GO"]):
     time.sleep(0.002)
 reg = None
+def mine():
+    return sum(p["throttle_ns"] for p in reg.procs() if p["pid"] == os.getpid())
 if os.environ.get("VGPU_SHARED_CACHE"):
     from amdvgpu.shim.region import Region
     reg = Region(os.environ["VGPU_SHARED_CACHE"])
     d0 = reg.device(0)
+    th0 = mine()
 n = 0
 t0 = time.perf_counter()
 while time.perf_counter() - t0 < {secs}:
@@ -70,12 +73,14 @@ while time.perf_counter() - t0 < {secs}:
     if n % 8 == 0:
         torch.cuda.synchronize()
 torch.cuda.synchronize()
-rate = n / (time.perf_counter() - t0)
-busy = None
+el = time.perf_counter() - t0
+rate = n / el
+busy = throttle = None
 if reg is not None:
     d1 = reg.device(0)
     busy = (d1["charged_ns"] - d0["charged_ns"]) / max(1, d1["wall_ns"] - d0["wall_ns"])
-emit(rate=rate, busy=busy)
+    throttle = (mine() - th0) / (el * 1e9)
+emit(rate=rate, busy=busy, throttle=throttle)
 """
 
 
@@ -183,30 +188,46 @@ def test_temporal_accuracy_two_tenants_stock_resnet(tmp_path):
 
 def test_temporal_four_light_tenants(tmp_path):
     """Small-batch inference (ResNet-50 b=4, launch-bound: the GPU idles between kernels)
-    at 25 %, four tenants at once: each gets within 5 points of what one such tenant gets
-    alone at 25 % (co-running light tenants neither steal from each other nor are
-    over-charged), and none is charged more than its share of the GPU's time. Alone, the
-    tenant uses its whole 25 %; together the four share the GPU's instants, so each is
-    charged less (18-23 % in profiles/r3i) for about the same progress."""
-    for d in ("n", "s", "t"):
+    at 25 %, four tenants at once, judged against what the hardware and the host give four
+    such tenants without any compute limit (`unlimited x4`, measured in the same window).
+
+    Alone, the tenant is charged its 25 % of the GPU's time, which buys it ~33-35 % of its
+    native throughput (it keeps the GPU only ~75 % busy by itself). Four at once share the
+    GPU's instants and the host: unlimited, the four together reach only ~120-130 % of one
+    native tenant (profiles/r4a), so each can get at most a quarter of that whatever the
+    limiter does. The bar is therefore physical:
+      * alone: charged 25 +- 5 % of the GPU's time;
+      * together: nobody is charged more than 25 + 3 %;
+      * each gets >= min(alone, unlimited-together / 4) - 5 points;
+      * the four together get >= 0.9 x min(4 x alone, unlimited-together).
+    Each tenant's throttle time (launches blocked at the gate) is printed: near zero
+    together means the limiter was not what held the tenants back."""
+    for d in ("n", "u", "s", "t"):
         (tmp_path / d).mkdir()
     native = _resnet_rates([None], tmp_path / "n", batch=4)[0]
+    free = [vgpu_env(mem_limit=32 * GiB) for _ in range(4)]
     solo = vgpu_env(cu_limit=25, cu_mode="temporal", mem_limit=32 * GiB)
     cs = [vgpu_env(cu_limit=25, cu_mode="temporal", mem_limit=32 * GiB) for _ in range(4)]
     try:
+        unlimited = _resnet_rates(free, tmp_path / "u", secs=6.0, batch=4)
         one = _resnet_rates([solo], tmp_path / "s", secs=6.0, batch=4, full=True)[0]
         four = _resnet_rates(cs, tmp_path / "t", secs=6.0, batch=4, full=True)
     finally:
-        for c in [solo] + cs:
+        for c in free + [solo] + cs:
             cleanup_region(c)
     alone = 100.0 * one["rate"] / native
+    ceiling = 100.0 * sum(unlimited) / native          # four unlimited tenants together
     together = [100.0 * r["rate"] / native for r in four]
     busy = [100.0 * r["busy"] for r in four]
-    print(json.dumps({"native": native, "alone_pct": alone, "together_pct": together, "busy_pct": busy,
-                      "alone_busy_pct": 100.0 * one["busy"]}))
+    throttle = [100.0 * r["throttle"] for r in four]
+    print(json.dumps({"native": native, "alone_pct": alone, "unlimited_together_pct": ceiling,
+                      "together_pct": together, "busy_pct": busy, "throttle_pct": throttle,
+                      "alone_busy_pct": 100.0 * one["busy"], "alone_throttle_pct": 100.0 * one["throttle"]}))
     assert abs(100.0 * one["busy"] - 25.0) <= 5.0, one
     assert all(b <= 25.0 + 3.0 for b in busy), busy
-    assert all(abs(t - alone) <= 5.0 for t in together), (alone, together)
+    floor = min(alone, ceiling / 4) - 5.0
+    assert all(t >= floor for t in together), (floor, together, alone, ceiling)
+    assert sum(together) >= 0.9 * min(4 * alone, ceiling), (sum(together), alone, ceiling)
 
 
 LATENCY_SPIN = """

@@ -18,8 +18,6 @@ import re
 
 FAMILIES = [
     ("spin (vgpu_spin, 8 WG/CU)", r"spin_kernel"),
-    ("fused BN+ReLU epilogue", r"bn_act_kernel"),
-    ("fused 1x1 conv (MFMA)", r"conv1x1"),
     ("CK / MIOpen convolution", r"conv_fwd|igemm|naive_conv|grouped_conv"),
     ("other", r"."),
 ]

@@ -29,7 +29,7 @@ def tenant(steps, warmup, sync_every, marks):
     import torch
     from amdvgpu.models.aibench import Runner, get_case
     torch.backends.cudnn.benchmark = True
-    r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False)
+    r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32)
     for _ in range(warmup):
         r.step()
     torch.cuda.synchronize()

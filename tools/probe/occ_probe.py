@@ -29,7 +29,7 @@ x = torch.zeros(1, device="cuda"); torch.cuda.synchronize()
 if kind == "resnet":
     from amdvgpu.models.aibench import Runner, get_case
     torch.backends.cudnn.benchmark = True
-    r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32, fuse=False)
+    r = Runner(get_case("resnet50-inf"), "cuda:0", dtype=torch.float32)
     for _ in range(5): r.step()
     torch.cuda.synchronize()
 print("READY", flush=True)

@@ -30,7 +30,7 @@ def tenant(steps, case, autotune):
     import torch
     from amdvgpu.models.aibench import Runner, get_case
     torch.backends.cudnn.benchmark = bool(autotune)
-    r = Runner(get_case(case), "cuda:0", dtype=torch.float32, fuse=False)
+    r = Runner(get_case(case), "cuda:0", dtype=torch.float32)
     for _ in range(5):
         r.step()
     torch.cuda.synchronize()
