@@ -7,7 +7,9 @@
 // glibc (Ubuntu 20.04: 2.31, RHEL 8: 2.28) do not have. Every glibc since then still
 // exports the original versions, so the references are pinned to them here, and the shim
 // links libdl / libpthread explicitly for the older images that keep the functions there.
-// stat/fstat (GLIBC_2.33) are not used at all (access / lseek instead). The reference's
+// stat/fstat (GLIBC_2.33) are not used at all (access / lseek / a raw newfstatat instead).
+// dlsym / dlvsym are not listed: the shim defines (interposes) both, in both versions, and
+// reaches glibc's through the C library's symbol table (src/shim/dlsym_hook.cpp). The reference's
 // libvgpu.so was built on Ubuntu 20.04 for the same reason.
 //
 // Force-included (-include) into every object of the non-sanitizer build; the sanitizer
@@ -18,7 +20,6 @@
 __asm__(".symver dlopen,dlopen@GLIBC_2.2.5");
 __asm__(".symver dlclose,dlclose@GLIBC_2.2.5");
 __asm__(".symver dladdr,dladdr@GLIBC_2.2.5");
-__asm__(".symver dlvsym,dlvsym@GLIBC_2.2.5");
 __asm__(".symver dlerror,dlerror@GLIBC_2.2.5");
 __asm__(".symver dl_iterate_phdr,dl_iterate_phdr@GLIBC_2.2.5");
 __asm__(".symver pthread_create,pthread_create@GLIBC_2.2.5");

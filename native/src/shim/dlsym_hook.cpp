@@ -1,8 +1,15 @@
-// dlsym interposition: lookups made on a library handle never consult the
+// dlsym / dlvsym interposition: lookups made on a library handle never consult the
 // preloaded shim, so hooked names are routed back into it here.
 //
-// Reference: libvgpu.so overrides dlsym [src/libvgpu.c:109-124] so that runtimes that
-// dlopen the driver still reach the hooks. On MI355X two kinds of callers need it:
+// Reference: libvgpu.so overrides dlsym [src/libvgpu.c:109-124] (__dlsym_hook_section routes
+// 199 hooked driver names) so that runtimes that dlopen the driver still reach the hooks.
+// On MI355X the lookups that need it:
+//   * ROCr entry points looked up on a libhsa-runtime64 handle (ctypes.CDLL(libhsa...),
+//     dlsym(dlopen("libhsa-runtime64.so.1"), "hsa_amd_memory_pool_allocate")): the HSA
+//     layer is where the quota, the CU mask and the shim's own initialisation live, so a
+//     lookup that found ROCr's definition of a name the shim exports under ROCR_1 gets the
+//     shim's (hsa_hooks.cpp), for callers outside ROCr and the shim - hsa_init included,
+//     so a ctypes-only HSA program initialises the shim;
 //   * HIP runtimes loaded by handle: Triton (every torch.compile tenant) dlopens
 //     libamdhip64 and resolves hipGetProcAddress with dlsym(handle, ...), then its launch
 //     entry points through it. Names starting with "hip" that the shim gates
@@ -14,16 +21,19 @@
 //     "amdsmi_" / "rsmi_" that resolve into an SMI library and have a virtualising hook
 //     are redirected (to smi_hooks.cpp), and only for callers outside the SMI libraries
 //     (libamd_smi embeds and calls rocm_smi itself, with node indices);
-//   * the rocm_smi hooks are reached only this way (not exported from the shim), so
-//     libamd_smi's internal calls to its own rsmi_* never hit the index remapping;
-//   * every other lookup is a guaranteed tail call ([[clang::musttail]]) into glibc,
-//     so RTLD_NEXT keeps resolving relative to the *original* caller - other
-//     interposers preloaded alongside the shim are unaffected.
-// Both glibc symbol versions are provided (dlsym@GLIBC_2.2.5 for old binaries,
-// dlsym@@GLIBC_2.34 for current ones). dlvsym is not interposed (the shim itself needs
-// glibc's to find the real dlsym, and no HIP consumer resolves entry points with it).
-// This file is compiled with clang (musttail).
+//   * the lookup functions themselves: dlsym(libc, "dlsym") or dlvsym(.., "dlvsym", ..)
+//     would hand out glibc's and skip all of the above, so those names get the shim's.
+// dlvsym is interposed as well, with the same routing (versions must match: ROCR_1 for
+// ROCr, the gate's version for HIP). Every lookup that is not routed is a guaranteed tail
+// call ([[clang::musttail]]) into glibc, so RTLD_NEXT keeps resolving relative to the
+// *original* caller - other interposers preloaded alongside the shim are unaffected.
+// glibc's own dlsym / dlvsym are found by reading the C library's dynamic symbol table
+// (dl_iterate_phdr): the shim cannot ask dlvsym for them once it interposes dlvsym.
+// Both glibc symbol versions are provided (GLIBC_2.2.5 for old binaries and C libraries,
+// GLIBC_2.34 for current ones). This file is compiled with clang (musttail).
 #include <dlfcn.h>
+#include <elf.h>
+#include <link.h>
 
 #include <atomic>
 #include <cstdlib>
@@ -46,6 +56,10 @@ rsmi_status_t rsmi_compute_process_info_get(rsmi_process_info_t*, uint32_t*);
 rsmi_status_t rsmi_compute_process_info_by_pid_get(uint32_t, rsmi_process_info_t*);
 rsmi_status_t rsmi_num_monitor_devices(uint32_t*);
 rsmi_status_t rsmi_compute_process_gpus_get(uint32_t, uint32_t*, uint32_t*);
+void* shim_dlsym_v234(void* handle, const char* name);
+void* shim_dlsym_v225(void* handle, const char* name);
+void* shim_dlvsym_v234(void* handle, const char* name, const char* version);
+void* shim_dlvsym_v225(void* handle, const char* name, const char* version);
 }
 
 namespace vgpu {
@@ -55,6 +69,7 @@ void* rsmi_remap_hook(const char* name);  // smi_hooks.cpp (generated index rema
 namespace {
 
 using DlsymFn = void* (*)(void*, const char*);
+using DlvsymFn = void* (*)(void*, const char*, const char*);
 
 // VGPU_HOOK_DLSYM=0 turns the redirection off (read once when the shim is loaded).
 bool g_dlsym_hook_on = true;
@@ -63,25 +78,155 @@ __attribute__((constructor)) void dlsym_hook_ctor() {
   if (s && (*s == '0' || *s == 'f' || *s == 'F' || *s == 'n' || *s == 'N')) g_dlsym_hook_on = false;
 }
 
+// ---------------------------------------------------------------- glibc's lookup functions
+
+// Looks `name`@`version` up in the dynamic symbol table of the loaded C library (libc.so.6,
+// or libdl.so.2 where glibc < 2.34 keeps the dl functions).
+struct ElfQuery {
+  const char* name;
+  const char* version;
+  void* found;
+};
+
+// Number of dynamic symbols from a DT_GNU_HASH table: past the highest bucket's chain end.
+size_t gnu_hash_count(const uint32_t* gh) {
+  const uint32_t nbuckets = gh[0], symoffset = gh[1], bloom_size = gh[2];
+  const uint32_t* buckets = reinterpret_cast<const uint32_t*>(reinterpret_cast<const ElfW(Addr)*>(gh + 4) + bloom_size);
+  const uint32_t* chain = buckets + nbuckets;
+  uint32_t last = 0;
+  for (uint32_t i = 0; i < nbuckets; i++)
+    if (buckets[i] > last) last = buckets[i];
+  if (last < symoffset) return symoffset;
+  while (!(chain[last - symoffset] & 1u)) last++;
+  return (size_t)last + 1;
+}
+
+int elf_lookup_cb(struct dl_phdr_info* info, size_t, void* data) {
+  ElfQuery* q = static_cast<ElfQuery*>(data);
+  const char* fn = info->dlpi_name;
+  if (!fn || !*fn) return 0;
+  const char* base_name = strrchr(fn, '/');
+  base_name = base_name ? base_name + 1 : fn;
+  if (strncmp(base_name, "libc.so.", 8) != 0 && strncmp(base_name, "libdl.so.", 9) != 0) return 0;
+  const ElfW(Addr) base = info->dlpi_addr;
+  const ElfW(Dyn)* dyn = nullptr;
+  for (int i = 0; i < info->dlpi_phnum; i++)
+    if (info->dlpi_phdr[i].p_type == PT_DYNAMIC) dyn = reinterpret_cast<const ElfW(Dyn)*>(base + info->dlpi_phdr[i].p_vaddr);
+  if (!dyn) return 0;
+  const ElfW(Sym)* symtab = nullptr;
+  const char* strtab = nullptr;
+  const ElfW(Half)* versym = nullptr;
+  const char* verdef = nullptr;
+  const uint32_t* hash = nullptr;
+  const uint32_t* gnu_hash = nullptr;
+  // ld.so relocates these d_ptr values in place on x86-64; a value below the load base is
+  // still an offset.
+  auto at = [base](ElfW(Addr) a) { return a < base ? a + base : a; };
+  for (const ElfW(Dyn)* d = dyn; d->d_tag != DT_NULL; d++) {
+    switch (d->d_tag) {
+      case DT_SYMTAB: symtab = reinterpret_cast<const ElfW(Sym)*>(at(d->d_un.d_ptr)); break;
+      case DT_STRTAB: strtab = reinterpret_cast<const char*>(at(d->d_un.d_ptr)); break;
+      case DT_VERSYM: versym = reinterpret_cast<const ElfW(Half)*>(at(d->d_un.d_ptr)); break;
+      case DT_VERDEF: verdef = reinterpret_cast<const char*>(at(d->d_un.d_ptr)); break;
+      case DT_HASH: hash = reinterpret_cast<const uint32_t*>(at(d->d_un.d_ptr)); break;
+      case DT_GNU_HASH: gnu_hash = reinterpret_cast<const uint32_t*>(at(d->d_un.d_ptr)); break;
+      default: break;
+    }
+  }
+  if (!symtab || !strtab || !versym || !verdef || (!hash && !gnu_hash)) return 0;
+  const size_t nsyms = hash ? hash[1] : gnu_hash_count(gnu_hash);
+  for (size_t i = 0; i < nsyms; i++) {
+    const ElfW(Sym)& s = symtab[i];
+    if (s.st_shndx == SHN_UNDEF || !s.st_value || strcmp(strtab + s.st_name, q->name) != 0) continue;
+    const ElfW(Half) ndx = versym[i] & 0x7fff;
+    for (const char* v = verdef;;) {
+      const ElfW(Verdef)* vd = reinterpret_cast<const ElfW(Verdef)*>(v);
+      if (vd->vd_ndx == ndx && vd->vd_cnt > 0) {
+        const ElfW(Verdaux)* aux = reinterpret_cast<const ElfW(Verdaux)*>(v + vd->vd_aux);
+        if (strcmp(strtab + aux->vda_name, q->version) == 0) {
+          q->found = reinterpret_cast<void*>(base + s.st_value);
+          return 1;
+        }
+        break;
+      }
+      if (!vd->vd_next) break;
+      v += vd->vd_next;
+    }
+  }
+  return 0;
+}
+
+void* libc_symbol(const char* name, const char* version) {
+  ElfQuery q{name, version, nullptr};
+  dl_iterate_phdr(elf_lookup_cb, &q);
+  return q.found;
+}
+
 std::atomic<DlsymFn> g_real_234{nullptr};
 std::atomic<DlsymFn> g_real_225{nullptr};
+std::atomic<DlvsymFn> g_realv_234{nullptr};
+std::atomic<DlvsymFn> g_realv_225{nullptr};
 
-// glibc's dlsym, found with dlvsym (not interposed: the shim routes dlsym lookups only).
-DlsymFn load_real(std::atomic<DlsymFn>& slot, const char* ver) {
-  DlsymFn f = slot.load(std::memory_order_acquire);
+// glibc's definition of `name` for symbol version `ver`, or its other version when the C
+// library predates it (glibc < 2.34 has only GLIBC_2.2.5).
+template <typename Fn>
+Fn load_real(std::atomic<Fn>& slot, const char* name, const char* ver) {
+  Fn f = slot.load(std::memory_order_acquire);
   if (__builtin_expect(f != nullptr, 1)) return f;
-  f = reinterpret_cast<DlsymFn>(dlvsym(RTLD_NEXT, "dlsym", ver));
-  if (!f) f = reinterpret_cast<DlsymFn>(dlvsym(RTLD_NEXT, "dlsym", ver[7] == '3' ? "GLIBC_2.2.5" : "GLIBC_2.34"));
+  f = reinterpret_cast<Fn>(libc_symbol(name, ver));
+  if (!f) f = reinterpret_cast<Fn>(libc_symbol(name, ver[7] == '3' ? "GLIBC_2.2.5" : "GLIBC_2.34"));
   slot.store(f, std::memory_order_release);
   return f;
 }
+
+DlsymFn real_dlsym_234() { return load_real(g_real_234, "dlsym", "GLIBC_2.34"); }
+DlsymFn real_dlsym_225() { return load_real(g_real_225, "dlsym", "GLIBC_2.2.5"); }
+DlvsymFn real_dlvsym_234() { return load_real(g_realv_234, "dlvsym", "GLIBC_2.34"); }
+DlvsymFn real_dlvsym_225() { return load_real(g_realv_225, "dlvsym", "GLIBC_2.2.5"); }
+
+// ---------------------------------------------------------------- where an address lives
+
+const char* object_of(const void* addr) {
+  Dl_info info;
+  if (!addr || !dladdr(addr, &info) || !info.dli_fname) return nullptr;
+  return info.dli_fname;
+}
+
+bool in_library(const void* addr, const char* soname_part) {
+  const char* f = object_of(addr);
+  return f && strstr(f, soname_part) && !strstr(f, "vgpu");
+}
+
+bool in_hip_library(const void* addr) { return in_library(addr, "libamdhip64"); }
+bool in_hsa_library(const void* addr) { return in_library(addr, "libhsa-runtime64"); }
+
+bool in_smi_library(const void* addr) {
+  const char* f = object_of(addr);
+  return f && (strstr(f, "amd_smi") || strstr(f, "rocm_smi")) && !strstr(f, "vgpu");
+}
+
+bool in_libc(const void* addr) {
+  const char* f = object_of(addr);
+  if (!f) return false;
+  const char* b = strrchr(f, '/');
+  b = b ? b + 1 : f;
+  return strncmp(b, "libc.so.", 8) == 0 || strncmp(b, "libdl.so.", 9) == 0;
+}
+
+bool in_shim(const void* addr) {
+  Dl_info a, self;
+  return addr && dladdr(addr, &a) && dladdr(reinterpret_cast<const void*>(&in_shim), &self) &&
+         a.dli_fbase == self.dli_fbase;
+}
+
+// ---------------------------------------------------------------- routing tables
 
 struct Hook {
   const char* name;
   void* fn;
 };
 
-const Hook kHooks[] = {
+const Hook kSmiHooks[] = {
     {"amdsmi_get_gpu_memory_total", reinterpret_cast<void*>(&amdsmi_get_gpu_memory_total)},
     {"amdsmi_get_gpu_memory_usage", reinterpret_cast<void*>(&amdsmi_get_gpu_memory_usage)},
     {"amdsmi_get_gpu_vram_usage", reinterpret_cast<void*>(&amdsmi_get_gpu_vram_usage)},
@@ -95,84 +240,128 @@ const Hook kHooks[] = {
     {"rsmi_compute_process_gpus_get", reinterpret_cast<void*>(&rsmi_compute_process_gpus_get)},
 };
 
-bool in_hip_library(const void* addr) {
-  Dl_info info;
-  if (!addr || !dladdr(addr, &info) || !info.dli_fname) return false;
-  return strstr(info.dli_fname, "libamdhip64") && !strstr(info.dli_fname, "vgpu");
-}
-
-bool in_shim(const void* addr) {
-  Dl_info a, self;
-  return addr && dladdr(addr, &a) && dladdr(reinterpret_cast<const void*>(&in_shim), &self) &&
-         a.dli_fbase == self.dli_fbase;
+// hsa* lookups on a library handle: the shim's definition (exported as name@ROCR_1) when
+// the lookup found ROCr's entry point of that name.
+__attribute__((noinline)) void* maybe_hook_hsa(const char* name, const char* version, void* found,
+                                               const void* caller) {
+  if (!found || (version && strcmp(version, "ROCR_1") != 0)) return nullptr;
+  if (!in_hsa_library(found) || in_hsa_library(caller) || in_shim(caller)) return nullptr;
+  return vgpu::hsa_hook_for_name(name);
 }
 
 // hip* lookups on a library handle: the shim's gate when the lookup found the runtime's
 // entry point that gate forwards to.
-__attribute__((noinline)) void* maybe_hook_hip(void* handle, const char* name, const char* version, void* found,
+__attribute__((noinline)) void* maybe_hook_hip(const char* name, const char* version, void* found,
                                                const void* caller) {
-  if (!found || handle == RTLD_NEXT || handle == RTLD_DEFAULT) return nullptr;
-  if (strncmp(name, "hip", 3) != 0 || !in_hip_library(found)) return nullptr;
+  if (!found || !in_hip_library(found)) return nullptr;
   if (in_hip_library(caller) || in_shim(caller)) return nullptr;
   return vgpu::hip_hook_for_name(name, version, found);
 }
 
-bool in_smi_library(const void* addr) {
-  Dl_info info;
-  if (!addr || !dladdr(addr, &info) || !info.dli_fname) return false;
-  const char* f = info.dli_fname;
-  return (strstr(f, "amd_smi") || strstr(f, "rocm_smi")) && !strstr(f, "vgpu");
-}
-
-__attribute__((noinline)) void* maybe_hook(void* handle, const char* name, DlsymFn real, const void* caller) {
-  if (handle == RTLD_NEXT || handle == RTLD_DEFAULT) return nullptr;
-  if (strncmp(name, "amdsmi_", 7) != 0 && strncmp(name, "rsmi_", 5) != 0) return nullptr;
+__attribute__((noinline)) void* maybe_hook_smi(const char* name, void* found, const void* caller) {
   void* hook = nullptr;
-  for (const Hook& h : kHooks)
+  for (const Hook& h : kSmiHooks)
     if (strcmp(name, h.name) == 0) hook = h.fn;
   if (!hook && name[0] == 'r') hook = vgpu::rsmi_remap_hook(name);
   if (!hook || in_smi_library(caller)) return nullptr;
-  void* p = real(handle, name);
-  return p && in_smi_library(p) ? hook : nullptr;
+  return found && in_smi_library(found) ? hook : nullptr;
+}
+
+// dlsym / dlvsym themselves, found in the C library: the shim's interposer of the same
+// symbol version (so a tenant cannot fetch glibc's and look ROCr up unrouted).
+__attribute__((noinline)) void* maybe_hook_lookup(const char* name, void* found, const void* caller) {
+  if (!found || in_shim(caller) || !in_libc(found)) return nullptr;
+  if (strcmp(name, "dlsym") == 0)
+    return found == reinterpret_cast<void*>(real_dlsym_225()) && found != reinterpret_cast<void*>(real_dlsym_234())
+               ? reinterpret_cast<void*>(&shim_dlsym_v225)
+               : reinterpret_cast<void*>(&shim_dlsym_v234);
+  if (strcmp(name, "dlvsym") == 0)
+    return found == reinterpret_cast<void*>(real_dlvsym_225()) && found != reinterpret_cast<void*>(real_dlvsym_234())
+               ? reinterpret_cast<void*>(&shim_dlvsym_v225)
+               : reinterpret_cast<void*>(&shim_dlvsym_v234);
+  return nullptr;
+}
+
+// Whether a looked-up name may be routed at all (cheap first-character filter: every other
+// lookup goes straight to glibc).
+inline bool routable(const char* name) {
+  switch (name[0]) {
+    case 'h': return name[1] == 'i' || (name[1] == 's' && name[2] == 'a' && name[3] == '_');
+    case 'a': return strncmp(name, "amdsmi_", 7) == 0;
+    case 'r': return strncmp(name, "rsmi_", 5) == 0;
+    case 'd': return name[1] == 'l' && (strcmp(name, "dlsym") == 0 || strcmp(name, "dlvsym") == 0);
+    default: return false;
+  }
+}
+
+// The routed answer for a lookup that found `found`, or null to keep it.
+void* route(const char* name, const char* version, void* found, const void* caller) {
+  switch (name[0]) {
+    case 'h': return name[1] == 'i' ? maybe_hook_hip(name, version, found, caller)
+                                    : maybe_hook_hsa(name, version, found, caller);
+    case 'a':
+    case 'r': return maybe_hook_smi(name, found, caller);
+    case 'd': return maybe_hook_lookup(name, found, caller);
+    default: return nullptr;
+  }
 }
 
 }  // namespace
 
 namespace vgpu {
-// The shim's own lookups must bypass the interposer (they want the real symbols).
-void* real_dlsym(void* handle, const char* name) { return load_real(g_real_234, "GLIBC_2.34")(handle, name); }
-void* real_dlvsym(void* handle, const char* name, const char* version) { return dlvsym(handle, name, version); }
+// The shim's own lookups must bypass the interposers (they want the real symbols). Called
+// from the shim, RTLD_NEXT stays relative to the shim.
+void* real_dlsym(void* handle, const char* name) { return real_dlsym_234()(handle, name); }
+void* real_dlvsym(void* handle, const char* name, const char* version) {
+  return real_dlvsym_234()(handle, name, version);
+}
 }  // namespace vgpu
 
 extern "C" {
 
-// A hip* lookup is resolved first (a plain call: the handle names the library, so the
-// result does not depend on the caller) and replaced by the gate when it is one; every
-// other lookup is a guaranteed tail call so RTLD_NEXT stays relative to the caller.
-#define VGPU_DLSYM_BODY(slot, ver)                                                              \
-  DlsymFn real = load_real(slot, ver);                                                          \
-  if (__builtin_expect(g_dlsym_hook_on && name != nullptr, 1)) {                                \
-    if (name[0] == 'h' && handle != RTLD_NEXT && handle != RTLD_DEFAULT) {                      \
-      void* p = real(handle, name);                                                             \
-      void* h = maybe_hook_hip(handle, name, nullptr, p, __builtin_return_address(0));          \
-      return h ? h : p;                                                                         \
-    }                                                                                           \
-    if (__builtin_expect(name[0] == 'a' || name[0] == 'r', 0)) {                                \
-      if (void* h = maybe_hook(handle, name, real, __builtin_return_address(0))) return h;      \
-    }                                                                                           \
-  }                                                                                             \
+// A routable lookup on a library handle is resolved first (a plain call: the handle names
+// the library, so the result does not depend on the caller) and replaced by the shim's
+// definition when it is one; every other lookup is a guaranteed tail call so RTLD_NEXT
+// stays relative to the caller.
+#define VGPU_DLSYM_BODY(realfn)                                                           \
+  DlsymFn real = realfn();                                                                \
+  if (__builtin_expect(g_dlsym_hook_on && name != nullptr, 1) && handle != RTLD_NEXT &&   \
+      handle != RTLD_DEFAULT && routable(name)) {                                         \
+    void* p = real(handle, name);                                                         \
+    void* h = route(name, nullptr, p, __builtin_return_address(0));                       \
+    return h ? h : p;                                                                     \
+  }                                                                                       \
   [[clang::musttail]] return real(handle, name);
 
+#define VGPU_DLVSYM_BODY(realfn)                                                          \
+  DlvsymFn real = realfn();                                                               \
+  if (__builtin_expect(g_dlsym_hook_on && name != nullptr, 1) && handle != RTLD_NEXT &&   \
+      handle != RTLD_DEFAULT && routable(name)) {                                         \
+    void* p = real(handle, name, version);                                                \
+    void* h = route(name, version, p, __builtin_return_address(0));                       \
+    return h ? h : p;                                                                     \
+  }                                                                                       \
+  [[clang::musttail]] return real(handle, name, version);
+
 __attribute__((visibility("default"))) void* shim_dlsym_v234(void* handle, const char* name) {
-  VGPU_DLSYM_BODY(g_real_234, "GLIBC_2.34")
+  VGPU_DLSYM_BODY(real_dlsym_234)
 }
 
 __attribute__((visibility("default"))) void* shim_dlsym_v225(void* handle, const char* name) {
-  VGPU_DLSYM_BODY(g_real_225, "GLIBC_2.2.5")
+  VGPU_DLSYM_BODY(real_dlsym_225)
+}
+
+__attribute__((visibility("default"))) void* shim_dlvsym_v234(void* handle, const char* name, const char* version) {
+  VGPU_DLVSYM_BODY(real_dlvsym_234)
+}
+
+__attribute__((visibility("default"))) void* shim_dlvsym_v225(void* handle, const char* name, const char* version) {
+  VGPU_DLVSYM_BODY(real_dlvsym_225)
 }
 
 }  // extern "C"
 
 __asm__(".symver shim_dlsym_v234, dlsym@@GLIBC_2.34");
 __asm__(".symver shim_dlsym_v225, dlsym@GLIBC_2.2.5");
-
+__asm__(".symver shim_dlvsym_v234, dlvsym@@GLIBC_2.34");
+__asm__(".symver shim_dlvsym_v225, dlvsym@GLIBC_2.2.5");

@@ -17,7 +17,10 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <vector>
 
@@ -197,6 +200,48 @@ hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
       s.region.uncharge(s.slot, rec.dev, rec.size, (MemKind)rec.kind);
   }
   return real_hsa_amd_memory_pool_free(ptr);
+}
+
+// The legacy region API reaches the same memory: ROCr's hsa_region_t and
+// hsa_amd_memory_pool_t handles name the same memory-region objects (a GPU's coarse-grained
+// VRAM region is its VRAM pool), so a region allocation is admitted like a pool allocation.
+// ROCr serves it without passing through the exported pool entry point, so nothing is
+// charged twice.
+hsa_status_t hsa_memory_allocate(hsa_region_t region, size_t size, void** ptr) {
+  VGPU_REAL_HSA(hsa_memory_allocate);
+  if (!real_hsa_memory_allocate) return HSA_STATUS_ERROR;
+  const hsa_amd_memory_pool_t pool{region.handle};
+  if (!ready() || size == 0) {
+    if (size && refused(pool)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+    return real_hsa_memory_allocate(region, size, ptr);
+  }
+  int dev = pool_ordinal(pool);
+  if (dev < 0) return real_hsa_memory_allocate(region, size, ptr);
+  ShimState& s = shim();
+  gate_suspend();
+  if (__builtin_expect(!s.agents[dev].authorised, 0)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  if (s.region.charge(s.slot, dev, size, kMemData) != Charge::kOk) {
+    VLOG_WARN("device %d OOM (region): request %zu bytes, usage %lu of limit %lu", dev, size,
+              (unsigned long)s.region.usage(dev), (unsigned long)s.region.limit(dev));
+    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  }
+  hsa_status_t st = real_hsa_memory_allocate(region, size, ptr);
+  if (st == HSA_STATUS_SUCCESS && ptr && *ptr) record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemData);
+  else s.region.uncharge(s.slot, dev, size, kMemData);
+  return st;
+}
+
+hsa_status_t hsa_memory_free(void* ptr) {
+  VGPU_REAL_HSA(hsa_memory_free);
+  if (!real_hsa_memory_free) return HSA_STATUS_ERROR;
+  ShimState& s = shim();
+  hsa_status_t st = real_hsa_memory_free(ptr);
+  if (st == HSA_STATUS_SUCCESS && ptr && s.phase.load(std::memory_order_relaxed) == 2) {
+    AllocRec rec;
+    if (take_alloc(reinterpret_cast<uintptr_t>(ptr), &rec) && s.slot >= 0 && !s.exiting.load())
+      s.region.uncharge(s.slot, rec.dev, rec.size, (MemKind)rec.kind);
+  }
+  return st;
 }
 
 hsa_status_t hsa_amd_vmem_handle_create(hsa_amd_memory_pool_t pool, size_t size, hsa_amd_memory_type_t type,
@@ -466,3 +511,39 @@ hsa_status_t hsa_amd_ipc_memory_detach(void* mapped_ptr) {
 }
 
 }  // extern "C"
+
+namespace vgpu {
+
+// Every ROCr entry point the shim defines (libvgpu_hip.map.in, ROCR_1). Lookups of these
+// names on a libhsa-runtime64 handle are routed here (dlsym_hook.cpp).
+const char* const kHsaHooked[] = {
+    "hsa_init", "hsa_amd_memory_pool_allocate", "hsa_amd_memory_pool_free", "hsa_amd_memory_pool_get_info",
+    "hsa_amd_vmem_handle_create", "hsa_amd_vmem_handle_release", "hsa_agent_get_info", "hsa_queue_create",
+    "hsa_queue_destroy", "hsa_amd_queue_cu_set_mask", "hsa_amd_ipc_memory_attach", "hsa_amd_ipc_memory_detach",
+    "hsa_memory_allocate", "hsa_memory_free",
+};
+constexpr int kNumHsaHooked = sizeof(kHsaHooked) / sizeof(kHsaHooked[0]);
+
+void* hsa_hook_for_name(const char* name) {
+  // The shim's own definitions, by symbol version from its own handle (and checked to lie
+  // in the shim: a lookup on the shim's handle also searches its dependencies).
+  static std::atomic<void*> self[kNumHsaHooked];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    Dl_info me;
+    if (!dladdr(reinterpret_cast<void*>(&hsa_hook_for_name), &me) || !me.dli_fname) return;
+    void* h = dlopen(me.dli_fname, RTLD_NOLOAD | RTLD_LAZY);
+    if (!h) return;
+    for (int i = 0; i < kNumHsaHooked; i++) {
+      void* p = real_dlvsym(h, kHsaHooked[i], "ROCR_1");
+      Dl_info di;
+      if (p && dladdr(p, &di) && di.dli_fbase == me.dli_fbase) self[i].store(p, std::memory_order_relaxed);
+    }
+    dlclose(h);
+  });
+  for (int i = 0; i < kNumHsaHooked; i++)
+    if (strcmp(kHsaHooked[i], name) == 0) return self[i].load(std::memory_order_relaxed);
+  return nullptr;
+}
+
+}  // namespace vgpu

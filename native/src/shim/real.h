@@ -19,6 +19,9 @@ void* real_dlvsym(void* handle, const char* name, const char* version);
 // entry point that hook forwards to. Null when the entry point is not hooked.
 void* hip_hook_for_real(const void* real);
 void* hip_hook_for_name(const char* name, const char* version, const void* real);
+// The shim's own definition of ROCr entry point `name` (exported as name@ROCR_1), or null
+// when the shim does not hook it (hsa_hooks.cpp).
+void* hsa_hook_for_name(const char* name);
 
 // Looks `name` (version `ver`, may be null) up in the first loaded object whose path
 // contains `lib_substr`; falls back to RTLD_NEXT. Returns null when absent (logged as an

@@ -71,7 +71,7 @@ hsa_status_t pool_cb(hsa_amd_memory_pool_t pool, void* data) {
   if (real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS)
     return HSA_STATUS_SUCCESS;
   if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
-  if (a->n_pools < 8) a->pools[a->n_pools++] = pool;
+  if (a->n_pools < kMaxAgentPools) a->pools[a->n_pools++] = pool;
   size_t sz = 0;
   uint32_t flags = 0;
   real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SIZE, &sz);
@@ -82,6 +82,23 @@ hsa_status_t pool_cb(hsa_amd_memory_pool_t pool, void* data) {
     real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc_ok);
     if (alloc_ok) a->vram_pool = pool;
   }
+  return HSA_STATUS_SUCCESS;
+}
+
+// The agent's global regions (legacy hsa_memory_allocate API): in ROCr a region handle and
+// the pool handle of the same memory are one object, but that is not part of the API, so
+// the handles are recorded with the pools either way (pool_ordinal covers both).
+hsa_status_t region_cb(hsa_region_t region, void* data) {
+  AgentInfo* a = static_cast<AgentInfo*>(data);
+  VGPU_REAL_HSA(hsa_region_get_info);
+  hsa_region_segment_t seg;
+  if (!real_hsa_region_get_info ||
+      real_hsa_region_get_info(region, HSA_REGION_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_REGION_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  for (int j = 0; j < a->n_pools; j++)
+    if (a->pools[j].handle == region.handle) return HSA_STATUS_SUCCESS;
+  if (a->n_pools < kMaxAgentPools) a->pools[a->n_pools++] = hsa_amd_memory_pool_t{region.handle};
   return HSA_STATUS_SUCCESS;
 }
 
@@ -138,6 +155,8 @@ hsa_status_t agent_cb(hsa_agent_t agent, void* data) {
     a.cpu_agent = cpu;
   VGPU_REAL_HSA(hsa_amd_agent_iterate_memory_pools);
   real_hsa_amd_agent_iterate_memory_pools(agent, pool_cb, &a);
+  VGPU_REAL_HSA(hsa_agent_iterate_regions);
+  if (real_hsa_agent_iterate_regions) real_hsa_agent_iterate_regions(agent, region_cb, &a);
   return HSA_STATUS_SUCCESS;
 }
 

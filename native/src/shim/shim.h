@@ -22,6 +22,8 @@
 
 namespace vgpu {
 
+constexpr int kMaxAgentPools = 16;
+
 struct AgentInfo {
   hsa_agent_t agent{0};
   hsa_agent_t cpu_agent{0};          // nearest CPU agent (host-spill pool owner)
@@ -38,7 +40,7 @@ struct AgentInfo {
   std::atomic<bool> temporal_active{false};  // GPU-time credit gates its launches
   CuMode mode = CuMode::kOff;                // effective enforcement mode
   CuMask mask;
-  hsa_amd_memory_pool_t pools[8]{};  // GPU-local pools of this agent
+  hsa_amd_memory_pool_t pools[kMaxAgentPools]{};  // GPU-local global pools (and regions) of this agent
   hsa_amd_memory_pool_t vram_pool{0};  // coarse-grained VRAM pool (host-PID probe allocations)
   int n_pools = 0;
 };

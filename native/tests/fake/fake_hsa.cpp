@@ -235,7 +235,12 @@ hsa_status_t hsa_amd_memory_pool_get_info(hsa_amd_memory_pool_t pool, hsa_amd_me
   return HSA_STATUS_SUCCESS;
 }
 
-hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t, void** ptr) {
+}  // extern "C"
+
+namespace {
+// Internal entry points: ROCr's exported functions never call each other through their
+// exported symbols (which the preloaded shim interposes), so neither does the fake.
+hsa_status_t pool_allocate_impl(hsa_amd_memory_pool_t pool, size_t size, void** ptr) {
   setup();
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
@@ -254,7 +259,7 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   return HSA_STATUS_SUCCESS;
 }
 
-hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
+hsa_status_t pool_free_impl(void* ptr) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   auto it = s.allocs.find(reinterpret_cast<uintptr_t>(ptr));
@@ -267,6 +272,41 @@ hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
   s.allocs.erase(it);
   return HSA_STATUS_SUCCESS;
 }
+}  // namespace
+
+extern "C" {
+
+hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t, void** ptr) {
+  return pool_allocate_impl(pool, size, ptr);
+}
+hsa_status_t hsa_amd_memory_pool_free(void* ptr) { return pool_free_impl(ptr); }
+
+// Legacy region API: the GPU's region handle is its pool handle (as in ROCr).
+hsa_status_t hsa_agent_iterate_regions(hsa_agent_t agent, hsa_status_t (*cb)(hsa_region_t, void*), void* data) {
+  int d = gpu_of(agent);
+  if (agent.handle == kCpuAgent) return cb(hsa_region_t{kCpuPool}, data);
+  if (d < 0) return HSA_STATUS_ERROR_INVALID_AGENT;
+  return cb(hsa_region_t{kGpuPoolBase + (uint64_t)d}, data);
+}
+hsa_status_t hsa_region_get_info(hsa_region_t region, hsa_region_info_t attr, void* value) {
+  if ((int)attr == HSA_REGION_INFO_SEGMENT) {
+    *static_cast<hsa_region_segment_t*>(value) = HSA_REGION_SEGMENT_GLOBAL;
+    return HSA_STATUS_SUCCESS;
+  }
+  if ((int)attr == HSA_REGION_INFO_RUNTIME_ALLOC_ALLOWED) {
+    *static_cast<bool*>(value) = true;
+    return HSA_STATUS_SUCCESS;
+  }
+  if ((int)attr == HSA_REGION_INFO_GLOBAL_FLAGS) {
+    *static_cast<uint32_t*>(value) = HSA_REGION_GLOBAL_FLAG_COARSE_GRAINED;
+    return HSA_STATUS_SUCCESS;
+  }
+  return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+}
+hsa_status_t hsa_memory_allocate(hsa_region_t region, size_t size, void** ptr) {
+  return pool_allocate_impl(hsa_amd_memory_pool_t{region.handle}, size, ptr);
+}
+hsa_status_t hsa_memory_free(void* ptr) { return pool_free_impl(ptr); }
 
 hsa_status_t hsa_amd_agents_allow_access(uint32_t, const hsa_agent_t*, const uint32_t*, const void*) {
   return HSA_STATUS_SUCCESS;
@@ -336,13 +376,13 @@ hsa_status_t hsa_amd_queue_set_priority(hsa_queue_t* queue, hsa_amd_queue_priori
 hsa_status_t hsa_amd_vmem_handle_create(hsa_amd_memory_pool_t pool, size_t size, hsa_amd_memory_type_t, uint64_t,
                                         hsa_amd_vmem_alloc_handle_t* handle) {
   void* p = nullptr;
-  hsa_status_t r = hsa_amd_memory_pool_allocate(pool, size, 0, &p);
+  hsa_status_t r = pool_allocate_impl(pool, size, &p);
   if (r == HSA_STATUS_SUCCESS) handle->handle = reinterpret_cast<uint64_t>(p);
   return r;
 }
 
 hsa_status_t hsa_amd_vmem_handle_release(hsa_amd_vmem_alloc_handle_t handle) {
-  return hsa_amd_memory_pool_free(reinterpret_cast<void*>(handle.handle));
+  return pool_free_impl(reinterpret_cast<void*>(handle.handle));
 }
 
 hsa_status_t hsa_amd_ipc_memory_attach(const hsa_amd_ipc_memory_t*, size_t len, uint32_t, const hsa_agent_t*,

@@ -112,16 +112,6 @@ def test_temporal_limiter_closed_loop(fake, limit):
     assert abs(got - limit) <= 5.0, got
 
 
-def test_exact_share_drives_the_grants(fake):
-    """VGPU_DEVICE_CU_SHARE (the exact share the plugin sends with the node ledger) sets the
-    limiter's grants; the whole-percent VGPU_DEVICE_CU_LIMIT still decides that the vGPU
-    is limited (and its CU slice)."""
-    e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="40", VGPU_DEVICE_CU_SHARE_0="25", VGPU_CU_MODE="temporal")
-    out = run(e, "stream", "run=1000,3", timeout=120)
-    got = [o for o in out if "run" in o][0]["busy_frac"]
-    assert abs(got - 0.25) <= 0.05, got
-
-
 def test_graph_launches_are_limited(fake):
     e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="temporal")
     out = run(e, "stream", "graph=5000,3", timeout=120)
@@ -420,6 +410,28 @@ def _ledger_daemon(fake, board, period_us=1000):
     from amdvgpu.shim.native import LEDGER, lib_path
     env = dict(os.environ, VGPU_KFD_ROOT=fake.kfd)
     return sp.Popen([lib_path(LEDGER), "--dir", str(board), "--period-us", str(period_us)], env=env)
+
+
+@pytest.mark.parametrize("ledger,want", [(True, 0.25), (False, 0.40)])
+def test_exact_share_drives_the_grants_with_the_ledger(fake, tmp_path, ledger, want):
+    """VGPU_DEVICE_CU_SHARE (the exact share the plugin sends with the node ledger) sets the
+    limiter's grants while the ledger's exact charges are in use; the whole-percent
+    VGPU_DEVICE_CU_LIMIT still decides that the vGPU is limited. Without a fresh ledger the
+    container charges itself from its own sampling, which over-charges on a crowded GPU, so
+    it keeps the rounded-up percent."""
+    board = tmp_path / "board"
+    board.mkdir()
+    e = _board_env(fake, tmp_path, "share", VGPU_DEVICE_CU_LIMIT="40", VGPU_DEVICE_CU_SHARE_0="25",
+                   VGPU_CU_MODE="temporal")
+    d = _ledger_daemon(fake, board) if ledger else None
+    try:
+        out = run(e, "stream", "run=1500,3", timeout=120)
+    finally:
+        if d:
+            d.terminate()
+            d.wait(timeout=10)
+    got = [o for o in out if "run" in o][0]["busy_frac"]
+    assert abs(got - want) <= 0.05, got
 
 
 @pytest.mark.parametrize("ledger", [True, False])
