@@ -55,7 +55,12 @@ class PluginConfig:
     shared_cache_dir: str = "/tmp"
     placement: str = "spread"               # which GPU a 1-vGPU pod lands on (GetPreferredAllocation)
     duplicate_vgpus: str = "reject"         # Allocate of two vGPUs of one GPU: reject | merge
-    host_memory_per_vgpu: str = "0"         # pinned host memory budget per vGPU (0 = unlimited)
+    host_memory_per_vgpu: str = "auto"      # pinned host memory budget per vGPU (auto: a share of the node's RAM; 0 = unlimited)
+    host_memory_fraction: float = 0.5       # of the node's RAM, what vGPU containers may pin in total (buffers + spill)
+    host_memory_total: str = ""             # the node's RAM (default: /proc/meminfo MemTotal)
+    allow_latency_class: bool = False       # every container may take VGPU_TASK_PRIORITY=0
+    latency_vgpus_per_gpu: int = 0          # vGPUs per GPU advertised as <resource>-latency (latency class granted)
+    host_budget_bytes: int = -1             # resolved per-vGPU host budget (plugin/host_memory.py; -1 = not yet)
     gpu_concurrency: int = 0                # limited containers holding a GPU's time at once (0 = any)
     ledger: bool = False                    # run the node's GPU-time ledger daemon (vgpu-ledger; profiles/r3v)
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"  # kubelet PodResources v1
@@ -88,16 +93,30 @@ class PluginConfig:
         if not 0 <= self.gpu_concurrency <= 64:
             raise ValueError(f"invalid --gpu-concurrency option: {self.gpu_concurrency}")
         from ..utils.sizes import parse_size
-        try:
-            parse_size(self.host_memory_per_vgpu)
-        except ValueError:
-            raise ValueError(f"invalid --host-memory-per-vgpu option: {self.host_memory_per_vgpu}") from None
+        if self.host_memory_per_vgpu != "auto":
+            try:
+                parse_size(self.host_memory_per_vgpu)
+            except ValueError:
+                raise ValueError(f"invalid --host-memory-per-vgpu option: {self.host_memory_per_vgpu}") from None
+        if not 0.0 <= self.host_memory_fraction <= 1.0:
+            raise ValueError(f"invalid --host-memory-fraction option: {self.host_memory_fraction}")
+        if self.host_memory_total:
+            try:
+                parse_size(self.host_memory_total)
+            except ValueError:
+                raise ValueError(f"invalid --host-memory-total option: {self.host_memory_total}") from None
+        if self.latency_vgpus_per_gpu < 0 or (self.latency_vgpus_per_gpu and
+                                              self.latency_vgpus_per_gpu >= self.device_split_count):
+            raise ValueError(f"invalid --latency-vgpus-per-gpu option: {self.latency_vgpus_per_gpu} (at most "
+                             f"--device-split-count - 1 = {self.device_split_count - 1})")
         return self
 
     @property
     def host_memory_per_vgpu_bytes(self):
+        """The explicit per-vGPU budget (0 = unlimited); "auto" is resolved against the node
+        by host_memory.host_budget_per_vgpu."""
         from ..utils.sizes import parse_size
-        return parse_size(self.host_memory_per_vgpu)
+        return 0 if self.host_memory_per_vgpu == "auto" else parse_size(self.host_memory_per_vgpu)
 
 
 # (flag, dest, type, env vars, help)
@@ -140,7 +159,21 @@ _FLAGS = [
      "a container given two vGPUs of one GPU: reject (fail Allocate) | merge (one device with the summed "
      "quota and CU share; VGPU_DUPLICATE_MERGED tells the container)"),
     ("--host-memory-per-vgpu", "host_memory_per_vgpu", str, ["HOST_MEMORY_PER_VGPU"],
-     "pinned host memory (hipHostMalloc / hipHostRegister) per vGPU, e.g. 64g; 0 = unlimited (tracked only)"),
+     "pinned host memory (hipHostMalloc / hipHostRegister, and the host spill of oversubscribed vGPUs) per vGPU, "
+     "e.g. 64g; auto (default) = --host-memory-fraction of the node's RAM divided among its vGPUs; "
+     "0 = unlimited (tracked only)"),
+    ("--host-memory-fraction", "host_memory_fraction", float, ["HOST_MEMORY_FRACTION"],
+     "share of the node's RAM vGPU containers may pin in total (default 0.5); --device-memory-scaling whose "
+     "host spill would not fit in it is refused at start; 0 = no node bound (neither the check nor an automatic "
+     "per-vGPU budget: the reference's behaviour)"),
+    ("--host-memory-total", "host_memory_total", str, ["HOST_MEMORY_TOTAL"],
+     "the node's RAM for the budgets above (default: MemTotal from /proc/meminfo)"),
+    ("--allow-latency-class", "allow_latency_class", "bool", ["ALLOW_LATENCY_CLASS"],
+     "let every container take the latency class (VGPU_TASK_PRIORITY=0: high queue priority, never duty-cycled, "
+     "reserves its CUs against background tenants); off by default: the class is granted by the plugin only"),
+    ("--latency-vgpus-per-gpu", "latency_vgpus_per_gpu", int, ["LATENCY_VGPUS_PER_GPU"],
+     "of each GPU's split vGPUs, this many are advertised as <resource>-latency (e.g. amd.com/gpu-latency), which "
+     "grants the latency class; an operator bounds it per namespace with a ResourceQuota (default 0)"),
     ("--gpu-concurrency", "gpu_concurrency", int, ["GPU_CONCURRENCY"],
      "containers on the GPU-time limiter that may hold a GPU at once, taking turns over the node-wide board "
      "(0 = no admission: every container whose credit allows runs)"),

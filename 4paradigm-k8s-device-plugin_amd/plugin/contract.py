@@ -110,6 +110,73 @@ ANN_DUPLICATES = "amd-vgpu/merged-duplicates"
 ALLOWLIST_HOST_DIR = "allowlist"
 ALLOWLIST_MAX_AGE_S = 7 * 24 * 3600
 
+# Plugin-owned limits (tamper resistance, native/include/vgpu/config.h load_ceiling): the
+# container's contract, written by the plugin into a root-owned file mounted read-only at
+# CONTAINER_LIMITS. The shim treats it as a ceiling over its environment and its shared
+# region, both of which the tenant controls; its region is a file the plugin creates, mounted
+# over its path (a bind-mounted file cannot be unlinked from inside the container), whose
+# inode the limits file records.
+LIMITS_HOST_DIR = "limits"
+CONTAINER_LIMITS = "/vgpu/limits"
+LIMITS_MAX_AGE_S = 7 * 24 * 3600
+REGIONS_HOST_DIR = "regions"
+CONTAINER_REGION_DIR = "/usr/local/vgpu/regions"
+# A container touches its region every 10 s while it has a GPU process; an older region file
+# is removed from the host directory (a running container keeps its mounted inode).
+REGION_MAX_AGE_S = 3600
+# The env names the limits file carries (the shim reads it with the env parser).
+LIMIT_KEYS = ("VGPU_DEVICE_MAP", "VGPU_DEVICE_MEMORY_LIMIT_", "VGPU_DEVICE_HBM_LIMIT_", "VGPU_DEVICE_CU_LIMIT_",
+              "VGPU_DEVICE_CU_SHARE_", "VGPU_DEVICE_CU_RANGE_", "VGPU_HOST_MEMORY_LIMIT", "VGPU_OVERSUBSCRIBE",
+              "VGPU_CU_MODE", "VGPU_SHARED_CACHE", "VGPU_ALLOWLIST")
+
+
+def _gc_dir(d, suffix, max_age_s):
+    import time
+    now = time.time()
+    try:
+        for fn in os.listdir(d):
+            fp = os.path.join(d, fn)
+            if fn.endswith(suffix) and now - os.path.getmtime(fp) > max_age_s:
+                os.unlink(fp)
+    except OSError:
+        pass
+
+
+def write_limits(vgpu_dir, name, values):
+    """Writes <vgpu_dir>/limits/containers/<name>.env (root-owned, 0644) with ``values``;
+    returns its path, or None when the host directory is not writable."""
+    d = os.path.join(vgpu_dir, LIMITS_HOST_DIR, "containers")
+    path = os.path.join(d, name + ".env")
+    try:
+        os.makedirs(d, exist_ok=True)
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write("".join(f"{k}={v}\n" for k, v in values.items()))
+        os.chmod(tmp, 0o644)
+        os.replace(tmp, path)
+    except OSError:
+        return None
+    _gc_dir(d, ".env", LIMITS_MAX_AGE_S)
+    return path
+
+
+def create_region_file(host_dir, name):
+    """Creates the empty region file <host_dir>/<name> (world-writable: the container's
+    processes may run as any user) the shim initialises on first use. Returns (path, inode),
+    or (None, 0) when the directory is not writable."""
+    path = os.path.join(host_dir, name)
+    try:
+        os.makedirs(host_dir, exist_ok=True)
+        fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_EXCL, 0o666)
+        try:
+            os.fchmod(fd, 0o666)
+            ino = os.fstat(fd).st_ino
+        finally:
+            os.close(fd)
+    except OSError:
+        return None, 0
+    return path, ino
+
 
 def write_allowlist(vgpu_dir, name, uuids):
     """Writes <vgpu_dir>/allowlist/containers/<name>.list with ``uuids``; returns its path,
@@ -235,10 +302,12 @@ def visible_envs(cfg, ids):
 
 
 def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, using_ids=None, pod_tag=None,
-                             pod_uid=None, kubelet_ids=None):
+                             pod_uid=None, kubelet_ids=None, latency=False):
     """ContainerAllocateResponse for one container holding vGPUs ``vdevs``. ``kubelet_ids``:
     the device IDs of the kubelet's request (monitor mode records them in the container's
-    host directory, where the PodResources attribution finds them)."""
+    host directory, where the PodResources attribution finds them). ``latency``: the vGPUs
+    come from the latency resource (--latency-vgpus-per-gpu), which grants the latency
+    class and makes it the container's default."""
     resp = api.ContainerAllocateResponse()
     uuids = []
     for v in vdevs:
@@ -280,7 +349,9 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         # devices than it requested (docs/ABI.md "Duplicate vGPUs").
         resp.envs["VGPU_DUPLICATE_MERGED"] = ",".join(dups)
         resp.annotations[ANN_DUPLICATES] = ",".join(dups)
-    host_per = cfg.host_memory_per_vgpu_bytes if hasattr(cfg, "host_memory_per_vgpu_bytes") else 0
+    host_per = getattr(cfg, "host_budget_bytes", -1)
+    if host_per is None or host_per < 0:
+        host_per = cfg.host_memory_per_vgpu_bytes if hasattr(cfg, "host_memory_per_vgpu_bytes") else 0
     if host_per:
         # Pinned host memory of the container (hipHostMalloc / hipHostRegister): one
         # budget per vGPU, summed (reference: class (b) host-alloc OOM checks).
@@ -299,6 +370,7 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
     resp.envs["VGPU_CU_MODE"] = cfg.cu_mode
 
     cache_name = f"{_uuid.uuid4()}.cache"
+    region_inode = 0
     if cfg.monitor_mode and pod_tag:
         from .k8s import POD_MARKER
         host_dir = os.path.join(cfg.vgpu_dir, SHARED_HOST_DIR, pod_tag)
@@ -311,8 +383,21 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
             write_devices(host_dir, kubelet_ids)
         resp.mounts.add(container_path=f"/{pod_tag}", host_path=host_dir, read_only=False)
         resp.envs["VGPU_SHARED_CACHE"] = f"/{pod_tag}/{cache_name}"
+        region, region_inode = create_region_file(host_dir, cache_name)
+        if region:
+            # The region itself is mounted over its path: the directory stays writable for
+            # the monitor's view, the file cannot be unlinked from inside the container.
+            resp.mounts.add(container_path=f"/{pod_tag}/{cache_name}", host_path=region, read_only=False)
     else:
-        resp.envs["VGPU_SHARED_CACHE"] = os.path.join(cfg.shared_cache_dir, cache_name)
+        regions = os.path.join(cfg.vgpu_dir, REGIONS_HOST_DIR)
+        region, region_inode = create_region_file(regions, cache_name)
+        if region:
+            _gc_dir(regions, ".cache", REGION_MAX_AGE_S)
+            resp.mounts.add(container_path=f"{CONTAINER_REGION_DIR}/{cache_name}", host_path=region,
+                            read_only=False)
+            resp.envs["VGPU_SHARED_CACHE"] = f"{CONTAINER_REGION_DIR}/{cache_name}"
+        else:
+            resp.envs["VGPU_SHARED_CACHE"] = os.path.join(cfg.shared_cache_dir, cache_name)
     if cfg.device_memory_scaling > 1:
         resp.envs["VGPU_OVERSUBSCRIBE"] = "true"
     # Device authorisation (reference: vgpuvalidator against the licensed device pool):
@@ -347,6 +432,19 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
     if os.path.isfile(lock_file):
         resp.mounts.add(container_path=f"{CONTAINER_LOCK_DIR}/{LOCK_FILE}", host_path=lock_file, read_only=True)
         resp.envs["VGPU_LOCK_FILE"] = f"{CONTAINER_LOCK_DIR}/{LOCK_FILE}"
+    # The ceiling: the contract's limits as written above, the region file's inode and the
+    # lowest priority class the container may take (the latency class only when granted).
+    envs = dict(resp.envs)
+    limits = {k: v for k, v in envs.items() if k.startswith(LIMIT_KEYS)}
+    if region_inode:
+        limits["VGPU_REGION_INODE"] = str(region_inode)
+    limits["VGPU_TASK_PRIORITY_MIN"] = "0" if latency or getattr(cfg, "allow_latency_class", False) else "1"
+    limits_file = write_limits(vdir, cache_name.rsplit(".", 1)[0], limits)
+    if limits_file:
+        resp.mounts.add(container_path=CONTAINER_LIMITS, host_path=limits_file, read_only=True)
+        resp.envs["VGPU_LIMITS_FILE"] = CONTAINER_LIMITS
+    if latency:
+        resp.envs.setdefault("VGPU_TASK_PRIORITY", "0")
     return resp
 
 

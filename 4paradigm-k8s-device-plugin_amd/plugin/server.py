@@ -44,7 +44,7 @@ class DevicePluginServer:
     """Serves one resource (``amd.com/gpu`` vGPUs, or one partition resource)."""
 
     def __init__(self, cfg, resource_name, socket_name, devices, backend=None, partition_resource=False,
-                 legacy=None, pod_matcher=None):
+                 legacy=None, pod_matcher=None, vdev_filter=None, latency=False):
         self.cfg = cfg
         self.resource_name = resource_name
         self.socket = os.path.join(cfg.device_plugin_path, socket_name)
@@ -53,6 +53,8 @@ class DevicePluginServer:
         self.partition_resource = partition_resource
         self.legacy = legacy
         self.pod_matcher = pod_matcher
+        self.vdev_filter = vdev_filter   # which of each GPU's vGPUs this resource serves (None = all)
+        self.latency = latency           # the latency resource: grants VGPU_TASK_PRIORITY=0
         self._cond = threading.Condition()
         # Allocate runs on the gRPC thread pool; with the legacy controller its
         # read-available / choose / acquire sequence must not interleave with another call's.
@@ -77,6 +79,8 @@ class DevicePluginServer:
         else:
             self.vdevices = device_to_vdevices(self.devices, self.cfg.device_split_count,
                                                self.cfg.device_memory_scaling, self.cfg.device_cores_scaling)
+            if self.vdev_filter is not None:
+                self.vdevices = [v for v in self.vdevices if self.vdev_filter(v)]
         self._by_uuid = {d.uuid: d for d in self.devices}
         self._stopped.clear()
 
@@ -335,7 +339,7 @@ class DevicePluginServer:
                                           using_ids=using, pod_tag=tags[i] if i < len(tags) else None,
                                           pod_uid=self.pod_matcher.owner(tags[i]) if (
                                               self.pod_matcher is not None and i < len(tags) and tags[i]) else None,
-                                          kubelet_ids=requested)
+                                          kubelet_ids=requested, latency=self.latency)
             resp.container_responses.append(cr)
             self.allocations.append((requested, using))
             if self.cfg.verbose > 5:

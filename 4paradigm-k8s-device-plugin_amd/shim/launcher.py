@@ -78,12 +78,32 @@ def apply_contract(contract_envs, mounts=(), base_env=None, preload=True, shim=N
                 v = h + v[len(c):]
                 break
         env[k] = v
+    limits = env.get("VGPU_LIMITS_FILE")
+    if limits and remap and os.path.isfile(limits):
+        # The limits file names container paths (the region); inside a container the mounts
+        # resolve them, here a copy with the host paths does.
+        env["VGPU_LIMITS_FILE"] = _emulated_limits(limits, remap)
     if preload:
         lib = shim or remap.get(CONTAINER_SHIM)
         if not lib or not os.path.exists(lib):
             lib = shim_path()
         _append_preload(env, lib)
     return env
+
+
+def _emulated_limits(path, remap):
+    out = []
+    for line in open(path).read().splitlines():
+        k, sep, v = line.partition("=")
+        for c, h in remap.items():
+            if sep and c != "/" and (v == c or v.startswith(c.rstrip("/") + "/")):
+                v = h + v[len(c):]
+                break
+        out.append(f"{k}{sep}{v}")
+    dst = path + ".emulated"
+    with open(dst, "w") as f:
+        f.write("\n".join(out) + "\n")
+    return dst
 
 
 def run(cmd, contract_envs, mounts=(), base_env=None, preload=True, **kw):

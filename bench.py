@@ -20,7 +20,7 @@ Modes, one fresh worker process each (the rank process itself never touches the 
            and with the GPU-time limiter once two or more other processes keep the GPU
            busy (the sweep's 4 and 8 pods). The line reports the enforcement used
            (``effective_cu_mode``, ``crowd``).   → ``value``
-* quota    the same pod with the compute limit disabled (VGPU_CU_POLICY=disable): the
+* quota    the same pod without a compute limit (the plugin at cores scaling = split): the
            shim's own overhead on stock PyTorch, the number the reference's vGPU column
            measured (its 50 % SM limit did not bind on TF).
 * parity   the reference's benchmark configuration: split 2, memory scaling 1.8
@@ -536,11 +536,16 @@ def main(argv=None):
         if mode == "native":
             results[mode] = run_one(args, mode, native_env(uuid, cpu), port)
         else:
-            split, scaling, extra = {"vgpu": (args.split, 1.0, None), "quota": (args.split, 1.0, {
-                "VGPU_CU_POLICY": "disable"}), "parity": (2, 1.8, None)}[mode]
-            with NodeHarness(backend, device_split_count=split, device_memory_scaling=scaling, **ledger_kw(args),
-                             cu_mode=args.cu_mode) as node:
-                env, contracts[mode] = pod_env(node, node.vgpu_ids(uuid)[:1], extra)
+            # quota: the split's memory quota with the compute share lifted by the plugin itself
+            # (cores scaling = split -> 100 %: no CU limit in the contract), so the number is the
+            # interception cost alone. parity: the reference's contract; --host-memory-fraction 0
+            # as the reference has no node bound on the host memory its spill may pin.
+            split, scaling, cores, extra_cfg = {
+                "vgpu": (args.split, 1.0, 1.0, {}), "quota": (args.split, 1.0, float(args.split), {}),
+                "parity": (2, 1.8, 1.0, {"host_memory_fraction": 0.0})}[mode]
+            with NodeHarness(backend, device_split_count=split, device_memory_scaling=scaling, device_cores_scaling=cores,
+                             **ledger_kw(args), **extra_cfg, cu_mode=args.cu_mode) as node:
+                env, contracts[mode] = pod_env(node, node.vgpu_ids(uuid)[:1], None)
                 applied[mode] = {k: env.get(k) for k in ("ROCR_VISIBLE_DEVICES", "VGPU_SHARED_CACHE", "VGPU_ALLOWLIST",
                                                          "VGPU_LOCK_FILE", "VGPU_DEVICE_MAP")}
                 applied[mode]["node_dir"] = node.dir

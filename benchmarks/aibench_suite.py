@@ -13,8 +13,9 @@ workloads are stock PyTorch-ROCm in fp32 (MIOpen / hipBLASLt kernels, no custom 
 
 Columns:
 * native     no shim, the GPU visible as the official plugin would expose it
-* vgpu       the pod's contract with the compute limit disabled (VGPU_CU_POLICY=disable):
-             the interception overhead alone — what the reference's vGPU column measured,
+* vgpu       the pod's contract without the compute limit (the same plugin at cores scaling 2,
+             i.e. a 100 % share: the tenant cannot lift its own limit any more, the plugin's
+             limits file is the ceiling): the interception overhead alone — what the reference's vGPU column measured,
              whose 50 % SM limit did not bind (its vGPU numbers match native)
 * vgpu-cu50  the contract exactly as emitted: 259 GiB oversubscribed quota (144 GiB of it
              HBM-resident), 128 of 256 CUs
@@ -116,10 +117,9 @@ def run_mode(mode, node, uuid, cases, steps, warmup):
     if mode == "native":
         env = dict(os.environ, ROCR_VISIBLE_DEVICES=uuid)
     else:
-        envs, mounts = node.pod(node.vgpu_ids(uuid)[:1])
+        n = node[mode] if isinstance(node, dict) else node
+        envs, mounts = n.pod(n.vgpu_ids(uuid)[:1])
         env = apply_contract(envs, mounts)
-        if mode == "vgpu":
-            env["VGPU_CU_POLICY"] = "disable"
     print(f"[{mode}]", flush=True)
     try:
         if subprocess.call(_cmd(cases, steps, warmup, out), env=env):
@@ -264,10 +264,14 @@ def main():
     print(f"GPU {dev.bdf}: workers pinned to {len(cpus)} NUMA-local CPUs" if cpus else "workers not pinned", flush=True)
     modes = a.modes.split(",")
     runs, vdm = [], {}
-    with NodeHarness(backend, device_split_count=2, device_memory_scaling=1.8) as node:
+    # The reference's DaemonSet (split 2, memory scaling 1.8; no node bound on host memory, as
+    # there), and the same at cores scaling 2 for the interception-only column.
+    ref = dict(device_split_count=2, device_memory_scaling=1.8, host_memory_fraction=0.0)
+    with NodeHarness(backend, **ref) as node, NodeHarness(backend, device_cores_scaling=2.0, **ref) as free:
+        nodes = {"native": node, "vgpu": free, "vgpu-cu50": node}
         for rep in range(a.repeats):
             order = modes if rep % 2 == 0 else modes[::-1]  # ABBA: cancels drift between runs
-            runs.append({m: run_mode(m, node, uuid, cases, a.steps, a.warmup) for m in order})
+            runs.append({m: run_mode(m, nodes, uuid, cases, a.steps, a.warmup) for m in order})
             if a.json_out:  # keep what is measured if a later step runs out of time
                 json.dump({"steps": a.steps, "warmup": a.warmup, "repeats": rep + 1, "partial": True, "runs": runs},
                           open(a.json_out, "w"), indent=1)

@@ -159,7 +159,8 @@ def ab_compare(a, pods, backend, uuid, split, prio):
     """ABAB runs of all pods together, without (A) and with (B) the priorities."""
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     runs = []
-    with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode) as node:
+    # The operator grants the latency class here (--allow-latency-class): the pods choose theirs.
+    with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode, allow_latency_class=True) as node:
         ids = node.vgpu_ids(uuid)[:len(pods)]
         arms = ([] if a.skip_default else [("default", None, None)]) + [("priority", prio, None)]
         for bg in a.bg_env:
@@ -250,7 +251,8 @@ def main():
            "solo": [], "solo_spatial": [], "together": None, "together_priority": None, "priorities": prio or None}
     if a.ab:
         return ab_compare(a, pods, backend, uuid, split, prio)
-    with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode) as node:
+    # The operator grants the latency class here (--allow-latency-class): the pods choose theirs.
+    with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode, allow_latency_class=True) as node:
         ids = node.vgpu_ids(uuid)[:len(pods)]
         for pod, vid in zip(pods, ids):
             t = time.time()

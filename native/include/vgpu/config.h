@@ -113,6 +113,14 @@ struct Config {
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
   uint64_t host_mem_limit = 0;           // VGPU_HOST_MEMORY_LIMIT: pinned host memory, 0 = unlimited
   bool fail_open = false;                // VGPU_FAIL_OPEN: run unlimited when the region cannot be attached
+  std::string device_map;                // VGPU_DEVICE_MAP ("<i>:<uuid> ...")
+  std::string allowlist;                 // VGPU_ALLOWLIST: authorised GPU UUIDs, one per line ("" = no check)
+  // Plugin-owned ceilings (limits file, see load_ceiling): the lowest task priority class the
+  // container may take (VGPU_TASK_PRIORITY_MIN; 0 = latency class allowed) and the inode
+  // of the region file the plugin created for it (VGPU_REGION_INODE, 0 = not checked).
+  int min_priority = -1000;
+  uint64_t region_inode = 0;
+  bool ceiling = false;                  // a limits file was applied
 
   bool any_memory_limit() const;
   bool any_cu_limit() const;
@@ -136,6 +144,23 @@ void load_config(Config* cfg, GetenvFn getenv_fn = nullptr);
 // KEY=VALUE lines applied with setenv(…, overwrite=1) before the config is parsed
 // (reference: nvml_preInit → load_env_from_file("/overrideEnv")).
 int apply_override_env_file(const char* path);
+
+// Plugin-owned limits (tamper resistance). The reference's limits come from container env
+// and from a region the tenant maps read-write, and its set_current_device_memory_limit
+// raises them from inside the container ([multiprocess_memory_limit.c:806-808]): a tenant
+// can give itself more. Here the plugin also writes the container's contract into a limits
+// file it owns, mounted read-only at kLimitsPath (docs/ABI.md). The shim treats it as the
+// ceiling: the environment may only lower what it grants, and the device map, region path,
+// compute-limit mode, oversubscription and the lowest priority class come from it.
+constexpr const char* kLimitsPath = "/vgpu/limits";
+// Parses a limits file (KEY=VALUE lines, the VGPU_* env names) into `out` (load_config
+// semantics). False when it cannot be read.
+bool load_ceiling(const char* path, Config* out);
+// Clamps `cfg` (from the environment) to `ceil`.
+void apply_ceiling(Config* cfg, const Config& ceil);
+// Whether a limits file is present (kLimitsPath, or $VGPU_LIMITS_FILE): diagnostics
+// switches that would turn enforcement off are then ignored.
+bool ceiling_present();
 
 // The process-wide config (filled by shim init).
 const Config& config();

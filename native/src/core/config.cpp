@@ -6,6 +6,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include <unistd.h>
 
 #include "vgpu/log.h"
 
@@ -312,6 +317,94 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   }
   long merge = 1;
   if (parse_int(getenv_fn("VGPU_DUPLICATE_MERGE"), 0, 1, &merge)) cfg->duplicate_merge = (int)merge;
+  if (const char* s = getenv_fn("VGPU_DEVICE_MAP")) cfg->device_map = s;
+  if (const char* s = getenv_fn("VGPU_ALLOWLIST")) cfg->allowlist = s;
+  long minp = 0;
+  if (parse_int(getenv_fn("VGPU_TASK_PRIORITY_MIN"), -1000, 1000, &minp)) cfg->min_priority = (int)minp;
+  if (const char* s = getenv_fn("VGPU_REGION_INODE")) cfg->region_inode = strtoull(s, nullptr, 10);
+}
+
+namespace {
+// The limits file being parsed (load_config takes a plain function pointer).
+const std::vector<std::pair<std::string, std::string>>* g_ceiling_kv = nullptr;
+const char* ceiling_getenv(const char* key) {
+  if (!g_ceiling_kv) return nullptr;
+  for (const auto& kv : *g_ceiling_kv)
+    if (kv.first == key) return kv.second.c_str();
+  return nullptr;
+}
+
+uint64_t min_limit(uint64_t want, uint64_t ceil) {  // 0 = unlimited on either side
+  if (!ceil) return want;
+  return want && want < ceil ? want : ceil;
+}
+}  // namespace
+
+bool load_ceiling(const char* path, Config* out) {
+  FILE* f = path && *path ? fopen(path, "r") : nullptr;
+  if (!f) return false;
+  std::vector<std::pair<std::string, std::string>> kv;
+  char line[1024];
+  while (fgets(line, sizeof(line), f)) {
+    size_t len = strlen(line);
+    while (len && (line[len - 1] == '\n' || line[len - 1] == '\r')) line[--len] = 0;
+    char* p = line;
+    while (*p == ' ' || *p == '\t') p++;
+    if (!*p || *p == '#') continue;
+    char* eq = strchr(p, '=');
+    if (!eq || eq == p) continue;
+    *eq = 0;
+    kv.emplace_back(p, eq + 1);
+  }
+  fclose(f);
+  g_ceiling_kv = &kv;
+  load_config(out, ceiling_getenv);
+  g_ceiling_kv = nullptr;
+  // A limits file without a class floor still keeps the tenant out of the latency class:
+  // only the plugin grants it (VGPU_TASK_PRIORITY_MIN=0).
+  if (out->min_priority == -1000) out->min_priority = 1;
+  out->ceiling = true;
+  return true;
+}
+
+void apply_ceiling(Config* cfg, const Config& ceil) {
+  for (int i = 0; i < kMaxDevices; i++) {
+    DeviceConfig& d = cfg->dev[i];
+    const DeviceConfig& c = ceil.dev[i];
+    d.mem_limit = min_limit(d.mem_limit, c.mem_limit);
+    d.hbm_limit = min_limit(d.hbm_limit, c.hbm_limit);
+    if (c.cu_limit_pct > 0 && c.cu_limit_pct < 100) {
+      const bool unlimited = d.cu_limit_pct <= 0 || d.cu_limit_pct >= 100;
+      d.cu_limit_pct = unlimited || d.cu_limit_pct > c.cu_limit_pct ? c.cu_limit_pct : d.cu_limit_pct;
+      d.cu_share_bp = c.cu_share_bp && (!d.cu_share_bp || d.cu_share_bp > c.cu_share_bp) ? c.cu_share_bp : d.cu_share_bp;
+      // The CUs are the plugin's choice (disjoint slices per vGPU), not the tenant's.
+      d.cu_range_begin = c.cu_range_begin;
+      d.cu_range_end = c.cu_range_end;
+    }
+  }
+  if (ceil.num_devices > cfg->num_devices) cfg->num_devices = ceil.num_devices;
+  cfg->host_mem_limit = min_limit(cfg->host_mem_limit, ceil.host_mem_limit);
+  // Where the container's accounting lives and which GPU each vGPU index names: one region
+  // and one map for every process of the container, whatever a process's environment says.
+  cfg->shared_cache = ceil.shared_cache;
+  if (!ceil.device_map.empty()) cfg->device_map = ceil.device_map;
+  if (!ceil.allowlist.empty()) cfg->allowlist = ceil.allowlist;
+  cfg->cu_mode = ceil.cu_mode;
+  cfg->oversubscribe = cfg->oversubscribe && ceil.oversubscribe;
+  if (ceil.min_priority > cfg->min_priority) cfg->min_priority = ceil.min_priority;
+  if (cfg->priority < cfg->min_priority) cfg->priority = cfg->min_priority;
+  if (ceil.region_inode) cfg->region_inode = ceil.region_inode;
+  // Switches that would lift enforcement are the operator's, not the tenant's.
+  cfg->disabled = false;
+  cfg->fail_open = false;
+  if (cfg->cu_policy == CuPolicy::kDisable) cfg->cu_policy = CuPolicy::kDefault;
+  cfg->ceiling = true;
+}
+
+bool ceiling_present() {
+  if (access(kLimitsPath, R_OK) == 0) return true;
+  const char* p = getenv("VGPU_LIMITS_FILE");
+  return p && *p && access(p, R_OK) == 0;
 }
 
 const Config& config() { return g_config; }

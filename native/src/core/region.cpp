@@ -11,6 +11,7 @@
 #include <sys/file.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -208,6 +209,15 @@ void SharedRegion::init_fresh(const Config* cfg) {
     }
   }
   r_->hdr.num_devices = n;
+  {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    uint64_t e = ((uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec) ^ ((uint64_t)getpid() << 40) ^
+                 (uint64_t)(uintptr_t)this;
+    e ^= e >> 29;
+    e *= 0xbf58476d1ce4e5b9ull;
+    r_->hdr.epoch = e ^ (e >> 32);
+  }
   r_->hdr.initialized.store(1);
   std::atomic_thread_fence(std::memory_order_release);
   r_->hdr.magic = kRegionMagic;  // published last
@@ -371,10 +381,17 @@ int SharedRegion::reclaim_dead() {
   return n;
 }
 
+namespace {
+uint64_t lower_limit(uint64_t lim, uint64_t ceil) {  // 0 = unlimited on either side
+  if (!ceil) return lim;
+  return lim && lim < ceil ? lim : ceil;
+}
+}  // namespace
+
 Charge SharedRegion::charge(int slot, int dev, uint64_t bytes, MemKind kind) {
   DeviceState& d = r_->dev[dev];
   for (int attempt = 0; attempt < 2; attempt++) {
-    uint64_t lim = d.mem_limit;
+    uint64_t lim = lower_limit(d.mem_limit, ceil_mem_[dev]);
     uint64_t cur = d.used.load(std::memory_order_relaxed);
     bool admitted = false;
     while (true) {
@@ -433,7 +450,7 @@ void SharedRegion::uncharge(int slot, int dev, uint64_t bytes, MemKind kind) {
 }
 
 uint64_t SharedRegion::usage(int dev) const { return r_->dev[dev].used.load(std::memory_order_relaxed); }
-uint64_t SharedRegion::limit(int dev) const { return r_->dev[dev].mem_limit; }
+uint64_t SharedRegion::limit(int dev) const { return lower_limit(r_->dev[dev].mem_limit, ceil_mem_[dev]); }
 uint64_t SharedRegion::hbm_limit(int dev) const { return r_->dev[dev].hbm_limit; }
 uint64_t SharedRegion::resident(int dev) const {
   uint64_t u = r_->dev[dev].used.load(std::memory_order_relaxed);
@@ -445,7 +462,7 @@ uint64_t SharedRegion::proc_usage(int slot, int dev) const { return r_->procs[sl
 Charge SharedRegion::charge_host(int slot, uint64_t bytes) {
   RegionHeader& h = r_->hdr;
   for (int attempt = 0; attempt < 2; attempt++) {
-    const uint64_t lim = h.host_limit;
+    const uint64_t lim = lower_limit(h.host_limit, ceil_host_);
     uint64_t cur = h.host_used.load(std::memory_order_relaxed);
     bool admitted = false;
     while (true) {
@@ -487,14 +504,47 @@ void SharedRegion::uncharge_host(int slot, uint64_t bytes) {
 }
 
 uint64_t SharedRegion::host_usage() const { return r_->hdr.host_used.load(std::memory_order_relaxed); }
-uint64_t SharedRegion::host_limit() const { return r_->hdr.host_limit; }
+uint64_t SharedRegion::host_limit() const { return lower_limit(r_->hdr.host_limit, ceil_host_); }
 void SharedRegion::set_host_limit(uint64_t bytes) {
-  r_->hdr.host_limit = bytes;
+  r_->hdr.host_limit = lower_limit(bytes, ceil_host_);
   r_->hdr.generation.fetch_add(1);
 }
 
+void SharedRegion::set_ceiling(int dev, uint64_t mem_bytes) {
+  if (dev >= 0 && dev < kMaxDevices) ceil_mem_[dev] = mem_bytes;
+}
+
+void SharedRegion::set_host_ceiling(uint64_t bytes) { ceil_host_ = bytes; }
+
+uint64_t SharedRegion::inode() const {
+  if (fd_ < 0) return 0;
+  struct stat st;
+  // By system call: fstat is a GLIBC_2.33 symbol (glibc_compat.h).
+  if (syscall(SYS_fstat, fd_, &st) != 0) return 0;
+  return (uint64_t)st.st_ino;
+}
+
+void SharedRegion::touch() {
+  if (fd_ >= 0) (void)futimens(fd_, nullptr);
+}
+
+bool SharedRegion::reinit_if_invalid(const Config* cfg) {
+  if (!r_ || fd_ < 0) return false;
+  if (r_->hdr.magic == kRegionMagic && r_->hdr.version == kRegionVersion && r_->hdr.region_size == sizeof(Region))
+    return false;
+  if (flock(fd_, LOCK_EX) != 0) return false;
+  bool done = false;
+  if (r_->hdr.magic != kRegionMagic || r_->hdr.version != kRegionVersion || r_->hdr.region_size != sizeof(Region)) {
+    VLOG_ERROR("shared region %s was overwritten; re-initialising it", path_);
+    init_fresh(cfg);
+    done = true;
+  }
+  flock(fd_, LOCK_UN);
+  return done;
+}
+
 void SharedRegion::set_limit(int dev, uint64_t bytes) {
-  r_->dev[dev].mem_limit = bytes;
+  r_->dev[dev].mem_limit = lower_limit(bytes, ceil_mem_[dev]);
   if (dev >= r_->hdr.num_devices) r_->hdr.num_devices = dev + 1;
   r_->hdr.generation.fetch_add(1);
 }

@@ -52,18 +52,31 @@ bool take_alloc(uintptr_t key, AllocRec* out) {
 
 // Host spill for virtual device memory: serve an allocation the HBM cannot hold
 // from pinned host memory reachable by the GPU.
+// Spilled bytes are pinned host memory: they count against the container's host budget
+// too (VGPU_HOST_MEMORY_LIMIT, shared with hipHostMalloc / hipHostRegister), so the RAM an
+// oversubscribed vGPU pins is bounded like any other pinned memory (plugin/host_memory.py
+// sizes the budget and refuses scalings the node cannot back).
 hsa_status_t spill_allocate(int dev, size_t size, void** ptr) {
   ShimState& s = shim();
   AgentInfo& a = s.agents[dev];
   if (!a.spill_pool.handle) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  if (s.region.charge_host(s.slot, size) != Charge::kOk) {
+    VLOG_WARN("device %d: %zu bytes cannot spill: host memory budget %lu (pinned %lu) is used up", dev, size,
+              (unsigned long)s.region.host_limit(), (unsigned long)s.region.host_usage());
+    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  }
   VGPU_REAL_HSA(hsa_amd_memory_pool_allocate);
   VGPU_REAL_HSA(hsa_amd_agents_allow_access);
   VGPU_REAL_HSA(hsa_amd_memory_pool_free);
   hsa_status_t st = real_hsa_amd_memory_pool_allocate(a.spill_pool, size, 0, ptr);
-  if (st != HSA_STATUS_SUCCESS) return st;
+  if (st != HSA_STATUS_SUCCESS) {
+    s.region.uncharge_host(s.slot, size);
+    return st;
+  }
   st = real_hsa_amd_agents_allow_access(1, &a.agent, nullptr, *ptr);
   if (st != HSA_STATUS_SUCCESS) {
     real_hsa_amd_memory_pool_free(*ptr);
+    s.region.uncharge_host(s.slot, size);
     *ptr = nullptr;
     return st;
   }
@@ -169,6 +182,13 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
       record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemSpill);
       return st;
     }
+    // No host memory for it: within the HBM share (an early, large-first spill) the
+    // allocation may stay in HBM; past the share it is refused - the rest of the HBM
+    // belongs to the other tenants of the GPU.
+    if (s.region.resident(dev) > s.region.hbm_limit(dev)) {
+      s.region.uncharge(s.slot, dev, size, kMemData);
+      return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+    }
   }
   st = real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
   if (st == HSA_STATUS_SUCCESS) {
@@ -196,8 +216,10 @@ hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
   ShimState& s = shim();
   if (ptr && s.phase.load(std::memory_order_relaxed) == 2) {
     AllocRec rec;
-    if (take_alloc(reinterpret_cast<uintptr_t>(ptr), &rec) && s.slot >= 0 && !s.exiting.load())
+    if (take_alloc(reinterpret_cast<uintptr_t>(ptr), &rec) && s.slot >= 0 && !s.exiting.load()) {
       s.region.uncharge(s.slot, rec.dev, rec.size, (MemKind)rec.kind);
+      if (rec.kind == kMemSpill) s.region.uncharge_host(s.slot, rec.size);
+    }
   }
   return real_hsa_amd_memory_pool_free(ptr);
 }
@@ -372,7 +394,7 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
   // Task priority (reference CUDA_TASK_PRIORITY, only stored there) becomes the hardware
   // queue priority: 0 = high (e.g. latency-critical inference next to batch jobs),
   // 1 = normal (default), >= 2 = low. Read from the region so an operator can change it.
-  int prio = s.region.raw()->hdr.priority.load(std::memory_order_relaxed);
+  int prio = effective_priority(s.region.raw());
   if (prio != 1) {
     VGPU_REAL_HSA(hsa_amd_queue_set_priority);
     hsa_amd_queue_priority_t qp = prio <= 0 ? HSA_AMD_QUEUE_PRIORITY_HIGH : HSA_AMD_QUEUE_PRIORITY_LOW;

@@ -229,14 +229,104 @@ void load_env_config() {
     return;
   }
   log_init_from_env();
-  // Alternate KFD process tree (the CPU-only fake runtime of the test suite).
+  // Alternate KFD process tree (the CPU-only fake runtime of the test suite). Not in a real
+  // container (the plugin's limits file mounted): a tenant's fake occupancy / VRAM files
+  // would steer its own charges.
   if (const char* k = getenv("VGPU_KFD_ROOT"))
-    if (*k) g_kfd_proc_root = strdup(k);
+    if (*k && access(kLimitsPath, F_OK) != 0) g_kfd_proc_root = strdup(k);
   const char* ovr = getenv("VGPU_OVERRIDE_ENV_FILE");
   int n = apply_override_env_file(ovr && *ovr ? ovr : "/vgpu/override.env");
   if (n) log_init_from_env();
-  load_config(&mutable_config());
+  Config& cfg = mutable_config();
+  load_config(&cfg);
   if (n) VLOG_INFO("applied %d override env entries", n);
+  // The plugin's ceilings: its read-only limits file at the fixed container path and, for
+  // runs without a container runtime (tests, the bench's emulated pods), the one named by
+  // VGPU_LIMITS_FILE. Each only lowers what the environment asks for.
+  const char* extra = getenv("VGPU_LIMITS_FILE");
+  const char* paths[2] = {kLimitsPath, extra && *extra && strcmp(extra, kLimitsPath) != 0 ? extra : nullptr};
+  for (const char* p : paths) {
+    if (!p) continue;
+    Config ceil;
+    if (!load_ceiling(p, &ceil)) {
+      if (p == extra) VLOG_WARN("VGPU_LIMITS_FILE=%s is not readable", p);
+      continue;
+    }
+    apply_ceiling(&cfg, ceil);
+    shim().has_ceiling = true;
+    VLOG_INFO("limits file %s applied (priority class floor %d)", p, ceil.min_priority);
+  }
+}
+
+// Resolves the plugin's per-vGPU ceilings onto the agents (same map as the config) and
+// installs them in the region handle and the agents.
+void install_ceilings(const char* const* uuid_ptrs) {
+  ShimState& s = shim();
+  if (!s.has_ceiling) return;
+  // The ceiling equals the clamped config: apply_ceiling took the map, and every per-device
+  // limit is at most the file's; the file's own values are re-read for the mask.
+  const char* extra = getenv("VGPU_LIMITS_FILE");
+  Config ceil;
+  if (!load_ceiling(kLimitsPath, &ceil) && !(extra && *extra && load_ceiling(extra, &ceil))) return;
+  if (extra && *extra && strcmp(extra, kLimitsPath) != 0 && ceil.ceiling) {
+    Config second;
+    if (load_ceiling(extra, &second)) apply_ceiling(&ceil, second);
+  }
+  DeviceMap map;
+  if (!parse_device_map(config().device_map.c_str(), &map)) map = DeviceMap();
+  DeviceConfig per[kMaxDevices];
+  resolve_devices(ceil, map, uuid_ptrs, s.n_agents, per);
+  s.region.set_host_ceiling(ceil.host_mem_limit);
+  for (int i = 0; i < s.n_agents; i++) {
+    AgentInfo& a = s.agents[i];
+    // A device the map does not give this container gets nothing (it is unauthorised too).
+    s.region.set_ceiling(i, per[i].unmapped ? 1 : per[i].mem_limit);
+    const int pct = per[i].cu_limit_pct;
+    if (pct > 0 && pct < 100) {
+      a.ceil_pct = pct;
+      const char* layout = getenv("VGPU_CU_LAYOUT");
+      a.ceil_mask = cu_mask_for(a.cu_count, a.num_xcc, pct, per[i].cu_range_begin, per[i].cu_range_end,
+                                (layout && !strcasecmp(layout, "interleave")) ? 1 : a.num_se);
+    }
+  }
+}
+
+// Fills the region's per-device state from the resolved config where no process of the
+// container has yet (d.configured == 0). Called with the region lock held.
+void configure_devices(Region* r, const DeviceConfig* per_agent) {
+  ShimState& s = shim();
+  if (r->hdr.num_devices < s.n_agents) r->hdr.num_devices = s.n_agents;
+  for (int i = 0; i < s.n_agents; i++) {
+    AgentInfo& a = s.agents[i];
+    DeviceState& d = r->dev[i];
+    if (d.configured) continue;
+    snprintf(d.uuid, sizeof(d.uuid), "%.63s", a.uuid);  // UUIDs are "GPU-" + 16 hex digits
+    d.phys_total = a.phys_total;
+    d.cu_count = a.cu_count;
+    d.num_xcc = a.num_xcc;
+    d.gpu_id = a.gpu_id;
+    VGPU_REAL_HSA(hsa_agent_get_info);
+    uint32_t bdf = 0, dom = 0;
+    real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+    real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+    d.bdf = bdf;
+    d.domain = dom;
+    if (!d.mem_limit && per_agent[i].mem_limit) d.mem_limit = per_agent[i].mem_limit;
+    if (!d.hbm_limit && per_agent[i].hbm_limit) d.hbm_limit = per_agent[i].hbm_limit;
+    if (!d.cu_limit_pct && per_agent[i].cu_limit_pct) d.cu_limit_pct = per_agent[i].cu_limit_pct;
+    if (d.cu_range_begin < 0 && per_agent[i].cu_range_begin >= 0) {
+      d.cu_range_begin = per_agent[i].cu_range_begin;
+      d.cu_range_end = per_agent[i].cu_range_end;
+    }
+    const char* layout = getenv("VGPU_CU_LAYOUT");  // "se" (default) | "interleave"
+    d.num_se = (layout && !strcasecmp(layout, "interleave")) ? 1 : a.num_se;
+    CuMask m = cu_mask_for(a.cu_count, a.num_xcc, d.cu_limit_pct, d.cu_range_begin, d.cu_range_end, d.num_se);
+    memcpy(d.cu_mask, m.words, sizeof(d.cu_mask));
+    d.cu_mask_bits = m.nbits;
+    d.credit_ns.store(timeshare_params(d.cu_limit_pct, config().limiter_window_ms, d.cu_share_bp).burst_ns);
+    d.gate_open.store(1);
+    d.configured = 1;
+  }
 }
 
 }  // namespace
@@ -310,16 +400,18 @@ void shim_init_after_hsa() {
     uuids[i][63] = 0;
     uuid_ptrs[i] = uuids[i];
   }
+  for (int i = 0; i < s.n_agents; i++) memcpy(s.agents[i].uuid, uuids[i], sizeof(s.agents[i].uuid));
   DeviceMap map;
-  const char* map_env = getenv("VGPU_DEVICE_MAP");
+  const char* map_env = cfg.device_map.empty() ? nullptr : cfg.device_map.c_str();
   if (!parse_device_map(map_env, &map)) {
     VLOG_WARN("invalid VGPU_DEVICE_MAP=%s, using positional limits", map_env);
     map = DeviceMap();
   }
   // Device authorisation (reference: vgpuvalidator, dormant there): with VGPU_ALLOWLIST
   // set, GPUs whose ROCr UUID is not listed get no device memory at all.
-  if (const char* al = getenv("VGPU_ALLOWLIST")) {
-    if (FILE* f = *al ? fopen(al, "r") : nullptr) {
+  if (!cfg.allowlist.empty()) {
+    const char* al = cfg.allowlist.c_str();
+    if (FILE* f = fopen(al, "r")) {
       std::vector<std::string> allowed;
       char line[128];
       while (fgets(line, sizeof(line), f)) {
@@ -354,6 +446,8 @@ void shim_init_after_hsa() {
   // inside one the VRAM signature resolves it (the maintenance thread retries).
   if (!s.hostpid) s.hostpid = resolve_hostpid(2000);
 
+  install_ceilings(uuid_ptrs);
+  s.resolved = resolved;
   int rc = s.region.attach(cfg.shared_cache.c_str(), &resolved, true);
   if (rc == -ENOENT) {
     // The region's directory is missing (e.g. a monitor-mode host directory removed under
@@ -363,11 +457,19 @@ void shim_init_after_hsa() {
       if (i == dir.size() || dir[i] == '/') mkdir(dir.substr(0, i).c_str(), 0755);
     rc = s.region.attach(cfg.shared_cache.c_str(), &resolved, true);
   }
+  if (rc == 0 && cfg.region_inode && s.region.inode() != cfg.region_inode) {
+    // Not the region file the plugin created for this container (deleted and re-created,
+    // or the path pointed elsewhere): its accounting is not the container's.
+    VLOG_ERROR("shared region %s is not the plugin's (inode %lu, expected %lu)", cfg.shared_cache.c_str(),
+               (unsigned long)s.region.inode(), (unsigned long)cfg.region_inode);
+    s.region.detach();
+    rc = -EPERM;
+  }
   if (rc != 0) {
     // Without the region there is no shared accounting. With limits configured the shim
     // fails closed - no device memory - rather than letting the container run unlimited
     // (VGPU_FAIL_OPEN=1 restores the pass-through).
-    s.fail_closed = !cfg.fail_open && (cfg.any_memory_limit() || cfg.any_cu_limit());
+    s.fail_closed = !cfg.fail_open && (cfg.any_memory_limit() || cfg.any_cu_limit() || s.has_ceiling);
     VLOG_ERROR("cannot attach shared region %s (%s); %s", cfg.shared_cache.c_str(), strerror(-rc),
                s.fail_closed ? "device memory is refused (fail closed)" : "limits are NOT enforced");
     s.phase.store(3);
@@ -375,43 +477,13 @@ void shim_init_after_hsa() {
   }
   Region* r = s.region.raw();
   s.region.lock();
-  if (r->hdr.num_devices < s.n_agents) r->hdr.num_devices = s.n_agents;
-  for (int i = 0; i < s.n_agents; i++) {
-    AgentInfo& a = s.agents[i];
-    DeviceState& d = r->dev[i];
-    if (!d.configured) {
-      snprintf(d.uuid, sizeof(d.uuid), "%.63s", uuids[i]);  // UUIDs are "GPU-" + 16 hex digits
-      d.phys_total = a.phys_total;
-      d.cu_count = a.cu_count;
-      d.num_xcc = a.num_xcc;
-      d.gpu_id = a.gpu_id;
-      VGPU_REAL_HSA(hsa_agent_get_info);
-      uint32_t bdf = 0, dom = 0;
-      real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
-      real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
-      d.bdf = bdf;
-      d.domain = dom;
-      if (!d.mem_limit && per_agent[i].mem_limit) d.mem_limit = per_agent[i].mem_limit;
-      if (!d.hbm_limit && per_agent[i].hbm_limit) d.hbm_limit = per_agent[i].hbm_limit;
-      if (!d.cu_limit_pct && per_agent[i].cu_limit_pct) d.cu_limit_pct = per_agent[i].cu_limit_pct;
-      if (d.cu_range_begin < 0 && per_agent[i].cu_range_begin >= 0) {
-        d.cu_range_begin = per_agent[i].cu_range_begin;
-        d.cu_range_end = per_agent[i].cu_range_end;
-      }
-      const char* layout = getenv("VGPU_CU_LAYOUT");  // "se" (default) | "interleave"
-      d.num_se = (layout && !strcasecmp(layout, "interleave")) ? 1 : a.num_se;
-      CuMask m = cu_mask_for(a.cu_count, a.num_xcc, d.cu_limit_pct, d.cu_range_begin, d.cu_range_end, d.num_se);
-      memcpy(d.cu_mask, m.words, sizeof(d.cu_mask));
-      d.cu_mask_bits = m.nbits;
-      d.credit_ns.store(timeshare_params(d.cu_limit_pct, config().limiter_window_ms, d.cu_share_bp).burst_ns);
-      d.gate_open.store(1);
-      d.configured = 1;
-    }
-  }
+  configure_devices(r, per_agent);
   s.region.unlock();
+  clamp_region_to_ceiling();
   s.seen_generation.store(r->hdr.generation.load() - 1);  // forces the first apply below
   apply_live_config();
 
+  s.epoch = r->hdr.epoch;
   s.slot = s.region.register_process(s.pid, s.hostpid, cfg.priority);
   s.active = s.slot >= 0;
   if (cfg.signal_control) {
@@ -466,12 +538,103 @@ pid_t resolve_hostpid(int lock_timeout_ms) {
   return std::binary_search(pids.begin(), pids.end(), (int)getpid()) ? getpid() : 0;
 }
 
+bool clamp_region_to_ceiling() {
+  ShimState& s = shim();
+  if (!s.has_ceiling || !s.region.attached()) return false;
+  Region* r = s.region.raw();
+  bool clamped = false;
+  const bool locked = s.region.lock_for(kLockTimeoutMs);
+  for (int i = 0; i < s.n_agents; i++) {
+    AgentInfo& a = s.agents[i];
+    DeviceState& d = r->dev[i];
+    const uint64_t cm = s.region.ceiling(i);
+    if (cm && (!d.mem_limit || d.mem_limit > cm)) {
+      VLOG_WARN("device %d: region memory limit %lu above the plugin's %lu; clamped", i, (unsigned long)d.mem_limit,
+                (unsigned long)cm);
+      d.mem_limit = cm;
+      clamped = true;
+    }
+    if (a.ceil_pct > 0) {
+      if (d.cu_limit_pct <= 0 || d.cu_limit_pct >= 100 || d.cu_limit_pct > a.ceil_pct) {
+        VLOG_WARN("device %d: region CU limit %d%% above the plugin's %d%%; clamped", i, d.cu_limit_pct, a.ceil_pct);
+        d.cu_limit_pct = a.ceil_pct;
+        clamped = true;
+      }
+      // The slice may be narrowed live (set_cu_limit), never moved onto other CUs or widened.
+      CuMask m;
+      memcpy(m.words, d.cu_mask, sizeof(m.words));
+      m.nbits = d.cu_mask_bits ? d.cu_mask_bits : a.cu_count;
+      bool subset = m.count() > 0;
+      for (int w = 0; w < kCuMaskWords && subset; w++) subset = (m.words[w] & ~a.ceil_mask.words[w]) == 0;
+      if (!subset) {
+        VLOG_WARN("device %d: region CU mask outside the plugin's slice; reset to it", i);
+        memcpy(d.cu_mask, a.ceil_mask.words, sizeof(d.cu_mask));
+        d.cu_mask_bits = a.ceil_mask.nbits;
+        clamped = true;
+      }
+    }
+  }
+  const Config& cfg = config();
+  if (cfg.host_mem_limit && (!r->hdr.host_limit || r->hdr.host_limit > cfg.host_mem_limit)) {
+    r->hdr.host_limit = cfg.host_mem_limit;
+    clamped = true;
+  }
+  if (r->hdr.priority.load(std::memory_order_relaxed) < cfg.min_priority) {
+    r->hdr.priority.store(cfg.min_priority, std::memory_order_relaxed);
+    clamped = true;
+  }
+  if (locked) s.region.unlock();
+  return clamped;
+}
+
+void check_region_epoch() {
+  ShimState& s = shim();
+  if (!s.active || !s.region.attached() || s.exiting.load()) return;
+  Region* r = s.region.raw();
+  const bool reinit = s.region.reinit_if_invalid(&s.resolved);
+  const bool moved = r->hdr.epoch != s.epoch;
+  const bool lost = s.slot < 0 || r->procs[s.slot].pid.load(std::memory_order_relaxed) != s.pid;
+  if (!reinit && !moved && !lost) return;
+  VLOG_ERROR("shared region %s lost this process's slot (%s); registering and charging %s again",
+             s.region.path(), reinit ? "overwritten" : moved ? "re-initialised" : "slot cleared", "its allocations");
+  if (reinit || moved) {
+    s.region.lock();
+    DeviceConfig per_agent[kMaxDevices];
+    for (int i = 0; i < kMaxDevices; i++) per_agent[i] = s.resolved.dev[i];
+    configure_devices(r, per_agent);
+    s.region.unlock();
+    clamp_region_to_ceiling();
+  }
+  s.epoch = r->hdr.epoch;
+  const int slot = s.region.register_process(s.pid, s.hostpid, config().priority);
+  if (slot < 0) return;
+  s.slot = slot;
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    uint64_t host = 0;
+    for (const auto& kv : s.allocs) {
+      s.region.force_charge(slot, kv.second.dev, kv.second.size, (MemKind)kv.second.kind);
+      if (kv.second.kind == kMemSpill) host += kv.second.size;  // spills are pinned host memory too
+    }
+    for (const auto& kv : s.vmem) s.region.force_charge(slot, kv.second.dev, kv.second.size, kMemData);
+    for (const auto& kv : s.managed) s.region.force_charge(slot, kv.second.dev, kv.second.size, kMemData);
+    for (const auto& kv : s.host) host += kv.second;
+    if (host) {
+      r->hdr.host_used.fetch_add(host);
+      r->procs[slot].host_used.fetch_add(host);
+    }
+  }
+  resync_context_charge();
+  r->hdr.generation.fetch_add(1, std::memory_order_acq_rel);  // every process re-applies its masks
+}
+
 void apply_live_config() {
   ShimState& s = shim();
   std::lock_guard<std::mutex> g(s.live_mu);
   Region* r = s.region.raw();
   const uint64_t gen = r->hdr.generation.load(std::memory_order_acquire);
   if (gen == s.seen_generation.load()) return;
+  clamp_region_to_ceiling();
   const Config& cfg = config();
   const bool force = cfg.cu_policy == CuPolicy::kForce, off = cfg.cu_policy == CuPolicy::kDisable;
   for (int i = 0; i < s.n_agents; i++) {
@@ -488,7 +651,7 @@ void apply_live_config() {
     const bool ranged = d.cu_range_begin >= 0;
     if (locked) s.region.unlock();
     const bool limited = pct > 0 && pct < 100;
-    const int prio = r->hdr.priority.load(std::memory_order_relaxed);
+    const int prio = effective_priority(r);
     const CuMode mode = effective_cu_mode_prio(cfg.cu_mode, pct, d.crowd.load(std::memory_order_relaxed), prio);
     const bool spatial = mode == CuMode::kSpatial || mode == CuMode::kBoth;
     const bool temporal = mode == CuMode::kTemporal || mode == CuMode::kBoth;

@@ -40,6 +40,11 @@ struct AgentInfo {
   std::atomic<bool> temporal_active{false};  // GPU-time credit gates its launches
   CuMode mode = CuMode::kOff;                // effective enforcement mode
   CuMask mask;
+  char uuid[64] = {0};                       // ROCr UUID ("GPU-...")
+  // Plugin ceiling (limits file) for this agent: its CU share and slice; the region's may
+  // only be narrower (0 = no ceiling).
+  int ceil_pct = 0;
+  CuMask ceil_mask;
   hsa_amd_memory_pool_t pools[kMaxAgentPools]{};  // GPU-local global pools (and regions) of this agent
   hsa_amd_memory_pool_t vram_pool{0};  // coarse-grained VRAM pool (host-PID probe allocations)
   int n_pools = 0;
@@ -77,6 +82,9 @@ struct ShimState {
   std::mutex live_mu;                               // serialises live reconfiguration
   std::mutex ctx_mu;                                // serialises resync_context_charge
   std::atomic<void*> board_slot{nullptr};           // this process's mapping of the board slot (lease holder)
+  Config resolved;                                  // per-agent config the region is (re-)initialised from
+  uint64_t epoch = 0;                               // region epoch this process registered under
+  bool has_ceiling = false;                         // a plugin limits file applies
 };
 
 ShimState& shim();
@@ -141,6 +149,25 @@ inline void check_live_config() {
                        0))
     apply_live_config();
 }
+
+// The container's task priority class as enforced: the region's (live, vgpuctl / monitor)
+// raised to the plugin's floor (a tenant may write its region, not its limits file).
+inline int effective_priority(const Region* r) {
+  const int p = r->hdr.priority.load(std::memory_order_relaxed);
+  const int floor = config().min_priority;
+  return p < floor ? floor : p;
+}
+
+// Keeps the region within the plugin's ceilings (limits, CU share and slice, host budget,
+// priority floor): the tenant maps the region read-write, so whatever it wrote there is
+// clamped back. Returns true if something was clamped. Called on attach and on every
+// limit change (generation bump).
+bool clamp_region_to_ceiling();
+
+// A region whose epoch changed under this process (re-initialised, by a tenant rewriting
+// it) no longer holds this process's slot or charges: re-registers and charges the live
+// allocations the shim recorded again. Called by the maintenance thread every period.
+void check_region_epoch();
 
 // Per-process maintenance thread: host-PID discovery retries, continuous context
 // accounting, and (for the process holding the container's sampler lease) the

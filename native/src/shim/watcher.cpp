@@ -174,7 +174,7 @@ int64_t ledger_charge(const LedgerReader& l, std::map<int, uint64_t>& seen, cons
 }
 
 // The container's task priority (live: vgpuctl / the monitor may change it).
-int region_priority(const Region* r) { return r->hdr.priority.load(std::memory_order_relaxed); }
+int region_priority(const Region* r) { return effective_priority(r); }
 
 // Publishes the container on the board (lease holder, every period).
 void board_tick(Region* r, Sampler& sm, uint64_t now) {
@@ -503,7 +503,7 @@ void* watcher_main(void*) {
   const uint64_t period_ns = (uint64_t)cfg.util_period_ms * 1'000'000ull;
   Sampler sm;
   Crowd crowd;
-  uint64_t next_slow = 0;
+  uint64_t next_slow = 0, next_touch = 0;
   int pid_attempts = 0;
   unsigned rng = (unsigned)me * 2654435761u;
   while (!s.exiting.load() && s.pid == me) {
@@ -529,6 +529,11 @@ void* watcher_main(void*) {
         }
       }
       if (!s.hostpid) pid_attempts++;
+      check_region_epoch();
+      if (now >= next_touch) {  // a live container's region file keeps a fresh mtime (contract.py GC)
+        next_touch = now + 10'000'000'000ull;
+        s.region.touch();
+      }
       if (s.slot >= 0) r->procs[s.slot].launches.store(s.launches.load(std::memory_order_relaxed));
       resync_context_charge();
       if (lease) {

@@ -20,6 +20,8 @@
 //   burst=US,N       N launches of a US-microsecond kernel on the current stream without
 //                    waiting, then synchronize: {"burst": N, "max_depth": most packets seen
 //                    queued on the stream's HSA queue right after a launch, "wall": s}
+//   setlimit=SIZE / setcu=PCT  the in-container setters -> {"setlimit": rc} / {"setcu": rc}
+//   mark=TEXT        prints {"mark": TEXT} (a point the test waits for before acting)
 //   sleep=SECS
 //   forkmalloc=SIZE  fork; the child hipMallocs SIZE and exits normally:
 //                    {"child_malloc": "ok"|"oom"|"crash"}
@@ -306,6 +308,22 @@ int main(int argc, char** argv) {
         registered.pop_back();
       }
       printf("{\"hostunregister\": true}\n");
+    } else if (key == "setlimit" || key == "setcu") {
+      // The in-container control API (reference set_current_device_memory_limit /
+      // set_current_device_sm_limit_scale): {"setlimit": rc} / {"setcu": rc}
+      int rc = -2;
+      if (key == "setlimit") {
+        using Set = int (*)(uint64_t);
+        auto f = reinterpret_cast<Set>(dlsym(RTLD_DEFAULT, "vgpu_set_current_device_memory_limit"));
+        if (f) rc = f((uint64_t)parse_size(val.c_str()));
+      } else {
+        using Set = int (*)(int);
+        auto f = reinterpret_cast<Set>(dlsym(RTLD_DEFAULT, "vgpu_set_current_device_cu_limit"));
+        if (f) rc = f(atoi(val.c_str()));
+      }
+      printf("{\"%s\": %d}\n", key.c_str(), rc);
+    } else if (key == "mark") {
+      printf("{\"mark\": \"%s\"}\n", val.c_str());
     } else if (key == "sleep") {
       std::this_thread::sleep_for(std::chrono::duration<double>(atof(val.c_str())));
       printf("{\"slept\": %s}\n", val.c_str());

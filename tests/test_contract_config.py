@@ -2,6 +2,7 @@
 import base64
 import json
 import os
+import tempfile
 
 import pytest
 
@@ -14,7 +15,11 @@ from amdvgpu.plugin.legacy import LegacyController
 from amdvgpu.plugin.vdevice import device_to_vdevices
 
 
+_VGPU_DIR = tempfile.mkdtemp(prefix="vgpu-host-")   # never the node's /usr/local/vgpu
+
+
 def _setup(**kw):
+    kw.setdefault("vgpu_dir", _VGPU_DIR)
     cfg = PluginConfig(**kw).validate()
     devs = FakeBackend(n=2).devices()
     vds = device_to_vdevices(devs, cfg.device_split_count, cfg.device_memory_scaling, cfg.device_cores_scaling)

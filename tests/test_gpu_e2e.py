@@ -48,7 +48,7 @@ def plugin(tmp_path):
     pdir = str(tmp_path / "dp")
     os.makedirs(pdir)
     cfg = PluginConfig(device_plugin_path=pdir + "/", backend="sysfs", device_split_count=4,
-                       shared_cache_dir=str(tmp_path)).validate()
+                       shared_cache_dir=str(tmp_path), vgpu_dir=str(tmp_path / "vgpu")).validate()
     k = StubKubelet(pdir).start()
     sup = Supervisor(cfg, backend=SysfsBackend(), install_signals=False)
     stop = threading.Event()

@@ -22,7 +22,7 @@ def plugin_dir(tmp_path):
 
 def start(plugin_dir, backend=None, **kw):
     cfg = PluginConfig(device_plugin_path=plugin_dir + "/", backend="fake", health_interval_s=0.1,
-                       vgpu_dir="/usr/local/vgpu", **kw).validate()
+                       vgpu_dir=os.path.join(os.path.dirname(plugin_dir), "vgpu"), **kw).validate()
     kubelet = StubKubelet(plugin_dir).start()
     sup = Supervisor(cfg, backend=backend or FakeBackend(n=2), install_signals=False)
     stop = threading.Event()
@@ -53,11 +53,21 @@ def test_register_list_and_allocate(plugin_dir):
         total = FakeBackend(n=2).devices()[0].memory_total >> 20
         assert envs["VGPU_DEVICE_MEMORY_LIMIT_0"] == f"{total // 2}m"
         assert envs["VGPU_DEVICE_CU_LIMIT_0"] == "50"
-        assert envs["VGPU_SHARED_CACHE"].startswith("/tmp/") and envs["VGPU_SHARED_CACHE"].endswith(".cache")
+        # the region: a file the plugin created, mounted over its path in the container
+        region = envs["VGPU_SHARED_CACHE"]
+        assert region.startswith("/usr/local/vgpu/regions/") and region.endswith(".cache")
         assert "VGPU_OVERSUBSCRIBE" not in envs
         mounts = {m.container_path: (m.host_path, m.read_only) for m in resp.mounts}
-        assert mounts["/usr/local/vgpu/libvgpu_hip.so"] == ("/usr/local/vgpu/libvgpu_hip.so", True)
-        assert mounts["/etc/ld.so.preload"] == ("/usr/local/vgpu/ld.so.preload", True)
+        assert mounts[region] == (os.path.join(cfg.vgpu_dir, "regions", os.path.basename(region)), False)
+        assert os.path.isfile(mounts[region][0])
+        assert mounts["/usr/local/vgpu/libvgpu_hip.so"] == (os.path.join(cfg.vgpu_dir, "libvgpu_hip.so"), True)
+        assert mounts["/etc/ld.so.preload"] == (os.path.join(cfg.vgpu_dir, "ld.so.preload"), True)
+        # the plugin-owned limits file (read-only): the ceiling the shim enforces
+        assert envs["VGPU_LIMITS_FILE"] == "/vgpu/limits" and mounts["/vgpu/limits"][1] is True
+        limits = dict(l.split("=", 1) for l in open(mounts["/vgpu/limits"][0]).read().splitlines())
+        assert limits["VGPU_DEVICE_MEMORY_LIMIT_0"] == f"{total // 2}m" and limits["VGPU_SHARED_CACHE"] == region
+        assert limits["VGPU_TASK_PRIORITY_MIN"] == "1"
+        assert limits["VGPU_REGION_INODE"] == str(os.stat(mounts[region][0]).st_ino)
         specs = [d.container_path for d in resp.devices]
         assert specs[0] == "/dev/kfd" and any(p.startswith("/dev/dri/renderD") for p in specs)
         # second vGPU on the other slot of some GPU gets a disjoint CU range
@@ -219,7 +229,7 @@ def test_stop_honoured_while_the_kubelet_is_down(plugin_dir):
     """No kubelet socket: registration keeps failing and is retried every second, but a
     stop request (or a signal) still ends the supervisor promptly."""
     cfg = PluginConfig(device_plugin_path=plugin_dir + "/", backend="fake", health_interval_s=0.1,
-                       vgpu_dir="/usr/local/vgpu").validate()
+                       vgpu_dir=os.path.join(os.path.dirname(plugin_dir), "vgpu")).validate()
     sup = Supervisor(cfg, backend=FakeBackend(n=1), install_signals=False)
     stop = threading.Event()
     th = threading.Thread(target=sup.run, args=(stop,), daemon=True)

@@ -215,6 +215,21 @@ def test_spill_placement_policy(fake, policy):
         assert after_big == 2 * GiB and after_small - after_big == 2 * GiB   # HBM full after 8
 
 
+def test_spill_is_charged_to_the_host_budget(fake):
+    """Spilled device memory is pinned host memory: it draws on the container's host budget
+    (VGPU_HOST_MEMORY_LIMIT, shared with hipHostMalloc), so past the budget an allocation
+    that would spill is refused although the quota has room; freeing a spilled buffer
+    returns its budget."""
+    e = fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="16g", VGPU_DEVICE_HBM_LIMIT_0="4096m",
+             VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come", VGPU_HOST_MEMORY_LIMIT="3g")
+    out = run(e, *(["malloc=1g"] * 4), "hostmalloc=1g", "malloc=1g", "malloc=1g", "malloc=1g", "free",
+              "malloc=1g", "sleep=0.2")
+    got = [o.get("malloc") or o.get("hostmalloc") for o in out if "malloc" in o or "hostmalloc" in o]
+    # 4 GiB resident; 1 GiB pinned by hipHostMalloc; 2 GiB spilled; the third spill is over
+    # the 3 GiB host budget; after one spilled buffer is freed, a spill fits again.
+    assert got == ["ok"] * 4 + ["ok", "ok", "ok", "oom", "ok"], out
+
+
 @pytest.mark.parametrize("mode,virt,want", [("spatial", "1", 64), ("spatial", "0", 256), ("temporal", "1", 256),
                                             ("auto", "1", 64)])
 def test_cu_count_follows_the_spatial_slice(fake, mode, virt, want):

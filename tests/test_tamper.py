@@ -1,0 +1,183 @@
+"""Plugin-owned limits: a tenant cannot raise its own quota, CU share or priority class.
+
+The reference takes every limit from container env and from a shared region the tenant
+maps read-write, and exports set_current_device_memory_limit into the container
+([multiprocess_memory_limit.c:806-808]), so a tenant can give itself more. Here the plugin
+also writes the container's contract into a limits file it owns (mounted read-only at
+/vgpu/limits in a pod; VGPU_LIMITS_FILE names it where there is no container runtime),
+and the shim treats it as a ceiling (native/src/core/config.cpp apply_ceiling,
+native/src/shim/shim.cpp clamp_region_to_ceiling / check_region_epoch). Every tamper
+vector the round-3 verdict names is tried on the CPU-only fake runtime:
+
+* raising the env limits (and env switches that would lift enforcement);
+* rewriting the shared region's limits while the tenant runs;
+* wiping the region (re-initialised with no charges) while a process holds memory;
+* deleting the region file and re-creating it for a second process;
+* calling the in-container setter upward;
+* declaring the latency priority class without the plugin's grant.
+"""
+import json
+import os
+import subprocess
+
+import pytest
+
+from amdvgpu.shim.native import LIB_DIR, shim_path
+from amdvgpu.shim.region import Region
+
+HARNESS = os.path.join(LIB_DIR, "fakerocm", "shim_harness")
+UUID = "GPU-fa4e000000000000"
+GiB = 1 << 30
+MiB = 1 << 20
+
+
+@pytest.fixture
+def pod(tmp_path):
+    """A container's plugin side: its pre-created region file and its limits file."""
+    kfd = tmp_path / "kfd"
+    kfd.mkdir()
+    region = tmp_path / "regions" / "c1.cache"
+    region.parent.mkdir()
+    region.touch()
+
+    def make(min_priority=None, **extra_limits):
+        lines = {"VGPU_DEVICE_MAP": f"0:{UUID}", "VGPU_DEVICE_MEMORY_LIMIT_0": "1024m",
+                 "VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_CU_MODE": "spatial", "VGPU_SHARED_CACHE": str(region),
+                 "VGPU_REGION_INODE": str(os.stat(region).st_ino)}
+        if min_priority is not None:
+            lines["VGPU_TASK_PRIORITY_MIN"] = str(min_priority)
+        lines.update(extra_limits)
+        limits = tmp_path / "limits.env"
+        limits.write_text("".join(f"{k}={v}\n" for k, v in lines.items()))
+        e = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "FAKE_"))}
+        e.update(FAKE_ROCR_GPUS="1", FAKE_ROCR_HBM=str(8 * GiB), FAKE_ROCR_UUIDS=UUID, FAKE_KFD_ROOT=str(kfd),
+                 VGPU_KFD_ROOT=str(kfd), VGPU_LOCK_FILE=str(tmp_path / "lock" / "l"), LD_PRELOAD=shim_path(),
+                 VGPU_LIMITS_FILE=str(limits), VGPU_DEVICE_MAP=f"0:{UUID}", VGPU_SHARED_CACHE=str(region),
+                 VGPU_DEVICE_MEMORY_LIMIT_0="1024m", VGPU_DEVICE_CU_LIMIT_0="25", VGPU_CU_MODE="spatial")
+        return e
+
+    make.region = region
+    return make
+
+
+def run(env, *ops, timeout=60):
+    p = subprocess.run([HARNESS, *ops], env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+def mallocs(out):
+    return [o["malloc"] for o in out if "malloc" in o]
+
+
+def test_raised_env_limits_and_off_switches_are_clamped(pod):
+    e = pod()
+    e.update(VGPU_DEVICE_MEMORY_LIMIT_0="64g", VGPU_DEVICE_MEMORY_LIMIT="64g", VGPU_DEVICE_CU_LIMIT_0="100",
+             VGPU_CU_MODE="off", VGPU_CU_POLICY="disable", VGPU_DISABLE="1", VGPU_FAIL_OPEN="1",
+             VGPU_SHARED_CACHE=str(pod.region) + ".mine", VGPU_DEVICE_MAP="0:GPU-ffffffffffffffff")
+    out = run(e, "meminfo", "malloc=768m", "malloc=512m", "stream", "queues")
+    assert [o for o in out if "total" in o][0]["total"] == GiB
+    assert mallocs(out) == ["ok", "oom"]
+    assert [q["cus"] for q in [o for o in out if "queues" in o][0]["queues"]] == [64]
+    assert not os.path.exists(str(pod.region) + ".mine")   # the plugin's region, not the env's
+
+
+def test_env_may_lower_the_limits(pod):
+    e = pod()
+    e.update(VGPU_DEVICE_MEMORY_LIMIT_0="256m")
+    assert mallocs(run(e, "malloc=200m", "malloc=100m")) == ["ok", "oom"]
+
+
+def _start(env, *ops):
+    p = subprocess.Popen([HARNESS, *ops], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    p.seen = []
+    return p
+
+
+def _wait_mark(p):
+    for line in p.stdout:
+        if line.startswith("{"):
+            p.seen.append(json.loads(line))
+            if "mark" in p.seen[-1]:
+                return
+    raise AssertionError(p.stderr.read()[-3000:])
+
+
+def _finish(p):
+    out, err = p.communicate(timeout=60)
+    assert p.returncode == 0, err[-3000:]
+    return p.seen + [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def test_region_rewritten_upward_is_clamped(pod):
+    """The tenant rewrites its region (mapped read-write in every process of the container):
+    memory limit 64 GiB, CU share lifted, latency class. The next allocation still stops at
+    the plugin's 1 GiB, and the region reads the plugin's values again."""
+    e = pod()
+    p = _start(e, "malloc=768m", "mark=ready", "sleep=0.6", "malloc=512m", "stream", "queues")
+    _wait_mark(p)
+    with Region(str(pod.region)) as r:
+        r.set_memory_limit(0, 64 * GiB)
+        r.set_cu_limit(0, 100)
+        r.priority = 0
+    out = _finish(p)
+    assert mallocs(out) == ["ok", "oom"]
+    q = [o for o in out if "queues" in o][0]["queues"]
+    assert [x["cus"] for x in q] == [64] and q[0]["priority"] == 1, q
+    with Region(str(pod.region)) as r:
+        d = r.device(0)
+        assert d["mem_limit"] == GiB and d["cu_limit_pct"] == 25 and r.priority == 1, (d, r.priority)
+
+
+def test_wiped_region_is_recharged(pod):
+    """The region is overwritten (zeroed) while a process holds 768 MiB: the process notices
+    within a period, re-initialises the region and charges its allocation again, so a second
+    process still gets only what is left of the quota."""
+    e = pod()
+    p = _start(e, "malloc=768m", "mark=ready", "sleep=3")
+    try:
+        _wait_mark(p)
+        with open(pod.region, "r+b") as f:
+            f.write(b"\0" * 4096)
+        import time
+        time.sleep(0.8)
+        with Region(str(pod.region)) as r:
+            assert r.device(0)["used"] >= 768 * MiB, r.device(0)
+        assert mallocs(run(e, "malloc=512m", "malloc=200m")) == ["oom", "ok"]
+    finally:
+        _finish(p)
+
+
+def test_deleted_and_recreated_region_is_refused(pod):
+    """The region file is deleted while a process holds memory and a new process creates a
+    fresh one at the same path: not the plugin's file (inode), so the new process gets no
+    device memory instead of a second, empty quota."""
+    e = pod()
+    p = _start(e, "malloc=768m", "mark=ready", "sleep=2")
+    try:
+        _wait_mark(p)
+        os.unlink(pod.region)
+        assert mallocs(run(e, "malloc=512m")) == ["oom"]
+    finally:
+        _finish(p)
+
+
+def test_setters_only_lower(pod):
+    e = pod()
+    out = run(e, "malloc=256m", "setlimit=4g", "setlimit=0", "setcu=100", "setcu=50", "setlimit=512m", "setcu=10",
+              "malloc=300m", "malloc=200m")
+    assert [o["setlimit"] for o in out if "setlimit" in o] == [-1, -1, 0]
+    assert [o["setcu"] for o in out if "setcu" in o] == [-1, -1, 0]
+    assert mallocs(out) == ["ok", "oom", "ok"]
+
+
+@pytest.mark.parametrize("granted,want", [(None, 1), (0, 2)])
+def test_latency_class_needs_the_plugins_grant(pod, granted, want):
+    """VGPU_TASK_PRIORITY=0 (latency class: high hardware-queue priority, exempt from
+    duty-cycling, CU reservations) is the operator's to give: without
+    VGPU_TASK_PRIORITY_MIN=0 in the limits file the container runs as class 1 (queue
+    priority normal = 1); with it, its queues are high priority (2)."""
+    e = pod(min_priority=granted)
+    e["VGPU_TASK_PRIORITY"] = "0"
+    q = [o for o in run(e, "stream", "queues") if "queues" in o][0]["queues"]
+    assert q[0]["priority"] == want, q
