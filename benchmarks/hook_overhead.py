@@ -85,6 +85,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20000)
     ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--modes", default="", help="comma-separated subset of the modes")
+    ap.add_argument("--probe", action="store_true", help="the C++ probe (native/tests/hip_launch_probe.hip) "
+                    "instead of the PyTorch worker")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--json-out")
@@ -95,7 +98,12 @@ def main():
     from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
     modes = {"native": None, "vgpu": dict(mem_limit=64 << 30),
              "vgpu-stats": dict(mem_limit=64 << 30, extra={"VGPU_STATS": "1"}),
-             "vgpu-temporal": dict(mem_limit=64 << 30, cu_limit=99, cu_mode="temporal")}
+             "vgpu-temporal": dict(mem_limit=64 << 30, cu_limit=99, cu_mode="temporal"),
+             # diagnostics: the gates made pass-throughs (trampolines stay), the dlsym routing off
+             "vgpu-nogate": dict(mem_limit=64 << 30, extra={"VGPU_HOOK_LAUNCH": "0"}),
+             "vgpu-nodlsym": dict(mem_limit=64 << 30, extra={"VGPU_HOOK_DLSYM": "0"})}
+    if a.modes:
+        modes = {m: modes[m] for m in a.modes.split(",")}
     best = {}
     for rep in range(a.repeats):
         for mode, kw in modes.items():
@@ -104,9 +112,15 @@ def main():
             fd, out = tempfile.mkstemp(suffix=".json")
             os.close(fd)
             try:
-                subprocess.check_call([sys.executable, os.path.abspath(__file__), "--worker", "--iters",
-                                       str(a.iters), "--out", out], env=env)
-                r = json.load(open(out))
+                if a.probe:
+                    from amdvgpu.shim.native import lib_path
+                    line = subprocess.check_output([lib_path("hip_launch_probe"), str(a.iters * 5), str(a.iters * 50)],
+                                                   env=env, text=True)
+                    r = json.loads([l for l in line.splitlines() if l.startswith("{")][-1])
+                else:
+                    subprocess.check_call([sys.executable, os.path.abspath(__file__), "--worker", "--iters",
+                                           str(a.iters), "--out", out], env=env)
+                    r = json.load(open(out))
             finally:
                 os.unlink(out)
                 cleanup_region(c)

@@ -43,6 +43,7 @@
 #include <rocm_smi/rocm_smi.h>
 
 #include "real.h"
+#include "vgpu/config.h"
 
 extern "C" {
 amdsmi_status_t amdsmi_get_gpu_memory_total(amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*);
@@ -74,6 +75,7 @@ using DlvsymFn = void* (*)(void*, const char*, const char*);
 // VGPU_HOOK_DLSYM=0 turns the redirection off (read once when the shim is loaded).
 bool g_dlsym_hook_on = true;
 __attribute__((constructor)) void dlsym_hook_ctor() {
+  if (vgpu::ceiling_present()) return;  // not a tenant's switch where the plugin set limits
   const char* s = getenv("VGPU_HOOK_DLSYM");
   if (s && (*s == '0' || *s == 'f' || *s == 'F' || *s == 'n' || *s == 'N')) g_dlsym_hook_on = false;
 }

@@ -133,6 +133,8 @@ inline void gate_suspend() {
 // launch block and the temporal GPU-time credit of device `dev` (dev < 0 = current HIP
 // device).
 void gate_launch(int dev);
+// VGPU_HOOK_LAUNCH (gates.cpp): false turns the launch gates into pass-throughs.
+extern bool g_launch_hooks_on;
 
 // Waits (bounded) until this process's HSA queues on device `dev` hold at most `cap`
 // AQL packets not yet consumed by the command processor (write - read index). Returns

@@ -214,6 +214,13 @@ hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
   return hipSuccess;
 }
 
+hipError_t hipStreamGetDevice(hipStream_t stream, hipDevice_t* device) {
+  init();
+  if (!device) return hipErrorInvalidValue;
+  *device = dev_of(stream);
+  return hipSuccess;
+}
+
 hipError_t hipStreamCreate(hipStream_t* stream) {
   init();
   FakeStream* s = new FakeStream{nullptr, t_dev};

@@ -8,6 +8,8 @@
 //   free             hipFree of the most recent successful allocation
 //   meminfo          hipMemGetInfo -> {"free": .., "total": ..}
 //   stream           hipStreamCreate on the current device (becomes the current stream)
+//   usestream=I      the I-th stream created so far becomes the current stream (the current
+//                    device stays: a stream of another device used from this thread)
 //   launch=US,N      N launches of a US-microsecond kernel, then synchronize
 //   run=US,SECS      back-to-back US-microsecond kernels for SECS seconds (sync every 8):
 //                    {"busy_frac": GPU time executed / wall, ...}
@@ -184,12 +186,19 @@ int main(int argc, char** argv) {
       (void)hipStreamCreate(&stream);
       streams.push_back(stream);
       printf("{\"stream\": %zu}\n", streams.size() - 1);
+    } else if (key == "usestream") {
+      // a stream created earlier (on whichever device), without changing the current device
+      const size_t i = (size_t)atoi(val.c_str());
+      stream = i < streams.size() ? streams[i] : nullptr;
+      printf("{\"usestream\": %zu}\n", i);
     } else if (key == "launch" || key == "graph" || key == "run") {
       unsigned us = (unsigned)atoi(val.c_str());
       double amount = atof(val.substr(val.find(',') + 1).c_str());
       uint32_t* k = &kernel_us[kslot++ % 64];
       *k = us;
-      uint64_t k0 = 0, b0 = fake_hip_busy_us(dev, &k0);
+      int sdev = dev;  // the device the stream's kernels run on
+      if (stream) (void)hipStreamGetDevice(stream, &sdev);
+      uint64_t k0 = 0, b0 = fake_hip_busy_us(sdev, &k0);
       double t0 = now_s();
       long n = 0;
       for (;; n++) {
@@ -201,7 +210,7 @@ int main(int argc, char** argv) {
       }
       (void)hipStreamSynchronize(stream);
       double wall = now_s() - t0;
-      uint64_t k1 = 0, b1 = fake_hip_busy_us(dev, &k1);
+      uint64_t k1 = 0, b1 = fake_hip_busy_us(sdev, &k1);
       printf("{\"%s\": %ld, \"wall\": %.6f, \"busy_us\": %llu, \"busy_frac\": %.4f}\n", key.c_str(), n, wall,
              (unsigned long long)(b1 - b0), (b1 - b0) / 1e6 / wall);
     } else if (key == "burst") {

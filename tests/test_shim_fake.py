@@ -103,6 +103,18 @@ def test_temporal_limit_routed_to_the_current_device(fake):
     assert procs == [] or True  # the harness has exited; its slot is released
 
 
+def test_temporal_limit_follows_the_launch_stream(fake):
+    """Only device 1 is limited (20 %, temporal). A stream created on device 1 and used while
+    the thread's current device is 0 - multi-GPU code keeping one stream per device - runs
+    on device 1's credit (the launch's stream decides, hipStreamGetDevice), at ~20 % busy;
+    a device-0 stream launched from the same thread runs at full speed."""
+    e = fake(gpus=2, VGPU_DEVICE_CU_LIMIT_1="20", VGPU_CU_MODE="temporal", VGPU_DEVICE_MEMORY_LIMIT_1="4g")
+    out = run(e, "dev=1", "stream", "dev=0", "usestream=0", "run=2000,3", "stream", "run=2000,1.5", timeout=120)
+    runs = [o for o in out if "run" in o]
+    assert abs(runs[0]["busy_frac"] - 0.20) <= 0.05, runs   # device 1's stream: its limit
+    assert runs[1]["busy_frac"] > 0.75, runs                # device 0's stream: unlimited
+
+
 @pytest.mark.parametrize("limit", [10, 50, 80])
 def test_temporal_limiter_closed_loop(fake, limit):
     """The real sampler + gate against the fake GPU: achieved busy fraction within 5 points."""
