@@ -109,10 +109,12 @@ def parse(argv=None):
 
 
 def worker(args):
+    t_spawn = time.time()
     import torch
     import torch.distributed as dist
 
     from amdvgpu.models.aibench import Runner, get_case
+    phases = {"import_s": time.time() - t_spawn}
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1)) if args.dist else 1
@@ -121,6 +123,8 @@ def worker(args):
     device = torch.device("cpu") if cpu else torch.device("cuda", 0)
     if not cpu:
         torch.cuda.set_device(device)
+        torch.zeros(1, device=device)  # HIP / ROCr (and the shim) initialised here
+    phases["gpu_init_s"] = time.time() - t_spawn - sum(phases.values())
     if world > 1:
         # The pods are independent tenants (no gradient exchange): the cross-rank group only
         # brackets the timed window and takes the max, so it runs on gloo over TCP and the
@@ -146,9 +150,18 @@ def worker(args):
         runner.x = runner.x[..., :64, :64].contiguous() if runner.x.dim() == 4 else runner.x[:, :16].contiguous()
     else:
         runner = Runner(case, device, dtype=dtype)
-    for _ in range(args.warmup):
-        runner.step()
     sync()
+    phases["model_s"] = time.time() - t_spawn - sum(phases.values())
+    for i in range(args.warmup):
+        runner.step()
+        if i == 0:
+            sync()
+            phases["first_step_s"] = time.time() - t_spawn - sum(phases.values())
+    sync()
+    phases["warmup_s"] = time.time() - t_spawn - sum(phases.values())
+    if args.go:  # where a pod's start-up goes (many-pod sweep points are dominated by it)
+        print("[bench-worker] start-up " + json.dumps({k: round(v, 2) for k, v in phases.items()}), file=sys.stderr,
+              flush=True)
 
     def barrier():
         sync()
@@ -169,7 +182,7 @@ def worker(args):
         sync()
         dt = time.perf_counter() - t0
         res = {"mode": args.mode, "ms_per_step": dt * 1000.0 / n, "items_per_step": runner.items_per_step,
-               "steps": n, "t0": t0, "t1": t0 + dt}
+               "steps": n, "t0": t0, "t1": t0 + dt, "startup": {k: round(v, 2) for k, v in phases.items()}}
     else:
         # The limiter's own account of the timed window (GPU time charged / wall time), read
         # from the pod's shared region like vgpuctl would: what the vGPU granted this pod.

@@ -143,17 +143,22 @@ def main():
         for lim in [int(x) for x in a.limits.split(",")]:
             extra = dict(kv.split("=", 1) for kv in a.extra.split(",") if kv)
             cs = [vgpu_env(cu_limit=lim, cu_mode="temporal", mem_limit=64 << 30, extra=extra) for _ in range(n)]
-            got = run_tenants(a.workload, cs, a.seconds, a.sync_every, a.batch)
+            full = run_tenants(a.workload, cs, a.seconds, a.sync_every, a.batch, full=True)
+            got = [r["throughput"] for r in full]
             ach = [100.0 * g / native for g in got]
             rows.append({"tenants": n, "limit_pct": lim, "throughput": got, "achieved_pct": ach,
+                         "charged_pct": [r.get("charged_pct") for r in full],
+                         "throttle_pct": [r.get("throttle_pct") for r in full],
                          "max_error_pts": max(abs(x - lim) for x in ach)})
             print(json.dumps(rows[-1]), flush=True)
     label = a.workload + (f" b={a.batch}" if a.batch else "") + (f" [{a.extra}]" if a.extra else "")
     md = [f"# temporal limit accuracy — {label} (native {native:.1f}/s, {a.seconds:.0f} s per point)", "",
-          "| tenants | limit % | achieved % (per tenant) | max error (pts) |", "|---|---|---|---|"]
+          "| tenants | limit % | achieved % (per tenant) | max error (pts) | charged % of GPU time |",
+          "|---|---|---|---|---|"]
     for r in rows:
+        ch = " / ".join("-" if x is None else f"{x:.1f}" for x in r["charged_pct"])
         md.append(f"| {r['tenants']} | {r['limit_pct']} | {' / '.join(f'{x:.1f}' for x in r['achieved_pct'])} | "
-                  f"{r['max_error_pts']:.1f} |")
+                  f"{r['max_error_pts']:.1f} | {ch} |")
     print("\n".join(md))
     if a.json_out:
         json.dump({"workload": a.workload, "native": native, "rows": rows}, open(a.json_out, "w"), indent=1)
