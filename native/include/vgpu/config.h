@@ -94,6 +94,8 @@ struct Config {
   int util_sample_us = 1000;             // temporal-mode occupancy sampling interval
   int sample_read_budget = 32;           // node-wide occupancy reads per interval (ratelimit.h)
   int limiter_window_ms = 40;            // temporal-mode credit window (ratelimit.h)
+  int limiter_solo_window_ms = 160;      // VGPU_LIMITER_SOLO_WINDOW_MS: the window while no other process
+                                         // keeps the GPU busy (longer on/off periods, fewer warm-ups; 0 = off)
   ChargeModel charge_model = ChargeModel::kShare;  // VGPU_CHARGE_MODEL: share | progress
   std::string board_dir;                 // VGPU_BOARD_DIR: node-wide board (vgpu/board.h), "" = none
   std::string board_slot;                // VGPU_BOARD_SLOT: this container's slot file in it

@@ -296,6 +296,8 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   if (parse_int(getenv_fn("VGPU_SAMPLE_READ_BUDGET"), 0, 1 << 20, &budget)) cfg->sample_read_budget = (int)budget;
   long window = 40;
   if (parse_int(getenv_fn("VGPU_LIMITER_WINDOW_MS"), 5, 2000, &window)) cfg->limiter_window_ms = (int)window;
+  long solo = 160;
+  if (parse_int(getenv_fn("VGPU_LIMITER_SOLO_WINDOW_MS"), 0, 5000, &solo)) cfg->limiter_solo_window_ms = (int)solo;
   if (const char* s = getenv_fn("VGPU_CHARGE_MODEL")) {
     if (!strcasecmp(s, "share")) cfg->charge_model = ChargeModel::kShare;
     else if (!strcasecmp(s, "progress")) cfg->charge_model = ChargeModel::kProgress;

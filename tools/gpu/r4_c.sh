@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-4 GPU study 3 (profiles/r4c):
+#   lone   a lone ResNet-50 b=50 pod at 25 % on the GPU-time limiter: solo window off /
+#          160 ms (default) / 320 ms (achieved share of native throughput, charged share)
+#   many   16 pods: start-up phases (bench sweep 1,16), then the same with the board's
+#          concurrency admission at 1 (time slicing) for the per-pod spread
+#   vmem   can host memory back a GPU-visible VMM range, and be swapped for HBM in place?
+# Each GPU step has its own time limit; a crash/timeout ends the script.
+out=${1:-gpurun_out/r4c}
+what=${2:-lone,many,vmem}
+mkdir -p "$out"
+if [[ $what == *lone* ]]; then
+  for w in 0 160 320; do
+    timeout -k 10 240 python -u benchmarks/temporal_accuracy.py --workload resnet50 --tenants 1 --limits 25 \
+      --seconds 8 --extra VGPU_LIMITER_SOLO_WINDOW_MS=$w --json-out "$out/lone_w$w.json" --md-out "$out/lone_w$w.md" \
+      > "$out/lone_w$w.log" 2>&1 || exit $?
+  done
+fi
+if [[ $what == *many* ]]; then
+  timeout -k 10 560 python -u bench.py --modes native --sweep on --sweep-tenants 1,16 --sweep-seconds 8 \
+    --time-budget 520 --json-out "$out/sweep16.json" > "$out/sweep16.log" 2>&1 || exit $?
+  timeout -k 10 400 python -u benchmarks/vgpu_scaling.py --policy default --tenants 16 --seconds 8 \
+    --pod-env VGPU_GPU_CONCURRENCY=1 --json-out "$out/conc1_16.json" --md-out "$out/conc1_16.md" \
+    > "$out/conc1_16.log" 2>&1 || exit $?
+fi
+if [[ $what == *vmem* ]]; then
+  timeout -k 10 60 4paradigm-k8s-device-plugin_amd/lib/vmem_probe 64 > "$out/vmem.json" 2> "$out/vmem.err"
+  echo "vmem_rc=$?" >> "$out/vmem.err"
+fi
