@@ -50,6 +50,8 @@ def worker(a):
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--cu-limit", type=int, default=0, help="vGPU CU share %% (0 = native, no shim)")
+    ap.add_argument("--cu-mode", default="spatial", help="the vGPU's VGPU_CU_MODE (spatial: CU mask; temporal: "
+                    "GPU-time limiter on all CUs)")
     ap.add_argument("--workload", default="spin,resnet")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--spin-us", type=int, default=200)
@@ -62,7 +64,7 @@ def main(argv=None):
            "--workload", a.workload, "--iters", str(a.iters), "--spin-us", str(a.spin_us)]
     if a.cu_limit <= 0:
         return subprocess.call(cmd)
-    contract = vgpu_env(mem_limit=72 << 30, cu_limit=a.cu_limit, cu_mode="spatial")
+    contract = vgpu_env(mem_limit=72 << 30, cu_limit=a.cu_limit, cu_mode=a.cu_mode)
     try:
         return subprocess.call(cmd, env=apply_contract(contract))
     finally:
