@@ -2,8 +2,10 @@
 # Round-4 GPU study 3 (profiles/r4c):
 #   lone   a lone ResNet-50 b=50 pod at 25 % on the GPU-time limiter: solo window off /
 #          160 ms (default) / 320 ms (achieved share of native throughput, charged share)
-#   many   16 pods: start-up phases (bench sweep 1,16), then the same with the board's
-#          concurrency admission at 1 (time slicing) for the per-pod spread
+#   many   16 pods: start-up phases (bench sweep 1,16); then 16 pods told the GPU's full CU
+#          count (VGPU_VIRTUAL_CU_COUNT=0: crowded pods run on all CUs, so libraries should
+#          size for 256, not the 16 of their slice); then the board's concurrency
+#          admission at 1 (time slicing) for the per-pod spread
 #   vmem   can host memory back a GPU-visible VMM range, and be swapped for HBM in place?
 # Each GPU step has its own time limit; a crash/timeout ends the script.
 out=${1:-gpurun_out/r4c}
@@ -19,6 +21,9 @@ fi
 if [[ $what == *many* ]]; then
   timeout -k 10 560 python -u bench.py --modes native --sweep on --sweep-tenants 1,16 --sweep-seconds 8 \
     --time-budget 520 --json-out "$out/sweep16.json" > "$out/sweep16.log" 2>&1 || exit $?
+  timeout -k 10 400 python -u benchmarks/vgpu_scaling.py --policy default --tenants 16 --seconds 8 \
+    --pod-env VGPU_VIRTUAL_CU_COUNT=0 --json-out "$out/fullcu_16.json" --md-out "$out/fullcu_16.md" \
+    > "$out/fullcu_16.log" 2>&1 || exit $?
   timeout -k 10 400 python -u benchmarks/vgpu_scaling.py --policy default --tenants 16 --seconds 8 \
     --pod-env VGPU_GPU_CONCURRENCY=1 --json-out "$out/conc1_16.json" --md-out "$out/conc1_16.md" \
     > "$out/conc1_16.log" 2>&1 || exit $?
