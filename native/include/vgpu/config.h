@@ -51,6 +51,14 @@ enum class SpillPolicy : int {
   kLargeFirst = 1,  // large allocations spill first; a reserve of the share stays for small ones
 };
 
+// What backs a spilled allocation (VGPU_SPILL_BACKING).
+enum class SpillBacking : int {
+  kAuto = 0,    // a migratable SVM range when the driver supports it, else pinned host memory
+  kSvm = 1,     // KFD shared virtual memory: pageable host RAM mapped into the GPU in place,
+                // migrated into HBM (same address) when the tenant's HBM share frees up
+  kPinned = 2,  // a pinned host-pool allocation (never moves)
+};
+
 // How the temporal limiter charges a container that shares the GPU (VGPU_CHARGE_MODEL).
 enum class ChargeModel : int {
   kShare = 0,     // wall time x its share of the resident waves (processor sharing)
@@ -82,6 +90,8 @@ struct Config {
   SpillPolicy spill_policy = SpillPolicy::kLargeFirst;  // VGPU_SPILL_POLICY
   uint64_t spill_large_bytes = 256ull << 20;  // VGPU_SPILL_LARGE: "large" allocation threshold
   uint64_t spill_reserve_bytes = 0;      // VGPU_SPILL_RESERVE: HBM kept for small ones (0 = auto)
+  SpillBacking spill_backing = SpillBacking::kAuto;  // VGPU_SPILL_BACKING: auto | svm | pinned
+  bool spill_promote = true;             // VGPU_SPILL_PROMOTE: move SVM spills into HBM once they fit
   int priority = 1;                      // VGPU_TASK_PRIORITY
   CuMode cu_mode = CuMode::kAuto;        // VGPU_CU_MODE
   CuPolicy cu_policy = CuPolicy::kDefault;

@@ -261,6 +261,13 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   if (const char* s = getenv_fn("VGPU_SPILL_RESERVE")) {
     if (!parse_size(s, &cfg->spill_reserve_bytes)) VLOG_WARN("invalid VGPU_SPILL_RESERVE=%s ignored", s);
   }
+  if (const char* s = getenv_fn("VGPU_SPILL_BACKING")) {
+    if (!strcasecmp(s, "auto")) cfg->spill_backing = SpillBacking::kAuto;
+    else if (!strcasecmp(s, "svm")) cfg->spill_backing = SpillBacking::kSvm;
+    else if (!strcasecmp(s, "pinned")) cfg->spill_backing = SpillBacking::kPinned;
+    else VLOG_WARN("invalid VGPU_SPILL_BACKING=%s, using auto", s);
+  }
+  cfg->spill_promote = parse_bool(getenv_fn("VGPU_SPILL_PROMOTE"), true);
   if (const char* s = getenv_fn("VGPU_HOST_MEMORY_LIMIT")) {
     if (!parse_size(s, &cfg->host_mem_limit)) {
       VLOG_WARN("invalid VGPU_HOST_MEMORY_LIMIT=%s ignored", s);

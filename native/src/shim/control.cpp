@@ -58,6 +58,12 @@ __attribute__((visibility("default"))) uint64_t vgpu_get_current_device_memory_u
   return ok() ? shim().region.usage(current_device()) : 0;
 }
 
+// Bytes of the current device's quota this process's container holds in host memory (virtual
+// device memory, spill.cpp): falls as spills are promoted into HBM.
+__attribute__((visibility("default"))) uint64_t vgpu_get_current_device_spilled() {
+  return ok() ? shim().region.raw()->dev[current_device()].spilled.load() : 0;
+}
+
 __attribute__((visibility("default"))) int vgpu_set_current_device_cu_limit(int pct) {
   if (!ok() || pct <= 0 || pct >= 100) return -1;
   const int dev = current_device();
@@ -76,11 +82,14 @@ __attribute__((visibility("default"))) int vgpu_shim_active() { return shim().ac
 __attribute__((visibility("default"))) void vgpu_view_allocator() {
   ShimState& s = shim();
   std::lock_guard<std::mutex> g(s.alloc_mu);
-  fprintf(stderr, "[vGPU] allocator: %zu live allocations, %zu vmem handles, slot %d\n", s.allocs.size(),
-          s.vmem.size(), s.slot);
+  fprintf(stderr, "[vGPU] allocator: %zu live allocations, %zu vmem handles, %zu SVM spills, slot %d\n",
+          s.allocs.size(), s.vmem.size(), s.svm.size(), s.slot);
   for (const auto& kv : s.allocs)
     fprintf(stderr, "  %p size=%lu dev=%d kind=%d\n", (void*)kv.first, (unsigned long)kv.second.size, kv.second.dev,
             kv.second.kind);
+  for (const auto& kv : s.svm)
+    fprintf(stderr, "  %p size=%lu dev=%d svm %s\n", (void*)kv.first, (unsigned long)kv.second.size, kv.second.dev,
+            kv.second.in_hbm ? "in HBM" : "in host memory");
 }
 
 }  // extern "C"

@@ -50,40 +50,6 @@ bool take_alloc(uintptr_t key, AllocRec* out) {
   return true;
 }
 
-// Host spill for virtual device memory: serve an allocation the HBM cannot hold
-// from pinned host memory reachable by the GPU.
-// Spilled bytes are pinned host memory: they count against the container's host budget
-// too (VGPU_HOST_MEMORY_LIMIT, shared with hipHostMalloc / hipHostRegister), so the RAM an
-// oversubscribed vGPU pins is bounded like any other pinned memory (plugin/host_memory.py
-// sizes the budget and refuses scalings the node cannot back).
-hsa_status_t spill_allocate(int dev, size_t size, void** ptr) {
-  ShimState& s = shim();
-  AgentInfo& a = s.agents[dev];
-  if (!a.spill_pool.handle) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
-  if (s.region.charge_host(s.slot, size) != Charge::kOk) {
-    VLOG_WARN("device %d: %zu bytes cannot spill: host memory budget %lu (pinned %lu) is used up", dev, size,
-              (unsigned long)s.region.host_limit(), (unsigned long)s.region.host_usage());
-    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
-  }
-  VGPU_REAL_HSA(hsa_amd_memory_pool_allocate);
-  VGPU_REAL_HSA(hsa_amd_agents_allow_access);
-  VGPU_REAL_HSA(hsa_amd_memory_pool_free);
-  hsa_status_t st = real_hsa_amd_memory_pool_allocate(a.spill_pool, size, 0, ptr);
-  if (st != HSA_STATUS_SUCCESS) {
-    s.region.uncharge_host(s.slot, size);
-    return st;
-  }
-  st = real_hsa_amd_agents_allow_access(1, &a.agent, nullptr, *ptr);
-  if (st != HSA_STATUS_SUCCESS) {
-    real_hsa_amd_memory_pool_free(*ptr);
-    s.region.uncharge_host(s.slot, size);
-    *ptr = nullptr;
-    return st;
-  }
-  VLOG_INFO("device %d: %zu bytes spilled to host memory at %p", dev, size, *ptr);
-  return HSA_STATUS_SUCCESS;
-}
-
 // Placement of an allocation of a tenant with virtual device memory: true = host memory.
 // First-come keeps HBM until the tenant's HBM share is used up. Large-first (default)
 // sends large allocations (datasets, caches: bulk data touched a slice at a time) to host
@@ -175,13 +141,8 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   // from host memory (VGPU_DEVICE_HBM_LIMIT_<i>, emitted by the plugin when
   // --device-memory-scaling > 1), so one tenant cannot crowd the others out of HBM.
   if (should_spill(dev, size)) {
-    st = spill_allocate(dev, size, ptr);
-    if (st == HSA_STATUS_SUCCESS) {
-      s.region.uncharge(s.slot, dev, size, kMemData);
-      s.region.force_charge(s.slot, dev, size, kMemSpill);
-      record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemSpill);
-      return st;
-    }
+    st = spill_allocate(dev, size, ptr);  // charged as spill and recorded
+    if (st == HSA_STATUS_SUCCESS) return st;
     // No host memory for it: within the HBM share (an early, large-first spill) the
     // allocation may stay in HBM; past the share it is refused - the rest of the HBM
     // belongs to the other tenants of the GPU.
@@ -198,12 +159,7 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   if (st == HSA_STATUS_ERROR_OUT_OF_RESOURCES && config().oversubscribe) {
     // Under quota but the physical HBM is exhausted: virtual device memory.
     st = spill_allocate(dev, size, ptr);
-    if (st == HSA_STATUS_SUCCESS) {
-      s.region.uncharge(s.slot, dev, size, kMemData);
-      s.region.force_charge(s.slot, dev, size, kMemSpill);
-      record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemSpill);
-      return st;
-    }
+    if (st == HSA_STATUS_SUCCESS) return st;
   }
   s.region.uncharge(s.slot, dev, size, kMemData);
   return st;
@@ -215,10 +171,12 @@ hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
   if (!real_hsa_amd_memory_pool_free) return HSA_STATUS_ERROR;
   ShimState& s = shim();
   if (ptr && s.phase.load(std::memory_order_relaxed) == 2) {
+    if (spill_release(ptr)) return HSA_STATUS_SUCCESS;  // an SVM spill: ROCr never saw it
     AllocRec rec;
     if (take_alloc(reinterpret_cast<uintptr_t>(ptr), &rec) && s.slot >= 0 && !s.exiting.load()) {
       s.region.uncharge(s.slot, rec.dev, rec.size, (MemKind)rec.kind);
       if (rec.kind == kMemSpill) s.region.uncharge_host(s.slot, rec.size);
+      else notify_device_memory_freed();
     }
   }
   return real_hsa_amd_memory_pool_free(ptr);
@@ -266,6 +224,18 @@ hsa_status_t hsa_memory_free(void* ptr) {
   return st;
 }
 
+// Peer access to a buffer (ROCclr grants it to the other GPUs of the process): an SVM spill
+// is not a ROCr allocation, so its access list is set on the SVM range instead.
+hsa_status_t hsa_amd_agents_allow_access(uint32_t num_agents, const hsa_agent_t* agents, const uint32_t* flags,
+                                         const void* ptr) {
+  VGPU_REAL_HSA(hsa_amd_agents_allow_access);
+  if (!real_hsa_amd_agents_allow_access) return HSA_STATUS_ERROR;
+  hsa_status_t st;
+  if (ptr && shim().phase.load(std::memory_order_relaxed) == 2 && svm_allow_access(ptr, num_agents, agents, &st))
+    return st;
+  return real_hsa_amd_agents_allow_access(num_agents, agents, flags, ptr);
+}
+
 hsa_status_t hsa_amd_vmem_handle_create(hsa_amd_memory_pool_t pool, size_t size, hsa_amd_memory_type_t type,
                                         uint64_t flags, hsa_amd_vmem_alloc_handle_t* handle) {
   VGPU_REAL_HSA(hsa_amd_vmem_handle_create);
@@ -308,7 +278,10 @@ hsa_status_t hsa_amd_vmem_handle_release(hsa_amd_vmem_alloc_handle_t handle) {
         s.vmem.erase(it);
       }
     }
-    if (rec.dev >= 0 && s.slot >= 0 && !s.exiting.load()) s.region.uncharge(s.slot, rec.dev, rec.size, kMemData);
+    if (rec.dev >= 0 && s.slot >= 0 && !s.exiting.load()) {
+      s.region.uncharge(s.slot, rec.dev, rec.size, kMemData);
+      notify_device_memory_freed();
+    }
   }
   return real_hsa_amd_vmem_handle_release(handle);
 }
@@ -542,7 +515,7 @@ const char* const kHsaHooked[] = {
     "hsa_init", "hsa_amd_memory_pool_allocate", "hsa_amd_memory_pool_free", "hsa_amd_memory_pool_get_info",
     "hsa_amd_vmem_handle_create", "hsa_amd_vmem_handle_release", "hsa_agent_get_info", "hsa_queue_create",
     "hsa_queue_destroy", "hsa_amd_queue_cu_set_mask", "hsa_amd_ipc_memory_attach", "hsa_amd_ipc_memory_detach",
-    "hsa_memory_allocate", "hsa_memory_free",
+    "hsa_memory_allocate", "hsa_memory_free", "hsa_amd_agents_allow_access",
 };
 constexpr int kNumHsaHooked = sizeof(kHsaHooked) / sizeof(kHsaHooked[0]);
 

@@ -191,6 +191,7 @@ void atfork_child() {
   s.managed.clear();
   s.ipc.clear();
   s.host.clear();
+  svm_forget();
   for (auto& b : s.ipc_bytes) b.store(0);
   s.queues.clear();
   s.hostpid = 0;
@@ -619,6 +620,7 @@ void check_region_epoch() {
     for (const auto& kv : s.vmem) s.region.force_charge(slot, kv.second.dev, kv.second.size, kMemData);
     for (const auto& kv : s.managed) s.region.force_charge(slot, kv.second.dev, kv.second.size, kMemData);
     for (const auto& kv : s.host) host += kv.second;
+    svm_recharge(slot, &host);
     if (host) {
       r->hdr.host_used.fetch_add(host);
       r->procs[slot].host_used.fetch_add(host);
@@ -750,7 +752,8 @@ void resync_context_charge() {
     int64_t vram = kfd_vram_usage(s.hostpid, a.gpu_id);
     if (vram < 0) continue;
     DeviceUsage& u = r->procs[s.slot].used[i];
-    int64_t tracked = (int64_t)u.kind[kMemData].load();
+    // Promoted SVM spills are charged as data; KFD may not count their pages in vram_<id>.
+    int64_t tracked = (int64_t)u.kind[kMemData].load() - svm_hbm_outside_kfd(i);
     // IPC imports are not in the importer's vram_<gpu_id> (measured on MI355X: a 1 GiB
     // import left the consumer's counter at its ~0.5 GiB runtime footprint,
     // profiles/r2e), so nothing is subtracted for them: the exporter alone holds the charge.

@@ -56,6 +56,17 @@ struct AllocRec {
   int kind;
 };
 
+// A spilled allocation backed by a KFD shared-virtual-memory range (spill.cpp): host RAM the
+// GPU reaches in place until it is promoted into HBM, at the same address.
+struct SvmRec {
+  uint64_t size;      // bytes charged (the allocation's size)
+  uint64_t mapped;    // bytes mapped (page-rounded)
+  int dev;
+  bool in_hbm;        // promoted: charged as HBM data, no longer as spill / host memory
+  uint64_t seq;       // allocation order (oldest is promoted first)
+  uint64_t retry_ns;  // a failed promotion is not retried before this time
+};
+
 struct ShimState {
   std::atomic<int> phase{0};         // 0 = not initialised, 1 = initialising, 2 = ready, 3 = inert
   bool active = false;               // accounting + gates enabled
@@ -73,6 +84,10 @@ struct ShimState {
   std::unordered_map<uintptr_t, AllocRec> ipc;      // IPC-attached pointers (owned by another process)
   std::unordered_map<uintptr_t, uint64_t> host;     // pinned host memory (host_hooks.cpp) → bytes
   std::unordered_map<uintptr_t, int> queues;        // hsa_queue_t* → ordinal
+  std::unordered_map<uintptr_t, SvmRec> svm;        // SVM-backed spills (spill.cpp) → record
+  std::mutex svm_mu;                                // serialises promotions with the frees of SVM spills
+  int64_t svm_hbm[kMaxDevices] = {};                // promoted SVM bytes per device (under ctx_mu)
+  int svm_kfd_vram = -1;                            // promoted SVM pages appear in KFD's vram_<gpu_id>: 1 / 0 / -1 unknown
   std::atomic<bool> exiting{false};
   std::atomic<bool> watcher_started{false};
   std::atomic<uint64_t> seen_generation{0};         // region generation the queues reflect
@@ -185,6 +200,25 @@ pid_t resolve_hostpid(int lock_timeout_ms);
 // that never pass the pool hooks (reference: per-context and per-module charges,
 // [context.c:49-86], [export_table.c:85-113]).
 void resync_context_charge();
+
+// Virtual device memory (spill.cpp). spill_allocate serves `size` bytes of device `dev`
+// from host memory - a migratable SVM range when the driver has them (VGPU_SPILL_BACKING),
+// else a pinned host-pool allocation - charged as spill and to the host budget, and records
+// it. spill_release undoes it for a pointer the shim spilled (false: not a spill).
+hsa_status_t spill_allocate(int dev, size_t size, void** ptr);
+bool spill_release(void* ptr);
+// Device memory of this process was freed: spills may fit into HBM now.
+void notify_device_memory_freed();
+// An SVM spill's GPU access list: hsa_amd_agents_allow_access on it (ROCr does not know the
+// range) becomes SVM access attributes. Returns false if `ptr` is not an SVM spill.
+bool svm_allow_access(const void* ptr, uint32_t n, const hsa_agent_t* agents, hsa_status_t* st);
+// Bytes of SVM spills of `dev` promoted into HBM that KFD's VRAM counter does not show
+// (resync_context_charge subtracts them from the tracked allocations).
+int64_t svm_hbm_outside_kfd(int dev);
+// Re-charges the SVM spills after the region was re-initialised (check_region_epoch).
+void svm_recharge(int slot, uint64_t* host);
+// Forgets the parent's SVM spills in a forked child (the ranges are not inherited).
+void svm_forget();
 
 // Drops the pinned host-memory charge of `p` (host_hooks.cpp) if the shim recorded it:
 // called after the runtime freed or unregistered it, through whichever entry point.

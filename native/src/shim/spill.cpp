@@ -1,0 +1,391 @@
+// Virtual device memory that moves: spilled allocations live in host memory until the
+// tenant's HBM share has room for them again, then they are promoted into HBM at the same
+// address, contents intact.
+//
+// Reference: with CUDA_OVERSUBSCRIBE every allocation becomes managed memory
+// (server.go:505-507 → libvgpu.so cuMemoryAllocate@0x32146, allocmode 0 →
+// cuMemAllocManaged) and the UVM driver moves hot pages back into device memory on demand.
+// MI355X has no recoverable GPU page faults on this pool (XNACK off), so nothing moves on
+// access. What KFD does have without XNACK is shared virtual memory (SVM): an ordinary range
+// of the process's host memory registered for a GPU (hsa_amd_svm_attributes_set) is mapped
+// into the GPU's page table in place, and hsa_amd_svm_prefetch_async migrates it into VRAM
+// and back. The driver performs the migration with the process's queues evicted around it
+// and restores the mapping before they resume, so a kernel never sees a half-moved range
+// and no user-level stop-the-world is needed (a VMM re-map could not give that guarantee
+// for work already queued).
+//
+// Placement: a spill is an anonymous mapping (MADV_DONTFORK: a forked child neither shares
+// nor copies it) registered for the owning GPU in place with host memory preferred; it is
+// charged as spill to the device quota and to the container's host budget, like the pinned
+// spill it replaces (VGPU_SPILL_BACKING=pinned keeps that: a host-pool allocation, reachable
+// by the GPU, that never moves). Promotion: a per-process thread (started with the first SVM
+// spill) checks every period - and at once when the process frees device memory - whether
+// the oldest spills fit: under the tenant's HBM share (VGPU_DEVICE_HBM_LIMIT_<i>) less the
+// large-first reserve, and in the GPU's free HBM less the same reserve (other tenants'
+// allocations come first). A promoted spill is charged as HBM data and released from the
+// host budget; a failed migration (the driver refused, HBM went to someone else) is undone
+// and retried after a back-off. Promoted ranges stay in HBM until freed.
+#include <errno.h>
+#include <pthread.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <vector>
+
+#include "real.h"
+#include "shim.h"
+#include "vgpu/kfd.h"
+#include "vgpu/log.h"
+#include "vgpu/ratelimit.h"
+
+namespace vgpu {
+
+namespace {
+
+constexpr uint64_t kPromoteBytesPerTick = 8ull << 30;        // migrated per period at most
+constexpr uint64_t kMigrateTimeoutNs = 60'000'000'000ull;    // one range's migration
+constexpr uint64_t kRetryBackoffNs = 10'000'000'000ull;      // after a failed promotion
+
+std::atomic<uint64_t> g_seq{0};
+std::atomic<bool> g_migrator{false};
+std::mutex g_wake_mu;
+std::condition_variable g_wake_cv;
+bool g_wake = false;
+
+// The driver has SVM and ROCr exposes it (checked once per process).
+bool svm_supported() {
+  static std::once_flag once;
+  static bool ok = false;
+  std::call_once(once, [] {
+    VGPU_REAL_HSA(hsa_system_get_info);
+    VGPU_REAL_HSA(hsa_amd_svm_attributes_set);
+    VGPU_REAL_HSA(hsa_amd_svm_attributes_get);
+    VGPU_REAL_HSA(hsa_amd_svm_prefetch_async);
+    VGPU_REAL_HSA(hsa_signal_create);
+    VGPU_REAL_HSA(hsa_signal_destroy);
+    VGPU_REAL_HSA(hsa_signal_wait_scacquire);
+    bool b = false;
+    ok = real_hsa_system_get_info && real_hsa_amd_svm_attributes_set && real_hsa_amd_svm_attributes_get &&
+         real_hsa_amd_svm_prefetch_async && real_hsa_signal_create && real_hsa_signal_destroy &&
+         real_hsa_signal_wait_scacquire &&
+         real_hsa_system_get_info((hsa_system_info_t)HSA_AMD_SYSTEM_INFO_SVM_SUPPORTED, &b) == HSA_STATUS_SUCCESS && b;
+    VLOG_INFO("virtual device memory: SVM ranges %s", ok ? "available (spills can be promoted into HBM)"
+                                                         : "unavailable (spills are pinned host memory)");
+  });
+  return ok;
+}
+
+size_t page_round(size_t n) {
+  const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+  return (n + pg - 1) / pg * pg;
+}
+
+bool accessible(uint64_t a) {
+  return a == HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE || a == HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE_IN_PLACE;
+}
+
+// An SVM range of `size` bytes the GPU of `dev` reaches in place, in host memory.
+hsa_status_t svm_map(int dev, size_t size, void** ptr, size_t* mapped) {
+  ShimState& s = shim();
+  const AgentInfo& a = s.agents[dev];
+  VGPU_REAL_HSA(hsa_amd_svm_attributes_set);
+  VGPU_REAL_HSA(hsa_amd_svm_attributes_get);
+  const size_t len = page_round(size);
+  void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (p == MAP_FAILED) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  madvise(p, len, MADV_DONTFORK);
+  hsa_amd_svm_attribute_pair_t attrs[2] = {{HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE_IN_PLACE, a.agent.handle},
+                                           {HSA_AMD_SVM_ATTRIB_PREFERRED_LOCATION, a.cpu_agent.handle}};
+  hsa_status_t st = real_hsa_amd_svm_attributes_set(p, len, attrs, 2);
+  // Used by a kernel only once the driver reports the GPU's access (no access = a fault).
+  hsa_amd_svm_attribute_pair_t q[1] = {{HSA_AMD_SVM_ATTRIB_ACCESS_QUERY, a.agent.handle}};
+  if (st == HSA_STATUS_SUCCESS) st = real_hsa_amd_svm_attributes_get(p, len, q, 1);
+  if (st == HSA_STATUS_SUCCESS && !accessible(q[0].attribute)) st = HSA_STATUS_ERROR_INVALID_AGENT;
+  if (st != HSA_STATUS_SUCCESS) {
+    munmap(p, len);
+    return st;
+  }
+  *ptr = p;
+  *mapped = len;
+  return HSA_STATUS_SUCCESS;
+}
+
+void wake_migrator() {
+  {
+    std::lock_guard<std::mutex> g(g_wake_mu);
+    g_wake = true;
+  }
+  g_wake_cv.notify_one();
+}
+
+// Migrates [p, p+len) to `agent` (a GPU or the CPU); true once the driver completed it.
+bool migrate(void* p, size_t len, hsa_agent_t agent) {
+  VGPU_REAL_HSA(hsa_amd_svm_attributes_set);
+  VGPU_REAL_HSA(hsa_amd_svm_prefetch_async);
+  VGPU_REAL_HSA(hsa_signal_create);
+  VGPU_REAL_HSA(hsa_signal_destroy);
+  VGPU_REAL_HSA(hsa_signal_wait_scacquire);
+  hsa_amd_svm_attribute_pair_t pref[1] = {{HSA_AMD_SVM_ATTRIB_PREFERRED_LOCATION, agent.handle}};
+  if (real_hsa_amd_svm_attributes_set(p, len, pref, 1) != HSA_STATUS_SUCCESS) return false;
+  hsa_signal_t sig;
+  if (real_hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) return false;
+  bool ok = false;
+  if (real_hsa_amd_svm_prefetch_async(p, len, agent, 0, nullptr, sig) == HSA_STATUS_SUCCESS)
+    ok = real_hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, kMigrateTimeoutNs, HSA_WAIT_STATE_BLOCKED) == 0;
+  real_hsa_signal_destroy(sig);
+  return ok;
+}
+
+// Promotes the SVM spills of `dev` that fit, oldest first; returns the bytes moved.
+uint64_t promote_device(int dev, uint64_t budget) {
+  ShimState& s = shim();
+  const Config& cfg = config();
+  AgentInfo& a = s.agents[dev];
+  const uint64_t share = s.region.hbm_limit(dev);
+  const uint64_t reserve = share ? spill_reserve(cfg, share) : 0;
+  std::vector<std::pair<uint64_t, uintptr_t>> order;  // (seq, ptr) of the spills in host memory
+  const uint64_t now = now_ns();
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    for (const auto& kv : s.svm)
+      if (kv.second.dev == dev && !kv.second.in_hbm && kv.second.retry_ns <= now)
+        order.emplace_back(kv.second.seq, kv.first);
+  }
+  if (order.empty()) return 0;
+  std::sort(order.begin(), order.end());
+  VGPU_REAL_HSA(hsa_agent_get_info);
+  uint64_t moved = 0;
+  for (const auto& o : order) {
+    if (moved >= budget || s.exiting.load()) break;
+    std::lock_guard<std::mutex> mg(s.svm_mu);  // a free of this range waits for its migration
+    SvmRec rec;
+    {
+      std::lock_guard<std::mutex> g(s.alloc_mu);
+      auto it = s.svm.find(o.second);
+      if (it == s.svm.end() || it->second.in_hbm) continue;
+      rec = it->second;
+    }
+    // Room under the share (the range counts as resident once moved) and in the GPU's HBM.
+    const uint64_t resident = s.region.resident(dev);
+    if (share && resident + rec.size + reserve > share) break;
+    uint64_t avail = 0;
+    if (real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &avail) !=
+            HSA_STATUS_SUCCESS ||
+        avail < rec.mapped + reserve)
+      break;
+    void* p = reinterpret_cast<void*>(o.second);
+    // The context charge (KFD VRAM less the tracked allocations) must not see the pages
+    // arrive before the charge moves: both under ctx_mu.
+    std::lock_guard<std::mutex> cg(s.ctx_mu);
+    const int64_t vram0 = s.hostpid && a.gpu_id ? kfd_vram_usage(s.hostpid, a.gpu_id) : -1;
+    s.region.uncharge(s.slot, dev, rec.size, kMemSpill);
+    s.region.force_charge(s.slot, dev, rec.size, kMemData);
+    const uint64_t t0 = now_ns();
+    if (!migrate(p, rec.mapped, a.agent)) {
+      s.region.uncharge(s.slot, dev, rec.size, kMemData);
+      s.region.force_charge(s.slot, dev, rec.size, kMemSpill);
+      migrate(p, rec.mapped, a.cpu_agent);  // whatever moved goes back; host memory preferred again
+      std::lock_guard<std::mutex> g(s.alloc_mu);
+      auto it = s.svm.find(o.second);
+      if (it != s.svm.end()) it->second.retry_ns = now_ns() + kRetryBackoffNs;
+      VLOG_WARN("device %d: %lu spilled bytes at %p could not be promoted into HBM; retrying later", dev,
+                (unsigned long)rec.size, p);
+      continue;
+    }
+    const int64_t vram1 = vram0 >= 0 ? kfd_vram_usage(s.hostpid, a.gpu_id) : -1;
+    if (s.svm_kfd_vram < 0 && vram0 >= 0 && vram1 >= 0)
+      s.svm_kfd_vram = vram1 - vram0 >= (int64_t)rec.mapped / 2 ? 1 : 0;
+    s.svm_hbm[dev] += (int64_t)rec.size;
+    s.region.uncharge_host(s.slot, rec.size);
+    {
+      std::lock_guard<std::mutex> g(s.alloc_mu);
+      auto it = s.svm.find(o.second);
+      if (it != s.svm.end()) it->second.in_hbm = true;
+    }
+    moved += rec.size;
+    VLOG_INFO("device %d: %lu spilled bytes at %p promoted into HBM in %.1f ms", dev, (unsigned long)rec.size, p,
+              (now_ns() - t0) / 1e6);
+  }
+  return moved;
+}
+
+void* migrator_main(void*) {
+  ShimState& s = shim();
+  const pid_t me = s.pid;
+  const uint64_t period_ns = (uint64_t)std::max(config().util_period_ms, 10) * 1'000'000ull;
+  while (!s.exiting.load() && s.pid == me) {
+    {
+      std::unique_lock<std::mutex> g(g_wake_mu);
+      g_wake_cv.wait_for(g, std::chrono::nanoseconds(period_ns), [] { return g_wake; });
+      g_wake = false;
+    }
+    if (s.exiting.load() || !s.active || s.slot < 0) continue;
+    uint64_t budget = kPromoteBytesPerTick;
+    for (int d = 0; d < s.n_agents && budget; d++) budget -= std::min(budget, promote_device(d, budget));
+  }
+  return nullptr;
+}
+
+void start_migrator() {
+  bool expected = false;
+  if (!config().spill_promote || !g_migrator.compare_exchange_strong(expected, true)) return;
+  pthread_t th;
+  pthread_attr_t attr;
+  pthread_attr_init(&attr);
+  pthread_attr_setdetachstate(&attr, PTHREAD_CREATE_DETACHED);
+  if (pthread_create(&th, &attr, migrator_main, nullptr) != 0) {
+    VLOG_ERROR("cannot start the spill migration thread; spills stay in host memory");
+    g_migrator.store(false);
+  }
+  pthread_attr_destroy(&attr);
+}
+
+hsa_status_t pinned_spill(int dev, size_t size, void** ptr) {
+  ShimState& s = shim();
+  AgentInfo& a = s.agents[dev];
+  if (!a.spill_pool.handle) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  VGPU_REAL_HSA(hsa_amd_memory_pool_allocate);
+  VGPU_REAL_HSA(hsa_amd_agents_allow_access);
+  VGPU_REAL_HSA(hsa_amd_memory_pool_free);
+  hsa_status_t st = real_hsa_amd_memory_pool_allocate(a.spill_pool, size, 0, ptr);
+  if (st != HSA_STATUS_SUCCESS) return st;
+  st = real_hsa_amd_agents_allow_access(1, &a.agent, nullptr, *ptr);
+  if (st != HSA_STATUS_SUCCESS) {
+    real_hsa_amd_memory_pool_free(*ptr);
+    *ptr = nullptr;
+  }
+  return st;
+}
+
+}  // namespace
+
+// Spilled bytes are host memory the container holds: they count against its host budget
+// (VGPU_HOST_MEMORY_LIMIT, shared with hipHostMalloc / hipHostRegister), so the RAM an
+// oversubscribed vGPU takes is bounded like any other (plugin/host_memory.py sizes the
+// budget and refuses scalings the node cannot back). The caller has charged `size` as data.
+hsa_status_t spill_allocate(int dev, size_t size, void** ptr) {
+  ShimState& s = shim();
+  const Config& cfg = config();
+  if (s.region.charge_host(s.slot, size) != Charge::kOk) {
+    VLOG_WARN("device %d: %zu bytes cannot spill: host memory budget %lu (in use %lu) is used up", dev, size,
+              (unsigned long)s.region.host_limit(), (unsigned long)s.region.host_usage());
+    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  }
+  hsa_status_t st = HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  const bool want_svm = cfg.spill_backing != SpillBacking::kPinned && s.agents[dev].cpu_agent.handle;
+  if (want_svm && svm_supported()) {
+    size_t mapped = 0;
+    st = svm_map(dev, size, ptr, &mapped);
+    if (st == HSA_STATUS_SUCCESS) {
+      s.region.uncharge(s.slot, dev, size, kMemData);
+      s.region.force_charge(s.slot, dev, size, kMemSpill);
+      {
+        std::lock_guard<std::mutex> g(s.alloc_mu);
+        s.svm[reinterpret_cast<uintptr_t>(*ptr)] = SvmRec{size, mapped, dev, false, g_seq.fetch_add(1), 0};
+      }
+      VLOG_INFO("device %d: %zu bytes spilled to host memory at %p (SVM, promotable)", dev, size, *ptr);
+      start_migrator();
+      return st;
+    }
+    VLOG_WARN("device %d: SVM spill of %zu bytes refused (status %d)%s", dev, size, (int)st,
+              cfg.spill_backing == SpillBacking::kSvm ? "" : "; using pinned host memory");
+  }
+  if (cfg.spill_backing != SpillBacking::kSvm) st = pinned_spill(dev, size, ptr);
+  if (st != HSA_STATUS_SUCCESS) {
+    s.region.uncharge_host(s.slot, size);
+    return st;
+  }
+  s.region.uncharge(s.slot, dev, size, kMemData);
+  s.region.force_charge(s.slot, dev, size, kMemSpill);
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    s.allocs[reinterpret_cast<uintptr_t>(*ptr)] = AllocRec{size, dev, kMemSpill};
+  }
+  VLOG_INFO("device %d: %zu bytes spilled to pinned host memory at %p", dev, size, *ptr);
+  return HSA_STATUS_SUCCESS;
+}
+
+bool spill_release(void* ptr) {
+  ShimState& s = shim();
+  if (!ptr) return false;
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    if (!s.svm.count(reinterpret_cast<uintptr_t>(ptr))) return false;
+  }
+  std::lock_guard<std::mutex> mg(s.svm_mu);  // not while the range migrates
+  SvmRec rec;
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    auto it = s.svm.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == s.svm.end()) return true;  // freed concurrently
+    rec = it->second;
+    s.svm.erase(it);
+  }
+  if (s.slot >= 0 && !s.exiting.load()) {
+    if (rec.in_hbm) {
+      std::lock_guard<std::mutex> cg(s.ctx_mu);
+      s.region.uncharge(s.slot, rec.dev, rec.size, kMemData);
+      s.svm_hbm[rec.dev] -= (int64_t)rec.size;
+    } else {
+      s.region.uncharge(s.slot, rec.dev, rec.size, kMemSpill);
+      s.region.uncharge_host(s.slot, rec.size);
+    }
+  }
+  munmap(ptr, rec.mapped);  // KFD drops the range (and its VRAM) with the mapping
+  return true;
+}
+
+void notify_device_memory_freed() {
+  if (g_migrator.load(std::memory_order_relaxed)) wake_migrator();
+}
+
+bool svm_allow_access(const void* ptr, uint32_t n, const hsa_agent_t* agents, hsa_status_t* st) {
+  ShimState& s = shim();
+  size_t mapped = 0;
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    auto it = s.svm.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == s.svm.end()) return false;
+    mapped = it->second.mapped;
+  }
+  VGPU_REAL_HSA(hsa_amd_svm_attributes_set);
+  std::vector<hsa_amd_svm_attribute_pair_t> attrs;
+  for (uint32_t i = 0; i < n; i++) attrs.push_back({HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE_IN_PLACE, agents[i].handle});
+  *st = attrs.empty() ? HSA_STATUS_SUCCESS
+                      : real_hsa_amd_svm_attributes_set(const_cast<void*>(ptr), mapped, attrs.data(), attrs.size());
+  return true;
+}
+
+int64_t svm_hbm_outside_kfd(int dev) {
+  ShimState& s = shim();
+  return s.svm_kfd_vram == 1 ? 0 : s.svm_hbm[dev];
+}
+
+void svm_recharge(int slot, uint64_t* host) {
+  ShimState& s = shim();
+  for (const auto& kv : s.svm) {
+    if (kv.second.in_hbm) {
+      s.region.force_charge(slot, kv.second.dev, kv.second.size, kMemData);
+    } else {
+      s.region.force_charge(slot, kv.second.dev, kv.second.size, kMemSpill);
+      *host += kv.second.size;
+    }
+  }
+}
+
+void svm_forget() {
+  ShimState& s = shim();
+  s.svm.clear();
+  for (auto& b : s.svm_hbm) b = 0;
+  new (&s.svm_mu) std::mutex();
+  g_migrator.store(false);
+  new (&g_wake_mu) std::mutex();
+  g_wake = false;
+}
+
+}  // namespace vgpu

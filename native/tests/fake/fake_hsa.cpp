@@ -17,9 +17,13 @@
 //                       partitions exposed as GPUs: consecutive agents share a BDF)
 //   FAKE_KFD_ROOT       fake /sys/class/kfd/kfd/proc (unset: no KFD tree)
 //   FAKE_KFD_PID_OFFSET host-PID offset (default 100000)
+//   FAKE_ROCR_NO_SVM    1: no shared virtual memory (hsa_amd_svm_* refuse, SVM_SUPPORTED false)
+//   FAKE_SVM_FAIL       1: every SVM prefetch into a GPU fails (the completion signal goes negative)
+//   FAKE_SVM_KFD_VRAM   0: SVM ranges migrated into HBM are not in KFD's vram_<gpu_id> (default 1)
 // Test-only introspection: fake_rocr_* functions below.
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <errno.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -56,6 +60,15 @@ struct FakeQueue {
   int priority;
 };
 
+// An SVM range: the application's own host memory registered for GPU access. Its pages are
+// real memory (the caller's mapping), so data survives a "migration", which only moves the
+// range's location and its bytes in and out of the GPU's HBM.
+struct SvmRange {
+  uint64_t size = 0;
+  std::map<uint64_t, uint64_t> access;  // agent -> access attribute
+  uint64_t pref = 0, loc = 0;           // preferred / current location (agent handle, 0 = host)
+};
+
 struct State {
   int n = 2;
   int cus = 256, xcc = 8, se = 32, parts = 1;
@@ -63,6 +76,7 @@ struct State {
   std::mutex mu;
   std::map<uintptr_t, std::pair<int, uint64_t>> allocs;  // ptr -> (dev or -1 for host, size)
   std::map<uintptr_t, FakeQueue*> queues;
+  std::map<uintptr_t, SvmRange> svm;
   char* arena = nullptr;
   uint64_t arena_size = 0, arena_next = 0;
   std::string kfd;  // fake KFD process dir of this process ("" = none)
@@ -155,6 +169,28 @@ void* bump(uint64_t size) {
   return p;
 }
 
+bool svm_on() { return !env_u64("FAKE_ROCR_NO_SVM", 0); }
+
+// Drops SVM ranges whose memory the application unmapped (KFD learns of it through its MMU
+// notifier): a range in HBM gives its bytes back. Caller holds the state lock.
+void svm_gc() {
+  State& s = st();
+  const long pg = sysconf(_SC_PAGESIZE);
+  for (auto it = s.svm.begin(); it != s.svm.end();) {
+    unsigned char v;
+    if (mincore(reinterpret_cast<void*>(it->first), (size_t)pg, &v) != 0 && errno == ENOMEM) {
+      const int d = gpu_of(hsa_agent_t{it->second.loc});
+      if (d >= 0) {
+        s.gpus[d].used.fetch_sub(it->second.size);
+        if (env_u64("FAKE_SVM_KFD_VRAM", 1)) kfd_update_vram(d);
+      }
+      it = s.svm.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -200,6 +236,10 @@ hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* 
     case HSA_AMD_AGENT_INFO_BDFID: *static_cast<uint32_t*>(value) = (uint32_t)(0x05 + 0x10 * (d / s.parts)) << 8; break;
     case HSA_AMD_AGENT_INFO_DOMAIN: *static_cast<uint32_t*>(value) = 0; break;
     case HSA_AMD_AGENT_INFO_MEMORY_AVAIL: {
+      {
+        std::lock_guard<std::mutex> g(s.mu);
+        svm_gc();
+      }
       uint64_t u = s.gpus[d].used.load();
       *static_cast<uint64_t*>(value) = s.gpus[d].hbm > u ? s.gpus[d].hbm - u : 0;
       break;
@@ -394,6 +434,105 @@ hsa_status_t hsa_amd_ipc_memory_attach(const hsa_amd_ipc_memory_t*, size_t len, 
 
 hsa_status_t hsa_amd_ipc_memory_detach(void*) { return HSA_STATUS_SUCCESS; }
 
+hsa_status_t hsa_system_get_info(hsa_system_info_t attr, void* value) {
+  switch ((int)attr) {
+    case HSA_AMD_SYSTEM_INFO_SVM_SUPPORTED: *static_cast<bool*>(value) = svm_on(); return HSA_STATUS_SUCCESS;
+    case HSA_AMD_SYSTEM_INFO_SVM_ACCESSIBLE_BY_DEFAULT: *static_cast<bool*>(value) = false; return HSA_STATUS_SUCCESS;
+    case HSA_AMD_SYSTEM_INFO_XNACK_ENABLED: *static_cast<bool*>(value) = false; return HSA_STATUS_SUCCESS;
+    default: return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  }
+}
+
+// Signals: every fake asynchronous operation completes before it returns, so a wait only
+// reads the value.
+hsa_status_t hsa_signal_create(hsa_signal_value_t initial, uint32_t, const hsa_agent_t*, hsa_signal_t* sig) {
+  sig->handle = reinterpret_cast<uint64_t>(new std::atomic<int64_t>(initial));
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t hsa_signal_destroy(hsa_signal_t sig) {
+  delete reinterpret_cast<std::atomic<int64_t>*>(sig.handle);
+  return HSA_STATUS_SUCCESS;
+}
+hsa_signal_value_t hsa_signal_wait_scacquire(hsa_signal_t sig, hsa_signal_condition_t, hsa_signal_value_t, uint64_t,
+                                             hsa_wait_state_t) {
+  return reinterpret_cast<std::atomic<int64_t>*>(sig.handle)->load();
+}
+void hsa_signal_store_relaxed(hsa_signal_t sig, hsa_signal_value_t v) {
+  reinterpret_cast<std::atomic<int64_t>*>(sig.handle)->store(v);
+}
+
+hsa_status_t hsa_amd_svm_attributes_set(void* ptr, size_t size, hsa_amd_svm_attribute_pair_t* list, size_t n) {
+  if (!svm_on()) return HSA_STATUS_ERROR;
+  setup();
+  std::lock_guard<std::mutex> g(st().mu);
+  svm_gc();
+  SvmRange& r = st().svm[reinterpret_cast<uintptr_t>(ptr)];
+  r.size = size;
+  for (size_t i = 0; i < n; i++) {
+    switch (list[i].attribute) {
+      case HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE:
+      case HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE_IN_PLACE: r.access[list[i].value] = list[i].attribute; break;
+      case HSA_AMD_SVM_ATTRIB_AGENT_NO_ACCESS: r.access.erase(list[i].value); break;
+      case HSA_AMD_SVM_ATTRIB_PREFERRED_LOCATION: r.pref = list[i].value; break;
+      case HSA_AMD_SVM_ATTRIB_GLOBAL_FLAG: case HSA_AMD_SVM_ATTRIB_READ_ONLY: case HSA_AMD_SVM_ATTRIB_GPU_EXEC: break;
+      default: return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+    }
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_amd_svm_attributes_get(void* ptr, size_t, hsa_amd_svm_attribute_pair_t* list, size_t n) {
+  if (!svm_on()) return HSA_STATUS_ERROR;
+  std::lock_guard<std::mutex> g(st().mu);
+  auto it = st().svm.find(reinterpret_cast<uintptr_t>(ptr));
+  for (size_t i = 0; i < n; i++) {
+    switch (list[i].attribute) {
+      case HSA_AMD_SVM_ATTRIB_ACCESS_QUERY: {
+        uint64_t a = HSA_AMD_SVM_ATTRIB_AGENT_NO_ACCESS;
+        if (it != st().svm.end() && it->second.access.count(list[i].value)) a = it->second.access[list[i].value];
+        list[i].attribute = a;
+        break;
+      }
+      case HSA_AMD_SVM_ATTRIB_PREFERRED_LOCATION: list[i].value = it != st().svm.end() ? it->second.pref : 0; break;
+      case HSA_AMD_SVM_ATTRIB_PREFETCH_LOCATION: list[i].value = it != st().svm.end() ? it->second.loc : 0; break;
+      default: return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+    }
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t hsa_amd_svm_prefetch_async(void* ptr, size_t size, hsa_agent_t agent, uint32_t, const hsa_signal_t*,
+                                        hsa_signal_t done) {
+  if (!svm_on()) return HSA_STATUS_ERROR;
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  svm_gc();
+  auto it = s.svm.find(reinterpret_cast<uintptr_t>(ptr));
+  if (it == s.svm.end()) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  SvmRange& r = it->second;
+  auto* sig = reinterpret_cast<std::atomic<int64_t>*>(done.handle);
+  const int to = gpu_of(agent), from = gpu_of(hsa_agent_t{r.loc});
+  const bool counted = env_u64("FAKE_SVM_KFD_VRAM", 1) != 0;
+  bool ok = to != from || to < 0;
+  if (to >= 0 && to != from && (env_u64("FAKE_SVM_FAIL", 0) || s.gpus[to].used.load() + size > s.gpus[to].hbm)) ok = false;
+  if (ok && to != from) {
+    if (from >= 0) {
+      s.gpus[from].used.fetch_sub(r.size);
+      if (counted) kfd_update_vram(from);
+    }
+    if (to >= 0) {
+      s.gpus[to].used.fetch_add(r.size);
+      if (counted) kfd_update_vram(to);
+    }
+    r.loc = to >= 0 ? agent.handle : 0;
+  }
+  if (sig) {
+    if (ok) sig->fetch_sub(1);
+    else sig->store(-1);
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
 // ---------------------------------------------------------------- test introspection
 // CU mask and priority last applied to `queue`; returns the number of mask changes.
 int fake_rocr_queue_state(const hsa_queue_t* queue, uint32_t* mask_words8, int* priority, int* device) {
@@ -407,7 +546,20 @@ int fake_rocr_queue_state(const hsa_queue_t* queue, uint32_t* mask_words8, int* 
 }
 
 // Bytes the fake runtime holds on GPU `dev` (what a real driver would report).
-uint64_t fake_rocr_used(int dev) { return dev >= 0 && dev < st().n ? st().gpus[dev].used.load() : 0; }
+uint64_t fake_rocr_used(int dev) {
+  {
+    std::lock_guard<std::mutex> g(st().mu);
+    svm_gc();
+  }
+  return dev >= 0 && dev < st().n ? st().gpus[dev].used.load() : 0;
+}
+
+// Where the SVM range at `ptr` lives: the GPU ordinal, -1 = host memory, -2 = not a range.
+int fake_rocr_svm_location(const void* ptr) {
+  std::lock_guard<std::mutex> g(st().mu);
+  auto it = st().svm.find(reinterpret_cast<uintptr_t>(ptr));
+  return it == st().svm.end() ? -2 : gpu_of(hsa_agent_t{it->second.loc});
+}
 
 // Memory the runtime allocates internally (scratch, code objects): bypasses every
 // allocation entry point, shows up only in KFD's per-process VRAM counter.

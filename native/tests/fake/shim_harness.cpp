@@ -39,6 +39,13 @@
 //                    call never reached the runtime}
 //   hostmalloc=SIZE  hipHostMalloc -> {"hostmalloc": "ok"|"oom"}; hostfree frees the last one
 //                    (hostfree_hipfree: through hipFree, which releases pinned memory too)
+//   freeidx=I        hipFree of the I-th successful allocation (of all made so far)
+//   fill=B / check=B the CPU writes byte B into / checks byte B in every byte of the most
+//                    recent allocation (spilled SVM memory only: the fake's HBM is not
+//                    mapped) -> {"check": "ok"|"bad"}
+//   where            where the most recent allocation lives: {"where": gpu ordinal, -1 = host
+//                    memory (an SVM range), -2 = not an SVM range}
+//   spilled          the shim's vgpu_get_current_device_spilled: {"spilled": bytes}
 //   hostregister=SIZE  hipHostRegister of a fresh heap buffer -> {"hostregister": "ok"|"oom"};
 //                    hostunregister unregisters (and frees) the last one
 #define __HIP_PLATFORM_AMD__ 1
@@ -48,6 +55,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 
 #include <chrono>
@@ -66,6 +74,7 @@ int fake_rocr_internal_alloc(int dev, int64_t bytes);
 int fake_rocr_host_pid();
 int fake_hip_device_cus(int dev);
 const char* fake_hip_last_call();
+int fake_rocr_svm_location(const void* ptr);
 }
 
 namespace {
@@ -153,7 +162,8 @@ int main(int argc, char** argv) {
   if (hipInit(0) != hipSuccess) return 1;
   int dev = 0;
   hipStream_t stream = nullptr;
-  std::vector<void*> ptrs;
+  std::vector<void*> ptrs, all_ptrs;
+  std::vector<size_t> sizes;
   std::vector<hipStream_t> streams;
   std::vector<void*> host_ptrs, registered;
   static uint32_t kernel_us[64];
@@ -170,14 +180,46 @@ int main(int argc, char** argv) {
     } else if (key == "malloc") {
       void* p = nullptr;
       hipError_t e = hipMalloc(&p, (size_t)parse_size(val.c_str()));
-      if (e == hipSuccess) ptrs.push_back(p);
+      if (e == hipSuccess) {
+        ptrs.push_back(p);
+        all_ptrs.push_back(p);
+        sizes.push_back((size_t)parse_size(val.c_str()));
+      }
       printf("{\"malloc\": \"%s\", \"bytes\": %lld}\n", e == hipSuccess ? "ok" : "oom", parse_size(val.c_str()));
     } else if (key == "free") {
       if (!ptrs.empty()) {
         (void)hipFree(ptrs.back());
+        std::replace(all_ptrs.begin(), all_ptrs.end(), ptrs.back(), static_cast<void*>(nullptr));
         ptrs.pop_back();
       }
       printf("{\"free\": true}\n");
+    } else if (key == "freeidx") {
+      const size_t i = (size_t)atoi(val.c_str());
+      if (i < all_ptrs.size() && all_ptrs[i]) {
+        (void)hipFree(all_ptrs[i]);
+        for (size_t j = 0; j < ptrs.size(); j++)
+          if (ptrs[j] == all_ptrs[i]) ptrs.erase(ptrs.begin() + (long)j);
+        all_ptrs[i] = nullptr;
+      }
+      printf("{\"freeidx\": %zu}\n", i);
+    } else if (key == "fill" || key == "check") {
+      const int b = atoi(val.c_str());
+      size_t bad = 0;
+      if (!ptrs.empty()) {
+        unsigned char* p = static_cast<unsigned char*>(ptrs.back());
+        const size_t n = sizes[std::find(all_ptrs.begin(), all_ptrs.end(), ptrs.back()) - all_ptrs.begin()];
+        if (key == "fill") memset(p, b, n);
+        else
+          for (size_t j = 0; j < n; j++) bad += p[j] != (unsigned char)b;
+      }
+      if (key == "fill") printf("{\"fill\": %d}\n", b);
+      else printf("{\"check\": \"%s\", \"bad\": %zu}\n", bad || ptrs.empty() ? "bad" : "ok", bad);
+    } else if (key == "where") {
+      printf("{\"where\": %d}\n", ptrs.empty() ? -2 : fake_rocr_svm_location(ptrs.back()));
+    } else if (key == "spilled") {
+      using Get = uint64_t (*)();
+      auto f = reinterpret_cast<Get>(dlsym(RTLD_DEFAULT, "vgpu_get_current_device_spilled"));
+      printf("{\"spilled\": %llu}\n", f ? (unsigned long long)f() : 0ull);
     } else if (key == "meminfo") {
       size_t f = 0, t = 0;
       (void)hipMemGetInfo(&f, &t);

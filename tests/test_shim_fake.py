@@ -242,6 +242,79 @@ def test_spill_is_charged_to_the_host_budget(fake):
     assert got == ["ok"] * 4 + ["ok", "ok", "ok", "oom", "ok"], out
 
 
+def _svm_env(fake, **kw):
+    # 64 MiB HBM share of a 256 MiB quota (reserve 16 MiB), first-come: the second buffer spills.
+    return fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="256m", VGPU_DEVICE_HBM_LIMIT_0="64m",
+                VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come", VGPU_HOST_MEMORY_LIMIT="128m", **kw)
+
+
+@pytest.mark.parametrize("kfd_counts", ["1", "0"])
+def test_svm_spill_is_promoted_when_the_share_frees_up(fake, kfd_counts):
+    """Virtual device memory that moves: a buffer spilled past the HBM share is an SVM range
+    (host memory the GPU reaches in place); once the buffer ahead of it is freed, the
+    migration thread promotes it into HBM at the same address - contents intact, the spill
+    counter back to 0, charged as HBM data (whether or not KFD's VRAM counter shows the
+    migrated pages), and its HBM charge released with it."""
+    e = _svm_env(fake, FAKE_SVM_KFD_VRAM=kfd_counts)
+    out = run(e, "malloc=48m", "malloc=32m", "where", "spilled", "fill=90", "freeidx=0", "sleep=0.6", "where",
+              "spilled", "check=90", "meminfo", "free", "meminfo", "sleep=0.3", "meminfo")
+    where = [o["where"] for o in out if "where" in o]
+    spilled = [o["spilled"] for o in out if "spilled" in o]
+    infos = [o for o in out if "free" in o and "total" in o]
+    assert [o["malloc"] for o in out if "malloc" in o] == ["ok", "ok"]
+    assert where == [-1, 0], out          # host memory, then GPU 0's HBM
+    assert spilled == [32 * MiB, 0], out
+    assert [o for o in out if "check" in o][0]["check"] == "ok"
+    assert infos[0]["free"] == 256 * MiB - 32 * MiB, infos   # charged once, as data
+    # KFD releases a freed range's VRAM after the unmap (the fake: at its next query); the
+    # context charge follows at the next resync.
+    assert infos[-1]["free"] == 256 * MiB, infos
+
+
+def test_svm_spill_waits_for_room(fake):
+    """Nothing was freed: the share (48 MiB resident + 32 + the 16 MiB reserve > 64 MiB)
+    has no room, so the spill stays in host memory."""
+    out = run(_svm_env(fake), "malloc=48m", "malloc=32m", "sleep=0.5", "where", "spilled")
+    assert [o["where"] for o in out if "where" in o] == [-1]
+    assert [o["spilled"] for o in out if "spilled" in o] == [32 * MiB]
+
+
+@pytest.mark.parametrize("how", ["pinned", "no-svm"])
+def test_pinned_spill_never_moves(fake, how):
+    """VGPU_SPILL_BACKING=pinned, or a driver without SVM: the spill is a pinned host-pool
+    allocation (not an SVM range) and stays in host memory after room frees up."""
+    kw = {"VGPU_SPILL_BACKING": "pinned"} if how == "pinned" else {"FAKE_ROCR_NO_SVM": "1"}
+    out = run(_svm_env(fake, **kw), "malloc=48m", "malloc=32m", "where", "freeidx=0", "sleep=0.5", "spilled")
+    assert [o["where"] for o in out if "where" in o] == [-2]
+    assert [o["spilled"] for o in out if "spilled" in o] == [32 * MiB]
+
+
+def test_failed_promotion_is_undone(fake):
+    """The driver refuses the migration: the spill stays in host memory, readable, charged as
+    spill and to the host budget exactly as before (no double charge)."""
+    out = run(_svm_env(fake, FAKE_SVM_FAIL="1"), "malloc=48m", "malloc=32m", "fill=7", "freeidx=0", "sleep=0.6",
+              "where", "spilled", "check=7", "meminfo")
+    assert [o["where"] for o in out if "where" in o] == [-1]
+    assert [o["spilled"] for o in out if "spilled" in o] == [32 * MiB]
+    assert [o for o in out if "check" in o][0]["check"] == "ok"
+    assert [o for o in out if "total" in o][0]["free"] == 256 * MiB - 32 * MiB
+
+
+def test_svm_spill_is_charged_to_the_host_budget(fake):
+    """An SVM spill draws on the host budget like a pinned one (128 MiB here): a spill past it
+    is refused; after a promotion its host memory is given back and a spill fits again."""
+    e = _svm_env(fake, VGPU_SPILL_PROMOTE="0")
+    out = run(e, "malloc=48m", "malloc=64m", "malloc=64m", "malloc=64m")
+    assert [o["malloc"] for o in out if "malloc" in o] == ["ok", "ok", "ok", "oom"]
+    # 48 MiB resident, 40 MiB spilled; 96 MiB more would take the budget to 136 MiB: refused.
+    # Freeing the 48 MiB buffer lets the 40 MiB spill into HBM, which returns its host memory:
+    # the 96 MiB spill fits the budget now.
+    out = run(_svm_env(fake), "malloc=48m", "malloc=40m", "malloc=96m", "freeidx=0", "sleep=0.6", "spilled",
+              "malloc=96m", "spilled")
+    assert [o["malloc"] for o in out if "malloc" in o] == ["ok", "ok", "oom", "ok"]
+    assert [o["spilled"] for o in out if "spilled" in o] == [0, 96 * MiB]
+
+
 @pytest.mark.parametrize("mode,virt,want", [("spatial", "1", 64), ("spatial", "0", 256), ("temporal", "1", 256),
                                             ("auto", "1", 64)])
 def test_cu_count_follows_the_spatial_slice(fake, mode, virt, want):
