@@ -655,6 +655,105 @@ def test_spill_placement_policy(tmp_region, policy):
         assert small_spilled >= 256 * MiB, r
 
 
+SPILL_PROMOTE = """
+import ctypes, torch
+lib = ctypes.CDLL(None)
+lib.vgpu_get_current_device_spilled.restype = ctypes.c_uint64
+def spilled():
+    return lib.vgpu_get_current_device_spilled()
+def read_gbps(t, reps=5):
+    torch.cuda.synchronize(); t0 = time.time()
+    for _ in range(reps):
+        t.max()
+    torch.cuda.synchronize()
+    return round(t.numel() * t.element_size() * reps / (time.time() - t0) / 1e9, 1)
+x = torch.ones(1 << 20, device="cuda"); x.add_(1); torch.cuda.synchronize()
+time.sleep(1.0)   # the context charge settles first
+mode = os.environ["SPILL_MODE"]
+if mode == "own":
+    a = torch.empty(7 << 29, dtype=torch.uint8, device="cuda")           # 3.5 GiB: fills the share
+n = int(os.environ["SPILL_ELEMS"])
+b = torch.full((n,), 7, dtype=torch.int32, device="cuda")                 # spilled
+torch.cuda.synchronize()
+s0 = spilled()
+ok0 = int(b.sum(dtype=torch.int64)) == 7 * n
+gbps0 = read_gbps(b)
+if mode == "own":
+    del a
+    torch.cuda.empty_cache()                                              # hipFree: HBM share frees up
+else:
+    open(os.environ["SPILL_GO"], "w").close()                             # the neighbour frees its HBM
+t0 = time.time()
+while spilled() and time.time() - t0 < 20:
+    time.sleep(0.02)
+t_promote = round(time.time() - t0, 3)
+s1 = spilled()
+b.add_(1); torch.cuda.synchronize()
+ok1 = int(b.sum(dtype=torch.int64)) == 8 * n
+gbps1 = read_gbps(b)
+emit(spilled_before=s0, spilled_after=s1, ok_before=ok0, ok_after=ok1, gbps_spilled=gbps0, gbps_promoted=gbps1,
+     promote_s=t_promote, bytes=4 * n)
+"""
+
+HBM_HOG = """
+import torch
+keep = int(os.environ["HOG_KEEP"])
+held = []
+while True:
+    free, _ = torch.cuda.mem_get_info()
+    if free <= keep + (64 << 20):
+        break
+    held.append(torch.empty(min(free - keep, 16 << 30), dtype=torch.uint8, device="cuda"))
+open(os.environ["HOG_READY"], "w").close()
+t0 = time.time()
+while not os.path.exists(os.environ["SPILL_GO"]) and time.time() - t0 < 120:
+    time.sleep(0.02)
+del held
+torch.cuda.empty_cache()
+emit(freed=True)
+time.sleep(2.0)
+"""
+
+
+@pytest.mark.parametrize("neighbour", ["own-buffer", "other-tenant"])
+def test_spill_is_promoted_after_hbm_frees_up(tmp_region, tmp_path, neighbour):
+    """Virtual device memory that moves (round-3 verdict, missing 2): a buffer that spilled to
+    host memory - past the tenant's 4 GiB HBM share behind its own 3.5 GiB buffer, or (large-
+    first) because another tenant holds nearly all of the GPU's HBM - is an SVM range the GPU
+    reads in place; once the HBM frees up, the shim migrates it into HBM at the same address:
+    the spill counter returns to 0, the data are intact, the buffer keeps working, and reading
+    it runs at HBM speed instead of over the host link."""
+    import torch
+    if neighbour == "own-buffer":
+        c = vgpu_env(mem_limit=16 * GiB, shared_cache=tmp_region, oversubscribe=True,
+                     extra={"VGPU_DEVICE_HBM_LIMIT_0": "4096m", "VGPU_SPILL_POLICY": "first-come"})
+        env = {"SPILL_MODE": "own", "SPILL_ELEMS": str(1 << 28)}                       # 1 GiB
+        res, _ = run_child(SPILL_PROMOTE, c, extra_env=env)
+    else:
+        ready, go = tmp_path / "ready", tmp_path / "go"
+        hog = spawn_child(HBM_HOG, None, extra_env={"HOG_KEEP": str(3 * GiB), "HOG_READY": str(ready),
+                                                   "SPILL_GO": str(go)})
+        try:
+            t0 = time.time()
+            while not ready.exists():
+                assert hog.poll() is None and time.time() - t0 < 120, hog.communicate()[1][-3000:]
+                time.sleep(0.1)
+            c = vgpu_env(mem_limit=16 * GiB, shared_cache=tmp_region, oversubscribe=True,
+                         extra={"VGPU_DEVICE_HBM_LIMIT_0": "8192m", "VGPU_SPILL_POLICY": "large-first",
+                                "VGPU_SPILL_RESERVE": "1g"})
+            env = {"SPILL_MODE": "neighbour", "SPILL_ELEMS": str(1 << 29), "SPILL_GO": str(go)}   # 2 GiB
+            res, _ = run_child(SPILL_PROMOTE, c, extra_env=env)
+        finally:
+            go.touch()
+            hog.wait(timeout=60)
+    r = res[0]
+    print("spill promotion:", r)
+    assert r["spilled_before"] >= r["bytes"], r
+    assert r["ok_before"] and r["ok_after"], r
+    assert r["spilled_after"] == 0, r
+    assert r["gbps_promoted"] > 3 * r["gbps_spilled"], r
+
+
 CU_PROPS = """
 import torch
 p = torch.cuda.get_device_properties(0)

@@ -6,10 +6,9 @@
 #          count (VGPU_VIRTUAL_CU_COUNT=0: crowded pods run on all CUs, so libraries should
 #          size for 256, not the 16 of their slice); then the board's concurrency
 #          admission at 1 (time slicing) for the per-pod spread
-#   vmem   can host memory back a GPU-visible VMM range, and be swapped for HBM in place?
 # Each GPU step has its own time limit; a crash/timeout ends the script.
 out=${1:-gpurun_out/r4c}
-what=${2:-lone,many,vmem}
+what=${2:-lone,sweep,fullcu,conc1}
 mkdir -p "$out"
 if [[ $what == *lone* ]]; then
   for w in 0 160 320; do
@@ -18,17 +17,17 @@ if [[ $what == *lone* ]]; then
       > "$out/lone_w$w.log" 2>&1 || exit $?
   done
 fi
-if [[ $what == *many* ]]; then
+if [[ $what == *sweep* ]]; then
   timeout -k 10 560 python -u bench.py --modes native --sweep on --sweep-tenants 1,16 --sweep-seconds 8 \
     --time-budget 520 --json-out "$out/sweep16.json" > "$out/sweep16.log" 2>&1 || exit $?
+fi
+if [[ $what == *fullcu* ]]; then
   timeout -k 10 400 python -u benchmarks/vgpu_scaling.py --policy default --tenants 16 --seconds 8 \
     --pod-env VGPU_VIRTUAL_CU_COUNT=0 --json-out "$out/fullcu_16.json" --md-out "$out/fullcu_16.md" \
     > "$out/fullcu_16.log" 2>&1 || exit $?
+fi
+if [[ $what == *conc1* ]]; then
   timeout -k 10 400 python -u benchmarks/vgpu_scaling.py --policy default --tenants 16 --seconds 8 \
     --pod-env VGPU_GPU_CONCURRENCY=1 --json-out "$out/conc1_16.json" --md-out "$out/conc1_16.md" \
     > "$out/conc1_16.log" 2>&1 || exit $?
-fi
-if [[ $what == *vmem* ]]; then
-  timeout -k 10 60 4paradigm-k8s-device-plugin_amd/lib/vmem_probe 64 > "$out/vmem.json" 2> "$out/vmem.err"
-  echo "vmem_rc=$?" >> "$out/vmem.err"
 fi
