@@ -33,7 +33,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <condition_variable>
 #include <mutex>
 #include <vector>
 
@@ -53,9 +52,7 @@ constexpr uint64_t kRetryBackoffNs = 10'000'000'000ull;      // after a failed p
 
 std::atomic<uint64_t> g_seq{0};
 std::atomic<bool> g_migrator{false};
-std::mutex g_wake_mu;
-std::condition_variable g_wake_cv;
-bool g_wake = false;
+std::atomic<bool> g_wake{false};  // device memory was freed: look again before the period ends
 
 // The driver has SVM and ROCr exposes it (checked once per process).
 bool svm_supported() {
@@ -113,14 +110,6 @@ hsa_status_t svm_map(int dev, size_t size, void** ptr, size_t* mapped) {
   *ptr = p;
   *mapped = len;
   return HSA_STATUS_SUCCESS;
-}
-
-void wake_migrator() {
-  {
-    std::lock_guard<std::mutex> g(g_wake_mu);
-    g_wake = true;
-  }
-  g_wake_cv.notify_one();
 }
 
 // Migrates [p, p+len) to `agent` (a GPU or the CPU); true once the driver completed it.
@@ -219,11 +208,13 @@ void* migrator_main(void*) {
   const pid_t me = s.pid;
   const uint64_t period_ns = (uint64_t)std::max(config().util_period_ms, 10) * 1'000'000ull;
   while (!s.exiting.load() && s.pid == me) {
-    {
-      std::unique_lock<std::mutex> g(g_wake_mu);
-      g_wake_cv.wait_for(g, std::chrono::nanoseconds(period_ns), [] { return g_wake; });
-      g_wake = false;
+    // Sleeps a period in 5 ms slices, cut short by a free (no condition variable: the shim
+    // keeps to glibc 2.17's symbols, test_native_core.py).
+    for (uint64_t slept = 0; slept < period_ns && !g_wake.load(std::memory_order_relaxed); slept += 5'000'000) {
+      struct timespec ts = {0, 5'000'000};
+      nanosleep(&ts, nullptr);
     }
+    g_wake.store(false, std::memory_order_relaxed);
     if (s.exiting.load() || !s.active || s.slot < 0) continue;
     uint64_t budget = kPromoteBytesPerTick;
     for (int d = 0; d < s.n_agents && budget; d++) budget -= std::min(budget, promote_device(d, budget));
@@ -341,7 +332,7 @@ bool spill_release(void* ptr) {
 }
 
 void notify_device_memory_freed() {
-  if (g_migrator.load(std::memory_order_relaxed)) wake_migrator();
+  if (g_migrator.load(std::memory_order_relaxed)) g_wake.store(true, std::memory_order_relaxed);
 }
 
 bool svm_allow_access(const void* ptr, uint32_t n, const hsa_agent_t* agents, hsa_status_t* st) {
@@ -384,8 +375,7 @@ void svm_forget() {
   for (auto& b : s.svm_hbm) b = 0;
   new (&s.svm_mu) std::mutex();
   g_migrator.store(false);
-  new (&g_wake_mu) std::mutex();
-  g_wake = false;
+  g_wake.store(false);
 }
 
 }  // namespace vgpu
