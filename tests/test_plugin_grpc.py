@@ -204,15 +204,15 @@ def test_eight_gpu_node_advertises_32_vgpus(plugin_dir):
         shutdown(k, stop, th)
 
 
-def test_grpc_server_watchdog_restarts_and_budget(plugin_dir):
+def test_grpc_server_watchdog_restarts_and_budget(plugin_dir, monkeypatch):
     """Socket deleted under the plugin -> served again and re-registered; more than 5
     restarts within the hour -> fatal, the supervisor exits (server.go:180-207)."""
+    from amdvgpu.plugin import server
+    monkeypatch.setattr(server, "WATCHDOG_PERIOD_S", 0.1)  # from the first tick on
     cfg, k, sup, stop, th = start(plugin_dir)
     try:
         k.wait_registered("amd.com/gpu")
         p = sup.plugins[0]
-        p.watchdog_period_s = 0.1
-        time.sleep(0.3)  # the watchdog thread picks up the shorter period after one tick
         n0 = len(k.registrations)
         os.unlink(p.socket)
         k.wait_registered("amd.com/gpu", count=n0 + 1, timeout=15)
