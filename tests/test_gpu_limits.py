@@ -98,6 +98,7 @@ def _spin_rates(contracts, secs=3.0):
 def _resnet_rates(contracts, tmp_path, secs=4.0, batch=None, full=False):
     """Stock fp32 ResNet-50 inference tenants, released together after warm-up. Returns
     each one's rate, or with ``full`` its result (rate and charged GPU-time fraction)."""
+    os.makedirs(tmp_path, exist_ok=True)
     go = str(tmp_path / "go")
     ps = []
     for i, c in enumerate(contracts):
@@ -106,7 +107,9 @@ def _resnet_rates(contracts, tmp_path, secs=4.0, batch=None, full=False):
                                extra_env={"VGPU_TEST_READY": ready, "VGPU_TEST_GO": go}), ready))
     deadline = time.time() + 240
     while not all(os.path.exists(r) for _, r in ps):
-        assert time.time() < deadline and all(p.poll() is None for p, _ in ps), "tenant failed to start"
+        if time.time() > deadline or any(p.poll() is not None for p, _ in ps):
+            errs = [p.communicate()[1][-2000:] for p, _ in ps if p.poll() is not None]
+            raise AssertionError(f"tenant failed to start: {errs}")
         time.sleep(0.05)
     open(go, "w").close()
     out = []

@@ -10,6 +10,10 @@
 out=${1:-gpurun_out/r4c}
 what=${2:-lone,sweep,fullcu,conc1}
 mkdir -p "$out"
+# The hardware scheduler's limits: processes mapped at once (one VMID each) and its policy.
+for f in hws_max_conc_proc sched_policy hws_gws_support mes sched_hw_submission; do
+  echo "$f=$(cat /sys/module/amdgpu/parameters/$f 2>/dev/null)"
+done > "$out/hws.txt"
 if [[ $what == *lone* ]]; then
   for w in 0 160 320; do
     timeout -k 10 240 python -u benchmarks/temporal_accuracy.py --workload resnet50 --tenants 1 --limits 25 \
@@ -25,6 +29,11 @@ if [[ $what == *fullcu* ]]; then
   timeout -k 10 400 python -u benchmarks/vgpu_scaling.py --policy default --tenants 16 --seconds 8 \
     --pod-env VGPU_VIRTUAL_CU_COUNT=0 --json-out "$out/fullcu_16.json" --md-out "$out/fullcu_16.md" \
     > "$out/fullcu_16.log" 2>&1 || exit $?
+fi
+if [[ $what == *conc8* ]]; then
+  timeout -k 10 400 python -u benchmarks/vgpu_scaling.py --policy default --tenants 16 --seconds 8 \
+    --pod-env VGPU_GPU_CONCURRENCY=8 --json-out "$out/conc8_16.json" --md-out "$out/conc8_16.md" \
+    > "$out/conc8_16.log" 2>&1 || exit $?
 fi
 if [[ $what == *conc1* ]]; then
   timeout -k 10 400 python -u benchmarks/vgpu_scaling.py --policy default --tenants 16 --seconds 8 \
