@@ -164,9 +164,13 @@ uint64_t promote_device(int dev, uint64_t budget) {
     if (share && resident + rec.size + reserve > share) break;
     uint64_t avail = 0;
     if (real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &avail) !=
-            HSA_STATUS_SUCCESS ||
-        avail < rec.mapped + reserve)
+        HSA_STATUS_SUCCESS)
       break;
+    // ROCr's free-memory figure does not drop as SVM pages move into VRAM (profiles/r4b):
+    // what this process promoted already is taken off it here.
+    const uint64_t promoted = (uint64_t)std::max<int64_t>(0, svm_hbm_outside_kfd(dev));
+    avail = avail > promoted ? avail - promoted : 0;
+    if (avail < rec.mapped + reserve) break;
     void* p = reinterpret_cast<void*>(o.second);
     // The context charge (KFD VRAM less the tracked allocations) must not see the pages
     // arrive before the charge moves: both under ctx_mu.
