@@ -256,6 +256,10 @@ def test_hip_allocations_are_accounted(tmp_region, kind):
 
 
 def test_allowlist_authorisation(tmp_region, tmp_path):
+    """VGPU_ALLOWLIST: a GPU whose UUID is not listed gets no device memory at all - not
+    through the pool API, not through the legacy region API HIP also uses while it brings the
+    device up - so HIP drops the device ("No HIP GPUs are available" with one GPU) or, if the
+    device came up, the first allocation fails."""
     from amdvgpu.plugin.devices import SysfsBackend
     uuid = SysfsBackend().devices()[0].uuid
     code = """
@@ -264,6 +268,8 @@ try:
     x = torch.empty(1 << 20, device="cuda"); ok = True
 except torch.OutOfMemoryError:
     ok = False
+except RuntimeError as e:   # the device did not come up: no memory for HIP's own buffers either
+    ok = "No HIP GPUs" not in str(e)
 emit(ok=ok)
 """
     allow = tmp_path / "allowlist"
