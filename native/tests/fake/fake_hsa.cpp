@@ -554,6 +554,13 @@ uint64_t fake_rocr_used(int dev) {
   return dev >= 0 && dev < st().n ? st().gpus[dev].used.load() : 0;
 }
 
+// Whether the SVM range at `ptr` lists `agent` as having access.
+int fake_rocr_svm_has_access(const void* ptr, uint64_t agent) {
+  std::lock_guard<std::mutex> g(st().mu);
+  auto it = st().svm.find(reinterpret_cast<uintptr_t>(ptr));
+  return it != st().svm.end() && it->second.access.count(agent) ? 1 : 0;
+}
+
 // Where the SVM range at `ptr` lives: the GPU ordinal, -1 = host memory, -2 = not a range.
 int fake_rocr_svm_location(const void* ptr) {
   std::lock_guard<std::mutex> g(st().mu);

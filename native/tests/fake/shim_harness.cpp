@@ -46,12 +46,16 @@
 //   where            where the most recent allocation lives: {"where": gpu ordinal, -1 = host
 //                    memory (an SVM range), -2 = not an SVM range}
 //   spilled          the shim's vgpu_get_current_device_spilled: {"spilled": bytes}
+//   peer=D           hsa_amd_agents_allow_access for GPU D on the most recent allocation (what
+//                    HIP does for peer devices): {"peer": status, "svm_access": whether the
+//                    fake's SVM range now lists that agent}
 //   hostregister=SIZE  hipHostRegister of a fresh heap buffer -> {"hostregister": "ok"|"oom"};
 //                    hostunregister unregisters (and frees) the last one
 #define __HIP_PLATFORM_AMD__ 1
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -75,6 +79,7 @@ int fake_rocr_host_pid();
 int fake_hip_device_cus(int dev);
 const char* fake_hip_last_call();
 int fake_rocr_svm_location(const void* ptr);
+int fake_rocr_svm_has_access(const void* ptr, uint64_t agent);
 }
 
 namespace {
@@ -216,6 +221,11 @@ int main(int argc, char** argv) {
       else printf("{\"check\": \"%s\", \"bad\": %zu}\n", bad || ptrs.empty() ? "bad" : "ok", bad);
     } else if (key == "where") {
       printf("{\"where\": %d}\n", ptrs.empty() ? -2 : fake_rocr_svm_location(ptrs.back()));
+    } else if (key == "peer") {
+      const uint64_t agent = (uint64_t)atoi(val.c_str()) + 1;  // the fake's GPU agent handles are 1..n
+      hsa_agent_t a{agent};
+      int st = ptrs.empty() ? -1 : (int)hsa_amd_agents_allow_access(1, &a, nullptr, ptrs.back());
+      printf("{\"peer\": %d, \"svm_access\": %d}\n", st, ptrs.empty() ? 0 : fake_rocr_svm_has_access(ptrs.back(), agent));
     } else if (key == "spilled") {
       using Get = uint64_t (*)();
       auto f = reinterpret_cast<Get>(dlsym(RTLD_DEFAULT, "vgpu_get_current_device_spilled"));

@@ -271,6 +271,17 @@ def test_svm_spill_is_promoted_when_the_share_frees_up(fake, kfd_counts):
     assert infos[-1]["free"] == 256 * MiB, infos
 
 
+def test_peer_access_to_an_svm_spill(fake):
+    """HIP grants the other GPUs of the process access to a new buffer
+    (hsa_amd_agents_allow_access); ROCr does not know an SVM spill, so the shim sets the
+    peer's access on the SVM range instead."""
+    e = fake(gpus=2, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT_0="256m", VGPU_DEVICE_HBM_LIMIT_0="64m",
+             VGPU_DEVICE_MEMORY_LIMIT_1="256m", VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come")
+    out = run(e, "malloc=48m", "malloc=32m", "where", "peer=1")
+    assert [o["where"] for o in out if "where" in o] == [-1]
+    assert [(o["peer"], o["svm_access"]) for o in out if "peer" in o] == [(0, 1)]
+
+
 def test_svm_spill_waits_for_room(fake):
     """Nothing was freed: the share (48 MiB resident + 32 + the 16 MiB reserve > 64 MiB)
     has no room, so the spill stays in host memory."""
