@@ -30,15 +30,25 @@ HBM = 309220868096
 
 def worker(case_name, steps, warmup, out, go_file, seconds):
     import faulthandler
+    t_spawn = time.time()
     faulthandler.dump_traceback_later(200, exit=False)  # a pod stuck in warm-up shows where
     import torch
     from amdvgpu.models.aibench import Runner, get_case
     torch.backends.cudnn.benchmark = True  # MIOpen find mode
     case = get_case(case_name)
+    t_import = time.time()
     r = Runner(case, "cuda:0", dtype=torch.float32)
-    for _ in range(warmup):
-        r.step()
     torch.cuda.synchronize()
+    t_model = time.time()
+    for i in range(warmup):
+        r.step()
+        if i == 0:
+            torch.cuda.synchronize()
+            t_first = time.time()
+    torch.cuda.synchronize()
+    startup = {"import_s": round(t_import - t_spawn, 2), "model_s": round(t_model - t_import, 2),
+               "first_step_s": round(t_first - t_model, 2) if warmup else 0.0,
+               "warmup_s": round(time.time() - (t_first if warmup else t_model), 2)}
     region = None
     if os.environ.get("VGPU_SHARED_CACHE") and os.path.exists(os.environ["VGPU_SHARED_CACHE"]):
         from amdvgpu.shim.region import Region
@@ -58,7 +68,7 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     res = {"ms_per_batch": (t1 - t0) * 1000 / n, "t0": t0, "t1": t1, "batch": case.batch, "steps": n,
-           "throughput": case.batch * n / (t1 - t0), "cu_mode": None, "crowd": None}
+           "throughput": case.batch * n / (t1 - t0), "cu_mode": None, "crowd": None, "startup": startup}
     if region:
         g1 = region.device(0)  # the enforcement the pod ended under, and the GPU time it was charged
         res.update(cu_mode=g1["cu_mode"], crowd=g1["crowd"])
@@ -118,7 +128,29 @@ def stuck_report(outs, regions, procs):
         print("STUCK " + json.dumps(info), flush=True)
 
 
-def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None, split=0, ledger=False):
+def miopen_dirs(mode, tmp, i):
+    """MIOpen's find-db and kernel cache for pod ``i``. ``home``: the process's default
+    (~/.config/miopen, ~/.cache/miopen: one set for every pod on this box - pods of a real node
+    each have their own filesystem); ``per-pod``: the pod's own copy of the default set (an
+    image that ships a tuned find-db); ``empty``: the pod's own empty set (a pod's first run)."""
+    if mode == "home":
+        return {}
+    import shutil
+    base = os.path.join(tmp, f"miopen{i}")
+    db, cache = os.path.join(base, "db"), os.path.join(base, "cache")
+    home = os.path.expanduser("~")
+    src_db, src_cache = os.path.join(home, ".config", "miopen"), os.path.join(home, ".cache", "miopen")
+    if mode == "per-pod" and os.path.isdir(src_db):
+        shutil.copytree(src_db, db)
+    if mode == "per-pod" and os.path.isdir(src_cache):
+        shutil.copytree(src_cache, cache)
+    os.makedirs(db, exist_ok=True)
+    os.makedirs(cache, exist_ok=True)
+    return {"MIOPEN_USER_DB_PATH": db, "MIOPEN_CUSTOM_CACHE_DIR": cache}
+
+
+def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None, split=0, ledger=False,
+              miopen="home"):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="scal-")
@@ -135,6 +167,7 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
             if hw_queues:
                 env["GPU_MAX_HW_QUEUES"] = str(hw_queues)
             env.update(pod_env or {})
+            env.update(miopen_dirs(miopen, tmp, i))
             procs.append(subprocess.Popen(cmd, env=env))
             outs.append(out)
         try:
@@ -162,7 +195,10 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
                     p.kill()
     span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
     agg = sum(r["batch"] * r["steps"] for r in res) / span
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
     return {"tenants": n, "policy": policy, "split": split or n, "hw_queues": hw_queues or None, "kfd_queues": queues,
+            "miopen_db": miopen, "startup": [r.get("startup") for r in res],
             "warmup_s": round(warm_s, 1), "pod_env": pod_env or None, "modes": sorted({str(r.get("cu_mode")) for r in res}),
             "aggregate_throughput": agg,
             "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res],
@@ -183,6 +219,8 @@ def main():
     ap.add_argument("--repeats", type=int, default=1)
     ap.add_argument("--split", type=int, default=0, help="vGPUs per GPU (default: one per pod)")
     ap.add_argument("--node-ledger", action="store_true", help="the plugin runs the node GPU-time ledger (vgpu-ledger)")
+    ap.add_argument("--miopen-db", default="home", choices=["home", "per-pod", "empty"],
+                    help="MIOpen find-db / kernel cache of the pods (see miopen_dirs)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--go")
@@ -209,7 +247,8 @@ def main():
                         if n == 1 and k > 0:
                             continue
                         r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq,
-                                      pe if n > 1 else None, a.split, ledger=a.node_ledger)
+                                      pe if n > 1 else None, a.split, ledger=a.node_ledger,
+                                      miopen=a.miopen_db if n > 1 else "home")
                         rows.append(r)
                         print(json.dumps(r), flush=True)
     base = {r["policy"]: r["aggregate_throughput"] for r in rows if r["tenants"] == 1}
