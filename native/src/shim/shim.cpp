@@ -654,7 +654,13 @@ void apply_live_config() {
     if (locked) s.region.unlock();
     const bool limited = pct > 0 && pct < 100;
     const int prio = effective_priority(r);
-    const CuMode mode = effective_cu_mode_prio(cfg.cu_mode, pct, d.crowd.load(std::memory_order_relaxed), prio);
+    // A thin slice (a few CUs per XCD) is no place for stock libraries' grids: in auto mode
+    // such a share is time-sliced on every CU whatever the crowd, and the runtime is told the
+    // whole GPU (profiles/r4c, r4g: 16 pods). The latency class keeps its slice.
+    const bool thin = cfg.cu_mode == CuMode::kAuto && limited && prio > 0 && cfg.auto_min_slice_cus > 0 &&
+                      m.count() > 0 && m.count() < cfg.auto_min_slice_cus;
+    const CuMode mode =
+        thin ? CuMode::kTemporal : effective_cu_mode_prio(cfg.cu_mode, pct, d.crowd.load(std::memory_order_relaxed), prio);
     const bool spatial = mode == CuMode::kSpatial || mode == CuMode::kBoth;
     const bool temporal = mode == CuMode::kTemporal || mode == CuMode::kBoth;
     const bool mask_on = !off && spatial && (limited || ranged) && m.count() < a.cu_count && m.count() > 0;
@@ -697,7 +703,7 @@ void apply_live_config() {
     // persistent grids in particular — fit the CUs it may get. In auto mode the slice is
     // reported whether or not the mask is on at this moment, so every process of the
     // container sees the same count however crowded the GPU was when it started.
-    const bool may_mask = spatial || cfg.cu_mode == CuMode::kAuto;
+    const bool may_mask = spatial || (cfg.cu_mode == CuMode::kAuto && !thin);
     const bool slice = !off && may_mask && (limited || ranged) && m.count() < a.cu_count && m.count() > 0;
     a.visible_cus.store(slice && cfg.virtual_cu_count ? m.count() : 0);
     // Leaving the GPU-time limiter (auto mode: the GPU calmed down; a live share change):

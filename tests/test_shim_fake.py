@@ -336,6 +336,21 @@ def test_cu_count_follows_the_spatial_slice(fake, mode, virt, want):
     assert out[-1]["cus"] == want
 
 
+@pytest.mark.parametrize("min_slice,want_cus,want_mask", [("32", 256, 256), ("0", 16, 16)])
+def test_thin_share_is_time_sliced_in_auto_mode(fake, min_slice, want_cus, want_mask):
+    """A split-16 share (a 16-CU slice, two CUs per XCD) in auto mode: time-sliced on every
+    CU even alone, and the runtime sees all 256 CUs (stock libraries size their grids for
+    the GPU the kernels actually run on); VGPU_AUTO_MIN_SLICE_CUS=0 keeps the round-3
+    behaviour (the slice as a mask while the GPU is not crowded)."""
+    e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="7", VGPU_DEVICE_CU_RANGE_0="0-16", VGPU_CU_MODE="auto",
+             VGPU_AUTO_MIN_SLICE_CUS=min_slice)
+    p = subprocess.Popen([HARNESS, "cus", "stream", "sleep=0.6", "queues"], env=e, stdout=subprocess.PIPE, text=True)
+    out = [json.loads(l) for l in p.stdout.read().splitlines() if l.startswith("{")]
+    assert p.wait(30) == 0
+    assert [o["cus"] for o in out if "cus" in o and "dev" in o and "queues" not in o] == [want_cus], out
+    assert [o for o in out if "queues" in o][0]["queues"][0]["cus"] == want_mask, out
+
+
 def _foreign(kfd, pid, occupancy):
     d = os.path.join(kfd, str(pid), "stats_1000")
     os.makedirs(d, exist_ok=True)
