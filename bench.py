@@ -76,11 +76,14 @@ def parse(argv=None):
     ap.add_argument("--cu-mode", default="auto", choices=["auto", "spatial", "temporal", "both", "off"])
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--sweep", default="auto", choices=["auto", "on", "off"])
-    ap.add_argument("--sweep-tenants", default="1,2,4,8,12")
+    ap.add_argument("--sweep-tenants", default="1,2,4,8,12,16")
     ap.add_argument("--sweep-seconds", type=float, default=6.0)
-    ap.add_argument("--sweep-find-db", default="own", choices=["own", "shared"],
-                    help="shared: the sweep's pods use one MIOpen find-db, filled by the lone pod (as a "
-                         "tenant image with a tuned find-db would ship); own: every pod runs its own find")
+    ap.add_argument("--sweep-find-db", default="per-pod", choices=["per-pod", "home", "empty"],
+                    help="MIOpen find-db and kernel cache of the sweep's pods: per-pod = each pod its own copy "
+                         "of what the lone pod left (a tenant image that ships a tuned find-db; pods of a node "
+                         "never share one file system); home = this process's own (~/.config/miopen: one sqlite "
+                         "set shared by every pod on this box); empty = each pod its own empty set (a pod's "
+                         "first run: every pod runs its own find)")
     ap.add_argument("--node", default="auto", choices=["auto", "on", "off"],
                     help="node point: all --split vGPUs of every GPU of the job busy at once (BASELINE config 5: "
                          "32 vGPUs on 8 GPUs); auto = on for multi-GPU runs (single-GPU runs take it from the sweep)")
@@ -393,21 +396,29 @@ def run_concurrent(args, envs, label, deadline=None, before_go=None):
                 p.kill()
 
 
+def miopen_env(mode, root, i):
+    """MIOpen find-db / kernel cache of sweep pod ``i`` (``--sweep-find-db``)."""
+    if mode == "home":
+        return None
+    import shutil
+    db, cache = os.path.join(root, f"pod{i}", "db"), os.path.join(root, f"pod{i}", "cache")
+    home = os.path.expanduser("~")
+    for src, dst in ((os.path.join(home, ".config", "miopen"), db), (os.path.join(home, ".cache", "miopen"), cache)):
+        if mode == "per-pod" and os.path.isdir(src):
+            shutil.copytree(src, dst, dirs_exist_ok=True)
+        os.makedirs(dst, exist_ok=True)
+    return {"MIOPEN_USER_DB_PATH": db, "MIOPEN_CUSTOM_CACHE_DIR": cache}
+
+
 def sweep(args, backend, uuid, tenants):
     import shutil
     rows, skipped = [], []
     end = T_START + args.time_budget
-    extra, db = None, None
-    if args.sweep_find_db == "shared":
-        db = tempfile.mkdtemp(prefix="bench-miopen-")
-        extra = {"MIOPEN_USER_DB_PATH": os.path.join(db, "db"), "MIOPEN_CUSTOM_CACHE_DIR": os.path.join(db, "cache")}
-        for d in extra.values():
-            os.makedirs(d)
+    root = tempfile.mkdtemp(prefix="bench-miopen-")
     try:
-        rows, skipped = _sweep_points(args, backend, uuid, tenants, end, extra)
+        rows, skipped = _sweep_points(args, backend, uuid, tenants, end, root)
     finally:
-        if db:
-            shutil.rmtree(db, ignore_errors=True)
+        shutil.rmtree(root, ignore_errors=True)
     base = next((r["aggregate"] for r in rows if r["tenants"] == 1), None)
     best = 0
     for r in rows:
@@ -421,7 +432,7 @@ def sweep(args, backend, uuid, tenants):
     return rows + skipped, best
 
 
-def _sweep_points(args, backend, uuid, tenants, end, extra):
+def _sweep_points(args, backend, uuid, tenants, end, root):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     rows, skipped = [], []
     last = None  # (pods, seconds) of the last measured point with several pods
@@ -437,7 +448,11 @@ def _sweep_points(args, backend, uuid, tenants, end, extra):
         try:
             with NodeHarness(backend, device_split_count=n, cu_mode=args.cu_mode, **ledger_kw(args)) as node:
                 ids = node.vgpu_ids(uuid)[:n]
-                pods = [pod_env(node, [i], extra) for i in ids]
+                # The lone pod runs on this process's own find-db (the native run filled it);
+                # with several, each pod gets its own (--sweep-find-db).
+                pods = [pod_env(node, [i], miopen_env(args.sweep_find_db if n > 1 else "home", root,
+                                                      k + 100 * n))
+                        for k, i in enumerate(ids)]
                 res = run_concurrent(args, [e for e, _ in pods], f"sweep{n}",
                                      deadline=end - args.sweep_seconds - 15.0)
                 c0 = pods[0][1]

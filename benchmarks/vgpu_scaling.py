@@ -46,9 +46,13 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
             torch.cuda.synchronize()
             t_first = time.time()
     torch.cuda.synchronize()
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)  # every thread of the pod, start-up only
     startup = {"import_s": round(t_import - t_spawn, 2), "model_s": round(t_model - t_import, 2),
                "first_step_s": round(t_first - t_model, 2) if warmup else 0.0,
-               "warmup_s": round(time.time() - (t_first if warmup else t_model), 2)}
+               "warmup_s": round(time.time() - (t_first if warmup else t_model), 2),
+               "cpu_user_s": round(ru.ru_utime, 2), "cpu_sys_s": round(ru.ru_stime, 2),
+               "max_rss_mb": round(ru.ru_maxrss / 1024, 1), "vol_ctx_switches": ru.ru_nvcsw}
     region = None
     if os.environ.get("VGPU_SHARED_CACHE") and os.path.exists(os.environ["VGPU_SHARED_CACHE"]):
         from amdvgpu.shim.region import Region
