@@ -175,14 +175,24 @@ def worker(args):
         open(args.result_file + ".ready", "w").close()
         while not os.path.exists(args.go):
             time.sleep(0.002)
+        # The pods wait for their GPU work blocked, not spinning: on this box every pod runs in
+        # one CPU quota, where many spinning pods starve each other's launch threads (on a node
+        # each pod has CPUs of its own). VGPU_BENCH_SYNC=spin keeps torch's default wait.
+        if not cpu and os.environ.get("VGPU_BENCH_SYNC", "block") != "spin":
+            def wait():
+                ev = torch.cuda.Event(blocking=True)
+                ev.record()
+                ev.synchronize()
+        else:
+            wait = sync
         n = 0
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < args.seconds:
             runner.step()
             n += 1
             if n % 4 == 0:
-                sync()
-        sync()
+                wait()
+        wait()
         dt = time.perf_counter() - t0
         res = {"mode": args.mode, "ms_per_step": dt * 1000.0 / n, "items_per_step": runner.items_per_step,
                "steps": n, "t0": t0, "t1": t0 + dt, "startup": {k: round(v, 2) for k, v in phases.items()}}

@@ -62,17 +62,31 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
     while not os.path.exists(go_file):
         time.sleep(0.005)
     g0 = region.device(0) if region else None
+    # Waits block (interrupt-driven) instead of spinning: the box runs every pod in one CPU
+    # quota (16 CPUs), where 16 spinning pods starve each other's launch threads; on a node
+    # each pod spins on CPUs of its own. VGPU_BENCH_SYNC=spin restores torch's default wait.
+    if os.environ.get("VGPU_BENCH_SYNC", "block") == "spin":
+        sync = torch.cuda.synchronize
+    else:
+        def sync():
+            ev = torch.cuda.Event(blocking=True)
+            ev.record()
+            ev.synchronize()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     n = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         r.step()
         n += 1
         if n % 4 == 0:
-            torch.cuda.synchronize()
-    torch.cuda.synchronize()
+            sync()
+    sync()
     t1 = time.perf_counter()
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu_window = round(ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime, 2)
     res = {"ms_per_batch": (t1 - t0) * 1000 / n, "t0": t0, "t1": t1, "batch": case.batch, "steps": n,
-           "throughput": case.batch * n / (t1 - t0), "cu_mode": None, "crowd": None, "startup": startup}
+           "throughput": case.batch * n / (t1 - t0), "cu_mode": None, "crowd": None, "startup": startup,
+           "cpu_s_in_window": cpu_window}
     if region:
         g1 = region.device(0)  # the enforcement the pod ended under, and the GPU time it was charged
         res.update(cu_mode=g1["cu_mode"], crowd=g1["crowd"])
@@ -207,7 +221,8 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
             "aggregate_throughput": agg,
             "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res],
             "per_tenant_granted_pct": [r.get("granted_pct") for r in res],
-            "per_tenant_images_per_gpu_ms": [r.get("images_per_gpu_ms") for r in res]}
+            "per_tenant_images_per_gpu_ms": [r.get("images_per_gpu_ms") for r in res],
+            "per_tenant_cpu_s": [r.get("cpu_s_in_window") for r in res]}
 
 
 def main():
