@@ -78,6 +78,8 @@ def parse(argv=None):
     ap.add_argument("--sweep", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--sweep-tenants", default="1,2,4,8,12,16")
     ap.add_argument("--sweep-seconds", type=float, default=6.0)
+    ap.add_argument("--sweep-autotune", type=int, default=1,
+                    help="0: the sweep's pods (the lone one too) skip MIOpen's per-process find (immediate mode)")
     ap.add_argument("--sweep-find-db", default="per-pod", choices=["per-pod", "home", "empty"],
                     help="MIOpen find-db and kernel cache of the sweep's pods: per-pod = each pod its own copy "
                          "of what the lone pod left (a tenant image that ships a tuned find-db; pods of a node "
@@ -145,7 +147,9 @@ def worker(args):
     if quota and not cpu and total != quota:
         raise SystemExit(f"vGPU shim not in effect: mem_get_info total {total} != quota {quota}")
 
-    torch.backends.cudnn.benchmark = True  # MIOpen find mode (the reference's TF autotunes too)
+    # MIOpen find mode (the reference's TF autotunes too); --sweep-autotune 0 gives the sweep's
+    # pods MIOpen's immediate mode (no per-process search) - the lone pod included.
+    torch.backends.cudnn.benchmark = not (args.go and not args.sweep_autotune)
     case = get_case(args.case)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     if cpu:
@@ -279,7 +283,7 @@ def worker_cmd(args, mode, result, port, dist=1, seconds=0.0, go=None):
     if args.cpu_rehearsal:
         cmd.append("--cpu-rehearsal")
     if go:
-        cmd += ["--seconds", str(seconds), "--go", go]
+        cmd += ["--seconds", str(seconds), "--go", go, "--sweep-autotune", str(args.sweep_autotune)]
     return cmd
 
 
