@@ -178,6 +178,11 @@ def test_amdsmi_reports_quota(tmp_region):
 
 
 def test_rccl_allreduce_through_shim(tmp_region):
+    """RCCL inside a vGPU: the communicator's set-up allocations go through the quota and its
+    kernels through the launch gates. One rank only - the test box has one GPU and RCCL
+    refuses two ranks on one device. The inter-GPU path (an all-reduce between pods on
+    different GPUs, against native) is bench.py's ``rccl_allreduce_between_pods`` on the
+    driver's multi-GPU runs, rehearsed with gloo in tests/test_bench_contract.py."""
     c = vgpu_env(mem_limit=16 * GiB, shared_cache=tmp_region)
     res, _ = run_child("""
 import torch, torch.distributed as dist
