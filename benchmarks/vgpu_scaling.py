@@ -84,9 +84,20 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
     t1 = time.perf_counter()
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     cpu_window = round(ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime, 2)
+    threads = {}  # where the pod's CPU time went, by thread name (whole life: start-up included)
+    tick = os.sysconf("SC_CLK_TCK")
+    for t in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{t}/stat") as f:
+                st = f.read()
+            name = st[st.index("(") + 1:st.rindex(")")]
+            fields = st[st.rindex(")") + 2:].split()
+            threads[name] = round(threads.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tick, 2)
+        except (OSError, ValueError, IndexError):
+            pass
     res = {"ms_per_batch": (t1 - t0) * 1000 / n, "t0": t0, "t1": t1, "batch": case.batch, "steps": n,
            "throughput": case.batch * n / (t1 - t0), "cu_mode": None, "crowd": None, "startup": startup,
-           "cpu_s_in_window": cpu_window}
+           "cpu_s_in_window": cpu_window, "cpu_s_by_thread": threads}
     if region:
         g1 = region.device(0)  # the enforcement the pod ended under, and the GPU time it was charged
         res.update(cu_mode=g1["cu_mode"], crowd=g1["crowd"])
@@ -222,7 +233,8 @@ def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_
             "per_tenant": [r["throughput"] for r in res], "per_tenant_ms": [r["ms_per_batch"] for r in res],
             "per_tenant_granted_pct": [r.get("granted_pct") for r in res],
             "per_tenant_images_per_gpu_ms": [r.get("images_per_gpu_ms") for r in res],
-            "per_tenant_cpu_s": [r.get("cpu_s_in_window") for r in res]}
+            "per_tenant_cpu_s": [r.get("cpu_s_in_window") for r in res],
+            "cpu_s_by_thread": [r.get("cpu_s_by_thread") for r in res]}
 
 
 def main():
