@@ -100,9 +100,9 @@ struct Config {
   bool signal_control = false;           // VGPU_SIGNAL_CONTROL: also honour SIGUSR1/2
   bool hook_smi = true;                  // VGPU_HOOK_SMI: virtualise amd-smi/rocm-smi
   bool virtual_cu_count = true;          // VGPU_VIRTUAL_CU_COUNT: report the spatial slice's CUs
-  int auto_min_slice_cus = 32;           // VGPU_AUTO_MIN_SLICE_CUS: in auto mode a share whose CU slice is
-                                         // thinner (split >= 9 of 256 CUs) is time-sliced only - never a mask
-                                         // - and the runtime sees every CU (0 = masks of any width)
+  int auto_min_slice_cus = 40;           // VGPU_AUTO_MIN_SLICE_CUS: in auto mode a share whose CU slice is
+                                         // thinner (at most 4 CUs per XCD: split >= 7 of 256 CUs) is time-sliced
+                                         // only - never a mask - and the runtime sees every CU (0 = any width)
   int util_period_ms = 120;              // monitor / OOM-killer / accounting period (reference: 120 ms)
   int util_sample_us = 1000;             // temporal-mode occupancy sampling interval
   int sample_read_budget = 32;           // node-wide occupancy reads per interval (ratelimit.h)

@@ -295,7 +295,7 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   cfg->fail_open = parse_bool(getenv_fn("VGPU_FAIL_OPEN"), false);
   cfg->hook_smi = parse_bool(getenv_fn("VGPU_HOOK_SMI"), true);
   cfg->virtual_cu_count = parse_bool(getenv_fn("VGPU_VIRTUAL_CU_COUNT"), true);
-  long min_slice = 32;
+  long min_slice = 40;
   if (parse_int(getenv_fn("VGPU_AUTO_MIN_SLICE_CUS"), 0, 1024, &min_slice)) cfg->auto_min_slice_cus = (int)min_slice;
   long period = 120;
   if (parse_int(getenv_fn("VGPU_UTIL_PERIOD_MS"), 10, 10000, &period)) cfg->util_period_ms = (int)period;

@@ -336,7 +336,7 @@ def test_cu_count_follows_the_spatial_slice(fake, mode, virt, want):
     assert out[-1]["cus"] == want
 
 
-@pytest.mark.parametrize("min_slice,want_cus,want_mask", [("32", 256, 256), ("0", 16, 16)])
+@pytest.mark.parametrize("min_slice,want_cus,want_mask", [("40", 256, 256), ("0", 16, 16)])
 def test_thin_share_is_time_sliced_in_auto_mode(fake, min_slice, want_cus, want_mask):
     """A split-16 share (a 16-CU slice, two CUs per XCD) in auto mode: time-sliced on every
     CU even alone, and the runtime sees all 256 CUs (stock libraries size their grids for

@@ -36,13 +36,18 @@ def tenant(steps, case, autotune):
     torch.cuda.synchronize()
     # The timed window as a roctx range: the summary counts only the kernels inside it
     # (warm-up, MIOpen find and model loading stay out of the per-step figures).
+    # rocprofv3 records the rocprofiler-sdk roctx (as the shim's own ranges use, trace.cpp);
+    # the legacy libroctx64 is only the fallback.
+    import ctypes
     roctx = None
-    try:
-        import ctypes
-        roctx = ctypes.CDLL("libroctx64.so")
+    for lib in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", "libroctx64.so.4"):
+        try:
+            roctx = ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
+            break
+        except OSError:
+            continue
+    if roctx:
         roctx.roctxRangePushA(b"vgpu-prof:timed")
-    except OSError:
-        roctx = None
     t0 = time.perf_counter()
     for _ in range(steps):
         r.step()
