@@ -789,13 +789,15 @@ emit(cus=p.multi_processor_count, ok=ok, conv_finite=bool(torch.isfinite(y).all(
 """
 
 
-@pytest.mark.parametrize("mode,want", [("spatial", 64), ("temporal", 256), ("auto", 64)])
-def test_runtime_sees_the_spatial_slice_cu_count(tmp_region, mode, want):
+@pytest.mark.parametrize("mode,pct,want", [("spatial", 25, 64), ("temporal", 25, 256), ("auto", 25, 64),
+                                           ("auto", 7, 256)])
+def test_runtime_sees_the_spatial_slice_cu_count(tmp_region, mode, pct, want):
     """Reference: cuDeviceGetAttribute virtualisation [device.c:130-134]. A 25 % vGPU with
     a CU slice (spatial, or auto whichever enforcement is on) reports 64 CUs to HIP
     (multiProcessorCount), so stock libraries size grids for the slice; stock GEMM / conv
-    still compute correctly. Explicitly temporal vGPUs keep 256."""
-    c = vgpu_env(mem_limit=24 * GiB, cu_limit=25, cu_mode=mode, shared_cache=tmp_region)
+    still compute correctly. Explicitly temporal vGPUs keep 256, and so does a thin share in
+    auto mode (7 %: a 16-CU slice is time-sliced on every CU, VGPU_AUTO_MIN_SLICE_CUS)."""
+    c = vgpu_env(mem_limit=24 * GiB, cu_limit=pct, cu_mode=mode, shared_cache=tmp_region)
     res, _ = run_child(CU_PROPS, c)
     r = res[0]
     assert r["cus"] == want, r
