@@ -114,3 +114,16 @@ def test_exact_share_sent_only_with_the_ledger():
     with NodeHarness(b, device_split_count=4, ledger=True) as node:   # 25 % is exact already
         envs, _ = node.pod(node.vgpu_ids(u)[:1])
     assert envs["VGPU_DEVICE_CU_LIMIT_0"] == "25" and "VGPU_DEVICE_CU_SHARE_0" not in envs
+
+
+def test_ledger_is_the_default_path():
+    """Round 4 picks one default: the plugin runs the node ledger and sends exact shares
+    unless --ledger=false (profiles/r4o)."""
+    from amdvgpu.plugin.config import PluginConfig
+    from amdvgpu.plugin.devices import FakeBackend
+    from amdvgpu.plugin.kubelet_stub import NodeHarness
+    assert PluginConfig().ledger is True
+    b = FakeBackend(n=1)
+    with NodeHarness(b, device_split_count=12) as node:
+        envs, _ = node.pod(node.vgpu_ids(b.devices()[0].uuid)[:1])
+    assert envs["VGPU_DEVICE_CU_LIMIT_0"] == "9" and envs["VGPU_DEVICE_CU_SHARE_0"] == "8.3333"
