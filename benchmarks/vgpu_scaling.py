@@ -34,7 +34,7 @@ def worker(case_name, steps, warmup, out, go_file, seconds):
     faulthandler.dump_traceback_later(200, exit=False)  # a pod stuck in warm-up shows where
     import torch
     from amdvgpu.models.aibench import Runner, get_case
-    torch.backends.cudnn.benchmark = True  # MIOpen find mode
+    torch.backends.cudnn.benchmark = os.environ.get("VGPU_BENCH_AUTOTUNE", "1") != "0"  # MIOpen find mode
     case = get_case(case_name)
     t_import = time.time()
     r = Runner(case, "cuda:0", dtype=torch.float32)
