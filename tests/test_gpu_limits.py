@@ -706,7 +706,7 @@ if mode == "own":
 else:
     open(os.environ["SPILL_GO"], "w").close()                             # the neighbour frees its HBM
 t0 = time.time()
-while spilled() and time.time() - t0 < 20:
+while spilled() and time.time() - t0 < float(os.environ.get("SPILL_WAIT", "20")):
     time.sleep(0.02)
 t_promote = round(time.time() - t0, 3)
 s1 = spilled()
@@ -774,6 +774,21 @@ def test_spill_is_promoted_after_hbm_frees_up(tmp_region, tmp_path, neighbour):
     assert r["ok_before"] and r["ok_after"], r
     assert r["spilled_after"] == 0, r
     assert r["gbps_promoted"] > 3 * r["gbps_spilled"], r
+
+
+def test_pinned_spill_backing_stays_in_host_memory(tmp_region):
+    """VGPU_SPILL_BACKING=pinned keeps the round-3 spill: a pinned host-pool allocation the
+    GPU reads in place, correct, and never moved (it stays spilled after HBM frees up)."""
+    c = vgpu_env(mem_limit=16 * GiB, shared_cache=tmp_region, oversubscribe=True,
+                 extra={"VGPU_DEVICE_HBM_LIMIT_0": "4096m", "VGPU_SPILL_POLICY": "first-come",
+                        "VGPU_SPILL_BACKING": "pinned"})
+    res, _ = run_child(SPILL_PROMOTE, c, extra_env={"SPILL_MODE": "own", "SPILL_ELEMS": str(1 << 28),
+                                                    "SPILL_WAIT": "2"})
+    r = res[0]
+    print("pinned spill:", r)
+    assert r["spilled_before"] >= r["bytes"], r
+    assert r["ok_before"] and r["ok_after"], r
+    assert r["spilled_after"] >= r["bytes"], r   # still in host memory: a pinned spill never moves
 
 
 CU_PROPS = """
