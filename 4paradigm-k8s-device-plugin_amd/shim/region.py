@@ -38,6 +38,7 @@ class DeviceInfo(C.Structure):
         ("cu_mask", C.c_uint32 * 8), ("credit_ns", C.c_int64), ("charged_ns", C.c_uint64),
         ("wall_ns", C.c_uint64), ("util_pct", C.c_int32), ("cu_mode", C.c_int32), ("gpu_id", C.c_uint32), ("bdf", C.c_uint32), ("domain", C.c_uint32), ("configured", C.c_uint32),
         ("hbm_limit", C.c_uint64), ("crowd", C.c_int32), ("preempt", C.c_int32), ("depth_cap", C.c_int32),
+        ("cu_share_bp", C.c_int32),
     ]
 
 
@@ -60,6 +61,7 @@ def lib():
             "vgpu_region_procs": (C.c_int, [P, C.POINTER(ProcInfo), C.c_int]),
             "vgpu_region_set_memory_limit": (C.c_int, [P, C.c_int, C.c_uint64]),
             "vgpu_region_set_cu_limit": (C.c_int, [P, C.c_int, C.c_int]),
+            "vgpu_region_set_cu_share": (C.c_int, [P, C.c_int, C.c_int]),
             "vgpu_region_suspend_all": (C.c_int, [P]),
             "vgpu_region_resume_all": (C.c_int, [P]),
             "vgpu_region_suspended": (C.c_int, [P]),
@@ -153,7 +155,7 @@ class Region:
             "charged_ns": d.charged_ns, "wall_ns": d.wall_ns, "util_pct": d.util_pct,
             "cu_mode": CU_MODES.get(d.cu_mode, str(d.cu_mode)), "gpu_id": d.gpu_id, "bdf": d.bdf, "domain": d.domain,
             "configured": bool(d.configured), "hbm_limit": d.hbm_limit, "crowd": d.crowd,
-            "preempt": bool(d.preempt), "depth_cap": d.depth_cap,
+            "preempt": bool(d.preempt), "depth_cap": d.depth_cap, "cu_share_bp": d.cu_share_bp,
         }
 
     def devices(self):
@@ -201,6 +203,10 @@ class Region:
 
     def set_cu_limit(self, dev, pct):
         return lib().vgpu_region_set_cu_limit(self._h, dev, int(pct))
+
+    def set_cu_share(self, dev, bp):
+        """Exact GPU-time share of the limiter's grants, basis points (0 = the CU limit)."""
+        return lib().vgpu_region_set_cu_share(self._h, dev, int(bp))
 
     def suspend_all(self):
         return lib().vgpu_region_suspend_all(self._h)

@@ -59,6 +59,7 @@ typedef struct {
   int32_t crowd;       /* auto mode: other busy processes seen on the GPU (-1 = not assessed) */
   int32_t preempt;     /* background class: launches held, a better class is busy (1) */
   int32_t depth_cap;   /* background class: packets in flight allowed per process (0 = any) */
+  int32_t cu_share_bp; /* exact GPU-time share of the grants, basis points (0 = cu_limit_pct) */
 } vgpu_device_info;
 
 /* Returns NULL on failure; *err receives -errno. */
@@ -73,6 +74,9 @@ int vgpu_region_proc_count(vgpu_region* r);
 int vgpu_region_procs(vgpu_region* r, vgpu_proc_info* out, int max);
 int vgpu_region_set_memory_limit(vgpu_region* r, int dev, uint64_t bytes);
 int vgpu_region_set_cu_limit(vgpu_region* r, int dev, int pct);
+/* Sets the exact GPU-time share (basis points, 0 = the whole-percent limit) as it stands in
+   the region: what a container's limiter grants from (a plugin ceiling clamps it). */
+int vgpu_region_set_cu_share(vgpu_region* r, int dev, int bp);
 int vgpu_region_suspend_all(vgpu_region* r);
 int vgpu_region_resume_all(vgpu_region* r);
 int vgpu_region_suspended(vgpu_region* r);

@@ -66,6 +66,7 @@ int vgpu_region_device_info(vgpu_region* r, int dev, vgpu_device_info* out) {
   out->crowd = d.crowd.load();
   out->preempt = d.preempt.load();
   out->depth_cap = d.depth_cap.load();
+  out->cu_share_bp = d.cu_share_bp;
   return 0;
 }
 
@@ -107,6 +108,13 @@ int vgpu_region_set_memory_limit(vgpu_region* r, int dev, uint64_t bytes) {
 int vgpu_region_set_cu_limit(vgpu_region* r, int dev, int pct) {
   if (dev < 0 || dev >= kMaxDevices || pct < 0 || pct > 100) return -EINVAL;
   r->r.set_cu_limit(dev, pct);
+  return 0;
+}
+
+int vgpu_region_set_cu_share(vgpu_region* r, int dev, int bp) {
+  if (dev < 0 || dev >= kMaxDevices || bp < 0 || bp > 10000) return -EINVAL;
+  r->r.raw()->dev[dev].cu_share_bp = bp;
+  r->r.raw()->hdr.generation.fetch_add(1);
   return 0;
 }
 

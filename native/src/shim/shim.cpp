@@ -285,6 +285,8 @@ void install_ceilings(const char* const* uuid_ptrs) {
     const int pct = per[i].cu_limit_pct;
     if (pct > 0 && pct < 100) {
       a.ceil_pct = pct;
+      // The grant basis: the file's exact share, or its whole-percent limit.
+      a.ceil_share_bp = per[i].cu_share_bp > 0 ? per[i].cu_share_bp : pct * 100;
       const char* layout = getenv("VGPU_CU_LAYOUT");
       a.ceil_mask = cu_mask_for(a.cu_count, a.num_xcc, pct, per[i].cu_range_begin, per[i].cu_range_end,
                                 (layout && !strcasecmp(layout, "interleave")) ? 1 : a.num_se);
@@ -559,6 +561,19 @@ bool clamp_region_to_ceiling() {
       if (d.cu_limit_pct <= 0 || d.cu_limit_pct >= 100 || d.cu_limit_pct > a.ceil_pct) {
         VLOG_WARN("device %d: region CU limit %d%% above the plugin's %d%%; clamped", i, d.cu_limit_pct, a.ceil_pct);
         d.cu_limit_pct = a.ceil_pct;
+        clamped = true;
+      }
+      // The exact share the GPU-time grants use (with the node ledger) is a limit too: the
+      // grant basis (the share, or the whole-percent limit when it is 0) may not exceed the
+      // file's share nor the region's (possibly lowered) limit.
+      const int pct_bp = d.cu_limit_pct * 100;
+      const int limit_bp = std::min(a.ceil_share_bp, pct_bp);
+      int share = d.cu_share_bp;
+      if ((share > 0 ? share : pct_bp) > limit_bp) share = limit_bp == pct_bp ? 0 : limit_bp;
+      if (share != d.cu_share_bp) {
+        VLOG_WARN("device %d: region GPU-time share %d bp outside the plugin's %d bp; clamped", i, d.cu_share_bp,
+                  a.ceil_share_bp);
+        d.cu_share_bp = share;
         clamped = true;
       }
       // The slice may be narrowed live (set_cu_limit), never moved onto other CUs or widened.

@@ -44,6 +44,7 @@ struct AgentInfo {
   // Plugin ceiling (limits file) for this agent: its CU share and slice; the region's may
   // only be narrower (0 = no ceiling).
   int ceil_pct = 0;
+  int ceil_share_bp = 0;                     // exact GPU-time share of the file (basis points, 0 = none)
   CuMask ceil_mask;
   hsa_amd_memory_pool_t pools[kMaxAgentPools]{};  // GPU-local global pools (and regions) of this agent
   hsa_amd_memory_pool_t vram_pool{0};  // coarse-grained VRAM pool (host-PID probe allocations)

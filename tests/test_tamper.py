@@ -129,6 +129,27 @@ def test_region_rewritten_upward_is_clamped(pod):
         assert d["mem_limit"] == GiB and d["cu_limit_pct"] == 25 and r.priority == 1, (d, r.priority)
 
 
+def test_region_share_rewritten_upward_is_clamped(pod):
+    """With the node ledger the limiter grants from the exact share (6.25 % at split 16, the
+    limits file's VGPU_DEVICE_CU_SHARE_0): a tenant writing 100 % into its region gets the
+    plugin's share back, and an operator's lower limit still lowers the grant basis."""
+    e = pod(VGPU_DEVICE_CU_LIMIT_0="7", VGPU_DEVICE_CU_SHARE_0="6.25", VGPU_CU_MODE="temporal")
+    e.update(VGPU_DEVICE_CU_LIMIT_0="7", VGPU_DEVICE_CU_SHARE_0="6.25", VGPU_CU_MODE="temporal")
+    p = _start(e, "malloc=1m", "mark=ready", "sleep=0.6", "mark=two", "sleep=0.6")
+    _wait_mark(p)
+    with Region(str(pod.region)) as r:
+        assert r.device(0)["cu_share_bp"] == 625
+        r.set_cu_share(0, 10000)
+    _wait_mark(p)
+    with Region(str(pod.region)) as r:
+        assert r.device(0)["cu_share_bp"] == 625, r.device(0)
+        r.set_cu_limit(0, 5)             # the operator lowers the limit live (share reset to 0)
+    _finish(p)
+    with Region(str(pod.region)) as r:
+        d = r.device(0)
+    assert d["cu_limit_pct"] == 5 and d["cu_share_bp"] == 0, d   # 5 % < 6.25 %: the limit is the basis
+
+
 def test_wiped_region_is_recharged(pod):
     """The region is overwritten (zeroed) while a process holds 768 MiB: the process notices
     within a period, re-initialises the region and charges its allocation again, so a second
