@@ -400,6 +400,10 @@ void apply_ceiling(Config* cfg, const Config& ceil) {
   cfg->shared_cache = ceil.shared_cache;
   if (!ceil.device_map.empty()) cfg->device_map = ceil.device_map;
   if (!ceil.allowlist.empty()) cfg->allowlist = ceil.allowlist;
+  // The board (and the node ledger in it) is the plugin's too: a board of the tenant's own
+  // could carry a forged ledger with no charges.
+  if (!ceil.board_dir.empty()) cfg->board_dir = ceil.board_dir;
+  if (!ceil.board_slot.empty()) cfg->board_slot = ceil.board_slot;
   cfg->cu_mode = ceil.cu_mode;
   cfg->oversubscribe = cfg->oversubscribe && ceil.oversubscribe;
   if (ceil.min_priority > cfg->min_priority) cfg->min_priority = ceil.min_priority;
@@ -408,6 +412,7 @@ void apply_ceiling(Config* cfg, const Config& ceil) {
   // Switches that would lift enforcement are the operator's, not the tenant's.
   cfg->disabled = false;
   cfg->fail_open = false;
+  cfg->use_ledger = true;  // the ledger's exact charges are not the tenant's to opt out of
   if (cfg->cu_policy == CuPolicy::kDisable) cfg->cu_policy = CuPolicy::kDefault;
   cfg->ceiling = true;
 }

@@ -150,6 +150,21 @@ def test_region_share_rewritten_upward_is_clamped(pod):
     assert d["cu_limit_pct"] == 5 and d["cu_share_bp"] == 0, d   # 5 % < 6.25 %: the limit is the basis
 
 
+def test_board_and_ledger_are_the_plugins(pod, tmp_path):
+    """The node board (and the GPU-time ledger in it) comes from the limits file: a tenant
+    pointing VGPU_BOARD_DIR at a directory of its own - where it could forge a ledger with no
+    charges - still publishes to, and reads, the plugin's board."""
+    plugin_board, own_board = tmp_path / "board", tmp_path / "mine"
+    plugin_board.mkdir()
+    own_board.mkdir()
+    e = pod(VGPU_BOARD_DIR=str(plugin_board), VGPU_BOARD_SLOT="c1.slot", VGPU_CU_MODE="temporal")
+    e.update(VGPU_BOARD_DIR=str(own_board), VGPU_BOARD_SLOT="forged.slot", VGPU_LEDGER="0",
+             VGPU_CU_MODE="temporal")
+    run(e, "malloc=1m", "stream", "launch=100,20", "sleep=0.6")
+    assert (plugin_board / "c1.slot").exists()
+    assert not any(own_board.iterdir())
+
+
 def test_wiped_region_is_recharged(pod):
     """The region is overwritten (zeroed) while a process holds 768 MiB: the process notices
     within a period, re-initialises the region and charges its allocation again, so a second
