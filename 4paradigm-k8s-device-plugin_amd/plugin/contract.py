@@ -127,7 +127,8 @@ REGION_MAX_AGE_S = 3600
 # The env names the limits file carries (the shim reads it with the env parser).
 LIMIT_KEYS = ("VGPU_DEVICE_MAP", "VGPU_DEVICE_MEMORY_LIMIT_", "VGPU_DEVICE_HBM_LIMIT_", "VGPU_DEVICE_CU_LIMIT_",
               "VGPU_DEVICE_CU_SHARE_", "VGPU_DEVICE_CU_RANGE_", "VGPU_HOST_MEMORY_LIMIT", "VGPU_OVERSUBSCRIBE",
-              "VGPU_CU_MODE", "VGPU_SHARED_CACHE", "VGPU_ALLOWLIST", "VGPU_BOARD_DIR", "VGPU_BOARD_SLOT")
+              "VGPU_CU_MODE", "VGPU_SHARED_CACHE", "VGPU_ALLOWLIST", "VGPU_BOARD_DIR", "VGPU_BOARD_SLOT",
+              "VGPU_GPU_CONCURRENCY")
 
 
 def _gc_dir(d, suffix, max_age_s):

@@ -404,6 +404,7 @@ void apply_ceiling(Config* cfg, const Config& ceil) {
   // could carry a forged ledger with no charges.
   if (!ceil.board_dir.empty()) cfg->board_dir = ceil.board_dir;
   if (!ceil.board_slot.empty()) cfg->board_slot = ceil.board_slot;
+  if (ceil.gpu_concurrency > 0) cfg->gpu_concurrency = ceil.gpu_concurrency;  // the node's admission
   cfg->cu_mode = ceil.cu_mode;
   cfg->oversubscribe = cfg->oversubscribe && ceil.oversubscribe;
   if (ceil.min_priority > cfg->min_priority) cfg->min_priority = ceil.min_priority;

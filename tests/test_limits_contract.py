@@ -131,3 +131,17 @@ def test_emulated_container_is_held_to_the_plugins_limits(tmp_path):
     assert [o for o in out if "total" in o][0]["total"] == 2 * GiB
     assert [o["malloc"] for o in out if "malloc" in o] == ["ok", "oom"]
     assert [q["cus"] for q in [o for o in out if "queues" in o][0]["queues"]] == [64]
+
+
+def test_limits_file_carries_the_board_and_admission(tmp_path):
+    """The node board (where the GPU-time ledger lives), the container's slot in it, the
+    exact share and the node's admission bound are ceilings like the quotas: the limits file
+    carries them, so a tenant's own env cannot move it to a board of its making."""
+    with NodeHarness(FakeBackend(n=1), device_split_count=16, gpu_concurrency=4,
+                     workdir=str(tmp_path / "node")) as node:
+        envs, mounts = node.pod(node.vgpu_ids(FakeBackend(n=1).devices()[0].uuid)[:1])
+        limits_host = dict(mounts)["/vgpu/limits"]
+        lim = dict(l.split("=", 1) for l in open(limits_host).read().splitlines())
+    for k in ("VGPU_BOARD_DIR", "VGPU_BOARD_SLOT", "VGPU_GPU_CONCURRENCY", "VGPU_DEVICE_CU_SHARE_0"):
+        assert lim.get(k) == envs[k], (k, lim.get(k), envs.get(k))
+
