@@ -282,6 +282,17 @@ def test_peer_access_to_an_svm_spill(fake):
     assert [(o["peer"], o["svm_access"]) for o in out if "peer" in o] == [(0, 1)]
 
 
+def test_svm_spill_survives_a_fork(fake):
+    """A forked child (DataLoader worker) neither inherits the parent's SVM spills (the ranges
+    are MADV_DONTFORK) nor disturbs them: the parent's spill is still promoted afterwards."""
+    out = run(_svm_env(fake), "malloc=48m", "malloc=32m", "fill=5", "forkmalloc=1m", "freeidx=0", "sleep=0.6",
+              "where", "check=5", "spilled")
+    assert [o["child_malloc"] for o in out if "child_malloc" in o] == ["ok"]
+    assert [o["where"] for o in out if "where" in o] == [0]
+    assert [o for o in out if "check" in o][0]["check"] == "ok"
+    assert [o["spilled"] for o in out if "spilled" in o] == [0]
+
+
 def test_svm_spill_waits_for_room(fake):
     """Nothing was freed: the share (48 MiB resident + 32 + the 16 MiB reserve > 64 MiB)
     has no room, so the spill stays in host memory."""
