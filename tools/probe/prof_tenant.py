@@ -107,6 +107,25 @@ def timed_window(d, steps):
             "top_timed": [(n[:70], round(t / 1e6 / steps, 3)) for n, t in top]}
 
 
+def hip_api_table(out, keys):
+    """Per-function HIP API call counts and mean duration (whole process) for every mode,
+    from rocprofv3's hip_api_stats.csv, the functions with the most total time first."""
+    per = {}
+    for k in keys:
+        f = find(os.path.join(out, k), "*hip_api_stats.csv")
+        for r in (csv.DictReader(open(f)) if f else []):
+            per.setdefault(r["Name"], {})[k] = (int(r["Calls"]), float(r["TotalDurationNs"]))
+    names = sorted(per, key=lambda n: -max(t for _, t in per[n].values()))[:25]
+    md = ["| HIP function | " + " | ".join(f"{k} calls / mean us" for k in keys) + " |", "|---|" + "---|" * len(keys)]
+    for n in names:
+        cells = []
+        for k in keys:
+            c, t = per[n].get(k, (0, 0.0))
+            cells.append(f"{c} / {t / c / 1e3:.2f}" if c else "-")
+        md.append(f"| {n} | " + " | ".join(cells) + " |")
+    return "\n".join(md)
+
+
 def summarize(d, steps):
     out = timed_window(d, steps)
     ks = find(d, "*kernel_stats.csv")
@@ -141,14 +160,35 @@ def main():
     ap.add_argument("--modes", default="native,vgpu-quota,vgpu-t25")
     ap.add_argument("--runs", type=int, default=1)
     ap.add_argument("--autotune", type=int, default=1)
+    ap.add_argument("--hip-api", action="store_true", help="also trace the HIP runtime API (per-function call "
+                    "counts and time in <out>/hip_api.md)")
     ap.add_argument("--prewarm", type=int, default=1, help="run the tenant once unprofiled first (fills MIOpen's "
                     "find-db, so no profiled process pays the search)")
     a = ap.parse_args()
     if a.tenant:
         return tenant(a.steps, a.case, a.autotune)
     from amdvgpu.shim.launcher import apply_contract, cleanup_region, vgpu_env
+    pods = {}
+
+    def pod_env(ledger):
+        # the suite's interception-only pod (benchmarks/aibench_suite.py: split 2, cores
+        # scaling 2, memory scaling 1.8), through a plugin and stub kubelet
+        if ledger not in pods:
+            from amdvgpu.plugin.devices import SysfsBackend
+            from amdvgpu.plugin.kubelet_stub import NodeHarness
+            backend = SysfsBackend()
+            h = NodeHarness(backend, device_split_count=2, device_memory_scaling=1.8, host_memory_fraction=0.0,
+                            device_cores_scaling=2.0, ledger=ledger)
+            h.__enter__()
+            pods[ledger] = (h, backend.devices()[0].uuid)
+        h, uuid = pods[ledger]
+        envs, mounts = h.pod(h.vgpu_ids(uuid)[:1])
+        return apply_contract(envs, mounts)
+
     contracts = {
         "native": lambda: None,
+        "vgpu-pod": lambda: "pod",
+        "vgpu-pod-noledger": lambda: "pod-noledger",
         "vgpu-quota": lambda: vgpu_env(mem_limit=72 << 30),
         "vgpu-t25": lambda: vgpu_env(mem_limit=72 << 30, cu_limit=25, cu_mode="temporal", extra={"VGPU_TRACE": "1"}),
     }
@@ -159,11 +199,14 @@ def main():
     for run in range(a.runs):
         for mode in (a.modes.split(",") if run % 2 == 0 else a.modes.split(",")[::-1]):
             c = contracts[mode]()
-            env = apply_contract(c) if c else dict(os.environ)
+            if isinstance(c, str):
+                env, c = pod_env(c == "pod"), None
+            else:
+                env = apply_contract(c) if c else dict(os.environ)
             key = mode if a.runs == 1 else f"{mode}.{run}"
             d = os.path.join(a.out, key)
-            cmd = ["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "--output-format", "csv", "-d", d, "-o", mode,
-                   "--",
+            cmd = ["rocprofv3", "--kernel-trace", "--marker-trace", *(["--hip-runtime-trace"] if a.hip_api else []),
+                   "--stats", "--output-format", "csv", "-d", d, "-o", mode, "--",
                    sys.executable, os.path.abspath(__file__), "--tenant", "--steps", str(a.steps), "--case", a.case,
                    "--autotune", str(a.autotune)]
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
@@ -191,7 +234,11 @@ def main():
     for m, r in sorted(res.items()):
         md += ["", f"Top kernels in the timed window ({m}, ms/step): " +
                "; ".join(f"{n} {t}" for n, t in r.get("top_timed", []))]
+    for h, _ in pods.values():
+        h.__exit__(None, None, None)
     os.makedirs(a.out, exist_ok=True)
+    if a.hip_api:
+        open(os.path.join(a.out, "hip_api.md"), "w").write(hip_api_table(a.out, sorted(res)) + "\n")
     open(os.path.join(a.out, "summary.md"), "w").write("\n".join(md) + "\n")
     json.dump(res, open(os.path.join(a.out, "summary.json"), "w"), indent=1)
     print("\n".join(md))
