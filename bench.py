@@ -192,17 +192,31 @@ def worker(args):
                 ev.synchronize()
         else:
             wait = sync
+        # When each step finished, on this process's perf_counter clock (shared by the pods of
+        # a host): a timing event after every step, read back once at the end, so the parent
+        # can rate every pod over the window in which all of them run (common_window()).
+        marks = []
         n = 0
         t0 = time.perf_counter()
+        if not cpu:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         while time.perf_counter() - t0 < args.seconds:
             runner.step()
             n += 1
+            if cpu:
+                marks.append(time.perf_counter())
+            else:
+                marks.append(torch.cuda.Event(enable_timing=True))
+                marks[-1].record()
             if n % 4 == 0:
                 wait()
         wait()
         dt = time.perf_counter() - t0
+        done = marks if cpu else [t0 + ev0.elapsed_time(e) / 1000.0 for e in marks]
         res = {"mode": args.mode, "ms_per_step": dt * 1000.0 / n, "items_per_step": runner.items_per_step,
-               "steps": n, "t0": t0, "t1": t0 + dt, "startup": {k: round(v, 2) for k, v in phases.items()}}
+               "steps": n, "t0": t0, "t1": t0 + dt, "step_done": done,
+               "startup": {k: round(v, 2) for k, v in phases.items()}}
     else:
         # The limiter's own account of the timed window (GPU time charged / wall time), read
         # from the pod's shared region like vgpuctl would: what the vGPU granted this pod.
@@ -413,6 +427,34 @@ def run_concurrent(args, envs, label, deadline=None, before_go=None):
                 p.kill()
 
 
+def common_window(res, min_frac=0.5):
+    """Every pod's throughput over the window in which all of them run: from the latest
+    start to the earliest last completed step. Each pod measures its own window, and these
+    differ at the ends by up to the steps it has queued (4 between waits: most of a second
+    for a 16-pod share of ResNet-50); a pod still running after the others stop has the GPU
+    to itself and looks faster, the others slower. A step counts in proportion to the part
+    of (previous completion, its completion] inside the window. Returns (per-pod items/s,
+    window seconds), or None when the window is shorter than ``min_frac`` of the pods'
+    median run (the own-window rates stand then)."""
+    if not res or any(not r.get("step_done") for r in res):
+        return None
+    w0 = max(r["t0"] for r in res)
+    w1 = min(r["step_done"][-1] for r in res)
+    runs = sorted(r["t1"] - r["t0"] for r in res)
+    if w1 - w0 < min_frac * runs[len(runs) // 2]:
+        return None
+    rates = []
+    for r in res:
+        items, prev = 0.0, r["t0"]
+        for done in r["step_done"]:
+            lo, hi = max(prev, w0), min(done, w1)
+            if hi > lo and done > prev:
+                items += r["items_per_step"] * (hi - lo) / (done - prev)
+            prev = done
+        rates.append(items / (w1 - w0))
+    return rates, w1 - w0
+
+
 def miopen_env(mode, root, i):
     """MIOpen find-db / kernel cache of sweep pod ``i`` (``--sweep-find-db``)."""
     if mode == "home":
@@ -479,10 +521,14 @@ def _sweep_points(args, backend, uuid, tenants, end, root):
             continue
         if n > 1:
             last = (n, now() - t_point)
-        tput = [r["items_per_step"] * r["steps"] / (r["t1"] - r["t0"]) for r in res]
+        own = [r["items_per_step"] * r["steps"] / (r["t1"] - r["t0"]) for r in res]
         span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
-        agg = sum(r["items_per_step"] * r["steps"] for r in res) / span
+        agg_span = sum(r["items_per_step"] * r["steps"] for r in res) / span
+        cw = common_window(res)
+        tput, agg = (cw[0], sum(cw[0])) if cw else (own, agg_span)
         rows.append({"tenants": n, "aggregate": round(agg, 2), "per_tenant": [round(t, 2) for t in tput],
+                     "window": f"common {cw[1]:.2f} s" if cw else "own",
+                     "per_tenant_own_window": [round(t, 2) for t in own], "aggregate_span": round(agg_span, 2),
                      "cu_limit_pct": int(c0.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0),
                      "cu_mode": c0.get("VGPU_CU_MODE"), "quota_mib": int(c0["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m"))})
         print(f"[bench] sweep {n} tenants: aggregate {agg:.1f}, per tenant {min(tput):.1f}..{max(tput):.1f} "
@@ -521,8 +567,11 @@ def node_point(args, backend, uuid, world, rank, port):
             envs = [pod_env(node, [i])[0] for i in ids]
             res = run_concurrent(args, envs, "node", deadline=T_START + args.time_budget - args.sweep_seconds - 15.0,
                                  before_go=gate)
+        own = [round(r["items_per_step"] * r["steps"] / (r["t1"] - r["t0"]), 2) for r in res]
+        cw = common_window(res)
         mine = {"ok": True, "uuid": uuid, "pods": len(res),
-                "per_pod": [round(r["items_per_step"] * r["steps"] / (r["t1"] - r["t0"]), 2) for r in res],
+                "per_pod": [round(t, 2) for t in cw[0]] if cw else own, "per_pod_own_window": own,
+                "window": f"common {cw[1]:.2f} s" if cw else "own",
                 "seconds": round(now() - t_point, 1)}
     except (Exception, SystemExit) as e:  # noqa: BLE001 - reported in the line, never a hang
         if not passed[0] and world > 1:

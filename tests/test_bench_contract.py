@@ -122,3 +122,30 @@ def test_sweep_respects_the_time_budget(monkeypatch):
     # 1 + 2 + 4 pods take 70 s; 8 pods are estimated at 80 s (150 < 200: run), 12 at 120 s.
     assert measured == [1, 2, 4, 8] and skipped == [12], rows
     assert best == 8
+
+
+def test_common_window_rates_pods_while_all_run():
+    """Concurrent pods are rated over the window in which all of them run. A pod whose own
+    window runs on after the others stop has the GPU to itself there; its own-window rate
+    flatters it and the common window does not."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    # two pods at 10 items/s while both run (steps of 1 s, 10 items); pod b runs 2 s longer
+    # alone at twice the rate (steps of 0.5 s)
+    a = {"items_per_step": 10, "steps": 6, "t0": 0.0, "t1": 6.0, "step_done": [1.0 * i for i in range(1, 7)]}
+    b_done = [1.0 * i for i in range(1, 7)] + [6.5, 7.0, 7.5, 8.0]
+    b = {"items_per_step": 10, "steps": 10, "t0": 0.0, "t1": 8.0, "step_done": b_done}
+    rates, w = bench.common_window([a, b])
+    assert w == pytest.approx(6.0) and rates == pytest.approx([10.0, 10.0])
+    # own windows: b looks 25 % faster
+    assert b["items_per_step"] * b["steps"] / (b["t1"] - b["t0"]) == pytest.approx(12.5)
+    # a step straddling the window's edge counts in proportion
+    c = {"items_per_step": 10, "steps": 3, "t0": 0.5, "t1": 6.5, "step_done": [2.5, 4.5, 6.5]}
+    rates, w = bench.common_window([a, c])
+    assert w == pytest.approx(5.5)  # 0.5 .. 6.0
+    assert rates[0] == pytest.approx(55.0 / 5.5) and rates[1] == pytest.approx((10 + 10 + 7.5) / 5.5)
+    # no per-step marks (older workers) or a window too short to rate: None
+    assert bench.common_window([dict(a, step_done=[]), b]) is None
+    late = {"items_per_step": 10, "steps": 1, "t0": 5.5, "t1": 6.0, "step_done": [6.0]}
+    assert bench.common_window([a, late]) is None
