@@ -195,8 +195,10 @@ def worker(args):
         # When each step finished, on this process's perf_counter clock (shared by the pods of
         # a host): a timing event after every step, read back once at the end, so the parent
         # can rate every pod over the window in which all of them run (common_window()).
+        import resource
         marks = []
         n = 0
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         if not cpu:
             ev0 = torch.cuda.Event(enable_timing=True)
@@ -213,9 +215,13 @@ def worker(args):
                 wait()
         wait()
         dt = time.perf_counter() - t0
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
         done = marks if cpu else [t0 + ev0.elapsed_time(e) / 1000.0 for e in marks]
         res = {"mode": args.mode, "ms_per_step": dt * 1000.0 / n, "items_per_step": runner.items_per_step,
                "steps": n, "t0": t0, "t1": t0 + dt, "step_done": done,
+               # CPU seconds of every thread of the pod in its window (the box runs all pods in
+               # one 16-CPU quota: a point whose pods need more is CPU-bound, not GPU-bound)
+               "cpu_s": round(ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime, 3),
                "startup": {k: round(v, 2) for k, v in phases.items()}}
     else:
         # The limiter's own account of the timed window (GPU time charged / wall time), read
@@ -529,6 +535,7 @@ def _sweep_points(args, backend, uuid, tenants, end, root):
         rows.append({"tenants": n, "aggregate": round(agg, 2), "per_tenant": [round(t, 2) for t in tput],
                      "window": f"common {cw[1]:.2f} s" if cw else "own",
                      "per_tenant_own_window": [round(t, 2) for t in own], "aggregate_span": round(agg_span, 2),
+                     "cpus_busy": round(sum(r.get("cpu_s", 0.0) for r in res) / span, 2),
                      "cu_limit_pct": int(c0.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0),
                      "cu_mode": c0.get("VGPU_CU_MODE"), "quota_mib": int(c0["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m"))})
         print(f"[bench] sweep {n} tenants: aggregate {agg:.1f}, per tenant {min(tput):.1f}..{max(tput):.1f} "

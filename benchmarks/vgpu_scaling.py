@@ -178,14 +178,15 @@ def miopen_dirs(mode, tmp, i):
     return {"MIOPEN_USER_DB_PATH": db, "MIOPEN_CUSTOM_CACHE_DIR": cache}
 
 
-def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None, split=0, ledger=False,
+def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None, split=0, ledger=None,
               miopen="home"):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="scal-")
     go = os.path.join(tmp, "go")
     procs, outs, regions = [], [], []
-    with NodeHarness(backend, device_split_count=split or n, cu_mode=MODES[policy], ledger=ledger) as node:
+    kw = {} if ledger is None else {"ledger": bool(ledger)}
+    with NodeHarness(backend, device_split_count=split or n, cu_mode=MODES[policy], **kw) as node:
         for i, vid in enumerate(node.vgpu_ids(uuid)[:n]):
             envs, mounts = node.pod([vid])
             out = os.path.join(tmp, f"t{i}.json")
@@ -249,7 +250,9 @@ def main():
                     help="KEY=V1,V2,...: extra env in every pod, one sweep per value (repeatable)")
     ap.add_argument("--repeats", type=int, default=1)
     ap.add_argument("--split", type=int, default=0, help="vGPUs per GPU (default: one per pod)")
-    ap.add_argument("--node-ledger", action="store_true", help="the plugin runs the node GPU-time ledger (vgpu-ledger)")
+    ap.add_argument("--node-ledger", type=int, choices=[0, 1], default=None,
+                    help="1/0: the plugin runs the node GPU-time ledger (vgpu-ledger) or not (default: the "
+                    "plugin's default, on)")
     ap.add_argument("--miopen-db", default="home", choices=["home", "per-pod", "empty"],
                     help="MIOpen find-db / kernel cache of the pods (see miopen_dirs)")
     ap.add_argument("--worker", action="store_true")

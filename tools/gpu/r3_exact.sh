@@ -7,4 +7,4 @@ tenants=${2:-1,12,16}
 reps=${3:-1}
 mkdir -p "$out"
 timeout -k 10 1080 python -u benchmarks/vgpu_scaling.py --policy default --seconds 10 --tenants "$tenants" \
-  --repeats "$reps" --node-ledger --json-out "$out/exact.json" --md-out "$out/exact.md" > "$out/exact.log" 2>&1
+  --repeats "$reps" --node-ledger 1 --json-out "$out/exact.json" --md-out "$out/exact.md" > "$out/exact.log" 2>&1

@@ -6,6 +6,6 @@ out=${1:-gpurun_out/r3u}
 tenants=${2:-1,12,16}
 reps=${3:-1}
 mkdir -p "$out"
-timeout -k 10 1080 python -u benchmarks/vgpu_scaling.py --policy default --seconds 10 --tenants "$tenants" --node-ledger \
+timeout -k 10 1080 python -u benchmarks/vgpu_scaling.py --policy default --seconds 10 --tenants "$tenants" --node-ledger 1 \
   --repeats "$reps" --pod-env "VGPU_LEDGER=1,0" --json-out "$out/ledger.json" --md-out "$out/ledger.md" \
   > "$out/ledger.log" 2>&1
