@@ -182,14 +182,24 @@ def worker(args):
         open(args.result_file + ".ready", "w").close()
         while not os.path.exists(args.go):
             time.sleep(0.002)
-        # The pods wait for their GPU work blocked, not spinning: on this box every pod runs in
-        # one CPU quota, where many spinning pods starve each other's launch threads (on a node
-        # each pod has CPUs of its own). VGPU_BENCH_SYNC=spin keeps torch's default wait.
-        if not cpu and os.environ.get("VGPU_BENCH_SYNC", "block") != "spin":
+        # How a pod waits for its GPU work. On this box every pod runs in one 16-CPU quota, and
+        # a GPU-bound pod's main thread stays busy through HIP's blocking event wait as through
+        # torch's synchronize (profiles/r4za): 16 waiting pods starve the ones that have work
+        # to launch (on a node each pod has CPUs of its own). The default, poll, keeps 3 steps
+        # in flight and sleeps between queries of the oldest step's event, so the GPU always
+        # has queued work and a waiting pod holds no CPU. VGPU_BENCH_SYNC=block: a blocking
+        # event wait every 4 steps (round 4 before r4zc); spin: torch's synchronize.
+        sync_mode = "cpu" if cpu else os.environ.get("VGPU_BENCH_SYNC", "poll")
+        if sync_mode == "block":
             def wait():
                 ev = torch.cuda.Event(blocking=True)
                 ev.record()
                 ev.synchronize()
+        elif sync_mode == "poll":
+            def wait():
+                for e in marks:
+                    while not e.query():
+                        time.sleep(0.0005)
         else:
             wait = sync
         # When each step finished, on this process's perf_counter clock (shared by the pods of
@@ -211,14 +221,18 @@ def worker(args):
             else:
                 marks.append(torch.cuda.Event(enable_timing=True))
                 marks[-1].record()
-            if n % 4 == 0:
+            if sync_mode == "poll":
+                if n > 3:
+                    while not marks[n - 4].query():
+                        time.sleep(0.0005)
+            elif n % 4 == 0:
                 wait()
         wait()
         dt = time.perf_counter() - t0
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
         done = marks if cpu else [t0 + ev0.elapsed_time(e) / 1000.0 for e in marks]
         res = {"mode": args.mode, "ms_per_step": dt * 1000.0 / n, "items_per_step": runner.items_per_step,
-               "steps": n, "t0": t0, "t1": t0 + dt, "step_done": done,
+               "steps": n, "t0": t0, "t1": t0 + dt, "step_done": done, "wait": sync_mode,
                # CPU seconds of every thread of the pod in its window (the box runs all pods in
                # one 16-CPU quota: a point whose pods need more is CPU-bound, not GPU-bound)
                "cpu_s": round(ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime, 3),
@@ -536,6 +550,7 @@ def _sweep_points(args, backend, uuid, tenants, end, root):
                      "window": f"common {cw[1]:.2f} s" if cw else "own",
                      "per_tenant_own_window": [round(t, 2) for t in own], "aggregate_span": round(agg_span, 2),
                      "cpus_busy": round(sum(r.get("cpu_s", 0.0) for r in res) / span, 2),
+                     "pod_wait": res[0].get("wait"),
                      "cu_limit_pct": int(c0.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0),
                      "cu_mode": c0.get("VGPU_CU_MODE"), "quota_mib": int(c0["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m"))})
         print(f"[bench] sweep {n} tenants: aggregate {agg:.1f}, per tenant {min(tput):.1f}..{max(tput):.1f} "
