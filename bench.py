@@ -89,6 +89,8 @@ def parse(argv=None):
                          "never share one file system); home = this process's own (~/.config/miopen: one sqlite "
                          "set shared by every pod on this box); empty = each pod its own empty set (a pod's "
                          "first run: every pod runs its own find)")
+    ap.add_argument("--sweep-pod-env", action="append", default=[],
+                    help="KEY=VALUE added to the env of every sweep pod (studies; repeatable)")
     ap.add_argument("--node", default="auto", choices=["auto", "on", "off"],
                     help="node point: all --split vGPUs of every GPU of the job busy at once (BASELINE config 5: "
                          "32 vGPUs on 8 GPUs); auto = on for multi-GPU runs (single-GPU runs take it from the sweep)")
@@ -529,8 +531,9 @@ def _sweep_points(args, backend, uuid, tenants, end, root):
                 ids = node.vgpu_ids(uuid)[:n]
                 # The lone pod runs on this process's own find-db (the native run filled it);
                 # with several, each pod gets its own (--sweep-find-db).
-                pods = [pod_env(node, [i], miopen_env(args.sweep_find_db if n > 1 else "home", root,
-                                                      k + 100 * n))
+                extra = dict(kv.split("=", 1) for kv in args.sweep_pod_env)
+                pods = [pod_env(node, [i], {**(miopen_env(args.sweep_find_db if n > 1 else "home", root,
+                                                          k + 100 * n + 1000 * len(rows)) or {}), **extra})
                         for k, i in enumerate(ids)]
                 res = run_concurrent(args, [e for e, _ in pods], f"sweep{n}",
                                      deadline=end - args.sweep_seconds - 15.0)
