@@ -54,7 +54,7 @@ class PluginConfig:
     node_name: str = ""
     shared_cache_dir: str = "/tmp"
     placement: str = "spread"               # which GPU a 1-vGPU pod lands on (GetPreferredAllocation)
-    duplicate_vgpus: str = "reject"         # Allocate of two vGPUs of one GPU: reject | merge
+    duplicate_vgpus: str = "merge"          # Allocate of two vGPUs of one GPU: merge (one device, summed share) | reject
     host_memory_per_vgpu: str = "auto"      # pinned host memory budget per vGPU (auto: a share of the node's RAM; 0 = unlimited)
     host_memory_fraction: float = 0.5       # of the node's RAM, what vGPU containers may pin in total (buffers + spill)
     host_memory_total: str = ""             # the node's RAM (default: /proc/meminfo MemTotal)
@@ -64,6 +64,7 @@ class PluginConfig:
     gpu_concurrency: int = 0                # limited containers holding a GPU's time at once (0 = any)
     ledger: bool = True                     # run the node's GPU-time ledger daemon (vgpu-ledger; profiles/r4o)
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"  # kubelet PodResources v1
+    active_oom_killer: bool = True          # the containers' memory backstop (limits file; reference ACTIVE_OOM_KILLER)
     version_requested: bool = False
     extra: dict = field(default_factory=dict)
 
@@ -156,8 +157,9 @@ _FLAGS = [
     ("--placement", "placement", str, ["PLACEMENT_POLICY"],
      "GPU choice for a new pod: spread (the GPU with the most free vGPUs) | binpack (the fullest GPU with room)"),
     ("--duplicate-vgpus", "duplicate_vgpus", str, ["DUPLICATE_VGPUS"],
-     "a container given two vGPUs of one GPU: reject (fail Allocate) | merge (one device with the summed "
-     "quota and CU share; VGPU_DUPLICATE_MERGED tells the container)"),
+     "a container given two vGPUs of one GPU: merge (default: one device with the summed quota and CU share; "
+     "VGPU_DUPLICATE_MERGED and the amd-vgpu/merged-duplicates annotation tell the container) | reject (fail "
+     "Allocate)"),
     ("--host-memory-per-vgpu", "host_memory_per_vgpu", str, ["HOST_MEMORY_PER_VGPU"],
      "pinned host memory (hipHostMalloc / hipHostRegister, and the host spill of oversubscribed vGPUs) per vGPU, "
      "e.g. 64g; auto (default) = --host-memory-fraction of the node's RAM divided among its vGPUs; "
@@ -185,7 +187,12 @@ _FLAGS = [
      "samples by itself"),
     ("--pod-resources-socket", "pod_resources_socket", str, ["POD_RESOURCES_SOCKET"],
      "kubelet PodResources socket: monitor mode attributes container directories to the pods holding their "
-     "vGPUs through it (missing socket: the Allocate-time pod match stands)"),
+     "vGPUs through it, and a container's host files (limits, region, allow-list, board slot) are removed only "
+     "once it lists the container's devices as free (missing socket: nothing is removed)"),
+    ("--active-oom-killer", "active_oom_killer", "bool", ["ACTIVE_OOM_KILLER"],
+     "the containers' memory backstop: kill a container's largest process when KFD-measured VRAM stays above "
+     "its quota (plus a slack); written into the plugin-owned limits file, so a tenant cannot turn it off "
+     "(default true, as the reference's ACTIVE_OOM_KILLER)"),
 ]
 
 

@@ -53,9 +53,6 @@ CONTAINER_LOCK_DIR = "/usr/local/vgpu/lock"
 # time to busy containers of higher priority.
 BOARD_HOST_DIR = "board"
 CONTAINER_BOARD_DIR = "/usr/local/vgpu/board"
-# A publishing container touches its slot's mtime every 10 s (board.h kBoardTouchS), so a
-# slot untouched for an hour belongs to a container with no GPU process for that long.
-BOARD_MAX_AGE_S = 3600
 
 
 def ensure_board_dir(vgpu_dir):
@@ -67,9 +64,9 @@ def ensure_board_dir(vgpu_dir):
 def board_slot(vgpu_dir, name):
     """Creates this container's slot file (world-writable: the container's processes may
     run as any user; only this container mounts it read-write). Returns its path, or None
-    when there is no board directory. Slots untouched for an hour are removed: their
-    containers have had no GPU process for that long (a live one touches its slot every
-    10 s), and every reader otherwise keeps stat-ing them."""
+    when there is no board directory. Removed with the container's other files once its
+    pod is gone (gc_container_files), never by age: an idle container's slot is still the
+    source of its bind mount when the container restarts."""
     d = os.path.join(vgpu_dir, BOARD_HOST_DIR)
     if not os.path.isdir(d):
         return None
@@ -80,15 +77,6 @@ def board_slot(vgpu_dir, name):
         os.chmod(path, 0o666)
     except OSError:
         return None
-    try:
-        import time
-        now = time.time()
-        for fn in os.listdir(d):
-            fp = os.path.join(d, fn)
-            if fn.endswith(".slot") and now - os.path.getmtime(fp) > BOARD_MAX_AGE_S:
-                os.unlink(fp)
-    except OSError:
-        pass
     return path
 
 
@@ -108,7 +96,6 @@ ANN_DUPLICATES = "amd-vgpu/merged-duplicates"
 
 
 ALLOWLIST_HOST_DIR = "allowlist"
-ALLOWLIST_MAX_AGE_S = 7 * 24 * 3600
 
 # Plugin-owned limits (tamper resistance, native/include/vgpu/config.h load_ceiling): the
 # container's contract, written by the plugin into a root-owned file mounted read-only at
@@ -118,12 +105,17 @@ ALLOWLIST_MAX_AGE_S = 7 * 24 * 3600
 # inode the limits file records.
 LIMITS_HOST_DIR = "limits"
 CONTAINER_LIMITS = "/vgpu/limits"
-LIMITS_MAX_AGE_S = 7 * 24 * 3600
 REGIONS_HOST_DIR = "regions"
 CONTAINER_REGION_DIR = "/usr/local/vgpu/regions"
-# A container touches its region every 10 s while it has a GPU process; an older region file
-# is removed from the host directory (a running container keeps its mounted inode).
-REGION_MAX_AGE_S = 3600
+# Per-container host files (limits, region, allow-list, board slot) are the sources of the
+# container's bind mounts, which the kubelet reuses from its checkpoint when a container
+# restarts (it does not call Allocate again). They live as long as the pod that holds the
+# container's devices: each Allocate records the device IDs in a manifest
+# (<vgpu_dir>/containers/<name>.devices), and gc_container_files removes a container's
+# files only when the kubelet's PodResources no longer lists those devices as held - never
+# by age, and never when PodResources cannot be asked.
+MANIFEST_HOST_DIR = "containers"
+CONTAINER_GC_GRACE_S = 600
 # The env names the limits file carries (the shim reads it with the env parser).
 LIMIT_KEYS = ("VGPU_DEVICE_MAP", "VGPU_DEVICE_MEMORY_LIMIT_", "VGPU_DEVICE_HBM_LIMIT_", "VGPU_DEVICE_CU_LIMIT_",
               "VGPU_DEVICE_CU_SHARE_", "VGPU_DEVICE_CU_RANGE_", "VGPU_HOST_MEMORY_LIMIT", "VGPU_OVERSUBSCRIBE",
@@ -131,16 +123,70 @@ LIMIT_KEYS = ("VGPU_DEVICE_MAP", "VGPU_DEVICE_MEMORY_LIMIT_", "VGPU_DEVICE_HBM_L
               "VGPU_GPU_CONCURRENCY")
 
 
-def _gc_dir(d, suffix, max_age_s):
-    import time
-    now = time.time()
+def write_manifest(vgpu_dir, name, resource, ids):
+    """Records which devices (kubelet IDs of ``resource``) container ``name``'s files serve."""
+    d = os.path.join(vgpu_dir, MANIFEST_HOST_DIR)
     try:
-        for fn in os.listdir(d):
-            fp = os.path.join(d, fn)
-            if fn.endswith(suffix) and now - os.path.getmtime(fp) > max_age_s:
-                os.unlink(fp)
+        os.makedirs(d, exist_ok=True)
+        tmp = os.path.join(d, name + ".devices.tmp")
+        with open(tmp, "w") as f:
+            f.write(f"resource={resource}\n" + "".join(f"{i}\n" for i in sorted(ids)))
+        os.replace(tmp, os.path.join(d, name + ".devices"))
     except OSError:
-        pass
+        return None
+    return os.path.join(d, name + ".devices")
+
+
+def _read_manifest(path):
+    try:
+        with open(path) as f:
+            lines = [x.strip() for x in f if x.strip()]
+    except OSError:
+        return None, None
+    res = lines[0][len("resource="):] if lines and lines[0].startswith("resource=") else ""
+    return res, frozenset(x for x in lines if not x.startswith("resource="))
+
+
+def container_files(vgpu_dir, name):
+    """Host files of container ``name`` (what Allocate created for it)."""
+    return [os.path.join(vgpu_dir, LIMITS_HOST_DIR, "containers", name + ".env"),
+            os.path.join(vgpu_dir, REGIONS_HOST_DIR, name + ".cache"),
+            os.path.join(vgpu_dir, ALLOWLIST_HOST_DIR, "containers", name + ".list"),
+            os.path.join(vgpu_dir, BOARD_HOST_DIR, name + ".slot")]
+
+
+def gc_container_files(vgpu_dir, held, grace_s=CONTAINER_GC_GRACE_S, now=None):
+    """Removes the host files of containers whose pods are gone. ``held``: {resource: set of
+    frozensets of device IDs} that live containers hold (kubelet PodResources), or None when
+    the service could not be asked - then nothing is removed. A manifest younger than
+    ``grace_s`` is kept (its container may not be admitted yet). Returns the removed names."""
+    import time
+    if held is None:
+        return []
+    now = time.time() if now is None else now
+    d = os.path.join(vgpu_dir, MANIFEST_HOST_DIR)
+    removed = []
+    try:
+        names = [fn[:-len(".devices")] for fn in os.listdir(d) if fn.endswith(".devices")]
+    except OSError:
+        return removed
+    for name in names:
+        path = os.path.join(d, name + ".devices")
+        try:
+            if now - os.path.getmtime(path) < grace_s:
+                continue
+        except OSError:
+            continue
+        res, ids = _read_manifest(path)
+        if res is None or not ids or ids in held.get(res, ()):
+            continue
+        for fp in container_files(vgpu_dir, name) + [path]:
+            try:
+                os.unlink(fp)
+            except OSError:
+                pass
+        removed.append(name)
+    return removed
 
 
 def write_limits(vgpu_dir, name, values):
@@ -157,7 +203,6 @@ def write_limits(vgpu_dir, name, values):
         os.replace(tmp, path)
     except OSError:
         return None
-    _gc_dir(d, ".env", LIMITS_MAX_AGE_S)
     return path
 
 
@@ -181,8 +226,8 @@ def create_region_file(host_dir, name):
 
 def write_allowlist(vgpu_dir, name, uuids):
     """Writes <vgpu_dir>/allowlist/containers/<name>.list with ``uuids``; returns its path,
-    or None if the host directory is not writable. Lists older than a week are removed
-    (containers that old have long since started; the shim reads the list once)."""
+    or None if the host directory is not writable (removed with the container's other files,
+    gc_container_files)."""
     d = os.path.join(vgpu_dir, ALLOWLIST_HOST_DIR, "containers")
     try:
         os.makedirs(d, exist_ok=True)
@@ -191,15 +236,6 @@ def write_allowlist(vgpu_dir, name, uuids):
             f.write("".join(u + "\n" for u in uuids))
     except OSError:
         return None
-    try:
-        import time
-        now = time.time()
-        for fn in os.listdir(d):
-            fp = os.path.join(d, fn)
-            if fn.endswith(".list") and now - os.path.getmtime(fp) > ALLOWLIST_MAX_AGE_S:
-                os.unlink(fp)
-    except OSError:
-        pass
     return path
 
 
@@ -303,7 +339,7 @@ def visible_envs(cfg, ids):
 
 
 def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, using_ids=None, pod_tag=None,
-                             pod_uid=None, kubelet_ids=None, latency=False):
+                             pod_uid=None, kubelet_ids=None, latency=False, resource=None):
     """ContainerAllocateResponse for one container holding vGPUs ``vdevs``. ``kubelet_ids``:
     the device IDs of the kubelet's request (monitor mode records them in the container's
     host directory, where the PodResources attribution finds them). ``latency``: the vGPUs
@@ -393,7 +429,6 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         regions = os.path.join(cfg.vgpu_dir, REGIONS_HOST_DIR)
         region, region_inode = create_region_file(regions, cache_name)
         if region:
-            _gc_dir(regions, ".cache", REGION_MAX_AGE_S)
             resp.mounts.add(container_path=f"{CONTAINER_REGION_DIR}/{cache_name}", host_path=region,
                             read_only=False)
             resp.envs["VGPU_SHARED_CACHE"] = f"{CONTAINER_REGION_DIR}/{cache_name}"
@@ -407,6 +442,8 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
     # on any other GPU. Falls back to the node-wide list when the host dir is read-only.
     resp.envs["VGPU_ALLOWLIST"] = CONTAINER_ALLOWLIST_DIR + "/allowlist"
     vdir = cfg.vgpu_dir
+    if kubelet_ids and resource:
+        write_manifest(vdir, cache_name.rsplit(".", 1)[0], resource, kubelet_ids)
     own_list = write_allowlist(vdir, cache_name.rsplit(".", 1)[0], uuids)
 
     resp.mounts.add(container_path=CONTAINER_SHIM, host_path=os.path.join(vdir, "libvgpu_hip.so"), read_only=True)
@@ -439,6 +476,8 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
     limits = {k: v for k, v in envs.items() if k.startswith(LIMIT_KEYS)}
     if region_inode:
         limits["VGPU_REGION_INODE"] = str(region_inode)
+    # The memory backstop (KFD-measured VRAM over the quota) is the plugin's to switch.
+    limits["VGPU_ACTIVE_OOM_KILLER"] = "1" if getattr(cfg, "active_oom_killer", True) else "0"
     limits["VGPU_TASK_PRIORITY_MIN"] = "0" if latency or getattr(cfg, "allow_latency_class", False) else "1"
     limits_file = write_limits(vdir, cache_name.rsplit(".", 1)[0], limits)
     if limits_file:

@@ -25,7 +25,7 @@ import grpc
 from ..parallel.topology import allocate_vdevices
 from . import api
 from .contract import (SHARED_HOST_DIR, build_container_response, build_partition_response, duplicate_gpus,
-                       gc_shared_dirs)
+                       gc_container_files, gc_shared_dirs)
 from .vdevice import device_to_vdevices, vdevices_by_ids
 
 log = logging.getLogger("amdvgpu.plugin")
@@ -163,19 +163,29 @@ class DevicePluginServer:
         stops answering (deleted, server died), serve again and re-register, at most
         RESTART_BUDGET times per hour; past that the plugin is marked fatal and the
         supervisor exits (the DaemonSet restarts the pod, like log.Fatal)."""
+        unregistered = False  # served again, but the kubelet has not heard of it yet
         while not self._stopped.wait(self.watchdog_period_s):
             if self._serving():
-                continue
-            log.error("device plugin socket %s is not serving; restarting the gRPC server", self.socket)
+                if not unregistered:
+                    continue
+            else:
+                log.error("device plugin socket %s is not serving; restarting the gRPC server", self.socket)
+                try:
+                    self.restart_server()
+                except RuntimeError as e:
+                    self.fatal = str(e)
+                    log.error("%s", e)
+                    return
+                except Exception as e:
+                    log.warning("gRPC server restart failed: %r", e)
+                    continue
             try:
-                self.restart_server()
                 self.register()
-            except RuntimeError as e:
-                self.fatal = str(e)
-                log.error("%s", e)
-                return
-            except Exception as e:  # kubelet away: the supervisor's inotify loop handles it
-                log.warning("re-register after restart failed: %s", e)
+                unregistered = False
+            except Exception as e:  # kubelet slow or away: retried next tick (a restarted kubelet
+                # also triggers the supervisor's inotify restart)
+                unregistered = True
+                log.warning("re-register after restart failed: %r; retrying", e)
 
     def options(self):
         return api.DevicePluginOptions(pre_start_required=False,
@@ -269,15 +279,25 @@ class DevicePluginServer:
         with self._alloc_mu:
             return self._allocate(request, context)
 
-    def _held_device_sets(self):
-        """Device-ID sets of this resource that live containers hold (kubelet PodResources),
-        or None when the service cannot be reached."""
+    def _held_by_resource(self):
+        """{resource: set of device-ID frozensets} that live containers hold (kubelet
+        PodResources), or None when the service cannot be reached."""
         from .podresources import list_pod_resources
         pods = list_pod_resources(self.cfg.pod_resources_socket, timeout=1.0)
         if pods is None:
             return None
-        return {frozenset(ids) for p in pods for c in p["containers"]
-                for res, ids in c["devices"].items() if res == self.resource_name and ids}
+        held = {}
+        for p in pods:
+            for c in p["containers"]:
+                for res, ids in c["devices"].items():
+                    if ids:
+                        held.setdefault(res, set()).add(frozenset(ids))
+        return held
+
+    def _held_device_sets(self):
+        """Device-ID sets of this resource that live containers hold, or None (see above)."""
+        held = self._held_by_resource()
+        return None if held is None else held.get(self.resource_name, set())
 
     def _allocate(self, request, context):
         resp = api.AllocateResponse()
@@ -290,6 +310,11 @@ class DevicePluginServer:
                 resp.container_responses.append(build_partition_response(self.cfg, [v.dev for v in vds]))
             return resp
 
+        # Host files of containers whose pods are gone (never by age: a restarted container
+        # re-mounts them from the kubelet's checkpointed response).
+        removed = gc_container_files(self.cfg.vgpu_dir, self._held_by_resource())
+        if removed:
+            log.info("removed the host files of %d departed container(s)", len(removed))
         tags = [None] * len(request.container_requests)
         if self.cfg.monitor_mode and self.pod_matcher is not None:
             try:
@@ -339,7 +364,8 @@ class DevicePluginServer:
                                           using_ids=using, pod_tag=tags[i] if i < len(tags) else None,
                                           pod_uid=self.pod_matcher.owner(tags[i]) if (
                                               self.pod_matcher is not None and i < len(tags) and tags[i]) else None,
-                                          kubelet_ids=requested, latency=self.latency)
+                                          kubelet_ids=requested, latency=self.latency,
+                                          resource=self.resource_name)
             resp.container_responses.append(cr)
             self.allocations.append((requested, using))
             if self.cfg.verbose > 5:

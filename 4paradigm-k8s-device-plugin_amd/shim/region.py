@@ -62,6 +62,7 @@ def lib():
             "vgpu_region_set_memory_limit": (C.c_int, [P, C.c_int, C.c_uint64]),
             "vgpu_region_set_cu_limit": (C.c_int, [P, C.c_int, C.c_int]),
             "vgpu_region_set_cu_share": (C.c_int, [P, C.c_int, C.c_int]),
+            "vgpu_region_set_hbm_limit": (C.c_int, [P, C.c_int, C.c_uint64]),
             "vgpu_region_suspend_all": (C.c_int, [P]),
             "vgpu_region_resume_all": (C.c_int, [P]),
             "vgpu_region_suspended": (C.c_int, [P]),
@@ -207,6 +208,10 @@ class Region:
     def set_cu_share(self, dev, bp):
         """Exact GPU-time share of the limiter's grants, basis points (0 = the CU limit)."""
         return lib().vgpu_region_set_cu_share(self._h, dev, int(bp))
+
+    def set_hbm_limit(self, dev, nbytes):
+        """HBM-resident share of an oversubscribed vGPU (0 = no cap)."""
+        return lib().vgpu_region_set_hbm_limit(self._h, dev, int(nbytes))
 
     def suspend_all(self):
         return lib().vgpu_region_suspend_all(self._h)

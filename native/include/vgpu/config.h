@@ -95,7 +95,7 @@ struct Config {
   int priority = 1;                      // VGPU_TASK_PRIORITY
   CuMode cu_mode = CuMode::kAuto;        // VGPU_CU_MODE
   CuPolicy cu_policy = CuPolicy::kDefault;
-  bool active_oom_killer = false;        // VGPU_ACTIVE_OOM_KILLER
+  bool active_oom_killer = true;         // VGPU_ACTIVE_OOM_KILLER (reference default: on)
   bool memory_override = false;          // VGPU_MEMORY_OVERRIDE
   bool signal_control = false;           // VGPU_SIGNAL_CONTROL: also honour SIGUSR1/2
   bool hook_smi = true;                  // VGPU_HOOK_SMI: virtualise amd-smi/rocm-smi

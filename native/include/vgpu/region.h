@@ -206,6 +206,12 @@ class SharedRegion {
   // Bytes of `dev` resident in HBM (charged minus spilled).
   uint64_t resident(int dev) const;
   uint64_t proc_usage(int slot, int dev) const;
+  // Moves `bytes` of `dev` from spill to HBM-resident data (an SVM spill promoted into HBM)
+  // if the container's resident bytes stay within `cap` (0 = no cap) - atomically with
+  // respect to concurrent allocations of the container's other processes. False: not moved.
+  bool promote_spill(int slot, int dev, uint64_t bytes, uint64_t cap);
+  // The reverse (a promotion that failed after the move): data back to spill.
+  void demote_to_spill(int slot, int dev, uint64_t bytes);
 
   // Pinned host memory (page-locked RAM is a node-wide resource the host-spill pool
   // shares): the same CAS admission with reclaim-and-retry as device memory.
@@ -221,7 +227,11 @@ class SharedRegion {
   // stored in the region.
   void set_ceiling(int dev, uint64_t mem_bytes);
   void set_host_ceiling(uint64_t bytes);
+  // The HBM-resident share of an oversubscribed vGPU (VGPU_DEVICE_HBM_LIMIT_<i>): a tenant
+  // writing 0 (no cap) into its region must not take the other tenants' HBM.
+  void set_hbm_ceiling(int dev, uint64_t bytes);
   uint64_t ceiling(int dev) const { return dev >= 0 && dev < kMaxDevices ? ceil_mem_[dev] : 0; }
+  uint64_t hbm_ceiling(int dev) const { return dev >= 0 && dev < kMaxDevices ? ceil_hbm_[dev] : 0; }
   // Re-initialises the mapped region in place when its header no longer holds a valid
   // layout (a tenant overwrote it); true if it did. Serialised with attach's file lock.
   bool reinit_if_invalid(const Config* cfg);
@@ -254,6 +264,7 @@ class SharedRegion {
   int fd_ = -1;
   char path_[512] = {0};
   uint64_t ceil_mem_[kMaxDevices] = {};
+  uint64_t ceil_hbm_[kMaxDevices] = {};
   uint64_t ceil_host_ = 0;
 };
 

@@ -77,6 +77,8 @@ int vgpu_region_set_cu_limit(vgpu_region* r, int dev, int pct);
 /* Sets the exact GPU-time share (basis points, 0 = the whole-percent limit) as it stands in
    the region: what a container's limiter grants from (a plugin ceiling clamps it). */
 int vgpu_region_set_cu_share(vgpu_region* r, int dev, int bp);
+/* Sets the HBM-resident share of an oversubscribed vGPU (0 = no cap; a plugin ceiling clamps it). */
+int vgpu_region_set_hbm_limit(vgpu_region* r, int dev, uint64_t bytes);
 int vgpu_region_suspend_all(vgpu_region* r);
 int vgpu_region_resume_all(vgpu_region* r);
 int vgpu_region_suspended(vgpu_region* r);

@@ -289,7 +289,7 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
     if (!strcasecmp(s, "force")) cfg->cu_policy = CuPolicy::kForce;
     else if (!strcasecmp(s, "disable")) cfg->cu_policy = CuPolicy::kDisable;
   }
-  cfg->active_oom_killer = parse_bool(getenv_fn("VGPU_ACTIVE_OOM_KILLER"), false);
+  cfg->active_oom_killer = parse_bool(getenv_fn("VGPU_ACTIVE_OOM_KILLER"), true);  // reference: unset = on
   cfg->memory_override = parse_bool(getenv_fn("VGPU_MEMORY_OVERRIDE"), false);
   cfg->signal_control = parse_bool(getenv_fn("VGPU_SIGNAL_CONTROL"), false);
   cfg->fail_open = parse_bool(getenv_fn("VGPU_FAIL_OPEN"), false);
@@ -407,6 +407,8 @@ void apply_ceiling(Config* cfg, const Config& ceil) {
   if (ceil.gpu_concurrency > 0) cfg->gpu_concurrency = ceil.gpu_concurrency;  // the node's admission
   cfg->cu_mode = ceil.cu_mode;
   cfg->oversubscribe = cfg->oversubscribe && ceil.oversubscribe;
+  // The memory backstop is the plugin's (on unless its limits file turns it off).
+  cfg->active_oom_killer = ceil.active_oom_killer;
   if (ceil.min_priority > cfg->min_priority) cfg->min_priority = ceil.min_priority;
   if (cfg->priority < cfg->min_priority) cfg->priority = cfg->min_priority;
   if (ceil.region_inode) cfg->region_inode = ceil.region_inode;

@@ -451,11 +451,51 @@ void SharedRegion::uncharge(int slot, int dev, uint64_t bytes, MemKind kind) {
 
 uint64_t SharedRegion::usage(int dev) const { return r_->dev[dev].used.load(std::memory_order_relaxed); }
 uint64_t SharedRegion::limit(int dev) const { return lower_limit(r_->dev[dev].mem_limit, ceil_mem_[dev]); }
-uint64_t SharedRegion::hbm_limit(int dev) const { return r_->dev[dev].hbm_limit; }
+uint64_t SharedRegion::hbm_limit(int dev) const { return lower_limit(r_->dev[dev].hbm_limit, ceil_hbm_[dev]); }
 uint64_t SharedRegion::resident(int dev) const {
-  uint64_t u = r_->dev[dev].used.load(std::memory_order_relaxed);
-  uint64_t s = r_->dev[dev].spilled.load(std::memory_order_relaxed);
+  // Sequentially consistent: pairs with promote_spill (an allocator charges `used`, then reads
+  // `spilled`; a promotion lowers `spilled`, then reads `used` - one of them sees the other).
+  uint64_t u = r_->dev[dev].used.load(std::memory_order_seq_cst);
+  uint64_t s = r_->dev[dev].spilled.load(std::memory_order_seq_cst);
   return u > s ? u - s : 0;
+}
+
+bool SharedRegion::promote_spill(int slot, int dev, uint64_t bytes, uint64_t cap) {
+  DeviceState& d = r_->dev[dev];
+  // Lower `spilled` first, then check the resident bytes it implies: an allocation charging
+  // `used` concurrently either sees this move (and spills itself) or is seen here (and the
+  // move is undone), so the two cannot jointly push the container past its HBM share.
+  uint64_t cur = d.spilled.load(std::memory_order_seq_cst);
+  do {
+    if (cur < bytes) return false;
+  } while (!d.spilled.compare_exchange_weak(cur, cur - bytes, std::memory_order_seq_cst));
+  if (cap) {
+    const uint64_t u = d.used.load(std::memory_order_seq_cst);
+    const uint64_t sp = d.spilled.load(std::memory_order_seq_cst);
+    if ((u > sp ? u - sp : 0) > cap) {
+      d.spilled.fetch_add(bytes, std::memory_order_seq_cst);
+      return false;
+    }
+  }
+  if (slot >= 0) {
+    DeviceUsage& u = r_->procs[slot].used[dev];
+    uint64_t have = u.kind[kMemSpill].load();
+    uint64_t moved = have < bytes ? have : bytes;
+    u.kind[kMemSpill].fetch_sub(moved);
+    u.kind[kMemData].fetch_add(moved);
+  }
+  return true;
+}
+
+void SharedRegion::demote_to_spill(int slot, int dev, uint64_t bytes) {
+  r_->dev[dev].spilled.fetch_add(bytes, std::memory_order_seq_cst);
+  if (slot >= 0) {
+    DeviceUsage& u = r_->procs[slot].used[dev];
+    uint64_t have = u.kind[kMemData].load();
+    uint64_t moved = have < bytes ? have : bytes;
+    u.kind[kMemData].fetch_sub(moved);
+    u.kind[kMemSpill].fetch_add(moved);
+  }
 }
 uint64_t SharedRegion::proc_usage(int slot, int dev) const { return r_->procs[slot].used[dev].total.load(); }
 
@@ -512,6 +552,10 @@ void SharedRegion::set_host_limit(uint64_t bytes) {
 
 void SharedRegion::set_ceiling(int dev, uint64_t mem_bytes) {
   if (dev >= 0 && dev < kMaxDevices) ceil_mem_[dev] = mem_bytes;
+}
+
+void SharedRegion::set_hbm_ceiling(int dev, uint64_t bytes) {
+  if (dev >= 0 && dev < kMaxDevices) ceil_hbm_[dev] = bytes;
 }
 
 void SharedRegion::set_host_ceiling(uint64_t bytes) { ceil_host_ = bytes; }

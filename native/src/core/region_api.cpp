@@ -118,6 +118,13 @@ int vgpu_region_set_cu_share(vgpu_region* r, int dev, int bp) {
   return 0;
 }
 
+int vgpu_region_set_hbm_limit(vgpu_region* r, int dev, uint64_t bytes) {
+  if (dev < 0 || dev >= kMaxDevices) return -EINVAL;
+  r->r.raw()->dev[dev].hbm_limit = bytes;
+  r->r.raw()->hdr.generation.fetch_add(1);
+  return 0;
+}
+
 int vgpu_region_suspend_all(vgpu_region* r) {
   r->r.suspend_all();
   return 0;

@@ -64,6 +64,11 @@ __attribute__((visibility("default"))) uint64_t vgpu_get_current_device_spilled(
   return ok() ? shim().region.raw()->dev[current_device()].spilled.load() : 0;
 }
 
+// Pinned host memory the container holds (VGPU_HOST_MEMORY_LIMIT's budget, host_hooks.cpp).
+__attribute__((visibility("default"))) uint64_t vgpu_get_host_memory_usage() {
+  return ok() ? shim().region.host_usage() : 0;
+}
+
 __attribute__((visibility("default"))) int vgpu_set_current_device_cu_limit(int pct) {
   if (!ok() || pct <= 0 || pct >= 100) return -1;
   const int dev = current_device();

@@ -191,7 +191,9 @@ hipError_t hipMallocManaged(void** dev_ptr, size_t size, unsigned int flags) {
   // The first HIP call of a process initialises the runtime (and the shim, from the
   // hsa_init hook) inside the real call, so `active` is only meaningful afterwards:
   // charge after the allocation and release it again when over the quota.
+  t_managed_alloc = true;  // the runtime's SVM calls for it are part of this allocation (svm_hooks.cpp)
   hipError_t e = real_hipMallocManaged(dev_ptr, size, flags);
+  t_managed_alloc = false;
   if (!s.active || size == 0 || e != hipSuccess || !dev_ptr || !*dev_ptr) return e;
   uintptr_t key = reinterpret_cast<uintptr_t>(*dev_ptr);
   {
@@ -277,7 +279,6 @@ hipError_t hipFree(void* ptr) {
   ShimState& s = shim();
   if (__builtin_expect(s.active && ptr != nullptr, 1)) {
     AllocRec rec{0, -1, 0};
-    bool pinned = false;
     {
       std::lock_guard<std::mutex> g(s.alloc_mu);
       if (!s.managed.empty()) {
@@ -287,16 +288,10 @@ hipError_t hipFree(void* ptr) {
           s.managed.erase(it);
         }
       }
-      pinned = !s.host.empty() && s.host.count(reinterpret_cast<uintptr_t>(ptr));
     }
     if (rec.dev >= 0 && s.slot >= 0 && !s.exiting.load()) s.region.uncharge(s.slot, rec.dev, rec.size, kMemData);
-    if (pinned) {
-      // hipFree also releases pinned host memory (hipHostMalloc): the host budget follows.
-      hipError_t e = real_hipFree(ptr);
-      if (e == hipSuccess) release_host(ptr);
-      return e;
-    }
   }
+  // Pinned host memory freed through hipFree is released in the ROCr free hook (hsa_hooks.cpp).
   return real_hipFree(ptr);
 }
 

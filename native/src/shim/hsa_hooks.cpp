@@ -127,7 +127,7 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   }
   int dev = pool_ordinal(pool);
   VLOG_DEBUG("pool_allocate pool=%lx size=%zu flags=%u dev=%d", (unsigned long)pool.handle, size, flags, dev);
-  if (dev < 0) return real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
+  if (dev < 0) return host_pool_allocate(pool, size, flags, ptr);  // pinned host memory (host_hooks.cpp)
   ShimState& s = shim();
   gate_suspend();
   if (__builtin_expect(!s.agents[dev].authorised, 0)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
@@ -165,21 +165,41 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   return st;
 }
 
+// The one release path of both free entry points (ROCr accepts either for a pool or region
+// allocation): an SVM spill is unmapped by the shim (ROCr never saw it); otherwise the
+// record is taken before the runtime frees the memory - once freed, another thread may get
+// the same address and record it - and the charges are dropped when the free succeeded
+// (put back when it did not).
+static hsa_status_t release_and_free(void* ptr, hsa_status_t (*real_free)(void*)) {
+  ShimState& s = shim();
+  if (!ptr || s.phase.load(std::memory_order_relaxed) != 2) return real_free(ptr);
+  if (spill_release(ptr)) return HSA_STATUS_SUCCESS;
+  const uintptr_t key = reinterpret_cast<uintptr_t>(ptr);
+  AllocRec rec;
+  HostRec host{0, 0};
+  const bool dev_mem = take_alloc(key, &rec);
+  const bool pinned = !dev_mem && take_host(ptr, &host);  // pinned host memory (host_hooks.cpp)
+  hsa_status_t st = real_free(ptr);
+  if (st != HSA_STATUS_SUCCESS) {
+    if (dev_mem) record_alloc(key, rec.size, rec.dev, rec.kind);
+    if (pinned) put_host(ptr, host);
+    return st;
+  }
+  if (s.slot < 0 || s.exiting.load()) return st;
+  if (dev_mem) {
+    s.region.uncharge(s.slot, rec.dev, rec.size, (MemKind)rec.kind);
+    if (rec.kind == kMemSpill) s.region.uncharge_host(s.slot, rec.size);  // a pinned spill
+    else notify_device_memory_freed();
+  }
+  if (pinned) s.region.uncharge_host(s.slot, host.each * host.n);
+  return st;
+}
+
 hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
   VGPU_REAL_HSA(hsa_amd_memory_pool_free);
   VGPU_STAT(kStatFree);
   if (!real_hsa_amd_memory_pool_free) return HSA_STATUS_ERROR;
-  ShimState& s = shim();
-  if (ptr && s.phase.load(std::memory_order_relaxed) == 2) {
-    if (spill_release(ptr)) return HSA_STATUS_SUCCESS;  // an SVM spill: ROCr never saw it
-    AllocRec rec;
-    if (take_alloc(reinterpret_cast<uintptr_t>(ptr), &rec) && s.slot >= 0 && !s.exiting.load()) {
-      s.region.uncharge(s.slot, rec.dev, rec.size, (MemKind)rec.kind);
-      if (rec.kind == kMemSpill) s.region.uncharge_host(s.slot, rec.size);
-      else notify_device_memory_freed();
-    }
-  }
-  return real_hsa_amd_memory_pool_free(ptr);
+  return release_and_free(ptr, real_hsa_amd_memory_pool_free);
 }
 
 // The legacy region API reaches the same memory: ROCr's hsa_region_t and
@@ -196,8 +216,25 @@ hsa_status_t hsa_memory_allocate(hsa_region_t region, size_t size, void** ptr) {
     return real_hsa_memory_allocate(region, size, ptr);
   }
   int dev = pool_ordinal(pool);
-  if (dev < 0) return real_hsa_memory_allocate(region, size, ptr);
   ShimState& s = shim();
+  if (dev < 0) {
+    // A CPU region: pinned host memory, charged to the host budget like a CPU-pool allocation.
+    if (!is_cpu_pool(pool) || s.slot < 0) return real_hsa_memory_allocate(region, size, ptr);
+    gate_suspend();
+    if (s.region.charge_host(s.slot, size) != Charge::kOk) {
+      VLOG_WARN("host memory OOM (region): request %zu bytes, pinned %lu of limit %lu", size,
+                (unsigned long)s.region.host_usage(), (unsigned long)s.region.host_limit());
+      return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+    }
+    hsa_status_t st = real_hsa_memory_allocate(region, size, ptr);
+    if (st == HSA_STATUS_SUCCESS && ptr && *ptr) {
+      std::lock_guard<std::mutex> g(s.alloc_mu);
+      s.host[reinterpret_cast<uintptr_t>(*ptr)] = HostRec{size, 1};
+    } else {
+      s.region.uncharge_host(s.slot, size);
+    }
+    return st;
+  }
   gate_suspend();
   if (__builtin_expect(!s.agents[dev].authorised, 0)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   if (s.region.charge(s.slot, dev, size, kMemData) != Charge::kOk) {
@@ -214,14 +251,7 @@ hsa_status_t hsa_memory_allocate(hsa_region_t region, size_t size, void** ptr) {
 hsa_status_t hsa_memory_free(void* ptr) {
   VGPU_REAL_HSA(hsa_memory_free);
   if (!real_hsa_memory_free) return HSA_STATUS_ERROR;
-  ShimState& s = shim();
-  hsa_status_t st = real_hsa_memory_free(ptr);
-  if (st == HSA_STATUS_SUCCESS && ptr && s.phase.load(std::memory_order_relaxed) == 2) {
-    AllocRec rec;
-    if (take_alloc(reinterpret_cast<uintptr_t>(ptr), &rec) && s.slot >= 0 && !s.exiting.load())
-      s.region.uncharge(s.slot, rec.dev, rec.size, (MemKind)rec.kind);
-  }
-  return st;
+  return release_and_free(ptr, real_hsa_memory_free);
 }
 
 // Peer access to a buffer (ROCclr grants it to the other GPUs of the process): an SVM spill
@@ -516,6 +546,8 @@ const char* const kHsaHooked[] = {
     "hsa_amd_vmem_handle_create", "hsa_amd_vmem_handle_release", "hsa_agent_get_info", "hsa_queue_create",
     "hsa_queue_destroy", "hsa_amd_queue_cu_set_mask", "hsa_amd_ipc_memory_attach", "hsa_amd_ipc_memory_detach",
     "hsa_memory_allocate", "hsa_memory_free", "hsa_amd_agents_allow_access",
+    "hsa_amd_svm_attributes_set", "hsa_amd_svm_prefetch_async",  // svm_hooks.cpp
+    "hsa_amd_memory_lock", "hsa_amd_memory_lock_to_pool", "hsa_amd_memory_unlock",  // host_hooks.cpp
 };
 constexpr int kNumHsaHooked = sizeof(kHsaHooked) / sizeof(kHsaHooked[0]);
 

@@ -102,6 +102,20 @@ hsa_status_t region_cb(hsa_region_t region, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
+// Every global pool of a CPU agent: allocations from them pin host memory (host_hooks.cpp).
+hsa_status_t cpu_pool_record_cb(hsa_amd_memory_pool_t pool, void* data) {
+  ShimState* s = static_cast<ShimState*>(data);
+  VGPU_REAL_HSA(hsa_amd_memory_pool_get_info);
+  hsa_amd_segment_t seg;
+  if (real_hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  for (int i = 0; i < s->n_cpu_pools; i++)
+    if (s->cpu_pools[i].handle == pool.handle) return HSA_STATUS_SUCCESS;
+  if (s->n_cpu_pools < kMaxAgentPools) s->cpu_pools[s->n_cpu_pools++] = pool;
+  return HSA_STATUS_SUCCESS;
+}
+
 hsa_status_t cpu_pool_cb(hsa_amd_memory_pool_t pool, void* data) {
   AgentInfo* a = static_cast<AgentInfo*>(data);
   VGPU_REAL_HSA(hsa_amd_memory_pool_get_info);
@@ -192,6 +206,7 @@ void atfork_child() {
   s.ipc.clear();
   s.host.clear();
   svm_forget();
+  svm_tenant_forget();
   for (auto& b : s.ipc_bytes) b.store(0);
   s.queues.clear();
   s.hostpid = 0;
@@ -282,6 +297,7 @@ void install_ceilings(const char* const* uuid_ptrs) {
     AgentInfo& a = s.agents[i];
     // A device the map does not give this container gets nothing (it is unauthorised too).
     s.region.set_ceiling(i, per[i].unmapped ? 1 : per[i].mem_limit);
+    s.region.set_hbm_ceiling(i, per[i].hbm_limit);
     const int pct = per[i].cu_limit_pct;
     if (pct > 0 && pct < 100) {
       a.ceil_pct = pct;
@@ -384,6 +400,11 @@ void shim_init_after_hsa() {
   s.n_agents = 0;
   VGPU_REAL_HSA(hsa_iterate_agents);
   if (real_hsa_iterate_agents) real_hsa_iterate_agents(agent_cb, &sc);
+  s.n_cpu_pools = 0;
+  for (int c = 0; c < sc.n_cpu; c++) {
+    VGPU_REAL_HSA(hsa_amd_agent_iterate_memory_pools);
+    real_hsa_amd_agent_iterate_memory_pools(sc.cpus[c], cpu_pool_record_cb, &s);
+  }
   for (int i = 0; i < s.n_agents; i++) {
     AgentInfo& a = s.agents[i];
     if (!a.cpu_agent.handle && sc.n_cpu) a.cpu_agent = sc.cpus[0];
@@ -557,6 +578,13 @@ bool clamp_region_to_ceiling() {
       d.mem_limit = cm;
       clamped = true;
     }
+    const uint64_t ch = s.region.hbm_ceiling(i);
+    if (ch && (!d.hbm_limit || d.hbm_limit > ch)) {
+      VLOG_WARN("device %d: region HBM share %lu above the plugin's %lu; clamped", i, (unsigned long)d.hbm_limit,
+                (unsigned long)ch);
+      d.hbm_limit = ch;
+      clamped = true;
+    }
     if (a.ceil_pct > 0) {
       if (d.cu_limit_pct <= 0 || d.cu_limit_pct >= 100 || d.cu_limit_pct > a.ceil_pct) {
         VLOG_WARN("device %d: region CU limit %d%% above the plugin's %d%%; clamped", i, d.cu_limit_pct, a.ceil_pct);
@@ -634,13 +662,14 @@ void check_region_epoch() {
     }
     for (const auto& kv : s.vmem) s.region.force_charge(slot, kv.second.dev, kv.second.size, kMemData);
     for (const auto& kv : s.managed) s.region.force_charge(slot, kv.second.dev, kv.second.size, kMemData);
-    for (const auto& kv : s.host) host += kv.second;
+    host += host_recorded_bytes();
     svm_recharge(slot, &host);
     if (host) {
       r->hdr.host_used.fetch_add(host);
       r->procs[slot].host_used.fetch_add(host);
     }
   }
+  svm_tenant_recharge(slot);
   resync_context_charge();
   r->hdr.generation.fetch_add(1, std::memory_order_acq_rel);  // every process re-applies its masks
 }
@@ -773,8 +802,9 @@ void resync_context_charge() {
     int64_t vram = kfd_vram_usage(s.hostpid, a.gpu_id);
     if (vram < 0) continue;
     DeviceUsage& u = r->procs[s.slot].used[i];
-    // Promoted SVM spills are charged as data; KFD may not count their pages in vram_<id>.
-    int64_t tracked = (int64_t)u.kind[kMemData].load() - svm_hbm_outside_kfd(i);
+    // Promoted SVM spills and the tenant's own SVM ranges are charged as data; KFD may not
+    // count their pages in vram_<id>.
+    int64_t tracked = (int64_t)u.kind[kMemData].load() - svm_hbm_outside_kfd(i) - svm_tenant_outside_kfd(i);
     // IPC imports are not in the importer's vram_<gpu_id> (measured on MI355X: a 1 GiB
     // import left the consumer's counter at its ~0.5 GiB runtime footprint,
     // profiles/r2e), so nothing is subtracted for them: the exporter alone holds the charge.

@@ -13,6 +13,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <map>
 #include <mutex>
 #include <unordered_map>
 
@@ -68,6 +69,23 @@ struct SvmRec {
   uint64_t retry_ns;  // a failed promotion is not retried before this time
 };
 
+// Pinned host memory of this process (host_hooks.cpp): a CPU-pool allocation (n = 1) or a
+// locked user range (n = times locked). Charged to the host budget `each` bytes per count.
+struct HostRec {
+  uint64_t each;
+  uint32_t n;
+};
+
+// A piece of a tenant's own SVM range (svm_hooks.cpp, hsa_amd_svm_attributes_set /
+// hsa_amd_svm_prefetch_async): where the tenant asked it to live, and the device whose
+// quota holds it (the prefetch location, else the preferred one; -1 = host memory).
+struct TenantSvmSeg {
+  uint64_t end;
+  int pref;     // preferred location: device ordinal, -1 = host / none
+  int loc;      // last prefetch target: device ordinal, -1 = host / none
+  int charged;  // device charged for the bytes, -1 = none
+};
+
 struct ShimState {
   std::atomic<int> phase{0};         // 0 = not initialised, 1 = initialising, 2 = ready, 3 = inert
   bool active = false;               // accounting + gates enabled
@@ -83,12 +101,18 @@ struct ShimState {
   std::unordered_map<uint64_t, AllocRec> vmem;      // vmem handle → record
   std::unordered_map<uintptr_t, AllocRec> managed;  // hipMallocManaged pointers charged at HIP level
   std::unordered_map<uintptr_t, AllocRec> ipc;      // IPC-attached pointers (owned by another process)
-  std::unordered_map<uintptr_t, uint64_t> host;     // pinned host memory (host_hooks.cpp) → bytes
+  std::unordered_map<uintptr_t, HostRec> host;      // pinned host memory (host_hooks.cpp)
+  hsa_amd_memory_pool_t cpu_pools[kMaxAgentPools]{};  // global pools of the CPU agents (pinned host memory)
+  int n_cpu_pools = 0;
   std::unordered_map<uintptr_t, int> queues;        // hsa_queue_t* → ordinal
   std::unordered_map<uintptr_t, SvmRec> svm;        // SVM-backed spills (spill.cpp) → record
   std::mutex svm_mu;                                // serialises promotions with the frees of SVM spills
   int64_t svm_hbm[kMaxDevices] = {};                // promoted SVM bytes per device (under ctx_mu)
   int svm_kfd_vram = -1;                            // promoted SVM pages appear in KFD's vram_<gpu_id>: 1 / 0 / -1 unknown
+  std::map<uintptr_t, TenantSvmSeg> tsvm;           // the tenant's own SVM ranges (svm_hooks.cpp), by start
+  std::mutex tsvm_mu;
+  int64_t tsvm_loc[kMaxDevices] = {};               // charged bytes prefetched onto a device (under ctx_mu)
+  int64_t tsvm_pref[kMaxDevices] = {};              // charged bytes only preferred there (never in VRAM)
   std::atomic<bool> exiting{false};
   std::atomic<bool> watcher_started{false};
   std::atomic<uint64_t> seen_generation{0};         // region generation the queues reflect
@@ -176,8 +200,8 @@ inline int effective_priority(const Region* r) {
   return p < floor ? floor : p;
 }
 
-// Keeps the region within the plugin's ceilings (limits, CU share and slice, host budget,
-// priority floor): the tenant maps the region read-write, so whatever it wrote there is
+// Keeps the region within the plugin's ceilings (limits, HBM share, CU share and slice, host
+// budget, priority floor): the tenant maps the region read-write, so whatever it wrote there is
 // clamped back. Returns true if something was clamped. Called on attach and on every
 // limit change (generation bump).
 bool clamp_region_to_ceiling();
@@ -221,9 +245,31 @@ void svm_recharge(int slot, uint64_t* host);
 // Forgets the parent's SVM spills in a forked child (the ranges are not inherited).
 void svm_forget();
 
-// Drops the pinned host-memory charge of `p` (host_hooks.cpp) if the shim recorded it:
-// called after the runtime freed or unregistered it, through whichever entry point.
-void release_host(void* p);
+// Pinned host memory (host_hooks.cpp), accounted where every path pins it: ROCr's CPU-pool
+// allocations and memory locks. host_pool_allocate serves an allocation from a pool that is
+// not a GPU's (charged to VGPU_HOST_MEMORY_LIMIT when it is a CPU pool).
+// recorded). take_host removes the record of `p` (false: none) without uncharging it, for a
+// caller that frees the memory next; put_host restores it when the free failed.
+bool is_cpu_pool(hsa_amd_memory_pool_t pool);
+hsa_status_t host_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr);
+bool take_host(void* p, HostRec* out);
+void put_host(void* p, const HostRec& rec);
+// Sum of the recorded pinned bytes (re-charged after the region was re-initialised).
+uint64_t host_recorded_bytes();
+
+// The tenant's own SVM ranges (svm_hooks.cpp). A range placed on a GPU (preferred location
+// or prefetch target) is admitted against that device's quota; moving it back to host
+// memory or unmapping it releases the charge. svm_tenant_reconcile drops ranges the
+// process unmapped (maintenance thread); svm_tenant_recharge re-charges them after the
+// region was re-initialised; svm_tenant_forget clears them in a forked child.
+void svm_tenant_reconcile();
+void svm_tenant_recharge(int slot);
+void svm_tenant_forget();
+// Bytes of `dev` the tenant's SVM ranges hold that KFD's vram counter does not show.
+int64_t svm_tenant_outside_kfd(int dev);
+// Set while HIP allocates managed memory (hipMallocManaged charges it as a whole): the SVM
+// calls the runtime makes for it are not charged again.
+extern thread_local bool t_managed_alloc;
 
 // The agent ordinal of HIP device `hipdev` (hipGetDevice / hipSetDevice numbering),
 // matched by PCI address: HIP_VISIBLE_DEVICES inside the container may reorder or hide

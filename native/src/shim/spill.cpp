@@ -32,6 +32,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <mutex>
 #include <vector>
@@ -47,7 +48,15 @@ namespace vgpu {
 namespace {
 
 constexpr uint64_t kPromoteBytesPerTick = 8ull << 30;        // migrated per period at most
-constexpr uint64_t kMigrateTimeoutNs = 60'000'000'000ull;    // one range's migration
+// One range's migration (VGPU_SPILL_MIGRATE_TIMEOUT_MS, default 60 s).
+uint64_t migrate_timeout_ns() {
+  static const uint64_t ns = [] {
+    const char* v = getenv("VGPU_SPILL_MIGRATE_TIMEOUT_MS");
+    const long ms = v && *v ? strtol(v, nullptr, 10) : 0;
+    return ms > 0 ? (uint64_t)ms * 1'000'000ull : 60'000'000'000ull;
+  }();
+  return ns;
+}
 constexpr uint64_t kRetryBackoffNs = 10'000'000'000ull;      // after a failed promotion
 
 std::atomic<uint64_t> g_seq{0};
@@ -112,31 +121,47 @@ hsa_status_t svm_map(int dev, size_t size, void** ptr, size_t* mapped) {
   return HSA_STATUS_SUCCESS;
 }
 
-// Migrates [p, p+len) to `agent` (a GPU or the CPU); true once the driver completed it.
-bool migrate(void* p, size_t len, hsa_agent_t agent) {
+// Outcome of one range's migration.
+enum class Migration { kDone, kFailed, kPending };
+
+// Migrates [p, p+len) to `agent` (a GPU or the CPU) and waits for the driver (bounded). A
+// migration still in flight at the bound keeps its completion signal: ROCr's async thread
+// signals it later, so it is left allocated (a few bytes) rather than destroyed under it.
+Migration migrate(void* p, size_t len, hsa_agent_t agent) {
   VGPU_REAL_HSA(hsa_amd_svm_attributes_set);
   VGPU_REAL_HSA(hsa_amd_svm_prefetch_async);
   VGPU_REAL_HSA(hsa_signal_create);
   VGPU_REAL_HSA(hsa_signal_destroy);
   VGPU_REAL_HSA(hsa_signal_wait_scacquire);
   hsa_amd_svm_attribute_pair_t pref[1] = {{HSA_AMD_SVM_ATTRIB_PREFERRED_LOCATION, agent.handle}};
-  if (real_hsa_amd_svm_attributes_set(p, len, pref, 1) != HSA_STATUS_SUCCESS) return false;
+  if (real_hsa_amd_svm_attributes_set(p, len, pref, 1) != HSA_STATUS_SUCCESS) return Migration::kFailed;
   hsa_signal_t sig;
-  if (real_hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) return false;
-  bool ok = false;
-  if (real_hsa_amd_svm_prefetch_async(p, len, agent, 0, nullptr, sig) == HSA_STATUS_SUCCESS)
-    ok = real_hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, kMigrateTimeoutNs, HSA_WAIT_STATE_BLOCKED) == 0;
+  if (real_hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) return Migration::kFailed;
+  if (real_hsa_amd_svm_prefetch_async(p, len, agent, 0, nullptr, sig) != HSA_STATUS_SUCCESS) {
+    real_hsa_signal_destroy(sig);
+    return Migration::kFailed;
+  }
+  const hsa_signal_value_t v =
+      real_hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, migrate_timeout_ns(), HSA_WAIT_STATE_BLOCKED);
+  if (v >= 1) return Migration::kPending;  // still in flight: the signal stays valid for ROCr
   real_hsa_signal_destroy(sig);
-  return ok;
+  return v == 0 ? Migration::kDone : Migration::kFailed;
 }
 
 // Promotes the SVM spills of `dev` that fit, oldest first; returns the bytes moved.
+//
+// The charge moves from spill to HBM data before the migration, atomically against the
+// container's concurrent allocations (SharedRegion::promote_spill: resident bytes stay within
+// the share less the reserve), and back if the driver refuses. ctx_mu is held only around
+// the bookkeeping, never across the migration (up to a minute), so the maintenance thread's
+// context re-sync and the container's sampler are not held up meanwhile.
 uint64_t promote_device(int dev, uint64_t budget) {
   ShimState& s = shim();
   const Config& cfg = config();
   AgentInfo& a = s.agents[dev];
   const uint64_t share = s.region.hbm_limit(dev);
   const uint64_t reserve = share ? spill_reserve(cfg, share) : 0;
+  const uint64_t cap = share ? (share > reserve ? share - reserve : 1) : 0;
   std::vector<std::pair<uint64_t, uintptr_t>> order;  // (seq, ptr) of the spills in host memory
   const uint64_t now = now_ns();
   {
@@ -159,9 +184,6 @@ uint64_t promote_device(int dev, uint64_t budget) {
       if (it == s.svm.end() || it->second.in_hbm) continue;
       rec = it->second;
     }
-    // Room under the share (the range counts as resident once moved) and in the GPU's HBM.
-    const uint64_t resident = s.region.resident(dev);
-    if (share && resident + rec.size + reserve > share) break;
     uint64_t avail = 0;
     if (real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &avail) !=
         HSA_STATUS_SUCCESS)
@@ -172,17 +194,25 @@ uint64_t promote_device(int dev, uint64_t budget) {
     avail = avail > promoted ? avail - promoted : 0;
     if (avail < rec.mapped + reserve) break;
     void* p = reinterpret_cast<void*>(o.second);
-    // The context charge (KFD VRAM less the tracked allocations) must not see the pages
-    // arrive before the charge moves: both under ctx_mu.
-    std::lock_guard<std::mutex> cg(s.ctx_mu);
-    const int64_t vram0 = s.hostpid && a.gpu_id ? kfd_vram_usage(s.hostpid, a.gpu_id) : -1;
-    s.region.uncharge(s.slot, dev, rec.size, kMemSpill);
-    s.region.force_charge(s.slot, dev, rec.size, kMemData);
+    int64_t vram0 = -1;
+    {
+      std::lock_guard<std::mutex> cg(s.ctx_mu);
+      // Room under the share (the range counts as resident once moved), decided atomically.
+      if (!s.region.promote_spill(s.slot, dev, rec.size, cap)) break;
+      s.svm_hbm[dev] += (int64_t)rec.size;
+      vram0 = s.hostpid && a.gpu_id ? kfd_vram_usage(s.hostpid, a.gpu_id) : -1;
+    }
     const uint64_t t0 = now_ns();
-    if (!migrate(p, rec.mapped, a.agent)) {
-      s.region.uncharge(s.slot, dev, rec.size, kMemData);
-      s.region.force_charge(s.slot, dev, rec.size, kMemSpill);
-      migrate(p, rec.mapped, a.cpu_agent);  // whatever moved goes back; host memory preferred again
+    const Migration m = migrate(p, rec.mapped, a.agent);
+    if (m == Migration::kFailed) {
+      {
+        std::lock_guard<std::mutex> cg(s.ctx_mu);
+        s.region.demote_to_spill(s.slot, dev, rec.size);
+        s.svm_hbm[dev] -= (int64_t)rec.size;
+      }
+      // Whatever moved goes back (the failed migration has completed); host memory preferred again.
+      if (migrate(p, rec.mapped, a.cpu_agent) == Migration::kPending)
+        VLOG_WARN("device %d: moving %p back to host memory is still in progress", dev, p);
       std::lock_guard<std::mutex> g(s.alloc_mu);
       auto it = s.svm.find(o.second);
       if (it != s.svm.end()) it->second.retry_ns = now_ns() + kRetryBackoffNs;
@@ -190,11 +220,19 @@ uint64_t promote_device(int dev, uint64_t budget) {
                 (unsigned long)rec.size, p);
       continue;
     }
-    const int64_t vram1 = vram0 >= 0 ? kfd_vram_usage(s.hostpid, a.gpu_id) : -1;
-    if (s.svm_kfd_vram < 0 && vram0 >= 0 && vram1 >= 0)
-      s.svm_kfd_vram = vram1 - vram0 >= (int64_t)rec.mapped / 2 ? 1 : 0;
-    s.svm_hbm[dev] += (int64_t)rec.size;
-    s.region.uncharge_host(s.slot, rec.size);
+    if (m == Migration::kPending) {
+      // Where the pages end up is the driver's; the range stays charged as HBM data (the
+      // conservative side for the other tenants) and is not moved again.
+      VLOG_ERROR("device %d: promotion of %lu bytes at %p did not finish within %lu ms; kept as HBM-resident", dev,
+                 (unsigned long)rec.size, p, (unsigned long)(migrate_timeout_ns() / 1000000ull));
+    }
+    {
+      std::lock_guard<std::mutex> cg(s.ctx_mu);
+      const int64_t vram1 = vram0 >= 0 && m == Migration::kDone ? kfd_vram_usage(s.hostpid, a.gpu_id) : -1;
+      if (s.svm_kfd_vram < 0 && vram0 >= 0 && vram1 >= 0)
+        s.svm_kfd_vram = vram1 - vram0 >= (int64_t)rec.mapped / 2 ? 1 : 0;
+      s.region.uncharge_host(s.slot, rec.size);
+    }
     {
       std::lock_guard<std::mutex> g(s.alloc_mu);
       auto it = s.svm.find(o.second);

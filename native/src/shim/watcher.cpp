@@ -479,8 +479,17 @@ void crowd_tick(Region* r, Sampler& sm, Crowd& c, uint64_t now) {
 }
 
 // Monitor-based usage (reference set_gpu_device_memory_monitor) and the active OOM killer.
+// The killer is the backstop for memory no hook saw (raw KFD ioctls, a runtime loaded
+// around the shim, runtime-internal growth - scratch, queues - that is charged without
+// admission): it acts when KFD's measured VRAM of the container stays above its quota plus
+// a slack (max(512 MiB, 1/16 of the quota): the context charge may legitimately overshoot
+// a little) for two consecutive periods. On by default as in the reference
+// (ACTIVE_OOM_KILLER unset = on); under a plugin limits file the tenant cannot turn it off.
+constexpr uint64_t kOomSlackMin = 512ull << 20;
 void monitor_tick(Region* r) {
   ShimState& s = shim();
+  static int over_ticks[kMaxDevices];
+  const bool killer = config().active_oom_killer || (r->hdr.flags & kFlagActiveOomKiller);
   for (int d = 0; d < s.n_agents; d++) {
     AgentInfo& a = s.agents[d];
     DeviceState& ds = r->dev[d];
@@ -501,11 +510,19 @@ void monitor_tick(Region* r) {
       }
     }
     ds.monitor_used.store(mon);
-    if ((r->hdr.flags & kFlagActiveOomKiller) && ds.mem_limit && mon > ds.mem_limit && worst_pid > 0) {
-      VLOG_ERROR("device %d: measured usage %lu exceeds limit %lu; killing largest consumer pid %d", d,
-                 (unsigned long)mon, (unsigned long)ds.mem_limit, worst_pid);
-      kill(worst_pid, SIGKILL);
+    const uint64_t limit = s.region.limit(d);  // the region's, within this process's ceiling
+    const uint64_t slack = std::max<uint64_t>(kOomSlackMin, limit / 16);
+    if (!killer || !limit || mon <= limit + slack || worst_pid <= 0) {
+      over_ticks[d] = 0;
+      continue;
     }
+    if (++over_ticks[d] < 2) continue;
+    over_ticks[d] = 0;
+    VLOG_ERROR("device %d: measured usage %lu exceeds limit %lu (+%lu slack); killing largest consumer pid %d", d,
+               (unsigned long)mon, (unsigned long)limit, (unsigned long)slack, worst_pid);
+    for (int i = 0; i < kMaxProcs; i++)
+      if (r->procs[i].pid.load(std::memory_order_relaxed) == worst_pid) r->procs[i].oom_events.fetch_add(1);
+    kill(worst_pid, SIGKILL);
   }
 }
 
@@ -550,6 +567,7 @@ void* watcher_main(void*) {
       }
       if (s.slot >= 0) r->procs[s.slot].launches.store(s.launches.load(std::memory_order_relaxed));
       resync_context_charge();
+      svm_tenant_reconcile();  // the tenant's SVM ranges it unmapped give their charge back
       if (lease) {
         collect_region_pids(r, sm);
         board_tick(r, sm, now);

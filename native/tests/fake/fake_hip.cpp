@@ -82,11 +82,14 @@ void gpu_loop(int d) {
 
 hsa_agent_t g_all[16];
 int g_nall = 0;
+hsa_agent_t g_cpu{0};
+hsa_amd_memory_pool_t g_cpu_pool{0};  // pinned host memory comes from here, as in CLR
 
 hsa_status_t agent_cb(hsa_agent_t a, void*) {
   hsa_device_type_t t;
   hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
   if (t == HSA_DEVICE_TYPE_GPU && g_nall < 16) g_all[g_nall++] = a;
+  if (t == HSA_DEVICE_TYPE_CPU && !g_cpu.handle) g_cpu = a;
   return HSA_STATUS_SUCCESS;
 }
 
@@ -116,6 +119,7 @@ void init() {
   hsa_init();  // the shim's hsa_init hook runs here, as inside CLR
   hsa_iterate_agents(agent_cb, nullptr);
   map_devices();
+  if (g_cpu.handle) hsa_amd_agent_iterate_memory_pools(g_cpu, pool_cb, &g_cpu_pool);
   for (int i = 0; i < g_n; i++) {
     hsa_amd_agent_iterate_memory_pools(g_dev[i].agent, pool_cb, &g_dev[i].pool);
     g_dev[i].th = std::thread(gpu_loop, i);
@@ -188,18 +192,9 @@ hipError_t hipMalloc(void** ptr, size_t size) {
   return s == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorOutOfMemory;
 }
 
-static std::mutex g_host_mu;
-static std::set<void*> g_host;  // hipHostMalloc'd pointers (hipFree releases them too, as CLR does)
-
 hipError_t hipFree(void* ptr) {
   if (!ptr) return hipSuccess;
-  {
-    std::lock_guard<std::mutex> l(g_host_mu);
-    if (g_host.erase(ptr)) {
-      free(ptr);
-      return hipSuccess;
-    }
-  }
+  // Device and pinned host memory alike are pool allocations (CLR frees both here).
   return hsa_amd_memory_pool_free(ptr) == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorInvalidValue;
 }
 
@@ -308,31 +303,68 @@ hipError_t hipGetProcAddress(const char* symbol, void** pfn, int, uint64_t, hipD
   return p ? hipSuccess : hipErrorNotFound;
 }
 
-// Pinned host memory (plain heap memory here).
+// Pinned host memory: a CPU-pool allocation, or a lock of the caller's range (as in CLR).
 hipError_t hipHostMalloc(void** ptr, size_t size, unsigned int) {
   init();
-  *ptr = malloc(size ? size : 1);
-  if (!*ptr) return hipErrorOutOfMemory;
-  std::lock_guard<std::mutex> l(g_host_mu);
-  g_host.insert(*ptr);
-  return hipSuccess;
+  fake_hip_record("hipHostMalloc");
+  if (!ptr) return hipErrorInvalidValue;
+  return hsa_amd_memory_pool_allocate(g_cpu_pool, size ? size : 1, 0, ptr) == HSA_STATUS_SUCCESS ? hipSuccess
+                                                                                                 : hipErrorOutOfMemory;
 }
 
 hipError_t hipHostFree(void* ptr) {
-  {
-    std::lock_guard<std::mutex> l(g_host_mu);
-    g_host.erase(ptr);
-  }
-  free(ptr);
-  return hipSuccess;
+  fake_hip_record("hipHostFree");
+  if (!ptr) return hipSuccess;
+  return hsa_amd_memory_pool_free(ptr) == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorInvalidValue;
 }
 
-hipError_t hipHostRegister(void* ptr, size_t, unsigned int) {
+hipError_t hipHostRegister(void* ptr, size_t size, unsigned int) {
   init();
-  return ptr ? hipSuccess : hipErrorInvalidValue;
+  fake_hip_record("hipHostRegister");
+  if (!ptr || !size) return hipErrorInvalidValue;
+  void* agent_ptr = nullptr;
+  hsa_status_t st = hsa_amd_memory_lock_to_pool(ptr, size, g_nall ? g_all : nullptr, g_nall, g_cpu_pool, 0, &agent_ptr);
+  return st == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorOutOfMemory;
 }
 
-hipError_t hipHostUnregister(void* ptr) { return ptr ? hipSuccess : hipErrorInvalidValue; }
+hipError_t hipHostUnregister(void* ptr) {
+  fake_hip_record("hipHostUnregister");
+  if (!ptr) return hipErrorInvalidValue;
+  return hsa_amd_memory_unlock(ptr) == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorHostMemoryNotRegistered;
+}
+
+// System-allocated memory placed with SVM attributes, as CLR does for hipMemAdvise /
+// hipMemPrefetchAsync on memory it did not allocate (device -1 = the CPU).
+hsa_agent_t placement_agent(int device) {
+  if (device >= 0 && device < g_n) return g_dev[device].agent;
+  return device == hipCpuDeviceId ? g_cpu : hsa_agent_t{0};
+}
+
+hipError_t hipMemPrefetchAsync(const void* ptr, size_t count, int device, hipStream_t) {
+  init();
+  fake_hip_record("hipMemPrefetchAsync");
+  hsa_agent_t a = placement_agent(device);
+  if (!ptr || !count || !a.handle) return hipErrorInvalidValue;
+  hsa_signal_t sig;
+  hsa_signal_create(1, 0, nullptr, &sig);
+  hsa_status_t st = hsa_amd_svm_prefetch_async(const_cast<void*>(ptr), count, a, 0, nullptr, sig);
+  hsa_signal_destroy(sig);
+  return st == HSA_STATUS_SUCCESS ? hipSuccess
+         : st == HSA_STATUS_ERROR_OUT_OF_RESOURCES ? hipErrorOutOfMemory : hipErrorInvalidValue;
+}
+
+hipError_t hipMemAdvise(const void* ptr, size_t count, hipMemoryAdvise advice, int device) {
+  init();
+  fake_hip_record("hipMemAdvise");
+  hsa_agent_t a = placement_agent(device);
+  if (!ptr || !count || !a.handle) return hipErrorInvalidValue;
+  hsa_amd_svm_attribute_pair_t attr{HSA_AMD_SVM_ATTRIB_PREFERRED_LOCATION, a.handle};
+  if (advice == hipMemAdviseSetAccessedBy) attr = {HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE_IN_PLACE, a.handle};
+  else if (advice != hipMemAdviseSetPreferredLocation) return hipSuccess;
+  hsa_status_t st = hsa_amd_svm_attributes_set(const_cast<void*>(ptr), count, &attr, 1);
+  return st == HSA_STATUS_SUCCESS ? hipSuccess
+         : st == HSA_STATUS_ERROR_OUT_OF_RESOURCES ? hipErrorOutOfMemory : hipErrorInvalidValue;
+}
 
 // Test introspection: GPU time executed on `dev` so far, and its kernel count.
 uint64_t fake_hip_busy_us(int dev, uint64_t* kernels) {

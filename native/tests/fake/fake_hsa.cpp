@@ -20,6 +20,8 @@
 //   FAKE_ROCR_NO_SVM    1: no shared virtual memory (hsa_amd_svm_* refuse, SVM_SUPPORTED false)
 //   FAKE_SVM_FAIL       1: every SVM prefetch into a GPU fails (the completion signal goes negative)
 //   FAKE_SVM_KFD_VRAM   0: SVM ranges migrated into HBM are not in KFD's vram_<gpu_id> (default 1)
+//   FAKE_ROCR_XNACK     1: recoverable page faults reported on (HSA_AMD_SYSTEM_INFO_XNACK_ENABLED)
+//   FAKE_SVM_HANG       1: prefetches into a GPU never complete (their signals stay at 1)
 // Test-only introspection: fake_rocr_* functions below.
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -77,6 +79,7 @@ struct State {
   std::map<uintptr_t, std::pair<int, uint64_t>> allocs;  // ptr -> (dev or -1 for host, size)
   std::map<uintptr_t, FakeQueue*> queues;
   std::map<uintptr_t, SvmRange> svm;
+  std::map<uintptr_t, int> locks;  // locked host ranges -> lock count
   char* arena = nullptr;
   uint64_t arena_size = 0, arena_next = 0;
   std::string kfd;  // fake KFD process dir of this process ("" = none)
@@ -288,7 +291,9 @@ hsa_status_t pool_allocate_impl(hsa_amd_memory_pool_t pool, size_t size, void** 
                                                                                      : -1;
   if (d < 0 && pool.handle != kCpuPool) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
   if (d >= 0 && s.gpus[d].used.load() + size > s.gpus[d].hbm) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
-  void* p = bump(size);
+  // Host memory is real (the application may touch pinned buffers); HBM is address space only.
+  void* p = d >= 0 ? bump(size) : mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (p == MAP_FAILED) p = nullptr;
   if (!p) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   s.allocs[reinterpret_cast<uintptr_t>(p)] = {d, size};
   if (d >= 0) {
@@ -308,6 +313,8 @@ hsa_status_t pool_free_impl(void* ptr) {
   if (d >= 0) {
     s.gpus[d].used.fetch_sub(it->second.second);
     kfd_update_vram(d);
+  } else {
+    munmap(ptr, it->second.second);
   }
   s.allocs.erase(it);
   return HSA_STATUS_SUCCESS;
@@ -347,6 +354,29 @@ hsa_status_t hsa_memory_allocate(hsa_region_t region, size_t size, void** ptr) {
   return pool_allocate_impl(hsa_amd_memory_pool_t{region.handle}, size, ptr);
 }
 hsa_status_t hsa_memory_free(void* ptr) { return pool_free_impl(ptr); }
+
+// Memory locks: a locked user range, counted per address (test introspection: fake_rocr_locked).
+static hsa_status_t lock_impl(void* host_ptr, size_t size, void** agent_ptr) {
+  if (!host_ptr || !size) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(st().mu);
+  st().locks[reinterpret_cast<uintptr_t>(host_ptr)]++;
+  if (agent_ptr) *agent_ptr = host_ptr;
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t hsa_amd_memory_lock(void* host_ptr, size_t size, hsa_agent_t*, int, void** agent_ptr) {
+  return lock_impl(host_ptr, size, agent_ptr);
+}
+hsa_status_t hsa_amd_memory_lock_to_pool(void* host_ptr, size_t size, hsa_agent_t*, int, hsa_amd_memory_pool_t,
+                                         uint32_t, void** agent_ptr) {
+  return lock_impl(host_ptr, size, agent_ptr);
+}
+hsa_status_t hsa_amd_memory_unlock(void* host_ptr) {
+  std::lock_guard<std::mutex> g(st().mu);
+  auto it = st().locks.find(reinterpret_cast<uintptr_t>(host_ptr));
+  if (it == st().locks.end()) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  if (--it->second == 0) st().locks.erase(it);
+  return HSA_STATUS_SUCCESS;
+}
 
 hsa_status_t hsa_amd_agents_allow_access(uint32_t, const hsa_agent_t*, const uint32_t*, const void*) {
   return HSA_STATUS_SUCCESS;
@@ -438,7 +468,7 @@ hsa_status_t hsa_system_get_info(hsa_system_info_t attr, void* value) {
   switch ((int)attr) {
     case HSA_AMD_SYSTEM_INFO_SVM_SUPPORTED: *static_cast<bool*>(value) = svm_on(); return HSA_STATUS_SUCCESS;
     case HSA_AMD_SYSTEM_INFO_SVM_ACCESSIBLE_BY_DEFAULT: *static_cast<bool*>(value) = false; return HSA_STATUS_SUCCESS;
-    case HSA_AMD_SYSTEM_INFO_XNACK_ENABLED: *static_cast<bool*>(value) = false; return HSA_STATUS_SUCCESS;
+    case HSA_AMD_SYSTEM_INFO_XNACK_ENABLED: *static_cast<bool*>(value) = env_u64("FAKE_ROCR_XNACK", 0) != 0; return HSA_STATUS_SUCCESS;
     default: return HSA_STATUS_ERROR_INVALID_ARGUMENT;
   }
 }
@@ -513,6 +543,11 @@ hsa_status_t hsa_amd_svm_prefetch_async(void* ptr, size_t size, hsa_agent_t agen
   auto* sig = reinterpret_cast<std::atomic<int64_t>*>(done.handle);
   const int to = gpu_of(agent), from = gpu_of(hsa_agent_t{r.loc});
   const bool counted = env_u64("FAKE_SVM_KFD_VRAM", 1) != 0;
+  if (sig && to >= 0 && env_u64("FAKE_SVM_HANG", 0)) {
+    // The migration never completes: the signal stays at its initial value (the caller may not
+    // destroy it - the fake's "driver" would still write it); the range does not move.
+    return HSA_STATUS_SUCCESS;
+  }
   bool ok = to != from || to < 0;
   if (to >= 0 && to != from && (env_u64("FAKE_SVM_FAIL", 0) || s.gpus[to].used.load() + size > s.gpus[to].hbm)) ok = false;
   if (ok && to != from) {

@@ -51,11 +51,27 @@
 //                    fake's SVM range now lists that agent}
 //   hostregister=SIZE  hipHostRegister of a fresh heap buffer -> {"hostregister": "ok"|"oom"};
 //                    hostunregister unregisters (and frees) the last one
+//   hsahost=SIZE     hsa_amd_memory_pool_allocate on the CPU pool, as a direct ROCr caller
+//                    (ctypes) would: {"hsahost": status}; hsahostfree frees the last one
+//   hsalock=SIZE     hsa_amd_memory_lock of a fresh heap buffer: {"hsalock": status};
+//                    hsaunlock unlocks (and frees) the last one
+//   hostusage        the container's pinned host memory: {"hostusage": bytes}
+//   hsamemfree       hsa_memory_free of the most recent allocation: {"hsamemfree": status}
+//   usage            the current device's charged bytes: {"usage": bytes}
+//   svmmap=SIZE      mmap SIZE bytes of ordinary memory and give the current device access
+//                    (SVM attributes, no placement): {"svmmap": status}
+//   svmprefetch=D    hsa_amd_svm_prefetch_async of the last range to GPU D (-1 = the CPU):
+//                    {"svmprefetch": status}
+//   svmpref=D        HSA_AMD_SVM_ATTRIB_PREFERRED_LOCATION of the last range: {"svmpref": status}
+//   hipprefetch=D / hipadvise=D  hipMemPrefetchAsync / hipMemAdvise(SetPreferredLocation) of
+//                    the last range: {"hipprefetch": rc} / {"hipadvise": rc}
+//   svmunmap         munmap of the last range: {"svmunmap": true}
 #define __HIP_PLATFORM_AMD__ 1
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <sys/mman.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -170,7 +186,35 @@ int main(int argc, char** argv) {
   std::vector<void*> ptrs, all_ptrs;
   std::vector<size_t> sizes;
   std::vector<hipStream_t> streams;
-  std::vector<void*> host_ptrs, registered;
+  std::vector<void*> host_ptrs, registered, hsa_host, hsa_locked;
+  std::vector<std::pair<void*, size_t>> svm_ranges;
+  hsa_agent_t cpu_agent{0};
+  std::vector<hsa_agent_t> gpu_agents;
+  hsa_amd_memory_pool_t cpu_pool{0};
+  (void)hsa_iterate_agents(
+      [](hsa_agent_t a, void* d) {
+        hsa_device_type_t t;
+        hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+        auto* v = static_cast<std::pair<hsa_agent_t*, std::vector<hsa_agent_t>*>*>(d);
+        if (t == HSA_DEVICE_TYPE_CPU && !v->first->handle) *v->first = a;
+        if (t == HSA_DEVICE_TYPE_GPU) v->second->push_back(a);
+        return HSA_STATUS_SUCCESS;
+      },
+      new std::pair<hsa_agent_t*, std::vector<hsa_agent_t>*>(&cpu_agent, &gpu_agents));
+  if (cpu_agent.handle)
+    (void)hsa_amd_agent_iterate_memory_pools(
+        cpu_agent,
+        [](hsa_amd_memory_pool_t p, void* d) {
+          *static_cast<hsa_amd_memory_pool_t*>(d) = p;
+          return HSA_STATUS_SUCCESS;
+        },
+        &cpu_pool);
+  auto agent_for = [&](int d) { return d >= 0 && d < (int)gpu_agents.size() ? gpu_agents[d] : cpu_agent; };
+  auto api_u64 = [](const char* name) {
+    using Get = uint64_t (*)();
+    auto f = reinterpret_cast<Get>(dlsym(RTLD_DEFAULT, name));
+    return f ? (unsigned long long)f() : 0ull;
+  };
   static uint32_t kernel_us[64];
   int kslot = 0;
   printf("{\"pid\": %d, \"fake_hostpid\": %d}\n", (int)getpid(), fake_rocr_host_pid());
@@ -369,6 +413,84 @@ int main(int argc, char** argv) {
         registered.pop_back();
       }
       printf("{\"hostunregister\": true}\n");
+    } else if (key == "hsamemfree") {
+      // the most recent device allocation, freed through ROCr's legacy entry point
+      int st = -1;
+      if (!ptrs.empty()) {
+        st = (int)hsa_memory_free(ptrs.back());
+        std::replace(all_ptrs.begin(), all_ptrs.end(), ptrs.back(), static_cast<void*>(nullptr));
+        ptrs.pop_back();
+      }
+      printf("{\"hsamemfree\": %d}\n", st);
+    } else if (key == "hsahost") {
+      void* p = nullptr;
+      int st = (int)hsa_amd_memory_pool_allocate(cpu_pool, (size_t)parse_size(val.c_str()), 0, &p);
+      if (st == 0) hsa_host.push_back(p);
+      printf("{\"hsahost\": %d}\n", st);
+    } else if (key == "hsahostfree") {
+      int st = -1;
+      if (!hsa_host.empty()) {
+        st = (int)hsa_amd_memory_pool_free(hsa_host.back());
+        hsa_host.pop_back();
+      }
+      printf("{\"hsahostfree\": %d}\n", st);
+    } else if (key == "hsalock") {
+      size_t n = (size_t)parse_size(val.c_str());
+      void* p = malloc(n ? n : 1);
+      void* agent_ptr = nullptr;
+      int st = (int)hsa_amd_memory_lock(p, n, nullptr, 0, &agent_ptr);
+      if (st == 0) hsa_locked.push_back(p);
+      else free(p);
+      printf("{\"hsalock\": %d}\n", st);
+    } else if (key == "hsaunlock") {
+      int st = -1;
+      if (!hsa_locked.empty()) {
+        st = (int)hsa_amd_memory_unlock(hsa_locked.back());
+        free(hsa_locked.back());
+        hsa_locked.pop_back();
+      }
+      printf("{\"hsaunlock\": %d}\n", st);
+    } else if (key == "hostusage") {
+      printf("{\"hostusage\": %llu}\n", api_u64("vgpu_get_host_memory_usage"));
+    } else if (key == "usage") {
+      printf("{\"usage\": %llu}\n", api_u64("vgpu_get_current_device_memory_usage"));
+    } else if (key == "svmmap") {
+      size_t n = (size_t)parse_size(val.c_str());
+      void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+      hsa_amd_svm_attribute_pair_t a{HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE_IN_PLACE, agent_for(dev).handle};
+      int st = p == MAP_FAILED ? -1 : (int)hsa_amd_svm_attributes_set(p, n, &a, 1);
+      if (p != MAP_FAILED) svm_ranges.emplace_back(p, n);
+      printf("{\"svmmap\": %d}\n", st);
+    } else if (key == "svmprefetch" || key == "svmpref") {
+      int st = -1;
+      if (!svm_ranges.empty()) {
+        const hsa_agent_t a = agent_for(atoi(val.c_str()));
+        if (key == "svmpref") {
+          hsa_amd_svm_attribute_pair_t at{HSA_AMD_SVM_ATTRIB_PREFERRED_LOCATION, a.handle};
+          st = (int)hsa_amd_svm_attributes_set(svm_ranges.back().first, svm_ranges.back().second, &at, 1);
+        } else {
+          hsa_signal_t sig;
+          hsa_signal_create(1, 0, nullptr, &sig);
+          st = (int)hsa_amd_svm_prefetch_async(svm_ranges.back().first, svm_ranges.back().second, a, 0, nullptr, sig);
+          hsa_signal_destroy(sig);
+        }
+      }
+      printf("{\"%s\": %d}\n", key.c_str(), st);
+    } else if (key == "hipprefetch" || key == "hipadvise") {
+      int rc = -1;
+      if (!svm_ranges.empty()) {
+        const int d = atoi(val.c_str());
+        rc = key == "hipprefetch"
+                 ? (int)hipMemPrefetchAsync(svm_ranges.back().first, svm_ranges.back().second, d, stream)
+                 : (int)hipMemAdvise(svm_ranges.back().first, svm_ranges.back().second, hipMemAdviseSetPreferredLocation, d);
+      }
+      printf("{\"%s\": %d}\n", key.c_str(), rc);
+    } else if (key == "svmunmap") {
+      if (!svm_ranges.empty()) {
+        munmap(svm_ranges.back().first, svm_ranges.back().second);
+        svm_ranges.pop_back();
+      }
+      printf("{\"svmunmap\": true}\n");
     } else if (key == "setlimit" || key == "setcu") {
       // The in-container control API (reference set_current_device_memory_limit /
       // set_current_device_sm_limit_scale): {"setlimit": rc} / {"setcu": rc}

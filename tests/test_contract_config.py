@@ -300,7 +300,8 @@ def test_placement_duplicate_and_host_memory_flags():
                                     "HOST_MEMORY_PER_VGPU": "512m"})
     assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("binpack", "merge", 512 << 20)
     cfg = parse_config([], environ={})
-    assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("spread", "reject", 0)
+    assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("spread", "merge", 0)
+    assert parse_config(["--duplicate-vgpus", "reject"], environ={}).duplicate_vgpus == "reject"
     for bad in (["--placement", "random"], ["--duplicate-vgpus", "allow"], ["--host-memory-per-vgpu", "lots"]):
         with pytest.raises(ValueError):
             parse_config(bad, environ={})
@@ -351,18 +352,54 @@ def test_board_slot_mounts(tmp_path):
     assert paths.index("/usr/local/vgpu/board") < paths.index(f"/usr/local/vgpu/board/{slots[0]}")
 
 
-def test_departed_board_slots_are_removed(tmp_path):
-    """A slot untouched for an hour (its container has had no publishing GPU process for
-    that long: a live one touches its slot every 10 s) is removed at the next Allocate;
-    younger ones stay."""
+def test_container_files_live_as_long_as_the_pod(tmp_path):
+    """A container's host files (limits, region, allow-list, board slot) are the sources of
+    its bind mounts, which the kubelet reuses when the container restarts: they are removed
+    only when PodResources no longer lists the container's devices as held - however old they
+    are - and never when PodResources cannot be asked (a week-old limits file or an
+    idle hour-old region broke the restart)."""
     import time
-    from amdvgpu.plugin.contract import BOARD_MAX_AGE_S, board_slot, ensure_board_dir
-    board = ensure_board_dir(str(tmp_path / "vgpu"))
-    old, young = os.path.join(board, "old.slot"), os.path.join(board, "young.slot")
-    for p in (old, young):
-        open(p, "w").close()
-    t = time.time() - BOARD_MAX_AGE_S - 60
-    os.utime(old, (t, t))
-    assert BOARD_MAX_AGE_S <= 3600
-    new = board_slot(str(tmp_path / "vgpu"), "new")
-    assert os.path.exists(new) and os.path.exists(young) and not os.path.exists(old)
+    from amdvgpu.plugin.config import PluginConfig
+    from amdvgpu.plugin.contract import build_container_response, container_files, gc_container_files
+    from amdvgpu.plugin.devices import FakeBackend
+    from amdvgpu.plugin.vdevice import device_to_vdevices
+    from amdvgpu.plugin.contract import ensure_board_dir
+    vdir = str(tmp_path / "vgpu")
+    ensure_board_dir(vdir)
+    cfg = PluginConfig(vgpu_dir=vdir, device_split_count=4).validate()
+    devs = FakeBackend(n=1).devices()
+    vds = device_to_vdevices(devs, 4, 1.0, 1.0)
+    by_uuid = {d.uuid: d for d in devs}
+    names = {}
+    for ids in (["a-0"], ["a-1"], ["a-2"]):
+        r = build_container_response(cfg, [vds[int(ids[0][-1])]], by_uuid, kubelet_ids=ids, resource="amd.com/gpu")
+        names[ids[0]] = os.path.basename(dict(r.envs)["VGPU_SHARED_CACHE"]).rsplit(".", 1)[0]
+    for n in names.values():
+        assert all(os.path.exists(f) for f in container_files(vdir, n)), container_files(vdir, n)
+    week = time.time() + 8 * 24 * 3600
+    assert gc_container_files(vdir, None, now=week) == []                         # no PodResources: keep all
+    assert gc_container_files(vdir, {"amd.com/gpu": set()}, now=time.time()) == []  # within the grace period
+    held = {"amd.com/gpu": {frozenset(["a-0"]), frozenset(["a-2"])}}
+    assert gc_container_files(vdir, held, now=week) == [names["a-1"]]
+    assert not any(os.path.exists(f) for f in container_files(vdir, names["a-1"]))
+    for k in ("a-0", "a-2"):
+        assert all(os.path.exists(f) for f in container_files(vdir, names[k]))
+    # the same IDs under another resource are not this container's
+    assert sorted(gc_container_files(vdir, {"amd.com/gpu-latency": held["amd.com/gpu"]}, now=week)) == \
+        sorted([names["a-0"], names["a-2"]])
+
+
+def test_limits_file_carries_the_oom_killer(tmp_path):
+    """The memory backstop is the plugin's: the limits file switches it (on by default)."""
+    from amdvgpu.plugin.config import PluginConfig
+    from amdvgpu.plugin.contract import build_container_response
+    from amdvgpu.plugin.devices import FakeBackend
+    from amdvgpu.plugin.vdevice import device_to_vdevices
+    devs = FakeBackend(n=1).devices()
+    vds = device_to_vdevices(devs, 2, 1.0, 1.0)
+    for on, want in ((True, "1"), (False, "0")):
+        cfg = PluginConfig(vgpu_dir=str(tmp_path / f"v{want}"), active_oom_killer=on).validate()
+        r = build_container_response(cfg, vds[:1], {d.uuid: d for d in devs})
+        mounts = {m.container_path: m.host_path for m in r.mounts}
+        limits = dict(l.split("=", 1) for l in open(mounts["/vgpu/limits"]).read().splitlines())
+        assert limits["VGPU_ACTIVE_OOM_KILLER"] == want

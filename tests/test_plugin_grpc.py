@@ -241,11 +241,12 @@ def test_stop_honoured_while_the_kubelet_is_down(plugin_dir):
     assert not th.is_alive()
 
 
-def test_duplicate_vgpus_rejected_by_default(plugin_dir):
-    """Two vGPUs of one GPU in one container: Allocate fails with a clear error (the
-    container would otherwise see one device with the summed share)."""
+def test_duplicate_vgpus_rejected_on_request(plugin_dir):
+    """--duplicate-vgpus=reject: two vGPUs of one GPU in one container fail Allocate with a
+    clear error (the container would otherwise see one device with the summed share)."""
     import grpc
-    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=4, backend=FakeBackend(n=1))
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=4, backend=FakeBackend(n=1),
+                                  duplicate_vgpus="reject")
     try:
         k.wait_registered("amd.com/gpu")
         devs = k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
@@ -258,20 +259,24 @@ def test_duplicate_vgpus_rejected_by_default(plugin_dir):
         shutdown(k, stop, th)
 
 
-def test_duplicate_vgpus_merged_on_request(plugin_dir):
-    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=4, backend=FakeBackend(n=1),
-                                  duplicate_vgpus="merge")
+def test_readme_two_vgpu_pod_admitted_on_a_one_gpu_node(plugin_dir):
+    """The reference README's sample pod requests two vGPUs (README.md:205). On a node with
+    one GPU the kubelet must hand it two vGPUs of that GPU; by default (merge) Allocate admits
+    it as one device with the summed quota and CU share, annotated for the operator."""
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=4, backend=FakeBackend(n=1))
     try:
         k.wait_registered("amd.com/gpu")
-        devs = k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
-        ids = sorted(devs)[:2]
-        resp = k.allocate_ids("amd.com/gpu", ids)
+        k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
+        ids, resp = k.allocate("amd.com/gpu", 2)   # the kubelet's flow: preferred allocation, then Allocate
         envs = dict(resp.envs)
         uuid = ids[0].rsplit("-", 1)[0]
+        assert ids[1].rsplit("-", 1)[0] == uuid
         assert envs["VGPU_DUPLICATE_MERGED"] == uuid
         assert dict(resp.annotations)["amd-vgpu/merged-duplicates"] == uuid
         assert envs["ROCR_VISIBLE_DEVICES"] == uuid  # one device in the container
         assert envs["VGPU_DEVICE_MAP"] == f"0:{uuid} 1:{uuid}"
+        total = FakeBackend(n=1).devices()[0].memory_total >> 20
+        assert envs["VGPU_DEVICE_MEMORY_LIMIT_0"] == envs["VGPU_DEVICE_MEMORY_LIMIT_1"] == f"{total // 4}m"
     finally:
         shutdown(k, stop, th)
 

@@ -1,0 +1,141 @@
+"""Paths to device and pinned host memory that pass no allocation entry point, end to end on
+the CPU-only fake runtime (native/tests/fake): each one is held to the container's quota.
+
+* The tenant's own shared virtual memory (svm_hooks.cpp): ordinary memory registered with
+  hsa_amd_svm_attributes_set and moved into HBM with hsa_amd_svm_prefetch_async (or by
+  HIP's hipMemPrefetchAsync / hipMemAdvise on system memory) - invisible to KFD's VRAM
+  counter and ROCr's free memory on MI355X (profiles/r4b). Reference: cuMemAllocManaged
+  is an accounted allocation ([memory.c:216-223], oom_check [allocator.c:35-53]).
+* Pinned host memory at the ROCr layer (host_hooks.cpp): CPU-pool allocations and
+  hsa_amd_memory_lock from a direct ROCr caller, and HIP's pinned memory counted exactly once.
+  Reference: class (b) cuMemAllocHost_v2 / cuMemHostAlloc / cuMemHostRegister_v2.
+"""
+import pytest
+
+from test_shim_fake import fake, run  # noqa: F401  (fixture)
+
+GiB = 1 << 30
+MiB = 1 << 20
+OOR = 0x1008        # HSA_STATUS_ERROR_OUT_OF_RESOURCES
+HIP_OOM = 2         # hipErrorOutOfMemory
+
+
+@pytest.fixture
+def svm_fake(fake):
+    """The fake as MI355X's KFD behaves (profiles/r4b): SVM pages in HBM are not in vram_<id>."""
+    def env(**kw):
+        kw.setdefault("FAKE_SVM_KFD_VRAM", "0")
+        return fake(**kw)
+    env.region = fake.region
+    env.kfd = fake.kfd
+    return env
+
+
+def _vals(out, key):
+    return [o[key] for o in out if key in o]
+
+
+def test_svm_prefetch_past_the_quota_is_refused(svm_fake):
+    """A direct ROCr caller maps 2x its 1 GiB quota of ordinary memory and prefetches it into
+    HBM: refused before the runtime sees it. 512 MiB fits and is charged as device data; moving
+    it back to the CPU gives the charge back."""
+    e = svm_fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
+    out = run(e, "svmmap=2g", "usage", "svmprefetch=0", "usage", "svmunmap",
+              "svmmap=512m", "svmprefetch=0", "usage", "malloc=768m", "svmprefetch=-1", "usage", "malloc=768m")
+    assert _vals(out, "svmmap") == [0, 0]
+    assert _vals(out, "svmprefetch") == [OOR, 0, 0], out
+    assert _vals(out, "usage") == [0, 0, 512 * MiB, 0], out
+    assert _vals(out, "malloc") == ["oom", "ok"], out   # 512 + 768 > 1024; after the move back it fits
+
+
+def test_hip_prefetch_of_system_memory_is_charged(svm_fake):
+    """hipMemPrefetchAsync of system-allocated memory reaches the same ROCr entry point: the
+    range is charged to the device it was prefetched to and a second one past the quota fails
+    with hipErrorOutOfMemory."""
+    e = svm_fake(gpus=2, VGPU_DEVICE_MEMORY_LIMIT_0="1g", VGPU_DEVICE_MEMORY_LIMIT_1="4g")
+    out = run(e, "svmmap=768m", "hipprefetch=0", "usage", "svmmap=512m", "hipprefetch=0", "hipprefetch=1", "usage",
+              "dev=1", "usage")
+    assert _vals(out, "hipprefetch") == [0, HIP_OOM, 0], out
+    assert _vals(out, "usage") == [768 * MiB, 768 * MiB, 512 * MiB], out
+
+
+@pytest.mark.parametrize("xnack,want", [("0", 0), ("1", 256 * MiB)])
+def test_preferred_location_charged_only_where_pages_can_follow_it(svm_fake, xnack, want):
+    """A preferred location moves pages only through recoverable faults (XNACK): with XNACK
+    the range is charged to the preferred GPU (hipMemAdvise SetPreferredLocation), without
+    it only a prefetch puts it in HBM."""
+    e = svm_fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g", FAKE_ROCR_XNACK=xnack)
+    out = run(e, "svmmap=256m", "hipadvise=0", "usage", "svmpref=-1", "usage")
+    assert _vals(out, "hipadvise") == [0]
+    assert _vals(out, "usage") == [want, 0], out
+
+
+def test_unmapped_svm_range_gives_its_charge_back(svm_fake):
+    """KFD drops a range the process unmaps: the maintenance thread sees it in
+    /proc/self/maps and releases the charge (the quota is usable again)."""
+    e = svm_fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
+    out = run(e, "svmmap=768m", "svmprefetch=0", "usage", "malloc=512m", "svmunmap", "sleep=0.5", "usage",
+              "malloc=512m")
+    assert _vals(out, "usage") == [768 * MiB, 0], out
+    assert _vals(out, "malloc") == ["oom", "ok"], out
+
+
+def test_partial_prefetch_charges_only_the_moved_pages(svm_fake):
+    """Prefetching a range twice (or two overlapping ranges) charges each page once."""
+    e = svm_fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
+    out = run(e, "svmmap=600m", "svmprefetch=0", "svmprefetch=0", "usage")
+    assert _vals(out, "svmprefetch") == [0, 0]
+    assert _vals(out, "usage") == [600 * MiB], out
+
+
+def test_svm_range_tracking_survives_region_rewrite(svm_fake):
+    """A tenant that re-initialises its region (clearing every charge) gets its prefetched SVM
+    ranges charged again, as for its allocations."""
+    import json
+    import subprocess
+    from test_shim_fake import HARNESS
+    e = svm_fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
+    p = subprocess.Popen([HARNESS, "svmmap=256m", "svmprefetch=0", "mark=ready", "sleep=1.0", "usage"], env=e,
+                         stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        if '"mark"' in line:
+            break
+    with open(svm_fake.region, "r+b") as f:   # wiped: every slot and charge gone
+        f.write(b"\0" * 4096)
+    rest = [json.loads(l) for l in p.stdout.read().splitlines() if l.startswith("{")]
+    assert p.wait(30) == 0
+    assert _vals(rest, "usage") == [256 * MiB], rest
+
+
+def test_direct_rocr_pinned_memory_is_held_to_the_host_budget(fake):
+    """A process pinning host memory through ROCr itself (a CPU-pool allocation, a memory
+    lock) is held to VGPU_HOST_MEMORY_LIMIT like hipHostMalloc; frees and unlocks give the
+    budget back."""
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g", VGPU_HOST_MEMORY_LIMIT="64m")
+    out = run(e, "hsahost=40m", "hsalock=20m", "hsahost=8m", "hostusage", "hsahostfree", "hsaunlock", "hostusage",
+              "hsalock=40m", "hsalock=30m", "hostusage")
+    assert _vals(out, "hsahost") == [0, OOR], out          # 40 + 20 + 8 > 64 MiB
+    assert _vals(out, "hsalock") == [0, 0, OOR], out       # 40 + 30 > 64 MiB
+    assert _vals(out, "hostusage") == [60 * MiB, 0, 40 * MiB], out
+
+
+def test_hip_pinned_memory_is_charged_once(fake):
+    """hipHostMalloc and hipHostRegister reach ROCr's pool allocation and memory lock: each is
+    charged exactly once (not again at the HIP layer), and hipFree of pinned memory releases it."""
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
+    out = run(e, "hostmalloc=24m", "hostusage", "hostregister=8m", "hostusage", "hostfree_hipfree", "hostusage",
+              "hostunregister", "hostusage")
+    assert _vals(out, "hostusage") == [24 * MiB, 32 * MiB, 8 * MiB, 0], out
+
+
+def test_pinned_spill_freed_through_hsa_memory_free(fake):
+    """ROCr accepts hsa_memory_free for a pool allocation: a pinned spill freed that way gives
+    back its spill charge and its host budget (the two free hooks differed)."""
+    e = fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="256m", VGPU_DEVICE_HBM_LIMIT_0="64m",
+             VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come", VGPU_HOST_MEMORY_LIMIT="128m",
+             VGPU_SPILL_BACKING="pinned")
+    out = run(e, "malloc=48m", "malloc=32m", "spilled", "hostusage", "hsamemfree", "spilled", "hostusage", "usage")
+    assert _vals(out, "hsamemfree") == [0]
+    assert _vals(out, "spilled") == [32 * MiB, 0], out
+    assert _vals(out, "hostusage") == [32 * MiB, 0], out
+    assert _vals(out, "usage") == [48 * MiB], out

@@ -322,6 +322,19 @@ def test_failed_promotion_is_undone(fake):
     assert [o for o in out if "total" in o][0]["free"] == 256 * MiB - 32 * MiB
 
 
+def test_promotion_that_never_completes(fake):
+    """The driver never finishes a promotion (its completion signal stays pending past the
+    bound): the shim does not destroy the signal under the driver nor start the reverse
+    migration over it; the range stays charged as HBM data (the conservative side for the
+    other tenants), its host budget released, and the process carries on."""
+    out = run(_svm_env(fake, FAKE_SVM_HANG="1", VGPU_SPILL_MIGRATE_TIMEOUT_MS="100"), "malloc=48m", "malloc=32m",
+              "fill=3", "freeidx=0", "sleep=0.8", "spilled", "check=3", "meminfo", "malloc=16m")
+    assert [o["spilled"] for o in out if "spilled" in o] == [0]
+    assert [o for o in out if "check" in o][0]["check"] == "ok"
+    assert [o for o in out if "total" in o][0]["free"] == 256 * MiB - 32 * MiB
+    assert [o["malloc"] for o in out if "malloc" in o] == ["ok", "ok", "ok"]
+
+
 def test_svm_spill_is_charged_to_the_host_budget(fake):
     """An SVM spill draws on the host budget like a pinned one (128 MiB here): a spill past it
     is refused; after a promotion its host memory is given back and a spill fits again."""

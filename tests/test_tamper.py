@@ -217,3 +217,23 @@ def test_latency_class_needs_the_plugins_grant(pod, granted, want):
     e["VGPU_TASK_PRIORITY"] = "0"
     q = [o for o in run(e, "stream", "queues") if "queues" in o][0]["queues"]
     assert q[0]["priority"] == want, q
+
+
+def test_region_hbm_share_rewritten_to_zero_still_spills(pod):
+    """An oversubscribed vGPU (2 GiB quota, 256 MiB HBM share): the tenant writes hbm_limit=0
+    ("no cap") into its region to keep its whole quota in HBM. The plugin's share still holds:
+    the next allocation past it spills to host memory, and the region reads the share again
+    (the HBM share was the one limit the ceiling did not cover)."""
+    e = pod(VGPU_DEVICE_MEMORY_LIMIT_0="2048m", VGPU_DEVICE_HBM_LIMIT_0="256m", VGPU_OVERSUBSCRIBE="true",
+            VGPU_SPILL_POLICY="first-come", VGPU_SPILL_BACKING="pinned")
+    e.update(VGPU_DEVICE_MEMORY_LIMIT_0="2048m", VGPU_DEVICE_HBM_LIMIT_0="256m", VGPU_OVERSUBSCRIBE="true",
+             VGPU_SPILL_POLICY="first-come", VGPU_SPILL_BACKING="pinned")
+    p = _start(e, "malloc=200m", "mark=ready", "sleep=0.6", "malloc=200m", "spilled")
+    _wait_mark(p)
+    with Region(str(pod.region)) as r:
+        r.set_hbm_limit(0, 0)
+    out = _finish(p)
+    assert mallocs(out) == ["ok", "ok"]
+    assert [o["spilled"] for o in out if "spilled" in o] == [200 * MiB], out
+    with Region(str(pod.region)) as r:
+        assert r.device(0)["hbm_limit"] == 256 * MiB
