@@ -66,6 +66,13 @@ enum class ChargeModel : int {
                   // tenant that co-runs without losing occupancy pays what it would alone
 };
 
+// Host waits of a HIP process (VGPU_SYNC_WAIT, native/src/shim/sync_hooks.cpp).
+enum class SyncWait : int {
+  kAuto = 0,    // poll with short sleeps while the GPU is crowded, else the runtime's own wait
+  kPoll = 1,    // always poll
+  kNative = 2,  // never (the runtime's wait, which spins a CPU)
+};
+
 // GPU_CORE_UTILIZATION_POLICY analogue.
 enum class CuPolicy : int { kDefault = 0, kForce = 1, kDisable = 2 };
 
@@ -96,6 +103,7 @@ struct Config {
   CuMode cu_mode = CuMode::kAuto;        // VGPU_CU_MODE
   CuPolicy cu_policy = CuPolicy::kDefault;
   bool active_oom_killer = true;         // VGPU_ACTIVE_OOM_KILLER (reference default: on)
+  SyncWait sync_wait = SyncWait::kAuto;  // VGPU_SYNC_WAIT: auto | poll | native
   bool memory_override = false;          // VGPU_MEMORY_OVERRIDE
   bool signal_control = false;           // VGPU_SIGNAL_CONTROL: also honour SIGUSR1/2
   bool hook_smi = true;                  // VGPU_HOOK_SMI: virtualise amd-smi/rocm-smi

@@ -8,8 +8,9 @@
 // exports the original versions, so the references are pinned to them here, and the shim
 // links libdl / libpthread explicitly for the older images that keep the functions there.
 // stat/fstat (GLIBC_2.33) are not used at all (access / lseek / a raw newfstatat instead).
-// dlsym / dlvsym are not listed: the shim defines (interposes) both, in both versions, and
-// reaches glibc's through the C library's symbol table (src/shim/dlsym_hook.cpp). The reference's
+// dlsym / dlvsym / dlopen / dlmopen are not listed: the shim defines (interposes) them, in
+// every version, and reaches glibc's through the C library's symbol table
+// (src/shim/dlsym_hook.cpp). The reference's
 // libvgpu.so was built on Ubuntu 20.04 for the same reason.
 //
 // Force-included (-include) into every object of the non-sanitizer build; the sanitizer
@@ -17,7 +18,6 @@
 // tests/test_native_core.py::test_shim_needs_only_old_glibc.
 #pragma once
 #if defined(__x86_64__) && !defined(VGPU_NO_GLIBC_COMPAT)
-__asm__(".symver dlopen,dlopen@GLIBC_2.2.5");
 __asm__(".symver dlclose,dlclose@GLIBC_2.2.5");
 __asm__(".symver dladdr,dladdr@GLIBC_2.2.5");
 __asm__(".symver dlerror,dlerror@GLIBC_2.2.5");

@@ -291,6 +291,12 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   }
   cfg->active_oom_killer = parse_bool(getenv_fn("VGPU_ACTIVE_OOM_KILLER"), true);  // reference: unset = on
   cfg->memory_override = parse_bool(getenv_fn("VGPU_MEMORY_OVERRIDE"), false);
+  if (const char* s = getenv_fn("VGPU_SYNC_WAIT")) {
+    if (!strcasecmp(s, "auto")) cfg->sync_wait = SyncWait::kAuto;
+    else if (!strcasecmp(s, "poll")) cfg->sync_wait = SyncWait::kPoll;
+    else if (!strcasecmp(s, "native") || !strcasecmp(s, "spin")) cfg->sync_wait = SyncWait::kNative;
+    else VLOG_WARN("invalid VGPU_SYNC_WAIT=%s, using auto", s);
+  }
   cfg->signal_control = parse_bool(getenv_fn("VGPU_SIGNAL_CONTROL"), false);
   cfg->fail_open = parse_bool(getenv_fn("VGPU_FAIL_OPEN"), false);
   cfg->hook_smi = parse_bool(getenv_fn("VGPU_HOOK_SMI"), true);

@@ -548,6 +548,7 @@ const char* const kHsaHooked[] = {
     "hsa_memory_allocate", "hsa_memory_free", "hsa_amd_agents_allow_access",
     "hsa_amd_svm_attributes_set", "hsa_amd_svm_prefetch_async",  // svm_hooks.cpp
     "hsa_amd_memory_lock", "hsa_amd_memory_lock_to_pool", "hsa_amd_memory_unlock",  // host_hooks.cpp
+    "hsa_signal_wait_scacquire",                                                       // sync_hooks.cpp
 };
 constexpr int kNumHsaHooked = sizeof(kHsaHooked) / sizeof(kHsaHooked[0]);
 

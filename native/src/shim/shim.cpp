@@ -39,7 +39,9 @@ const char* const kStatNames[kStatCount] = {"hsa_agent_get_info", "hsa_amd_memor
 void print_stats() {
   fprintf(stderr, "[vGPU stats pid %d]", (int)getpid());
   for (int i = 0; i < kStatCount; i++) fprintf(stderr, " %s=%lu", kStatNames[i], (unsigned long)g_stats[i].load());
-  fprintf(stderr, "\n");
+  fprintf(stderr, " blocking_waits=%lu polled=%lu wait_ms=%.1f wakeups=%lu active_waits=%lu active_ms=%.1f\n",
+          (unsigned long)g_sync_waits.load(), (unsigned long)g_sync_polled.load(), g_sync_wait_ns.load() / 1e6,
+          (unsigned long)g_sync_wakeups.load(), (unsigned long)g_sync_active.load(), g_sync_active_ns.load() / 1e6);
 }
 
 __attribute__((constructor)) void stats_ctor() {
@@ -404,6 +406,19 @@ void shim_init_after_hsa() {
   for (int c = 0; c < sc.n_cpu; c++) {
     VGPU_REAL_HSA(hsa_amd_agent_iterate_memory_pools);
     real_hsa_amd_agent_iterate_memory_pools(sc.cpus[c], cpu_pool_record_cb, &s);
+  }
+  // A GPU agent's region list (legacy API) also names the system memory regions it can reach
+  // - the CPU pools under another name: host memory, not the GPU's (measured on MI355X: a
+  // CPU-pool allocation was charged to the device quota, profiles/r5b).
+  for (int i = 0; i < s.n_agents; i++) {
+    AgentInfo& a = s.agents[i];
+    int kept = 0;
+    for (int j = 0; j < a.n_pools; j++) {
+      bool host = false;
+      for (int c = 0; c < s.n_cpu_pools && !host; c++) host = s.cpu_pools[c].handle == a.pools[j].handle;
+      if (!host) a.pools[kept++] = a.pools[j];
+    }
+    a.n_pools = kept;
   }
   for (int i = 0; i < s.n_agents; i++) {
     AgentInfo& a = s.agents[i];

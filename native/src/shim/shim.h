@@ -142,6 +142,9 @@ enum StatId : int {
 };
 extern bool g_stats_on;
 extern std::atomic<uint64_t> g_stats[kStatCount];
+// Host waits (sync_hooks.cpp): blocking waits, of which polled, their time, poll wake-ups.
+extern std::atomic<uint64_t> g_sync_waits, g_sync_polled, g_sync_wait_ns, g_sync_wakeups, g_sync_active,
+    g_sync_active_ns;
 #define VGPU_STAT(id)                                                                  \
   do {                                                                                 \
     if (__builtin_expect(::vgpu::g_stats_on, 0))                                       \

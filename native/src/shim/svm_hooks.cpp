@@ -4,10 +4,9 @@
 // KFD's SVM API registers an ordinary range of a process's memory for GPU access and moves
 // it into a GPU's HBM on request (hsa_amd_svm_prefetch_async) or, with recoverable page
 // faults, towards its preferred location (HSA_AMD_SVM_ATTRIB_PREFERRED_LOCATION). Neither
-// passes an allocation entry point, and migrated pages show up neither in KFD's per-process
-// vram_<gpu_id> nor in ROCr's free-memory figure (profiles/r4b) - so without these hooks any
-// process could mmap memory and prefetch it into HBM past its quota, invisible to every
-// backstop. libamdhip64 imports both entry points: hipMemAdvise and hipMemPrefetchAsync on
+// passes an allocation entry point, and ROCr's free-memory figure does not show migrated
+// pages (profiles/r4b); KFD's per-process vram_<gpu_id> does (profiles/r5b), so the OOM killer
+// would catch a large escape after the fact - these hooks refuse it before the driver sees it. libamdhip64 imports both entry points: hipMemAdvise and hipMemPrefetchAsync on
 // system-allocated memory reach them as well.
 //
 // Reference: cuMemAllocManaged is an accounted allocation ([memory.c:216-223], oom_check +
@@ -208,8 +207,9 @@ int64_t svm_tenant_outside_kfd(int dev) {
   ShimState& s = shim();
   if (dev < 0 || dev >= kMaxDevices) return 0;
   // Pages only preferred on a device never left host memory; prefetched ones are in VRAM,
-  // which KFD's counter shows only where the driver counts SVM pages (spill.cpp measures it).
-  return s.tsvm_pref[dev] + (s.svm_kfd_vram == 1 ? 0 : s.tsvm_loc[dev]);
+  // which KFD's per-process counter shows (measured on MI355X, profiles/r5b) unless a spill
+  // promotion found otherwise (spill.cpp measures it around its first migration).
+  return s.tsvm_pref[dev] + (s.svm_kfd_vram == 0 ? s.tsvm_loc[dev] : 0);
 }
 
 void svm_tenant_reconcile() {

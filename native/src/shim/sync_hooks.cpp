@@ -1,0 +1,108 @@
+// Host waits on a crowded GPU: polling with short sleeps instead of the runtime's busy wait.
+//
+// Every HIP synchronisation (hipDeviceSynchronize - torch.cuda.synchronize -,
+// hipStreamSynchronize, hipEventSynchronize) ends in ROCr's hsa_signal_wait_scacquire, which
+// libamdhip64 imports. A GPU-bound PyTorch process spends its waits spinning on a CPU there
+// (profiles/r4za: 1.1-1.6 CPUs busy per pod whatever the wait style, natively too). On a GPU
+// shared by many pods that is one spinning core per pod doing nothing but wait for its turn:
+// 16 pods of one GPU hold 16 cores, 128 on an 8-GPU node. The reference's throttle sleeps
+// rather than spins (rate_limiter [multiprocess_utilization_watcher.c:53-72], nanosleep 10 ms).
+//
+// Here a blocking wait (HSA_WAIT_STATE_BLOCKED) of a process whose GPU is crowded (the
+// maintenance thread's crowd count: two or more other busy processes, watcher.cpp) becomes a
+// loop of acquire-loads and nanosleeps; the sleep grows with the time already waited (1/8 of
+// it, 20 us to 500 us), so a wait overshoots its completion by at most ~12 % (and 0.5 ms),
+// and a multi-millisecond wait costs a few dozen wake-ups instead of a core. A lone pod keeps
+// ROCr's own wait (no added latency); VGPU_SYNC_WAIT=poll|native forces either way.
+#include <time.h>
+
+#include <algorithm>
+#include <atomic>
+
+#include "real.h"
+#include "shim.h"
+#include "vgpu/config.h"
+#include "vgpu/ratelimit.h"
+
+namespace vgpu {
+
+std::atomic<uint64_t> g_sync_waits{0};      // blocking waits seen (VGPU_STATS)
+std::atomic<uint64_t> g_sync_polled{0};     // of which polled
+std::atomic<uint64_t> g_sync_wait_ns{0};    // time inside them
+std::atomic<uint64_t> g_sync_wakeups{0};    // sleeps taken while polling
+std::atomic<uint64_t> g_sync_active{0};     // active (spin-hinted) waits
+std::atomic<uint64_t> g_sync_active_ns{0};
+
+namespace {
+
+bool satisfied(hsa_signal_condition_t c, hsa_signal_value_t v, hsa_signal_value_t cmp) {
+  switch (c) {
+    case HSA_SIGNAL_CONDITION_EQ: return v == cmp;
+    case HSA_SIGNAL_CONDITION_NE: return v != cmp;
+    case HSA_SIGNAL_CONDITION_LT: return v < cmp;
+    case HSA_SIGNAL_CONDITION_GTE: return v >= cmp;
+    default: return true;
+  }
+}
+
+// Whether this process's waits should poll now.
+bool poll_now() {
+  const SyncWait m = config().sync_wait;
+  if (m == SyncWait::kPoll) return true;
+  if (m == SyncWait::kNative) return false;
+  ShimState& s = shim();
+  if (!s.active || s.phase.load(std::memory_order_relaxed) != 2) return false;
+  const Region* r = s.region.raw();
+  for (int d = 0; d < s.n_agents; d++)
+    if (r->dev[d].crowd.load(std::memory_order_relaxed) > kAutoSpatialMaxCrowd) return true;
+  return false;
+}
+
+}  // namespace
+
+}  // namespace vgpu
+
+using namespace vgpu;
+
+extern "C" {
+
+hsa_signal_value_t hsa_signal_wait_scacquire(hsa_signal_t signal, hsa_signal_condition_t condition,
+                                             hsa_signal_value_t compare_value, uint64_t timeout_hint,
+                                             hsa_wait_state_t wait_state_hint) {
+  VGPU_REAL_HSA(hsa_signal_wait_scacquire);
+  if (__builtin_expect(wait_state_hint != HSA_WAIT_STATE_BLOCKED || !poll_now(), 1)) {
+    if (__builtin_expect(!g_stats_on, 1))
+      return real_hsa_signal_wait_scacquire(signal, condition, compare_value, timeout_hint, wait_state_hint);
+    const uint64_t t0 = now_ns();
+    hsa_signal_value_t v =
+        real_hsa_signal_wait_scacquire(signal, condition, compare_value, timeout_hint, wait_state_hint);
+    const bool blocked = wait_state_hint == HSA_WAIT_STATE_BLOCKED;
+    (blocked ? g_sync_waits : g_sync_active).fetch_add(1, std::memory_order_relaxed);
+    (blocked ? g_sync_wait_ns : g_sync_active_ns).fetch_add(now_ns() - t0, std::memory_order_relaxed);
+    return v;
+  }
+  VGPU_REAL_HSA(hsa_signal_load_scacquire);
+  if (!real_hsa_signal_load_scacquire)
+    return real_hsa_signal_wait_scacquire(signal, condition, compare_value, timeout_hint, wait_state_hint);
+  const uint64_t t0 = now_ns();
+  hsa_signal_value_t v = real_hsa_signal_load_scacquire(signal);
+  uint64_t wakeups = 0;
+  while (!satisfied(condition, v, compare_value)) {
+    const uint64_t el = now_ns() - t0;
+    if (el >= timeout_hint) break;
+    const uint64_t sl = std::min<uint64_t>(std::max<uint64_t>(el / 8, 20'000), 500'000);
+    struct timespec ts = {0, (long)std::min<uint64_t>(sl, timeout_hint - el)};
+    nanosleep(&ts, nullptr);
+    wakeups++;
+    v = real_hsa_signal_load_scacquire(signal);
+  }
+  if (__builtin_expect(g_stats_on, 0)) {
+    g_sync_waits.fetch_add(1, std::memory_order_relaxed);
+    g_sync_polled.fetch_add(1, std::memory_order_relaxed);
+    g_sync_wait_ns.fetch_add(now_ns() - t0, std::memory_order_relaxed);
+    g_sync_wakeups.fetch_add(wakeups, std::memory_order_relaxed);
+  }
+  return v;
+}
+
+}  // extern "C"

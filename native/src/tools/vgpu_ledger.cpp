@@ -5,8 +5,13 @@
 // vGPU container has on the board, and integrates each process's processor-sharing
 // charge from that one snapshot into <board>/ledger.<gpu_id> (root-owned, 0644: the
 // containers mount the directory read-only). GPUs without limited containers cost
-// nothing; the period stretches when the node-wide reads per base period exceed the
-// read budget, as the containers' own samplers do (ratelimit.h sample_period_ns).
+// nothing.
+//
+// One sampling thread per GPU: an occupancy read costs the GPU it walks, not the node, so
+// each GPU's period is its own - it stretches only when that GPU's reads per base period
+// exceed the read budget (ratelimit.h sample_period_ns), never because other GPUs of the
+// node are busy too. An 8-GPU node at split 16 (128 processes) keeps the 1 ms period on every
+// GPU (tests/test_multigpu.py); a single loop over every GPU would stretch it to 4 ms.
 //
 //   vgpu-ledger --dir <board dir> [--period-us 1000] [--read-budget 32] [--samples N] [--gpu ID]...
 //
@@ -21,12 +26,16 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "vgpu/board.h"
@@ -48,10 +57,15 @@ constexpr uint64_t kForgetNs = 2'000'000'000ull;
 struct Gpu {
   uint32_t gpu_id = 0;
   LedgerFile* f = nullptr;
-  std::vector<int> pids;
+  std::vector<int> pids;               // sampling thread's copy
   std::map<int, int64_t> prev_ppm;    // share at the previous sample, parts per million
   std::map<int, uint64_t> gone_since;  // entry PIDs no longer on the GPU
   uint64_t last_ns = 0;
+  // Shared with the board thread: the GPU's current processes, and the stop request.
+  std::mutex mu;
+  std::vector<int> next_pids;
+  std::atomic<bool> stop{false};
+  std::thread th;
 };
 
 LedgerFile* create_ledger(const std::string& dir, uint32_t gpu_id) {
@@ -160,6 +174,23 @@ const char* arg_str(int argc, char** argv, const char* name) {
   return nullptr;
 }
 
+// One GPU's sampling loop (its own period and read budget).
+void gpu_loop(Gpu* g, int64_t base_ns, int budget, long max_samples) {
+  long rounds = 0;
+  while (!g_stop && !g->stop.load(std::memory_order_relaxed)) {
+    {
+      std::lock_guard<std::mutex> l(g->mu);
+      g->pids = g->next_pids;
+    }
+    const int64_t reads = sample(*g, now_ns());
+    const int64_t period = sample_period_ns(base_ns, reads, budget, std::max<int64_t>(10'000'000, base_ns));
+    g->f->period_ns.store((uint64_t)period, std::memory_order_relaxed);
+    if (max_samples && ++rounds >= max_samples) break;
+    struct timespec ts = {(time_t)(period / 1000000000), (long)(period % 1000000000)};
+    nanosleep(&ts, nullptr);
+  }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -171,7 +202,7 @@ int main(int argc, char** argv) {
   }
   const int64_t base_ns = std::max(100L, arg_long(argc, argv, "--period-us", 1000)) * 1000;
   const int budget = (int)arg_long(argc, argv, "--read-budget", 32);
-  const long max_samples = arg_long(argc, argv, "--samples", 0);  // tests: stop after N rounds
+  const long max_samples = arg_long(argc, argv, "--samples", 0);  // tests: each GPU stops after N rounds
   if (const char* k = getenv("VGPU_KFD_ROOT")) g_kfd_proc_root = k;
   prctl(PR_SET_PDEATHSIG, SIGTERM);
   const pid_t parent = getppid();
@@ -183,47 +214,57 @@ int main(int argc, char** argv) {
     if (!strcmp(argv[i], "--gpu")) always.insert((uint32_t)strtoul(argv[i + 1], nullptr, 10));
   Board board;
   board.open_readonly(dir);
-  std::map<uint32_t, Gpu> gpus;
-  uint64_t next_refresh = 0;
-  long rounds = 0;
+  std::map<uint32_t, std::unique_ptr<Gpu>> gpus;
+  auto retire = [](std::unique_ptr<Gpu>& g) {
+    g->stop.store(true);
+    if (g->th.joinable()) g->th.join();
+    munmap(g->f, sizeof(LedgerFile));
+  };
+  // The board thread (this one): which GPUs hold limited containers, and their processes.
   while (!g_stop && getppid() == parent) {
     const uint64_t now = now_ns();
-    if (now >= next_refresh) {
-      next_refresh = now + 100'000'000ull;
-      std::set<uint32_t> active = always;
-      for (const BoardPeer& p : board.refresh(now))
-        for (uint32_t id : p.gpu_ids)
-          if (id) active.insert(id);
-      for (uint32_t id : active) {
-        Gpu& g = gpus[id];
-        if (!g.f) {
-          g.gpu_id = id;
-          g.f = create_ledger(dir, id);
-          if (!g.f) {
-            fprintf(stderr, "vgpu-ledger: cannot create %s\n", ledger_path(dir, id).c_str());
-            gpus.erase(id);
-            continue;
-          }
+    std::set<uint32_t> active = always;
+    for (const BoardPeer& p : board.refresh(now))
+      for (uint32_t id : p.gpu_ids)
+        if (id) active.insert(id);
+    for (uint32_t id : active) {
+      std::unique_ptr<Gpu>& g = gpus[id];
+      if (!g) {
+        g.reset(new Gpu());
+        g->gpu_id = id;
+        g->f = create_ledger(dir, id);
+        if (!g->f) {
+          fprintf(stderr, "vgpu-ledger: cannot create %s\n", ledger_path(dir, id).c_str());
+          gpus.erase(id);
+          continue;
         }
-        g.pids = kfd_pids_on_gpu(id);
+        g->next_pids = kfd_pids_on_gpu(id);
+        g->th = std::thread(gpu_loop, g.get(), base_ns, budget, max_samples);
+        continue;
       }
-      // A GPU no container holds any more is no longer sampled (its ledger goes stale).
-      for (auto it = gpus.begin(); it != gpus.end();) {
-        if (active.count(it->first)) {
-          ++it;
-        } else {
-          munmap(it->second.f, sizeof(LedgerFile));
-          it = gpus.erase(it);
-        }
+      std::vector<int> pids = kfd_pids_on_gpu(id);
+      std::lock_guard<std::mutex> l(g->mu);
+      g->next_pids.swap(pids);
+    }
+    // A GPU no container holds any more is no longer sampled (its ledger goes stale).
+    for (auto it = gpus.begin(); it != gpus.end();) {
+      if (active.count(it->first)) {
+        ++it;
+      } else {
+        retire(it->second);
+        it = gpus.erase(it);
       }
     }
-    int64_t reads = 0;
-    for (auto& kv : gpus) reads += sample(kv.second, now_ns());
-    const int64_t period = sample_period_ns(base_ns, reads, budget, std::max<int64_t>(10'000'000, base_ns));
-    for (auto& kv : gpus) kv.second.f->period_ns.store((uint64_t)period, std::memory_order_relaxed);
-    if (max_samples && ++rounds >= max_samples) break;
-    struct timespec ts = {(time_t)(period / 1000000000), (long)(period % 1000000000)};
+    if (max_samples) {  // tests: done once every GPU thread has taken its samples
+      bool all_done = !gpus.empty();
+      for (auto& kv : gpus)
+        all_done = all_done && kv.second->f->samples.load(std::memory_order_relaxed) >= (uint64_t)max_samples;
+      if (all_done) break;
+    }
+    struct timespec ts = {0, 100'000'000};
     nanosleep(&ts, nullptr);
   }
+  g_stop = 1;
+  for (auto& kv : gpus) retire(kv.second);
   return 0;
 }

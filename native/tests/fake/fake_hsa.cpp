@@ -31,6 +31,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -328,11 +329,14 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
 }
 hsa_status_t hsa_amd_memory_pool_free(void* ptr) { return pool_free_impl(ptr); }
 
-// Legacy region API: the GPU's region handle is its pool handle (as in ROCr).
+// Legacy region API: the GPU's region handle is its pool handle (as in ROCr), and a GPU agent
+// also lists the system memory regions it can reach - the CPU pool (ROCr's VisitRegion).
 hsa_status_t hsa_agent_iterate_regions(hsa_agent_t agent, hsa_status_t (*cb)(hsa_region_t, void*), void* data) {
   int d = gpu_of(agent);
   if (agent.handle == kCpuAgent) return cb(hsa_region_t{kCpuPool}, data);
   if (d < 0) return HSA_STATUS_ERROR_INVALID_AGENT;
+  hsa_status_t r = cb(hsa_region_t{kCpuPool}, data);
+  if (r != HSA_STATUS_SUCCESS) return r;
   return cb(hsa_region_t{kGpuPoolBase + (uint64_t)d}, data);
 }
 hsa_status_t hsa_region_get_info(hsa_region_t region, hsa_region_info_t attr, void* value) {
@@ -483,9 +487,25 @@ hsa_status_t hsa_signal_destroy(hsa_signal_t sig) {
   delete reinterpret_cast<std::atomic<int64_t>*>(sig.handle);
   return HSA_STATUS_SUCCESS;
 }
-hsa_signal_value_t hsa_signal_wait_scacquire(hsa_signal_t sig, hsa_signal_condition_t, hsa_signal_value_t, uint64_t,
-                                             hsa_wait_state_t) {
+// A wait spins until the condition holds or the timeout passes (as ROCr's busy wait does).
+hsa_signal_value_t hsa_signal_wait_scacquire(hsa_signal_t sig, hsa_signal_condition_t cond, hsa_signal_value_t cmp,
+                                             uint64_t timeout, hsa_wait_state_t) {
+  auto* a = reinterpret_cast<std::atomic<int64_t>*>(sig.handle);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const int64_t v = a->load();
+    const bool ok = cond == HSA_SIGNAL_CONDITION_EQ ? v == cmp : cond == HSA_SIGNAL_CONDITION_NE ? v != cmp
+                    : cond == HSA_SIGNAL_CONDITION_LT ? v < cmp : v >= cmp;
+    if (ok || (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                      .count() >= timeout)
+      return v;
+  }
+}
+hsa_signal_value_t hsa_signal_load_scacquire(hsa_signal_t sig) {
   return reinterpret_cast<std::atomic<int64_t>*>(sig.handle)->load();
+}
+void hsa_signal_subtract_screlease(hsa_signal_t sig, hsa_signal_value_t v) {
+  reinterpret_cast<std::atomic<int64_t>*>(sig.handle)->fetch_sub(v);
 }
 void hsa_signal_store_relaxed(hsa_signal_t sig, hsa_signal_value_t v) {
   reinterpret_cast<std::atomic<int64_t>*>(sig.handle)->store(v);
@@ -594,6 +614,12 @@ int fake_rocr_svm_has_access(const void* ptr, uint64_t agent) {
   std::lock_guard<std::mutex> g(st().mu);
   auto it = st().svm.find(reinterpret_cast<uintptr_t>(ptr));
   return it != st().svm.end() && it->second.access.count(agent) ? 1 : 0;
+}
+
+// KFD's MMU notifier: ranges the application unmapped are dropped (with their VRAM) now.
+void fake_rocr_svm_gc() {
+  std::lock_guard<std::mutex> g(st().mu);
+  svm_gc();
 }
 
 // Where the SVM range at `ptr` lives: the GPU ordinal, -1 = host memory, -2 = not a range.

@@ -57,6 +57,8 @@
 //                    hsaunlock unlocks (and frees) the last one
 //   hostusage        the container's pinned host memory: {"hostusage": bytes}
 //   hsamemfree       hsa_memory_free of the most recent allocation: {"hsamemfree": status}
+//   waitsig=MS       a blocking hsa_signal_wait_scacquire on a signal another thread completes
+//                    after MS ms: {"waitsig": wall ms, "cpu_ms": the waiting thread's CPU ms}
 //   usage            the current device's charged bytes: {"usage": bytes}
 //   svmmap=SIZE      mmap SIZE bytes of ordinary memory and give the current device access
 //                    (SVM attributes, no placement): {"svmmap": status}
@@ -72,6 +74,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <sys/mman.h>
+#include <time.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -96,6 +99,7 @@ int fake_hip_device_cus(int dev);
 const char* fake_hip_last_call();
 int fake_rocr_svm_location(const void* ptr);
 int fake_rocr_svm_has_access(const void* ptr, uint64_t agent);
+void fake_rocr_svm_gc();
 }
 
 namespace {
@@ -413,6 +417,26 @@ int main(int argc, char** argv) {
         registered.pop_back();
       }
       printf("{\"hostunregister\": true}\n");
+    } else if (key == "waitsig") {
+      // A blocking ROCr wait on a signal another thread completes after MS milliseconds (a
+      // kernel finishing): {"waitsig": wall ms, "cpu_ms": this thread's CPU time in the wait}
+      const int ms = atoi(val.c_str());
+      hsa_signal_t sig;
+      hsa_signal_create(1, 0, nullptr, &sig);
+      std::thread done([&] {
+        std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+        hsa_signal_store_relaxed(sig, 0);
+      });
+      struct timespec c0, c1;
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c0);
+      const double t0 = now_s();
+      hsa_signal_value_t v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+      const double wall = now_s() - t0;
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c1);
+      done.join();
+      hsa_signal_destroy(sig);
+      printf("{\"waitsig\": %.3f, \"cpu_ms\": %.3f, \"value\": %ld}\n", wall * 1e3,
+             (c1.tv_sec - c0.tv_sec) * 1e3 + (c1.tv_nsec - c0.tv_nsec) / 1e6, (long)v);
     } else if (key == "hsamemfree") {
       // the most recent device allocation, freed through ROCr's legacy entry point
       int st = -1;
@@ -488,6 +512,7 @@ int main(int argc, char** argv) {
     } else if (key == "svmunmap") {
       if (!svm_ranges.empty()) {
         munmap(svm_ranges.back().first, svm_ranges.back().second);
+        fake_rocr_svm_gc();  // the driver drops the range at once (MMU notifier)
         svm_ranges.pop_back();
       }
       printf("{\"svmunmap\": true}\n");

@@ -97,8 +97,10 @@ emit(rc3=rc3)
     assert res[0]["rc1"] == 0 and res[0]["rc2"] == 2  # hipErrorOutOfMemory
     assert res[0]["torch_pinned"] is False             # 600 + 512 MiB > 1 GiB
     assert res[1]["rc3"] == 0                          # the free returned the budget
-    assert host["limit"] == GiB and host["used"] == 600 * MiB, host
-    assert per_proc == [600 * MiB]
+    # charged where ROCr pins memory: the 600 MiB, plus whatever the runtime pinned for its
+    # own staging buffers (pinned RAM all the same)
+    assert host["limit"] == GiB and 600 * MiB <= host["used"] < 728 * MiB, host
+    assert len(per_proc) == 1 and per_proc[0] == host["used"], (per_proc, host)
 
 
 def test_unlimited_pinned_memory_is_tracked(tmp_region):

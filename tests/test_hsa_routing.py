@@ -86,7 +86,9 @@ hsa.hsa_iterate_agents(agent_cb, None)
 hsa.hsa_amd_agent_iterate_memory_pools(c_uint64(gpus[0]), pool_cb, None)
 hsa.hsa_agent_iterate_regions(c_uint64(gpus[0]), region_cb, None)
 pool = c_uint64(pools[0])
-region = c_uint64(regions[0])
+# the GPU's own memory: a GPU agent's region list also names the system regions it can reach
+# (ROCr); in ROCr a region and the pool of the same memory share one handle
+region = c_uint64([g for g in regions if g in pools][0])
 MiB = 1 << 20
 quota = int(os.environ["QUOTA_MIB"]) * MiB
 allocs = []

@@ -20,11 +20,12 @@ OOR = 0x1008        # HSA_STATUS_ERROR_OUT_OF_RESOURCES
 HIP_OOM = 2         # hipErrorOutOfMemory
 
 
-@pytest.fixture
-def svm_fake(fake):
-    """The fake as MI355X's KFD behaves (profiles/r4b): SVM pages in HBM are not in vram_<id>."""
+@pytest.fixture(params=["1", "0"], ids=["kfd-counts-svm", "kfd-blind-to-svm"])
+def svm_fake(fake, request):
+    """The fake as MI355X's KFD behaves - migrated SVM pages are in vram_<id> (profiles/r5b) -
+    and as a driver that does not count them."""
     def env(**kw):
-        kw.setdefault("FAKE_SVM_KFD_VRAM", "0")
+        kw.setdefault("FAKE_SVM_KFD_VRAM", request.param)
         return fake(**kw)
     env.region = fake.region
     env.kfd = fake.kfd
@@ -123,9 +124,12 @@ def test_hip_pinned_memory_is_charged_once(fake):
     """hipHostMalloc and hipHostRegister reach ROCr's pool allocation and memory lock: each is
     charged exactly once (not again at the HIP layer), and hipFree of pinned memory releases it."""
     e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
-    out = run(e, "hostmalloc=24m", "hostusage", "hostregister=8m", "hostusage", "hostfree_hipfree", "hostusage",
-              "hostunregister", "hostusage")
+    out = run(e, "hostmalloc=24m", "hostusage", "usage", "hostregister=8m", "hostusage", "hostfree_hipfree",
+              "hostusage", "hostunregister", "hostusage")
     assert _vals(out, "hostusage") == [24 * MiB, 32 * MiB, 8 * MiB, 0], out
+    # host memory, not the device's: a GPU agent's region list names the system regions too
+    # (ROCr), and they must not count as the GPU's (measured on MI355X, profiles/r5b)
+    assert _vals(out, "usage") == [0], out
 
 
 def test_pinned_spill_freed_through_hsa_memory_free(fake):
@@ -139,3 +143,21 @@ def test_pinned_spill_freed_through_hsa_memory_free(fake):
     assert _vals(out, "spilled") == [32 * MiB, 0], out
     assert _vals(out, "hostusage") == [32 * MiB, 0], out
     assert _vals(out, "usage") == [48 * MiB], out
+
+
+@pytest.mark.parametrize("mode,cpu_bound", [("poll", 0.25), ("native", None)])
+def test_blocking_wait_polls_instead_of_spinning(fake, mode, cpu_bound):
+    """A blocking ROCr wait (every hipDeviceSynchronize / hipStreamSynchronize /
+    hipEventSynchronize ends in one) spins a CPU in the runtime; VGPU_SYNC_WAIT=poll - what a
+    crowded GPU gets by default - turns it into acquire-loads and growing sleeps: the wait
+    still returns once the signal completes (within ~12 % + 0.5 ms), on a fraction of a CPU."""
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g", VGPU_SYNC_WAIT=mode)
+    out = run(e, "waitsig=200", "waitsig=5")
+    long, short = [o for o in out if "waitsig" in o]
+    assert long["value"] == 0 and short["value"] == 0
+    assert 199 <= long["waitsig"], long
+    if cpu_bound is not None:
+        assert long["waitsig"] <= 200 * 1.15 + 1.5 and short["waitsig"] <= 5 * 1.15 + 1.5, (long, short)
+        assert long["cpu_ms"] <= cpu_bound * long["waitsig"], long
+    else:
+        assert long["cpu_ms"] >= 0.4 * long["waitsig"], long   # the runtime's spin (the fake spins too)

@@ -96,6 +96,9 @@ def main():
                 cleanup_region(c)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         print(mode, a.sync, " ".join(a.extra_env), line[-1] if line else out.stderr[-2000:], flush=True)
+        for l in out.stderr.splitlines():   # VGPU_STATS=1: the shim's per-process counters
+            if l.startswith("[vGPU stats"):
+                print("   ", l, flush=True)
         if out.returncode != 0:
             raise SystemExit(out.returncode)
 
