@@ -2,8 +2,9 @@
 items 1-3): each is held to the container's limits by the preloaded shim.
 
 * SVM residency: ordinary memory registered with ``hsa_amd_svm_attributes_set`` and moved into
-  HBM with ``hsa_amd_svm_prefetch_async`` - KFD's vram counter and ROCr's free memory do not
-  show it (profiles/r4b), so only the hook can hold it to the quota
+  HBM with ``hsa_amd_svm_prefetch_async`` passes no allocation entry point and ROCr's free
+  memory does not show it (profiles/r4b); KFD's per-process counter does (profiles/r5b), so the
+  OOM killer would act after the fact - the hook refuses it up front
   (native/src/shim/svm_hooks.cpp; reference: cuMemAllocManaged is accounted, [memory.c:216-223]).
 * Pinned host memory through ROCr (a CPU-pool allocation, a memory lock) is held to
   VGPU_HOST_MEMORY_LIMIT (host_hooks.cpp; reference class (b)).
