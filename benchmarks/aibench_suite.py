@@ -26,7 +26,8 @@ Statistics: --repeats R runs of native / vgpu / vgpu-cu50 in alternating (ABBA) 
 per case the overhead is the median over repeats of the paired ms/batch ratio, with a
 95 % confidence interval (t-interval on the paired log-ratios).
 
-    python benchmarks/aibench_suite.py [--cases all] [--repeats 5] [--steps 10] [--json-out F] [--md-out F]
+    python benchmarks/aibench_suite.py [--cases all] [--repeats 5] [--steps 10 | --window SECONDS]
+                                       [--json-out F] [--md-out F]
 """
 import argparse
 import json
@@ -110,6 +111,9 @@ def _cmd(cases, steps, warmup, out, extra=()):
             "--warmup", str(warmup), "--out", out, "--autotune", str(AUTOTUNE), *extra]
 
 
+WINDOW = 0.0  # --window: each case timed over this many seconds instead of --steps
+
+
 def run_mode(mode, node, uuid, cases, steps, warmup):
     from amdvgpu.shim.launcher import apply_contract
     fd, out = tempfile.mkstemp(suffix=".json")
@@ -122,7 +126,8 @@ def run_mode(mode, node, uuid, cases, steps, warmup):
         env = apply_contract(envs, mounts)
     print(f"[{mode}]", flush=True)
     try:
-        if subprocess.call(_cmd(cases, steps, warmup, out), env=env):
+        extra = ["--seconds", str(WINDOW)] if WINDOW else []
+        if subprocess.call(_cmd(cases, steps, warmup, out, extra), env=env):
             raise SystemExit(f"{mode} worker failed")
         return json.load(open(out))
     finally:
@@ -229,6 +234,8 @@ def main():
     ap.add_argument("--repeats", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--window", type=float, default=0.0,
+                    help="time each case over this many seconds (every 4th step synchronised) instead of --steps")
     ap.add_argument("--vdm", type=int, default=1, help="also run the two-pod virtual-device-memory column")
     ap.add_argument("--vdm-seconds", type=float, default=3.0)
     ap.add_argument("--worker", action="store_true")
@@ -245,8 +252,9 @@ def main():
     ap.add_argument("--autotune", type=int, default=1,
                     help="MIOpen find mode (cudnn.benchmark); 0 = deterministic heuristic solver choice")
     a = ap.parse_args()
-    global AUTOTUNE
+    global AUTOTUNE, WINDOW
     AUTOTUNE = a.autotune
+    WINDOW = a.window
     from amdvgpu.models.aibench import CASES
     cases = [c.name for c in CASES] if a.cases == "all" else a.cases.split(",")
     if a.worker:

@@ -53,7 +53,8 @@ enum class SpillPolicy : int {
 
 // What backs a spilled allocation (VGPU_SPILL_BACKING).
 enum class SpillBacking : int {
-  kAuto = 0,    // a migratable SVM range when the driver supports it, else pinned host memory
+  kAuto = 0,    // large allocations (>= VGPU_SPILL_LARGE): a migratable SVM range when the driver
+                // supports it; smaller ones: pinned host memory (exportable over IPC), else SVM
   kSvm = 1,     // KFD shared virtual memory: pageable host RAM mapped into the GPU in place,
                 // migrated into HBM (same address) when the tenant's HBM share frees up
   kPinned = 2,  // a pinned host-pool allocation (never moves)

@@ -310,7 +310,12 @@ hsa_status_t spill_allocate(int dev, size_t size, void** ptr) {
     return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   }
   hsa_status_t st = HSA_STATUS_ERROR_OUT_OF_RESOURCES;
-  const bool want_svm = cfg.spill_backing != SpillBacking::kPinned && s.agents[dev].cpu_agent.handle;
+  // auto: an allocation below VGPU_SPILL_LARGE is pinned host memory - a ROCr allocation, so
+  // it can still be exported to another process (hipIpcGetMemHandle: PyTorch's CUDA tensor
+  // sharing, RCCL's transport buffers), which an SVM range cannot; large ones (datasets,
+  // caches) are SVM ranges, promotable into HBM later (tests/test_gpu_spill_ipc.py).
+  const bool small = cfg.spill_backing == SpillBacking::kAuto && size < cfg.spill_large_bytes;
+  const bool want_svm = cfg.spill_backing != SpillBacking::kPinned && !small && s.agents[dev].cpu_agent.handle;
   if (want_svm && svm_supported()) {
     size_t mapped = 0;
     st = svm_map(dev, size, ptr, &mapped);
@@ -329,6 +334,20 @@ hsa_status_t spill_allocate(int dev, size_t size, void** ptr) {
               cfg.spill_backing == SpillBacking::kSvm ? "" : "; using pinned host memory");
   }
   if (cfg.spill_backing != SpillBacking::kSvm) st = pinned_spill(dev, size, ptr);
+  if (st != HSA_STATUS_SUCCESS && small && s.agents[dev].cpu_agent.handle && svm_supported()) {
+    size_t mapped = 0;  // no pinned memory left for a small one: an SVM range still serves it
+    st = svm_map(dev, size, ptr, &mapped);
+    if (st == HSA_STATUS_SUCCESS) {
+      s.region.uncharge(s.slot, dev, size, kMemData);
+      s.region.force_charge(s.slot, dev, size, kMemSpill);
+      {
+        std::lock_guard<std::mutex> g(s.alloc_mu);
+        s.svm[reinterpret_cast<uintptr_t>(*ptr)] = SvmRec{size, mapped, dev, false, g_seq.fetch_add(1), 0};
+      }
+      start_migrator();
+      return st;
+    }
+  }
   if (st != HSA_STATUS_SUCCESS) {
     s.region.uncharge_host(s.slot, size);
     return st;

@@ -198,6 +198,21 @@ hipError_t hipFree(void* ptr) {
   return hsa_amd_memory_pool_free(ptr) == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorInvalidValue;
 }
 
+void fake_hip_record(const char* name);
+
+// CLR exports a buffer through ROCr's IPC (hsa_amd_ipc_memory_create), which fails for memory
+// that is no ROCr allocation.
+hipError_t hipIpcGetMemHandle(hipIpcMemHandle_t* handle, void* ptr) {
+  init();
+  fake_hip_record("hipIpcGetMemHandle");
+  if (!handle || !ptr) return hipErrorInvalidValue;
+  hsa_amd_ipc_memory_t h;
+  if (hsa_amd_ipc_memory_create(ptr, 0, &h) != HSA_STATUS_SUCCESS) return hipErrorInvalidDevicePointer;
+  memset(handle, 0, sizeof(*handle));
+  memcpy(handle, &h, sizeof(h) < sizeof(*handle) ? sizeof(h) : sizeof(*handle));
+  return hipSuccess;
+}
+
 hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
   init();
   uint64_t avail = 0;
@@ -235,7 +250,6 @@ hipError_t hipStreamDestroy(hipStream_t stream) {
   return hipSuccess;
 }
 
-void fake_hip_record(const char* name);
 
 hipError_t hipLaunchKernel(const void* function_address, dim3, dim3, void**, size_t, hipStream_t stream) {
   init();

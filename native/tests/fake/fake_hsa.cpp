@@ -459,6 +459,20 @@ hsa_status_t hsa_amd_vmem_handle_release(hsa_amd_vmem_alloc_handle_t handle) {
   return pool_free_impl(reinterpret_cast<void*>(handle.handle));
 }
 
+// IPC export works on ROCr allocations only (a pool allocation, device or system memory):
+// ordinary memory registered as an SVM range is no KFD buffer object ROCr could share.
+// len 0 = the whole allocation (the fake HIP's hipIpcGetMemHandle does not know the size).
+hsa_status_t hsa_amd_ipc_memory_create(void* ptr, size_t len, hsa_amd_ipc_memory_t* handle) {
+  std::lock_guard<std::mutex> g(st().mu);
+  auto it = st().allocs.find(reinterpret_cast<uintptr_t>(ptr));
+  if (it == st().allocs.end() || (len && len != it->second.second)) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  if (handle) {
+    memset(handle, 0, sizeof(*handle));
+    memcpy(handle, &it->first, sizeof(it->first));
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
 hsa_status_t hsa_amd_ipc_memory_attach(const hsa_amd_ipc_memory_t*, size_t len, uint32_t, const hsa_agent_t*,
                                        void** mapped_ptr) {
   std::lock_guard<std::mutex> g(st().mu);

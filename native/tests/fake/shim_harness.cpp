@@ -68,6 +68,7 @@
 //   hipprefetch=D / hipadvise=D  hipMemPrefetchAsync / hipMemAdvise(SetPreferredLocation) of
 //                    the last range: {"hipprefetch": rc} / {"hipadvise": rc}
 //   svmunmap         munmap of the last range: {"svmunmap": true}
+//   ipcexport        hipIpcGetMemHandle of the most recent allocation: {"ipcexport": rc}
 #define __HIP_PLATFORM_AMD__ 1
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
@@ -478,6 +479,10 @@ int main(int argc, char** argv) {
       printf("{\"hostusage\": %llu}\n", api_u64("vgpu_get_host_memory_usage"));
     } else if (key == "usage") {
       printf("{\"usage\": %llu}\n", api_u64("vgpu_get_current_device_memory_usage"));
+    } else if (key == "ipcexport") {
+      hipIpcMemHandle_t h;
+      int rc = ptrs.empty() ? -1 : (int)hipIpcGetMemHandle(&h, ptrs.back());
+      printf("{\"ipcexport\": %d}\n", rc);
     } else if (key == "svmmap") {
       size_t n = (size_t)parse_size(val.c_str());
       void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);

@@ -283,12 +283,17 @@ def _background_rate_next_to(neighbour_prio, tmp_path):
             time.sleep(0.05)
         time.sleep(1.0)  # on the board, busy
         rate = _spin_rates([bg], secs=3.0)[0]
+        with Region(bg["VGPU_SHARED_CACHE"]) as r:   # the limiter's side, for a failure's message
+            d = r.device(0)
+            diag = {"samples": r.samples, "other_refreshes": r.other_refreshes, "charged_ns": d["charged_ns"],
+                    "wall_ns": d["wall_ns"], "preempt": d["preempt"], "cu_mode": d["cu_mode"],
+                    "hostpids": [p["hostpid"] for p in r.procs()]}
     finally:
         open(stop, "w").close()
         svc.communicate(timeout=120)
         cleanup_region(nb)
         cleanup_region(bg)
-    return rate
+    return rate, diag
 
 
 def test_background_class_yields_to_a_busy_latency_class(tmp_path):
@@ -298,11 +303,11 @@ def test_background_class_yields_to_a_busy_latency_class(tmp_path):
     background trainers (profiles/r3d, r3j)."""
     (tmp_path / "eq").mkdir()
     (tmp_path / "lat").mkdir()
-    equal = _background_rate_next_to(2, tmp_path / "eq")
-    behind = _background_rate_next_to(0, tmp_path / "lat")
-    print(json.dumps({"next_to_equal": equal, "next_to_latency": behind}))
+    equal, d_eq = _background_rate_next_to(2, tmp_path / "eq")
+    behind, d_lat = _background_rate_next_to(0, tmp_path / "lat")
+    print(json.dumps({"next_to_equal": equal, "next_to_latency": behind, "limiter": [d_eq, d_lat]}))
     assert equal > 0, equal
-    assert behind < 0.3 * equal, (equal, behind)
+    assert behind < 0.3 * equal, (equal, behind, d_eq, d_lat)
 
 
 IDLE_ON_BOARD = """

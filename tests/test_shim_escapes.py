@@ -75,7 +75,7 @@ def test_unmapped_svm_range_gives_its_charge_back(svm_fake):
     """KFD drops a range the process unmaps: the maintenance thread sees it in
     /proc/self/maps and releases the charge (the quota is usable again)."""
     e = svm_fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
-    out = run(e, "svmmap=768m", "svmprefetch=0", "usage", "malloc=512m", "svmunmap", "sleep=0.5", "usage",
+    out = run(e, "svmmap=768m", "svmprefetch=0", "usage", "malloc=512m", "svmunmap", "sleep=1.5", "usage",
               "malloc=512m")
     assert _vals(out, "usage") == [768 * MiB, 0], out
     assert _vals(out, "malloc") == ["oom", "ok"], out
