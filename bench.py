@@ -184,14 +184,14 @@ def worker(args):
         open(args.result_file + ".ready", "w").close()
         while not os.path.exists(args.go):
             time.sleep(0.002)
-        # How a pod waits for its GPU work. On this box every pod runs in one 16-CPU quota, and
-        # a GPU-bound pod's main thread stays busy through HIP's blocking event wait as through
-        # torch's synchronize (profiles/r4za): 16 waiting pods starve the ones that have work
-        # to launch (on a node each pod has CPUs of its own). The default, poll, keeps 3 steps
-        # in flight and sleeps between queries of the oldest step's event, so the GPU always
-        # has queued work and a waiting pod holds no CPU. VGPU_BENCH_SYNC=block: a blocking
-        # event wait every 4 steps (round 4 before r4zc); spin: torch's synchronize.
-        sync_mode = "cpu" if cpu else os.environ.get("VGPU_BENCH_SYNC", "poll")
+        # How a pod waits for its GPU work. The default, spin, is a stock tenant's: torch's
+        # synchronize every 4 steps. HIP spins a core through it (profiles/r4za); on a crowded
+        # GPU the shim turns that wait into polling with short sleeps (sync_hooks.cpp,
+        # profiles/r5c), so 16 waiting pods do not starve the ones that have work to launch.
+        # VGPU_BENCH_SYNC=poll: the harness polls itself (3 steps in flight, 0.5 ms sleeps
+        # between event queries; round 4's default); block: a blocking event wait every 4
+        # steps.
+        sync_mode = "cpu" if cpu else os.environ.get("VGPU_BENCH_SYNC", "spin")
         if sync_mode == "block":
             def wait():
                 ev = torch.cuda.Event(blocking=True)

@@ -54,9 +54,10 @@ enum class SpillPolicy : int {
 // What backs a spilled allocation (VGPU_SPILL_BACKING).
 enum class SpillBacking : int {
   kAuto = 0,    // large allocations (>= VGPU_SPILL_LARGE): a migratable SVM range when the driver
-                // supports it; smaller ones: pinned host memory (exportable over IPC), else SVM
-  kSvm = 1,     // KFD shared virtual memory: pageable host RAM mapped into the GPU in place,
-                // migrated into HBM (same address) when the tenant's HBM share frees up
+                // supports it; smaller ones: pinned host memory, else SVM
+  kSvm = 1,     // (default) KFD shared virtual memory: pageable host RAM mapped into the GPU in
+                // place, migrated into HBM (same address) when the tenant's HBM share frees up;
+                // pinned host memory where the driver has no SVM
   kPinned = 2,  // a pinned host-pool allocation (never moves)
 };
 
@@ -98,7 +99,7 @@ struct Config {
   SpillPolicy spill_policy = SpillPolicy::kLargeFirst;  // VGPU_SPILL_POLICY
   uint64_t spill_large_bytes = 256ull << 20;  // VGPU_SPILL_LARGE: "large" allocation threshold
   uint64_t spill_reserve_bytes = 0;      // VGPU_SPILL_RESERVE: HBM kept for small ones (0 = auto)
-  SpillBacking spill_backing = SpillBacking::kAuto;  // VGPU_SPILL_BACKING: auto | svm | pinned
+  SpillBacking spill_backing = SpillBacking::kSvm;  // VGPU_SPILL_BACKING: svm | auto | pinned
   bool spill_promote = true;             // VGPU_SPILL_PROMOTE: move SVM spills into HBM once they fit
   int priority = 1;                      // VGPU_TASK_PRIORITY
   CuMode cu_mode = CuMode::kAuto;        // VGPU_CU_MODE

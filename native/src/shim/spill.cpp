@@ -310,13 +310,14 @@ hsa_status_t spill_allocate(int dev, size_t size, void** ptr) {
     return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   }
   hsa_status_t st = HSA_STATUS_ERROR_OUT_OF_RESOURCES;
-  // auto: an allocation below VGPU_SPILL_LARGE is pinned host memory - a ROCr allocation, so
-  // it can still be exported to another process (hipIpcGetMemHandle: PyTorch's CUDA tensor
-  // sharing, RCCL's transport buffers), which an SVM range cannot; large ones (datasets,
-  // caches) are SVM ranges, promotable into HBM later (tests/test_gpu_spill_ipc.py).
+  // svm (default): an SVM range, promotable into HBM later; pinned host memory only where the
+  // driver has no SVM. auto: below VGPU_SPILL_LARGE pinned host memory (never moves), large
+  // ones SVM ranges. Neither placement exports over IPC on MI355X - KFD shares device memory
+  // only (tests/test_gpu_spill_ipc.py, profiles/r5e).
   const bool small = cfg.spill_backing == SpillBacking::kAuto && size < cfg.spill_large_bytes;
   const bool want_svm = cfg.spill_backing != SpillBacking::kPinned && !small && s.agents[dev].cpu_agent.handle;
-  if (want_svm && svm_supported()) {
+  const bool svm_ok = want_svm && svm_supported();
+  if (svm_ok) {
     size_t mapped = 0;
     st = svm_map(dev, size, ptr, &mapped);
     if (st == HSA_STATUS_SUCCESS) {
@@ -333,7 +334,7 @@ hsa_status_t spill_allocate(int dev, size_t size, void** ptr) {
     VLOG_WARN("device %d: SVM spill of %zu bytes refused (status %d)%s", dev, size, (int)st,
               cfg.spill_backing == SpillBacking::kSvm ? "" : "; using pinned host memory");
   }
-  if (cfg.spill_backing != SpillBacking::kSvm) st = pinned_spill(dev, size, ptr);
+  if (cfg.spill_backing != SpillBacking::kSvm || !svm_ok) st = pinned_spill(dev, size, ptr);
   if (st != HSA_STATUS_SUCCESS && small && s.agents[dev].cpu_agent.handle && svm_supported()) {
     size_t mapped = 0;  // no pinned memory left for a small one: an SVM range still serves it
     st = svm_map(dev, size, ptr, &mapped);

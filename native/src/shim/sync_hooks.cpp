@@ -8,9 +8,12 @@
 // 16 pods of one GPU hold 16 cores, 128 on an 8-GPU node. The reference's throttle sleeps
 // rather than spins (rate_limiter [multiprocess_utilization_watcher.c:53-72], nanosleep 10 ms).
 //
-// Here a blocking wait (HSA_WAIT_STATE_BLOCKED) of a process whose GPU is crowded (the
-// maintenance thread's crowd count: two or more other busy processes, watcher.cpp) becomes a
-// loop of acquire-loads and nanosleeps; the sleep grows with the time already waited (1/8 of
+// Here a blocking wait (HSA_WAIT_STATE_BLOCKED) - or an active one with a long time-out, the
+// spin-until-done wait HIP uses when it schedules waits as "spin" (its default when the host
+// has more cores than GPUs) - of a process whose GPU is crowded (the maintenance thread's
+// crowd count: two or more other busy processes, watcher.cpp) becomes a loop of
+// acquire-loads and nanosleeps; an active wait with a short time-out (HIP's brief spin before
+// it blocks) stays as it is; the sleep grows with the time already waited (1/8 of
 // it, 20 us to 500 us), so a wait overshoots its completion by at most ~12 % (and 0.5 ms),
 // and a multi-millisecond wait costs a few dozen wake-ups instead of a core. A lone pod keeps
 // ROCr's own wait (no added latency); VGPU_SYNC_WAIT=poll|native forces either way.
@@ -34,6 +37,10 @@ std::atomic<uint64_t> g_sync_active{0};     // active (spin-hinted) waits
 std::atomic<uint64_t> g_sync_active_ns{0};
 
 namespace {
+
+// An active wait longer than this is a spin-until-done wait (HIP passes an unlimited
+// time-out); shorter ones are the brief spin ahead of a blocking wait.
+constexpr uint64_t kActiveSpinNs = 1'000'000;
 
 bool satisfied(hsa_signal_condition_t c, hsa_signal_value_t v, hsa_signal_value_t cmp) {
   switch (c) {
@@ -70,7 +77,8 @@ hsa_signal_value_t hsa_signal_wait_scacquire(hsa_signal_t signal, hsa_signal_con
                                              hsa_signal_value_t compare_value, uint64_t timeout_hint,
                                              hsa_wait_state_t wait_state_hint) {
   VGPU_REAL_HSA(hsa_signal_wait_scacquire);
-  if (__builtin_expect(wait_state_hint != HSA_WAIT_STATE_BLOCKED || !poll_now(), 1)) {
+  const bool long_wait = wait_state_hint == HSA_WAIT_STATE_BLOCKED || timeout_hint > kActiveSpinNs;
+  if (__builtin_expect(!long_wait || !poll_now(), 1)) {
     if (__builtin_expect(!g_stats_on, 1))
       return real_hsa_signal_wait_scacquire(signal, condition, compare_value, timeout_hint, wait_state_hint);
     const uint64_t t0 = now_ns();

@@ -459,13 +459,15 @@ hsa_status_t hsa_amd_vmem_handle_release(hsa_amd_vmem_alloc_handle_t handle) {
   return pool_free_impl(reinterpret_cast<void*>(handle.handle));
 }
 
-// IPC export works on ROCr allocations only (a pool allocation, device or system memory):
-// ordinary memory registered as an SVM range is no KFD buffer object ROCr could share.
+// IPC export works on device memory only, as measured on MI355X (profiles/r5e): a GPU-pool
+// allocation exports; a system-pool allocation (pinned host memory) and ordinary memory
+// registered as an SVM range do not.
 // len 0 = the whole allocation (the fake HIP's hipIpcGetMemHandle does not know the size).
 hsa_status_t hsa_amd_ipc_memory_create(void* ptr, size_t len, hsa_amd_ipc_memory_t* handle) {
   std::lock_guard<std::mutex> g(st().mu);
   auto it = st().allocs.find(reinterpret_cast<uintptr_t>(ptr));
-  if (it == st().allocs.end() || (len && len != it->second.second)) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  if (it == st().allocs.end() || it->second.first < 0 || (len && len != it->second.second))
+    return HSA_STATUS_ERROR_INVALID_ARGUMENT;
   if (handle) {
     memset(handle, 0, sizeof(*handle));
     memcpy(handle, &it->first, sizeof(it->first));

@@ -58,7 +58,8 @@
 //   hostusage        the container's pinned host memory: {"hostusage": bytes}
 //   hsamemfree       hsa_memory_free of the most recent allocation: {"hsamemfree": status}
 //   waitsig=MS       a blocking hsa_signal_wait_scacquire on a signal another thread completes
-//                    after MS ms: {"waitsig": wall ms, "cpu_ms": the waiting thread's CPU ms}
+//                    after MS ms: {"waitsig": wall ms, "cpu_ms": the waiting thread's CPU ms};
+//                    waitspin=MS the same as an active (spin) wait with no time-out
 //   usage            the current device's charged bytes: {"usage": bytes}
 //   svmmap=SIZE      mmap SIZE bytes of ordinary memory and give the current device access
 //                    (SVM attributes, no placement): {"svmmap": status}
@@ -418,7 +419,7 @@ int main(int argc, char** argv) {
         registered.pop_back();
       }
       printf("{\"hostunregister\": true}\n");
-    } else if (key == "waitsig") {
+    } else if (key == "waitsig" || key == "waitspin") {
       // A blocking ROCr wait on a signal another thread completes after MS milliseconds (a
       // kernel finishing): {"waitsig": wall ms, "cpu_ms": this thread's CPU time in the wait}
       const int ms = atoi(val.c_str());
@@ -431,12 +432,13 @@ int main(int argc, char** argv) {
       struct timespec c0, c1;
       clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c0);
       const double t0 = now_s();
-      hsa_signal_value_t v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+      hsa_signal_value_t v = hsa_signal_wait_scacquire(
+          sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, key == "waitsig" ? HSA_WAIT_STATE_BLOCKED : HSA_WAIT_STATE_ACTIVE);
       const double wall = now_s() - t0;
       clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c1);
       done.join();
       hsa_signal_destroy(sig);
-      printf("{\"waitsig\": %.3f, \"cpu_ms\": %.3f, \"value\": %ld}\n", wall * 1e3,
+      printf("{\"%s\": %.3f, \"cpu_ms\": %.3f, \"value\": %ld}\n", key.c_str(), wall * 1e3,
              (c1.tv_sec - c0.tv_sec) * 1e3 + (c1.tv_nsec - c0.tv_nsec) / 1e6, (long)v);
     } else if (key == "hsamemfree") {
       // the most recent device allocation, freed through ROCr's legacy entry point

@@ -7,6 +7,6 @@ def sum_consumer(q, out):
     error that opening it raised, as a string)."""
     try:
         t = q.get(timeout=60)
-        out.put(float(t.float().sum().item()))
+        out.put(float(t.sum().item()))   # integer sum: exact
     except Exception as e:  # noqa: BLE001  (reported to the producer)
         out.put("consumer: " + repr(e)[:300])

@@ -290,9 +290,14 @@ def _background_rate_next_to(neighbour_prio, tmp_path):
                     "hostpids": [p["hostpid"] for p in r.procs()]}
     finally:
         open(stop, "w").close()
-        svc.communicate(timeout=120)
+        _, svc_err = svc.communicate(timeout=120)
         cleanup_region(nb)
         cleanup_region(bg)
+    # the neighbour kept the GPU busy throughout (a neighbour that died early - killed, say -
+    # leaves the background tenant alone at its 50 %)
+    diag["neighbour_rc"] = svc.returncode
+    if svc.returncode != 0:
+        diag["neighbour_err"] = svc_err[-1500:]
     return rate, diag
 
 

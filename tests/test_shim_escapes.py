@@ -75,9 +75,11 @@ def test_unmapped_svm_range_gives_its_charge_back(svm_fake):
     """KFD drops a range the process unmaps: the maintenance thread sees it in
     /proc/self/maps and releases the charge (the quota is usable again)."""
     e = svm_fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g")
-    out = run(e, "svmmap=768m", "svmprefetch=0", "usage", "malloc=512m", "svmunmap", "sleep=1.5", "usage",
-              "malloc=512m")
-    assert _vals(out, "usage") == [768 * MiB, 0], out
+    # (usage is read after the context re-sync has run: the runtime's own footprint is in it)
+    out = run(e, "sleep=1.2", "usage", "svmmap=768m", "svmprefetch=0", "usage", "malloc=512m", "svmunmap",
+              "sleep=1.5", "usage", "malloc=400m")
+    base, moved, after = _vals(out, "usage")
+    assert moved - base == 768 * MiB and after == base, out
     assert _vals(out, "malloc") == ["oom", "ok"], out
 
 
@@ -148,16 +150,21 @@ def test_pinned_spill_freed_through_hsa_memory_free(fake):
 @pytest.mark.parametrize("mode,cpu_bound", [("poll", 0.25), ("native", None)])
 def test_blocking_wait_polls_instead_of_spinning(fake, mode, cpu_bound):
     """A blocking ROCr wait (every hipDeviceSynchronize / hipStreamSynchronize /
-    hipEventSynchronize ends in one) spins a CPU in the runtime; VGPU_SYNC_WAIT=poll - what a
+    hipEventSynchronize ends in one, or in an active wait without time-out) spins a CPU in
+    the runtime; VGPU_SYNC_WAIT=poll - what a
     crowded GPU gets by default - turns it into acquire-loads and growing sleeps: the wait
     still returns once the signal completes (within ~12 % + 0.5 ms), on a fraction of a CPU."""
     e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g", VGPU_SYNC_WAIT=mode)
-    out = run(e, "waitsig=200", "waitsig=5")
+    out = run(e, "waitsig=200", "waitsig=5", "waitspin=200")
     long, short = [o for o in out if "waitsig" in o]
-    assert long["value"] == 0 and short["value"] == 0
-    assert 199 <= long["waitsig"], long
+    spin = [o for o in out if "waitspin" in o][0]
+    assert long["value"] == 0 and short["value"] == 0 and spin["value"] == 0
+    assert 199 <= long["waitsig"] and 199 <= spin["waitspin"], (long, spin)
     if cpu_bound is not None:
         assert long["waitsig"] <= 200 * 1.15 + 1.5 and short["waitsig"] <= 5 * 1.15 + 1.5, (long, short)
         assert long["cpu_ms"] <= cpu_bound * long["waitsig"], long
+        # HIP's spin-until-done wait (an active wait with no time-out) polls the same way
+        assert spin["waitspin"] <= 200 * 1.15 + 1.5 and spin["cpu_ms"] <= cpu_bound * spin["waitspin"], spin
     else:
         assert long["cpu_ms"] >= 0.4 * long["waitsig"], long   # the runtime's spin (the fake spins too)
+        assert spin["cpu_ms"] >= 0.4 * spin["waitspin"], spin

@@ -244,36 +244,34 @@ def test_spill_is_charged_to_the_host_budget(fake):
 
 def _svm_env(fake, **kw):
     # 64 MiB HBM share of a 256 MiB quota (reserve 16 MiB), first-come: the second buffer spills
-    # - as an SVM range (these buffers are below VGPU_SPILL_LARGE, which auto backs with pinned
-    # memory: test_small_spills_are_pinned_large_ones_svm).
-    kw.setdefault("VGPU_SPILL_BACKING", "svm")
+    # - as an SVM range (VGPU_SPILL_BACKING=svm, the default).
     return fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="256m", VGPU_DEVICE_HBM_LIMIT_0="64m",
                 VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come", VGPU_HOST_MEMORY_LIMIT="128m", **kw)
 
 
 def test_small_spills_are_pinned_large_ones_svm(fake):
-    """VGPU_SPILL_BACKING=auto (default): a spill below VGPU_SPILL_LARGE is pinned host memory
-    (a ROCr allocation, exportable over IPC); a large one is an SVM range (promotable)."""
+    """VGPU_SPILL_BACKING=auto: a spill below VGPU_SPILL_LARGE is pinned host memory (never
+    moves); a large one is an SVM range (promotable)."""
     e = fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="256m", VGPU_DEVICE_HBM_LIMIT_0="64m",
-             VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come", VGPU_SPILL_LARGE="40m")
+             VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come", VGPU_SPILL_LARGE="40m",
+             VGPU_SPILL_BACKING="auto")
     out = run(e, "malloc=60m", "malloc=32m", "where", "malloc=48m", "where", "spilled")
     assert [o["where"] for o in out if "where" in o] == [-2, -1], out   # pinned (not a range), then SVM
     assert [o["spilled"] for o in out if "spilled" in o] == [80 * MiB], out
 
 
-def test_spilled_buffers_and_ipc_export(fake):
-    """hipIpcGetMemHandle (PyTorch's CUDA tensor sharing, RCCL's transport buffers) on buffers
-    past the HBM share: the default policy's small spill is pinned memory, a ROCr allocation
-    that exports; a large (SVM) spill is no ROCr allocation and its export fails with an error
-    - not a crash - as it does with backing svm for any size. HBM-resident buffers export."""
+@pytest.mark.parametrize("backing", ["svm", "auto", "pinned"])
+def test_spilled_buffers_and_ipc_export(fake, backing):
+    """hipIpcGetMemHandle (PyTorch's CUDA tensor sharing) on buffers of an oversubscribed vGPU:
+    one in HBM exports; one past the HBM share - an SVM range or pinned host memory - does not
+    (KFD shares device memory only, as measured on MI355X: tests/test_gpu_spill_ipc.py, the
+    fake runtime mirrors it), and the export fails with an error, not a crash."""
     e = fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="256m", VGPU_DEVICE_HBM_LIMIT_0="64m",
-             VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come", VGPU_SPILL_LARGE="40m")
-    out = run(e, "malloc=60m", "ipcexport", "malloc=32m", "where", "ipcexport", "malloc=48m", "where", "ipcexport")
-    assert [o["where"] for o in out if "where" in o] == [-2, -1], out
-    assert [o["ipcexport"] == 0 for o in out if "ipcexport" in o] == [True, True, False], out
-    out = run(_svm_env(fake), "malloc=48m", "malloc=32m", "where", "ipcexport")
-    assert [o["where"] for o in out if "where" in o] == [-1], out
-    assert [o["ipcexport"] for o in out if "ipcexport" in o] != [0], out
+             VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come", VGPU_SPILL_BACKING=backing)
+    out = run(e, "malloc=40m", "ipcexport", "malloc=32m", "where", "ipcexport", "malloc=1m", "ipcexport")
+    assert [o["where"] for o in out if "where" in o] == ([-1] if backing == "svm" else [-2]), out
+    # (the 1 MiB buffer after it still fits the share: HBM, exportable)
+    assert [o["ipcexport"] == 0 for o in out if "ipcexport" in o] == [True, False, True], out
 
 
 @pytest.mark.parametrize("kfd_counts", ["1", "0"])
@@ -334,8 +332,7 @@ def test_svm_spill_waits_for_room(fake):
 def test_pinned_spill_never_moves(fake, how):
     """VGPU_SPILL_BACKING=pinned, or a driver without SVM: the spill is a pinned host-pool
     allocation (not an SVM range) and stays in host memory after room frees up."""
-    kw = {"VGPU_SPILL_BACKING": "pinned"} if how == "pinned" else {"FAKE_ROCR_NO_SVM": "1", "VGPU_SPILL_BACKING": "auto",
-                                                                  "VGPU_SPILL_LARGE": "16m"}
+    kw = {"VGPU_SPILL_BACKING": "pinned"} if how == "pinned" else {"FAKE_ROCR_NO_SVM": "1"}
     out = run(_svm_env(fake, **kw), "malloc=48m", "malloc=32m", "where", "freeidx=0", "sleep=0.5", "spilled")
     assert [o["where"] for o in out if "where" in o] == [-2]
     assert [o["spilled"] for o in out if "spilled" in o] == [32 * MiB]

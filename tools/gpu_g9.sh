@@ -1,0 +1,15 @@
+# Round-5 GPU study (profiles/r5f): the suite's noisy cases re-measured - one case, native vs
+# the quota-only vGPU, 8 ABBA repeats of a 10 s timed window each.
+#   bash tools/gpu_g9.sh <case>
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+out=gpurun_out/r5f
+mkdir -p $out
+c=$1
+timeout -k 10 1050 python -u benchmarks/aibench_suite.py --cases $c --modes native,vgpu --repeats 8 --window 10 \
+  --vdm 0 --json-out $out/$c.json --md-out $out/$c.md > $out/$c.log 2>&1
+rc=$?
+echo "suite_rc=$rc" >> $out/$c.log
+tail -6 $out/$c.log
+exit $rc

@@ -38,7 +38,60 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, REPO)
 
 
-def tenant(case, seconds, go, batch):
+def _cpu_limit():
+    """The CPUs this process may use: (affinity count, cgroup cpu.max quota in CPUs or None)."""
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return len(os.sched_getaffinity(0)), quota
+
+
+def _numa_nodes():
+    """NUMA node -> the CPUs of it this process may use."""
+    allowed = os.sched_getaffinity(0)
+    out = {}
+    for d in glob.glob("/sys/devices/system/node/node[0-9]*"):
+        try:
+            cpus = set()
+            for part in open(os.path.join(d, "cpulist")).read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                if lo:
+                    cpus.update(range(int(lo), int(hi or lo) + 1))
+            out[int(os.path.basename(d)[4:])] = sorted(cpus & allowed)
+        except (OSError, ValueError):
+            pass
+    return out
+
+
+def _gpu_node():
+    """The NUMA node of the GPU this job sees (sysfs backend), -1 if unknown."""
+    try:
+        from amdvgpu.plugin.devices import SysfsBackend
+        bdf = SysfsBackend().devices()[0].bdf
+        return int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+    except Exception:  # noqa: BLE001
+        return -1
+
+
+def _where():
+    """The CPU the calling thread ran on last, and that CPU's NUMA node."""
+    try:
+        st = open("/proc/thread-self/stat").read()
+        cpu = int(st[st.rindex(")") + 2:].split()[36])
+    except (OSError, ValueError, IndexError):
+        return -1, -1
+    node = next((n for n, cs in _numa_nodes().items() if cpu in cs), -1)
+    return cpu, node
+
+
+def tenant(case, seconds, go, batch, cpus):
+    if cpus:
+        os.sched_setaffinity(0, {int(c) for c in cpus.split(",")})
+    import resource
+
     import torch
     from amdvgpu.models.aibench import Runner, get_case
     torch.backends.cudnn.benchmark = True
@@ -49,44 +102,120 @@ def tenant(case, seconds, go, batch):
     open(go + f".ready.{os.getpid()}", "w").close()
     while not os.path.exists(go):
         time.sleep(0.001)
+    ru0, c0 = resource.getrusage(resource.RUSAGE_SELF), time.thread_time()
     n, t0 = 0, time.perf_counter()
+    seen = {}   # NUMA nodes the main thread ran on, sampled every 8 steps
     while time.perf_counter() - t0 < seconds:
         r.step()
         n += 1
         if n % 4 == 0:
             torch.cuda.synchronize()
+        if n % 8 == 0:
+            node = _where()[1]
+            seen[node] = seen.get(node, 0) + 1
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    ru1, c1 = resource.getrusage(resource.RUSAGE_SELF), time.thread_time()
+    aff, quota = _cpu_limit()
     print(json.dumps({"pid": os.getpid(), "case": case, "steps": n, "ms_per_step": round(dt * 1e3 / n, 3),
-                      "items_per_s": round(n * r.items_per_step / dt, 1)}), flush=True)
+                      "items_per_s": round(n * r.items_per_step / dt, 1),
+                      # CPU seconds per second of the window: all threads, and the main thread
+                      "cpus_busy": round((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime) / dt, 3),
+                      "main_thread_busy": round((c1 - c0) / dt, 3),
+                      "invol_ctx": ru1.ru_nivcsw - ru0.ru_nivcsw, "affinity": aff, "cgroup_cpus": quota,
+                      "cpu_last": _where()[0], "numa_seen": seen}),
+          flush=True)
+
+
+def burner(go, seconds):
+    """A CPU-only neighbour: spins one core for the window (no GPU)."""
+    while not os.path.exists(go):
+        time.sleep(0.001)
+    t0 = time.perf_counter()
+    x = 0
+    while time.perf_counter() - t0 < seconds:
+        x += 1
 
 
 def launch(a):
     go = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"cotenancy-go-{os.getpid()}")
     args = [sys.executable, os.path.abspath(__file__), "--tenant", "--case", a.case, "--seconds", str(a.seconds),
             "--go", go] + (["--batch", str(a.batch)] if a.batch else [])
+    allowed = sorted(os.sched_getaffinity(0))
+    nodes, gnode = _numa_nodes(), _gpu_node()
+    local = nodes.get(gnode, [])
+    remote = [c for n, cs in sorted(nodes.items()) if n != gnode for c in cs]
+
+    def cpus_of(i):
+        """Tenant i's CPUs: --placement local / remote = disjoint slices of the GPU's NUMA node
+        / of the other nodes; split = even tenants local, odd ones remote; none = --pin K of
+        all allowed CPUs (or unpinned)."""
+        k = max(1, a.pin or 4)
+        if a.placement == "local":
+            pool, j = local, i
+        elif a.placement == "remote":
+            pool, j = remote, i
+        elif a.placement == "split":
+            pool, j = (local if i % 2 == 0 else remote), i // 2
+        elif a.pin:
+            pool, j = allowed, i
+        else:
+            return []
+        return pool[j * k:(j + 1) * k]
+
     def cmd(i):
+        c = list(args)
+        cs = cpus_of(i)
+        if cs:
+            c += ["--cpus", ",".join(str(x) for x in cs)]
         if not a.trace:
-            return args
-        return ["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", os.path.join(a.trace, f"t{i}"),
-                "-o", f"t{i}", "--"] + args
+            return c
+        prof = ["rocprofv3", "--kernel-trace"] + (["--hip-trace", "--stats"] if a.hip_stats else [])
+        return prof + ["--output-format", "csv", "-d", os.path.join(a.trace, f"t{i}"), "-o", f"t{i}", "--"] + c
     procs = [subprocess.Popen(cmd(i), stdout=subprocess.PIPE, text=True) for i in range(a.procs)]
+    burners = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--burner", "--go", go,
+                                 "--seconds", str(a.seconds)]) for _ in range(a.burners)]
     deadline = time.time() + 600
     while len(glob.glob(go + ".ready.*")) < a.procs and time.time() < deadline:
         if any(p.poll() not in (None, 0) for p in procs):
             break
         time.sleep(0.05)
     open(go, "w").close()
+
     def result(p):   # the tenant's line (rocprofv3 prints its own lines around it)
         lines = [ln for ln in p.communicate(timeout=600)[0].splitlines() if ln.startswith('{"pid"')]
         return json.loads(lines[-1])
     outs = [result(p) for p in procs]
+    for b in burners:
+        b.wait(timeout=600)
     for f in glob.glob(go + "*"):
         os.unlink(f)
     agg = sum(o["items_per_s"] for o in outs)
-    print(json.dumps({"case": a.case, "procs": a.procs, "aggregate_items_per_s": round(agg, 1), "tenants": outs}),
-          flush=True)
+    aff, quota = _cpu_limit()
+    print(json.dumps({"case": a.case, "procs": a.procs, "burners": a.burners, "pin": a.pin,
+                      "placement": a.placement, "gpu_numa_node": gnode,
+                      "numa_cpus": {n: len(cs) for n, cs in nodes.items()},
+                      "aggregate_items_per_s": round(agg, 1), "affinity": aff, "cgroup_cpus": quota,
+                      "tenants": outs}), flush=True)
     return 0 if all(p.returncode == 0 for p in procs) else 1
+
+
+def hip_stats(d):
+    """Per tenant: the HIP API calls that took the most time (rocprofv3 --hip-trace --stats)."""
+    out = {}
+    for f in glob.glob(os.path.join(d, "**", "*hip_api_stats.csv"), recursive=True):
+        rows = []
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                try:
+                    rows.append((row["Name"], int(row["Calls"]), float(row["TotalDurationNs"]) / 1e6,
+                                 float(row["AverageNs"]) / 1e3))
+                except (KeyError, ValueError):
+                    continue
+        rows.sort(key=lambda r: -r[2])
+        out[_tenant_of_path(d, f)] = [{"api": n, "calls": c, "total_ms": round(t, 1), "avg_us": round(av, 2)}
+                                      for n, c, t, av in rows[:6]]
+    return out
 
 
 def merge(iv):
@@ -164,6 +293,9 @@ def analyze(d):
         both = iv if both is None else intersect(both, iv)
     res["both"] = round(length(both) / win, 4) if len(clipped) > 1 else None
     res["any"] = round(length(merge([x for iv in clipped.values() for x in iv])) / win, 4)
+    hs = hip_stats(d)
+    if hs:
+        res["hip_api"] = hs
     return res
 
 
@@ -177,12 +309,21 @@ def main():
     ap.add_argument("--go")
     ap.add_argument("--analyze")
     ap.add_argument("--trace", default="", help="rocprofv3 kernel trace of every tenant under this directory")
+    ap.add_argument("--hip-stats", action="store_true", help="with --trace: HIP API trace and stats too")
+    ap.add_argument("--pin", type=int, default=0, help="pin tenant i to K CPUs of its own")
+    ap.add_argument("--burners", type=int, default=0, help="CPU-only processes spinning during the window")
+    ap.add_argument("--placement", default="none", choices=["none", "local", "remote", "split"],
+                    help="pin the tenants (--pin CPUs each, default 4) to the GPU's NUMA node, the others, or both")
+    ap.add_argument("--burner", action="store_true")
+    ap.add_argument("--cpus", default="")
     a = ap.parse_args()
     if a.analyze:
         print(json.dumps(analyze(a.analyze)))
         return 0
     if a.tenant:
-        return tenant(a.case, a.seconds, a.go, a.batch)
+        return tenant(a.case, a.seconds, a.go, a.batch, a.cpus)
+    if a.burner:
+        return burner(a.go, a.seconds)
     return launch(a)
 
 
