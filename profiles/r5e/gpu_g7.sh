@@ -10,4 +10,4 @@ rc=$?
 echo "pytest rc=$rc" >> gpurun_out/g7_ipc.log
 grep -E "PASSED|FAILED|passed|failed|AssertionError" gpurun_out/g7_ipc.log
 case $rc in 0|1) ;; *) exit $rc ;; esac
-bash tools/gpu_g5.sh
+bash profiles/r5d/gpu_g5.sh

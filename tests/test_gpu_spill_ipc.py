@@ -26,7 +26,10 @@ from ipc_helpers import sum_consumer as consumer
 
 if True:
     ctx = mp.get_context("spawn")
-    a = torch.ones({resident} << 20, dtype=torch.uint8, device="cuda")      # most of the HBM share
+    torch.zeros(1, device="cuda"); torch.cuda.synchronize(); time.sleep(1.0)   # runtime footprint charged
+    d = Region(os.environ["VGPU_SHARED_CACHE"]).device(0)
+    room = d["hbm_limit"] - (d["used"] - d["spilled"])                      # what the share has left
+    a = torch.ones(room - (160 << 20), dtype=torch.uint8, device="cuda")    # most of it
     c = torch.full((32 << 20,), 3, dtype=torch.uint8, device="cuda")        # still inside it (HBM)
     c_spilled = Region(os.environ["VGPU_SHARED_CACHE"]).device(0)["spilled"]
     b = torch.full(({spill} << 20,), 2, dtype=torch.uint8, device="cuda")   # past it: spilled
@@ -116,7 +119,7 @@ def _share(tmp_region, backing, which):
     c = vgpu_env(mem_limit=8 * GiB, shared_cache=tmp_region, oversubscribe=True,
                  extra={"VGPU_DEVICE_HBM_LIMIT_0": "1024m", "VGPU_SPILL_POLICY": "first-come",
                         "VGPU_SPILL_BACKING": backing})
-    res, p = run_child(SHARE.format(resident=800, spill=200, repo=REPO, which=which), c, timeout=130, check=False)
+    res, p = run_child(SHARE.format(spill=200, repo=REPO, which=which), c, timeout=130, check=False)
     assert res, p.stderr[-3000:]
     r = res[0]
     assert r["spilled"] >= 200 * MiB, r
