@@ -16,6 +16,7 @@ ID_UUID, ID_INDEX = "uuid", "index"
 CU_MODES = ("auto", "spatial", "temporal", "both", "off")
 PLACEMENTS = ("spread", "binpack")
 DUPLICATE_POLICIES = ("reject", "merge")
+NUMA_SPREAD_MODES = ("auto", "on", "off")
 DEFAULT_RESOURCE = "amd.com/gpu"
 DEFAULT_PLUGIN_DIR = "/var/lib/kubelet/device-plugins/"
 DEFAULT_VGPU_DIR = "/usr/local/vgpu"
@@ -65,6 +66,7 @@ class PluginConfig:
     ledger: bool = True                     # run the node's GPU-time ledger daemon (vgpu-ledger; profiles/r4o)
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"  # kubelet PodResources v1
     active_oom_killer: bool = True          # the containers' memory backstop (limits file; reference ACTIVE_OOM_KILLER)
+    numa_spread: str = "auto"               # co-tenant pods of a GPU on different CPU sockets: auto | on | off
     version_requested: bool = False
     extra: dict = field(default_factory=dict)
 
@@ -91,6 +93,8 @@ class PluginConfig:
             raise ValueError(f"invalid --placement option: {self.placement}")
         if self.duplicate_vgpus not in DUPLICATE_POLICIES:
             raise ValueError(f"invalid --duplicate-vgpus option: {self.duplicate_vgpus}")
+        if self.numa_spread not in NUMA_SPREAD_MODES:
+            raise ValueError(f"invalid --numa-spread option: {self.numa_spread}")
         if not 0 <= self.gpu_concurrency <= 64:
             raise ValueError(f"invalid --gpu-concurrency option: {self.gpu_concurrency}")
         from ..utils.sizes import parse_size
@@ -193,6 +197,13 @@ _FLAGS = [
      "the containers' memory backstop: kill a container's largest process when KFD-measured VRAM stays above "
      "its quota (plus a slack); written into the plugin-owned limits file, so a tenant cannot turn it off "
      "(default true, as the reference's ACTIVE_OOM_KILLER)"),
+    ("--numa-spread", "numa_spread", str, ["NUMA_SPREAD"],
+     "run the processes of vGPU k of a GPU on the CPUs of NUMA node order[k mod n] (the GPU's own node first, "
+     "then the others): two launch-bound pods of one GPU whose threads share a CPU socket run no faster together "
+     "than one alone, on two sockets up to twice as fast (profiles/r5d). The shim narrows a container's CPU "
+     "affinity to that node when its allowed CPUs span more (VGPU_CPU_NODE; a tenant opts out with "
+     "VGPU_CPU_SPREAD=0), and ListAndWatch advertises the node as the vGPU's topology. auto (default) = on for "
+     "split > 1 on nodes with two or more CPU nodes | on | off"),
 ]
 
 

@@ -379,6 +379,11 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
                 resp.envs[f"VGPU_DEVICE_CU_RANGE_{i}"] = f"{v.cu_range[0]}-{v.cu_range[1]}"
         dmap.append(f"{i}:{v.uuid}")
     resp.envs["VGPU_DEVICE_MAP"] = " ".join(dmap)
+    nodes = [v.cpu_node for v in vdevs if getattr(v, "cpu_node", -1) >= 0]
+    if nodes:
+        # --numa-spread: the shim keeps the container's processes on this node's CPUs (the
+        # first vGPU's, for a container holding several)
+        resp.envs["VGPU_CPU_NODE"] = str(nodes[0])
     dups = duplicate_gpus(vdevs)
     if dups:
         # --duplicate-vgpus=merge: the shim merges the vGPUs of one GPU into that device

@@ -87,8 +87,21 @@ class Backend:
         """Returns a list of HealthEvent since the last call (non-blocking)."""
         return []
 
+    def cpu_numa_nodes(self):
+        """The node's NUMA nodes that have CPUs, sorted."""
+        return cpu_numa_nodes()
+
     def close(self):
         pass
+
+
+def cpu_numa_nodes(sys_root="/sys"):
+    """NUMA nodes with at least one CPU (``/sys/devices/system/node/node<n>/cpulist``)."""
+    out = []
+    for d in glob.glob(os.path.join(sys_root, "devices", "system", "node", "node[0-9]*")):
+        if _read(os.path.join(d, "cpulist"), ""):
+            out.append(int(os.path.basename(d)[4:]))
+    return sorted(out)
 
 
 # ----------------------------------------------------------------------------- sysfs
@@ -379,6 +392,9 @@ class FakeBackend(Backend):
     def devices(self):
         return [GpuDevice(**{k: v for k, v in d.__dict__.items() if k != "links"}, links=dict(d.links))
                 for d in self._devs]
+
+    def cpu_numa_nodes(self):
+        return sorted({d.numa_node for d in self._devs if d.numa_node >= 0})
 
     def inject(self, uuid, healthy, reason="injected"):
         with self._lock:

@@ -28,6 +28,7 @@ class StubKubelet:
         self.registrations = []
         self._registered = threading.Condition()
         self.devices = {}          # resource -> {id: health}
+        self.topologies = {}       # resource -> {id: [numa node, ...]}
         self._streams = {}
         self._server = None
         self.allocated = set()
@@ -91,12 +92,17 @@ class StubKubelet:
         try:
             for resp in stub.ListAndWatch(api.Empty()):
                 self.devices[resource] = {d.ID: d.health for d in resp.devices}
+                self.topologies[resource] = {d.ID: [n.ID for n in d.topology.nodes] for d in resp.devices}
         except grpc.RpcError:
             pass
 
     def stub_for(self, resource):
         reg = next(r for r in reversed(self.registrations) if r.resource_name == resource)
         return api.device_plugin_stub(self._channel(reg.endpoint))
+
+    def topology(self, resource):
+        """NUMA nodes of each advertised device (its TopologyInfo), as last listed."""
+        return dict(self.topologies.get(resource, {}))
 
     def wait_devices(self, resource, timeout=10.0, predicate=None):
         t0 = time.time()

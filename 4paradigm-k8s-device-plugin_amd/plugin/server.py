@@ -26,7 +26,7 @@ from ..parallel.topology import allocate_vdevices
 from . import api
 from .contract import (SHARED_HOST_DIR, build_container_response, build_partition_response, duplicate_gpus,
                        gc_container_files, gc_shared_dirs)
-from .vdevice import device_to_vdevices, vdevices_by_ids
+from .vdevice import assign_cpu_nodes, device_to_vdevices, vdevices_by_ids
 
 log = logging.getLogger("amdvgpu.plugin")
 
@@ -81,6 +81,12 @@ class DevicePluginServer:
                                                self.cfg.device_memory_scaling, self.cfg.device_cores_scaling)
             if self.vdev_filter is not None:
                 self.vdevices = [v for v in self.vdevices if self.vdev_filter(v)]
+            spread = getattr(self.cfg, "numa_spread", "off")
+            if spread == "on" or (spread == "auto" and self.cfg.device_split_count > 1):
+                nodes = self.backend.cpu_numa_nodes() if hasattr(self.backend, "cpu_numa_nodes") else []
+                assign_cpu_nodes(self.vdevices, nodes)
+                if any(v.cpu_node >= 0 for v in self.vdevices):
+                    log.info("numa spread: the vGPUs of each GPU alternate over CPU nodes %s", nodes)
         self._by_uuid = {d.uuid: d for d in self.devices}
         self._stopped.clear()
 
@@ -236,8 +242,11 @@ class DevicePluginServer:
         out = []
         for v in self.vdevices:
             d = api.Device(ID=v.id, health=api.HEALTHY if v.dev.healthy else api.UNHEALTHY)
-            if v.dev.numa_node >= 0:
-                d.topology.nodes.add(ID=v.dev.numa_node)
+            # --numa-spread: the CPU node the container's processes will run on, so that a
+            # topology-aware kubelet gives an exclusive-CPU pod its CPUs there too
+            node = v.cpu_node if v.cpu_node >= 0 else v.dev.numa_node
+            if node >= 0:
+                d.topology.nodes.add(ID=node)
             out.append(d)
         return out
 

@@ -73,6 +73,7 @@ class VDevice:
     cu_pct: int            # 0 = unlimited
     cu_range: tuple        # (begin, end) logical CUs, or None
     cu_share: float = 0.0  # exact share in percent (100 * cores_scaling / split); 0 = unlimited
+    cpu_node: int = -1     # NUMA node whose CPUs the container's processes run on (--numa-spread), -1 = any
 
     @property
     def uuid(self):
@@ -131,3 +132,21 @@ def physical_uuid(vdevice_id):
     """'<uuid>-<slot>' -> '<uuid>'."""
     base, _, slot = vdevice_id.rpartition("-")
     return base if slot.isdigit() and base else vdevice_id
+
+
+def assign_cpu_nodes(vdevices, cpu_nodes):
+    """--numa-spread: vGPU ``slot`` of a GPU gets CPU node ``order[slot % len(order)]``, where
+    ``order`` is the GPU's own NUMA node followed by the node's other CPU nodes. Co-tenant
+    pods of one GPU then launch from different CPU sockets: two launch-bound PyTorch pods
+    whose threads share a socket run no faster together than one alone on MI355X, on two
+    sockets at up to twice the rate, and a lone pod runs as fast from either socket
+    (profiles/r5d). Partitions and GPUs without a NUMA node keep -1."""
+    nodes = sorted(set(cpu_nodes))
+    for v in vdevices:
+        v.cpu_node = -1
+        home = getattr(v.dev, "numa_node", -1)
+        if len(nodes) < 2 or home < 0 or getattr(v.dev, "is_partition", False):
+            continue
+        order = ([home] if home in nodes else []) + [n for n in nodes if n != home]
+        v.cpu_node = order[v.slot % len(order)]
+    return vdevices

@@ -134,16 +134,58 @@ def run_mode(mode, node, uuid, cases, steps, warmup):
         os.unlink(out)
 
 
-def run_vdm(node, uuid, cases, warmup, seconds, pods=2):
+def numa_cpus():
+    """NUMA node -> the CPUs of it this process may use."""
+    allowed = os.sched_getaffinity(0)
+    out = {}
+    base = "/sys/devices/system/node"
+    for d in sorted(os.listdir(base)) if os.path.isdir(base) else []:
+        if d.startswith("node") and d[4:].isdigit():
+            try:
+                cpus = parse_cpulist(open(os.path.join(base, d, "cpulist")).read()) & allowed
+            except OSError:
+                continue
+            if cpus:
+                out[int(d[4:])] = sorted(cpus)
+    return out
+
+
+def vdm_cpus(bdf, pods, placement):
+    """Each VDM pod's CPUs. Two launch-bound processes whose threads run on one CPU socket do
+    not run faster together than one alone on MI355X, while on two sockets they run at twice
+    the rate (profiles/r5d). `product` (default) leaves the pods unpinned by the harness: the
+    plugin's --numa-spread (default auto) gives the two vGPUs different CPU nodes and the shim
+    keeps each pod there; `spread` pins pod i to NUMA node i mod nodes, GPU-local first, from
+    here; `local` pins every pod to the GPU's node (round 4's setup)."""
+    if placement in ("product", "none"):
+        return [[] for _ in range(pods)]
+    local = gpu_local_cpus(bdf)
+    if placement == "local" or not local:
+        return [local for _ in range(pods)]
+    nodes = numa_cpus()
+    order = [cs for cs in nodes.values() if set(cs) & set(local)] + \
+            [cs for cs in nodes.values() if not set(cs) & set(local)]
+    return [order[i % len(order)] for i in range(pods)]
+
+
+VDM_PLACEMENT = "product"
+
+
+def run_vdm(node, uuid, cases, warmup, seconds, pods=2, bdf=""):
     from amdvgpu.shim.launcher import apply_contract
     sync = tempfile.mkdtemp(prefix="vdm-")
     procs, outs = [], []
+    cpus = vdm_cpus(bdf, pods, VDM_PLACEMENT)
     for i, vid in enumerate(node.vgpu_ids(uuid)[:pods]):
         envs, mounts = node.pod([vid])
         out = os.path.join(sync, f"res{i}.json")
+        env = apply_contract(envs, mounts)
+        env.pop("AIBENCH_CPUS", None)
+        if cpus[i]:
+            env["AIBENCH_CPUS"] = ",".join(map(str, cpus[i]))
         procs.append(subprocess.Popen(_cmd(cases, 0, warmup, out, ["--seconds", str(seconds), "--sync-dir", sync,
                                                                    "--tag", str(i), "--peers", str(pods)]),
-                                      env=apply_contract(envs, mounts)))
+                                      env=env))
         outs.append(out)
     print(f"[vdm x{pods}]", flush=True)
     for p in procs:
@@ -249,11 +291,15 @@ def main():
     ap.add_argument("--merge", nargs="+", default=None,
                     help="render one table from the --json-out files of runs over disjoint case lists")
     ap.add_argument("--pin", type=int, default=1, help="pin every worker to the GPU's NUMA-local CPUs")
+    ap.add_argument("--vdm-placement", default="product", choices=["product", "spread", "local"],
+                    help="CPUs of the two VDM pods: the plugin's --numa-spread places them (default), pinned one "
+                         "per NUMA node from here, or both pinned GPU-local (round 4)")
     ap.add_argument("--autotune", type=int, default=1,
                     help="MIOpen find mode (cudnn.benchmark); 0 = deterministic heuristic solver choice")
     a = ap.parse_args()
-    global AUTOTUNE, WINDOW
+    global AUTOTUNE, WINDOW, VDM_PLACEMENT
     AUTOTUNE = a.autotune
+    VDM_PLACEMENT = a.vdm_placement
     WINDOW = a.window
     from amdvgpu.models.aibench import CASES
     cases = [c.name for c in CASES] if a.cases == "all" else a.cases.split(",")
@@ -284,12 +330,12 @@ def main():
                 json.dump({"steps": a.steps, "warmup": a.warmup, "repeats": rep + 1, "partial": True, "runs": runs},
                           open(a.json_out, "w"), indent=1)
         if a.vdm:
-            vdm = run_vdm(node, uuid, cases, a.warmup, a.vdm_seconds)
+            vdm = run_vdm(node, uuid, cases, a.warmup, a.vdm_seconds, bdf=dev.bdf)
     md, summary = table(runs, vdm, cases)
     print(md)
     if a.json_out:
         json.dump({"steps": a.steps, "warmup": a.warmup, "repeats": a.repeats, "autotune": a.autotune,
-                   "pinned_cpus": len(cpus), "summary": summary, "runs": runs,
+                   "pinned_cpus": len(cpus), "vdm_placement": VDM_PLACEMENT, "summary": summary, "runs": runs,
                    "vdm": vdm}, open(a.json_out, "w"), indent=1)
     if a.md_out:
         open(a.md_out, "w").write(md + "\n")

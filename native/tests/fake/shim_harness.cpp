@@ -70,8 +70,10 @@
 //                    the last range: {"hipprefetch": rc} / {"hipadvise": rc}
 //   svmunmap         munmap of the last range: {"svmunmap": true}
 //   ipcexport        hipIpcGetMemHandle of the most recent allocation: {"ipcexport": rc}
+//   affinity         the CPUs this process may run on: {"affinity": [cpu, ...]}
 #define __HIP_PLATFORM_AMD__ 1
 #include <dlfcn.h>
+#include <sched.h>
 #include <hip/hip_runtime_api.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -280,6 +282,18 @@ int main(int argc, char** argv) {
       using Get = uint64_t (*)();
       auto f = reinterpret_cast<Get>(dlsym(RTLD_DEFAULT, "vgpu_get_current_device_spilled"));
       printf("{\"spilled\": %llu}\n", f ? (unsigned long long)f() : 0ull);
+    } else if (key == "affinity") {
+      cpu_set_t set;
+      CPU_ZERO(&set);
+      sched_getaffinity(0, sizeof(set), &set);
+      printf("{\"affinity\": [");
+      bool first = true;
+      for (int c = 0; c < CPU_SETSIZE; c++)
+        if (CPU_ISSET(c, &set)) {
+          printf("%s%d", first ? "" : ", ", c);
+          first = false;
+        }
+      printf("]}\n");
     } else if (key == "meminfo") {
       size_t f = 0, t = 0;
       (void)hipMemGetInfo(&f, &t);

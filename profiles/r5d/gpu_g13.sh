@@ -32,3 +32,10 @@ unset GPU_MAX_HW_QUEUES &&
 export HSA_ENABLE_INTERRUPT=0 &&
 echo "nointr pair local+local: $(pair $LOCAL $L2)"
 } 2>&1 | tee -a $O/launch_probe.txt
+# CPU placement vs host-memory placement, for the PyTorch LSTM pair
+C="timeout -k 10 240 python3 -u tools/probe/cotenancy.py --seconds 4 --case lstm-inf --procs 2"
+for v in "local split" "remote split" "split local" "split remote" "local local"; do
+  set -- $v
+  $C --placement $1 --mem $2 > $O/mem_$1_$2.json 2> $O/mem_$1_$2.err || exit $?
+  tail -1 $O/mem_$1_$2.json | python3 -c "import json,sys; d=json.load(sys.stdin); print('cpus $1 mem $2', d['aggregate_items_per_s'], [t['items_per_s'] for t in d['tenants']])" | tee -a $O/launch_probe.txt
+done

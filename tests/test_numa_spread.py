@@ -1,0 +1,117 @@
+"""--numa-spread: co-tenant pods of one GPU launch from different CPU sockets.
+
+Two launch-bound PyTorch processes of one MI355X whose threads share a CPU socket run no
+faster together than one alone (LSTM inference 1.00x). One per socket, they run at 2.0x
+(ResNet-152 b=10: 1.00x vs 1.55x). A lone process runs as fast from either socket
+(profiles/r5d). The plugin gives vGPU k of a GPU the CPU node order[k mod n], the GPU's own
+node first, and tells the container (VGPU_CPU_NODE). The shim narrows each process's CPU
+affinity to that node before main() (native/src/shim/numa_spread.cpp).
+"""
+import os
+
+import pytest
+
+from amdvgpu.plugin.config import PluginConfig as Config
+from amdvgpu.plugin.devices import FakeBackend
+from amdvgpu.plugin.vdevice import assign_cpu_nodes, device_to_vdevices
+from test_plugin_grpc import plugin_dir, shutdown, start  # noqa: F401  (fixture)
+from test_shim_fake import fake, run  # noqa: F401  (fixture)
+
+
+def test_vgpus_of_a_gpu_alternate_over_cpu_nodes():
+    """2 GPUs on node 1 and 2 GPUs on node 0 of a 2-socket node, split 4: each GPU's vGPUs 0
+    and 2 stay on its own node, vGPUs 1 and 3 go to the other one."""
+    devs = FakeBackend(n=4, topology="pcie").devices()       # GPUs 0-1 on node 0, 2-3 on node 1
+    vds = assign_cpu_nodes(device_to_vdevices(devs, 4), [0, 1])
+    for v in vds:
+        home = v.dev.numa_node
+        assert v.cpu_node == (home if v.slot % 2 == 0 else 1 - home), (v.id, home, v.cpu_node)
+
+
+def test_no_spread_on_one_cpu_node_or_for_partitions():
+    devs = FakeBackend(n=2, topology="pcie").devices()
+    assert all(v.cpu_node == -1 for v in assign_cpu_nodes(device_to_vdevices(devs, 4), [0]))
+    parts = FakeBackend(n=1, partitions_per_gpu=8, compute_partition="CPX").devices()
+    assert all(v.cpu_node == -1 for v in assign_cpu_nodes(device_to_vdevices(parts, 1), [0, 1]))
+
+
+def test_numa_spread_option():
+    assert Config().numa_spread == "auto"
+    with pytest.raises(ValueError):
+        Config(numa_spread="sometimes").validate()
+
+
+@pytest.mark.parametrize("mode,spread", [("auto", True), ("off", False)])
+def test_allocate_tells_the_container_its_cpu_node(plugin_dir, mode, spread):  # noqa: F811
+    """Through the stub kubelet, split 2 on a 2-GPU PCIe node (one GPU per socket): the two
+    vGPUs of a GPU are advertised on different NUMA nodes and their containers get
+    VGPU_CPU_NODE for them; with --numa-spread off the GPU's own node only and no env."""
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=2, numa_spread=mode,
+                                  backend=FakeBackend(n=2, topology="pcie", numa_split=1))
+    try:
+        k.wait_registered("amd.com/gpu")
+        k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
+        topo = k.topology("amd.com/gpu")
+        by_uuid = {d.uuid: d for d in FakeBackend(n=2, topology="pcie", numa_split=1).devices()}
+        for vid, nodes in topo.items():
+            uuid, slot = vid.rsplit("-", 1)
+            home = by_uuid[uuid].numa_node
+            assert nodes == [home if not spread or int(slot) == 0 else 1 - home], (vid, nodes)
+        got = {}
+        for _ in range(4):
+            (vid,), r = k.allocate("amd.com/gpu", 1)
+            got[vid] = dict(r.envs).get("VGPU_CPU_NODE")
+        for vid, node in got.items():
+            if spread:
+                assert node == str(topo[vid][0]), (vid, node)
+            else:
+                assert node is None
+    finally:
+        shutdown(k, stop, th)
+
+
+def _fake_sysfs(tmp_path, nodes):
+    for n, cpus in nodes.items():
+        d = tmp_path / "sys" / "devices" / "system" / "node" / f"node{n}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(",".join(map(str, cpus)) + "\n")
+    return str(tmp_path / "sys")
+
+
+def _allowed():
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) < 2:
+        pytest.skip("needs two CPUs")
+    return cpus
+
+
+def test_shim_narrows_affinity_to_the_cpu_node(fake, tmp_path):  # noqa: F811
+    """VGPU_CPU_NODE=1 with node 1 = the upper half of this process's CPUs: the harness runs
+    on that half only; VGPU_CPU_SPREAD=0 (tenant opt-out) and an unknown node leave it alone."""
+    cpus = _allowed()
+    half = len(cpus) // 2
+    root = _fake_sysfs(tmp_path, {0: cpus[:half], 1: cpus[half:]})
+    out = run(fake(gpus=1, VGPU_CPU_NODE="1", VGPU_SYSFS_ROOT=root), "affinity")
+    assert out[-1]["affinity"] == cpus[half:]
+    out = run(fake(gpus=1, VGPU_CPU_NODE="1", VGPU_SYSFS_ROOT=root, VGPU_CPU_SPREAD="0"), "affinity")
+    assert out[-1]["affinity"] == cpus
+    out = run(fake(gpus=1, VGPU_CPU_NODE="7", VGPU_SYSFS_ROOT=root), "affinity")
+    assert out[-1]["affinity"] == cpus
+
+
+def test_shim_keeps_an_affinity_already_inside_the_node(fake, tmp_path):  # noqa: F811
+    """A container whose CPUs are an exclusive set inside the node (the kubelet's CPU
+    manager) or that do not meet it keeps them."""
+    cpus = _allowed()
+    half = len(cpus) // 2
+    root = _fake_sysfs(tmp_path, {0: cpus[:half], 1: cpus[half:]})
+    e = fake(gpus=1, VGPU_CPU_NODE="0", VGPU_SYSFS_ROOT=root)
+    import subprocess
+    from test_shim_fake import HARNESS
+    import json
+    for subset in (cpus[:1], cpus[half:half + 1]):
+        p = subprocess.run(["taskset", "-c", ",".join(map(str, subset)), HARNESS, "affinity"], env=e,
+                           capture_output=True, text=True, timeout=60)
+        assert p.returncode == 0, p.stderr[-2000:]
+        got = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")][-1]["affinity"]
+        assert got == subset

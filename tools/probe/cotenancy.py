@@ -87,9 +87,20 @@ def _where():
     return cpu, node
 
 
-def tenant(case, seconds, go, batch, cpus):
+def _bind_memory(node):
+    """set_mempolicy(MPOL_BIND, {node}) for this process (before the runtime allocates)."""
+    import ctypes
+    libc = ctypes.CDLL(None, use_errno=True)
+    mask = ctypes.c_ulong(1 << node)
+    if libc.syscall(238, 2, ctypes.byref(mask), ctypes.c_ulong(64 + 1)) != 0:   # SYS_set_mempolicy, MPOL_BIND
+        raise OSError(ctypes.get_errno(), "set_mempolicy")
+
+
+def tenant(case, seconds, go, batch, cpus, mem_node=-1):
     if cpus:
         os.sched_setaffinity(0, {int(c) for c in cpus.split(",")})
+    if mem_node >= 0:
+        _bind_memory(mem_node)
     import resource
 
     import torch
@@ -151,6 +162,13 @@ def launch(a):
         / of the other nodes; split = even tenants local, odd ones remote; none = --pin K of
         all allowed CPUs (or unpinned)."""
         k = max(1, a.pin or 4)
+        if a.cpu_lists:   # explicit: "64-67;96-99" = tenant 0 on 64-67, tenant 1 on 96-99
+            spec = a.cpu_lists.split(";")[i % len(a.cpu_lists.split(";"))]
+            out = []
+            for part in spec.split(","):
+                lo, _, hi = part.partition("-")
+                out += list(range(int(lo), int(hi or lo) + 1))
+            return out
         if a.placement == "local":
             pool, j = local, i
         elif a.placement == "remote":
@@ -163,11 +181,24 @@ def launch(a):
             return []
         return pool[j * k:(j + 1) * k]
 
+    def mem_of(i):
+        """--mem local / remote / split: tenant i's host memory bound to that NUMA node."""
+        if a.mem == "none" or gnode < 0:
+            return -1
+        other = next((n for n in sorted(nodes) if n != gnode), gnode)
+        if a.mem == "local":
+            return gnode
+        if a.mem == "remote":
+            return other
+        return gnode if i % 2 == 0 else other
+
     def cmd(i):
         c = list(args)
         cs = cpus_of(i)
         if cs:
             c += ["--cpus", ",".join(str(x) for x in cs)]
+        if mem_of(i) >= 0:
+            c += ["--mem-node", str(mem_of(i))]
         if not a.trace:
             return c
         prof = ["rocprofv3", "--kernel-trace"] + (["--hip-trace", "--stats"] if a.hip_stats else [])
@@ -193,7 +224,7 @@ def launch(a):
     agg = sum(o["items_per_s"] for o in outs)
     aff, quota = _cpu_limit()
     print(json.dumps({"case": a.case, "procs": a.procs, "burners": a.burners, "pin": a.pin,
-                      "placement": a.placement, "gpu_numa_node": gnode,
+                      "placement": a.placement, "mem": a.mem, "gpu_numa_node": gnode,
                       "numa_cpus": {n: len(cs) for n, cs in nodes.items()},
                       "aggregate_items_per_s": round(agg, 1), "affinity": aff, "cgroup_cpus": quota,
                       "tenants": outs}), flush=True)
@@ -314,14 +345,31 @@ def main():
     ap.add_argument("--burners", type=int, default=0, help="CPU-only processes spinning during the window")
     ap.add_argument("--placement", default="none", choices=["none", "local", "remote", "split"],
                     help="pin the tenants (--pin CPUs each, default 4) to the GPU's NUMA node, the others, or both")
+    ap.add_argument("--mem", default="none", choices=["none", "local", "remote", "split"],
+                    help="bind each tenant's host memory to the GPU's NUMA node, another one, or alternate")
+    ap.add_argument("--mem-node", type=int, default=-1)
+    ap.add_argument("--cpu-lists", default="", help='explicit CPUs per tenant, e.g. "64-67;96-99"')
+    ap.add_argument("--l3", action="store_true", help="print the L3 (CCD) domains of the allowed CPUs and exit")
     ap.add_argument("--burner", action="store_true")
     ap.add_argument("--cpus", default="")
     a = ap.parse_args()
+    if a.l3:
+        doms = {}
+        for c in sorted(os.sched_getaffinity(0)):
+            try:
+                doms.setdefault(open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list").read().strip(),
+                                None)
+            except OSError:
+                pass
+        print(json.dumps({"l3_domains": list(doms), "numa": {n: f"{cs[0]}..{cs[-1]} ({len(cs)})"
+                                                             for n, cs in _numa_nodes().items()},
+                          "gpu_node": _gpu_node()}))
+        return 0
     if a.analyze:
         print(json.dumps(analyze(a.analyze)))
         return 0
     if a.tenant:
-        return tenant(a.case, a.seconds, a.go, a.batch, a.cpus)
+        return tenant(a.case, a.seconds, a.go, a.batch, a.cpus, a.mem_node)
     if a.burner:
         return burner(a.go, a.seconds)
     return launch(a)
