@@ -168,3 +168,21 @@ def test_blocking_wait_polls_instead_of_spinning(fake, mode, cpu_bound):
     else:
         assert long["cpu_ms"] >= 0.4 * long["waitsig"], long   # the runtime's spin (the fake spins too)
         assert spin["cpu_ms"] >= 0.4 * spin["waitspin"], spin
+
+
+def test_auto_wait_polls_only_on_a_crowded_gpu(fake):
+    """VGPU_SYNC_WAIT=auto (default): a pod alone on its GPU keeps the runtime's spinning wait
+    (no added latency); once two other processes keep the GPU busy (the crowd count of auto
+    mode), the same wait polls with sleeps and holds a fraction of a CPU."""
+    from test_shim_fake import _foreign
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g", VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="auto")
+    out = run(e, "stream", "sleep=0.5", "waitspin=200")
+    alone = [o for o in out if "waitspin" in o][0]
+    for pid in (424270, 424271):
+        _foreign(fake.kfd, pid, 40)
+    out = run(e, "stream", "sleep=1.0", "waitspin=200", "waitsig=200")
+    crowded = [o for o in out if "waitspin" in o or "waitsig" in o]
+    assert alone["cpu_ms"] >= 0.4 * alone["waitspin"], alone
+    for o in crowded:
+        wall = o.get("waitspin", o.get("waitsig"))
+        assert 199 <= wall <= 200 * 1.15 + 1.5 and o["cpu_ms"] <= 0.25 * wall, crowded
