@@ -208,6 +208,13 @@ def worker(args):
         # a host): a timing event after every step, read back once at the end, so the parent
         # can rate every pod over the window in which all of them run (common_window()).
         import resource
+        # The limiter's account of the window, read from the pod's region like vgpuctl: the
+        # GPU time charged to the pod and the enforcement it ran under (why a pod falls behind)
+        region = None
+        if not cpu and os.environ.get("VGPU_SHARED_CACHE") and os.path.exists(os.environ["VGPU_SHARED_CACHE"]):
+            from amdvgpu.shim.region import Region
+            region = Region(os.environ["VGPU_SHARED_CACHE"])
+        g0 = region.device(0) if region else None
         marks = []
         n = 0
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
@@ -239,6 +246,13 @@ def worker(args):
                # one 16-CPU quota: a point whose pods need more is CPU-bound, not GPU-bound)
                "cpu_s": round(ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime, 3),
                "startup": {k: round(v, 2) for k, v in phases.items()}}
+        g1 = region.device(0) if region else None
+        if g0 and g1 and g1["wall_ns"] > g0["wall_ns"]:
+            res["granted_pct"] = round(100.0 * (g1["charged_ns"] - g0["charged_ns"]) / (g1["wall_ns"] - g0["wall_ns"]), 2)
+            res["cu_mode_end"] = g1["cu_mode"]
+            res["crowd_end"] = g1["crowd"]
+        if region:
+            region.close()
     else:
         # The limiter's own account of the timed window (GPU time charged / wall time), read
         # from the pod's shared region like vgpuctl would: what the vGPU granted this pod.
@@ -554,6 +568,10 @@ def _sweep_points(args, backend, uuid, tenants, end, root):
                      "per_tenant_own_window": [round(t, 2) for t in own], "aggregate_span": round(agg_span, 2),
                      "cpus_busy": round(sum(r.get("cpu_s", 0.0) for r in res) / span, 2),
                      "pod_wait": res[0].get("wait"),
+                     # per pod: GPU time charged by its limiter over its window (% of wall), and the
+                     # enforcement at the end of the window
+                     "granted_pct": [r.get("granted_pct") for r in res],
+                     "cu_mode_end": sorted({str(r.get("cu_mode_end")) for r in res}),
                      "cu_limit_pct": int(c0.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0),
                      "cu_mode": c0.get("VGPU_CU_MODE"), "quota_mib": int(c0["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m"))})
         print(f"[bench] sweep {n} tenants: aggregate {agg:.1f}, per tenant {min(tput):.1f}..{max(tput):.1f} "
