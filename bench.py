@@ -215,6 +215,7 @@ def worker(args):
             from amdvgpu.shim.region import Region
             region = Region(os.environ["VGPU_SHARED_CACHE"])
         g0 = region.device(0) if region else None
+        th0 = sum(p["throttle_ns"] for p in region.procs()) if region else 0
         marks = []
         n = 0
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
@@ -251,6 +252,11 @@ def worker(args):
             res["granted_pct"] = round(100.0 * (g1["charged_ns"] - g0["charged_ns"]) / (g1["wall_ns"] - g0["wall_ns"]), 2)
             res["cu_mode_end"] = g1["cu_mode"]
             res["crowd_end"] = g1["crowd"]
+            # time this pod's launches waited at the limiter's gate, % of the window
+            res["throttled_pct"] = round(100.0 * (sum(p["throttle_ns"] for p in region.procs()) - th0) /
+                                         (g1["wall_ns"] - g0["wall_ns"]), 2)
+            # the processes the pod's limiter charges for (container pid, host pid)
+            res["region_procs"] = [[p["pid"], p["hostpid"]] for p in region.procs()] + [["self", os.getpid()]]
         if region:
             region.close()
     else:
@@ -571,6 +577,8 @@ def _sweep_points(args, backend, uuid, tenants, end, root):
                      # per pod: GPU time charged by its limiter over its window (% of wall), and the
                      # enforcement at the end of the window
                      "granted_pct": [r.get("granted_pct") for r in res],
+                     "throttled_pct": [r.get("throttled_pct") for r in res],
+                     "region_procs": [r.get("region_procs") for r in res],
                      "cu_mode_end": sorted({str(r.get("cu_mode_end")) for r in res}),
                      "cu_limit_pct": int(c0.get("VGPU_DEVICE_CU_LIMIT_0", "0") or 0),
                      "cu_mode": c0.get("VGPU_CU_MODE"), "quota_mib": int(c0["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m"))})

@@ -475,9 +475,13 @@ uint64_t wait_queue_depth(int dev, int cap) {
   constexpr uint64_t kMaxWaitNs = 20'000'000ull;
   if (queued_packets(dev) <= (uint64_t)cap) return 0;
   const uint64_t t0 = now_ns();
-  struct timespec ts = {0, 20'000};
   trace_push("vgpu:depth");
-  while (queued_packets(dev) > (uint64_t)cap && now_ns() - t0 < kMaxWaitNs) nanosleep(&ts, nullptr);
+  // Sleeps grow with the time waited (1/8 of it, 20 us to 500 us), as the host waits do
+  // (sync_hooks.cpp): a long drain costs a few dozen wake-ups, not a core.
+  for (uint64_t el = 0; queued_packets(dev) > (uint64_t)cap && el < kMaxWaitNs; el = now_ns() - t0) {
+    struct timespec ts = {0, (long)std::min<uint64_t>(std::max<uint64_t>(el / 8, 20'000), 500'000)};
+    nanosleep(&ts, nullptr);
+  }
   trace_pop();
   return now_ns() - t0;
 }

@@ -398,7 +398,15 @@ void sample_tick(Region* r, Sampler& sm) {
       if (!hold) ds.gate_open.store(0, std::memory_order_release);
       sm.board.publish_gate(d, hold, sm.want_since[d]);
     }
-    if (background) preempt_tick(sm, ds, a.gpu_id, prio, d, yield, now);
+    if (background) {
+      preempt_tick(sm, ds, a.gpu_id, prio, d, yield, now);
+    } else {
+      // On the limiter, a bounded queue (VGPU_CROWD_DEPTH) keeps each pod's debt to a few
+      // kernels: the credit gate then paces it kernel by kernel instead of admitting a whole
+      // synchronize-to-synchronize batch at once.
+      const int cap = config().crowd_depth;
+      if (ds.depth_cap.load(std::memory_order_relaxed) != cap) ds.depth_cap.store(cap, std::memory_order_relaxed);
+    }
     sm.opened[d] = was_closed && ds.gate_open.load(std::memory_order_relaxed);
     sm.prev_pm[d] = pm;
   }

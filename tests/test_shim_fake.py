@@ -824,6 +824,20 @@ def test_background_class_bounded_depth(fake, tmp_path, depth, bound):
             assert r.device(0)["depth_cap"] in (0, depth)  # 0 once the process left
 
 
+@pytest.mark.parametrize("depth,bound", [(0, None), (8, 9)])
+def test_crowd_depth_bounds_work_in_flight(fake, depth, bound):
+    """VGPU_CROWD_DEPTH: a normal-class container on the GPU-time limiter keeps at most
+    `depth` packets in flight, so its credit gate paces it kernel by kernel; without it a
+    burst between two synchronizes queues whole."""
+    e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="temporal", VGPU_CROWD_DEPTH=str(depth))
+    out = run(e, "stream", "run=1000,0.5", "burst=2000,40", timeout=120)
+    burst = [o for o in out if "burst" in o][0]
+    if bound is None:
+        assert burst["max_depth"] >= 30, burst
+    else:
+        assert 1 <= burst["max_depth"] <= bound, burst
+
+
 def test_background_class_keeps_off_the_latency_class_cus(fake, tmp_path):
     """A latency-class tenant (priority 0) publishes its CU slice on the board; a
     background tenant (priority >= 2) on the same GPU re-masks its queues to the rest of
