@@ -401,10 +401,11 @@ void sample_tick(Region* r, Sampler& sm) {
     if (background) {
       preempt_tick(sm, ds, a.gpu_id, prio, d, yield, now);
     } else {
-      // On the limiter, a bounded queue (VGPU_CROWD_DEPTH) keeps each pod's debt to a few
-      // kernels: the credit gate then paces it kernel by kernel instead of admitting a whole
-      // synchronize-to-synchronize batch at once.
-      const int cap = config().crowd_depth;
+      // On the limiter of a crowded GPU (three or more processes on it), a bounded queue
+      // (VGPU_CROWD_DEPTH) keeps each pod's debt to a few kernels: the credit gate then paces
+      // it kernel by kernel instead of admitting a whole synchronize-to-synchronize batch at
+      // once (profiles/r5c). A pod alone under a GPU-time limit keeps its full queue.
+      const int cap = sm.procs > 2 ? config().crowd_depth : 0;
       if (ds.depth_cap.load(std::memory_order_relaxed) != cap) ds.depth_cap.store(cap, std::memory_order_relaxed);
     }
     sm.opened[d] = was_closed && ds.gate_open.load(std::memory_order_relaxed);

@@ -824,11 +824,15 @@ def test_background_class_bounded_depth(fake, tmp_path, depth, bound):
             assert r.device(0)["depth_cap"] in (0, depth)  # 0 once the process left
 
 
-@pytest.mark.parametrize("depth,bound", [(0, None), (8, 9)])
-def test_crowd_depth_bounds_work_in_flight(fake, depth, bound):
-    """VGPU_CROWD_DEPTH: a normal-class container on the GPU-time limiter keeps at most
-    `depth` packets in flight, so its credit gate paces it kernel by kernel; without it a
-    burst between two synchronizes queues whole."""
+@pytest.mark.parametrize("depth,crowded,bound", [(0, True, None), (8, True, 9), (8, False, None)])
+def test_crowd_depth_bounds_work_in_flight(fake, depth, crowded, bound):
+    """VGPU_CROWD_DEPTH: a normal-class container on the GPU-time limiter of a crowded GPU
+    (two other busy processes) keeps at most `depth` packets in flight, so its credit gate
+    paces it kernel by kernel; without the bound, or alone on its GPU, a burst between two
+    synchronizes queues whole."""
+    if crowded:
+        for pid in (424280, 424281):
+            _foreign(fake.kfd, pid, 40)
     e = fake(gpus=1, VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="temporal", VGPU_CROWD_DEPTH=str(depth))
     out = run(e, "stream", "run=1000,0.5", "burst=2000,40", timeout=120)
     burst = [o for o in out if "burst" in o][0]
