@@ -134,10 +134,11 @@ struct Config {
   int preempt_depth = 4;                 // VGPU_PREEMPT_DEPTH: background class - at most this many AQL
                                          // packets in flight per device while a better class shares the
                                          // GPU (0 = unbounded)
-  int crowd_depth = 0;                   // VGPU_CROWD_DEPTH: on the GPU-time limiter (a crowded GPU), at
+  int crowd_depth = 16;                  // VGPU_CROWD_DEPTH: on the GPU-time limiter of a crowded GPU, at
                                          // most this many AQL packets in flight per device and process, so
                                          // the credit gate acts per kernel instead of per queued batch
-                                         // (0 = unbounded; profiles/r5c)
+                                         // (0 = unbounded; 16 pods: slowest pod 0.96-1.01 of 1/N against
+                                         // 0.79-0.99 unbounded, profiles/r5c)
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
   uint64_t host_mem_limit = 0;           // VGPU_HOST_MEMORY_LIMIT: pinned host memory, 0 = unlimited

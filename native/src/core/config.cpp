@@ -329,7 +329,7 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   if (parse_int(getenv_fn("VGPU_PREEMPT_HOLD_MS"), 0, 10000, &hold)) cfg->preempt_hold_ms = (int)hold;
   long depth = 4;
   if (parse_int(getenv_fn("VGPU_PREEMPT_DEPTH"), 0, 4096, &depth)) cfg->preempt_depth = (int)depth;
-  long crowd_depth = 0;
+  long crowd_depth = 16;
   if (parse_int(getenv_fn("VGPU_CROWD_DEPTH"), 0, 65536, &crowd_depth)) cfg->crowd_depth = (int)crowd_depth;
   if (const char* s = getenv_fn("VGPU_LOCK_FILE")) {
     if (*s) cfg->lock_file = s;
