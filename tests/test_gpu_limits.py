@@ -265,9 +265,27 @@ emit(ok=True)
 """
 
 
-def _background_rate_next_to(neighbour_prio, tmp_path):
-    """A background tenant (priority 2, GPU-time limiter at 50 %) spins for 3 s next to a
-    neighbour container of priority `neighbour_prio` that keeps the GPU busy."""
+BG_RATE = """
+import torch
+from amdvgpu.ops import spin
+torch.zeros(1, device="cuda"); torch.cuda.synchronize()
+n = 0
+t0 = time.perf_counter()        # no warm-up launch: a held tenant would never get past it
+while time.perf_counter() - t0 < {secs}:
+    spin(2048, 500)
+    n += 1
+    if n % 16 == 0:
+        torch.cuda.synchronize()
+torch.cuda.synchronize()
+emit(rate=n / (time.perf_counter() - t0))
+"""
+
+
+def _background_rate_next_to(neighbour_prio, tmp_path, secs=3.0):
+    """A background tenant (priority 2, GPU-time limiter at 50 %) spins for `secs` next to a
+    neighbour container of priority `neighbour_prio` that keeps the GPU busy. The neighbour
+    stops 2 s after the window: a tenant held at its launch gate for the whole window is let
+    go then, ends its loop at once, and its rate counts what it launched while held."""
     board = tmp_path / "board"
     board.mkdir()
     ready, stop = str(tmp_path / "ready"), str(tmp_path / "stop")
@@ -282,7 +300,18 @@ def _background_rate_next_to(neighbour_prio, tmp_path):
             assert time.time() < deadline and svc.poll() is None, "neighbour failed to start"
             time.sleep(0.05)
         time.sleep(1.0)  # on the board, busy
-        rate = _spin_rates([bg], secs=3.0)[0]
+        p = spawn_child(BG_RATE.format(secs=secs), bg)
+        t_end = time.time() + 60
+        while p.poll() is None and not os.path.exists(bg["VGPU_SHARED_CACHE"]) and time.time() < t_end:
+            time.sleep(0.05)
+        try:
+            p.wait(timeout=secs + 2.0 + 30.0)   # start-up (import torch) + the window + 2 s
+        except subprocess.TimeoutExpired:
+            pass
+        open(stop, "w").close()                  # the neighbour stops: a held tenant is let go
+        o, e = p.communicate(timeout=120)
+        assert p.returncode == 0, e[-3000:]
+        rate = child_results(o)[0]["rate"]
         with Region(bg["VGPU_SHARED_CACHE"]) as r:   # the limiter's side, for a failure's message
             d = r.device(0)
             diag = {"samples": r.samples, "other_refreshes": r.other_refreshes, "charged_ns": d["charged_ns"],
