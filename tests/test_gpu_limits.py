@@ -268,9 +268,9 @@ emit(ok=True)
 BG_RATE = """
 import torch
 from amdvgpu.ops import spin
-torch.zeros(1, device="cuda"); torch.cuda.synchronize()
+open(os.environ["VGPU_TEST_STARTED"], "w").close()
 n = 0
-t0 = time.perf_counter()        # no warm-up launch: a held tenant would never get past it
+t0 = time.perf_counter()        # before any launch: a held tenant would never get past a warm-up
 while time.perf_counter() - t0 < {secs}:
     spin(2048, 500)
     n += 1
@@ -281,7 +281,7 @@ emit(rate=n / (time.perf_counter() - t0))
 """
 
 
-def _background_rate_next_to(neighbour_prio, tmp_path, secs=3.0):
+def _background_rate_next_to(neighbour_prio, tmp_path, secs=5.0):
     """A background tenant (priority 2, GPU-time limiter at 50 %) spins for `secs` next to a
     neighbour container of priority `neighbour_prio` that keeps the GPU busy. The neighbour
     stops 2 s after the window: a tenant held at its launch gate for the whole window is let
@@ -300,12 +300,13 @@ def _background_rate_next_to(neighbour_prio, tmp_path, secs=3.0):
             assert time.time() < deadline and svc.poll() is None, "neighbour failed to start"
             time.sleep(0.05)
         time.sleep(1.0)  # on the board, busy
-        p = spawn_child(BG_RATE.format(secs=secs), bg)
-        t_end = time.time() + 60
-        while p.poll() is None and not os.path.exists(bg["VGPU_SHARED_CACHE"]) and time.time() < t_end:
+        started = str(tmp_path / "started")
+        p = spawn_child(BG_RATE.format(secs=secs), bg, extra_env={"VGPU_TEST_STARTED": started})
+        t_end = time.time() + 240
+        while p.poll() is None and not os.path.exists(started) and time.time() < t_end:
             time.sleep(0.05)
         try:
-            p.wait(timeout=secs + 2.0 + 30.0)   # start-up (import torch) + the window + 2 s
+            p.wait(timeout=secs + 2.0)            # the window (and the context's set-up) + 2 s
         except subprocess.TimeoutExpired:
             pass
         open(stop, "w").close()                  # the neighbour stops: a held tenant is let go
