@@ -3,6 +3,11 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r5h
+timeout -k 10 300 python -u -m pytest -v -s --timeout 280 --timeout-method thread -p no:cacheprovider -m gpu \
+  "tests/test_gpu_limits.py::test_background_class_yields_to_a_busy_latency_class" > gpurun_out/r5h/bg_test.log 2>&1
+rc=$?
+grep -E "next_to_equal|PASSED|FAILED" gpurun_out/r5h/bg_test.log | cut -c1-600
+case $rc in 0|1) ;; *) exit $rc ;; esac
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r5h/smoke.log 2>&1 || { tail -20 gpurun_out/r5h/smoke.log; exit 1; }
 tail -2 gpurun_out/r5h/smoke.log
 timeout -k 10 660 python -u bench.py --json-out gpurun_out/r5h/bench.json > gpurun_out/r5h/bench.log 2>&1
