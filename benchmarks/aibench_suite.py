@@ -134,6 +134,15 @@ def run_mode(mode, node, uuid, cases, steps, warmup):
         os.unlink(out)
 
 
+def l3_domain_of(cpu, allowed):
+    """The CPUs sharing `cpu`'s L3 cache, within `allowed` (`allowed` if unknown)."""
+    try:
+        dom = parse_cpulist(open(f"/sys/devices/system/cpu/cpu{cpu}/cache/index3/shared_cpu_list").read())
+    except OSError:
+        return allowed
+    return sorted(dom & set(allowed)) or allowed
+
+
 def numa_cpus():
     """NUMA node -> the CPUs of it this process may use."""
     allowed = os.sched_getaffinity(0)
@@ -290,7 +299,8 @@ def main():
     ap.add_argument("--md-out", default=None)
     ap.add_argument("--merge", nargs="+", default=None,
                     help="render one table from the --json-out files of runs over disjoint case lists")
-    ap.add_argument("--pin", type=int, default=1, help="pin every worker to the GPU's NUMA-local CPUs")
+    ap.add_argument("--pin", type=int, default=1,
+                    help="pin every worker to the GPU's NUMA-local CPUs (1), to one L3 domain of them (2), or not (0)")
     ap.add_argument("--vdm-placement", default="product", choices=["product", "spread", "local"],
                     help="CPUs of the two VDM pods: the plugin's --numa-spread places them (default), pinned one "
                          "per NUMA node from here, or both pinned GPU-local (round 4)")
@@ -313,6 +323,10 @@ def main():
     dev = backend.devices()[0]
     uuid = dev.uuid
     cpus = gpu_local_cpus(dev.bdf) if a.pin else []
+    if a.pin == 2 and cpus:
+        # one L3 domain (CCD) of the GPU's node: launch-bound cases (thousands of kernels per
+        # step) vary less from process to process when their threads stay on one CCD
+        cpus = l3_domain_of(cpus[0], cpus)
     if cpus:
         os.environ["AIBENCH_CPUS"] = ",".join(map(str, cpus))
     print(f"GPU {dev.bdf}: workers pinned to {len(cpus)} NUMA-local CPUs" if cpus else "workers not pinned", flush=True)

@@ -8,8 +8,8 @@ out=gpurun_out/r5f
 mkdir -p $out
 c=$1
 timeout -k 10 1050 python -u benchmarks/aibench_suite.py --cases $c --modes native,vgpu --repeats 8 --window 10 \
-  --vdm 0 --json-out $out/$c.json --md-out $out/$c.md > $out/$c.log 2>&1
+  --vdm 0 ${PIN:+--pin $PIN} --json-out $out/$c$TAG.json --md-out $out/$c$TAG.md > $out/$c$TAG.log 2>&1
 rc=$?
-echo "suite_rc=$rc" >> $out/$c.log
-tail -6 $out/$c.log
+echo "suite_rc=$rc" >> $out/$c$TAG.log
+tail -6 $out/$c$TAG.log
 exit $rc
