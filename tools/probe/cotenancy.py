@@ -203,7 +203,14 @@ def launch(a):
             return c
         prof = ["rocprofv3", "--kernel-trace"] + (["--hip-trace", "--stats"] if a.hip_stats else [])
         return prof + ["--output-format", "csv", "-d", os.path.join(a.trace, f"t{i}"), "-o", f"t{i}", "--"] + c
-    procs = [subprocess.Popen(cmd(i), stdout=subprocess.PIPE, text=True) for i in range(a.procs)]
+    def env_of(i):
+        env = dict(os.environ)
+        if a.shim:   # each tenant a quota-only vGPU of its own (the shim preloaded, no limits)
+            from amdvgpu.shim.launcher import apply_contract, vgpu_env
+            env = apply_contract(vgpu_env(mem_limit=64 << 30))
+        env.update(dict(kv.split("=", 1) for kv in a.env))
+        return env
+    procs = [subprocess.Popen(cmd(i), stdout=subprocess.PIPE, text=True, env=env_of(i)) for i in range(a.procs)]
     burners = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--burner", "--go", go,
                                  "--seconds", str(a.seconds)]) for _ in range(a.burners)]
     deadline = time.time() + 600
@@ -224,7 +231,7 @@ def launch(a):
     agg = sum(o["items_per_s"] for o in outs)
     aff, quota = _cpu_limit()
     print(json.dumps({"case": a.case, "procs": a.procs, "burners": a.burners, "pin": a.pin,
-                      "placement": a.placement, "mem": a.mem, "gpu_numa_node": gnode,
+                      "placement": a.placement, "mem": a.mem, "shim": a.shim, "env": a.env, "gpu_numa_node": gnode,
                       "numa_cpus": {n: len(cs) for n, cs in nodes.items()},
                       "aggregate_items_per_s": round(agg, 1), "affinity": aff, "cgroup_cpus": quota,
                       "tenants": outs}), flush=True)
@@ -351,6 +358,8 @@ def main():
     ap.add_argument("--cpu-lists", default="", help='explicit CPUs per tenant, e.g. "64-67;96-99"')
     ap.add_argument("--l3", action="store_true", help="print the L3 (CCD) domains of the allowed CPUs and exit")
     ap.add_argument("--burner", action="store_true")
+    ap.add_argument("--shim", action="store_true", help="run every tenant in a quota-only vGPU")
+    ap.add_argument("--env", action="append", default=[], help="KEY=VALUE for every tenant")
     ap.add_argument("--cpus", default="")
     a = ap.parse_args()
     if a.l3:
