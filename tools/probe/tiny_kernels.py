@@ -70,7 +70,7 @@ def point(a, procs):
         from amdvgpu.shim.launcher import apply_contract, vgpu_env
     for i in range(procs):
         if a.shim:
-            env = apply_contract(vgpu_env(mem_limit=64 << 30))
+            env = apply_contract(vgpu_env(mem_limit=64 << 30, cu_limit=a.cu_limit or None))
         env.update(dict(kv.split("=", 1) for kv in a.env))
         cpus = nodes[i % len(nodes)][(i // len(nodes)) * 4:(i // len(nodes)) * 4 + 4]
         ps.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--tenant", "--go", go,
@@ -102,6 +102,7 @@ def main():
                     help="torch.cuda.synchronize (HIP spins) or a blocking event wait")
     ap.add_argument("--sync-every", type=int, default=64)
     ap.add_argument("--shim", action="store_true", help="run every process in a quota-only vGPU")
+    ap.add_argument("--cu-limit", type=int, default=0, help="with --shim: the vGPUs' CU share (auto mode)")
     ap.add_argument("--env", action="append", default=[], help="KEY=VALUE for every process")
     a = ap.parse_args()
     if a.tenant:
@@ -112,7 +113,7 @@ def main():
         agg = sum(rates)
         one = one or agg
         print(json.dumps({"procs": n, "nblocks": a.nblocks, "us": a.us, "wait": a.wait, "sync_every": a.sync_every,
-                          "shim": a.shim, "env": a.env, "aggregate_kernels_per_s": round(agg, 1),
+                          "shim": a.shim, "cu_limit": a.cu_limit, "env": a.env, "aggregate_kernels_per_s": round(agg, 1),
                           "vs_one": round(agg / one, 3), "per_proc": rates}), flush=True)
     return 0
 
