@@ -45,6 +45,12 @@ cross-rank group is gloo). ``value`` is the whole-job vGPU throughput (sum over 
 With N > 1 an RCCL all-reduce between the ranks' pods is probed afterwards, natively and
 inside the pods, and its bus bandwidth compared (``rccl_allreduce_between_pods``).
 
+Ranks: under torch.distributed.run each rank takes its GPU from LOCAL_RANK. Called as
+``python bench.py --gpus N`` (N > 1) with no launcher, the process starts the N ranks
+itself (torch.distributed.run on 127.0.0.1, before anything touches a GPU) and exits with
+their code, so the line always covers the N GPUs it names; N beyond the GPUs the job can
+see (render nodes it may open, ROCR/HIP_VISIBLE_DEVICES) is refused with a non-zero exit.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--case resnet50-inf] [--sweep auto|on|off]
 """
 import argparse
@@ -654,12 +660,96 @@ def node_summary(records, split, native_per_gpu):
     return s
 
 
+def make_backend(cpu, world):
+    """The rank's device inventory: the node's GPUs from KFD sysfs (no GPU context), or in
+    the CPU rehearsal a fake node of WORLD_SIZE GPUs (``VGPU_BENCH_FAKE_GPUS`` overrides
+    the count, so a too-small node can be rehearsed)."""
+    from amdvgpu.plugin.devices import FakeBackend, SysfsBackend
+    if cpu:
+        return FakeBackend(n=int(os.environ.get("VGPU_BENCH_FAKE_GPUS", 0) or max(world, 1)))
+    return SysfsBackend()
+
+
+def visible_devices(backend, cpu):
+    """The GPUs this job may use, in KFD order: every GPU whose render node this process can
+    open (a container sees every GPU's sysfs but only its own device nodes), narrowed by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES (indices or UUIDs) when set. Reads sysfs
+    and device-node permissions only; never opens a GPU context."""
+    devs = backend.devices()
+    if cpu:
+        return devs
+    usable = [d for d in devs if d.render_minor < 0 or os.access(f"/dev/dri/renderD{d.render_minor}", os.R_OK | os.W_OK)]
+    devs = usable or devs
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        sel = os.environ.get(var)
+        if sel is None:
+            continue
+        picked = []
+        for tok in (t.strip() for t in sel.split(",") if t.strip()):
+            if tok.isdigit():
+                if int(tok) < len(devs):
+                    picked.append(devs[int(tok)])
+            else:
+                picked += [d for d in devs if d.uuid == tok]
+        devs = picked
+    return devs
+
+
+def free_port_range(span=32):
+    """A free port P on 127.0.0.1 whose next ``span`` ports are free as well: the ranks'
+    worker process groups sit on MASTER_PORT+1, +2, ... (one per mode and probe)."""
+    import socket
+    for _ in range(200):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        if p + span >= 65536:
+            continue
+        ok = True
+        for q in range(p + 1, p + span + 1):
+            t = socket.socket()
+            try:
+                t.bind(("127.0.0.1", q))
+            except OSError:
+                ok = False
+            finally:
+                t.close()
+            if not ok:
+                break
+        if ok:
+            return p
+    raise SystemExit("bench: no free port range on 127.0.0.1 for the ranks")
+
+
+def self_launch(args, argv):
+    """``--gpus N > 1`` without a launcher: this process (which never touches a GPU) starts
+    the N ranks itself under torch.distributed.run - one rank per GPU, rendezvous on
+    127.0.0.1 - and exits with their exit code; rank 0 prints the line. A job asking for
+    more GPUs than are visible is refused (non-zero exit), never measured on fewer."""
+    devices = visible_devices(make_backend(args.cpu_rehearsal, args.gpus), args.cpu_rehearsal)
+    if args.gpus > len(devices):
+        print(f"bench: --gpus {args.gpus} but only {len(devices)} GPU(s) visible to this job "
+              f"({', '.join(d.uuid for d in devices) or 'none'}); refusing to report a smaller job",
+              file=sys.stderr, flush=True)
+        return 2
+    port = int(os.environ.get("MASTER_PORT", 0) or 0) or free_port_range()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    print(f"[bench] launching {args.gpus} ranks (torch.distributed.run, master 127.0.0.1:{port})",
+          file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
     if args.worker:
         return worker(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args, argv)
     from amdvgpu.models.aibench import get_case
-    from amdvgpu.plugin.devices import FakeBackend, SysfsBackend
     from amdvgpu.plugin.kubelet_stub import NodeHarness
 
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -668,10 +758,11 @@ def main(argv=None):
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     cpu = args.cpu_rehearsal
-    backend = FakeBackend(n=max(world, 1)) if cpu else SysfsBackend()
-    devices = backend.devices()
-    if local >= len(devices):
-        raise SystemExit(f"LOCAL_RANK {local} but only {len(devices)} GPUs")
+    backend = make_backend(cpu, world)
+    devices = visible_devices(backend, cpu)
+    if world > len(devices):
+        # every rank refuses alike, so none waits on a rendezvous the others never reach
+        raise SystemExit(f"bench: WORLD_SIZE {world} but only {len(devices)} GPU(s) visible to this job")
     uuid = devices[local].uuid
     base_port = int(os.environ.get("MASTER_PORT", 29500))
     modes = [m for m in args.modes.split(",") if m]

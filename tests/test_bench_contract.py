@@ -96,6 +96,56 @@ def test_node_point_survives_a_failing_rank(tmp_path):
     assert node["gpus_measured"] == 1 and len(node["failures"]) == 1 and node["vgpus"] == 8, node
 
 
+@pytest.mark.slow
+def test_bench_self_launches_its_ranks(tmp_path):
+    """``python bench.py --gpus N`` with no launcher (how the driver may call it on an 8-GPU
+    node) starts the N ranks itself: the line says n_gpus N, every rank ran its own pods
+    and the node point covers all N GPUs."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4", "--steps", "2", "--warmup", "1",
+           "--sweep-seconds", "1", "--cpu-rehearsal"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1", VGPU_BENCH_CONTRACT_DIR=str(tmp_path))
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 4 and r["config"]["global_batch"] == 200 and r["steps"] == 2 and r["warmup"] == 1
+    assert r["node"]["vgpus"] == 16 and r["node"]["gpus_measured"] == 4, r["node"]
+    assert r["rccl_allreduce_between_pods"]["vgpu"]["ok"]
+    ranks = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(4)]
+    assert sorted(x["local_rank"] for x in ranks) == [0, 1, 2, 3] and len({x["uuid"] for x in ranks}) == 4
+
+
+@pytest.mark.parametrize("fake", [True, False])
+def test_bench_refuses_more_gpus_than_visible(fake):
+    """--gpus N beyond the GPUs this job can see exits non-zero with a message, instead of
+    quietly measuring fewer GPUs under an n_gpus it did not run (this container has no GPU:
+    the sysfs inventory is empty; the rehearsal fakes a 1-GPU node)."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    if fake:
+        cmd.append("--cpu-rehearsal")
+        env["VGPU_BENCH_FAKE_GPUS"] = "1"
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=REPO)
+    assert p.returncode != 0 and "refusing" in p.stderr, p.stderr
+    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+def test_visible_devices_honours_rocr_visible_devices(monkeypatch):
+    sys.path.insert(0, REPO)
+    import bench
+    from amdvgpu.plugin.devices import FakeBackend
+    be = FakeBackend(n=4)
+    uu = [d.uuid for d in be.devices()]
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", f"2,{uu[0]}")
+    # FakeBackend devices have no render node: all usable, then narrowed by the variable
+    assert [d.uuid for d in bench.visible_devices(be, cpu=False)] == [uu[2], uu[0]]
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    assert len(bench.visible_devices(be, cpu=False)) == 4
+
+
 def test_sweep_respects_the_time_budget(monkeypatch):
     """The driver kills bench.py at its own limit: sweep points that would not finish within
     --time-budget are skipped and reported, and max_vgpus_per_gpu only counts measured points."""
