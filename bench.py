@@ -362,12 +362,19 @@ def ledger_kw(args):
     return {} if args.ledger is None else {"ledger": args.ledger}
 
 
+# The job's own device selection (e.g. HIP_VISIBLE_DEVICES=0..7 on an 8-GPU node) indexes
+# the node's GPUs; inside a pod (ROCR_VISIBLE_DEVICES = its GPU) those indices mean nothing.
+HOST_SELECTORS = ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
+
+
 def pod_env(node, ids, extra=None):
     """(process env, contract envs) for a container holding vGPUs ``ids``."""
     from amdvgpu.shim.launcher import apply_contract
     envs, mounts = node.pod(ids)
     env = apply_contract(envs, mounts)
     env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    for k in HOST_SELECTORS:  # a container starts without the host job's device selection
+        env.pop(k, None)
     if extra:
         env.update(extra)
     return env, envs
@@ -376,6 +383,8 @@ def pod_env(node, ids, extra=None):
 def native_env(uuid, cpu):
     env = dict(os.environ)
     env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    for k in HOST_SELECTORS:
+        env.pop(k, None)
     if not cpu:
         env["ROCR_VISIBLE_DEVICES"] = uuid  # the official plugin exposes the GPU the same way
     return env
@@ -681,9 +690,9 @@ def visible_devices(backend, cpu):
     usable = [d for d in devs if d.render_minor < 0 or os.access(f"/dev/dri/renderD{d.render_minor}", os.R_OK | os.W_OK)]
     devs = usable or devs
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
-        sel = os.environ.get(var)
-        if sel is None:
-            continue
+        sel = os.environ.get(var, "").strip()
+        if not sel:
+            continue  # unset or empty: no narrowing
         picked = []
         for tok in (t.strip() for t in sel.split(",") if t.strip()):
             if tok.isdigit():
