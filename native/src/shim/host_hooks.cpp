@@ -37,16 +37,14 @@ bool charge_host(size_t size) {
   return false;
 }
 
-// Records one more pin of `size` bytes at `p` (an allocation, or a lock of a user range).
+// Records one more pin of `size` bytes at `p` (an allocation, or a lock of a user range):
+// a re-lock of a pinned address keeps its own size, so the unlocks refund what was charged.
 void record_host(void* p, uint64_t size) {
   ShimState& s = shim();
   std::lock_guard<std::mutex> g(s.alloc_mu);
-  auto it = s.host.find(reinterpret_cast<uintptr_t>(p));
-  if (it == s.host.end()) {
-    s.host[reinterpret_cast<uintptr_t>(p)] = HostRec{size, 1};
-  } else {
-    it->second.n++;
-  }
+  HostRec& h = s.host[reinterpret_cast<uintptr_t>(p)];
+  h.pins.push_back(size);
+  h.total += size;
 }
 
 bool accounting() {
@@ -95,14 +93,14 @@ void put_host(void* p, const HostRec& rec) {
   ShimState& s = shim();
   std::lock_guard<std::mutex> g(s.alloc_mu);
   HostRec& h = s.host[reinterpret_cast<uintptr_t>(p)];
-  if (!h.n) h.each = rec.each;
-  h.n += rec.n;
+  h.pins.insert(h.pins.begin(), rec.pins.begin(), rec.pins.end());
+  h.total += rec.total;
 }
 
 uint64_t host_recorded_bytes() {
   ShimState& s = shim();
   uint64_t n = 0;
-  for (const auto& kv : s.host) n += kv.second.each * kv.second.n;
+  for (const auto& kv : s.host) n += kv.second.total;
   return n;
 }
 
@@ -138,29 +136,32 @@ hsa_status_t hsa_amd_memory_lock_to_pool(void* host_ptr, size_t size, hsa_agent_
   return st;
 }
 
-// One lock less: the record is taken before the real unlock (a concurrent lock of the same
-// address must not find it half-released) and put back if the runtime refused.
+// One lock less: the latest pin's record is taken before the real unlock (a concurrent lock
+// of the same address must not find it half-released), its own size refunded, and put back
+// if the runtime refused. lock(p, 2G), lock(p, 1G), unlock, unlock refunds 1G then 2G.
 hsa_status_t hsa_amd_memory_unlock(void* host_ptr) {
   VGPU_REAL_HSA(hsa_amd_memory_unlock);
   if (!real_hsa_amd_memory_unlock) return HSA_STATUS_ERROR;
   ShimState& s = shim();
   if (!host_ptr || s.phase.load(std::memory_order_acquire) != 2) return real_hsa_amd_memory_unlock(host_ptr);
-  uint64_t each = 0;
+  uint64_t pin = 0;
   {
     std::lock_guard<std::mutex> g(s.alloc_mu);
     auto it = s.host.find(reinterpret_cast<uintptr_t>(host_ptr));
-    if (it != s.host.end()) {
-      each = it->second.each;
-      if (--it->second.n == 0) s.host.erase(it);
+    if (it != s.host.end() && !it->second.pins.empty()) {
+      pin = it->second.pins.back();
+      it->second.pins.pop_back();
+      it->second.total -= pin;
+      if (it->second.pins.empty()) s.host.erase(it);
     }
   }
   hsa_status_t st = real_hsa_amd_memory_unlock(host_ptr);
-  if (!each) return st;
+  if (!pin) return st;
   if (st != HSA_STATUS_SUCCESS) {
-    record_host(host_ptr, each);
+    record_host(host_ptr, pin);
     return st;
   }
-  if (s.slot >= 0 && !s.exiting.load()) s.region.uncharge_host(s.slot, each);
+  if (s.slot >= 0 && !s.exiting.load()) s.region.uncharge_host(s.slot, pin);
   return st;
 }
 

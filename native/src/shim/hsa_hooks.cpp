@@ -175,8 +175,8 @@ static hsa_status_t release_and_free(void* ptr, hsa_status_t (*real_free)(void*)
   if (!ptr || s.phase.load(std::memory_order_relaxed) != 2) return real_free(ptr);
   if (spill_release(ptr)) return HSA_STATUS_SUCCESS;
   const uintptr_t key = reinterpret_cast<uintptr_t>(ptr);
-  AllocRec rec;
-  HostRec host{0, 0};
+  AllocRec rec{0, -1, 0};
+  HostRec host;
   const bool dev_mem = take_alloc(key, &rec);
   const bool pinned = !dev_mem && take_host(ptr, &host);  // pinned host memory (host_hooks.cpp)
   hsa_status_t st = real_free(ptr);
@@ -191,7 +191,7 @@ static hsa_status_t release_and_free(void* ptr, hsa_status_t (*real_free)(void*)
     if (rec.kind == kMemSpill) s.region.uncharge_host(s.slot, rec.size);  // a pinned spill
     else notify_device_memory_freed();
   }
-  if (pinned) s.region.uncharge_host(s.slot, host.each * host.n);
+  if (pinned) s.region.uncharge_host(s.slot, host.total);
   return st;
 }
 
@@ -229,7 +229,9 @@ hsa_status_t hsa_memory_allocate(hsa_region_t region, size_t size, void** ptr) {
     hsa_status_t st = real_hsa_memory_allocate(region, size, ptr);
     if (st == HSA_STATUS_SUCCESS && ptr && *ptr) {
       std::lock_guard<std::mutex> g(s.alloc_mu);
-      s.host[reinterpret_cast<uintptr_t>(*ptr)] = HostRec{size, 1};
+      HostRec& h = s.host[reinterpret_cast<uintptr_t>(*ptr)];
+      h.pins.push_back(size);
+      h.total += size;
     } else {
       s.region.uncharge_host(s.slot, size);
     }
@@ -382,7 +384,7 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
   ShimState& s = shim();
   AgentInfo& a = s.agents[dev];
   {
-    std::lock_guard<std::mutex> g(s.alloc_mu);
+    std::lock_guard<std::mutex> g(s.queue_mu);
     s.queues[reinterpret_cast<uintptr_t>(*queue)] = dev;
   }
   if (a.mask_active.load()) {
@@ -420,7 +422,7 @@ hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* queue, uint32_t num_cu
   ShimState& s = shim();
   int dev = -1;
   {
-    std::lock_guard<std::mutex> g(s.alloc_mu);
+    std::lock_guard<std::mutex> g(s.queue_mu);
     auto it = s.queues.find(reinterpret_cast<uintptr_t>(queue));
     if (it != s.queues.end()) dev = it->second;
   }
@@ -449,7 +451,8 @@ namespace vgpu {
 namespace {
 
 // Packets of this process's queues on `dev` the CP has not consumed yet. The queue map's
-// lock keeps hsa_queue_destroy (which erases under it first) from freeing a queue while
+// own lock (not the allocation lock: this runs on every gated launch of a crowded GPU)
+// keeps hsa_queue_destroy (which erases under it first) from freeing a queue while
 // its indices are read.
 uint64_t queued_packets(int dev) {
   VGPU_REAL_HSA(hsa_queue_load_write_index_relaxed);
@@ -457,7 +460,7 @@ uint64_t queued_packets(int dev) {
   if (!real_hsa_queue_load_write_index_relaxed || !real_hsa_queue_load_read_index_relaxed) return 0;
   ShimState& s = shim();
   uint64_t n = 0;
-  std::lock_guard<std::mutex> g(s.alloc_mu);
+  std::lock_guard<std::mutex> g(s.queue_mu);
   for (const auto& q : s.queues) {
     if (q.second != dev) continue;
     const hsa_queue_t* h = reinterpret_cast<const hsa_queue_t*>(q.first);
@@ -495,7 +498,7 @@ hsa_status_t hsa_queue_destroy(hsa_queue_t* queue) {
   if (!real_hsa_queue_destroy) return HSA_STATUS_ERROR;
   ShimState& s = shim();
   if (s.phase.load(std::memory_order_relaxed) == 2) {
-    std::lock_guard<std::mutex> g(s.alloc_mu);
+    std::lock_guard<std::mutex> g(s.queue_mu);
     s.queues.erase(reinterpret_cast<uintptr_t>(queue));
   }
   return real_hsa_queue_destroy(queue);

@@ -189,8 +189,14 @@ void on_signal_resume(int) {
 // not be copied half-updated, and the child (which has only the forking thread) must not
 // inherit a lock that thread can never release. The table's lock is taken around the
 // fork; in the child both locks are re-created unlocked.
-void atfork_prepare() { shim().alloc_mu.lock(); }
-void atfork_parent() { shim().alloc_mu.unlock(); }
+void atfork_prepare() {
+  shim().alloc_mu.lock();
+  shim().queue_mu.lock();
+}
+void atfork_parent() {
+  shim().queue_mu.unlock();
+  shim().alloc_mu.unlock();
+}
 
 void atfork_child() {
   // A forked child is a different process: it must not inherit the parent's slot
@@ -200,6 +206,7 @@ void atfork_child() {
   new (&s.alloc_mu) std::mutex();  // held by this thread since atfork_prepare
   new (&s.live_mu) std::mutex();   // may be held by a parent thread that does not exist here
   new (&s.ctx_mu) std::mutex();
+  new (&s.queue_mu) std::mutex();  // held by this thread since atfork_prepare
   s.slot = -1;
   s.active = false;
   s.allocs.clear();
@@ -778,7 +785,7 @@ void apply_live_config() {
       // old mask); new queues pick the mask up in hsa_queue_create.
       std::vector<hsa_queue_t*> qs;
       {
-        std::lock_guard<std::mutex> q(s.alloc_mu);
+        std::lock_guard<std::mutex> q(s.queue_mu);
         for (auto& kv : s.queues)
           if (kv.second == i) qs.push_back(reinterpret_cast<hsa_queue_t*>(kv.first));
       }

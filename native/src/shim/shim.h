@@ -16,6 +16,7 @@
 #include <map>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 #include "vgpu/config.h"
 #include "vgpu/cumask.h"
@@ -69,11 +70,13 @@ struct SvmRec {
   uint64_t retry_ns;  // a failed promotion is not retried before this time
 };
 
-// Pinned host memory of this process (host_hooks.cpp): a CPU-pool allocation (n = 1) or a
-// locked user range (n = times locked). Charged to the host budget `each` bytes per count.
+// Pinned host memory of this process at one address (host_hooks.cpp): a CPU-pool allocation
+// (one pin) or a user range locked once or more, each lock with its own size. Every pin is
+// charged to the host budget by its own size; an unlock releases the latest pin (LIFO), a
+// free all of them.
 struct HostRec {
-  uint64_t each;
-  uint32_t n;
+  uint64_t total = 0;           // bytes charged for the pins below
+  std::vector<uint64_t> pins;   // each pin's size, oldest first
 };
 
 // A piece of a tenant's own SVM range (svm_hooks.cpp, hsa_amd_svm_attributes_set /
@@ -104,7 +107,9 @@ struct ShimState {
   std::unordered_map<uintptr_t, HostRec> host;      // pinned host memory (host_hooks.cpp)
   hsa_amd_memory_pool_t cpu_pools[kMaxAgentPools]{};  // global pools of the CPU agents (pinned host memory)
   int n_cpu_pools = 0;
-  std::unordered_map<uintptr_t, int> queues;        // hsa_queue_t* → ordinal
+  std::unordered_map<uintptr_t, int> queues;        // hsa_queue_t* → ordinal (under queue_mu)
+  std::mutex queue_mu;                              // the queue map only: the crowded launch path reads
+                                                    // it (wait_queue_depth) without meeting allocations
   std::unordered_map<uintptr_t, SvmRec> svm;        // SVM-backed spills (spill.cpp) → record
   std::mutex svm_mu;                                // serialises promotions with the frees of SVM spills
   int64_t svm_hbm[kMaxDevices] = {};                // promoted SVM bytes per device (under ctx_mu)

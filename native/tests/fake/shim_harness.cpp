@@ -54,7 +54,8 @@
 //   hsahost=SIZE     hsa_amd_memory_pool_allocate on the CPU pool, as a direct ROCr caller
 //                    (ctypes) would: {"hsahost": status}; hsahostfree frees the last one
 //   hsalock=SIZE     hsa_amd_memory_lock of a fresh heap buffer: {"hsalock": status};
-//                    hsaunlock unlocks (and frees) the last one
+//                    hsaunlock unlocks (and frees) the last one; relock=SIZE locks the last
+//                    locked buffer again with its own size
 //   hostusage        the container's pinned host memory: {"hostusage": bytes}
 //   hsamemfree       hsa_memory_free of the most recent allocation: {"hsamemfree": status}
 //   waitsig=MS       a blocking hsa_signal_wait_scacquire on a signal another thread completes
@@ -483,12 +484,22 @@ int main(int argc, char** argv) {
       if (st == 0) hsa_locked.push_back(p);
       else free(p);
       printf("{\"hsalock\": %d}\n", st);
+    } else if (key == "relock") {
+      // the last locked buffer locked once more, with a size of its own
+      int st = -1;
+      void* agent_ptr = nullptr;
+      if (!hsa_locked.empty()) {
+        st = (int)hsa_amd_memory_lock(hsa_locked.back(), (size_t)parse_size(val.c_str()), nullptr, 0, &agent_ptr);
+        if (st == 0) hsa_locked.push_back(hsa_locked.back());
+      }
+      printf("{\"relock\": %d}\n", st);
     } else if (key == "hsaunlock") {
       int st = -1;
       if (!hsa_locked.empty()) {
-        st = (int)hsa_amd_memory_unlock(hsa_locked.back());
-        free(hsa_locked.back());
+        void* p = hsa_locked.back();
+        st = (int)hsa_amd_memory_unlock(p);
         hsa_locked.pop_back();
+        if (std::find(hsa_locked.begin(), hsa_locked.end(), p) == hsa_locked.end()) free(p);  // its last lock
       }
       printf("{\"hsaunlock\": %d}\n", st);
     } else if (key == "hostusage") {

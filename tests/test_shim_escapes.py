@@ -122,6 +122,24 @@ def test_direct_rocr_pinned_memory_is_held_to_the_host_budget(fake):
     assert _vals(out, "hostusage") == [60 * MiB, 0, 40 * MiB], out
 
 
+def test_relocked_address_refunds_each_pin_by_its_own_size(fake):
+    """A pinned address locked again with another size: each unlock refunds the size of the
+    pin it releases (the latest first), so lock(p, 2x), lock(p, x), unlock, unlock leaves the
+    host budget where it started, in either order of sizes, and 100 such cycles never let
+    the tenant pin past VGPU_HOST_MEMORY_LIMIT."""
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g", VGPU_HOST_MEMORY_LIMIT="64m")
+    out = run(e, "hsalock=20m", "relock=10m", "hostusage", "hsaunlock", "hostusage", "hsaunlock", "hostusage",
+              "hsalock=10m", "relock=20m", "hsaunlock", "hostusage", "hsaunlock", "hostusage")
+    assert _vals(out, "hsalock") == [0, 0] and _vals(out, "relock") == [0, 0], out
+    assert _vals(out, "hostusage") == [30 * MiB, 20 * MiB, 0, 10 * MiB, 0], out
+    ops = []
+    for _ in range(100):
+        ops += ["hsalock=20m", "relock=10m", "hsaunlock", "hsaunlock"]
+    out = run(e, *ops, "hostusage", "hsalock=40m", "relock=30m", "hostusage")
+    assert _vals(out, "hostusage") == [0, 40 * MiB], out
+    assert _vals(out, "relock")[-1] == OOR, out  # 40 + 30 > 64 MiB: the budget still holds
+
+
 def test_hip_pinned_memory_is_charged_once(fake):
     """hipHostMalloc and hipHostRegister reach ROCr's pool allocation and memory lock: each is
     charged exactly once (not again at the HIP layer), and hipFree of pinned memory releases it."""
