@@ -15,8 +15,9 @@
 // acquire-loads and nanosleeps; an active wait with a short time-out (HIP's brief spin before
 // it blocks) stays as it is; the sleep grows with the time already waited (1/8 of
 // it, 20 us to 500 us), so a wait overshoots its completion by at most ~12 % (and 0.5 ms),
-// and a multi-millisecond wait costs a few dozen wake-ups instead of a core. A lone pod keeps
-// ROCr's own wait (no added latency); VGPU_SYNC_WAIT=poll|native forces either way.
+// and a multi-millisecond wait costs a few dozen wake-ups instead of a core. A lone pod, and
+// a pod of the latency class (priority 0), keeps ROCr's own wait (no added latency);
+// VGPU_SYNC_WAIT=poll|native forces either way.
 #include <time.h>
 
 #include <algorithm>
@@ -52,7 +53,13 @@ bool satisfied(hsa_signal_condition_t c, hsa_signal_value_t v, hsa_signal_value_
   }
 }
 
-// Whether this process's waits should poll now.
+// Whether this process's waits should poll now. The latency class (task priority 0: a
+// request-serving pod next to batch tenants) keeps ROCr's own wait - a polled wait may
+// overshoot its completion by up to 1/8 of it, which such a pod's tail latency would pay;
+// its one spinning core is the price of its class. Otherwise the device the wait is for
+// decides: in a multi-GPU container, the calling thread's current HIP device (HIP's
+// synchronisations wait in the calling thread), so a crowded GPU does not make the waits
+// for an uncrowded one poll.
 bool poll_now() {
   const SyncWait m = config().sync_wait;
   if (m == SyncWait::kPoll) return true;
@@ -60,9 +67,12 @@ bool poll_now() {
   ShimState& s = shim();
   if (!s.active || s.phase.load(std::memory_order_relaxed) != 2) return false;
   const Region* r = s.region.raw();
-  for (int d = 0; d < s.n_agents; d++)
-    if (r->dev[d].crowd.load(std::memory_order_relaxed) > kAutoSpatialMaxCrowd) return true;
-  return false;
+  if (effective_priority(r) <= 0) return false;
+  bool any = false;
+  for (int d = 0; d < s.n_agents; d++) any |= r->dev[d].crowd.load(std::memory_order_relaxed) > kAutoSpatialMaxCrowd;
+  if (!any || s.n_agents == 1) return any;
+  const int d = current_hip_agent();
+  return d >= 0 && d < s.n_agents && r->dev[d].crowd.load(std::memory_order_relaxed) > kAutoSpatialMaxCrowd;
 }
 
 }  // namespace

@@ -404,8 +404,10 @@ void sample_tick(Region* r, Sampler& sm) {
       // On the limiter of a crowded GPU (three or more processes on it), a bounded queue
       // (VGPU_CROWD_DEPTH) keeps each pod's debt to a few kernels: the credit gate then paces
       // it kernel by kernel instead of admitting a whole synchronize-to-synchronize batch at
-      // once (profiles/r5c). A pod alone under a GPU-time limit keeps its full queue.
-      const int cap = sm.procs > 2 ? config().crowd_depth : 0;
+      // once (profiles/r5c). A pod alone under a GPU-time limit keeps its full queue. Counted
+      // on this GPU: a crowded GPU of a multi-GPU container does not bound the others.
+      const int on_gpu = (int)(sm.mine.size() + sm.others[d].size());
+      const int cap = on_gpu > 2 ? config().crowd_depth : 0;
       if (ds.depth_cap.load(std::memory_order_relaxed) != cap) ds.depth_cap.store(cap, std::memory_order_relaxed);
     }
     sm.opened[d] = was_closed && ds.gate_open.load(std::memory_order_relaxed);

