@@ -242,11 +242,12 @@ class DevicePluginServer:
         out = []
         for v in self.vdevices:
             d = api.Device(ID=v.id, health=api.HEALTHY if v.dev.healthy else api.UNHEALTHY)
-            # --numa-spread: the CPU node the container's processes will run on, so that a
-            # topology-aware kubelet gives an exclusive-CPU pod its CPUs there too
-            node = v.cpu_node if v.cpu_node >= 0 else v.dev.numa_node
-            if node >= 0:
-                d.topology.nodes.add(ID=node)
+            # The GPU's own PCIe NUMA node: what a topology-aware kubelet aligns an exclusive-CPU
+            # pod's CPUs and memory with. The --numa-spread CPU node is a placement inside the
+            # shared pool and travels in the contract only (VGPU_CPU_NODE); the shim keeps an
+            # exclusive cpuset whole (native/src/shim/numa_spread.cpp).
+            if v.dev.numa_node >= 0:
+                d.topology.nodes.add(ID=v.dev.numa_node)
             out.append(d)
         return out
 

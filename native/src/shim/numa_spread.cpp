@@ -12,9 +12,16 @@
 // - while its only thread is the one that runs the constructors - the process's CPU affinity
 // is narrowed to that node's CPUs. Threads and processes it creates later inherit it.
 //
-// Nothing is narrowed when the allowed CPUs are already within the node (an exclusive cpuset
-// from the kubelet's CPU manager, say), or do not meet it. A tenant opts out with
-// VGPU_CPU_SPREAD=0: this is a placement hint, not a limit.
+// It is a placement within the shared pool, never a cut of CPUs the pod was granted. Nothing is
+// narrowed when
+// * the allowed CPUs are already within the node, or do not meet it;
+// * they are the container's own: the kubelet's CPU manager (static policy) gives a Guaranteed
+//   pod with an integer CPU request an exclusive cpuset of exactly that many CPUs, so a CPU
+//   quota (cgroup cpu.max, or cpu.cfs_quota_us / cpu.cfs_period_us) equal to the allowed
+//   count marks an exclusive set - kept whole even when it spans both sockets;
+// * the node's share of the allowed CPUs is smaller than the container's CPU quota (it would
+//   throttle a CPU-heavy tenant - DataLoader workers, tokenizers - below what it pays for).
+// A tenant opts out with VGPU_CPU_SPREAD=0: this is a placement hint, not a limit.
 #include <sched.h>
 
 #include <cstdio>
@@ -50,6 +57,48 @@ bool parse_cpulist(const char* s, cpu_set_t* out) {
   return any;
 }
 
+bool read_small(const std::string& path, char* buf, size_t n) {
+  FILE* f = fopen(path.c_str(), "re");
+  if (!f) return false;
+  const size_t got = fread(buf, 1, n - 1, f);
+  fclose(f);
+  buf[got] = 0;
+  return got > 0;
+}
+
+// The container's CPU quota in CPUs (rounded up), or -1 when it has none (unlimited, or no
+// cgroup file readable). `fs` is the cgroup mount (/sys/fs/cgroup). Inside a container the
+// cgroup namespace makes its own cgroup the root; otherwise /proc/self/cgroup names it.
+long cpu_quota_cpus(const std::string& fs) {
+  char buf[256];
+  std::string rel;
+  if (FILE* f = fopen("/proc/self/cgroup", "re")) {
+    char line[1024];
+    while (fgets(line, sizeof(line), f))
+      if (strncmp(line, "0::", 3) == 0) {
+        rel = line + 3;
+        while (!rel.empty() && (rel.back() == '\n' || rel.back() == '/')) rel.pop_back();
+      }
+    fclose(f);
+  }
+  long long quota = -1, period = 0;
+  for (const std::string& dir : {fs + rel, fs}) {   // cgroup v2
+    if (!read_small(dir + "/cpu.max", buf, sizeof(buf))) continue;
+    if (strncmp(buf, "max", 3) == 0) return -1;
+    if (sscanf(buf, "%lld %lld", &quota, &period) == 2 && quota > 0 && period > 0) return (long)((quota + period - 1) / period);
+    return -1;
+  }
+  for (const char* ctl : {"/cpu,cpuacct", "/cpu"}) {  // cgroup v1
+    char p[64];
+    if (!read_small(fs + ctl + "/cpu.cfs_quota_us", buf, sizeof(buf))) continue;
+    quota = atoll(buf);
+    if (!read_small(fs + ctl + "/cpu.cfs_period_us", p, sizeof(p))) return -1;
+    period = atoll(p);
+    return quota > 0 && period > 0 ? (long)((quota + period - 1) / period) : -1;
+  }
+  return -1;
+}
+
 __attribute__((constructor)) void numa_spread_ctor() {
   const char* node = getenv("VGPU_CPU_NODE");
   if (!node || !*node) return;
@@ -60,19 +109,23 @@ __attribute__((constructor)) void numa_spread_ctor() {
   if (end == node || n < 0) return;
   log_init_from_env();
   const char* root = getenv("VGPU_SYSFS_ROOT");   // tests: a fake sysfs tree
-  const std::string path = std::string(root && *root ? root : "/sys") + "/devices/system/node/node" +
-                           std::to_string(n) + "/cpulist";
-  FILE* f = fopen(path.c_str(), "re");
-  if (!f) return;
+  const std::string sys = root && *root ? root : "/sys";
   char buf[4096] = {0};
-  const size_t got = fread(buf, 1, sizeof(buf) - 1, f);
-  fclose(f);
-  buf[got] = 0;
+  if (!read_small(sys + "/devices/system/node/node" + std::to_string(n) + "/cpulist", buf, sizeof(buf))) return;
   cpu_set_t want, allowed, both;
   if (!parse_cpulist(buf, &want) || sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
   CPU_AND(&both, &want, &allowed);
   const int nb = CPU_COUNT(&both), na = CPU_COUNT(&allowed);
   if (nb == 0 || nb == na) return;   // no overlap, or already within the node
+  const long quota = cpu_quota_cpus(sys + "/fs/cgroup");
+  if (quota == na) {
+    VLOG_INFO("CPU affinity kept: %d CPUs = the container's CPU quota (an exclusive cpuset)", na);
+    return;
+  }
+  if (quota > nb) {
+    VLOG_INFO("CPU affinity kept: NUMA node %ld holds %d of the allowed CPUs, below the quota of %ld", n, nb, quota);
+    return;
+  }
   if (sched_setaffinity(0, sizeof(both), &both) == 0)
     VLOG_INFO("CPU affinity narrowed to NUMA node %ld: %d of %d allowed CPUs (--numa-spread)", n, nb, na);
 }
