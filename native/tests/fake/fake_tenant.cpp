@@ -20,4 +20,13 @@ unsigned long long tenant_total() {
   return t;
 }
 
+// One launch of a 10-microsecond fake kernel on the null stream, then a synchronize: 0 on
+// success. (The fake's "kernel" is a uint32 duration in microseconds.)
+int tenant_launch() {
+  static uint32_t us = 10;
+  if (hipInit(0) != hipSuccess) return -1;
+  hipError_t e = hipLaunchKernel(&us, dim3(1), dim3(64), nullptr, 0, nullptr);
+  return e != hipSuccess ? (int)e : (int)hipDeviceSynchronize();
+}
+
 }  // extern "C"

@@ -98,3 +98,55 @@ def test_dlmopen_of_the_rocm_runtime_is_refused(env):
 def test_dlmopen_only_logged_outside_a_vgpu_container(env):
     env.pop("VGPU_DEVICE_MEMORY_LIMIT")
     assert child(env, DLMOPEN) == {"hip": True, "other": True}
+
+
+TENANT_AFTER_HIP = """
+import threading, time
+hip = ctypes.CDLL(os.path.join(FAKE, "libamdhip64.so"), mode=os.RTLD_NOW | os.RTLD_GLOBAL)  # torch's HIP
+hip.hipInit(0)
+t = ctypes.CDLL(os.path.join(FAKE, "libfaketenant.so"), mode=os.RTLD_NOW | DEEP)
+t.tenant_total.restype = ctypes.c_ulonglong
+me = ctypes.CDLL(None)
+assert t.tenant_launch() == 0
+me.vgpu_suspend_all()
+threading.Timer(0.15, me.vgpu_resume_all).start()
+t0 = time.time()
+rc = t.tenant_launch()
+blocked = time.time() - t0
+print(json.dumps(dict(rc=rc, blocked=blocked, total=t.tenant_total(), big=t.tenant_malloc(ctypes.c_ulonglong(3 << 30)))))
+"""
+
+
+def test_deepbind_tenant_module_after_hip_is_gated(env):
+    """The usual order: HIP is already loaded (torch imported) when a tenant module
+    that links HIP is loaded with RTLD_DEEPBIND. Its hip* imports would bind to HIP ahead of the
+    shim; they are rebound, so its launches pass the launch gate (held while the container is
+    suspended) and its memory queries see the quota."""
+    r = child(env, TENANT_AFTER_HIP)
+    assert r["rc"] == 0 and r["blocked"] >= 0.12, r
+    assert r["total"] == 2 * GiB and r["big"] == 2, r
+
+
+def test_deepbind_tenant_module_after_hip_escapes_without_the_hooks(env):
+    env["VGPU_HOOK_DLSYM"] = "0"
+    r = child(env, TENANT_AFTER_HIP)
+    assert r["rc"] == 0 and r["blocked"] < 0.1, r   # control: the launch skipped the gate
+
+
+BARE_NAME = """
+import shutil, tempfile
+d = tempfile.mkdtemp()
+# a loader library with RUNPATH=$ORIGIN next to the tenant module: its DEEPBIND dlopen of the
+# bare name must still find the module (the caller's RUNPATH), with ROCm loaded
+hip = ctypes.CDLL(os.path.join(FAKE, "libamdhip64.so"), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+for f in ("libfaketenant.so", "libdeeploader.so"):
+    shutil.copy(os.path.join(FAKE, f), d)
+ld = ctypes.CDLL(os.path.join(d, "libdeeploader.so"))
+ld.deep_open.restype = ctypes.c_void_p
+h = ld.deep_open(b"libfaketenant.so", DEEP | 2)
+print(json.dumps(dict(found=bool(h))))
+"""
+
+
+def test_deepbind_bare_name_uses_the_callers_runpath(env):
+    assert child(env, BARE_NAME) == {"found": True}
