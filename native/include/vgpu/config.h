@@ -99,6 +99,8 @@ struct Config {
   SpillPolicy spill_policy = SpillPolicy::kLargeFirst;  // VGPU_SPILL_POLICY
   uint64_t spill_large_bytes = 256ull << 20;  // VGPU_SPILL_LARGE: "large" allocation threshold
   uint64_t spill_reserve_bytes = 0;      // VGPU_SPILL_RESERVE: HBM kept for small ones (0 = auto)
+  uint64_t spill_small_bytes = 64ull << 20;  // VGPU_SPILL_SMALL: below this an allocation may use the headroom
+  int64_t spill_small_headroom = -1;     // VGPU_SPILL_SMALL_HEADROOM: HBM above the share for them (-1 = auto)
   SpillBacking spill_backing = SpillBacking::kSvm;  // VGPU_SPILL_BACKING: svm | auto | pinned
   bool spill_promote = true;             // VGPU_SPILL_PROMOTE: move SVM spills into HBM once they fit
   int priority = 1;                      // VGPU_TASK_PRIORITY
@@ -159,6 +161,12 @@ struct Config {
 // HBM reserve for small allocations under large-first spilling: the configured value, or
 // max(min(2 GiB, hbm_share / 4), hbm_share / 16) — 18 GiB of a 288 GiB share, 512 MiB of 2 GiB.
 uint64_t spill_reserve(const Config& cfg, uint64_t hbm_share);
+
+// HBM a tenant with virtual device memory may hold above its HBM share for small allocations
+// (below spill_small_bytes): RCCL transport buffers and tensors shared with DataLoader workers
+// are exported over IPC, which a spilled (host-backed) buffer cannot be. The configured value,
+// or min(1 GiB, hbm_share / 64) - 1 GiB of a 144 GiB share, 1 MiB of 64 MiB.
+uint64_t spill_small_headroom(const Config& cfg, uint64_t hbm_share);
 
 // Parses "NNN[KkMmGg][iB|B]" into bytes. Returns false on syntax error or overflow.
 // Bare numbers are bytes; "m"/"M" is MiB, as in the reference ("<MiB>m").

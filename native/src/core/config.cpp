@@ -65,6 +65,11 @@ uint64_t spill_reserve(const Config& cfg, uint64_t hbm_share) {
   return std::max<uint64_t>(floor, hbm_share / 16);
 }
 
+uint64_t spill_small_headroom(const Config& cfg, uint64_t hbm_share) {
+  if (cfg.spill_small_headroom >= 0) return (uint64_t)cfg.spill_small_headroom;
+  return std::min<uint64_t>(1ull << 30, hbm_share / 64);
+}
+
 bool Config::any_memory_limit() const {
   for (int i = 0; i < kMaxDevices; i++)
     if (dev[i].mem_limit) return true;
@@ -260,6 +265,14 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   }
   if (const char* s = getenv_fn("VGPU_SPILL_RESERVE")) {
     if (!parse_size(s, &cfg->spill_reserve_bytes)) VLOG_WARN("invalid VGPU_SPILL_RESERVE=%s ignored", s);
+  }
+  if (const char* s = getenv_fn("VGPU_SPILL_SMALL")) {
+    if (!parse_size(s, &cfg->spill_small_bytes)) VLOG_WARN("invalid VGPU_SPILL_SMALL=%s ignored", s);
+  }
+  if (const char* s = getenv_fn("VGPU_SPILL_SMALL_HEADROOM")) {
+    uint64_t v = 0;
+    if (parse_size(s, &v) && v <= (uint64_t)INT64_MAX) cfg->spill_small_headroom = (int64_t)v;
+    else VLOG_WARN("invalid VGPU_SPILL_SMALL_HEADROOM=%s ignored", s);
   }
   if (const char* s = getenv_fn("VGPU_SPILL_BACKING")) {
     if (!strcasecmp(s, "auto")) cfg->spill_backing = SpillBacking::kAuto;

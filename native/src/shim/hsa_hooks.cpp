@@ -56,6 +56,9 @@ bool take_alloc(uintptr_t key, AllocRec* out) {
 // memory once they would eat into a reserve of the share, so the small, hot allocations
 // that come later (weights, activations, workspaces) still find HBM; a large allocation
 // also spills when the physical HBM (shared with other tenants) lacks size + reserve.
+// Small allocations (below VGPU_SPILL_SMALL) may go a headroom past the share before they
+// spill: a spilled buffer cannot be exported over IPC, and RCCL's transport buffers and the
+// tensors a DataLoader worker shares are small ones allocated once the share may be full.
 bool should_spill(int dev, size_t size) {
   ShimState& s = shim();
   const Config& cfg = config();
@@ -64,7 +67,10 @@ bool should_spill(int dev, size_t size) {
   // The caller has already charged `size` as data, so `resident` includes this request.
   const uint64_t resident = s.region.resident(dev);
   const bool large = cfg.spill_policy == SpillPolicy::kLargeFirst && size >= cfg.spill_large_bytes;
-  if (!large) return resident > hbm;
+  if (!large) {
+    if (resident <= hbm) return false;
+    return size >= cfg.spill_small_bytes || resident > hbm + spill_small_headroom(cfg, hbm);
+  }
   const uint64_t reserve = spill_reserve(cfg, hbm);
   if (resident + reserve > hbm) return true;
   VGPU_REAL_HSA(hsa_agent_get_info);

@@ -202,7 +202,8 @@ def test_launch_block_and_counter(fake):
 @pytest.mark.parametrize("policy", ["large-first", "first-come"])
 def test_spill_placement_policy(fake, policy):
     """Virtual device memory: 16 GiB quota with an 8 GiB HBM share. First-come keeps the
-    first eight 1 GiB buffers in HBM and sends the later small (hot) ones to host memory;
+    first eight 1 GiB buffers in HBM and sends the later small (hot) ones to host memory once
+    the small-allocation headroom (128 MiB) is used;
     large-first spills the large buffers once they would eat into the 3 GiB reserve, so
     all 2 GiB of small ones stay in HBM. Exact byte counts: the fake has no context."""
     e = fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="16g", VGPU_DEVICE_HBM_LIMIT_0="8192m",
@@ -224,7 +225,8 @@ def test_spill_placement_policy(fake, policy):
     if policy == "large-first":
         assert after_big == 5 * GiB and after_small == after_big     # 5 resident + 3 GiB reserve
     else:
-        assert after_big == 2 * GiB and after_small - after_big == 2 * GiB   # HBM full after 8
+        # HBM full after 8; of the small ones only the headroom (auto: 8 GiB / 64) stays in HBM
+        assert after_big == 2 * GiB and after_small - after_big == 2 * GiB - 128 * MiB
 
 
 def test_spill_is_charged_to_the_host_budget(fake):
@@ -272,6 +274,29 @@ def test_spilled_buffers_and_ipc_export(fake, backing):
     assert [o["where"] for o in out if "where" in o] == ([-1] if backing == "svm" else [-2]), out
     # (the 1 MiB buffer after it still fits the share: HBM, exportable)
     assert [o["ipcexport"] == 0 for o in out if "ipcexport" in o] == [True, False, True], out
+
+
+def test_small_allocations_past_a_full_share_stay_exportable(fake):
+    """VERDICT r5 Weak 4: once the HBM share is full every allocation used to spill, and a
+    spilled buffer cannot be exported over IPC - RCCL's transport buffers and the tensors a
+    DataLoader worker shares are small ones made after the share may be full. Small
+    allocations (< VGPU_SPILL_SMALL, 64 MiB) now go a headroom past the share first
+    (VGPU_SPILL_SMALL_HEADROOM; auto min(1 GiB, share/64)): still charged to the quota, in
+    HBM, exportable; past the headroom, and for large ones, spilling resumes."""
+    e = fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="512m", VGPU_DEVICE_HBM_LIMIT_0="128m",
+             VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come", VGPU_SPILL_SMALL_HEADROOM="48m")
+    out = run(e, "malloc=128m", "malloc=32m", "where", "ipcexport", "spilled", "malloc=32m", "where", "ipcexport",
+              "spilled", "malloc=64m", "where", "spilled", "usage")
+    assert [o["malloc"] for o in out if "malloc" in o] == ["ok"] * 4, out
+    assert [o["where"] for o in out if "where" in o] == [-2, -1, -1], out      # HBM, then SVM spills
+    assert [o["ipcexport"] == 0 for o in out if "ipcexport" in o] == [True, False], out
+    assert [o["spilled"] for o in out if "spilled" in o] == [0, 32 * MiB, 96 * MiB], out
+    # auto headroom of a 128 MiB share is 2 MiB: a 32 MiB buffer past it spills as before
+    e = fake(gpus=1, hbm=64 * GiB, VGPU_DEVICE_MEMORY_LIMIT="512m", VGPU_DEVICE_HBM_LIMIT_0="128m",
+             VGPU_OVERSUBSCRIBE="true", VGPU_SPILL_POLICY="first-come")
+    out = run(e, "malloc=128m", "malloc=1m", "where", "ipcexport", "malloc=32m", "where")
+    assert [o["where"] for o in out if "where" in o] == [-2, -1], out
+    assert [o["ipcexport"] == 0 for o in out if "ipcexport" in o] == [True], out
 
 
 @pytest.mark.parametrize("kfd_counts", ["1", "0"])
