@@ -17,7 +17,7 @@ if has build; then
 fi
 if has tests; then
   step tests
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q -rs -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -rs -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
   rc=$?; tail -15 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 fi
 if has smoke; then
