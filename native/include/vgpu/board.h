@@ -17,6 +17,7 @@
 #include <sys/types.h>
 
 #include <atomic>
+#include <cstddef>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -46,8 +47,16 @@ struct alignas(64) BoardSlot {
   std::atomic<uint64_t> want_since[kMaxDevices];  // waiting for admission since (0 = not waiting)
   std::atomic<int32_t> npids;
   std::atomic<int32_t> hostpids[kBoardMaxPids];
+  // Appended after the version-1 fields (a reader accepts a version-1 slot that ends here and
+  // reads them as 0): virtual device memory made visible node-wide.
+  std::atomic<uint64_t> svm_vram[kMaxDevices];     // the container's SVM bytes in each GPU's VRAM
+  std::atomic<uint64_t> hbm_want[kMaxDevices];     // refused HBM within its share: bytes wanted ...
+  std::atomic<uint64_t> hbm_want_ns[kMaxDevices];  // ... since (CLOCK_MONOTONIC; 0 = none)
 };
+constexpr size_t kBoardSlotV1Size = offsetof(BoardSlot, svm_vram);
 
+// An HBM request older than this is over (the requester gave up or was served).
+constexpr uint64_t kBoardWantNs = 3'000'000'000ull;
 // Slot staleness: a slot whose heartbeat is older than this is ignored.
 constexpr uint64_t kBoardStaleNs = 2'000'000'000ull;
 // A publishing container touches its slot file's mtime every kBoardTouchS; readers skip,
@@ -64,6 +73,9 @@ struct BoardPeer {
   std::vector<int> gate;                     // per device
   std::vector<uint64_t> want_since;          // per device
   std::vector<int> hostpids;
+  std::vector<uint64_t> svm_vram;            // per device
+  std::vector<uint64_t> hbm_want;            // per device (0 = none, or stale)
+  std::vector<uint64_t> hbm_want_ns;         // per device: when it was (re-)published
 };
 
 // A container's view of the board directory: its own slot (read-write) and the others.
@@ -89,6 +101,13 @@ class Board {
   void leave();
   // Gate state of device `dev` for the concurrency admission (every sample).
   void publish_gate(int dev, bool open, uint64_t want_since);
+  // Virtual device memory of device `dev`: the container's SVM bytes in VRAM, and HBM it was
+  // refused within its share (0 = none) since `want_ns`.
+  void publish_memory(int dev, uint64_t svm_vram, uint64_t hbm_want, uint64_t want_ns);
+  // Sum over live peers of their SVM bytes in GPU `gpu_id`'s VRAM, and the largest HBM a
+  // peer there is waiting for (requests older than kBoardWantNs are dropped).
+  uint64_t peers_svm_vram(uint32_t gpu_id) const;
+  uint64_t peers_hbm_want(uint32_t gpu_id, uint64_t* newest_ns = nullptr) const;
 
   // Concurrency admission (VGPU_GPU_CONCURRENCY = k): may this container open its gate on
   // GPU `gpu_id`, given it has wanted to since `want_since`? Yes while fewer than k

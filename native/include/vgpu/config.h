@@ -103,6 +103,8 @@ struct Config {
   int64_t spill_small_headroom = -1;     // VGPU_SPILL_SMALL_HEADROOM: HBM above the share for them (-1 = auto)
   SpillBacking spill_backing = SpillBacking::kSvm;  // VGPU_SPILL_BACKING: svm | auto | pinned
   bool spill_promote = true;             // VGPU_SPILL_PROMOTE: move SVM spills into HBM once they fit
+  int demote_wait_ms = 2000;             // VGPU_DEMOTE_WAIT_MS: HBM refused within the quota - wait this
+                                         // long for co-tenants to demote promoted spills (0 = never)
   int priority = 1;                      // VGPU_TASK_PRIORITY
   CuMode cu_mode = CuMode::kAuto;        // VGPU_CU_MODE
   CuPolicy cu_policy = CuPolicy::kDefault;

@@ -50,7 +50,14 @@ struct alignas(64) DeviceUsage {
   std::atomic<uint64_t> total;            // sum of all kinds
   std::atomic<uint64_t> kind[kMemKinds];
   std::atomic<uint64_t> peak;
+  // Bytes of this process's shared virtual memory in the device's VRAM (promoted spills, the
+  // tenant's own prefetched ranges): HBM that ROCr's free-memory figure does not show
+  // (profiles/r4b). Part of `kind[kMemData]`, not added to it. Published on the node board so
+  // other containers see that HBM as taken.
+  std::atomic<uint64_t> svm_vram;
 };
+// svm_vram sits in what was alignment padding in layout v5: the layout is unchanged.
+static_assert(sizeof(DeviceUsage) == 64, "DeviceUsage layout changed");
 
 struct alignas(64) ProcSlot {
   std::atomic<int32_t> pid;               // 0 = free slot
@@ -108,9 +115,20 @@ struct alignas(64) DeviceState {
   // Exact GPU-time share of the limiter's grants, basis points (0 = cu_limit_pct): the
   // plugin's CU limit is a whole percent rounded up, so a split-16 vGPU's 6.25 % is 7 %.
   int32_t cu_share_bp;
+  // Virtual device memory made visible node-wide (written by the container's sampler from the
+  // node board): SVM bytes other containers hold in this GPU's VRAM, which ROCr's free-memory
+  // figure does not show.
+  std::atomic<uint64_t> node_svm_vram;
+  // HBM pressure: this container was refused HBM within its share (hbm_want bytes, at
+  // hbm_want_ns, CLOCK_MONOTONIC) - published on the board so co-tenants demote promoted
+  // spills; and the bytes of its own promoted spills the container was asked to demote for
+  // a co-tenant (its processes' migrators work it off).
+  std::atomic<uint64_t> hbm_want;
+  std::atomic<uint64_t> hbm_want_ns;
+  std::atomic<uint64_t> demote_want;
 };
-// preempt / depth_cap / cu_share_bp sit in what was tail padding in layout v5: the layout
-// is unchanged.
+// preempt / depth_cap / cu_share_bp and the fields after them sit in what was tail padding in
+// layout v5: the layout is unchanged.
 static_assert(sizeof(DeviceState) == 320, "DeviceState layout changed");
 
 struct RegionHeader {
@@ -210,8 +228,11 @@ class SharedRegion {
   // if the container's resident bytes stay within `cap` (0 = no cap) - atomically with
   // respect to concurrent allocations of the container's other processes. False: not moved.
   bool promote_spill(int slot, int dev, uint64_t bytes, uint64_t cap);
-  // The reverse (a promotion that failed after the move): data back to spill.
+  // The reverse (a promotion that failed after the move, or a demotion): data back to spill.
   void demote_to_spill(int slot, int dev, uint64_t bytes);
+  // SVM bytes of `dev` in VRAM: this process's (published by it) and the container's sum.
+  void set_svm_vram(int slot, int dev, uint64_t bytes);
+  uint64_t svm_vram(int dev) const;
 
   // Pinned host memory (page-locked RAM is a node-wide resource the host-spill pool
   // shares): the same CAS admission with reclaim-and-retry as device memory.

@@ -111,6 +111,33 @@ void Board::publish_gate(int dev, bool open, uint64_t want_since) {
   self_->want_since[dev].store(want_since, std::memory_order_relaxed);
 }
 
+void Board::publish_memory(int dev, uint64_t svm_vram, uint64_t hbm_want, uint64_t want_ns) {
+  if (!self_ || dev < 0 || dev >= kMaxDevices) return;
+  self_->svm_vram[dev].store(svm_vram, std::memory_order_relaxed);
+  self_->hbm_want_ns[dev].store(hbm_want ? want_ns : 0, std::memory_order_relaxed);
+  self_->hbm_want[dev].store(hbm_want, std::memory_order_relaxed);
+}
+
+uint64_t Board::peers_svm_vram(uint32_t gpu_id) const {
+  uint64_t n = 0;
+  for (const BoardPeer& p : peers_)
+    for (size_t i = 0; i < p.gpu_ids.size() && i < p.svm_vram.size(); i++)
+      if (p.gpu_ids[i] == gpu_id) n += p.svm_vram[i];
+  return n;
+}
+
+uint64_t Board::peers_hbm_want(uint32_t gpu_id, uint64_t* newest_ns) const {
+  uint64_t n = 0, newest = 0;
+  for (const BoardPeer& p : peers_)
+    for (size_t i = 0; i < p.gpu_ids.size() && i < p.hbm_want.size() && i < p.hbm_want_ns.size(); i++)
+      if (p.gpu_ids[i] == gpu_id && p.hbm_want[i]) {
+        n = std::max(n, p.hbm_want[i]);
+        newest = std::max(newest, p.hbm_want_ns[i]);
+      }
+  if (newest_ns) *newest_ns = newest;
+  return n;
+}
+
 bool Board::waiting(uint32_t gpu_id) const {
   for (const BoardPeer& p : peers_)
     for (size_t i = 0; i < p.gpu_ids.size() && i < p.want_since.size(); i++)
@@ -149,11 +176,13 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
     int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
     if (fd < 0) continue;
     BoardSlot s;
+    memset(static_cast<void*>(&s), 0, sizeof(s));
     // A plain read of a slot another container keeps rewriting: fields may be torn, so
-    // every value is bounds-checked and the heartbeat decides liveness.
+    // every value is bounds-checked and the heartbeat decides liveness. A slot of an older
+    // shim ends after the version-1 fields: the appended ones read as 0.
     const ssize_t got = pread(fd, static_cast<void*>(&s), sizeof(s), 0);
     ::close(fd);
-    if (got != (ssize_t)sizeof(s) || s.magic != kBoardMagic || s.version != kBoardVersion) continue;
+    if (got < (ssize_t)kBoardSlotV1Size || s.magic != kBoardMagic || s.version != kBoardVersion) continue;
     const uint64_t hb = s.heartbeat_ns.load(std::memory_order_relaxed);
     if (!hb || hb > now + kBoardStaleNs || now - hb > kBoardStaleNs) continue;
     BoardPeer p;
@@ -164,6 +193,11 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
       p.masks.emplace_back(s.cu_mask[i], s.cu_mask[i] + kCuMaskWords);
       p.gate.push_back(s.gate[i].load(std::memory_order_relaxed));
       p.want_since.push_back(s.want_since[i].load(std::memory_order_relaxed));
+      p.svm_vram.push_back(s.svm_vram[i].load(std::memory_order_relaxed));
+      const uint64_t wn = s.hbm_want_ns[i].load(std::memory_order_relaxed);
+      const bool fresh = wn && wn <= now + kBoardStaleNs && now - wn < kBoardWantNs;
+      p.hbm_want.push_back(fresh ? s.hbm_want[i].load(std::memory_order_relaxed) : 0);
+      p.hbm_want_ns.push_back(fresh ? wn : 0);
     }
     const int n = std::max(0, std::min(s.npids.load(std::memory_order_relaxed), kBoardMaxPids));
     for (int i = 0; i < n; i++) {

@@ -281,6 +281,10 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
     else VLOG_WARN("invalid VGPU_SPILL_BACKING=%s, using auto", s);
   }
   cfg->spill_promote = parse_bool(getenv_fn("VGPU_SPILL_PROMOTE"), true);
+  {
+    long ms = 0;
+    if (parse_int(getenv_fn("VGPU_DEMOTE_WAIT_MS"), 0, 60000, &ms)) cfg->demote_wait_ms = (int)ms;
+  }
   if (const char* s = getenv_fn("VGPU_HOST_MEMORY_LIMIT")) {
     if (!parse_size(s, &cfg->host_mem_limit)) {
       VLOG_WARN("invalid VGPU_HOST_MEMORY_LIMIT=%s ignored", s);

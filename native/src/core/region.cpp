@@ -344,6 +344,7 @@ void SharedRegion::clear_slot_locked(int slot) {
     uint64_t t = s.used[d].total.exchange(0);
     uint64_t sp = s.used[d].kind[kMemSpill].load();
     for (int k = 0; k < kMemKinds; k++) s.used[d].kind[k].store(0);
+    s.used[d].svm_vram.store(0);
     if (t) r_->dev[d].used.fetch_sub(t);
     if (sp) r_->dev[d].spilled.fetch_sub(sp);
   }
@@ -452,6 +453,19 @@ void SharedRegion::uncharge(int slot, int dev, uint64_t bytes, MemKind kind) {
 uint64_t SharedRegion::usage(int dev) const { return r_->dev[dev].used.load(std::memory_order_relaxed); }
 uint64_t SharedRegion::limit(int dev) const { return lower_limit(r_->dev[dev].mem_limit, ceil_mem_[dev]); }
 uint64_t SharedRegion::hbm_limit(int dev) const { return lower_limit(r_->dev[dev].hbm_limit, ceil_hbm_[dev]); }
+void SharedRegion::set_svm_vram(int slot, int dev, uint64_t bytes) {
+  if (!r_ || slot < 0 || slot >= kMaxProcs || dev < 0 || dev >= kMaxDevices) return;
+  r_->procs[slot].used[dev].svm_vram.store(bytes, std::memory_order_relaxed);
+}
+
+uint64_t SharedRegion::svm_vram(int dev) const {
+  if (!r_ || dev < 0 || dev >= kMaxDevices) return 0;
+  uint64_t n = 0;
+  for (int i = 0; i < kMaxProcs; i++)
+    if (r_->procs[i].pid.load(std::memory_order_relaxed)) n += r_->procs[i].used[dev].svm_vram.load(std::memory_order_relaxed);
+  return n;
+}
+
 uint64_t SharedRegion::resident(int dev) const {
   // Sequentially consistent: pairs with promote_spill (an allocator charges `used`, then reads
   // `spilled`; a promotion lowers `spilled`, then reads `used` - one of them sees the other).

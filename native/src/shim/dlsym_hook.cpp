@@ -611,22 +611,61 @@ __attribute__((visibility("default"))) void* shim_dlvsym_v225(void* handle, cons
   }                                                                                       \
   return deepbind_open(real, file, mode, __builtin_return_address(0));
 
-// The directories of the calling object's DT_RUNPATH (or DT_RPATH), $ORIGIN expanded.
+// The directories of the calling object's DT_RUNPATH (or DT_RPATH), $ORIGIN expanded. The
+// object is found by address with dl_iterate_phdr (dladdr1 is a GLIBC_2.34 symbol, which the
+// shim must not need: test_native_core.py).
+struct CallerObject {
+  uintptr_t addr;
+  ElfW(Addr) base = 0;
+  const ElfW(Dyn)* dyn = nullptr;
+  std::string name;
+};
+
+static int caller_object_cb(struct dl_phdr_info* info, size_t, void* data) {
+  CallerObject* c = static_cast<CallerObject*>(data);
+  bool inside = false;
+  const ElfW(Dyn)* dyn = nullptr;
+  for (int i = 0; i < info->dlpi_phnum; i++) {
+    const ElfW(Phdr)& ph = info->dlpi_phdr[i];
+    const uintptr_t lo = info->dlpi_addr + ph.p_vaddr;
+    if (ph.p_type == PT_LOAD && c->addr >= lo && c->addr < lo + ph.p_memsz) inside = true;
+    if (ph.p_type == PT_DYNAMIC) dyn = reinterpret_cast<const ElfW(Dyn)*>(lo);
+  }
+  if (!inside) return 0;
+  c->base = info->dlpi_addr;
+  c->dyn = dyn;
+  c->name = info->dlpi_name ? info->dlpi_name : "";
+  return 1;
+}
+
 static std::vector<std::string> caller_search_dirs(const void* caller) {
   std::vector<std::string> dirs;
-  Dl_info di;
-  struct link_map* lm = nullptr;
-  if (!caller || !dladdr1(caller, &di, reinterpret_cast<void**>(&lm), RTLD_DL_LINKMAP) || !lm || !lm->l_ld) return dirs;
+  CallerObject c;
+  c.addr = reinterpret_cast<uintptr_t>(caller);
+  if (!caller || !dl_iterate_phdr(caller_object_cb, &c) || !c.dyn) return dirs;
   const char* strtab = nullptr;
   ElfW(Addr) runpath = 0, rpath = 0;
   bool has_runpath = false, has_rpath = false;
-  for (const ElfW(Dyn)* d = lm->l_ld; d->d_tag != DT_NULL; d++) {
-    if (d->d_tag == DT_STRTAB) strtab = reinterpret_cast<const char*>(d->d_un.d_ptr < lm->l_addr ? d->d_un.d_ptr + lm->l_addr : d->d_un.d_ptr);
-    if (d->d_tag == DT_RUNPATH) { runpath = d->d_un.d_val; has_runpath = true; }
-    if (d->d_tag == DT_RPATH) { rpath = d->d_un.d_val; has_rpath = true; }
+  for (const ElfW(Dyn)* d = c.dyn; d->d_tag != DT_NULL; d++) {
+    if (d->d_tag == DT_STRTAB)
+      strtab = reinterpret_cast<const char*>(d->d_un.d_ptr < c.base ? d->d_un.d_ptr + c.base : d->d_un.d_ptr);
+    if (d->d_tag == DT_RUNPATH) {
+      runpath = d->d_un.d_val;
+      has_runpath = true;
+    }
+    if (d->d_tag == DT_RPATH) {
+      rpath = d->d_un.d_val;
+      has_rpath = true;
+    }
   }
   if (!strtab || (!has_runpath && !has_rpath)) return dirs;
-  std::string origin = di.dli_fname ? di.dli_fname : "";
+  // The main program's name is empty in the list: /proc/self/exe's directory is its origin.
+  std::string origin = c.name;
+  if (origin.empty()) {
+    char exe[4096];
+    const ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+    origin = n > 0 ? std::string(exe, (size_t)n) : ".";
+  }
   origin = origin.find('/') == std::string::npos ? "." : origin.substr(0, origin.rfind('/'));
   std::string list = strtab + (has_runpath ? runpath : rpath), cur;
   for (size_t i = 0; i <= list.size(); i++) {

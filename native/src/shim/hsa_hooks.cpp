@@ -75,11 +75,25 @@ bool should_spill(int dev, size_t size) {
   if (resident + reserve > hbm) return true;
   VGPU_REAL_HSA(hsa_agent_get_info);
   uint64_t avail = 0;
-  if (real_hsa_agent_get_info(s.agents[dev].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &avail) ==
-          HSA_STATUS_SUCCESS &&
-      avail < size + reserve)
-    return true;
-  return false;
+  if (real_hsa_agent_get_info(s.agents[dev].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &avail) !=
+      HSA_STATUS_SUCCESS)
+    return false;
+  const uint64_t hidden = hidden_vram(dev);  // SVM pages in VRAM, node-wide: not in ROCr's figure
+  avail = avail > hidden ? avail - hidden : 0;
+  return avail < size + reserve;
+}
+
+// One real allocation attempt, retried by reclaim_peer_hbm while co-tenants demote.
+struct PoolAttempt {
+  hsa_amd_memory_pool_t pool;
+  size_t size;
+  uint32_t flags;
+  void** ptr;
+};
+hsa_status_t pool_attempt(void* c) {
+  VGPU_REAL_HSA(hsa_amd_memory_pool_allocate);
+  const PoolAttempt* a = static_cast<const PoolAttempt*>(c);
+  return real_hsa_amd_memory_pool_allocate(a->pool, a->size, a->flags, a->ptr);
 }
 
 // Limits are configured but the region could not be attached: GPU memory is refused.
@@ -158,6 +172,11 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
     }
   }
   st = real_hsa_amd_memory_pool_allocate(pool, size, flags, ptr);
+  if (st == HSA_STATUS_ERROR_OUT_OF_RESOURCES) {
+    // Within the quota but the GPU's HBM is full: co-tenants' promoted spills give it back.
+    PoolAttempt at{pool, size, flags, ptr};
+    st = reclaim_peer_hbm(dev, size, pool_attempt, &at);
+  }
   if (st == HSA_STATUS_SUCCESS) {
     record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemData);
     return st;
@@ -371,7 +390,13 @@ hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* 
   uint64_t used = s.region.usage(dev);
   uint64_t avail = lim > used ? lim - used : 0;
   uint64_t* v = static_cast<uint64_t*>(value);
-  if (!config().oversubscribe && *v < avail) avail = *v;  // other tenants may hold HBM
+  if (!config().oversubscribe) {
+    // Other tenants may hold HBM - SVM pages in VRAM too, which ROCr's figure leaves out
+    // (this container's and, from the node board, the other containers').
+    const uint64_t hidden = hidden_vram(dev);
+    const uint64_t phys = *v > hidden ? *v - hidden : 0;
+    if (phys < avail) avail = phys;
+  }
   *v = avail;
   return st;
 }

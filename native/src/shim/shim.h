@@ -248,6 +248,18 @@ bool svm_allow_access(const void* ptr, uint32_t n, const hsa_agent_t* agents, hs
 // Bytes of SVM spills of `dev` promoted into HBM that KFD's VRAM counter does not show
 // (resync_context_charge subtracts them from the tracked allocations).
 int64_t svm_hbm_outside_kfd(int dev);
+// HBM of `dev` that holds shared virtual memory - this container's promoted spills and
+// prefetched ranges, and other containers' (node board) - when ROCr's free-memory figure does
+// not show it (measured at the first migration; assumed until then, as on MI355X,
+// profiles/r4b): taken off MEMORY_AVAIL wherever the shim decides by free HBM.
+uint64_t hidden_vram(int dev);
+// Stores this process's SVM bytes in each device's VRAM in its region slot (the sampler sums
+// them for the node board). Called by the maintenance thread every period and after moves.
+void publish_svm_vram();
+// Physical HBM refused within the quota while co-tenants hold promoted spills on the GPU:
+// asks them (node board) to demote spills and retries `attempt` until it succeeds or
+// VGPU_DEMOTE_WAIT_MS passes. Returns the last status.
+hsa_status_t reclaim_peer_hbm(int dev, size_t size, hsa_status_t (*attempt)(void*), void* ctx);
 // Re-charges the SVM spills after the region was re-initialised (check_region_epoch).
 void svm_recharge(int slot, uint64_t* host);
 // Forgets the parent's SVM spills in a forked child (the ranges are not inherited).

@@ -24,7 +24,16 @@
 // large-first reserve, and in the GPU's free HBM less the same reserve (other tenants'
 // allocations come first). A promoted spill is charged as HBM data and released from the
 // host budget; a failed migration (the driver refused, HBM went to someone else) is undone
-// and retried after a back-off. Promoted ranges stay in HBM until freed.
+// and retried after a back-off.
+//
+// Node-wide (the node board, vgpu/board.h): ROCr's free-memory figure does not show SVM pages
+// in VRAM (profiles/r4b), so every process publishes its promoted spills and prefetched ranges
+// (region slot -> the container's sampler -> its board slot), and every container takes the
+// other containers' off the free HBM it places, promotes and reports by (hidden_vram). A
+// tenant refused HBM within its quota while co-tenants hold promoted spills on the GPU asks for
+// it on the board; their migrators demote their youngest promoted spills back to host memory
+// (contents intact, charged as spill again) and the refused allocation is retried
+// (reclaim_peer_hbm) - the two-way movement the reference's UVM spill has.
 #include <errno.h>
 #include <pthread.h>
 #include <sys/mman.h>
@@ -58,6 +67,27 @@ uint64_t migrate_timeout_ns() {
   return ns;
 }
 constexpr uint64_t kRetryBackoffNs = 10'000'000'000ull;      // after a failed promotion
+constexpr uint64_t kDemoteBackoffNs = 30'000'000'000ull;     // a demoted spill stays in host memory
+constexpr uint64_t kBlindProbeBytes = 64ull << 20;           // migrations that measure MEMORY_AVAIL
+
+// Whether ROCr's free-memory figure (HSA_AMD_AGENT_INFO_MEMORY_AVAIL) leaves out SVM pages in
+// VRAM: -1 not measured yet (assumed, as measured on MI355X), 1 it does, 0 it shows them.
+std::atomic<int> g_avail_blind{-1};
+
+uint64_t real_mem_avail(const AgentInfo& a) {
+  VGPU_REAL_HSA(hsa_agent_get_info);
+  uint64_t v = 0;
+  if (!real_hsa_agent_get_info ||
+      real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &v) != HSA_STATUS_SUCCESS)
+    return 0;
+  return v;
+}
+
+// This process's SVM bytes in the VRAM of `dev` (plain loads of fields ctx_mu guards: an
+// aligned 64-bit load is never torn, and a momentarily stale value is harmless here).
+uint64_t own_svm_vram(const ShimState& s, int dev) {
+  return (uint64_t)std::max<int64_t>(0, s.svm_hbm[dev] + s.tsvm_loc[dev]);
+}
 
 std::atomic<uint64_t> g_seq{0};
 std::atomic<bool> g_migrator{false};
@@ -159,6 +189,8 @@ uint64_t promote_device(int dev, uint64_t budget) {
   ShimState& s = shim();
   const Config& cfg = config();
   AgentInfo& a = s.agents[dev];
+  // A co-tenant on this GPU is short of HBM (the container was asked to demote): nothing moves up.
+  if (s.region.raw()->dev[dev].demote_want.load(std::memory_order_relaxed)) return 0;
   const uint64_t share = s.region.hbm_limit(dev);
   const uint64_t reserve = share ? spill_reserve(cfg, share) : 0;
   const uint64_t cap = share ? (share > reserve ? share - reserve : 1) : 0;
@@ -188,10 +220,11 @@ uint64_t promote_device(int dev, uint64_t budget) {
     if (real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MEMORY_AVAIL, &avail) !=
         HSA_STATUS_SUCCESS)
       break;
+    const uint64_t avail_raw = avail;
     // ROCr's free-memory figure does not drop as SVM pages move into VRAM (profiles/r4b):
-    // what this process promoted already is taken off it here.
-    const uint64_t promoted = (uint64_t)std::max<int64_t>(0, svm_hbm_outside_kfd(dev));
-    avail = avail > promoted ? avail - promoted : 0;
+    // what this container and the others on the GPU (node board) hold that way is taken off.
+    const uint64_t hidden = hidden_vram(dev);
+    avail = avail > hidden ? avail - hidden : 0;
     if (avail < rec.mapped + reserve) break;
     void* p = reinterpret_cast<void*>(o.second);
     int64_t vram0 = -1;
@@ -226,6 +259,12 @@ uint64_t promote_device(int dev, uint64_t budget) {
       VLOG_ERROR("device %d: promotion of %lu bytes at %p did not finish within %lu ms; kept as HBM-resident", dev,
                  (unsigned long)rec.size, p, (unsigned long)(migrate_timeout_ns() / 1000000ull));
     }
+    if (m == Migration::kDone && rec.mapped >= kBlindProbeBytes && g_avail_blind.load() < 0) {
+      // First migration of a size that shows: does ROCr's free figure follow SVM pages?
+      const uint64_t after = real_mem_avail(a);
+      g_avail_blind.store(avail_raw >= after + rec.mapped / 2 ? 0 : 1);
+      VLOG_INFO("device %d: ROCr's free HBM %s SVM pages in VRAM", dev, g_avail_blind.load() ? "omits" : "counts");
+    }
     {
       std::lock_guard<std::mutex> cg(s.ctx_mu);
       const int64_t vram1 = vram0 >= 0 && m == Migration::kDone ? kfd_vram_usage(s.hostpid, a.gpu_id) : -1;
@@ -239,10 +278,81 @@ uint64_t promote_device(int dev, uint64_t budget) {
       if (it != s.svm.end()) it->second.in_hbm = true;
     }
     moved += rec.size;
+    publish_svm_vram();
     VLOG_INFO("device %d: %lu spilled bytes at %p promoted into HBM in %.1f ms", dev, (unsigned long)rec.size, p,
               (now_ns() - t0) / 1e6);
   }
   return moved;
+}
+
+// Demotes this process's promoted spills of `dev`, youngest first, until `want` bytes moved:
+// back to host memory (the driver migrates the pages: contents intact), charged as spill and
+// to the host budget again, and kept there for a back-off. Returns the bytes moved.
+uint64_t demote_device(int dev, uint64_t want) {
+  ShimState& s = shim();
+  AgentInfo& a = s.agents[dev];
+  std::vector<std::pair<uint64_t, uintptr_t>> order;  // (seq, ptr) of the promoted spills
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    for (const auto& kv : s.svm)
+      if (kv.second.dev == dev && kv.second.in_hbm) order.emplace_back(kv.second.seq, kv.first);
+  }
+  std::sort(order.rbegin(), order.rend());
+  uint64_t moved = 0;
+  for (const auto& o : order) {
+    if (moved >= want || s.exiting.load()) break;
+    std::lock_guard<std::mutex> mg(s.svm_mu);
+    SvmRec rec;
+    {
+      std::lock_guard<std::mutex> g(s.alloc_mu);
+      auto it = s.svm.find(o.second);
+      if (it == s.svm.end() || !it->second.in_hbm) continue;
+      rec = it->second;
+    }
+    if (s.region.charge_host(s.slot, rec.size) != Charge::kOk) {
+      VLOG_WARN("device %d: cannot demote %lu bytes for a co-tenant: the host memory budget is used up", dev,
+                (unsigned long)rec.size);
+      break;
+    }
+    void* p = reinterpret_cast<void*>(o.second);
+    const uint64_t t0 = now_ns();
+    const Migration m = migrate(p, rec.mapped, a.cpu_agent);
+    if (m == Migration::kFailed) {
+      s.region.uncharge_host(s.slot, rec.size);
+      VLOG_WARN("device %d: demotion of %lu bytes at %p failed", dev, (unsigned long)rec.size, p);
+      continue;
+    }
+    {
+      std::lock_guard<std::mutex> cg(s.ctx_mu);
+      s.region.demote_to_spill(s.slot, dev, rec.size);
+      s.svm_hbm[dev] -= (int64_t)rec.size;
+    }
+    {
+      std::lock_guard<std::mutex> g(s.alloc_mu);
+      auto it = s.svm.find(o.second);
+      if (it != s.svm.end()) {
+        it->second.in_hbm = false;
+        it->second.retry_ns = now_ns() + kDemoteBackoffNs;
+      }
+    }
+    moved += rec.size;
+    publish_svm_vram();
+    VLOG_INFO("device %d: %lu promoted bytes at %p demoted to host memory for a co-tenant in %.1f ms", dev,
+              (unsigned long)rec.size, p, (now_ns() - t0) / 1e6);
+  }
+  return moved;
+}
+
+// The container was asked to demote `demote_want` bytes of `dev` (its sampler, for a co-tenant
+// short of HBM): this process does its part and takes it off the request.
+void demote_for_peers(int dev) {
+  ShimState& s = shim();
+  std::atomic<uint64_t>& want = s.region.raw()->dev[dev].demote_want;
+  uint64_t w = want.load(std::memory_order_relaxed);
+  if (!w || s.svm_hbm[dev] <= 0) return;
+  const uint64_t moved = demote_device(dev, w);
+  while (moved && !want.compare_exchange_weak(w, w > moved ? w - moved : 0)) {
+  }
 }
 
 void* migrator_main(void*) {
@@ -258,6 +368,7 @@ void* migrator_main(void*) {
     }
     g_wake.store(false, std::memory_order_relaxed);
     if (s.exiting.load() || !s.active || s.slot < 0) continue;
+    for (int d = 0; d < s.n_agents; d++) demote_for_peers(d);
     uint64_t budget = kPromoteBytesPerTick;
     for (int d = 0; d < s.n_agents && budget; d++) budget -= std::min(budget, promote_device(d, budget));
   }
@@ -417,6 +528,56 @@ bool svm_allow_access(const void* ptr, uint32_t n, const hsa_agent_t* agents, hs
 int64_t svm_hbm_outside_kfd(int dev) {
   ShimState& s = shim();
   return s.svm_kfd_vram == 1 ? 0 : s.svm_hbm[dev];
+}
+
+uint64_t hidden_vram(int dev) {
+  ShimState& s = shim();
+  if (dev < 0 || dev >= s.n_agents || !s.region.attached() || g_avail_blind.load(std::memory_order_relaxed) == 0)
+    return 0;
+  const Region* r = s.region.raw();
+  // The container's sum, with this process's current bytes for what it last published.
+  const uint64_t mine_pub = s.slot >= 0 ? r->procs[s.slot].used[dev].svm_vram.load(std::memory_order_relaxed) : 0;
+  const uint64_t container = s.region.svm_vram(dev);
+  const uint64_t own = (container > mine_pub ? container - mine_pub : 0) + own_svm_vram(s, dev);
+  return own + r->dev[dev].node_svm_vram.load(std::memory_order_relaxed);
+}
+
+void publish_svm_vram() {
+  ShimState& s = shim();
+  if (s.slot < 0 || !s.region.attached()) return;
+  for (int d = 0; d < s.n_agents; d++) s.region.set_svm_vram(s.slot, d, own_svm_vram(s, d));
+}
+
+hsa_status_t reclaim_peer_hbm(int dev, size_t size, hsa_status_t (*attempt)(void*), void* ctx) {
+  ShimState& s = shim();
+  const Config& cfg = config();
+  Region* r = s.region.raw();
+  if (cfg.demote_wait_ms <= 0 || dev < 0 || dev >= s.n_agents || !r->dev[dev].node_svm_vram.load())
+    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  DeviceState& d = r->dev[dev];
+  VLOG_INFO("device %d: %zu bytes refused by the driver within the quota; co-tenants hold %lu bytes of promoted "
+            "spills here - asking them to demote", dev, size, (unsigned long)d.node_svm_vram.load());
+  const uint64_t t0 = now_ns(), limit = (uint64_t)cfg.demote_wait_ms * 1'000'000ull;
+  uint64_t asked = 0;
+  hsa_status_t st = HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  trace_push("vgpu:reclaim");
+  for (uint64_t el = 0; el < limit; el = now_ns() - t0) {
+    if (!asked || el - asked >= 1'000'000'000ull) {  // (re-)published every second: a fresh request
+      d.hbm_want.store(std::max<uint64_t>(size, d.hbm_want.load()));
+      d.hbm_want_ns.store(now_ns());
+      asked = std::max<uint64_t>(el, 1);
+    }
+    struct timespec ts = {0, 20'000'000};
+    nanosleep(&ts, nullptr);
+    st = attempt(ctx);
+    if (st != HSA_STATUS_ERROR_OUT_OF_RESOURCES) break;
+  }
+  d.hbm_want_ns.store(0);
+  d.hbm_want.store(0);
+  trace_pop();
+  VLOG_INFO("device %d: %zu bytes %s after %.0f ms", dev, size, st == HSA_STATUS_SUCCESS ? "allocated" : "still refused",
+            (now_ns() - t0) / 1e6);
+  return st;
 }
 
 void svm_recharge(int slot, uint64_t* host) {

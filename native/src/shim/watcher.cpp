@@ -134,6 +134,8 @@ struct Sampler {
   std::map<int, uint64_t> ledger_seen[kMaxDevices];
   uint64_t ledger_retry_ns[kMaxDevices] = {};
   uint64_t others_busy_ns[kMaxDevices] = {};  // last sample at which another process had waves resident
+  uint64_t mem_refresh_ns = 0;                // next read of the peers' memory (memory_board_tick)
+  uint64_t want_seen_ns[kMaxDevices] = {};    // the peers' HBM request already served
 };
 
 // The credit window of device `d`: the configured one, or the longer solo window while no
@@ -188,6 +190,44 @@ int64_t ledger_charge(const LedgerReader& l, std::map<int, uint64_t>& seen, cons
 // The container's task priority (live: vgpuctl / the monitor may change it).
 int region_priority(const Region* r) { return effective_priority(r); }
 
+// Virtual device memory across containers (lease holder, every period): publishes the
+// container's SVM bytes in each GPU's VRAM and any HBM it was refused within its quota; reads
+// the peers' (every 250 ms while either matters here, else every second) into the region:
+// the SVM VRAM of the other containers on each GPU (hidden_vram), and a demotion request when
+// a peer on the GPU waits for HBM while this container holds promoted spills there - once per
+// request (a peer re-publishes its request every second while it still waits).
+void memory_board_tick(Region* r, Sampler& sm, const uint32_t* ids, uint64_t now) {
+  ShimState& s = shim();
+  bool mine = false;
+  for (int d = 0; d < s.n_agents; d++) {
+    DeviceState& ds = r->dev[d];
+    const uint64_t svm = s.region.svm_vram(d);
+    const uint64_t want_ns = ds.hbm_want_ns.load(std::memory_order_relaxed);
+    const bool fresh = want_ns && now - want_ns < kBoardWantNs;
+    sm.board.publish_memory(d, svm, fresh ? ds.hbm_want.load(std::memory_order_relaxed) : 0, want_ns);
+    mine |= svm || fresh || ds.node_svm_vram.load(std::memory_order_relaxed);
+  }
+  if (now < sm.mem_refresh_ns) return;
+  sm.mem_refresh_ns = now + (mine ? 250'000'000ull : 1'000'000'000ull);
+  sm.board.refresh(now);
+  for (int d = 0; d < s.n_agents; d++) {
+    DeviceState& ds = r->dev[d];
+    ds.node_svm_vram.store(sm.board.peers_svm_vram(ids[d]), std::memory_order_relaxed);
+    uint64_t newest = 0;
+    const uint64_t want = sm.board.peers_hbm_want(ids[d], &newest);
+    const uint64_t svm = s.region.svm_vram(d);
+    if (!want) {
+      sm.want_seen_ns[d] = 0;
+      ds.demote_want.store(0, std::memory_order_relaxed);
+    } else if (newest != sm.want_seen_ns[d] && svm) {
+      sm.want_seen_ns[d] = newest;
+      ds.demote_want.store(std::min(want, svm), std::memory_order_relaxed);
+      VLOG_INFO("device %d: a co-tenant waits for %lu bytes of HBM; demoting up to %lu bytes of promoted spills", d,
+                (unsigned long)want, (unsigned long)std::min(want, svm));
+    }
+  }
+}
+
 // Publishes the container on the board (lease holder, every period).
 void board_tick(Region* r, Sampler& sm, uint64_t now) {
   const Config& cfg = config();
@@ -214,6 +254,7 @@ void board_tick(Region* r, Sampler& sm, uint64_t now) {
       memcpy(masks[i], s.agents[i].mask.words, sizeof(masks[i]));
   }
   sm.board.publish(region_priority(r), ids, s.n_agents, sm.mine, now, masks);
+  memory_board_tick(r, sm, ids, now);
   // Background class: keep off the CU slices of latency-class tenants on the same GPU.
   // Stored in the region, so every process of the container re-masks its queues.
   if (region_priority(r) < kPrioBackground) return;
@@ -579,6 +620,7 @@ void* watcher_main(void*) {
       if (s.slot >= 0) r->procs[s.slot].launches.store(s.launches.load(std::memory_order_relaxed));
       resync_context_charge();
       svm_tenant_reconcile();  // the tenant's SVM ranges it unmapped give their charge back
+      publish_svm_vram();      // for the node board (hidden_vram)
       if (lease) {
         collect_region_pids(r, sm);
         board_tick(r, sm, now);

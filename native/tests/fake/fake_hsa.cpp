@@ -22,10 +22,16 @@
 //   FAKE_SVM_KFD_VRAM   0: SVM ranges migrated into HBM are not in KFD's vram_<gpu_id> (default 1)
 //   FAKE_ROCR_XNACK     1: recoverable page faults reported on (HSA_AMD_SYSTEM_INFO_XNACK_ENABLED)
 //   FAKE_SVM_HANG       1: prefetches into a GPU never complete (their signals stay at 1)
+//   FAKE_ROCR_SHARED_HBM  file: the GPUs' HBM is shared by every process naming the same
+//                       file (a node: several containers' processes on one physical GPU);
+//                       admission and MEMORY_AVAIL then see every process's usage
+//   FAKE_SVM_AVAIL_BLIND  1: MEMORY_AVAIL does not count SVM pages migrated into HBM (as ROCr
+//                       on MI355X, profiles/r4b); admission still does (the VRAM is taken)
 // Test-only introspection: fake_rocr_* functions below.
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <errno.h>
+#include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -49,8 +55,16 @@ constexpr uint64_t kCpuPool = 2000;
 struct FakeGpu {
   std::string uuid;
   uint64_t hbm = 8ull << 30;
-  std::atomic<uint64_t> used{0};
+  std::atomic<uint64_t> used{0};     // this process's bytes in HBM (SVM included)
+  std::atomic<uint64_t> svm_used{0};  // of which SVM pages
   uint32_t gpu_id = 0;
+};
+
+// Node-wide HBM of each GPU (FAKE_ROCR_SHARED_HBM): bytes in use by every process, and of
+// them SVM pages.
+struct SharedHbm {
+  std::atomic<uint64_t> used[16];
+  std::atomic<uint64_t> svm[16];
 };
 
 struct FakeQueue {
@@ -84,6 +98,7 @@ struct State {
   char* arena = nullptr;
   uint64_t arena_size = 0, arena_next = 0;
   std::string kfd;  // fake KFD process dir of this process ("" = none)
+  SharedHbm* node = nullptr;  // FAKE_ROCR_SHARED_HBM (null: this process's HBM is its own)
   bool inited = false;
   int init_count = 0;
 };
@@ -105,10 +120,36 @@ void write_file(const std::string& path, uint64_t v) {
   fclose(f);
 }
 
+// HBM bytes in use on GPU `d` as the driver sees them (every process on a shared node).
+uint64_t hbm_used(int d) {
+  State& s = st();
+  return s.node ? s.node->used[d].load() : s.gpus[d].used.load();
+}
+
+// MEMORY_AVAIL's view: without the SVM pages when FAKE_SVM_AVAIL_BLIND=1.
+uint64_t hbm_used_avail(int d) {
+  State& s = st();
+  const bool blind = env_u64("FAKE_SVM_AVAIL_BLIND", 0) != 0;
+  const uint64_t u = hbm_used(d);
+  const uint64_t v = blind ? (s.node ? s.node->svm[d].load() : s.gpus[d].svm_used.load()) : 0;
+  return u > v ? u - v : 0;
+}
+
+void add_used(int d, int64_t delta, bool svm) {
+  State& s = st();
+  s.gpus[d].used.fetch_add((uint64_t)delta);
+  if (svm) s.gpus[d].svm_used.fetch_add((uint64_t)delta);
+  if (s.node) {
+    s.node->used[d].fetch_add((uint64_t)delta);
+    if (svm) s.node->svm[d].fetch_add((uint64_t)delta);
+  }
+}
+
 void kfd_update_vram(int dev) {
   State& s = st();
   if (s.kfd.empty() || dev < 0) return;
-  write_file(s.kfd + "/vram_" + std::to_string(s.gpus[dev].gpu_id), s.gpus[dev].used.load());
+  const uint64_t svm = env_u64("FAKE_SVM_KFD_VRAM", 1) ? 0 : s.gpus[dev].svm_used.load();
+  write_file(s.kfd + "/vram_" + std::to_string(s.gpus[dev].gpu_id), s.gpus[dev].used.load() - svm);
 }
 
 void setup() {
@@ -140,6 +181,16 @@ void setup() {
     s.gpus[i].uuid = i < (int)uuids.size() ? uuids[i] : buf;
     s.gpus[i].hbm = hbm;
     s.gpus[i].gpu_id = 1000 + i;
+  }
+  if (const char* path = getenv("FAKE_ROCR_SHARED_HBM")) {
+    int fd = open(path, O_RDWR | O_CREAT, 0666);
+    if (fd >= 0) {
+      if (ftruncate(fd, sizeof(SharedHbm)) == 0) {
+        void* m = mmap(nullptr, sizeof(SharedHbm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        if (m != MAP_FAILED) s.node = static_cast<SharedHbm*>(m);
+      }
+      close(fd);
+    }
   }
   s.arena_size = 1ull << 42;  // 4 TiB of address space, never touched
   void* p = mmap(nullptr, s.arena_size, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
@@ -185,7 +236,7 @@ void svm_gc() {
     if (mincore(reinterpret_cast<void*>(it->first), (size_t)pg, &v) != 0 && errno == ENOMEM) {
       const int d = gpu_of(hsa_agent_t{it->second.loc});
       if (d >= 0) {
-        s.gpus[d].used.fetch_sub(it->second.size);
+        add_used(d, -(int64_t)it->second.size, true);
         if (env_u64("FAKE_SVM_KFD_VRAM", 1)) kfd_update_vram(d);
       }
       it = s.svm.erase(it);
@@ -244,7 +295,7 @@ hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* 
         std::lock_guard<std::mutex> g(s.mu);
         svm_gc();
       }
-      uint64_t u = s.gpus[d].used.load();
+      uint64_t u = hbm_used_avail(d);
       *static_cast<uint64_t*>(value) = s.gpus[d].hbm > u ? s.gpus[d].hbm - u : 0;
       break;
     }
@@ -291,14 +342,14 @@ hsa_status_t pool_allocate_impl(hsa_amd_memory_pool_t pool, size_t size, void** 
   int d = pool.handle >= kGpuPoolBase && pool.handle < kGpuPoolBase + (uint64_t)s.n ? (int)(pool.handle - kGpuPoolBase)
                                                                                      : -1;
   if (d < 0 && pool.handle != kCpuPool) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
-  if (d >= 0 && s.gpus[d].used.load() + size > s.gpus[d].hbm) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  if (d >= 0 && hbm_used(d) + size > s.gpus[d].hbm) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   // Host memory is real (the application may touch pinned buffers); HBM is address space only.
   void* p = d >= 0 ? bump(size) : mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
   if (p == MAP_FAILED) p = nullptr;
   if (!p) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   s.allocs[reinterpret_cast<uintptr_t>(p)] = {d, size};
   if (d >= 0) {
-    s.gpus[d].used.fetch_add(size);
+    add_used(d, (int64_t)size, false);
     kfd_update_vram(d);
   }
   *ptr = p;
@@ -312,7 +363,7 @@ hsa_status_t pool_free_impl(void* ptr) {
   if (it == s.allocs.end()) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
   int d = it->second.first;
   if (d >= 0) {
-    s.gpus[d].used.fetch_sub(it->second.second);
+    add_used(d, -(int64_t)it->second.second, false);
     kfd_update_vram(d);
   } else {
     munmap(ptr, it->second.second);
@@ -585,14 +636,14 @@ hsa_status_t hsa_amd_svm_prefetch_async(void* ptr, size_t size, hsa_agent_t agen
     return HSA_STATUS_SUCCESS;
   }
   bool ok = to != from || to < 0;
-  if (to >= 0 && to != from && (env_u64("FAKE_SVM_FAIL", 0) || s.gpus[to].used.load() + size > s.gpus[to].hbm)) ok = false;
+  if (to >= 0 && to != from && (env_u64("FAKE_SVM_FAIL", 0) || hbm_used(to) + size > s.gpus[to].hbm)) ok = false;
   if (ok && to != from) {
     if (from >= 0) {
-      s.gpus[from].used.fetch_sub(r.size);
+      add_used(from, -(int64_t)r.size, true);
       if (counted) kfd_update_vram(from);
     }
     if (to >= 0) {
-      s.gpus[to].used.fetch_add(r.size);
+      add_used(to, (int64_t)r.size, true);
       if (counted) kfd_update_vram(to);
     }
     r.loc = to >= 0 ? agent.handle : 0;
@@ -649,8 +700,7 @@ int fake_rocr_svm_location(const void* ptr) {
 // allocation entry point, shows up only in KFD's per-process VRAM counter.
 int fake_rocr_internal_alloc(int dev, int64_t bytes) {
   if (dev < 0 || dev >= st().n) return -1;
-  if (bytes >= 0) st().gpus[dev].used.fetch_add((uint64_t)bytes);
-  else st().gpus[dev].used.fetch_sub((uint64_t)-bytes);
+  add_used(dev, bytes, false);
   kfd_update_vram(dev);
   return 0;
 }

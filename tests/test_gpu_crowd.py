@@ -5,7 +5,11 @@ Four 25 % pods of stock PyTorch (ResNet-V2-50 b=50 inference, synchronizing with
 ``Allocate`` of the plugin with its default policy: the GPU-time limiter on a crowded GPU,
 the crowd-depth bound on each pod's queue (VGPU_CROWD_DEPTH, watcher.cpp) and the shim's
 polled waits (sync_hooks.cpp). Driven through bench.py's sweep (the same pods and the same
-common-window rating as the headline number's node point).
+common-window rating as the headline number's node point). The vgpu mode runs first, as in
+the default bench: a 25 % pod starts on its 64-CU slice (auto mode, not crowded yet), so
+MIOpen looks its convolutions up for 64 CUs; that mode's find fills those entries, which the
+sweep's pods copy (without them every pod compiles fallback kernels for ~30 s and runs them
+at 0.6x, profiles/r6c).
 
 Bars:
 * the four pods together hold less than one CPU (stock waits spin a core each natively:
@@ -29,7 +33,7 @@ pytestmark = pytest.mark.gpu
 def test_four_crowded_pods_on_stock_waits(tmp_path):
     out = tmp_path / "line.json"
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--steps", "10", "--warmup", "3",
-           "--modes", "native", "--sweep", "on", "--sweep-tenants", "1,4", "--sweep-seconds", "5",
+           "--modes", "native,vgpu", "--sweep", "on", "--sweep-tenants", "1,4", "--sweep-seconds", "5",
            "--time-budget", "300", "--json-out", str(out)]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=420, env=env, cwd=REPO)
