@@ -26,6 +26,7 @@ MiB = 1 << 20
 A_CODE = """
 import torch
 from amdvgpu.shim.region import Region
+torch.zeros(1, device="cuda")                                           # the shim attaches its region
 reg = Region(os.environ["VGPU_SHARED_CACHE"])
 x = torch.empty(20 << 30, dtype=torch.uint8, device="cuda")            # most of the 24 GiB share
 y = torch.full((8 << 30,), 7, dtype=torch.uint8, device="cuda")         # past it: spilled (SVM)
