@@ -15,7 +15,7 @@ LIST_ENVVAR, LIST_AMD_RUNTIME, LIST_VOLUME_MOUNTS = "envvar", "amd-container-run
 ID_UUID, ID_INDEX = "uuid", "index"
 CU_MODES = ("auto", "spatial", "temporal", "both", "off")
 PLACEMENTS = ("spread", "binpack")
-DUPLICATE_POLICIES = ("reject", "merge")
+DUPLICATE_POLICIES = ("reject", "merge", "split")
 NUMA_SPREAD_MODES = ("auto", "on", "off")
 DEFAULT_RESOURCE = "amd.com/gpu"
 DEFAULT_PLUGIN_DIR = "/var/lib/kubelet/device-plugins/"
@@ -162,8 +162,9 @@ _FLAGS = [
      "GPU choice for a new pod: spread (the GPU with the most free vGPUs) | binpack (the fullest GPU with room)"),
     ("--duplicate-vgpus", "duplicate_vgpus", str, ["DUPLICATE_VGPUS"],
      "a container given two vGPUs of one GPU: merge (default: one device with the summed quota and CU share; "
-     "VGPU_DUPLICATE_MERGED and the amd-vgpu/merged-duplicates annotation tell the container) | reject (fail "
-     "Allocate)"),
+     "VGPU_DUPLICATE_MERGED and the amd-vgpu/merged-duplicates annotation tell the container) | split (one HIP "
+     "device per vGPU, each with its own quota: the shim virtualises the device ordinals, VGPU_DUPLICATE_SPLIT) | "
+     "reject (fail Allocate)"),
     ("--host-memory-per-vgpu", "host_memory_per_vgpu", str, ["HOST_MEMORY_PER_VGPU"],
      "pinned host memory (hipHostMalloc / hipHostRegister, and the host spill of oversubscribed vGPUs) per vGPU, "
      "e.g. 64g; auto (default) = --host-memory-fraction of the node's RAM divided among its vGPUs; "

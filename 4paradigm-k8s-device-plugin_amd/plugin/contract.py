@@ -93,6 +93,7 @@ def ensure_lock_file(vgpu_dir):
 ANN_REQUEST = "amd-vgpu/request"
 ANN_USING = "amd-vgpu/using"
 ANN_DUPLICATES = "amd-vgpu/merged-duplicates"
+ANN_SPLIT = "amd-vgpu/split-duplicates"
 
 
 ALLOWLIST_HOST_DIR = "allowlist"
@@ -385,7 +386,13 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         # first vGPU's, for a container holding several)
         resp.envs["VGPU_CPU_NODE"] = str(nodes[0])
     dups = duplicate_gpus(vdevs)
-    if dups:
+    if dups and getattr(cfg, "duplicate_vgpus", "merge") == "split":
+        # --duplicate-vgpus=split: one HIP device per vGPU, each with its own quota; the shim
+        # virtualises the device ordinals (native/src/shim/vdev_hooks.cpp). Compute stays per
+        # physical GPU, with the vGPUs' shares summed (docs/ABI.md "Duplicate vGPUs").
+        resp.envs["VGPU_DUPLICATE_SPLIT"] = "1"
+        resp.annotations[ANN_SPLIT] = ",".join(dups)
+    elif dups:
         # --duplicate-vgpus=merge: the shim merges the vGPUs of one GPU into that device
         # (quotas and CU shares add up); the container is told, since it sees fewer
         # devices than it requested (docs/ABI.md "Duplicate vGPUs").

@@ -365,7 +365,8 @@ class DevicePluginServer:
                 # with the summed share: refused instead (--duplicate-vgpus=merge keeps it).
                 self._fail(context, f"allocation for '{self.resource_name}' holds several vGPUs of one GPU "
                                     f"({', '.join(dups)}); a container sees one device per physical GPU "
-                                    f"(plugin flag --duplicate-vgpus=merge accepts this as one merged device)")
+                                    f"(plugin flag --duplicate-vgpus=merge accepts this as one merged device, "
+                                    f"=split as separate devices)")
             unhealthy = [v.id for v in vds if not v.dev.healthy]
             if unhealthy:
                 log.warning("allocating unhealthy vGPUs %s", unhealthy)

@@ -145,6 +145,7 @@ struct Config {
                                          // 0.79-0.99 unbounded, profiles/r5c)
   std::string lock_file = "/tmp/vgpulock/lock";  // host-PID discovery lock (reference /tmp/vgpulock/lock)
   int duplicate_merge = 1;               // merge two vGPUs of one physical GPU
+  int duplicate_split = 0;               // VGPU_DUPLICATE_SPLIT: ... or keep them two devices (vdev_hooks.cpp)
   uint64_t host_mem_limit = 0;           // VGPU_HOST_MEMORY_LIMIT: pinned host memory, 0 = unlimited
   bool fail_open = false;                // VGPU_FAIL_OPEN: run unlimited when the region cannot be attached
   std::string device_map;                // VGPU_DEVICE_MAP ("<i>:<uuid> ...")

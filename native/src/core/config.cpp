@@ -353,6 +353,8 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   }
   long merge = 1;
   if (parse_int(getenv_fn("VGPU_DUPLICATE_MERGE"), 0, 1, &merge)) cfg->duplicate_merge = (int)merge;
+  long split = 0;
+  if (parse_int(getenv_fn("VGPU_DUPLICATE_SPLIT"), 0, 1, &split)) cfg->duplicate_split = (int)split;
   if (const char* s = getenv_fn("VGPU_DEVICE_MAP")) cfg->device_map = s;
   if (const char* s = getenv_fn("VGPU_ALLOWLIST")) cfg->allowlist = s;
   long minp = 0;

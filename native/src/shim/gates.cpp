@@ -40,16 +40,17 @@ bool g_launch_hooks_on = true;
 
 namespace {
 
-enum GateKind : int { k_launch, k_graph, k_copy, k_set, k_suspend, k_hook, k_host };
+enum GateKind : int { k_launch, k_graph, k_copy, k_set, k_suspend, k_device, k_hook, k_host };
 
 struct GateDef {
   const char* name;
   const char* version;
   GateKind kind;
+  unsigned devargs;  // device rows: bit i = argument i+1 is a device ordinal
 };
 
 const GateDef kGates[] = {
-#define VGPU_GATE(idx, kind, name, ver) {#name, ver, k_##kind},
+#define VGPU_GATE(idx, kind, name, ver, mask) {#name, ver, k_##kind, mask},
 #include "hip_gates.inc"
 #undef VGPU_GATE
 };
@@ -154,9 +155,16 @@ void* hip_hook_for_name(const char* name, const char* version, const void* real)
 
 extern "C" {
 
-// Called by the generated trampolines (hip_gates.S) with the row index of the entry point.
-__attribute__((visibility("hidden"))) void* vgpu_gate_enter(int idx) {
+// Called by the generated trampolines (hip_gates.S) with the row index of the entry point
+// and the saved argument registers (rdi rsi rdx rcx r8 r9, in order).
+__attribute__((visibility("hidden"))) void* vgpu_gate_enter(int idx, uint64_t* regs) {
   switch (kGates[idx].kind) {
+    case k_device:
+      gate_suspend();
+      if (__builtin_expect(vdev_split_active(), 0))
+        for (int a = 0; a < 6; a++)
+          if (kGates[idx].devargs & (1u << a)) regs[a] = (uint64_t)(uint32_t)vdev_to_phys((int)(uint32_t)regs[a]);
+      break;
     case k_launch:
       VGPU_STAT(kStatLaunch);
       launch_gate();

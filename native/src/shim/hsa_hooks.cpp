@@ -114,6 +114,39 @@ inline bool ready() {
   return ph == 2 && s.active && !s.exiting.load(std::memory_order_relaxed);
 }
 
+// The charge of an allocation on the calling thread's virtual device (split duplicate
+// vGPUs, vdev_hooks.cpp): taken on construction, given back on destruction unless the
+// allocation succeeded (commit records it for the free).
+class VirtualCharge {
+ public:
+  VirtualCharge(int dev, size_t size) : size_(size) {
+    ShimState& s = shim();
+    slot_ = vdev_charge_slot(dev);
+    if (slot_ >= 0 && s.region.charge(s.slot, slot_, size, kMemData) != Charge::kOk) {
+      VLOG_WARN("virtual device (slot %d) OOM: request %zu bytes, usage %lu of limit %lu", slot_, size,
+                (unsigned long)s.region.usage(slot_), (unsigned long)s.region.limit(slot_));
+      failed_ = true;
+    }
+  }
+  ~VirtualCharge() {
+    if (slot_ >= 0 && !failed_ && !committed_) shim().region.uncharge(shim().slot, slot_, size_, kMemData);
+  }
+  bool ok() const { return !failed_; }
+  void commit(void* p) const {
+    if (slot_ < 0) return;
+    committed_ = true;
+    ShimState& s = shim();
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    s.vcharge[reinterpret_cast<uintptr_t>(p)] = AllocRec{size_, slot_, kMemData};
+  }
+
+ private:
+  size_t size_;
+  int slot_ = -1;
+  bool failed_ = false;
+  mutable bool committed_ = false;
+};
+
 }  // namespace
 
 extern "C" {
@@ -156,13 +189,19 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
               (unsigned long)s.region.usage(dev), (unsigned long)s.region.limit(dev));
     return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   }
+  // Split duplicate vGPUs: the calling thread's virtual device has its own quota too.
+  const VirtualCharge vc(dev, size);
+  if (!vc.ok()) {
+    s.region.uncharge(s.slot, dev, size, kMemData);
+    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+  }
   hsa_status_t st;
   // Virtual device memory: past the tenant's HBM-resident share the quota is served
   // from host memory (VGPU_DEVICE_HBM_LIMIT_<i>, emitted by the plugin when
   // --device-memory-scaling > 1), so one tenant cannot crowd the others out of HBM.
   if (should_spill(dev, size)) {
     st = spill_allocate(dev, size, ptr);  // charged as spill and recorded
-    if (st == HSA_STATUS_SUCCESS) return st;
+    if (st == HSA_STATUS_SUCCESS) return vc.commit(*ptr), st;
     // No host memory for it: within the HBM share (an early, large-first spill) the
     // allocation may stay in HBM; past the share it is refused - the rest of the HBM
     // belongs to the other tenants of the GPU.
@@ -179,15 +218,30 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
   }
   if (st == HSA_STATUS_SUCCESS) {
     record_alloc(reinterpret_cast<uintptr_t>(*ptr), size, dev, kMemData);
-    return st;
+    return vc.commit(*ptr), st;
   }
   if (st == HSA_STATUS_ERROR_OUT_OF_RESOURCES && config().oversubscribe) {
     // Under quota but the physical HBM is exhausted: virtual device memory.
     st = spill_allocate(dev, size, ptr);
-    if (st == HSA_STATUS_SUCCESS) return st;
+    if (st == HSA_STATUS_SUCCESS) return vc.commit(*ptr), st;
   }
   s.region.uncharge(s.slot, dev, size, kMemData);
   return st;
+}
+
+// Split duplicate vGPUs: the allocation's charge on its virtual device goes with it.
+static void release_virtual_charge(void* ptr) {
+  ShimState& s = shim();
+  AllocRec rec{0, -1, 0};
+  {
+    std::lock_guard<std::mutex> g(s.alloc_mu);
+    if (s.vcharge.empty()) return;
+    auto it = s.vcharge.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == s.vcharge.end()) return;
+    rec = it->second;
+    s.vcharge.erase(it);
+  }
+  if (s.slot >= 0 && !s.exiting.load()) s.region.uncharge(s.slot, rec.dev, rec.size, kMemData);
 }
 
 // The one release path of both free entry points (ROCr accepts either for a pool or region
@@ -198,6 +252,7 @@ hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t siz
 static hsa_status_t release_and_free(void* ptr, hsa_status_t (*real_free)(void*)) {
   ShimState& s = shim();
   if (!ptr || s.phase.load(std::memory_order_relaxed) != 2) return real_free(ptr);
+  release_virtual_charge(ptr);
   if (spill_release(ptr)) return HSA_STATUS_SUCCESS;
   const uintptr_t key = reinterpret_cast<uintptr_t>(ptr);
   AllocRec rec{0, -1, 0};

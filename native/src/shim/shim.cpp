@@ -214,6 +214,7 @@ void atfork_child() {
   s.managed.clear();
   s.ipc.clear();
   s.host.clear();
+  s.vcharge.clear();
   svm_forget();
   svm_tenant_forget();
   for (auto& b : s.ipc_bytes) b.store(0);
@@ -487,6 +488,32 @@ void shim_init_after_hsa() {
   }
   for (int i = 0; i < kMaxDevices; i++) resolved.dev[i] = i < s.n_agents ? per_agent[i] : DeviceConfig();
   resolved.num_devices = s.n_agents;
+  if (cfg.duplicate_split && map.duplicates) {
+    // Split duplicate vGPUs (vdev_hooks.cpp): each vGPU of a GPU that backs several gets a
+    // region slot of its own after the agents' - agent by agent, in map order - holding its
+    // quota; the agent's slot keeps the summed quota as the physical guard.
+    int next = s.n_agents;
+    for (int a = 0; a < s.n_agents; a++) {
+      char au[64];
+      normalize_uuid(uuids[a], au, sizeof(au));
+      int idx[kMaxDevices], c = 0;
+      for (int j = 0; j < map.n; j++) {
+        char mu[64];
+        normalize_uuid(map.e[j].uuid, mu, sizeof(mu));
+        if (!strcmp(mu, au)) idx[c++] = map.e[j].vidx;
+      }
+      for (int k = 0; c > 1 && k < c && next < kMaxDevices; k++, next++) {
+        DeviceConfig v = cfg.dev[idx[k]];
+        v.cu_limit_pct = 0;  // compute stays per physical GPU (the agent's slot)
+        v.cu_range_begin = v.cu_range_end = -1;
+        memcpy(v.uuid, uuids[a], sizeof(v.uuid) - 1);
+        v.uuid[sizeof(v.uuid) - 1] = 0;
+        resolved.dev[next] = v;
+      }
+    }
+    resolved.num_devices = next;
+    VLOG_INFO("duplicate vGPUs split: %d virtual quota slot(s)", next - s.n_agents);
+  }
 
   // Host PID: sysfs is not PID-namespaced; outside a container it equals getpid(),
   // inside one the VRAM signature resolves it (the maintenance thread retries).

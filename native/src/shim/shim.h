@@ -105,6 +105,7 @@ struct ShimState {
   std::unordered_map<uintptr_t, AllocRec> managed;  // hipMallocManaged pointers charged at HIP level
   std::unordered_map<uintptr_t, AllocRec> ipc;      // IPC-attached pointers (owned by another process)
   std::unordered_map<uintptr_t, HostRec> host;      // pinned host memory (host_hooks.cpp)
+  std::unordered_map<uintptr_t, AllocRec> vcharge;  // split duplicate vGPUs: the virtual slot charged (dev = slot)
   hsa_amd_memory_pool_t cpu_pools[kMaxAgentPools]{};  // global pools of the CPU agents (pinned host memory)
   int n_cpu_pools = 0;
   std::unordered_map<uintptr_t, int> queues;        // hsa_queue_t* → ordinal (under queue_mu)
@@ -297,5 +298,15 @@ extern thread_local bool t_managed_alloc;
 int hip_device_agent(int hipdev);
 // hip_device_agent of the calling thread's current HIP device (0 when unknown).
 int current_hip_agent();
+
+// Split duplicate vGPUs (vdev_hooks.cpp, VGPU_DUPLICATE_SPLIT): two vGPUs of one physical GPU
+// are two HIP devices of the container, each with its own quota. vdev_split_active() is one
+// relaxed load; vdev_to_phys maps a virtual ordinal to the physical one (negative ordinals -
+// hipCpuDeviceId, hipInvalidDeviceId - and everything when split is off pass unchanged).
+bool vdev_split_active();
+int vdev_to_phys(int v);
+// The region slot holding the quota of the virtual device the calling thread allocates on
+// device (agent) `dev`, or -1 (no split, or no virtual device of that agent).
+int vdev_charge_slot(int dev);
 
 }  // namespace vgpu

@@ -172,8 +172,11 @@ hipError_t hipGetDevice(int* d) {
   return hipSuccess;
 }
 
+void fake_hip_record(const char* name);
+
 hipError_t hipDeviceGetAttribute(int* value, hipDeviceAttribute_t attr, int d) {
   init();
+  fake_hip_record("hipDeviceGetAttribute");
   if (!value || d < 0 || d >= g_n) return hipErrorInvalidDevice;
   uint32_t bdf = 0, dom = 0;
   hsa_agent_get_info(g_dev[d].agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
@@ -221,6 +224,38 @@ hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
   hsa_amd_memory_pool_get_info(g_dev[t_dev].pool, HSA_AMD_MEMORY_POOL_INFO_SIZE, &total);
   *free_b = avail;
   *total_b = total;
+  return hipSuccess;
+}
+
+hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600* prop, int d) {
+  init();
+  if (!prop || d < 0 || d >= g_n) return hipErrorInvalidDevice;
+  memset(prop, 0, sizeof(*prop));
+  snprintf(prop->name, sizeof(prop->name), "fake gfx950 %d", d);
+  size_t total = 0;
+  hsa_amd_memory_pool_get_info(g_dev[d].pool, HSA_AMD_MEMORY_POOL_INFO_SIZE, &total);
+  prop->totalGlobalMem = total;
+  prop->multiProcessorCount = 256;
+  return hipSuccess;
+}
+
+hipError_t hipDeviceTotalMem(size_t* bytes, hipDevice_t d) {
+  init();
+  if (!bytes || d < 0 || d >= g_n) return hipErrorInvalidDevice;
+  return hsa_amd_memory_pool_get_info(g_dev[d].pool, HSA_AMD_MEMORY_POOL_INFO_SIZE, bytes) == HSA_STATUS_SUCCESS
+             ? hipSuccess : hipErrorInvalidValue;
+}
+
+hipError_t hipDeviceCanAccessPeer(int* can, int d, int peer) {
+  init();
+  if (!can || d < 0 || d >= g_n || peer < 0 || peer >= g_n) return hipErrorInvalidDevice;
+  *can = d != peer;
+  return hipSuccess;
+}
+
+hipError_t hipDeviceEnablePeerAccess(int peer, unsigned int) {
+  init();
+  if (peer < 0 || peer >= g_n || peer == t_dev) return hipErrorInvalidDevice;  // CLR: not itself
   return hipSuccess;
 }
 

@@ -7,6 +7,9 @@
 //   malloc=SIZE      hipMalloc (K/M/G suffixes) -> {"malloc": "ok"|"oom"}
 //   free             hipFree of the most recent successful allocation
 //   meminfo          hipMemGetInfo -> {"free": .., "total": ..}
+//   count            hipGetDeviceCount and hipGetDevice -> {"count": n, "current": d}
+//   props=D          hipGetDeviceProperties / hipDeviceTotalMem of device D -> {"total": .., "totalmem": ..}
+//   canpeer=A,B      hipDeviceCanAccessPeer(A, B), then hipDeviceEnablePeerAccess(B) from the current device
 //   stream           hipStreamCreate on the current device (becomes the current stream)
 //   usestream=I      the I-th stream created so far becomes the current stream (the current
 //                    device stays: a stream of another device used from this thread)
@@ -295,6 +298,26 @@ int main(int argc, char** argv) {
           first = false;
         }
       printf("]}\n");
+    } else if (key == "count") {
+      int n = -1;
+      hipError_t e = hipGetDeviceCount(&n);
+      int cur = -1;
+      (void)hipGetDevice(&cur);
+      printf("{\"count\": %d, \"rc\": %d, \"current\": %d}\n", n, (int)e, cur);
+    } else if (key == "props") {
+      hipDeviceProp_t p;
+      const int d = atoi(val.c_str());
+      hipError_t e = hipGetDeviceProperties(&p, d);
+      size_t tm = 0;
+      hipError_t e2 = hipDeviceTotalMem(&tm, d);
+      printf("{\"props\": %d, \"rc\": %d, \"total\": %zu, \"totalmem\": %zu, \"rc2\": %d}\n", d, (int)e,
+             e == hipSuccess ? (size_t)p.totalGlobalMem : 0, tm, (int)e2);
+    } else if (key == "canpeer") {
+      const int a = atoi(val.c_str()), b = atoi(val.substr(val.find(',') + 1).c_str());
+      int can = -1;
+      hipError_t e = hipDeviceCanAccessPeer(&can, a, b);
+      hipError_t e2 = hipDeviceEnablePeerAccess(b, 0);
+      printf("{\"canpeer\": %d, \"rc\": %d, \"enable\": %d}\n", can, (int)e, (int)e2);
     } else if (key == "meminfo") {
       size_t f = 0, t = 0;
       (void)hipMemGetInfo(&f, &t);

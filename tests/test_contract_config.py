@@ -302,6 +302,7 @@ def test_placement_duplicate_and_host_memory_flags():
     cfg = parse_config([], environ={})
     assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("spread", "merge", 0)
     assert parse_config(["--duplicate-vgpus", "reject"], environ={}).duplicate_vgpus == "reject"
+    assert parse_config(["--duplicate-vgpus", "split"], environ={}).duplicate_vgpus == "split"
     for bad in (["--placement", "random"], ["--duplicate-vgpus", "allow"], ["--host-memory-per-vgpu", "lots"]):
         with pytest.raises(ValueError):
             parse_config(bad, environ={})

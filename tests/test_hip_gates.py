@@ -22,7 +22,7 @@ from amdvgpu.shim.native import LIB_DIR, shim_path
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DEF = os.path.join(REPO, "native", "src", "shim", "hip_gates.def")
 HARNESS = os.path.join(LIB_DIR, "fakerocm", "shim_harness")
-TRAMPOLINE_KINDS = ("launch", "graph", "copy", "set", "suspend")
+TRAMPOLINE_KINDS = ("launch", "graph", "copy", "set", "suspend", "device")
 ROCM_HIP = "/opt/rocm/lib/libamdhip64.so"
 
 # Exported entry points that must be gated, by name pattern: every kernel launch and graph
@@ -38,7 +38,7 @@ def table():
     for line in open(DEF):
         line = line.split("#", 1)[0].split()
         if line:
-            rows.append(tuple(line))
+            rows.append(tuple(line[:3]))   # (device rows carry argument positions too)
     return rows
 
 

@@ -259,6 +259,26 @@ def test_duplicate_vgpus_rejected_on_request(plugin_dir):
         shutdown(k, stop, th)
 
 
+def test_duplicate_vgpus_split_into_separate_devices(plugin_dir):
+    """--duplicate-vgpus=split: the same two-vGPU pod on a one-GPU node gets both vGPUs as
+    separate devices - the map names the GPU twice with a quota each, and the shim is told to
+    keep them apart (VGPU_DUPLICATE_SPLIT; tests/test_duplicate_split.py runs the shim side)."""
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=4, backend=FakeBackend(n=1),
+                                  duplicate_vgpus="split")
+    try:
+        k.wait_registered("amd.com/gpu")
+        k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
+        ids, resp = k.allocate("amd.com/gpu", 2)
+        envs = dict(resp.envs)
+        uuid = ids[0].rsplit("-", 1)[0]
+        assert envs["VGPU_DUPLICATE_SPLIT"] == "1" and "VGPU_DUPLICATE_MERGED" not in envs
+        assert dict(resp.annotations)["amd-vgpu/split-duplicates"] == uuid
+        assert envs["VGPU_DEVICE_MAP"] == f"0:{uuid} 1:{uuid}"
+        assert envs["VGPU_DEVICE_MEMORY_LIMIT_0"] == envs["VGPU_DEVICE_MEMORY_LIMIT_1"]
+    finally:
+        shutdown(k, stop, th)
+
+
 def test_readme_two_vgpu_pod_admitted_on_a_one_gpu_node(plugin_dir):
     """The reference README's sample pod requests two vGPUs (README.md:205). On a node with
     one GPU the kubelet must hand it two vGPUs of that GPU; by default (merge) Allocate admits
