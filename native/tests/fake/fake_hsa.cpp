@@ -31,6 +31,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <errno.h>
+#include <pthread.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -152,9 +153,30 @@ void kfd_update_vram(int dev) {
   write_file(s.kfd + "/vram_" + std::to_string(s.gpus[dev].gpu_id), s.gpus[dev].used.load() - svm);
 }
 
+// A forked child is a new KFD process: its own (empty) process directory and no HBM of its
+// own - what the driver gives a child that opens the GPU, so the shim's host-PID discovery in
+// the child finds the child, not the parent.
+void fake_atfork_child() {
+  State& s = st();
+  if (!s.inited || s.kfd.empty()) return;
+  const char* root = getenv("FAKE_KFD_ROOT");
+  if (!root) return;
+  s.kfd = std::string(root) + "/" + std::to_string((int)getpid() + (int)env_u64("FAKE_KFD_PID_OFFSET", 100000));
+  mkdir(s.kfd.c_str(), 0777);
+  for (int i = 0; i < s.n; i++) {
+    s.gpus[i].used.store(0);
+    s.gpus[i].svm_used.store(0);
+    std::string stats = s.kfd + "/stats_" + std::to_string(s.gpus[i].gpu_id);
+    mkdir(stats.c_str(), 0777);
+    write_file(stats + "/cu_occupancy", 0);
+    kfd_update_vram(i);
+  }
+}
+
 void setup() {
   State& s = st();
   if (s.inited) return;
+  pthread_atfork(nullptr, nullptr, fake_atfork_child);
   s.n = (int)env_u64("FAKE_ROCR_GPUS", 2);
   if (s.n < 1) s.n = 1;
   if (s.n > 16) s.n = 16;

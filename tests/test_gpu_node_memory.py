@@ -38,13 +38,19 @@ t0 = time.time()
 while reg.device(0)["spilled"] and time.time() - t0 < 30:
     time.sleep(0.1)
 promoted = spilled0 - reg.device(0)["spilled"]
-emit(phase="promoted", spilled0=spilled0, promoted=promoted, promote_s=round(time.time() - t0, 2))
+def kfd_vram():   # KFD's count of this process's VRAM (SVM pages included on MI355X, profiles/r5b)
+    import glob
+    for f in glob.glob(f"/sys/class/kfd/kfd/proc/{os.getpid()}/vram_*"):
+        return int(open(f).read())
+    return -1
+emit(phase="promoted", spilled0=spilled0, promoted=promoted, promote_s=round(time.time() - t0, 2), vram=kfd_vram())
 open(os.environ["A_READY"], "w").close()
 t0 = time.time()
 while not os.path.exists(os.environ["A_DONE"]) and time.time() - t0 < 120:
     time.sleep(0.1)
+vram_after = kfd_vram()
 ok = bool((y == 7).all().item())
-emit(phase="after", spilled=reg.device(0)["spilled"], intact=ok)
+emit(phase="after", spilled=reg.device(0)["spilled"], intact=ok, vram=vram_after)
 """
 
 NATIVE_FREE = """
@@ -82,13 +88,15 @@ def test_promoted_spill_is_seen_and_given_back_across_containers(tmp_path):
             time.sleep(0.1)
         assert os.path.exists(common["A_READY"]), pa.stderr.read()[-3000:] if pa.poll() is not None else "A not ready"
         (native,), _ = run_child(NATIVE_FREE, None, preload=False, timeout=120)
-        b = vgpu_env(mem_limit=300 * GiB, shared_cache=str(tmp_path / "b.cache"),
+        b = vgpu_env(mem_limit=300 * GiB, shared_cache=str(tmp_path / "b.cache"), log_level=2,
                      extra={**common, "VGPU_BOARD_SLOT": "b.slot"})
         (rb,), pb = run_child(B_CODE, b, timeout=120, check=False)
     finally:
         open(common["A_DONE"], "w").close()
         out, err = pa.communicate(timeout=120)
     ra = child_results(out)
+    print("A log:", [l for l in err.splitlines() if "vGPU" in l][-6:])
+    print("B log:", [l for l in pb.stderr.splitlines() if "vGPU" in l][-6:])
     promoted = [r for r in ra if r.get("phase") == "promoted"][0]
     after = [r for r in ra if r.get("phase") == "after"][0]
     print(json.dumps({"a": ra, "native_free": native["free"], "b": rb}))
