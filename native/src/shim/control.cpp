@@ -64,6 +64,13 @@ __attribute__((visibility("default"))) uint64_t vgpu_get_current_device_spilled(
   return ok() ? shim().region.raw()->dev[current_device()].spilled.load() : 0;
 }
 
+// HBM of the current device holding shared virtual memory - this container's promoted spills
+// and prefetched ranges, and (node board) other containers' - that ROCr's free-memory figure
+// does not show; the shim takes it off the free HBM it reports and places by (spill.cpp).
+__attribute__((visibility("default"))) uint64_t vgpu_get_current_device_hidden_vram() {
+  return ok() ? hidden_vram(current_device()) : 0;
+}
+
 // Pinned host memory the container holds (VGPU_HOST_MEMORY_LIMIT's budget, host_hooks.cpp).
 __attribute__((visibility("default"))) uint64_t vgpu_get_host_memory_usage() {
   return ok() ? shim().region.host_usage() : 0;

@@ -38,9 +38,10 @@ t0 = time.time()
 while reg.device(0)["spilled"] and time.time() - t0 < 30:
     time.sleep(0.1)
 promoted = spilled0 - reg.device(0)["spilled"]
+hostpid = [p["hostpid"] for p in reg.procs() if p["pid"] == os.getpid()][0]
 def kfd_vram():   # KFD's count of this process's VRAM (SVM pages included on MI355X, profiles/r5b)
     import glob
-    for f in glob.glob(f"/sys/class/kfd/kfd/proc/{os.getpid()}/vram_*"):
+    for f in glob.glob(f"/sys/class/kfd/kfd/proc/{hostpid}/vram_*"):
         return int(open(f).read())
     return -1
 emit(phase="promoted", spilled0=spilled0, promoted=promoted, promote_s=round(time.time() - t0, 2), vram=kfd_vram())
@@ -62,6 +63,10 @@ B_CODE = """
 import torch
 time.sleep(1.5)                                  # the sampler has read the board
 free, total = torch.cuda.mem_get_info(0)
+import ctypes
+shim = ctypes.CDLL(None)
+shim.vgpu_get_current_device_hidden_vram.restype = ctypes.c_uint64
+hidden = shim.vgpu_get_current_device_hidden_vram()
 want = free + (7 << 30)                          # needs 7 of A's 8 GiB: more than B sees free, within its quota
 t0 = time.time()
 try:
@@ -70,7 +75,7 @@ try:
     ok = True
 except torch.OutOfMemoryError as e:
     ok = False
-emit(free=free, total=total, want=want, ok=ok, alloc_s=round(time.time() - t0, 2))
+emit(free=free, total=total, want=want, ok=ok, alloc_s=round(time.time() - t0, 2), hidden=hidden)
 """
 
 
@@ -101,8 +106,9 @@ def test_promoted_spill_is_seen_and_given_back_across_containers(tmp_path):
     after = [r for r in ra if r.get("phase") == "after"][0]
     print(json.dumps({"a": ra, "native_free": native["free"], "b": rb}))
     assert promoted["promoted"] >= 8 * GiB, promoted
-    # B sees ROCr's free figure less A's promoted 8 GiB (B's own runtime footprint aside)
-    hidden = native["free"] - rb["free"]
-    assert 8 * GiB - 256 * MiB <= hidden <= 8 * GiB + 2 * GiB, (native, rb)
+    # B takes A's promoted 8 GiB off ROCr's free figure (B's and the probe's own runtime
+    # footprints differ by up to ~1 GiB between runs)
+    assert rb["hidden"] == 8 * GiB, rb
+    assert 7 * GiB <= native["free"] - rb["free"] <= 9 * GiB + 512 * MiB, (native, rb)
     assert rb["ok"], rb                            # served: A's spill gave the HBM back
     assert after["intact"], after                  # A's data survived the move
