@@ -321,10 +321,26 @@ void install_ceilings(const char* const* uuid_ptrs) {
 }
 
 // Fills the region's per-device state from the resolved config where no process of the
-// container has yet (d.configured == 0). Called with the region lock held.
-void configure_devices(Region* r, const DeviceConfig* per_agent) {
+// container has yet (d.configured == 0). Called with the region lock held. The resolved
+// limits win over what is there: a region first created by a process that never
+// initialised ROCr (amd-smi, torch's device count through amdsmi) holds the raw
+// per-vGPU values of the environment, not the per-agent ones - for two vGPUs of one GPU,
+// vGPU 0's quota where the merged GPU has both.
+void configure_devices(Region* r, const DeviceConfig* per_agent, const Config& resolved) {
   ShimState& s = shim();
   if (r->hdr.num_devices < s.n_agents) r->hdr.num_devices = s.n_agents;
+  // Split duplicate vGPUs: their own quota slots after the agents' (vdev_hooks.cpp).
+  for (int i = s.n_agents; i < resolved.num_devices && i < kMaxDevices; i++) {
+    DeviceState& d = r->dev[i];
+    if (d.configured) continue;
+    snprintf(d.uuid, sizeof(d.uuid), "%.63s", resolved.dev[i].uuid);
+    d.mem_limit = resolved.dev[i].mem_limit;
+    d.hbm_limit = 0;
+    d.cu_limit_pct = 0;
+    d.gate_open.store(1);
+    d.configured = 1;
+    if (r->hdr.num_devices < i + 1) r->hdr.num_devices = i + 1;
+  }
   for (int i = 0; i < s.n_agents; i++) {
     AgentInfo& a = s.agents[i];
     DeviceState& d = r->dev[i];
@@ -340,10 +356,10 @@ void configure_devices(Region* r, const DeviceConfig* per_agent) {
     real_hsa_agent_get_info(a.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
     d.bdf = bdf;
     d.domain = dom;
-    if (!d.mem_limit && per_agent[i].mem_limit) d.mem_limit = per_agent[i].mem_limit;
-    if (!d.hbm_limit && per_agent[i].hbm_limit) d.hbm_limit = per_agent[i].hbm_limit;
-    if (!d.cu_limit_pct && per_agent[i].cu_limit_pct) d.cu_limit_pct = per_agent[i].cu_limit_pct;
-    if (d.cu_range_begin < 0 && per_agent[i].cu_range_begin >= 0) {
+    if (per_agent[i].mem_limit) d.mem_limit = per_agent[i].mem_limit;
+    if (per_agent[i].hbm_limit) d.hbm_limit = per_agent[i].hbm_limit;
+    if (per_agent[i].cu_limit_pct) d.cu_limit_pct = per_agent[i].cu_limit_pct;
+    if (per_agent[i].cu_range_begin >= 0) {
       d.cu_range_begin = per_agent[i].cu_range_begin;
       d.cu_range_end = per_agent[i].cu_range_end;
     }
@@ -550,7 +566,7 @@ void shim_init_after_hsa() {
   }
   Region* r = s.region.raw();
   s.region.lock();
-  configure_devices(r, per_agent);
+  configure_devices(r, per_agent, resolved);
   s.region.unlock();
   clamp_region_to_ceiling();
   s.seen_generation.store(r->hdr.generation.load() - 1);  // forces the first apply below
@@ -694,7 +710,7 @@ void check_region_epoch() {
     s.region.lock();
     DeviceConfig per_agent[kMaxDevices];
     for (int i = 0; i < kMaxDevices; i++) per_agent[i] = s.resolved.dev[i];
-    configure_devices(r, per_agent);
+    configure_devices(r, per_agent, s.resolved);
     s.region.unlock();
     clamp_region_to_ceiling();
   }

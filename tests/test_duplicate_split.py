@@ -64,3 +64,24 @@ def test_split_quota_is_shared_by_the_containers_processes(fake):  # noqa: F811
     p.stdout.read()
     assert p.wait(30) == 0
     assert [o["malloc"] for o in _one(out, "malloc")] == ["oom", "ok", "ok"], out
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_region_created_by_an_smi_process_first(fake, split):  # noqa: F811
+    """torch counts devices through amdsmi before it initialises HIP, so a process that never
+    initialises ROCr may create the container's region first, with the environment's raw
+    per-vGPU limits. The first GPU process then writes the resolved ones: the merged GPU holds
+    both vGPUs' quota (3 GiB), and with split each vGPU its own."""
+    import subprocess
+    import sys
+    from test_rsmi_remap import CHILD, FAKE_RSMI
+    e = _env(fake, split)
+    p = subprocess.run([sys.executable, "-c", CHILD, FAKE_RSMI], env=e, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr[-2000:]
+    if split:
+        out = run(e, "props=0", "props=1", "dev=1", "malloc=1500m", "dev=0", "malloc=1500m")
+        assert [p["total"] for p in _one(out, "props")] == [GiB, 2 * GiB], out
+        assert [o["malloc"] for o in _one(out, "malloc")] == ["ok", "oom"], out
+    else:
+        out = run(e, "meminfo", "malloc=2500m")
+        assert _one(out, "free")[0]["total"] == 3 * GiB and _one(out, "malloc")[0]["malloc"] == "ok", out
