@@ -352,7 +352,12 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         if v.uuid not in uuids:
             uuids.append(v.uuid)
     ids = device_ids(cfg, devices_by_uuid, uuids)
-    resp.envs.update(visible_envs(cfg, ids))
+    split = getattr(cfg, "duplicate_vgpus", "merge") == "split" and len(uuids) < len(vdevs)
+    # --duplicate-vgpus=split: one entry per vGPU, so frameworks that count devices from the
+    # visible list (torch.cuda.device_count) see every vGPU; ROCr lists a GPU named twice once
+    # (profiles/r4dup) and the shim presents the second one.
+    vis_ids = device_ids(cfg, devices_by_uuid, [v.uuid for v in vdevs]) if split else ids
+    resp.envs.update(visible_envs(cfg, vis_ids))
     if cfg.device_list_strategy == LIST_VOLUME_MOUNTS:
         for i in ids:
             resp.mounts.add(container_path=os.path.join(VOLUME_MOUNTS_ROOT, i), host_path=VOLUME_MOUNTS_HOST)
@@ -407,12 +412,14 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         resp.envs["VGPU_HOST_MEMORY_LIMIT"] = format_mib(host_per * len(vdevs))
     # PCI addresses of the container's GPUs: in-container amd-smi lists only these
     # (reference: nvmlDeviceGetCount / GetHandleByIndex remapping, nvml/hook.c:438-527).
-    bdfs = [devices_by_uuid[u].bdf for u in uuids if u in devices_by_uuid and devices_by_uuid[u].bdf]
+    # (split duplicates: one entry per vGPU, so amd-smi lists every vGPU)
+    listed = [v.uuid for v in vdevs] if split else uuids
+    bdfs = [devices_by_uuid[u].bdf for u in listed if u in devices_by_uuid and devices_by_uuid[u].bdf]
     if bdfs:
         resp.envs["VGPU_DEVICE_BDFS"] = ",".join(bdfs)
         # KFD gpu_ids of the same devices: compute partitions exposed as GPUs share a PCI
         # address, and amd-smi inside the container must list only this container's.
-        gids = [str(devices_by_uuid[u].gpu_id or 0) for u in uuids if u in devices_by_uuid and devices_by_uuid[u].bdf]
+        gids = [str(devices_by_uuid[u].gpu_id or 0) for u in listed if u in devices_by_uuid and devices_by_uuid[u].bdf]
         if any(g != "0" for g in gids):
             resp.envs["VGPU_DEVICE_GPU_IDS"] = ",".join(gids)
     # Always explicit, so a container never depends on the shim's built-in default.

@@ -151,6 +151,23 @@ std::vector<Bdf> visible_bdfs() {
   return out;
 }
 
+bool amdsmi_visible(amdsmi_processor_handle h, const std::vector<Bdf>& vis);
+
+// Split duplicate vGPUs (VGPU_DUPLICATE_SPLIT): a GPU the device list names k times is listed
+// k times - one entry per vGPU, as the container's HIP devices are (vdev_hooks.cpp).
+int visible_times(amdsmi_processor_handle h, const std::vector<Bdf>& vis) {
+  if (!amdsmi_visible(h, vis)) return 0;
+  if (!config().duplicate_split) return 1;
+  VGPU_REAL_IMPL(amdsmi_get_gpu_device_bdf, "libamd_smi", nullptr);
+  amdsmi_bdf_t b;
+  b.as_uint = 0;
+  if (!real_amdsmi_get_gpu_device_bdf || real_amdsmi_get_gpu_device_bdf(h, &b) != AMDSMI_STATUS_SUCCESS) return 1;
+  int k = 0;
+  for (const Bdf& v : vis)
+    if (v.domain == (b.as_uint >> 16) && v.bdfid == (uint32_t)(b.as_uint & 0xffff)) k++;
+  return k > 0 ? k : 1;
+}
+
 bool amdsmi_visible(amdsmi_processor_handle h, const std::vector<Bdf>& vis) {
   VGPU_REAL_IMPL(amdsmi_get_gpu_device_bdf, "libamd_smi", nullptr);
   if (!real_amdsmi_get_gpu_device_bdf) return true;
@@ -210,10 +227,11 @@ RsmiMap& rsmi_map() {
   for (uint32_t i = 0; i < n; i++) {
     uint64_t id = 0;
     if (real_rsmi_dev_pci_id_get(i, &id) != RSMI_STATUS_SUCCESS) continue;
+    // (split duplicate vGPUs: one index per entry of the device list naming this GPU)
     for (const Bdf& v : vis)
       if (v.domain == (id >> 32) && v.bdfid == (uint32_t)(id & 0xffff)) {
         m->phys.push_back(i);
-        break;
+        if (!config().duplicate_split) break;
       }
   }
   m->identity = false;
@@ -328,7 +346,7 @@ amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle socket, uint32
   if (n && (st = real_amdsmi_get_processor_handles(socket, &n, all.data())) != AMDSMI_STATUS_SUCCESS) return st;
   std::vector<amdsmi_processor_handle> mine;
   for (uint32_t i = 0; i < n && i < all.size(); i++)
-    if (amdsmi_visible(all[i], vis)) mine.push_back(all[i]);
+    for (int k = visible_times(all[i], vis); k > 0; k--) mine.push_back(all[i]);
   if (!handles) {
     *count = (uint32_t)mine.size();
     return AMDSMI_STATUS_SUCCESS;

@@ -85,3 +85,13 @@ def test_region_created_by_an_smi_process_first(fake, split):  # noqa: F811
     else:
         out = run(e, "meminfo", "malloc=2500m")
         assert _one(out, "free")[0]["total"] == 3 * GiB and _one(out, "malloc")[0]["malloc"] == "ok", out
+
+
+def test_smi_lists_every_vgpu_with_split(tmp_path):
+    """In-container rocm-smi / amd-smi list one device per vGPU with split (the plugin names
+    the GPU once per vGPU in VGPU_DEVICE_BDFS), once per GPU with merge."""
+    from test_rsmi_remap import run as rsmi_run
+    two = rsmi_run(tmp_path, VGPU_DEVICE_BDFS="0000:05:00.0,0000:05:00.0", VGPU_DUPLICATE_SPLIT="1")
+    assert two["n"] == 2 and [i for _st, i in two["ids"][:2]] == [0x1000, 0x1000], two
+    one = rsmi_run(tmp_path, VGPU_DEVICE_BDFS="0000:05:00.0,0000:05:00.0")
+    assert one["n"] == 1, one

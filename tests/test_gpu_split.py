@@ -36,17 +36,21 @@ emit(n=n, totals=[t for _f, t in info], props=props, cur=cur, close=abs(b - ref)
 """
 
 
-def _uuid():
+def _gpu():
     from amdvgpu.plugin.devices import SysfsBackend
     devs = SysfsBackend().devices()
     assert devs, "no GPU in sysfs"
-    return devs[0].uuid
+    return devs[0]
 
 
 def test_two_vgpus_of_one_gpu_are_two_torch_devices(tmp_region):
-    uuid = _uuid()
-    c = vgpu_env(shared_cache=tmp_region, device_map=[uuid, uuid], per_device_mem=[4 * GiB, 6 * GiB],
-                 extra={"VGPU_DUPLICATE_SPLIT": "1", "SPLIT_UUID": uuid})
+    g = _gpu()
+    # As the plugin's contract for --duplicate-vgpus=split (contract.py): the GPU named once per
+    # vGPU in the visible list and the BDF list. (HIP_VISIBLE_DEVICES, which the GPU box sets,
+    # is widened to match: torch prefers it over ROCR_VISIBLE_DEVICES.)
+    c = vgpu_env(shared_cache=tmp_region, device_map=[g.uuid, g.uuid], per_device_mem=[4 * GiB, 6 * GiB],
+                 extra={"VGPU_DUPLICATE_SPLIT": "1", "SPLIT_UUID": g.uuid, "ROCR_VISIBLE_DEVICES": f"{g.uuid},{g.uuid}",
+                        "HIP_VISIBLE_DEVICES": "0,1", "VGPU_DEVICE_BDFS": f"{g.bdf},{g.bdf}"})
     res, p = run_child(SPLIT, c, timeout=300, check=False)
     assert res, p.stderr[-3000:]
     r = res[0]

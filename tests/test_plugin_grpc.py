@@ -275,6 +275,10 @@ def test_duplicate_vgpus_split_into_separate_devices(plugin_dir):
         assert dict(resp.annotations)["amd-vgpu/split-duplicates"] == uuid
         assert envs["VGPU_DEVICE_MAP"] == f"0:{uuid} 1:{uuid}"
         assert envs["VGPU_DEVICE_MEMORY_LIMIT_0"] == envs["VGPU_DEVICE_MEMORY_LIMIT_1"]
+        # one entry per vGPU: torch.cuda.device_count() counts the visible list, amd-smi the BDFs
+        assert envs["ROCR_VISIBLE_DEVICES"] == f"{uuid},{uuid}"
+        bdf = FakeBackend(n=1).devices()[0].bdf
+        assert envs["VGPU_DEVICE_BDFS"] == f"{bdf},{bdf}"
     finally:
         shutdown(k, stop, th)
 
