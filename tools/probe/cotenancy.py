@@ -201,7 +201,8 @@ def launch(a):
             c += ["--mem-node", str(mem_of(i))]
         if not a.trace:
             return c
-        prof = ["rocprofv3", "--kernel-trace"] + (["--hip-trace", "--stats"] if a.hip_stats else [])
+        prof = ["rocprofv3", "--kernel-trace"] + (["--hip-trace"] if a.hip_stats else []) + \
+            (["--hsa-trace"] if a.hsa_stats else []) + (["--stats"] if a.hip_stats or a.hsa_stats else [])
         return prof + ["--output-format", "csv", "-d", os.path.join(a.trace, f"t{i}"), "-o", f"t{i}", "--"] + c
     def env_of(i):
         env = dict(os.environ)
@@ -238,10 +239,11 @@ def launch(a):
     return 0 if all(p.returncode == 0 for p in procs) else 1
 
 
-def hip_stats(d):
-    """Per tenant: the HIP API calls that took the most time (rocprofv3 --hip-trace --stats)."""
+def hip_stats(d, api="hip"):
+    """Per tenant: the HIP (or HSA) API calls that took the most time (rocprofv3
+    --hip-trace / --hsa-trace --stats)."""
     out = {}
-    for f in glob.glob(os.path.join(d, "**", "*hip_api_stats.csv"), recursive=True):
+    for f in glob.glob(os.path.join(d, "**", f"*{api}_api_stats.csv"), recursive=True):
         rows = []
         with open(f) as fh:
             for row in csv.DictReader(fh):
@@ -252,7 +254,7 @@ def hip_stats(d):
                     continue
         rows.sort(key=lambda r: -r[2])
         out[_tenant_of_path(d, f)] = [{"api": n, "calls": c, "total_ms": round(t, 1), "avg_us": round(av, 2)}
-                                      for n, c, t, av in rows[:6]]
+                                      for n, c, t, av in rows[:10]]
     return out
 
 
@@ -331,9 +333,10 @@ def analyze(d):
         both = iv if both is None else intersect(both, iv)
     res["both"] = round(length(both) / win, 4) if len(clipped) > 1 else None
     res["any"] = round(length(merge([x for iv in clipped.values() for x in iv])) / win, 4)
-    hs = hip_stats(d)
-    if hs:
-        res["hip_api"] = hs
+    for api in ("hip", "hsa"):
+        hs = hip_stats(d, api)
+        if hs:
+            res[f"{api}_api"] = hs
     return res
 
 
@@ -348,6 +351,7 @@ def main():
     ap.add_argument("--analyze")
     ap.add_argument("--trace", default="", help="rocprofv3 kernel trace of every tenant under this directory")
     ap.add_argument("--hip-stats", action="store_true", help="with --trace: HIP API trace and stats too")
+    ap.add_argument("--hsa-stats", action="store_true", help="with --trace: HSA API trace and stats too")
     ap.add_argument("--pin", type=int, default=0, help="pin tenant i to K CPUs of its own")
     ap.add_argument("--burners", type=int, default=0, help="CPU-only processes spinning during the window")
     ap.add_argument("--placement", default="none", choices=["none", "local", "remote", "split"],
