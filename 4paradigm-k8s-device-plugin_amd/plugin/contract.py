@@ -114,7 +114,8 @@ CONTAINER_REGION_DIR = "/usr/local/vgpu/regions"
 # container's devices: each Allocate records the device IDs in a manifest
 # (<vgpu_dir>/containers/<name>.devices), and gc_container_files removes a container's
 # files only when the kubelet's PodResources no longer lists those devices as held - never
-# by age, and never when PodResources cannot be asked.
+# by age (except files older than the manifests themselves, LEGACY_GC_AGE_S), and never when
+# PodResources cannot be asked.
 MANIFEST_HOST_DIR = "containers"
 CONTAINER_GC_GRACE_S = 600
 # The env names the limits file carries (the shim reads it with the env parser).
@@ -170,7 +171,7 @@ def gc_container_files(vgpu_dir, held, grace_s=CONTAINER_GC_GRACE_S, now=None):
     try:
         names = [fn[:-len(".devices")] for fn in os.listdir(d) if fn.endswith(".devices")]
     except OSError:
-        return removed
+        names = []
     for name in names:
         path = os.path.join(d, name + ".devices")
         try:
@@ -182,6 +183,37 @@ def gc_container_files(vgpu_dir, held, grace_s=CONTAINER_GC_GRACE_S, now=None):
         if res is None or not ids or ids in held.get(res, ()):
             continue
         for fp in container_files(vgpu_dir, name) + [path]:
+            try:
+                os.unlink(fp)
+            except OSError:
+                pass
+        removed.append(name)
+    return removed + _gc_legacy_container_files(vgpu_dir, now)
+
+
+# Containers allocated by a plugin older than the manifests (round 4) have host files but no
+# manifest, so PodResources cannot vouch for them either way. They are removed once their
+# limits file is this old: far past any pod's restart of a node the plugin was upgraded on,
+# and only when PodResources answered (the caller returns early otherwise).
+LEGACY_GC_AGE_S = 30 * 24 * 3600
+
+
+def _gc_legacy_container_files(vgpu_dir, now):
+    d = os.path.join(vgpu_dir, LIMITS_HOST_DIR, "containers")
+    try:
+        names = [fn[:-len(".env")] for fn in os.listdir(d) if fn.endswith(".env")]
+    except OSError:
+        return []
+    removed = []
+    for name in names:
+        if os.path.exists(os.path.join(vgpu_dir, MANIFEST_HOST_DIR, name + ".devices")):
+            continue
+        try:
+            if now - os.path.getmtime(os.path.join(d, name + ".env")) < LEGACY_GC_AGE_S:
+                continue
+        except OSError:
+            continue
+        for fp in container_files(vgpu_dir, name):
             try:
                 os.unlink(fp)
             except OSError:

@@ -390,6 +390,24 @@ def test_container_files_live_as_long_as_the_pod(tmp_path):
         sorted([names["a-0"], names["a-2"]])
 
 
+def test_pre_manifest_container_files_go_once_they_are_a_month_old(tmp_path):
+    """host files of containers allocated before manifests existed are removed
+    once their limits file is 30 days old - never younger, never without PodResources."""
+    import time
+    from amdvgpu.plugin.contract import LEGACY_GC_AGE_S, container_files, gc_container_files
+    vdir = tmp_path / "vgpu"
+    files = [p for p in container_files(str(vdir), "old-ctr")]
+    for p in files:
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        open(p, "w").close()
+    now = time.time()
+    assert gc_container_files(str(vdir), None, now=now + 2 * LEGACY_GC_AGE_S) == []
+    assert gc_container_files(str(vdir), {}, now=now + LEGACY_GC_AGE_S / 2) == []
+    assert all(os.path.exists(p) for p in files)
+    assert gc_container_files(str(vdir), {}, now=now + LEGACY_GC_AGE_S + 60) == ["old-ctr"]
+    assert not any(os.path.exists(p) for p in files)
+
+
 def test_limits_file_carries_the_oom_killer(tmp_path):
     """The memory backstop is the plugin's: the limits file switches it (on by default)."""
     from amdvgpu.plugin.config import PluginConfig
