@@ -52,6 +52,10 @@ struct alignas(64) BoardSlot {
   std::atomic<uint64_t> svm_vram[kMaxDevices];     // the container's SVM bytes in each GPU's VRAM
   std::atomic<uint64_t> hbm_want[kMaxDevices];     // refused HBM within its share: bytes wanted ...
   std::atomic<uint64_t> hbm_want_ns[kMaxDevices];  // ... since (CLOCK_MONOTONIC; 0 = none)
+  // Appended (round 6): the CPU node the container's processes run on (VGPU_CPU_NODE), plus
+  // one (0 = unknown, as an older slot reads): the concurrency admission pairs containers of
+  // different CPU sockets.
+  std::atomic<int32_t> cpu_node1;
 };
 constexpr size_t kBoardSlotV1Size = offsetof(BoardSlot, svm_vram);
 
@@ -76,6 +80,7 @@ struct BoardPeer {
   std::vector<uint64_t> svm_vram;            // per device
   std::vector<uint64_t> hbm_want;            // per device (0 = none, or stale)
   std::vector<uint64_t> hbm_want_ns;         // per device: when it was (re-)published
+  int cpu_node = -1;                         // VGPU_CPU_NODE (-1 = unknown)
 };
 
 // A container's view of the board directory: its own slot (read-write) and the others.
@@ -101,6 +106,8 @@ class Board {
   void leave();
   // Gate state of device `dev` for the concurrency admission (every sample).
   void publish_gate(int dev, bool open, uint64_t want_since);
+  // The CPU node the container's processes run on (-1 = none / unknown).
+  void publish_cpu_node(int node);
   // Virtual device memory of device `dev`: the container's SVM bytes in VRAM, and HBM it was
   // refused within its share (0 = none) since `want_ns`.
   void publish_memory(int dev, uint64_t svm_vram, uint64_t hbm_want, uint64_t want_ns);
@@ -111,11 +118,15 @@ class Board {
 
   // Concurrency admission (VGPU_GPU_CONCURRENCY = k): may this container open its gate on
   // GPU `gpu_id`, given it has wanted to since `want_since`? Yes while fewer than k
-  // peers hold their gates open there and fewer than (k - open) peers have been waiting
-  // longer. Peers as of the last refresh().
-  bool admit(uint32_t gpu_id, int k, uint64_t want_since) const;
-  // Whether a peer on GPU `gpu_id` is waiting for admission.
-  bool waiting(uint32_t gpu_id) const;
+  // peers hold their gates open there and fewer than (k - open) peers that could be admitted
+  // have been waiting longer. CPU-socket aware: when the GPU's containers run on D > 1
+  // CPU nodes (`node`, the peers' published ones), at most ceil(k / D) holders per node -
+  // two launch-bound processes on one socket run no faster together than one alone
+  // (profiles/r5d), so k = 2 takes turns in cross-socket pairs. Peers as of the last refresh().
+  bool admit(uint32_t gpu_id, int k, uint64_t want_since, int node = -1) const;
+  // Whether a peer on GPU `gpu_id` waits for admission that this container's turn stands in
+  // the way of: any waiting peer, or with CPU nodes known only one of its own node.
+  bool waiting(uint32_t gpu_id, int node = -1) const;
 
   // Re-reads the other slots (live ones only). Cheap enough for every 100 ms.
   const std::vector<BoardPeer>& refresh(uint64_t now);

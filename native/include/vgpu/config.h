@@ -129,6 +129,8 @@ struct Config {
   int gpu_concurrency = 0;               // VGPU_GPU_CONCURRENCY: limited containers whose GPU-time
                                          // gates may be open together on one GPU (0 = any number)
   int gpu_slice_ms = 20;                 // VGPU_GPU_SLICE_MS: turn length under that admission
+  int cpu_node = -1;                     // VGPU_CPU_NODE (unless VGPU_CPU_SPREAD=0): the CPU node the
+                                         // container's processes run on, published on the board
   bool use_ledger = true;                // VGPU_LEDGER: take charges from the node's GPU-time ledger
                                          // (vgpu/ledger.h) when its daemon keeps it fresh (the plugin
                                          // runs the daemon only with --ledger: profiles/r3v)

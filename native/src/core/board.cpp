@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <set>
 
 #include "vgpu/log.h"
 
@@ -111,6 +113,10 @@ void Board::publish_gate(int dev, bool open, uint64_t want_since) {
   self_->want_since[dev].store(want_since, std::memory_order_relaxed);
 }
 
+void Board::publish_cpu_node(int node) {
+  if (self_) self_->cpu_node1.store(node >= 0 ? node + 1 : 0, std::memory_order_relaxed);
+}
+
 void Board::publish_memory(int dev, uint64_t svm_vram, uint64_t hbm_want, uint64_t want_ns) {
   if (!self_ || dev < 0 || dev >= kMaxDevices) return;
   self_->svm_vram[dev].store(svm_vram, std::memory_order_relaxed);
@@ -138,24 +144,60 @@ uint64_t Board::peers_hbm_want(uint32_t gpu_id, uint64_t* newest_ns) const {
   return n;
 }
 
-bool Board::waiting(uint32_t gpu_id) const {
+namespace {
+
+// Holders per CPU node and the distinct nodes of the containers on `gpu_id` (this one's
+// `node` included); the per-node cap of k holders (k when the nodes are unknown or one).
+struct NodeLoad {
+  std::map<int, int> held;
+  std::set<int> nodes;
+  int cap = 0;
+  bool room(int n) const {
+    if (n < 0 || nodes.size() <= 1) return true;
+    auto it = held.find(n);
+    return (it == held.end() ? 0 : it->second) < cap;
+  }
+};
+
+NodeLoad node_load(const std::vector<BoardPeer>& peers, uint32_t gpu_id, int k, int node) {
+  NodeLoad l;
+  if (node >= 0) l.nodes.insert(node);
+  for (const BoardPeer& p : peers)
+    for (size_t i = 0; i < p.gpu_ids.size() && i < p.gate.size(); i++) {
+      if (p.gpu_ids[i] != gpu_id) continue;
+      if (p.cpu_node >= 0) l.nodes.insert(p.cpu_node);
+      if (p.gate[i] && p.cpu_node >= 0) l.held[p.cpu_node]++;
+    }
+  // Socket awareness needs this container's node too: without it every node counts alike.
+  if (node < 0) l.nodes.clear();
+  const int d = (int)l.nodes.size();
+  l.cap = d > 1 ? (k + d - 1) / d : k;
+  return l;
+}
+
+}  // namespace
+
+bool Board::waiting(uint32_t gpu_id, int node) const {
   for (const BoardPeer& p : peers_)
     for (size_t i = 0; i < p.gpu_ids.size() && i < p.want_since.size(); i++)
-      if (p.gpu_ids[i] == gpu_id && p.want_since[i] && !p.gate[i]) return true;
+      if (p.gpu_ids[i] == gpu_id && p.want_since[i] && !p.gate[i] &&
+          (node < 0 || p.cpu_node < 0 || p.cpu_node == node))
+        return true;
   return false;
 }
 
-bool Board::admit(uint32_t gpu_id, int k, uint64_t want_since) const {
+bool Board::admit(uint32_t gpu_id, int k, uint64_t want_since, int node) const {
   if (k <= 0) return true;
+  const NodeLoad load = node_load(peers_, gpu_id, k, node);
   int open = 0, ahead = 0;
   for (const BoardPeer& p : peers_) {
     for (size_t i = 0; i < p.gpu_ids.size() && i < p.gate.size(); i++) {
       if (p.gpu_ids[i] != gpu_id) continue;
       if (p.gate[i]) open++;
-      else if (p.want_since[i] && p.want_since[i] < want_since) ahead++;
+      else if (p.want_since[i] && p.want_since[i] < want_since && load.room(p.cpu_node)) ahead++;
     }
   }
-  return open < k && ahead < k - open;
+  return open < k && ahead < k - open && load.room(node);
 }
 
 const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
@@ -199,6 +241,8 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
       p.hbm_want.push_back(fresh ? s.hbm_want[i].load(std::memory_order_relaxed) : 0);
       p.hbm_want_ns.push_back(fresh ? wn : 0);
     }
+    const int32_t cn = got >= (ssize_t)sizeof(BoardSlot) ? s.cpu_node1.load(std::memory_order_relaxed) : 0;
+    p.cpu_node = cn > 0 && cn <= 64 ? cn - 1 : -1;
     const int n = std::max(0, std::min(s.npids.load(std::memory_order_relaxed), kBoardMaxPids));
     for (int i = 0; i < n; i++) {
       const int pid = s.hostpids[i].load(std::memory_order_relaxed);

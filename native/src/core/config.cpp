@@ -341,6 +341,10 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   long slice = 20;
   if (parse_int(getenv_fn("VGPU_GPU_SLICE_MS"), 1, 10000, &slice)) cfg->gpu_slice_ms = (int)slice;
   if (const char* s = getenv_fn("VGPU_BOARD_SLOT")) cfg->board_slot = s;
+  long cpu_node = -1;
+  const char* spread = getenv_fn("VGPU_CPU_SPREAD");
+  if (!(spread && spread[0] == '0') && parse_int(getenv_fn("VGPU_CPU_NODE"), 0, 63, &cpu_node))
+    cfg->cpu_node = (int)cpu_node;
   if (const char* s = getenv_fn("VGPU_LEDGER")) cfg->use_ledger = !(s[0] == '0' && !s[1]);
   long hold = 3;
   if (parse_int(getenv_fn("VGPU_PREEMPT_HOLD_MS"), 0, 10000, &hold)) cfg->preempt_hold_ms = (int)hold;

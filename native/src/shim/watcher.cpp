@@ -242,6 +242,7 @@ void board_tick(Region* r, Sampler& sm, uint64_t now) {
       return;
     }
     shim().board_slot.store(sm.board.self());  // on_exit takes the container off the board
+    sm.board.publish_cpu_node(cfg.cpu_node);
   }
   ShimState& s = shim();
   uint32_t ids[kMaxDevices];
@@ -413,7 +414,11 @@ void sample_tick(Region* r, Sampler& sm) {
       // Concurrency admission, round robin: while its credit allows, a container holds
       // the GPU for a slice, then yields to the longest-waiting peer; at most `conc`
       // containers of the GPU hold it at once. The containers take turns in small groups
-      // instead of all overlapping (the credit still caps each one's share).
+      // instead of all overlapping (the credit still caps each one's share). Three or more
+      // processes with launches in flight on one GPU each dispatch at a quarter of the rate
+      // two reach (profiles/r6f: a CP-side cross-process cost, not the CPU), and two on one
+      // CPU socket run no faster than one (profiles/r5d): with CPU nodes known the groups
+      // are cross-socket (Board::admit).
       const bool credit_ok = ds.gate_open.load(std::memory_order_relaxed);
       const int64_t slice = (int64_t)config().gpu_slice_ms * 1'000'000ll;
       bool hold = false;
@@ -422,14 +427,14 @@ void sample_tick(Region* r, Sampler& sm) {
         sm.want_since[d] = 0;
       } else if (sm.admitted[d]) {
         hold = true;
-        if ((int64_t)(now - sm.open_since[d]) >= slice && sm.board.waiting(a.gpu_id)) {
+        if ((int64_t)(now - sm.open_since[d]) >= slice && sm.board.waiting(a.gpu_id, config().cpu_node)) {
           sm.admitted[d] = false;  // slice used up and someone waits: to the back of the queue
           sm.want_since[d] = now;
           hold = false;
         }
       } else {
         if (!sm.want_since[d]) sm.want_since[d] = now;
-        if (sm.board.admit(a.gpu_id, conc, sm.want_since[d])) {
+        if (sm.board.admit(a.gpu_id, conc, sm.want_since[d], config().cpu_node)) {
           sm.admitted[d] = true;
           sm.open_since[d] = now;
           sm.want_since[d] = 0;

@@ -990,6 +990,38 @@ static void test_board() {
     b2.publish(kPrioBackground, gpus_b, 1, {5151}, now);
     CHECK_EQ(a.refresh(now).size(), 1u);
   }
+  // Concurrency admission across CPU sockets (k = 2, nodes published): a holder on node 0,
+  // a waiter of node 0 that came first and one of node 1 - the node-1 one is admitted next to
+  // the holder, the node-0 one waits for the holder's turn to end.
+  {
+    Board h, w0, w1;
+    CHECK_EQ(h.open(dir, "h.slot"), 0);
+    CHECK_EQ(w0.open(dir, "w0.slot"), 0);
+    CHECK_EQ(w1.open(dir, "w1.slot"), 0);
+    const uint32_t g[1] = {7000};
+    for (Board* x : {&h, &w0, &w1}) x->publish(kPrioNormal, g, 1, {}, now);
+    h.publish_cpu_node(0);
+    w0.publish_cpu_node(0);
+    w1.publish_cpu_node(1);
+    h.publish_gate(0, true, 0);
+    w0.publish_gate(0, false, now - 2000);
+    w1.publish_gate(0, false, now - 1000);
+    w1.refresh(now);
+    w0.refresh(now);
+    h.refresh(now);
+    CHECK(w1.admit(7000, 2, now - 1000, 1));   // node 1 is free: the earlier node-0 waiter is not ahead
+    CHECK(!w0.admit(7000, 2, now - 2000, 0));  // node 0 holds its one place
+    CHECK(h.waiting(7000, 0));                 // the holder's turn stands in w0's way
+    CHECK(!w1.waiting(7000, 1));               // nobody of node 1 waits behind w1
+    // Without nodes (a container that does not publish one): plain first-come admission.
+    CHECK(!w1.admit(7000, 2, now - 1000, -1));  // w0 came first and one place is left
+    CHECK(w0.admit(7000, 2, now - 2000, -1));
+    // Every container on one node: the cap is k, as without nodes.
+    w1.publish_cpu_node(0);
+    w0.refresh(now);
+    CHECK(w0.admit(7000, 2, now - 2000, 0));
+    for (Board* x : {&h, &w0, &w1}) x->leave();
+  }
   // A stale heartbeat (the container is gone) or a departed slot is ignored.
   CHECK_EQ(a.refresh(now + kBoardStaleNs + 1).size(), 0u);
   b.leave();

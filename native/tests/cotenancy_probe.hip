@@ -226,6 +226,22 @@ Result tenant(double start, double seconds, double spin_us, int grid, Wait w, in
   return r;
 }
 
+// A tenant that sets up exactly like an active one (HIP, its stream's hardware queue, the
+// warm-up kernels) and then sleeps through the window: does a process whose queues are mapped
+// but idle slow the active ones?
+void idle_tenant(double start, double seconds, int grid, int cpu) {
+  pin_to(cpu);
+  hipStream_t s;
+  uint64_t* out = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
+  if (hipMalloc(&out, sizeof(uint64_t) * 2 * kRing) != hipSuccess) return;
+  for (int i = 0; i < 64; i++) spin_kernel<<<grid, 64, 0, s>>>(1000, out, i % kRing);
+  (void)hipStreamSynchronize(s);
+  while (realtime_s() < start + seconds + 0.5) usleep(10000);
+  (void)hipFree(out);
+  (void)hipStreamDestroy(s);
+}
+
 void print_result(FILE* f, const Result& r) {
   fprintf(f, "{\"ok\": %s, \"kernels\": %ld, \"kps\": %.1f, \"p50_us\": %.2f, \"p90_us\": %.2f, \"max_us\": %.2f, "
              "\"launch_us\": %.3f, \"wait_us\": %.2f, \"cpu\": %d, \"node\": %d}",
@@ -249,7 +265,7 @@ std::string module_param(const char* name) {
 
 int main(int argc, char** argv) {
   if (argc < 4) {
-    fprintf(stderr, "usage: %s procs|streams N SECONDS [SPIN_US] [GRID] [spin|block|poll] [none|same|split|gpu]\n",
+    fprintf(stderr, "usage: %s procs|streams N SECONDS [SPIN_US] [GRID] [spin|block|poll] [none|same|split|gpu] [IDLE]\n",
             argv[0]);
     return 2;
   }
@@ -265,8 +281,9 @@ int main(int argc, char** argv) {
     fprintf(stderr, "unknown wait %s\n", wait_s.c_str());
     return 2;
   }
-  std::vector<int> cpus(n);
-  for (int i = 0; i < n; i++) cpus[i] = pin_cpu(pin, i);
+  const int idle = argc > 8 ? std::max(0, std::min(32, atoi(argv[8]))) : 0;  // procs mode: idle co-tenants
+  std::vector<int> cpus(n + idle);
+  for (int i = 0; i < n + idle; i++) cpus[i] = pin_cpu(pin, i);
   const double start = realtime_s() + 3.0 + 0.1 * n;  // every tenant warmed up by then
   std::vector<Result> res(n);
   if (mode == "procs") {
@@ -286,11 +303,24 @@ int main(int argc, char** argv) {
       fds[i] = p[0];
       kids[i] = c;
     }
+    std::vector<pid_t> idlers;
+    for (int i = 0; i < idle; i++) {
+      pid_t c = fork();
+      if (c == 0) {
+        idle_tenant(start, seconds, grid, cpus[n + i]);
+        _exit(0);
+      }
+      if (c > 0) idlers.push_back(c);
+    }
     for (int i = 0; i < n; i++) {
       if (read(fds[i], &res[i], sizeof(Result)) != (ssize_t)sizeof(Result)) res[i] = Result();
       close(fds[i]);
       int st = 0;
       waitpid(kids[i], &st, 0);
+    }
+    for (pid_t c : idlers) {
+      int st = 0;
+      waitpid(c, &st, 0);
     }
   } else if (mode == "streams") {
     std::vector<std::thread> th;
@@ -302,11 +332,11 @@ int main(int argc, char** argv) {
   }
   double agg = 0;
   for (const Result& r : res) agg += r.kps;
-  printf("{\"mode\": \"%s\", \"tenants\": %d, \"wait\": \"%s\", \"pin\": \"%s\", \"seconds\": %.1f, \"spin_us\": %.1f, "
+  printf("{\"mode\": \"%s\", \"tenants\": %d, \"idle\": %d, \"wait\": \"%s\", \"pin\": \"%s\", \"seconds\": %.1f, \"spin_us\": %.1f, "
          "\"grid\": %d, \"aggregate_kps\": %.1f, "
          "\"amdgpu\": {\"hws_max_conc_proc\": %s, \"sched_policy\": %s, \"cwsr_enable\": %s, \"mes\": %s, "
          "\"sched_hw_submission\": %s}, \"per_tenant\": [",
-         mode.c_str(), n, wait_s.c_str(), pin.c_str(), seconds, spin_us, grid, agg, module_param("hws_max_conc_proc").c_str(),
+         mode.c_str(), n, mode == "procs" ? idle : 0, wait_s.c_str(), pin.c_str(), seconds, spin_us, grid, agg, module_param("hws_max_conc_proc").c_str(),
          module_param("sched_policy").c_str(), module_param("cwsr_enable").c_str(), module_param("mes").c_str(),
          module_param("sched_hw_submission").c_str());
   for (int i = 0; i < n; i++) {

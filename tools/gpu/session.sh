@@ -55,8 +55,10 @@ if has oversub; then
 fi
 if has prof; then
   step prof
-  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- \
-    python3 bench.py --steps 10 --warmup 3 --modes vgpu > $OUT/prof.log 2>&1
-  rc=$?; tail -3 $OUT/prof.log; [ $rc -eq 0 ] || exit $rc
+  # rocprofv3 --kernel-trace --marker-trace --stats of the headline tenant: native, quota-only
+  # vGPU, 25 % temporal vGPU (tools/probe/prof_tenant.py: each mode a child under its own
+  # rocprofv3, the program after --; summary.md + per-mode kernel stats)
+  timeout -k 10 700 python -u tools/probe/prof_tenant.py --out $OUT/prof --steps 30 > $OUT/prof.log 2>&1
+  rc=$?; head -12 $OUT/prof/summary.md 2>/dev/null; [ $rc -eq 0 ] || exit $rc
 fi
 echo "== done $(date +%T)"
