@@ -179,10 +179,12 @@ def test_blocking_wait_polls_instead_of_spinning(fake, mode, cpu_bound):
     assert long["value"] == 0 and short["value"] == 0 and spin["value"] == 0
     assert 199 <= long["waitsig"] and 199 <= spin["waitspin"], (long, spin)
     if cpu_bound is not None:
-        assert long["waitsig"] <= 200 * 1.15 + 1.5 and short["waitsig"] <= 5 * 1.15 + 1.5, (long, short)
+        # + 4 ms: the fake completes its signal from a thread, and on a loaded host (the suite
+        # under xdist) either side can be scheduled a few ms late
+        assert long["waitsig"] <= 200 * 1.15 + 4 and short["waitsig"] <= 5 * 1.15 + 4, (long, short)
         assert long["cpu_ms"] <= cpu_bound * long["waitsig"], long
         # HIP's spin-until-done wait (an active wait with no time-out) polls the same way
-        assert spin["waitspin"] <= 200 * 1.15 + 1.5 and spin["cpu_ms"] <= cpu_bound * spin["waitspin"], spin
+        assert spin["waitspin"] <= 200 * 1.15 + 4 and spin["cpu_ms"] <= cpu_bound * spin["waitspin"], spin
     else:
         assert long["cpu_ms"] >= 0.4 * long["waitsig"], long   # the runtime's spin (the fake spins too)
         assert spin["cpu_ms"] >= 0.4 * spin["waitspin"], spin
