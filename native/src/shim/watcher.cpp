@@ -423,6 +423,7 @@ void sample_tick(Region* r, Sampler& sm) {
       const int64_t slice = (int64_t)config().gpu_slice_ms * 1'000'000ll;
       bool hold = false;
       if (!credit_ok) {
+        if (sm.admitted[d] || sm.want_since[d]) VLOG_DEBUG("device %d: no credit, out of the turns", d);
         sm.admitted[d] = false;
         sm.want_since[d] = 0;
       } else if (sm.admitted[d]) {
@@ -431,10 +432,14 @@ void sample_tick(Region* r, Sampler& sm) {
           sm.admitted[d] = false;  // slice used up and someone waits: to the back of the queue
           sm.want_since[d] = now;
           hold = false;
+          VLOG_DEBUG("device %d: turn over after %.1f ms (CPU node %d)", d, (now - sm.open_since[d]) / 1e6,
+                     config().cpu_node);
         }
       } else {
         if (!sm.want_since[d]) sm.want_since[d] = now;
         if (sm.board.admit(a.gpu_id, conc, sm.want_since[d], config().cpu_node)) {
+          VLOG_DEBUG("device %d: admitted after %.1f ms of waiting (CPU node %d)", d,
+                     (now - sm.want_since[d]) / 1e6, config().cpu_node);
           sm.admitted[d] = true;
           sm.open_since[d] = now;
           sm.want_since[d] = 0;
