@@ -124,9 +124,11 @@ class Board {
   // two launch-bound processes on one socket run no faster together than one alone
   // (profiles/r5d), so k = 2 takes turns in cross-socket pairs. Peers as of the last refresh().
   bool admit(uint32_t gpu_id, int k, uint64_t want_since, int node = -1) const;
-  // Whether a peer on GPU `gpu_id` waits for admission that this container's turn stands in
-  // the way of: any waiting peer, or with CPU nodes known only one of its own node.
-  bool waiting(uint32_t gpu_id, int node = -1) const;
+  // Whether a peer on GPU `gpu_id` waits for admission that this container's turn (k places,
+  // this container on CPU node `node`) stands in the way of: any waiting peer when nodes are
+  // unknown; with nodes, one of its own node, any when this node holds more than its share of
+  // the places, or one whose node has room when all k places are taken.
+  bool waiting(uint32_t gpu_id, int k = 0, int node = -1) const;
 
   // Re-reads the other slots (live ones only). Cheap enough for every 100 ms.
   const std::vector<BoardPeer>& refresh(uint64_t now);

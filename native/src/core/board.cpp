@@ -177,13 +177,31 @@ NodeLoad node_load(const std::vector<BoardPeer>& peers, uint32_t gpu_id, int k, 
 
 }  // namespace
 
-bool Board::waiting(uint32_t gpu_id, int node) const {
+bool Board::waiting(uint32_t gpu_id, int k, int node) const {
+  // This container holds a turn on `gpu_id` (CPU node `node`). A waiter is in its way when
+  // nodes are unknown (plain round robin), when it is of the same node, when this node holds
+  // more than its cap (peers' nodes were not known yet when it was admitted), or when all k
+  // places are taken and the waiter's node has room.
+  const NodeLoad load = node_load(peers_, gpu_id, k, node);
+  int open = 1;  // this container
+  bool any = false, blocked_by_total = false, same = false;
   for (const BoardPeer& p : peers_)
-    for (size_t i = 0; i < p.gpu_ids.size() && i < p.want_since.size(); i++)
-      if (p.gpu_ids[i] == gpu_id && p.want_since[i] && !p.gate[i] &&
-          (node < 0 || p.cpu_node < 0 || p.cpu_node == node))
-        return true;
-  return false;
+    for (size_t i = 0; i < p.gpu_ids.size() && i < p.want_since.size() && i < p.gate.size(); i++) {
+      if (p.gpu_ids[i] != gpu_id) continue;
+      if (p.gate[i]) {
+        open++;
+        continue;
+      }
+      if (!p.want_since[i]) continue;
+      any = true;
+      if (node < 0 || p.cpu_node < 0 || load.nodes.size() <= 1 || p.cpu_node == node) same = true;
+      else if (load.room(p.cpu_node)) blocked_by_total = true;
+    }
+  if (!any) return false;
+  if (same) return true;
+  auto it = load.held.find(node);
+  const int mine = 1 + (it == load.held.end() ? 0 : it->second);
+  return mine > load.cap || (blocked_by_total && open >= k);
 }
 
 bool Board::admit(uint32_t gpu_id, int k, uint64_t want_since, int node) const {

@@ -428,7 +428,7 @@ void sample_tick(Region* r, Sampler& sm) {
         sm.want_since[d] = 0;
       } else if (sm.admitted[d]) {
         hold = true;
-        if ((int64_t)(now - sm.open_since[d]) >= slice && sm.board.waiting(a.gpu_id, config().cpu_node)) {
+        if ((int64_t)(now - sm.open_since[d]) >= slice && sm.board.waiting(a.gpu_id, conc, config().cpu_node)) {
           sm.admitted[d] = false;  // slice used up and someone waits: to the back of the queue
           sm.want_since[d] = now;
           hold = false;

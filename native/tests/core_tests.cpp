@@ -1011,8 +1011,29 @@ static void test_board() {
     h.refresh(now);
     CHECK(w1.admit(7000, 2, now - 1000, 1));   // node 1 is free: the earlier node-0 waiter is not ahead
     CHECK(!w0.admit(7000, 2, now - 2000, 0));  // node 0 holds its one place
-    CHECK(h.waiting(7000, 0));                 // the holder's turn stands in w0's way
-    CHECK(!w1.waiting(7000, 1));               // nobody of node 1 waits behind w1
+    CHECK(h.waiting(7000, 2, 0));              // the holder's turn stands in w0's way
+    CHECK(!w1.waiting(7000, 2, 1));            // nobody of node 1 waits behind w1
+    // Two holders of node 0 (admitted before the nodes were known) and a node-1 waiter: all
+    // places are taken and node 0 is over its share, so its holders yield after their turn.
+    {
+      Board h2;
+      CHECK_EQ(h2.open(dir, "h2.slot"), 0);
+      h2.publish(kPrioNormal, g, 1, {}, now);
+      h2.publish_cpu_node(0);
+      h2.publish_gate(0, true, 0);
+      w0.publish_gate(0, false, 0);  // w0 not waiting now
+      h.refresh(now);
+      CHECK(h.waiting(7000, 2, 0));   // over node 0's share, and w1 (node 1, room) is blocked by the total
+      w1.publish_gate(0, false, 0);   // nobody waits: nobody yields
+      h.refresh(now);
+      CHECK(!h.waiting(7000, 2, 0));
+      h2.leave();
+      w0.publish_gate(0, false, now - 2000);
+      w1.publish_gate(0, false, now - 1000);
+      w0.refresh(now);
+      w1.refresh(now);
+      h.refresh(now);
+    }
     // Without nodes (a container that does not publish one): plain first-come admission.
     CHECK(!w1.admit(7000, 2, now - 1000, -1));  // w0 came first and one place is left
     CHECK(w0.admit(7000, 2, now - 2000, -1));

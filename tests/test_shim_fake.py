@@ -968,3 +968,26 @@ def test_blocked_launch_released_when_the_gpu_calms_down(fake, tmp_path):
             n.wait(timeout=60)
     frac = [o for o in out if "run" in o][0]["busy_frac"]
     assert frac > 0.3, frac  # crowded (25 %), then its own CUs again (~100 %)
+
+
+def test_pair_turns_span_cpu_sockets_without_starving(fake, tmp_path):
+    """VGPU_GPU_CONCURRENCY=2 with CPU nodes (--numa-spread): the GPU is held in cross-socket
+    pairs. The two node-0 containers start first and both take a place before the node-1 ones
+    have published their nodes (what happened on MI355X, profiles/r6k): node 0 is then over its
+    share, so its holders yield after their turn, and every container runs ~half the time."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+
+    def env(i, node):
+        return _board_env(fake, tmp_path, f"t{i}", VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="temporal",
+                          VGPU_GPU_CONCURRENCY="2", VGPU_CPU_NODE=str(node))
+    first = [sp.Popen([HARNESS, "stream", "run=1000,5"], env=env(i, 0), stdout=sp.PIPE, text=True) for i in (1, 3)]
+    time.sleep(0.5)
+    later = [sp.Popen([HARNESS, "stream", "run=1000,4.5"], env=env(i, 1), stdout=sp.PIPE, text=True) for i in (0, 2)]
+    fracs = []
+    for p in first + later:
+        out, _ = p.communicate(timeout=120)
+        assert p.returncode == 0
+        fracs.append([json.loads(l) for l in out.splitlines() if '"run"' in l][0]["busy_frac"])
+    assert min(fracs) >= 0.3, fracs      # nobody starved (before the fix: the node-1 pair ~0)
+    assert sum(fracs) <= 2.4, fracs      # and at most ~two hold at once
