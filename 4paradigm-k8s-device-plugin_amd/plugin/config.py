@@ -62,7 +62,7 @@ class PluginConfig:
     allow_latency_class: bool = False       # every container may take VGPU_TASK_PRIORITY=0
     latency_vgpus_per_gpu: int = 0          # vGPUs per GPU advertised as <resource>-latency (latency class granted)
     host_budget_bytes: int = -1             # resolved per-vGPU host budget (plugin/host_memory.py; -1 = not yet)
-    gpu_concurrency: int = 0                # limited containers holding a GPU's time at once (0 = any)
+    gpu_concurrency: int = 0                # limited containers holding a GPU's time at once (0 = any, -1 = auto)
     ledger: bool = True                     # run the node's GPU-time ledger daemon (vgpu-ledger; profiles/r4o)
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"  # kubelet PodResources v1
     active_oom_killer: bool = True          # the containers' memory backstop (limits file; reference ACTIVE_OOM_KILLER)
@@ -95,7 +95,7 @@ class PluginConfig:
             raise ValueError(f"invalid --duplicate-vgpus option: {self.duplicate_vgpus}")
         if self.numa_spread not in NUMA_SPREAD_MODES:
             raise ValueError(f"invalid --numa-spread option: {self.numa_spread}")
-        if not 0 <= self.gpu_concurrency <= 64:
+        if not -1 <= self.gpu_concurrency <= 64:
             raise ValueError(f"invalid --gpu-concurrency option: {self.gpu_concurrency}")
         from ..utils.sizes import parse_size
         if self.host_memory_per_vgpu != "auto":
@@ -125,6 +125,11 @@ class PluginConfig:
 
 
 # (flag, dest, type, env vars, help)
+def concurrency_value(v):
+    """--gpu-concurrency: an int (0..64) or "auto" (-1)."""
+    return -1 if str(v).strip().lower() == "auto" else int(v)
+
+
 _FLAGS = [
     ("--partition-strategy", "partition_strategy", str, ["PARTITION_STRATEGY", "MIG_STRATEGY"],
      "compute/memory partition strategy: none | single | mixed"),
@@ -181,9 +186,11 @@ _FLAGS = [
     ("--latency-vgpus-per-gpu", "latency_vgpus_per_gpu", int, ["LATENCY_VGPUS_PER_GPU"],
      "of each GPU's split vGPUs, this many are advertised as <resource>-latency (e.g. amd.com/gpu-latency), which "
      "grants the latency class; an operator bounds it per namespace with a ResourceQuota (default 0)"),
-    ("--gpu-concurrency", "gpu_concurrency", int, ["GPU_CONCURRENCY"],
-     "containers on the GPU-time limiter that may hold a GPU at once, taking turns over the node-wide board "
-     "(0 = no admission: every container whose credit allows runs)"),
+    ("--gpu-concurrency", "gpu_concurrency", concurrency_value, ["GPU_CONCURRENCY"],
+     "containers on the GPU-time limiter that may hold a GPU at once, taking turns over the node-wide board, in "
+     "pairs of different CPU sockets when --numa-spread places them (0 = no admission: every container whose credit "
+     "allows runs; auto = pairs while the GPU's containers launch more than VGPU_PAIRS_ON_RATE (40k) kernels/s "
+     "together - dispatch-bound pods, which three at once slow down - and everybody at once otherwise)"),
     ("--ledger", "ledger", "bool", ["VGPU_NODE_LEDGER"],
      "run the node GPU-time ledger (vgpu-ledger): one KFD occupancy sampler for every limited container of the "
      "node instead of one per container (n reads per period instead of n^2, one consistent snapshot), and "
@@ -239,7 +246,7 @@ def parse_config(argv=None, environ=None):
             continue
         if typ == "bool":
             val = _env_bool(val, getattr(cfg, dest))
-        elif typ in (int, float):
+        elif typ in (int, float, concurrency_value):
             val = typ(val)
         setattr(cfg, dest, val)
     cfg.disable_healthchecks = environ.get("DP_DISABLE_HEALTHCHECKS", "")

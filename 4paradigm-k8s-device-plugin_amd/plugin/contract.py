@@ -516,7 +516,7 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         resp.envs["VGPU_BOARD_DIR"] = CONTAINER_BOARD_DIR
         resp.envs["VGPU_BOARD_SLOT"] = os.path.basename(slot)
         if getattr(cfg, "gpu_concurrency", 0):
-            resp.envs["VGPU_GPU_CONCURRENCY"] = str(cfg.gpu_concurrency)
+            resp.envs["VGPU_GPU_CONCURRENCY"] = "auto" if cfg.gpu_concurrency < 0 else str(cfg.gpu_concurrency)
     lock_file = os.path.join(vdir, LOCK_HOST_DIR, LOCK_FILE)
     if os.path.isfile(lock_file):
         resp.mounts.add(container_path=f"{CONTAINER_LOCK_DIR}/{LOCK_FILE}", host_path=lock_file, read_only=True)

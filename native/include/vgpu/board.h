@@ -56,6 +56,7 @@ struct alignas(64) BoardSlot {
   // one (0 = unknown, as an older slot reads): the concurrency admission pairs containers of
   // different CPU sockets.
   std::atomic<int32_t> cpu_node1;
+  std::atomic<uint32_t> launch_rate;  // the container's kernel launches per second (EWMA)
 };
 constexpr size_t kBoardSlotV1Size = offsetof(BoardSlot, svm_vram);
 
@@ -81,7 +82,12 @@ struct BoardPeer {
   std::vector<uint64_t> hbm_want;            // per device (0 = none, or stale)
   std::vector<uint64_t> hbm_want_ns;         // per device: when it was (re-)published
   int cpu_node = -1;                         // VGPU_CPU_NODE (-1 = unknown)
+  uint32_t launch_rate = 0;                  // kernel launches per second
 };
+
+// Automatic pair turns (VGPU_GPU_CONCURRENCY=auto): below VGPU_PAIRS_OFF_RATE launches/s of
+// all the containers of a GPU for this long, they stop taking turns.
+constexpr uint64_t kPairsOffNs = 2'000'000'000ull;
 
 // A container's view of the board directory: its own slot (read-write) and the others.
 class Board {
@@ -108,6 +114,10 @@ class Board {
   void publish_gate(int dev, bool open, uint64_t want_since);
   // The CPU node the container's processes run on (-1 = none / unknown).
   void publish_cpu_node(int node);
+  // The container's kernel launches per second.
+  void publish_launch_rate(uint32_t per_s);
+  // Sum of the live peers' launch rates on GPU `gpu_id`.
+  uint64_t peers_launch_rate(uint32_t gpu_id) const;
   // Virtual device memory of device `dev`: the container's SVM bytes in VRAM, and HBM it was
   // refused within its share (0 = none) since `want_ns`.
   void publish_memory(int dev, uint64_t svm_vram, uint64_t hbm_want, uint64_t want_ns);

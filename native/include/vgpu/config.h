@@ -127,7 +127,15 @@ struct Config {
   std::string board_dir;                 // VGPU_BOARD_DIR: node-wide board (vgpu/board.h), "" = none
   std::string board_slot;                // VGPU_BOARD_SLOT: this container's slot file in it
   int gpu_concurrency = 0;               // VGPU_GPU_CONCURRENCY: limited containers whose GPU-time
-                                         // gates may be open together on one GPU (0 = any number)
+                                         // gates may be open together on one GPU (0 = any number;
+                                         // -1 = "auto": 2 while the GPU's containers launch more than
+                                         // pairs_on_rate kernels/s together, else any number)
+  // VGPU_PAIRS_ON_RATE / VGPU_PAIRS_OFF_RATE: the "auto" thresholds. Three or more processes with
+  // launches in flight each dispatch at about a quarter of the rate two reach (profiles/r6f): a
+  // dispatch-bound crowd (4 LSTM pods: ~110k launches/s) gains from pairs, a compute-bound one
+  // (16 ResNet-50 b=50 pods: ~16k/s) loses (profiles/r6k).
+  uint32_t pairs_on_rate = 40000;
+  uint32_t pairs_off_rate = 20000;
   int gpu_slice_ms = 20;                 // VGPU_GPU_SLICE_MS: turn length under that admission
   int cpu_node = -1;                     // VGPU_CPU_NODE (unless VGPU_CPU_SPREAD=0): the CPU node the
                                          // container's processes run on, published on the board

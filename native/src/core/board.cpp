@@ -117,6 +117,17 @@ void Board::publish_cpu_node(int node) {
   if (self_) self_->cpu_node1.store(node >= 0 ? node + 1 : 0, std::memory_order_relaxed);
 }
 
+void Board::publish_launch_rate(uint32_t per_s) {
+  if (self_) self_->launch_rate.store(per_s, std::memory_order_relaxed);
+}
+
+uint64_t Board::peers_launch_rate(uint32_t gpu_id) const {
+  uint64_t n = 0;
+  for (const BoardPeer& p : peers_)
+    if (std::find(p.gpu_ids.begin(), p.gpu_ids.end(), gpu_id) != p.gpu_ids.end()) n += p.launch_rate;
+  return n;
+}
+
 void Board::publish_memory(int dev, uint64_t svm_vram, uint64_t hbm_want, uint64_t want_ns) {
   if (!self_ || dev < 0 || dev >= kMaxDevices) return;
   self_->svm_vram[dev].store(svm_vram, std::memory_order_relaxed);
@@ -261,6 +272,7 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
     }
     const int32_t cn = got >= (ssize_t)sizeof(BoardSlot) ? s.cpu_node1.load(std::memory_order_relaxed) : 0;
     p.cpu_node = cn > 0 && cn <= 64 ? cn - 1 : -1;
+    if (got >= (ssize_t)sizeof(BoardSlot)) p.launch_rate = std::min<uint32_t>(s.launch_rate.load(std::memory_order_relaxed), 10'000'000u);
     const int n = std::max(0, std::min(s.npids.load(std::memory_order_relaxed), kBoardMaxPids));
     for (int i = 0; i < n; i++) {
       const int pid = s.hostpids[i].load(std::memory_order_relaxed);

@@ -337,7 +337,12 @@ void load_config(Config* cfg, GetenvFn raw_getenv) {
   }
   if (const char* s = getenv_fn("VGPU_BOARD_DIR")) cfg->board_dir = s;
   long conc = 0;
-  if (parse_int(getenv_fn("VGPU_GPU_CONCURRENCY"), 0, 64, &conc)) cfg->gpu_concurrency = (int)conc;
+  if (const char* c = getenv_fn("VGPU_GPU_CONCURRENCY"); c && !strcasecmp(c, "auto")) cfg->gpu_concurrency = -1;
+  else if (parse_int(c, 0, 64, &conc)) cfg->gpu_concurrency = (int)conc;
+  long pr = 0;
+  if (parse_int(getenv_fn("VGPU_PAIRS_ON_RATE"), 1, 100000000, &pr)) cfg->pairs_on_rate = (uint32_t)pr;
+  if (parse_int(getenv_fn("VGPU_PAIRS_OFF_RATE"), 0, 100000000, &pr)) cfg->pairs_off_rate = (uint32_t)pr;
+  if (cfg->pairs_off_rate > cfg->pairs_on_rate) cfg->pairs_off_rate = cfg->pairs_on_rate;
   long slice = 20;
   if (parse_int(getenv_fn("VGPU_GPU_SLICE_MS"), 1, 10000, &slice)) cfg->gpu_slice_ms = (int)slice;
   if (const char* s = getenv_fn("VGPU_BOARD_SLOT")) cfg->board_slot = s;
@@ -435,7 +440,7 @@ void apply_ceiling(Config* cfg, const Config& ceil) {
   // could carry a forged ledger with no charges.
   if (!ceil.board_dir.empty()) cfg->board_dir = ceil.board_dir;
   if (!ceil.board_slot.empty()) cfg->board_slot = ceil.board_slot;
-  if (ceil.gpu_concurrency > 0) cfg->gpu_concurrency = ceil.gpu_concurrency;  // the node's admission
+  if (ceil.gpu_concurrency != 0) cfg->gpu_concurrency = ceil.gpu_concurrency;  // the node's admission
   cfg->cu_mode = ceil.cu_mode;
   cfg->oversubscribe = cfg->oversubscribe && ceil.oversubscribe;
   // The memory backstop is the plugin's (on unless its limits file turns it off).

@@ -136,7 +136,57 @@ struct Sampler {
   uint64_t others_busy_ns[kMaxDevices] = {};  // last sample at which another process had waves resident
   uint64_t mem_refresh_ns = 0;                // next read of the peers' memory (memory_board_tick)
   uint64_t want_seen_ns[kMaxDevices] = {};    // the peers' HBM request already served
+  // Automatic pair turns (VGPU_GPU_CONCURRENCY=auto): the container's launch rate and, per
+  // GPU, whether its containers take turns in pairs now.
+  uint64_t rate_launches = 0, rate_at_ns = 0;
+  double launch_rate = 0;                     // kernel launches per second (EWMA)
+  bool pairs_on[kMaxDevices] = {};
+  uint64_t pairs_low_since[kMaxDevices] = {};
 };
+
+// The concurrency admission's k on device `d` (0 = everybody at once).
+int concurrency_on(const Sampler& sm, int d) {
+  const int k = sm.board.attached() ? config().gpu_concurrency : 0;
+  return k >= 0 ? k : (sm.pairs_on[d] ? 2 : 0);
+}
+
+// VGPU_GPU_CONCURRENCY=auto (lease holder, every period): the container's launch rate from
+// its processes' launch counters, published on the board; per GPU, pairs switch on while the
+// GPU's containers together launch more than VGPU_PAIRS_ON_RATE kernels/s and off after
+// kPairsOffNs below VGPU_PAIRS_OFF_RATE (the rates of a waiting container fall, those of the holders do not).
+void pairs_tick(Region* r, Sampler& sm, const uint32_t* ids, uint64_t now) {
+  ShimState& s = shim();
+  uint64_t total = 0;
+  for (int i = 0; i < kMaxProcs; i++)
+    if (r->procs[i].pid.load(std::memory_order_relaxed)) total += r->procs[i].launches.load(std::memory_order_relaxed);
+  if (sm.rate_at_ns && now > sm.rate_at_ns) {
+    const double inst = total >= sm.rate_launches ? (double)(total - sm.rate_launches) * 1e9 / (now - sm.rate_at_ns) : 0;
+    sm.launch_rate = 0.5 * sm.launch_rate + 0.5 * inst;
+  }
+  sm.rate_launches = total;
+  sm.rate_at_ns = now;
+  sm.board.publish_launch_rate((uint32_t)std::min(sm.launch_rate, 1e7));
+  if (config().gpu_concurrency >= 0) return;
+  VLOG_DEBUG("container launch rate %.0f/s", sm.launch_rate);
+  sm.board.refresh(now);
+  for (int d = 0; d < s.n_agents; d++) {
+    const uint64_t rate = (uint64_t)sm.launch_rate + sm.board.peers_launch_rate(ids[d]);
+    if (rate >= config().pairs_on_rate) {
+      if (!sm.pairs_on[d]) VLOG_INFO("device %d: %lu launches/s on the GPU -> pair turns", d, (unsigned long)rate);
+      sm.pairs_on[d] = true;
+      sm.pairs_low_since[d] = 0;
+    } else if (sm.pairs_on[d] && rate < config().pairs_off_rate) {
+      if (!sm.pairs_low_since[d]) sm.pairs_low_since[d] = now;
+      if (now - sm.pairs_low_since[d] >= kPairsOffNs) {
+        VLOG_INFO("device %d: %lu launches/s on the GPU -> all at once", d, (unsigned long)rate);
+        sm.pairs_on[d] = false;
+        sm.pairs_low_since[d] = 0;
+      }
+    } else {
+      sm.pairs_low_since[d] = 0;
+    }
+  }
+}
 
 // The credit window of device `d`: the configured one, or the longer solo window while no
 // other process has kept the GPU busy for a second. Alone on the GPU nobody waits behind
@@ -256,6 +306,7 @@ void board_tick(Region* r, Sampler& sm, uint64_t now) {
   }
   sm.board.publish(region_priority(r), ids, s.n_agents, sm.mine, now, masks);
   memory_board_tick(r, sm, ids, now);
+  pairs_tick(r, sm, ids, now);
   // Background class: keep off the CU slices of latency-class tenants on the same GPU.
   // Stored in the region, so every process of the container re-masks its queues.
   if (region_priority(r) < kPrioBackground) return;
@@ -312,13 +363,14 @@ void sample_tick(Region* r, Sampler& sm) {
   sm.last_ns = now;
   collect_region_pids(r, sm);
   const bool refresh = now - sm.others_at_ns > 100'000'000ull;
-  const int conc = sm.board.attached() ? config().gpu_concurrency : 0;
+  bool any_conc = false;
+  for (int d = 0; d < s.n_agents; d++) any_conc |= concurrency_on(sm, d) > 0;
   if (refresh) {
     sm.others_at_ns = now;
     sm.procs = 1;
   }
   // Peers: every sample for the concurrency admission, every 100 ms for the classes.
-  if (conc > 0 || (refresh && sm.board.attached() && region_priority(r) >= kPrioBackground)) sm.board.refresh(now);
+  if (any_conc || (refresh && sm.board.attached() && region_priority(r) >= kPrioBackground)) sm.board.refresh(now);
   for (int d = 0; d < s.n_agents; d++) {
     AgentInfo& a = s.agents[d];
     if (!a.temporal_active.load(std::memory_order_relaxed) || !a.gpu_id) {
@@ -410,6 +462,12 @@ void sample_tick(Region* r, Sampler& sm) {
     // room for that (the plugin emits the percent rounded up for this reason).
     timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, window_ms(sm, d, now), led ? ds.cu_share_bp : 0), dt,
                     charge, yield ? 0 : dt);
+    const int conc = concurrency_on(sm, d);
+    if (conc <= 0 && (sm.admitted[d] || sm.want_since[d])) {  // pairs switched off: out of the turns
+      sm.admitted[d] = false;
+      sm.want_since[d] = 0;
+      sm.board.publish_gate(d, false, 0);
+    }
     if (conc > 0) {
       // Concurrency admission, round robin: while its credit allows, a container holds
       // the GPU for a slice, then yields to the longest-waiting peer; at most `conc`

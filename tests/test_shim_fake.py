@@ -991,3 +991,34 @@ def test_pair_turns_span_cpu_sockets_without_starving(fake, tmp_path):
         fracs.append([json.loads(l) for l in out.splitlines() if '"run"' in l][0]["busy_frac"])
     assert min(fracs) >= 0.3, fracs      # nobody starved (before the fix: the node-1 pair ~0)
     assert sum(fracs) <= 2.4, fracs      # and at most ~two hold at once
+
+
+@pytest.mark.parametrize("kernel_us,pairs", [(20, True), (1000, False)])
+def test_auto_pair_turns_follow_the_launch_rate(fake, tmp_path, kernel_us, pairs):
+    """VGPU_GPU_CONCURRENCY=auto: four containers of one GPU take turns in pairs while they
+    launch more than VGPU_PAIRS_ON_RATE kernels/s together (dispatch-bound: tiny kernels;
+    default 40k/s, scaled down here to the fake GPU's rates), and all run at once
+    when they launch few long kernels (compute-bound) - the two cases pair turns help and hurt
+    on MI355X (profiles/r6k)."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+    envs = [_board_env(fake, tmp_path, f"t{i}", VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="temporal",
+                       VGPU_GPU_CONCURRENCY="auto", VGPU_CPU_NODE=str(i % 2), VGPU_LOG_LEVEL="2",
+                       # the fake GPU launches ~3k kernels/s per container: thresholds to scale
+                       VGPU_PAIRS_ON_RATE="4000", VGPU_PAIRS_OFF_RATE="2000")
+            for i in range(4)]
+    ps = [sp.Popen([HARNESS, "stream", "sleep=0.5", f"run={kernel_us},4"], env=e, stdout=sp.PIPE,
+                   stderr=sp.PIPE, text=True) for e in envs]
+    fracs, logs = [], ""
+    for p in ps:
+        out, err = p.communicate(timeout=120)
+        assert p.returncode == 0, err[-2000:]
+        logs += err
+        fracs.append([json.loads(l) for l in out.splitlines() if '"run"' in l][0]["busy_frac"])
+    if pairs:
+        assert "-> pair turns" in logs, logs[-3000:]
+        assert min(fracs) >= 0.2, fracs
+        assert sum(fracs) <= 2.6, fracs
+    else:
+        assert "-> pair turns" not in logs
+        assert sum(fracs) > 2.6, fracs
