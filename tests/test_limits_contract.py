@@ -145,3 +145,17 @@ def test_limits_file_carries_the_board_and_admission(tmp_path):
     for k in ("VGPU_BOARD_DIR", "VGPU_BOARD_SLOT", "VGPU_GPU_CONCURRENCY", "VGPU_DEVICE_CU_SHARE_0"):
         assert lim.get(k) == envs[k], (k, lim.get(k), envs.get(k))
 
+
+
+def test_gpu_concurrency_auto_reaches_the_container(tmp_path):
+    """--gpu-concurrency=auto: the contract (env and limits file) says "auto", which the shim
+    reads as pair turns while the GPU's containers launch more than VGPU_PAIRS_ON_RATE
+    kernels/s together (tests/test_shim_fake.py::test_auto_pair_turns_follow_the_launch_rate)."""
+    from amdvgpu.plugin.config import parse_config
+    assert parse_config(["--gpu-concurrency", "auto"]).gpu_concurrency == -1
+    assert parse_config([], {"GPU_CONCURRENCY": "auto"}).gpu_concurrency == -1
+    with NodeHarness(FakeBackend(n=1), device_split_count=4, gpu_concurrency=-1,
+                     workdir=str(tmp_path / "node")) as node:
+        envs, mounts = node.pod(node.vgpu_ids(FakeBackend(n=1).devices()[0].uuid)[:1])
+        lim = dict(l.split("=", 1) for l in open(dict(mounts)["/vgpu/limits"]).read().splitlines())
+    assert envs["VGPU_GPU_CONCURRENCY"] == "auto" and lim["VGPU_GPU_CONCURRENCY"] == "auto"
