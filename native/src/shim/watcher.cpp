@@ -142,12 +142,29 @@ struct Sampler {
   double launch_rate = 0;                     // kernel launches per second (EWMA)
   bool pairs_on[kMaxDevices] = {};
   uint64_t pairs_low_since[kMaxDevices] = {};
+  // Steadiness (auto): of the samples at which the container was free to launch, the share
+  // with new launches since the previous one. A batch pod launches at every sample; a
+  // request-serving pod idles between requests and is kept out of the turns (profiles/r6a).
+  uint64_t act_launches = 0;
+  uint32_t act_ticks = 0, act_busy = 0;
+  double activity = 1.0;
+  bool steady = true;
 };
 
 // The concurrency admission's k on device `d` (0 = everybody at once).
 int concurrency_on(const Sampler& sm, int d) {
   const int k = sm.board.attached() ? config().gpu_concurrency : 0;
-  return k >= 0 ? k : (sm.pairs_on[d] ? 2 : 0);
+  return k >= 0 ? k : (sm.pairs_on[d] && sm.steady ? 2 : 0);
+}
+
+// The container's launches so far: this process's live counter, the others' as published.
+uint64_t container_launches(const Region* r) {
+  ShimState& s = shim();
+  uint64_t total = s.launches.load(std::memory_order_relaxed);
+  for (int i = 0; i < kMaxProcs; i++)
+    if (i != s.slot && r->procs[i].pid.load(std::memory_order_relaxed))
+      total += r->procs[i].launches.load(std::memory_order_relaxed);
+  return total;
 }
 
 // VGPU_GPU_CONCURRENCY=auto (lease holder, every period): the container's launch rate from
@@ -167,6 +184,15 @@ void pairs_tick(Region* r, Sampler& sm, const uint32_t* ids, uint64_t now) {
   sm.rate_at_ns = now;
   sm.board.publish_launch_rate((uint32_t)std::min(sm.launch_rate, 1e7));
   if (config().gpu_concurrency >= 0) return;
+  if (sm.act_ticks >= 20) {
+    sm.activity = 0.6 * sm.activity + 0.4 * ((double)sm.act_busy / sm.act_ticks);
+    sm.act_ticks = sm.act_busy = 0;
+    const bool steady = sm.steady ? sm.activity >= 0.6 : sm.activity >= 0.8;
+    if (steady != sm.steady)
+      VLOG_INFO("launching at %.0f %% of the samples: %s", sm.activity * 100,
+                steady ? "steady, takes pair turns" : "bursty, kept out of the pair turns");
+    sm.steady = steady;
+  }
   VLOG_DEBUG("container launch rate %.0f/s", sm.launch_rate);
   sm.board.refresh(now);
   for (int d = 0; d < s.n_agents; d++) {
@@ -462,6 +488,15 @@ void sample_tick(Region* r, Sampler& sm) {
     // room for that (the plugin emits the percent rounded up for this reason).
     timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, window_ms(sm, d, now), led ? ds.cu_share_bp : 0), dt,
                     charge, yield ? 0 : dt);
+    if (d == 0 && config().gpu_concurrency < 0 && sm.pairs_on[d]) {
+      // Steadiness: only samples at which the container was free to launch count.
+      const uint64_t total = container_launches(r);
+      if (!sm.want_since[d] && ds.gate_open.load(std::memory_order_relaxed)) {
+        sm.act_ticks++;
+        if (total != sm.act_launches) sm.act_busy++;
+      }
+      sm.act_launches = total;
+    }
     const int conc = concurrency_on(sm, d);
     if (conc <= 0 && (sm.admitted[d] || sm.want_since[d])) {  // pairs switched off: out of the turns
       sm.admitted[d] = false;

@@ -1022,3 +1022,29 @@ def test_auto_pair_turns_follow_the_launch_rate(fake, tmp_path, kernel_us, pairs
     else:
         assert "-> pair turns" not in logs
         assert sum(fracs) > 2.6, fracs
+
+
+def test_bursty_container_is_kept_out_of_auto_pair_turns(fake, tmp_path):
+    """VGPU_GPU_CONCURRENCY=auto: a container that launches in bursts with idle gaps (a
+    request-serving pod) is kept out of the pair turns - it runs whenever its credit allows -
+    while the steady ones take turns (profiles/r6a: a class-less b=1 service waiting for turns
+    went from 24 to 96 ms P99)."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+
+    def env(i):
+        return _board_env(fake, tmp_path, f"t{i}", VGPU_DEVICE_CU_LIMIT="25", VGPU_CU_MODE="temporal",
+                          VGPU_GPU_CONCURRENCY="auto", VGPU_CPU_NODE=str(i % 2), VGPU_LOG_LEVEL="2",
+                          VGPU_PAIRS_ON_RATE="4000", VGPU_PAIRS_OFF_RATE="2000")
+    steady = [sp.Popen([HARNESS, "stream", "sleep=0.5", "run=20,5"], env=env(i), stdout=sp.PIPE, stderr=sp.PIPE,
+                       text=True) for i in range(3)]
+    bursts = ["sleep=0.5"] + [x for _ in range(120) for x in ("run=20,0.004", "sleep=0.03")]
+    service = sp.Popen([HARNESS, "stream"] + bursts, env=env(3), stdout=sp.PIPE, stderr=sp.PIPE, text=True)
+    logs = []
+    for p in steady + [service]:
+        out, err = p.communicate(timeout=120)
+        assert p.returncode == 0, err[-2000:]
+        logs.append(err)
+    assert "-> pair turns" in "".join(logs[:3])
+    assert "bursty, kept out of the pair turns" in logs[3], logs[3][-3000:]
+    assert not any("bursty" in l for l in logs[:3]), [l[-1500:] for l in logs[:3]]
