@@ -29,6 +29,7 @@ namespace vgpu {
 
 bool g_stats_on = false;
 std::atomic<uint64_t> g_stats[kStatCount];
+std::atomic<uint64_t> g_turns{0}, g_turn_held_ns{0}, g_turn_wait_ns{0}, g_turn_wait_max_ns{0};
 
 namespace {
 const char* const kStatNames[kStatCount] = {"hsa_agent_get_info", "hsa_amd_memory_pool_get_info",
@@ -38,6 +39,9 @@ const char* const kStatNames[kStatCount] = {"hsa_agent_get_info", "hsa_amd_memor
 
 void print_stats() {
   fprintf(stderr, "[vGPU stats pid %d]", (int)getpid());
+  if (g_turns.load())
+    fprintf(stderr, " turns=%lu held_ms=%.1f waited_ms=%.1f max_wait_ms=%.1f", (unsigned long)g_turns.load(),
+            g_turn_held_ns.load() / 1e6, g_turn_wait_ns.load() / 1e6, g_turn_wait_max_ns.load() / 1e6);
   for (int i = 0; i < kStatCount; i++) fprintf(stderr, " %s=%lu", kStatNames[i], (unsigned long)g_stats[i].load());
   fprintf(stderr, " blocking_waits=%lu polled=%lu wait_ms=%.1f wakeups=%lu active_waits=%lu active_ms=%.1f\n",
           (unsigned long)g_sync_waits.load(), (unsigned long)g_sync_polled.load(), g_sync_wait_ns.load() / 1e6,

@@ -147,6 +147,9 @@ enum StatId : int {
   kStatLaunch, kStatGraphLaunch, kStatCopy, kStatSet, kStatCount
 };
 extern bool g_stats_on;
+// Concurrency admission of this process's sampler (VGPU_STATS): turns taken, time held, time
+// waited for them and the longest wait.
+extern std::atomic<uint64_t> g_turns, g_turn_held_ns, g_turn_wait_ns, g_turn_wait_max_ns;
 extern std::atomic<uint64_t> g_stats[kStatCount];
 // Host waits (sync_hooks.cpp): blocking waits, of which polled, their time, poll wake-ups.
 extern std::atomic<uint64_t> g_sync_waits, g_sync_polled, g_sync_wait_ns, g_sync_wakeups, g_sync_active,

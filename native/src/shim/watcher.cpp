@@ -525,6 +525,7 @@ void sample_tick(Region* r, Sampler& sm) {
           sm.admitted[d] = false;  // slice used up and someone waits: to the back of the queue
           sm.want_since[d] = now;
           hold = false;
+          g_turn_held_ns.fetch_add(now - sm.open_since[d], std::memory_order_relaxed);
           VLOG_DEBUG("device %d: turn over after %.1f ms (CPU node %d)", d, (now - sm.open_since[d]) / 1e6,
                      config().cpu_node);
         }
@@ -533,6 +534,11 @@ void sample_tick(Region* r, Sampler& sm) {
         if (sm.board.admit(a.gpu_id, conc, sm.want_since[d], config().cpu_node)) {
           VLOG_DEBUG("device %d: admitted after %.1f ms of waiting (CPU node %d)", d,
                      (now - sm.want_since[d]) / 1e6, config().cpu_node);
+          const uint64_t waited = now - sm.want_since[d];
+          g_turns.fetch_add(1, std::memory_order_relaxed);
+          g_turn_wait_ns.fetch_add(waited, std::memory_order_relaxed);
+          if (waited > g_turn_wait_max_ns.load(std::memory_order_relaxed))
+            g_turn_wait_max_ns.store(waited, std::memory_order_relaxed);
           sm.admitted[d] = true;
           sm.open_since[d] = now;
           sm.want_since[d] = 0;

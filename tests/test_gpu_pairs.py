@@ -34,6 +34,9 @@ def _four_pods(tmp_path, conc):
         procs = []
         for vid in node.vgpu_ids(uuid)[:4]:
             env = apply_contract(*node.pod([vid]))
+            # HIP's own wait: a crowded GPU's polled waits (sync_hooks.cpp) would cap a pod that
+            # waits every 8 tiny kernels at ~40k kernels/s whatever the admission does
+            env.update(VGPU_SYNC_WAIT="native", VGPU_STATS="1")
             procs.append(subprocess.Popen([PROBE, "procs", "1", "4", "2", "4", "spin", "none"], env=env,
                                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
         outs = []
@@ -41,6 +44,7 @@ def _four_pods(tmp_path, conc):
             out, err = p.communicate(timeout=90)
             assert p.returncode == 0, err[-2000:]
             outs.append(json.loads(out.strip().splitlines()[-1]))
+            print("\n".join(l for l in err.splitlines() if "turns=" in l))
     return [o["per_tenant"][0]["kps"] for o in outs]
 
 
