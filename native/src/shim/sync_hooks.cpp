@@ -14,10 +14,13 @@
 // crowd count: two or more other busy processes, watcher.cpp) becomes a loop of
 // acquire-loads and nanosleeps; an active wait with a short time-out (HIP's brief spin before
 // it blocks) stays as it is; the sleep grows with the time already waited (1/8 of
-// it, 20 us to 500 us), so a wait overshoots its completion by at most ~12 % (and 0.5 ms),
+// it, 20 us to 500 us, after a 30 us spin that catches the short waits of tiny-kernel pods;
+// the polling thread's timer slack is lowered to 1 us so a short sleep stays short), so a
+// wait overshoots its completion by at most ~12 % (and 0.5 ms),
 // and a multi-millisecond wait costs a few dozen wake-ups instead of a core. A lone pod, and
 // a pod of the latency class (priority 0), keeps ROCr's own wait (no added latency);
 // VGPU_SYNC_WAIT=poll|native forces either way.
+#include <sys/prctl.h>
 #include <time.h>
 
 #include <algorithm>
@@ -42,6 +45,17 @@ namespace {
 // An active wait longer than this is a spin-until-done wait (HIP passes an unlimited
 // time-out); shorter ones are the brief spin ahead of a blocking wait.
 constexpr uint64_t kActiveSpinNs = 1'000'000;
+// A polled wait spins this long before it sleeps.
+constexpr uint64_t kPollSpinNs = 30'000;
+
+// The polling thread's timer slack (Linux default 50 us, per thread) down to 1 us, once: a
+// 20 us sleep then wakes after ~20 us instead of ~70 us.
+void lower_timer_slack() {
+  static thread_local bool done = false;
+  if (done) return;
+  done = true;
+  (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+}
 
 bool satisfied(hsa_signal_condition_t c, hsa_signal_value_t v, hsa_signal_value_t cmp) {
   switch (c) {
@@ -105,6 +119,13 @@ hsa_signal_value_t hsa_signal_wait_scacquire(hsa_signal_t signal, hsa_signal_con
   const uint64_t t0 = now_ns();
   hsa_signal_value_t v = real_hsa_signal_load_scacquire(signal);
   uint64_t wakeups = 0;
+  // A short spin first: a pod that waits every few tiny kernels would otherwise pay a sleep's
+  // wake-up latency on every wait (profiles/r6a3: 8-kernel waits capped at ~40k kernels/s).
+  while (!satisfied(condition, v, compare_value) && now_ns() - t0 < kPollSpinNs) {
+    __builtin_ia32_pause();
+    v = real_hsa_signal_load_scacquire(signal);
+  }
+  if (!satisfied(condition, v, compare_value)) lower_timer_slack();
   while (!satisfied(condition, v, compare_value)) {
     const uint64_t el = now_ns() - t0;
     if (el >= timeout_hint) break;
