@@ -57,6 +57,7 @@ struct alignas(64) BoardSlot {
   // different CPU sockets.
   std::atomic<int32_t> cpu_node1;
   std::atomic<uint32_t> launch_rate;  // the container's kernel launches per second (EWMA)
+  std::atomic<int32_t> steady1;       // 0 unknown, 1 bursty (idles between launches), 2 steady
 };
 constexpr size_t kBoardSlotV1Size = offsetof(BoardSlot, svm_vram);
 
@@ -83,6 +84,7 @@ struct BoardPeer {
   std::vector<uint64_t> hbm_want_ns;         // per device: when it was (re-)published
   int cpu_node = -1;                         // VGPU_CPU_NODE (-1 = unknown)
   uint32_t launch_rate = 0;                  // kernel launches per second
+  int steady = -1;                           // -1 unknown, 0 bursty, 1 steady
 };
 
 // Automatic pair turns (VGPU_GPU_CONCURRENCY=auto): below VGPU_PAIRS_OFF_RATE launches/s of
@@ -118,6 +120,10 @@ class Board {
   void publish_launch_rate(uint32_t per_s);
   // Sum of the live peers' launch rates on GPU `gpu_id`.
   uint64_t peers_launch_rate(uint32_t gpu_id) const;
+  // Whether the container launches steadily (a batch pod) or in bursts (a serving pod).
+  void publish_steady(bool steady);
+  // Whether a live peer on GPU `gpu_id` launching at least `min_rate` kernels/s is bursty.
+  bool bursty_peer_on(uint32_t gpu_id, uint32_t min_rate) const;
   // Virtual device memory of device `dev`: the container's SVM bytes in VRAM, and HBM it was
   // refused within its share (0 = none) since `want_ns`.
   void publish_memory(int dev, uint64_t svm_vram, uint64_t hbm_want, uint64_t want_ns);

@@ -128,6 +128,18 @@ uint64_t Board::peers_launch_rate(uint32_t gpu_id) const {
   return n;
 }
 
+void Board::publish_steady(bool steady) {
+  if (self_) self_->steady1.store(steady ? 2 : 1, std::memory_order_relaxed);
+}
+
+bool Board::bursty_peer_on(uint32_t gpu_id, uint32_t min_rate) const {
+  for (const BoardPeer& p : peers_)
+    if (p.steady == 0 && p.launch_rate >= min_rate &&
+        std::find(p.gpu_ids.begin(), p.gpu_ids.end(), gpu_id) != p.gpu_ids.end())
+      return true;
+  return false;
+}
+
 void Board::publish_memory(int dev, uint64_t svm_vram, uint64_t hbm_want, uint64_t want_ns) {
   if (!self_ || dev < 0 || dev >= kMaxDevices) return;
   self_->svm_vram[dev].store(svm_vram, std::memory_order_relaxed);
@@ -272,7 +284,11 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
     }
     const int32_t cn = got >= (ssize_t)sizeof(BoardSlot) ? s.cpu_node1.load(std::memory_order_relaxed) : 0;
     p.cpu_node = cn > 0 && cn <= 64 ? cn - 1 : -1;
-    if (got >= (ssize_t)sizeof(BoardSlot)) p.launch_rate = std::min<uint32_t>(s.launch_rate.load(std::memory_order_relaxed), 10'000'000u);
+    if (got >= (ssize_t)sizeof(BoardSlot)) {
+      p.launch_rate = std::min<uint32_t>(s.launch_rate.load(std::memory_order_relaxed), 10'000'000u);
+      const int32_t st = s.steady1.load(std::memory_order_relaxed);
+      p.steady = st == 1 ? 0 : st == 2 ? 1 : -1;
+    }
     const int n = std::max(0, std::min(s.npids.load(std::memory_order_relaxed), kBoardMaxPids));
     for (int i = 0; i < n; i++) {
       const int pid = s.hostpids[i].load(std::memory_order_relaxed);

@@ -144,17 +144,23 @@ struct Sampler {
   uint64_t pairs_low_since[kMaxDevices] = {};
   // Steadiness (auto): of the samples at which the container was free to launch, the share
   // with new launches since the previous one. A batch pod launches at every sample; a
-  // request-serving pod idles between requests and is kept out of the turns (profiles/r6a).
+  // request-serving pod idles between requests, and while one is busy on a GPU its pods do
+  // not take pair turns: it would wait for them (profiles/r6a).
   uint64_t act_launches = 0;
   uint32_t act_ticks = 0, act_busy = 0;
+  bool act_prev_free = false;
   double activity = 1.0;
   bool steady = true;
 };
 
+// A container launching fewer kernels per second than this is idle as far as the automatic
+// pair turns are concerned, bursty or not.
+constexpr uint32_t kBurstyMinRate = 500;
+
 // The concurrency admission's k on device `d` (0 = everybody at once).
 int concurrency_on(const Sampler& sm, int d) {
   const int k = sm.board.attached() ? config().gpu_concurrency : 0;
-  return k >= 0 ? k : (sm.pairs_on[d] && sm.steady ? 2 : 0);
+  return k >= 0 ? k : (sm.pairs_on[d] ? 2 : 0);
 }
 
 // The container's launches so far: this process's live counter, the others' as published.
@@ -190,14 +196,22 @@ void pairs_tick(Region* r, Sampler& sm, const uint32_t* ids, uint64_t now) {
     const bool steady = sm.steady ? sm.activity >= 0.6 : sm.activity >= 0.8;
     if (steady != sm.steady)
       VLOG_INFO("launching at %.0f %% of the samples: %s", sm.activity * 100,
-                steady ? "steady, takes pair turns" : "bursty, kept out of the pair turns");
+                steady ? "steady" : "bursty, no pair turns on its GPU");
     sm.steady = steady;
   }
+  sm.board.publish_steady(sm.steady);
   VLOG_DEBUG("container launch rate %.0f/s", sm.launch_rate);
   sm.board.refresh(now);
   for (int d = 0; d < s.n_agents; d++) {
     const uint64_t rate = (uint64_t)sm.launch_rate + sm.board.peers_launch_rate(ids[d]);
-    if (rate >= config().pairs_on_rate) {
+    // A busy bursty container on the GPU (a pod serving requests) would wait for turns: no
+    // pairs there, whatever the rate (profiles/r6a).
+    const bool bursty = (!sm.steady && sm.launch_rate >= kBurstyMinRate) || sm.board.bursty_peer_on(ids[d], kBurstyMinRate);
+    if (bursty) {
+      if (sm.pairs_on[d]) VLOG_INFO("device %d: a bursty container is busy on the GPU -> all at once", d);
+      sm.pairs_on[d] = false;
+      sm.pairs_low_since[d] = 0;
+    } else if (rate >= config().pairs_on_rate) {
       if (!sm.pairs_on[d]) VLOG_INFO("device %d: %lu launches/s on the GPU -> pair turns", d, (unsigned long)rate);
       sm.pairs_on[d] = true;
       sm.pairs_low_since[d] = 0;
@@ -488,13 +502,17 @@ void sample_tick(Region* r, Sampler& sm) {
     // room for that (the plugin emits the percent rounded up for this reason).
     timeshare_apply(ds, timeshare_params(ds.cu_limit_pct, window_ms(sm, d, now), led ? ds.cu_share_bp : 0), dt,
                     charge, yield ? 0 : dt);
-    if (d == 0 && config().gpu_concurrency < 0 && sm.pairs_on[d]) {
+    if (d == 0 && config().gpu_concurrency < 0) {
       // Steadiness: only samples at which the container was free to launch count.
       const uint64_t total = container_launches(r);
-      if (!sm.want_since[d] && ds.gate_open.load(std::memory_order_relaxed)) {
+      // Free for the whole interval: not waiting for a turn, and the credit gate open at this
+      // sample and the previous one (a pod the limiter throttles is not idle by choice).
+      const bool free_now = !sm.want_since[d] && ds.gate_open.load(std::memory_order_relaxed);
+      if (free_now && sm.act_prev_free) {
         sm.act_ticks++;
         if (total != sm.act_launches) sm.act_busy++;
       }
+      sm.act_prev_free = free_now;
       sm.act_launches = total;
     }
     const int conc = concurrency_on(sm, d);

@@ -1024,11 +1024,11 @@ def test_auto_pair_turns_follow_the_launch_rate(fake, tmp_path, kernel_us, pairs
         assert sum(fracs) > 2.6, fracs
 
 
-def test_bursty_container_is_kept_out_of_auto_pair_turns(fake, tmp_path):
-    """VGPU_GPU_CONCURRENCY=auto: a container that launches in bursts with idle gaps (a
-    request-serving pod) is kept out of the pair turns - it runs whenever its credit allows -
-    while the steady ones take turns (profiles/r6a: a class-less b=1 service waiting for turns
-    went from 24 to 96 ms P99)."""
+def test_bursty_container_switches_auto_pair_turns_off(fake, tmp_path):
+    """VGPU_GPU_CONCURRENCY=auto: while a container that launches in bursts with idle gaps (a
+    request-serving pod) is busy on the GPU, its containers take no pair turns - the service
+    would wait for them (profiles/r6a: a class-less b=1 service went from 24 to 96 ms P99;
+    keeping only the service out of the turns still left 37.8 ms, profiles/r6a3)."""
     import subprocess as sp
     (tmp_path / "board").mkdir()
 
@@ -1045,6 +1045,8 @@ def test_bursty_container_is_kept_out_of_auto_pair_turns(fake, tmp_path):
         out, err = p.communicate(timeout=120)
         assert p.returncode == 0, err[-2000:]
         logs.append(err)
-    assert "-> pair turns" in "".join(logs[:3])
-    assert "bursty, kept out of the pair turns" in logs[3], logs[3][-3000:]
-    assert not any("bursty" in l for l in logs[:3]), [l[-1500:] for l in logs[:3]]
+    assert "bursty, no pair turns on its GPU" in logs[3], logs[3][-3000:]
+    for log in logs[:3]:
+        # whatever happened before the service was seen, the steady pods end without pairs
+        last = max(("-> pair turns", "-> all at once"), key=lambda m: log.rfind(m))
+        assert log.rfind(last) < 0 or last == "-> all at once", log[-2000:]
