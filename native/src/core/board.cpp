@@ -267,7 +267,9 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
     ::close(fd);
     if (got < (ssize_t)kBoardSlotV1Size || s.magic != kBoardMagic || s.version != kBoardVersion) continue;
     const uint64_t hb = s.heartbeat_ns.load(std::memory_order_relaxed);
-    if (!hb || hb > now + kBoardStaleNs || now - hb > kBoardStaleNs) continue;
+    // A heartbeat newer than `now` (the peer published after the caller read its clock) is
+    // fresh: `now - hb` would wrap and drop a live peer at random.
+    if (!hb || hb > now + kBoardStaleNs || (hb < now && now - hb > kBoardStaleNs)) continue;
     BoardPeer p;
     p.priority = s.priority.load(std::memory_order_relaxed);
     const int ndev = std::max(0, std::min(s.ndev, kMaxDevices));
@@ -278,7 +280,7 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
       p.want_since.push_back(s.want_since[i].load(std::memory_order_relaxed));
       p.svm_vram.push_back(s.svm_vram[i].load(std::memory_order_relaxed));
       const uint64_t wn = s.hbm_want_ns[i].load(std::memory_order_relaxed);
-      const bool fresh = wn && wn <= now + kBoardStaleNs && now - wn < kBoardWantNs;
+      const bool fresh = wn && wn <= now + kBoardStaleNs && (wn >= now || now - wn < kBoardWantNs);
       p.hbm_want.push_back(fresh ? s.hbm_want[i].load(std::memory_order_relaxed) : 0);
       p.hbm_want_ns.push_back(fresh ? wn : 0);
     }

@@ -51,7 +51,8 @@ bool LedgerReader::fresh(uint64_t now) const {
   // period stretches with the processes on the node), never less than kLedgerStaleNs.
   const uint64_t period = f_->period_ns.load(std::memory_order_relaxed);
   const uint64_t stale = period < kLedgerStaleNs / kLedgerStalePeriods ? kLedgerStaleNs : period * kLedgerStalePeriods;
-  return hb && hb <= now + stale && now - hb <= stale;
+  // A heartbeat newer than `now` (written after the caller read its clock) is fresh.
+  return hb && hb <= now + stale && (hb >= now || now - hb <= stale);
 }
 
 const LedgerEntry* LedgerReader::find(int pid) const {

@@ -558,6 +558,8 @@ uint64_t queued_packets(int dev) {
 
 }  // namespace
 
+uint64_t packets_queued(int dev) { return queued_packets(dev); }
+
 uint64_t wait_queue_depth(int dev, int cap) {
   // Bounded: a queue can also hold packets that wait on something only this thread would
   // launch later (a barrier on another stream's event), which must never deadlock.

@@ -185,6 +185,8 @@ inline void gate_suspend() {
 // launch block and the temporal GPU-time credit of device `dev` (dev < 0 = current HIP
 // device).
 void gate_launch(int dev);
+// Packets of this process's queues on device `dev` the command processor has not taken yet.
+uint64_t packets_queued(int dev);
 // VGPU_HOOK_LAUNCH (gates.cpp): false turns the launch gates into pass-throughs.
 extern bool g_launch_hooks_on;
 

@@ -143,7 +143,8 @@ struct Sampler {
   bool pairs_on[kMaxDevices] = {};
   uint64_t pairs_low_since[kMaxDevices] = {};
   // Steadiness (auto): of the samples at which the container was free to launch, the share
-  // with new launches since the previous one. A batch pod launches at every sample; a
+  // with launches or work of its own on the GPU since the previous one. A batch pod is busy at
+  // every sample; a
   // request-serving pod idles between requests, and while one is busy on a GPU its pods do
   // not take pair turns: it would wait for them (profiles/r6a).
   uint64_t act_launches = 0;
@@ -200,7 +201,7 @@ void pairs_tick(Region* r, Sampler& sm, const uint32_t* ids, uint64_t now) {
     sm.steady = steady;
   }
   sm.board.publish_steady(sm.steady);
-  VLOG_DEBUG("container launch rate %.0f/s", sm.launch_rate);
+  VLOG_DEBUG("container launch rate %.0f/s, %s", sm.launch_rate, sm.steady ? "steady" : "bursty");
   sm.board.refresh(now);
   for (int d = 0; d < s.n_agents; d++) {
     const uint64_t rate = (uint64_t)sm.launch_rate + sm.board.peers_launch_rate(ids[d]);
@@ -510,7 +511,10 @@ void sample_tick(Region* r, Sampler& sm) {
       const bool free_now = !sm.want_since[d] && ds.gate_open.load(std::memory_order_relaxed);
       if (free_now && sm.act_prev_free) {
         sm.act_ticks++;
-        if (total != sm.act_launches) sm.act_busy++;
+        // Busy: it launched, or work of its own was queued or resident meanwhile (a batch pod
+        // waiting for its kernels is not idle; a serving pod between requests has nothing
+        // on the GPU).
+        if (total != sm.act_launches || charge > 0 || packets_queued(d) > 0) sm.act_busy++;
       }
       sm.act_prev_free = free_now;
       sm.act_launches = total;

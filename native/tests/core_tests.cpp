@@ -1034,6 +1034,16 @@ static void test_board() {
       w1.refresh(now);
       h.refresh(now);
     }
+    // Launch rates and steadiness (auto pair turns): a bursty peer busy on the GPU is seen.
+    w1.publish_launch_rate(2500);
+    w1.publish_steady(false);
+    h.refresh(now);
+    CHECK_EQ(h.peers_launch_rate(7000), 2500u);
+    CHECK(h.bursty_peer_on(7000, 500));
+    CHECK(!h.bursty_peer_on(7000, 5000));   // below the rate that counts as busy
+    w1.publish_steady(true);
+    h.refresh(now);
+    CHECK(!h.bursty_peer_on(7000, 500));
     // Without nodes (a container that does not publish one): plain first-come admission.
     CHECK(!w1.admit(7000, 2, now - 1000, -1));  // w0 came first and one place is left
     CHECK(w0.admit(7000, 2, now - 2000, -1));
@@ -1043,6 +1053,9 @@ static void test_board() {
     CHECK(w0.admit(7000, 2, now - 2000, 0));
     for (Board* x : {&h, &w0, &w1}) x->leave();
   }
+  // A heartbeat written after the reader took its clock is fresh, not "stale by 2^64 ns":
+  // peers used to drop out of refresh() at random this way.
+  CHECK_EQ(a.refresh(now - 1000).size(), 1u);
   // A stale heartbeat (the container is gone) or a departed slot is ignored.
   CHECK_EQ(a.refresh(now + kBoardStaleNs + 1).size(), 0u);
   b.leave();
@@ -1076,6 +1089,7 @@ static void test_ledger_fresh() {
   LedgerReader r;
   CHECK(r.open(dir, gid));
   CHECK(r.fresh(now + 10'000'000));
+  CHECK(r.fresh(now - 1000));                      // written after the reader took its clock
   CHECK(!r.fresh(now + kLedgerStaleNs + 1));       // short period: the fixed floor applies
   // A daemon whose period stretched (every GPU of a busy node read in turn): stale only after
   // a few of its own periods, not after the fixed 50 ms.

@@ -1038,7 +1038,7 @@ def test_bursty_container_switches_auto_pair_turns_off(fake, tmp_path):
                           VGPU_PAIRS_ON_RATE="4000", VGPU_PAIRS_OFF_RATE="2000")
     steady = [sp.Popen([HARNESS, "stream", "sleep=0.5", "run=20,5"], env=env(i), stdout=sp.PIPE, stderr=sp.PIPE,
                        text=True) for i in range(3)]
-    bursts = ["sleep=0.5"] + [x for _ in range(120) for x in ("run=20,0.004", "sleep=0.03")]
+    bursts = ["sleep=0.5"] + [x for _ in range(220) for x in ("run=20,0.008", "sleep=0.02")]  # outlives the others
     service = sp.Popen([HARNESS, "stream"] + bursts, env=env(3), stdout=sp.PIPE, stderr=sp.PIPE, text=True)
     logs = []
     for p in steady + [service]:
