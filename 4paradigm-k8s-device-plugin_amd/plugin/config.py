@@ -62,9 +62,9 @@ class PluginConfig:
     allow_latency_class: bool = False       # every container may take VGPU_TASK_PRIORITY=0
     latency_vgpus_per_gpu: int = 0          # vGPUs per GPU advertised as <resource>-latency (latency class granted)
     host_budget_bytes: int = -1             # resolved per-vGPU host budget (plugin/host_memory.py; -1 = not yet)
-    gpu_concurrency: int = 0                # limited containers holding a GPU's time at once (0 = any, -1 = auto:
-                                            # cross-socket pairs while the GPU is dispatch-bound, profiles/r6k;
-                                            # opt-in: turn waits cost latency pods without a class, profiles/r6a)
+    gpu_concurrency: int = -1               # limited containers holding a GPU's time at once (0 = any, -1 = auto:
+                                            # cross-socket pairs while the GPU is dispatch-bound and no bursty
+                                            # serving pod is busy on it, profiles/r6k, r6a5)
     ledger: bool = True                     # run the node's GPU-time ledger daemon (vgpu-ledger; profiles/r4o)
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"  # kubelet PodResources v1
     active_oom_killer: bool = True          # the containers' memory backstop (limits file; reference ACTIVE_OOM_KILLER)
@@ -192,8 +192,8 @@ _FLAGS = [
      "containers on the GPU-time limiter that may hold a GPU at once, taking turns over the node-wide board, in "
      "pairs of different CPU sockets when --numa-spread places them (0 = no admission: every container whose credit "
      "allows runs; auto = pairs while the GPU's containers launch more than VGPU_PAIRS_ON_RATE (40k) kernels/s "
-     "together - dispatch-bound pods, which three at once slow down - and everybody at once otherwise; for nodes "
-     "that pack launch-bound batch pods: a request-serving pod without the latency class waits for its turns)"),
+     "together - dispatch-bound pods, which three at once slow down - and no container that launches in bursts (a "
+     "serving pod) is busy there, everybody at once otherwise; the default)"),
     ("--ledger", "ledger", "bool", ["VGPU_NODE_LEDGER"],
      "run the node GPU-time ledger (vgpu-ledger): one KFD occupancy sampler for every limited container of the "
      "node instead of one per container (n reads per period instead of n^2, one consistent snapshot), and "
