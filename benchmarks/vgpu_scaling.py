@@ -179,13 +179,15 @@ def miopen_dirs(mode, tmp, i):
 
 
 def run_point(backend, uuid, case, n, policy, warmup, seconds, hw_queues=0, pod_env=None, split=0, ledger=None,
-              miopen="home"):
+              miopen="home", conc=None):
     from amdvgpu.plugin.kubelet_stub import NodeHarness
     from amdvgpu.shim.launcher import apply_contract
     tmp = tempfile.mkdtemp(prefix="scal-")
     go = os.path.join(tmp, "go")
     procs, outs, regions = [], [], []
     kw = {} if ledger is None else {"ledger": bool(ledger)}
+    if conc is not None:
+        kw["gpu_concurrency"] = conc
     with NodeHarness(backend, device_split_count=split or n, cu_mode=MODES[policy], **kw) as node:
         for i, vid in enumerate(node.vgpu_ids(uuid)[:n]):
             envs, mounts = node.pod([vid])
@@ -255,6 +257,8 @@ def main():
                     "plugin's default, on)")
     ap.add_argument("--miopen-db", default="home", choices=["home", "per-pod", "empty"],
                     help="MIOpen find-db / kernel cache of the pods (see miopen_dirs)")
+    ap.add_argument("--gpu-concurrency", type=lambda v: -1 if v == "auto" else int(v), default=None,
+                    help="the plugin's --gpu-concurrency (default: the plugin's own default)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--go")
@@ -282,7 +286,7 @@ def main():
                             continue
                         r = run_point(backend, uuid, a.case, n, pol, a.warmup, a.seconds, hq,
                                       pe if n > 1 else None, a.split, ledger=a.node_ledger,
-                                      miopen=a.miopen_db if n > 1 else "home")
+                                      miopen=a.miopen_db if n > 1 else "home", conc=a.gpu_concurrency)
                         rows.append(r)
                         print(json.dumps(r), flush=True)
     base = {r["policy"]: r["aggregate_throughput"] for r in rows if r["tenants"] == 1}
