@@ -161,7 +161,7 @@ def ab_compare(a, pods, backend, uuid, split, prio):
     runs = []
     # The operator grants the latency class here (--allow-latency-class): the pods choose theirs.
     with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode, allow_latency_class=True,
-                     gpu_concurrency=a.gpu_concurrency) as node:
+                     **({} if a.gpu_concurrency is None else {"gpu_concurrency": a.gpu_concurrency})) as node:
         ids = node.vgpu_ids(uuid)[:len(pods)]
         arms = ([] if a.skip_default else [("default", None, None)]) + [("priority", prio, None)]
         for bg in a.bg_env:
@@ -225,8 +225,8 @@ def main():
     ap.add_argument("--skip-default", action="store_true", help="with --ab: no arm without priorities")
     ap.add_argument("--trace-latency", default="", help="with --ab: rocprofv3 kernel trace of the latency pods "
                                                           "under DIR/<arm>_<run>")
-    ap.add_argument("--gpu-concurrency", type=lambda v: -1 if v == "auto" else int(v), default=0,
-                    help="the plugin's --gpu-concurrency for every pod (auto = pair turns while dispatch-bound)")
+    ap.add_argument("--gpu-concurrency", type=lambda v: -1 if v == "auto" else int(v), default=None,
+                    help="the plugin's --gpu-concurrency for every pod (default: the plugin's own, auto)")
     ap.add_argument("--json-out")
     ap.add_argument("--md-out")
     ap.add_argument("--worker", action="store_true")
@@ -256,7 +256,7 @@ def main():
         return ab_compare(a, pods, backend, uuid, split, prio)
     # The operator grants the latency class here (--allow-latency-class): the pods choose theirs.
     with NodeHarness(backend, device_split_count=split, cu_mode=a.cu_mode, allow_latency_class=True,
-                     gpu_concurrency=a.gpu_concurrency) as node:
+                     **({} if a.gpu_concurrency is None else {"gpu_concurrency": a.gpu_concurrency})) as node:
         ids = node.vgpu_ids(uuid)[:len(pods)]
         for pod, vid in zip(pods, ids):
             t = time.time()
