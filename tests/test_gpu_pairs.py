@@ -3,9 +3,9 @@
 Three or more processes with launches in flight each dispatch at about a quarter of the rate
 two reach: the command processor, not the host (profiles/r6f). The concurrency admission
 (VGPU_GPU_CONCURRENCY, the node board) lets two containers of a crowded GPU hold it at a time,
-one per CPU socket. Four split-4 pods from a real Allocate each run the C++ tiny-kernel probe
-(native/tests/cotenancy_probe.hip: 2 us kernels, well inside each pod's 25 % of GPU time; a
-wait every 8), first all at once, then with pair turns. The pairs must beat all-at-once
+one per CPU socket. Four split-4 pods (50 % of the GPU's time each) from a real Allocate each
+run the C++ tiny-kernel probe (native/tests/cotenancy_probe.hip: 2 us kernels, a wait every
+8), first all at once, then with pair turns. The pairs must beat all-at-once
 clearly, and no pod may starve (the round-6 bug where one socket's pods kept both places,
 profiles/r6k/starve).
 """
@@ -29,8 +29,11 @@ def _four_pods(tmp_path, conc):
     from amdvgpu.shim.launcher import apply_contract
     backend = SysfsBackend()
     uuid = backend.devices()[0].uuid
-    with NodeHarness(backend, device_split_count=4, cu_mode="temporal", gpu_concurrency=conc,
-                     workdir=str(tmp_path / f"node{conc}")) as node:
+    # Cores scaling 2: each split-4 vGPU is entitled to 50 % of the GPU's time, so a pod that
+    # holds its turn (2 us kernels at ~200k/s: ~40 % busy) runs on the admission alone, not
+    # into its GPU-time share.
+    with NodeHarness(backend, device_split_count=4, device_cores_scaling=2.0, cu_mode="temporal",
+                     gpu_concurrency=conc, workdir=str(tmp_path / f"node{conc}")) as node:
         procs = []
         for vid in node.vgpu_ids(uuid)[:4]:
             env = apply_contract(*node.pod([vid]))
