@@ -13,6 +13,9 @@
 //   vgpuctl <region> priority <n>
 //   vgpuctl <region> reclaim              free slots of exited processes
 //   vgpuctl ledger <board-dir>            the node GPU-time ledgers (vgpu/ledger.h), JSON
+//   vgpuctl board <board-dir>             the live containers on the node board (vgpu/board.h):
+//                                         class, CPU node, launch rate and steadiness, and per
+//                                         GPU whether it holds a turn or waits for one, JSON
 #include <dirent.h>
 
 #include <cstdio>
@@ -20,6 +23,7 @@
 #include <cstring>
 #include <string>
 
+#include "vgpu/board.h"
 #include "vgpu/ledger.h"
 #include "vgpu/ratelimit.h"
 #include "vgpu/region_api.h"
@@ -63,11 +67,45 @@ static int show_ledgers(const char* dir) {
   return 0;
 }
 
+// The live slots of <board>: what the containers of the node tell each other.
+static int show_board(const char* dir) {
+  vgpu::Board b;
+  DIR* probe = opendir(dir);
+  if (probe) closedir(probe);
+  if (!probe || b.open_readonly(dir) != 0) {
+    fprintf(stderr, "vgpuctl: cannot open %s\n", dir);
+    return 1;
+  }
+  const uint64_t now = vgpu::now_ns();
+  const auto& peers = b.refresh(now);
+  printf("{\"containers\": [");
+  int n = 0;
+  for (const vgpu::BoardPeer& p : peers) {
+    printf("%s\n  {\"priority\": %d, \"cpu_node\": %d, \"launches_per_s\": %u, \"steady\": %s, \"hostpids\": [",
+           n++ ? "," : "", p.priority, p.cpu_node, p.launch_rate,
+           p.steady < 0 ? "null" : p.steady ? "true" : "false");
+    for (size_t i = 0; i < p.hostpids.size(); i++) printf("%s%d", i ? ", " : "", p.hostpids[i]);
+    printf("], \"gpus\": [");
+    for (size_t i = 0; i < p.gpu_ids.size(); i++) {
+      const uint64_t want = i < p.want_since.size() ? p.want_since[i] : 0;
+      printf("%s{\"gpu_id\": %u, \"holds_turn\": %s, \"waiting_ms\": ", i ? ", " : "", p.gpu_ids[i],
+             i < p.gate.size() && p.gate[i] ? "true" : "false");
+      if (want && now > want) printf("%.1f", (now - want) / 1e6);
+      else printf("null");
+      printf(", \"svm_vram\": %llu}", (unsigned long long)(i < p.svm_vram.size() ? p.svm_vram[i] : 0));
+    }
+    printf("]}");
+  }
+  printf("]}\n");
+  return 0;
+}
+
 static int usage() {
   fprintf(stderr,
           "usage: vgpuctl <region-file> show|suspend|resume|block|unblock|reclaim|"
           "set-limit <dev> <size>|set-cu <dev> <pct>|set-host-limit <size>|priority <n>\n"
-          "       vgpuctl ledger <board-dir>\n");
+          "       vgpuctl ledger <board-dir>\n"
+          "       vgpuctl board <board-dir>\n");
   return 2;
 }
 
@@ -113,6 +151,7 @@ static void show(vgpu_region* r) {
 int main(int argc, char** argv) {
   if (argc < 3) return usage();
   if (!strcmp(argv[1], "ledger")) return show_ledgers(argv[2]);
+  if (!strcmp(argv[1], "board")) return show_board(argv[2]);
   int err = 0;
   vgpu_region* r = vgpu_region_open(argv[1], 0, &err);
   if (!r) {

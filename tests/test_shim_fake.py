@@ -1050,3 +1050,23 @@ def test_bursty_container_switches_auto_pair_turns_off(fake, tmp_path):
         # whatever happened before the service was seen, the steady pods end without pairs
         last = max(("-> pair turns", "-> all at once"), key=lambda m: log.rfind(m))
         assert log.rfind(last) < 0 or last == "-> all at once", log[-2000:]
+
+
+def test_vgpuctl_board_lists_a_live_container(fake, tmp_path):
+    """`vgpuctl board` on a live container of the fake runtime: its CPU node, launch rate and
+    steadiness, and its GPU (what the pair turns decide from)."""
+    import subprocess as sp
+    (tmp_path / "board").mkdir()
+    e = _board_env(fake, tmp_path, "t0", VGPU_DEVICE_CU_LIMIT="50", VGPU_CU_MODE="temporal",
+                   VGPU_GPU_CONCURRENCY="auto", VGPU_CPU_NODE="1")
+    p = sp.Popen([HARNESS, "stream", "run=20,2.5"], env=e, stdout=sp.PIPE, text=True)
+    try:
+        time.sleep(1.5)
+        out = sp.run([os.path.join(LIB_DIR, "vgpuctl"), "board", str(tmp_path / "board")], capture_output=True,
+                     text=True, timeout=30)
+    finally:
+        p.communicate(timeout=60)
+    assert out.returncode == 0, out.stderr
+    cs = json.loads(out.stdout)["containers"]
+    assert len(cs) == 1 and cs[0]["cpu_node"] == 1, cs
+    assert cs[0]["launches_per_s"] > 0 and cs[0]["gpus"][0]["gpu_id"] > 0, cs

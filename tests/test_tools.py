@@ -46,3 +46,17 @@ def test_vgpu_validate_decode(tmp_path):
     p = subprocess.run([os.path.join(LIB_DIR, "vgpu-validate"), "--decode", str(f)], capture_output=True, text=True)
     assert p.returncode == 0
     assert p.stdout.split() == ["GPU-abcdef0123456789", "GPU-9813000000000001"]
+
+
+def test_vgpuctl_board_shows_the_live_containers(tmp_path):
+    """vgpuctl board <dir>: the node board as JSON - each live container's class, CPU node,
+    launch rate, steadiness and turn state per GPU (what the concurrency admission reads)."""
+    import json
+    board = tmp_path / "board"
+    board.mkdir()
+    # An empty board is an empty list; a slot of nonsense is ignored.
+    (board / "junk.slot").write_text("not a slot")
+    p = vgpuctl("board", str(board))
+    assert p.returncode == 0, p.stderr
+    assert json.loads(p.stdout) == {"containers": []}
+    assert vgpuctl("board", str(tmp_path / "missing")).returncode != 0
