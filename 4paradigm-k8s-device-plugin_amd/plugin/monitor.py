@@ -97,9 +97,50 @@ def ledger_metrics(w, board_dir):
                      p["charged_ns"] / 1e9)
 
 
+def _board_json(board_dir):
+    """The node board's live containers, as ``vgpuctl board`` reads them (None when the tool or
+    the board is missing)."""
+    import subprocess
+    from ..shim import native
+    if not os.path.isdir(board_dir):
+        return None
+    try:
+        p = subprocess.run([native.lib_path(native.VGPUCTL), "board", board_dir], capture_output=True, text=True,
+                           timeout=10)
+        return json.loads(p.stdout) if p.returncode == 0 else None
+    except (native.NativeMissing, OSError, ValueError, subprocess.TimeoutExpired):
+        return None
+
+
+def board_metrics(w, board_dir):
+    """The node board (``native/include/vgpu/board.h``): per container its launch rate, whether
+    it launches steadily (batch) or in bursts (serving), its CPU node, and per GPU whether it
+    holds a turn of the concurrency admission or waits for one (``--gpu-concurrency``).
+    Labelled by region file, like the container metrics."""
+    data = _board_json(board_dir) or {}
+    for c in data.get("containers", []):
+        lb = {"region": c["container"] + ".cache"}
+        w.metric("vgpu_board_launches_per_second", "gauge", "node board: the container's kernel launches per second",
+                 lb, c["launches_per_s"])
+        if c.get("steady") is not None:
+            w.metric("vgpu_board_steady", "gauge", "node board: 1 launches steadily (batch), 0 in bursts (serving)",
+                     lb, int(c["steady"]))
+        w.metric("vgpu_board_cpu_node", "gauge", "node board: the CPU node of the container's processes (-1 = none)",
+                 lb, c["cpu_node"])
+        for g in c.get("gpus", []):
+            gl = dict(lb, gpu_id=g["gpu_id"])
+            w.metric("vgpu_board_holds_turn", "gauge", "node board: 1 while the container holds a turn on the GPU",
+                     gl, int(g["holds_turn"]))
+            if g.get("waiting_ms") is not None:
+                w.metric("vgpu_board_waiting_seconds", "gauge", "node board: how long the container has waited for "
+                         "its turn", gl, g["waiting_ms"] / 1e3)
+
+
 def render_metrics(root, pod_resources_socket=None, resources=("amd.com/gpu",), board_dir=None):
     w = MetricsWriter()
-    ledger_metrics(w, board_dir or os.path.join(os.path.dirname(os.path.normpath(root)), "board"))
+    board_dir = board_dir or os.path.join(os.path.dirname(os.path.normpath(root)), "board")
+    ledger_metrics(w, board_dir)
+    board_metrics(w, board_dir)
     regions = discover(root)
     w.metric("vgpu_monitor_regions", "gauge", "container regions found", {}, sum(len(v) for v in regions.values()))
     who = owners(root, pod_resources_socket, resources)

@@ -73,6 +73,7 @@ constexpr int64_t kBoardSkipAgeS = 60;
 
 // Another container as read from its slot.
 struct BoardPeer {
+  std::string name;                          // its slot file's name without ".slot" (the container)
   int priority = kPrioNormal;
   std::vector<uint32_t> gpu_ids;
   std::vector<std::vector<uint32_t>> masks;  // per device, kCuMaskWords words (all 0 = no mask)

@@ -271,6 +271,7 @@ const std::vector<BoardPeer>& Board::refresh(uint64_t now) {
     // fresh: `now - hb` would wrap and drop a live peer at random.
     if (!hb || hb > now + kBoardStaleNs || (hb < now && now - hb > kBoardStaleNs)) continue;
     BoardPeer p;
+    p.name.assign(e->d_name, len - 5);
     p.priority = s.priority.load(std::memory_order_relaxed);
     const int ndev = std::max(0, std::min(s.ndev, kMaxDevices));
     p.gpu_ids.assign(s.gpu_id, s.gpu_id + ndev);

@@ -81,8 +81,9 @@ static int show_board(const char* dir) {
   printf("{\"containers\": [");
   int n = 0;
   for (const vgpu::BoardPeer& p : peers) {
-    printf("%s\n  {\"priority\": %d, \"cpu_node\": %d, \"launches_per_s\": %u, \"steady\": %s, \"hostpids\": [",
-           n++ ? "," : "", p.priority, p.cpu_node, p.launch_rate,
+    printf("%s\n  {\"container\": \"%s\", \"priority\": %d, \"cpu_node\": %d, \"launches_per_s\": %u, "
+           "\"steady\": %s, \"hostpids\": [",
+           n++ ? "," : "", p.name.c_str(), p.priority, p.cpu_node, p.launch_rate,
            p.steady < 0 ? "null" : p.steady ? "true" : "false");
     for (size_t i = 0; i < p.hostpids.size(); i++) printf("%s%d", i ? ", " : "", p.hostpids[i]);
     printf("], \"gpus\": [");

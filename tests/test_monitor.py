@@ -100,3 +100,23 @@ def test_control_token_and_bind_policy(tmp_path):
     finally:
         ctl.shutdown()
         r.close()
+
+
+def test_board_metrics(tmp_path, monkeypatch):
+    """The node board's containers become metrics labelled by region file: launch rate,
+    steadiness, CPU node, and per GPU the turn held or waited for (`vgpuctl board` output)."""
+    from amdvgpu.plugin import monitor
+    assert monitor._board_json(str(tmp_path / "missing")) is None
+    board = {"containers": [
+        {"container": "c1", "priority": 1, "cpu_node": 1, "launches_per_s": 70000, "steady": True, "hostpids": [7],
+         "gpus": [{"gpu_id": 4242, "holds_turn": True, "waiting_ms": None, "svm_vram": 0}]},
+        {"container": "c2", "priority": 1, "cpu_node": 0, "launches_per_s": 900, "steady": False, "hostpids": [8],
+         "gpus": [{"gpu_id": 4242, "holds_turn": False, "waiting_ms": 12.5, "svm_vram": 0}]}]}
+    monkeypatch.setattr(monitor, "_board_json", lambda d: board)
+    w = monitor.MetricsWriter()
+    monitor.board_metrics(w, str(tmp_path))
+    text = w.text()
+    assert 'vgpu_board_launches_per_second{region="c1.cache"} 70000' in text
+    assert 'vgpu_board_steady{region="c2.cache"} 0' in text
+    assert 'vgpu_board_holds_turn{region="c1.cache",gpu_id="4242"} 1' in text
+    assert 'vgpu_board_waiting_seconds{region="c2.cache",gpu_id="4242"} 0.0125' in text
