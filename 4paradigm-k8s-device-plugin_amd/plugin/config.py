@@ -55,7 +55,8 @@ class PluginConfig:
     node_name: str = ""
     shared_cache_dir: str = "/tmp"
     placement: str = "spread"               # which GPU a 1-vGPU pod lands on (GetPreferredAllocation)
-    duplicate_vgpus: str = "merge"          # Allocate of two vGPUs of one GPU: merge (one device, summed share) | reject
+    duplicate_vgpus: str = "split"          # Allocate of two vGPUs of one GPU: split (one device per vGPU, as the
+                                            # reference) | merge (one device, summed share) | reject
     host_memory_per_vgpu: str = "auto"      # pinned host memory budget per vGPU (auto: a share of the node's RAM; 0 = unlimited)
     host_memory_fraction: float = 0.5       # of the node's RAM, what vGPU containers may pin in total (buffers + spill)
     host_memory_total: str = ""             # the node's RAM (default: /proc/meminfo MemTotal)
@@ -168,10 +169,10 @@ _FLAGS = [
     ("--placement", "placement", str, ["PLACEMENT_POLICY"],
      "GPU choice for a new pod: spread (the GPU with the most free vGPUs) | binpack (the fullest GPU with room)"),
     ("--duplicate-vgpus", "duplicate_vgpus", str, ["DUPLICATE_VGPUS"],
-     "a container given two vGPUs of one GPU: merge (default: one device with the summed quota and CU share; "
-     "VGPU_DUPLICATE_MERGED and the amd-vgpu/merged-duplicates annotation tell the container) | split (one HIP "
-     "device per vGPU, each with its own quota: the shim virtualises the device ordinals, VGPU_DUPLICATE_SPLIT) | "
-     "reject (fail Allocate)"),
+     "a container given two vGPUs of one GPU: split (default, as the reference: one HIP device per vGPU, each "
+     "with its own quota; the shim virtualises the device ordinals, VGPU_DUPLICATE_SPLIT) | merge (one device with "
+     "the summed quota and CU share; VGPU_DUPLICATE_MERGED and the amd-vgpu/merged-duplicates annotation tell the "
+     "container) | reject (fail Allocate)"),
     ("--host-memory-per-vgpu", "host_memory_per_vgpu", str, ["HOST_MEMORY_PER_VGPU"],
      "pinned host memory (hipHostMalloc / hipHostRegister, and the host spill of oversubscribed vGPUs) per vGPU, "
      "e.g. 64g; auto (default) = --host-memory-fraction of the node's RAM divided among its vGPUs; "

@@ -384,7 +384,7 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         if v.uuid not in uuids:
             uuids.append(v.uuid)
     ids = device_ids(cfg, devices_by_uuid, uuids)
-    split = getattr(cfg, "duplicate_vgpus", "merge") == "split" and len(uuids) < len(vdevs)
+    split = getattr(cfg, "duplicate_vgpus", "split") == "split" and len(uuids) < len(vdevs)
     # --duplicate-vgpus=split: one entry per vGPU, so frameworks that count devices from the
     # visible list (torch.cuda.device_count) see every vGPU; ROCr lists a GPU named twice once
     # (profiles/r4dup) and the shim presents the second one.
@@ -423,7 +423,7 @@ def build_container_response(cfg, vdevs, devices_by_uuid, request_ids=None, usin
         # first vGPU's, for a container holding several)
         resp.envs["VGPU_CPU_NODE"] = str(nodes[0])
     dups = duplicate_gpus(vdevs)
-    if dups and getattr(cfg, "duplicate_vgpus", "merge") == "split":
+    if dups and getattr(cfg, "duplicate_vgpus", "split") == "split":
         # --duplicate-vgpus=split: one HIP device per vGPU, each with its own quota; the shim
         # virtualises the device ordinals (native/src/shim/vdev_hooks.cpp). Compute stays per
         # physical GPU, with the vGPUs' shares summed (docs/ABI.md "Duplicate vGPUs").

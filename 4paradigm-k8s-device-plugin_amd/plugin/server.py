@@ -360,13 +360,12 @@ class DevicePluginServer:
             dups = duplicate_gpus(vds)
             if dups and self.cfg.duplicate_vgpus == "reject":
                 # Reference [device.c:81-155] keeps duplicates as separate virtual devices
-                # (virtual PCI ids, cooperative launch off). A ROCm process cannot be shown two
-                # devices backed by one agent, so the container would silently see one GPU
-                # with the summed share: refused instead (--duplicate-vgpus=merge keeps it).
+                # (virtual PCI ids, cooperative launch off); so does the default =split (the shim
+                # virtualises the device ordinals, vdev_hooks.cpp). =reject refuses them.
                 self._fail(context, f"allocation for '{self.resource_name}' holds several vGPUs of one GPU "
-                                    f"({', '.join(dups)}); a container sees one device per physical GPU "
-                                    f"(plugin flag --duplicate-vgpus=merge accepts this as one merged device, "
-                                    f"=split as separate devices)")
+                                    f"({', '.join(dups)}), refused by --duplicate-vgpus=reject "
+                                    f"(plugin flag --duplicate-vgpus=split presents them as separate devices, "
+                                    f"=merge as one merged device)")
             unhealthy = [v.id for v in vds if not v.dev.healthy]
             if unhealthy:
                 log.warning("allocating unhealthy vGPUs %s", unhealthy)

@@ -3,10 +3,10 @@
 // Reference: its shim keeps a container's duplicate vGPUs apart as separate virtual devices
 // with virtual PCI bus ids (`assigning_virtual_pcibusID` [device.c:81-117], the device map
 // [nvml/util.c:135-162], NVIDIA_DEVICE_MAP server.go:490,493) and disables cooperative launch
-// on them [device.c:130-134]. ROCm enumerates one device per GPU agent, so by default the
-// plugin merges them (one device, summed quota and CU share: docs/ABI.md "Duplicate vGPUs").
-// With --duplicate-vgpus=split (VGPU_DUPLICATE_SPLIT=1) the shim presents them as separate
-// devices at the HIP layer instead:
+// on them [device.c:130-134]. ROCm enumerates one device per GPU agent, so with the plugin's
+// default --duplicate-vgpus=split (VGPU_DUPLICATE_SPLIT=1) the shim presents them as separate
+// devices at the HIP layer (=merge: one device, summed quota and CU share; docs/ABI.md
+// "Duplicate vGPUs"):
 //
 //   * hipGetDeviceCount counts every vGPU; virtual device v is backed by physical device
 //     phys(v) (the vGPUs of one GPU are consecutive, in VGPU_DEVICE_MAP order);

@@ -300,7 +300,7 @@ def test_placement_duplicate_and_host_memory_flags():
                                     "HOST_MEMORY_PER_VGPU": "512m"})
     assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("binpack", "merge", 512 << 20)
     cfg = parse_config([], environ={})
-    assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("spread", "merge", 0)
+    assert (cfg.placement, cfg.duplicate_vgpus, cfg.host_memory_per_vgpu_bytes) == ("spread", "split", 0)
     assert parse_config(["--duplicate-vgpus", "reject"], environ={}).duplicate_vgpus == "reject"
     assert parse_config(["--duplicate-vgpus", "split"], environ={}).duplicate_vgpus == "split"
     for bad in (["--placement", "random"], ["--duplicate-vgpus", "allow"], ["--host-memory-per-vgpu", "lots"]):

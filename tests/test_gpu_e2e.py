@@ -94,6 +94,38 @@ emit(total=total, ms=dt * 1000, ips=50 / dt, ncu=ncu, mode=Region(os.environ["VG
     print(f"slice: ResNet-V2-50 b=50 fp32 inference in a 1/4 vGPU (64 CUs): {r['ips']:.1f} img/s")
 
 
+def test_readme_two_vgpu_pod_sees_two_devices(plugin):
+    """The reference README's pod (two vGPUs, README.md:193-206) on a one-GPU node, through the
+    plugin's default Allocate (--duplicate-vgpus=split): stock PyTorch sees two devices, each
+    with its own 1/4 quota, runs on cuda:1 and copies between them (reference: duplicates as
+    separate virtual devices, [device.c:81-155])."""
+    code = CHILD_PRELUDE + """
+import torch
+n = torch.cuda.device_count()
+totals = [torch.cuda.mem_get_info(d)[1] for d in range(n)]
+torch.cuda.set_device(1)
+a = torch.randn(512, 512, device="cuda:1")
+s = (a @ a).sum().item()
+ref = (a.cpu() @ a.cpu()).sum().item()
+same = bool(torch.equal(a.to("cuda:0").cpu(), a.cpu()))
+torch.cuda.synchronize()
+emit(n=n, totals=totals, cur=torch.cuda.current_device(), close=abs(s - ref) <= 1e-3 * max(1.0, abs(ref)), same=same)
+"""
+    import json
+    import sys
+    # a container does not inherit the host job's device selection (the GPU box sets one)
+    base = {k: v for k, v in os.environ.items()
+            if k not in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")}
+    ids, envs, proc = run_pod(plugin, "amd.com/gpu", 2, [sys.executable, "-c", code], base_env=base,
+                              capture_output=True, text=True, timeout=300)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    assert envs["VGPU_DUPLICATE_SPLIT"] == "1", envs
+    r = [json.loads(l[7:]) for l in proc.stdout.splitlines() if l.startswith("RESULT ")][0]
+    quota = int(envs["VGPU_DEVICE_MEMORY_LIMIT_0"].rstrip("m")) * MiB
+    assert r["n"] == 2 and r["totals"] == [quota, quota], r
+    assert r["cur"] == 1 and r["close"] and r["same"], r
+
+
 def test_oversubscription_spills_past_hbm_share(tmp_region):
     c = vgpu_env(mem_limit=8 * GiB, shared_cache=tmp_region, oversubscribe=True,
                  extra={"VGPU_DEVICE_HBM_LIMIT_0": "2048m"})

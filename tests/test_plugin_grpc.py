@@ -254,7 +254,7 @@ def test_duplicate_vgpus_rejected_on_request(plugin_dir):
         with pytest.raises(grpc.RpcError) as e:
             k.allocate_ids("amd.com/gpu", ids)
         assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
-        assert "several vGPUs of one GPU" in e.value.details() and "--duplicate-vgpus=merge" in e.value.details()
+        assert "several vGPUs of one GPU" in e.value.details() and "--duplicate-vgpus=split" in e.value.details()
     finally:
         shutdown(k, stop, th)
 
@@ -285,22 +285,43 @@ def test_duplicate_vgpus_split_into_separate_devices(plugin_dir):
 
 def test_readme_two_vgpu_pod_admitted_on_a_one_gpu_node(plugin_dir):
     """The reference README's sample pod requests two vGPUs (README.md:205). On a node with
-    one GPU the kubelet must hand it two vGPUs of that GPU; by default (merge) Allocate admits
-    it as one device with the summed quota and CU share, annotated for the operator."""
+    one GPU the kubelet must hand it two vGPUs of that GPU; by default (split) Allocate admits
+    it as two devices, as the reference does ([device.c:81-155]): the GPU named once per vGPU
+    in the visible list, one quota per device ordinal."""
     cfg, k, sup, stop, th = start(plugin_dir, device_split_count=4, backend=FakeBackend(n=1))
     try:
+        assert cfg.duplicate_vgpus == "split"
         k.wait_registered("amd.com/gpu")
         k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
         ids, resp = k.allocate("amd.com/gpu", 2)   # the kubelet's flow: preferred allocation, then Allocate
         envs = dict(resp.envs)
         uuid = ids[0].rsplit("-", 1)[0]
         assert ids[1].rsplit("-", 1)[0] == uuid
-        assert envs["VGPU_DUPLICATE_MERGED"] == uuid
-        assert dict(resp.annotations)["amd-vgpu/merged-duplicates"] == uuid
-        assert envs["ROCR_VISIBLE_DEVICES"] == uuid  # one device in the container
+        assert envs["VGPU_DUPLICATE_SPLIT"] == "1" and "VGPU_DUPLICATE_MERGED" not in envs
+        assert dict(resp.annotations)["amd-vgpu/split-duplicates"] == uuid
+        assert envs["ROCR_VISIBLE_DEVICES"] == f"{uuid},{uuid}"  # two devices in the container
         assert envs["VGPU_DEVICE_MAP"] == f"0:{uuid} 1:{uuid}"
         total = FakeBackend(n=1).devices()[0].memory_total >> 20
         assert envs["VGPU_DEVICE_MEMORY_LIMIT_0"] == envs["VGPU_DEVICE_MEMORY_LIMIT_1"] == f"{total // 4}m"
+    finally:
+        shutdown(k, stop, th)
+
+
+def test_readme_two_vgpu_pod_merged_on_request(plugin_dir):
+    """--duplicate-vgpus=merge: the README pod's two vGPUs of one GPU become one device with the
+    summed quota and CU share, annotated for the operator."""
+    cfg, k, sup, stop, th = start(plugin_dir, device_split_count=4, backend=FakeBackend(n=1),
+                                  duplicate_vgpus="merge")
+    try:
+        k.wait_registered("amd.com/gpu")
+        k.wait_devices("amd.com/gpu", predicate=lambda d: len(d) == 4)
+        ids, resp = k.allocate("amd.com/gpu", 2)
+        envs = dict(resp.envs)
+        uuid = ids[0].rsplit("-", 1)[0]
+        assert envs["VGPU_DUPLICATE_MERGED"] == uuid and "VGPU_DUPLICATE_SPLIT" not in envs
+        assert dict(resp.annotations)["amd-vgpu/merged-duplicates"] == uuid
+        assert envs["ROCR_VISIBLE_DEVICES"] == uuid  # one device in the container
+        assert envs["VGPU_DEVICE_MAP"] == f"0:{uuid} 1:{uuid}"
     finally:
         shutdown(k, stop, th)
 
