@@ -29,6 +29,7 @@
 #include <hip/hip_deprecated.h>  // hipDeviceProp_tR0000: the hip_4.2 hipGetDeviceProperties
 
 #include <atomic>
+#include <cstdint>
 #include <cstring>
 #include <mutex>
 
@@ -65,11 +66,8 @@ int real_device_count() {
 bool build() {
   int st = g_state.load(std::memory_order_acquire);
   if (__builtin_expect(st != 0, 1)) return st == 1;
-  const Config& cfg = config();
-  if (!cfg.duplicate_split) {
-    g_state.store(2, std::memory_order_release);
-    return false;
-  }
+  // The shim's configuration is read when it initialises (with ROCr): a program whose first
+  // HIP call takes a device ordinal (hipSetDevice(1), hipGetDeviceProperties) gets here first.
   ShimState& s = shim();
   if (s.phase.load(std::memory_order_acquire) == 0) (void)real_device_count();  // HIP (and the shim) initialise
   const int ph = s.phase.load(std::memory_order_acquire);
@@ -78,6 +76,11 @@ bool build() {
     return false;
   }
   if (ph != 2 || !s.active) return false;  // not yet: asked again on the next call
+  const Config& cfg = config();
+  if (!cfg.duplicate_split) {
+    g_state.store(2, std::memory_order_release);
+    return false;
+  }
   std::lock_guard<std::mutex> g(g_build_mu);
   if ((st = g_state.load()) != 0) return st == 1;
   DeviceMap map;
@@ -247,6 +250,22 @@ hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600* prop, int device) {
   uint64_t lim = 0, used = 0;
   slot_quota(device, &lim, &used);
   if (e == hipSuccess && prop && lim) prop->totalGlobalMem = lim;
+  return e;
+}
+
+// Device attributes of virtual device v: the backing GPU's, except its global memory, which is
+// v's own quota (hipDeviceAttributeTotalGlobalMem is an int: a quota past INT32_MAX saturates,
+// as the runtime saturates the whole 288 GB GPU: profiles/r6y).
+hipError_t hipDeviceGetAttribute(int* value, hipDeviceAttribute_t attr, int device) {
+  VGPU_REAL_HIP(hipDeviceGetAttribute);
+  if (!real_hipDeviceGetAttribute) return hipErrorNotSupported;
+  if (!split()) return real_hipDeviceGetAttribute(value, attr, device);
+  if (device < 0 || device >= g_nvirt) return hipErrorInvalidDevice;
+  hipError_t e = real_hipDeviceGetAttribute(value, attr, g_virt[device].phys);
+  if (e != hipSuccess || !value || attr != hipDeviceAttributeTotalGlobalMem) return e;
+  uint64_t lim = 0, used = 0;
+  slot_quota(device, &lim, &used);
+  if (lim) *value = lim > (uint64_t)INT32_MAX ? INT32_MAX : (int)lim;
   return e;
 }
 

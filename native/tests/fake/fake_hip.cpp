@@ -185,6 +185,12 @@ hipError_t hipDeviceGetAttribute(int* value, hipDeviceAttribute_t attr, int d) {
     case hipDeviceAttributePciBusId: *value = (int)(bdf >> 8); return hipSuccess;
     case hipDeviceAttributePciDeviceId: *value = (int)((bdf >> 3) & 0x1f); return hipSuccess;
     case hipDeviceAttributePciDomainId: *value = (int)dom; return hipSuccess;
+    case hipDeviceAttributeTotalGlobalMem: {  // CLR: the pool size, saturated to an int
+      size_t total = 0;
+      hsa_amd_memory_pool_get_info(g_dev[d].pool, HSA_AMD_MEMORY_POOL_INFO_SIZE, &total);
+      *value = total > (size_t)INT32_MAX ? INT32_MAX : (int)total;
+      return hipSuccess;
+    }
     default: return hipErrorInvalidValue;
   }
 }

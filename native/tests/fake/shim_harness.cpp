@@ -8,7 +8,8 @@
 //   free             hipFree of the most recent successful allocation
 //   meminfo          hipMemGetInfo -> {"free": .., "total": ..}
 //   count            hipGetDeviceCount and hipGetDevice -> {"count": n, "current": d}
-//   props=D          hipGetDeviceProperties / hipDeviceTotalMem of device D -> {"total": .., "totalmem": ..}
+//   props=D          hipGetDeviceProperties / hipDeviceTotalMem / the TotalGlobalMem attribute of device D
+//                    -> {"total": .., "totalmem": .., "attrmem": ..}
 //   canpeer=A,B      hipDeviceCanAccessPeer(A, B), then hipDeviceEnablePeerAccess(B) from the current device
 //   stream           hipStreamCreate on the current device (becomes the current stream)
 //   usestream=I      the I-th stream created so far becomes the current stream (the current
@@ -192,7 +193,10 @@ void gates(const std::string& mode) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (hipInit(0) != hipSuccess) return 1;
+  // HARNESS_LAZY_INIT=1: no hipInit and no agent scan up front, so the first command is the
+  // program's first HIP call (e.g. hipSetDevice(1) before anything else)
+  const bool lazy = getenv("HARNESS_LAZY_INIT") != nullptr;
+  if (!lazy && hipInit(0) != hipSuccess) return 1;
   int dev = 0;
   hipStream_t stream = nullptr;
   std::vector<void*> ptrs, all_ptrs;
@@ -203,6 +207,7 @@ int main(int argc, char** argv) {
   hsa_agent_t cpu_agent{0};
   std::vector<hsa_agent_t> gpu_agents;
   hsa_amd_memory_pool_t cpu_pool{0};
+  if (!lazy)
   (void)hsa_iterate_agents(
       [](hsa_agent_t a, void* d) {
         hsa_device_type_t t;
@@ -310,8 +315,10 @@ int main(int argc, char** argv) {
       hipError_t e = hipGetDeviceProperties(&p, d);
       size_t tm = 0;
       hipError_t e2 = hipDeviceTotalMem(&tm, d);
-      printf("{\"props\": %d, \"rc\": %d, \"total\": %zu, \"totalmem\": %zu, \"rc2\": %d}\n", d, (int)e,
-             e == hipSuccess ? (size_t)p.totalGlobalMem : 0, tm, (int)e2);
+      int am = -1;
+      hipError_t e3 = hipDeviceGetAttribute(&am, hipDeviceAttributeTotalGlobalMem, d);
+      printf("{\"props\": %d, \"rc\": %d, \"total\": %zu, \"totalmem\": %zu, \"rc2\": %d, \"attrmem\": %d, "
+             "\"rc3\": %d}\n", d, (int)e, e == hipSuccess ? (size_t)p.totalGlobalMem : 0, tm, (int)e2, am, (int)e3);
     } else if (key == "canpeer") {
       const int a = atoi(val.c_str()), b = atoi(val.substr(val.find(',') + 1).c_str());
       int can = -1;

@@ -30,6 +30,9 @@ def test_two_vgpus_of_one_gpu_are_two_devices(fake):  # noqa: F811
     assert counts[0]["count"] == 2 and counts[0]["current"] == 0, counts
     props = _one(out, "props")
     assert [p["total"] for p in props] == [GiB, 2 * GiB] and [p["totalmem"] for p in props] == [GiB, 2 * GiB], props
+    # an int attribute: a 2 GiB quota does not fit and saturates, as the MI355X runtime's own
+    # answer for the whole GPU does (profiles/r6y)
+    assert [p["attrmem"] for p in props] == [GiB, 2**31 - 1] and [p["rc3"] for p in props] == [0, 0], props
     info = _one(out, "free")
     assert info[0]["total"] == 2 * GiB and info[0]["free"] == 2 * GiB, info        # device 1: its own quota
     assert info[1]["free"] == 2 * GiB - 1500 * MiB, info
@@ -39,6 +42,17 @@ def test_two_vgpus_of_one_gpu_are_two_devices(fake):  # noqa: F811
     peer = _one(out, "canpeer")[0]
     assert peer["canpeer"] == 1 and peer["rc"] == 0 and peer["enable"] == 0, peer   # one GPU's memory
     assert _one(out, "dev")[-1]["rc"] != 0   # no device 2
+
+
+def test_split_holds_when_the_first_hip_call_takes_an_ordinal(fake):  # noqa: F811
+    """A program whose first HIP call is hipSetDevice(1) (no hipGetDeviceCount before it): the
+    split is decided after the shim has initialised, so device 1 exists and holds its quota."""
+    e = dict(_env(fake, True), HARNESS_LAZY_INIT="1")   # no hipInit / agent scan up front
+    out = run(e, "dev=1", "meminfo", "malloc=1500m", "count")
+    assert _one(out, "dev")[0]["rc"] == 0, out
+    assert _one(out, "free")[0]["total"] == 2 * GiB, out
+    assert [o["malloc"] for o in _one(out, "malloc")] == ["ok"], out
+    assert _one(out, "count")[0]["count"] == 2 and _one(out, "count")[0]["current"] == 1, out
 
 
 def test_merge_keeps_one_device_with_the_summed_quota(fake):  # noqa: F811

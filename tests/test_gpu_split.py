@@ -31,8 +31,15 @@ except torch.OutOfMemoryError:
     oom0 = True
 x0 = torch.empty(3 << 30, dtype=torch.uint8, device="cuda:0")         # fits device 0
 torch.cuda.synchronize()
+import ctypes
+hip = ctypes.CDLL("libamdhip64.so")
+attr = []
+for d in range(n):
+    v = ctypes.c_int(-1)
+    rc = hip.hipDeviceGetAttribute(ctypes.byref(v), 84, d)   # hipDeviceAttributeTotalGlobalMem
+    attr.append([rc, v.value])
 emit(n=n, totals=[t for _f, t in info], props=props, cur=cur, close=abs(b - ref) <= 1e-3 * max(1.0, abs(ref)),
-     same=same, oom0=oom0, dev_of=[str(big1.device), str(x0.device)])
+     same=same, oom0=oom0, dev_of=[str(big1.device), str(x0.device)], attr=attr)
 """
 
 
@@ -59,3 +66,33 @@ def test_two_vgpus_of_one_gpu_are_two_torch_devices(tmp_region):
     assert r["cur"] == 1 and r["close"] and r["same"], r
     assert r["oom0"], r                      # device 0's own quota holds
     assert r["dev_of"] == ["cuda:1", "cuda:0"], r
+    # the int attribute: each device's own quota, saturated (4 and 6 GiB exceed an int)
+    assert r["attr"] == [[0, 2**31 - 1], [0, 2**31 - 1]], r
+
+
+NATIVE_ATTR = """
+import ctypes
+hip = ctypes.CDLL("libamdhip64.so")
+v = ctypes.c_int(-1)
+rc = hip.hipDeviceGetAttribute(ctypes.byref(v), 84, 0)   # hipDeviceAttributeTotalGlobalMem
+emit(rc=rc, v=v.value)
+"""
+
+
+def test_total_global_mem_attribute_of_split_vgpus(tmp_region):
+    """The int TotalGlobalMem attribute per virtual device: a vGPU's own quota when it fits an
+    int (1 GiB), saturated otherwise (the runtime's own answer for the whole GPU is printed)."""
+    g = _gpu()
+    native, _ = run_child(NATIVE_ATTR, None)
+    c = vgpu_env(shared_cache=tmp_region, device_map=[g.uuid, g.uuid], per_device_mem=[1 << 30, 6 * GiB],
+                 extra={"VGPU_DUPLICATE_SPLIT": "1", "ROCR_VISIBLE_DEVICES": f"{g.uuid},{g.uuid}",
+                        "HIP_VISIBLE_DEVICES": "0,1", "VGPU_DEVICE_BDFS": f"{g.bdf},{g.bdf}"})
+    res, p = run_child(NATIVE_ATTR.replace(", 84, 0)", ", 84, 0)\nw = ctypes.c_int(-1)\n"
+                                           "rc1 = hip.hipDeviceGetAttribute(ctypes.byref(w), 84, 1)")
+                       .replace("emit(rc=rc, v=v.value)", "emit(rc=rc, v=v.value, rc1=rc1, w=w.value)"), c,
+                       timeout=300, check=False)
+    assert res, p.stderr[-3000:]
+    print("native TotalGlobalMem attribute:", native[0], "split:", res[0])
+    assert native[0]["rc"] == 0, native
+    assert res[0]["rc"] == 0 and res[0]["v"] == 1 << 30, res
+    assert res[0]["rc1"] == 0 and res[0]["w"] == 2**31 - 1, res
